@@ -1,0 +1,293 @@
+// BN254 base field Fp and scalar field Fr on gfx950: 8 x 32-bit limbs,
+// Montgomery form (R = 2^256), one element per lane.
+//
+// The reference delegates all of this to github.com/IBM/mathlib -> gnark-crypto
+// ecc/bn254 (go.mod:8, go.mod:75; not vendored).  Every G1.Mul/Add and
+// Curve.ModMul on the verification path (rp/bulletproof.go:252-509,
+// rp/ipa.go:190-356, transfer/typeandsum.go:230-277) bottoms out here.
+//
+// Multiplication is the "no-carry" CIOS variant: both moduli have a top limb
+// < 2^31 - 1, so the extra carry word of textbook CIOS is never needed and one
+// product costs 2*8*8 + 8 = 136 v_mad_u64_u32.  There is no MFMA here: this is
+// carry-propagating modular integer arithmetic, not a dense contraction.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define FTS_DEV __device__ __forceinline__
+
+namespace fts {
+
+struct FpP {
+  static constexpr uint32_t M[8] = {0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u,
+                                    0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  static constexpr uint32_t INV = 0xe4866389u;  // -M^-1 mod 2^32
+  static constexpr uint32_t ONE[8] = {0xc58f0d9du, 0xd35d438du, 0xf5c70b3du, 0x0a78eb28u,
+                                      0x7879462cu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
+  static constexpr uint32_t R2[8] = {0x538afa89u, 0xf32cfc5bu, 0xd44501fbu, 0xb5e71911u,
+                                     0x0a417ff6u, 0x47ab1effu, 0xcab8351fu, 0x06d89f71u};
+};
+
+struct FrP {
+  static constexpr uint32_t M[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
+                                    0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  static constexpr uint32_t INV = 0xefffffffu;
+  static constexpr uint32_t ONE[8] = {0x4ffffffbu, 0xac96341cu, 0x9f60cd29u, 0x36fc7695u,
+                                      0x7879462eu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
+  static constexpr uint32_t R2[8] = {0xae216da7u, 0x1bb8e645u, 0xe35c59e3u, 0x53fe3ab1u,
+                                     0x53bb8085u, 0x8c49833du, 0x7f4e44a5u, 0x0216d0b1u};
+};
+
+template <class P>
+struct Field {
+  uint32_t v[8];
+};
+
+using Fp = Field<FpP>;
+using Fr = Field<FrP>;
+
+// ---------------------------------------------------------------- helpers
+FTS_DEV uint32_t addc(uint32_t a, uint32_t b, uint32_t cin, uint32_t& cout) {
+  uint32_t c;
+  uint32_t s = __builtin_addc(a, b, cin, &c);
+  cout = c;
+  return s;
+}
+FTS_DEV uint32_t subb(uint32_t a, uint32_t b, uint32_t bin, uint32_t& bout) {
+  uint32_t c;
+  uint32_t s = __builtin_subc(a, b, bin, &c);
+  bout = c;
+  return s;
+}
+
+template <class P>
+FTS_DEV Field<P> f_zero() {
+  Field<P> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = 0;
+  return r;
+}
+template <class P>
+FTS_DEV Field<P> f_one() {
+  Field<P> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = P::ONE[i];
+  return r;
+}
+template <class P>
+FTS_DEV bool f_is_zero(const Field<P>& a) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o |= a.v[i];
+  return o == 0;
+}
+template <class P>
+FTS_DEV bool f_eq(const Field<P>& a, const Field<P>& b) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o |= a.v[i] ^ b.v[i];
+  return o == 0;
+}
+
+// r = a - M if a >= M else a   (a < 2M)
+template <class P>
+FTS_DEV void f_reduce_once(Field<P>& a) {
+  uint32_t t[8], bw = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = subb(a.v[i], P::M[i], bw, bw);
+  // bw == 1  <=> a < M  -> keep a
+  const bool keep = bw != 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) a.v[i] = keep ? a.v[i] : t[i];
+}
+
+template <class P>
+FTS_DEV Field<P> f_add(const Field<P>& a, const Field<P>& b) {
+  Field<P> r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = addc(a.v[i], b.v[i], c, c);
+  // moduli < 2^254 so a + b < 2^255: no carry out of limb 7
+  f_reduce_once(r);
+  return r;
+}
+
+template <class P>
+FTS_DEV Field<P> f_sub(const Field<P>& a, const Field<P>& b) {
+  Field<P> r;
+  uint32_t bw = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = subb(a.v[i], b.v[i], bw, bw);
+  // if borrow: add M back
+  const uint32_t mask = 0u - bw;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = addc(r.v[i], P::M[i] & mask, c, c);
+  return r;
+}
+
+template <class P>
+FTS_DEV Field<P> f_neg(const Field<P>& a) {
+  return f_sub(f_zero<P>(), a);
+}
+
+template <class P>
+FTS_DEV Field<P> f_dbl(const Field<P>& a) {
+  return f_add(a, a);
+}
+
+// Montgomery product a*b*R^-1 mod M (no-carry CIOS, fully reduced output).
+template <class P>
+FTS_DEV Field<P> f_mul(const Field<P>& a, const Field<P>& b) {
+  uint32_t t[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t bi = b.v[i];
+    uint64_t A = (uint64_t)a.v[0] * bi + t[0];
+    t[0] = (uint32_t)A;
+    const uint32_t m = t[0] * P::INV;
+    uint64_t C = (uint64_t)m * P::M[0] + t[0];
+#pragma unroll
+    for (int j = 1; j < 8; j++) {
+      A = (uint64_t)a.v[j] * bi + t[j] + (A >> 32);
+      t[j] = (uint32_t)A;
+      C = (uint64_t)m * P::M[j] + t[j] + (C >> 32);
+      t[j - 1] = (uint32_t)C;
+    }
+    t[7] = (uint32_t)(C >> 32) + (uint32_t)(A >> 32);
+  }
+  Field<P> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = t[i];
+  f_reduce_once(r);
+  return r;
+}
+
+// acc(96-bit: pair + ovf) += x*y.  v_mad_u64_u32's carry-out feeds the
+// overflow word, so a column of products needs no extra register moves.
+FTS_DEV void mac96(uint64_t& acc, uint32_t& ovf, uint32_t x, uint32_t y) {
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\t"
+      "v_addc_co_u32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(ovf)
+      : "v"(x), "v"(y)
+      : "vcc");
+}
+FTS_DEV void mac96s(uint64_t& acc, uint32_t& ovf, uint32_t x, uint32_t y_uniform) {
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\t"
+      "v_addc_co_u32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(ovf)
+      : "v"(x), "s"(y_uniform)
+      : "vcc");
+}
+
+// Montgomery product, finely-integrated product scanning (FIPS): column k of
+// a*b and of m*M are summed in a 96-bit accumulator, m[k] is produced as soon
+// as column k < 8 is complete.  Same 136 multiplies as CIOS, but the
+// accumulator stays in one register triple.
+template <class P>
+FTS_DEV Field<P> f_mul_fips(const Field<P>& a, const Field<P>& b) {
+  uint32_t m[8], t[8];
+  uint64_t acc = 0;
+  uint32_t ovf = 0;
+#pragma unroll
+  for (int k = 0; k < 15; k++) {
+#pragma unroll
+    for (int i = (k > 7 ? k - 7 : 0); i <= (k < 7 ? k : 7); i++) mac96(acc, ovf, a.v[i], b.v[k - i]);
+#pragma unroll
+    for (int i = (k > 7 ? k - 7 : 0); i < (k < 8 ? k : 8); i++) mac96s(acc, ovf, m[i], P::M[k - i]);
+    if (k < 8) {
+      m[k] = (uint32_t)acc * P::INV;
+      mac96s(acc, ovf, m[k], P::M[0]);
+    } else {
+      t[k - 8] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)ovf << 32);
+    ovf = 0;
+  }
+  t[7] = (uint32_t)acc;
+  Field<P> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = t[i];
+  f_reduce_once(r);
+  return r;
+}
+
+template <class P>
+FTS_DEV Field<P> f_sqr(const Field<P>& a) {
+  return f_mul(a, a);
+}
+
+// Montgomery form <-> canonical integer (both as 8 little-endian limbs)
+template <class P>
+FTS_DEV Field<P> f_to_mont(const Field<P>& a) {
+  Field<P> r2;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r2.v[i] = P::R2[i];
+  return f_mul(a, r2);
+}
+template <class P>
+FTS_DEV Field<P> f_from_mont(const Field<P>& a) {
+  Field<P> one = f_zero<P>();
+  one.v[0] = 1;
+  return f_mul(a, one);
+}
+
+// a^e for a 256-bit exponent given as 8 LE limbs (square-and-multiply, MSB first)
+template <class P>
+FTS_DEV Field<P> f_pow(const Field<P>& a, const uint32_t e[8]) {
+  Field<P> r = f_one<P>();
+  bool started = false;
+  for (int i = 7; i >= 0; i--) {
+    for (int b = 31; b >= 0; b--) {
+      if (started) r = f_sqr(r);
+      if ((e[i] >> b) & 1u) {
+        r = started ? f_mul(r, a) : a;
+        started = true;
+      }
+    }
+  }
+  return r;
+}
+
+// inverse via Fermat (a^(M-2)); inv(0) = 0
+template <class P>
+FTS_DEV Field<P> f_inv(const Field<P>& a) {
+  uint32_t e[8];
+  uint32_t bw = 0;
+  e[0] = subb(P::M[0], 2u, 0, bw);
+#pragma unroll
+  for (int i = 1; i < 8; i++) e[i] = subb(P::M[i], 0u, bw, bw);
+  return f_pow(a, e);
+}
+
+// canonical (non-Montgomery) limbs < M ?
+template <class P>
+FTS_DEV bool limbs_lt_mod(const uint32_t a[8]) {
+  uint32_t bw = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) (void)subb(a[i], P::M[i], bw, bw);
+  return bw != 0;
+}
+
+// big-endian 32 bytes -> LE limbs (no reduction)
+FTS_DEV void be32_to_limbs(const uint8_t* b, uint32_t out[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint8_t* q = b + 28 - 4 * i;
+    out[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
+  }
+}
+FTS_DEV void limbs_to_be32(const uint32_t in[8], uint8_t* b) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint8_t* q = b + 28 - 4 * i;
+    q[0] = (uint8_t)(in[i] >> 24);
+    q[1] = (uint8_t)(in[i] >> 16);
+    q[2] = (uint8_t)(in[i] >> 8);
+    q[3] = (uint8_t)in[i];
+  }
+}
+
+}  // namespace fts

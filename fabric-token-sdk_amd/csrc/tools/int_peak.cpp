@@ -1,0 +1,155 @@
+// Integer-ALU roofline microbenchmark for gfx950 ("measure the
+// v_mad_u64_u32 rate with a microbenchmark").  Prints one JSON line:
+//   mad_u64_u32 per second (chip), full-rate u32 ops per second, and the
+//   8x32-limb Montgomery Fp multiplication rate of device/field.hpp.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include "../device/field.hpp"
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1);} } while (0)
+
+constexpr int MAD_ITERS = 4096;
+constexpr int MAD_CHAINS = 8;
+
+__global__ void __launch_bounds__(256) k_mad(const uint32_t* in, uint64_t* out) {
+  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t a = in[tid & 1023] | 1u, b = in[(tid + 7) & 1023] | 3u;
+  uint64_t acc[MAD_CHAINS];
+#pragma unroll
+  for (int c = 0; c < MAD_CHAINS; c++) acc[c] = tid + c;
+  for (int i = 0; i < MAD_ITERS; i++) {
+#pragma unroll
+    for (int c = 0; c < MAD_CHAINS; c++) {
+      // v_mad_u64_u32: acc = a*b + acc  (mix the high word back so it is not folded)
+      acc[c] = (uint64_t)(a ^ (uint32_t)(acc[c] >> 32)) * b + (uint32_t)acc[c];
+    }
+  }
+  uint64_t s = 0;
+#pragma unroll
+  for (int c = 0; c < MAD_CHAINS; c++) s ^= acc[c];
+  out[tid] = s;
+}
+
+constexpr int ADD_ITERS = 8192;
+__global__ void __launch_bounds__(256) k_add(const uint32_t* in, uint32_t* out) {
+  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t x[8];
+#pragma unroll
+  for (int c = 0; c < 8; c++) x[c] = in[(tid + c) & 1023];
+  for (int i = 0; i < ADD_ITERS; i++) {
+#pragma unroll
+    for (int c = 0; c < 8; c++) x[c] = (x[c] + x[(c + 1) & 7]) ^ 0x9e3779b9u;
+  }
+  uint32_t s = 0;
+#pragma unroll
+  for (int c = 0; c < 8; c++) s ^= x[c];
+  out[tid] = s;
+}
+
+constexpr int MUL_ITERS = 256;
+__global__ void __launch_bounds__(256) k_fpmul(const uint32_t* in, uint32_t* out) {
+  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  fts::Fp a, b;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a.v[i] = in[(tid * 8 + i) & 1023];
+    b.v[i] = in[(tid * 8 + i + 5) & 1023];
+  }
+  a.v[7] &= 0x0fffffffu;
+  b.v[7] &= 0x0fffffffu;
+  for (int i = 0; i < MUL_ITERS; i++) {
+    a = fts::f_mul(a, b);
+    b = fts::f_mul(b, a);
+  }
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) s ^= a.v[i] ^ b.v[i];
+  out[tid] = s;
+}
+
+__global__ void __launch_bounds__(256) k_fpmul_fips(const uint32_t* in, uint32_t* out) {
+  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  fts::Fp a, b;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a.v[i] = in[(tid * 8 + i) & 1023];
+    b.v[i] = in[(tid * 8 + i + 5) & 1023];
+  }
+  a.v[7] &= 0x0fffffffu;
+  b.v[7] &= 0x0fffffffu;
+  for (int i = 0; i < MUL_ITERS; i++) {
+    a = fts::f_mul_fips(a, b);
+    b = fts::f_mul_fips(b, a);
+  }
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) s ^= a.v[i] ^ b.v[i];
+  out[tid] = s;
+}
+
+int main() {
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  const int cus = prop.multiProcessorCount;
+  const int blocks = cus * 8, threads = 256;
+  const size_t n = (size_t)blocks * threads;
+  uint32_t* d_in;
+  uint64_t* d_out;
+  CK(hipMalloc(&d_in, 1024 * 4));
+  CK(hipMalloc(&d_out, n * 8));
+  uint32_t h[1024];
+  for (int i = 0; i < 1024; i++) h[i] = 0x12345678u * (i + 1) ^ (i << 13);
+  CK(hipMemcpy(d_in, h, sizeof(h), hipMemcpyHostToDevice));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  float ms;
+
+  k_mad<<<blocks, threads>>>(d_in, d_out);
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < 5; r++) k_mad<<<blocks, threads>>>(d_in, d_out);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  double mad_rate = 5.0 * n * MAD_ITERS * MAD_CHAINS / (ms * 1e-3);
+
+  k_add<<<blocks, threads>>>(d_in, (uint32_t*)d_out);
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < 5; r++) k_add<<<blocks, threads>>>(d_in, (uint32_t*)d_out);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  double add_rate = 5.0 * n * ADD_ITERS * 8 * 2 / (ms * 1e-3);  // add + xor
+
+  k_fpmul<<<blocks, threads>>>(d_in, (uint32_t*)d_out);
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < 5; r++) k_fpmul<<<blocks, threads>>>(d_in, (uint32_t*)d_out);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  double fpmul_rate = 5.0 * n * MUL_ITERS * 2 / (ms * 1e-3);
+
+  uint32_t* h1 = (uint32_t*)malloc(n * 4);
+  uint32_t* h2 = (uint32_t*)malloc(n * 4);
+  CK(hipMemcpy(h1, d_out, n * 4, hipMemcpyDeviceToHost));
+  k_fpmul_fips<<<blocks, threads>>>(d_in, (uint32_t*)d_out);
+  CK(hipDeviceSynchronize());
+  CK(hipMemcpy(h2, d_out, n * 4, hipMemcpyDeviceToHost));
+  int mism = 0;
+  for (size_t i = 0; i < n; i++) mism += h1[i] != h2[i];
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < 5; r++) k_fpmul_fips<<<blocks, threads>>>(d_in, (uint32_t*)d_out);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  double fips_rate = 5.0 * n * MUL_ITERS * 2 / (ms * 1e-3);
+  printf("{\"fips_fp_mul_per_s\": %.4e, \"fips_mismatch\": %d}\n", fips_rate, mism);
+  printf("{\"device\": \"%s\", \"cus\": %d, \"clock_khz\": %d, \"mad_u64_u32_per_s\": %.4e, "
+         "\"u32_ops_per_s\": %.4e, \"fp_mul_per_s\": %.4e, \"fp_mul_mad_equiv_per_s\": %.4e}\n",
+         prop.gcnArchName, cus, prop.clockRate, mad_rate, add_rate, fpmul_rate, fpmul_rate * 136.0);
+  return 0;
+}
