@@ -1,0 +1,61 @@
+// Device-side layout shared by the range-proof kernels and the host driver.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fts {
+
+// per-proof point slots (raw BE on input, affine Montgomery after decode)
+//   0 T1, 1 T2, 2 C, 3 D, 4 V, 5..5+k-1 L_j, 5+k..5+2k-1 R_j
+constexpr int RP_PT_T1 = 0, RP_PT_T2 = 1, RP_PT_C = 2, RP_PT_D = 3, RP_PT_V = 4, RP_PT_L = 5;
+inline __host__ __device__ int rp_npts(int k) { return 5 + 2 * k; }
+
+// per-proof scalars (canonical Fr LE limbs, host-reduced mod r)
+constexpr int RP_SC_TAU = 0, RP_SC_DELTA = 1, RP_SC_IP = 2, RP_SC_A = 3, RP_SC_B = 4, RP_NSC = 5;
+
+// per-proof challenge block (Fr, Montgomery form, 8 words each)
+//   0 x, 1 x^2, 2 y, 3 y^-1, 4 z, 5 z^2, 6 polEval, 7 x0, 8.. x_j, 8+k.. x_j^-1
+constexpr int CH_X = 0, CH_X2 = 1, CH_Y = 2, CH_YINV = 3, CH_Z = 4, CH_Z2 = 5, CH_POL = 6, CH_X0 = 7, CH_XJ = 8;
+inline __host__ __device__ int rp_nch(int k) { return 8 + 2 * k; }
+
+// fixed-base table slots in the context (per base: FB_WORDS_PER_BASE words)
+//   0..n-1 G_i (left), n..2n-1 H_i (right), 2n G=ped1, 2n+1 H=ped2, 2n+2 P,
+//   2n+3 Q, 2n+4 K = sum H_i - sum G_i, 2n+5 ped0
+inline __host__ __device__ int tb_G(int n) { return 2 * n; }
+inline __host__ __device__ int tb_H(int n) { return 2 * n + 1; }
+inline __host__ __device__ int tb_P(int n) { return 2 * n + 2; }
+inline __host__ __device__ int tb_Q(int n) { return 2 * n + 3; }
+inline __host__ __device__ int tb_K(int n) { return 2 * n + 4; }
+inline __host__ __device__ int tb_ped0(int n) { return 2 * n + 5; }
+inline __host__ __device__ int tb_count(int n) { return 2 * n + 6; }
+
+// x0 transcript (rp/ipa.go:200-213): DER SEQUENCE{ OCTET(array), OCTET("||"), OCTET(Zb(ip)) }
+// array = 2n+2 records (H'_0..H'_{n-1}, G_0..G_{n-1}, Q, com) of 130 bytes, last w/o "||"
+inline __host__ __device__ uint32_t x0_array_len(int n) { return 130u * (2u * n + 2u) - 2u; }
+inline __host__ __device__ uint32_t x0_msg_len(int n) { return x0_array_len(n) + 46u; }
+inline __host__ __device__ uint32_t x0_slot_bytes(int n) { return ((x0_msg_len(n) + 9u + 63u) / 64u) * 64u; }
+
+// small transcripts slot (x: 258 B, y: 388 B, x_j: 258 B, z: 32 B) -> 512 B scratch each
+constexpr uint32_t SMALL_SLOT = 512;
+
+// device buffers of one range-proof batch (filled by fts_api.cpp)
+struct RpBatchDev {
+  int B, n, k;
+  uint8_t* raw;        // [B][5+2k][64] raw BE points (slot V from the caller)
+  uint32_t* sc;        // [B][5][8] canonical Fr
+  int32_t* status;     // [B] verdicts (host-parse verdicts on entry)
+  int32_t* ipa_flag;   // [B] deferred IPA structural verdicts
+  uint32_t* pts;       // [B][5+2k][16] affine Montgomery
+  uint32_t* ch;        // [B][8+2k][8] challenges (Montgomery Fr)
+  uint8_t* small_msgs; // [B][SMALL_SLOT]
+  uint32_t* hpj;       // [B][n][24]
+  uint32_t* hpa;       // [B][n][16]
+  uint8_t* hp_be;      // [B][n][64]
+  uint32_t* com;       // [B][16]
+  uint8_t* com_be;     // [B][64]
+  uint8_t* x0_msgs;    // [B][x0_slot_bytes(n)]
+  uint32_t* terms;     // [B][6+2n+2k][24]
+  uint32_t* scratch;   // var-base lane tables
+};
+
+}  // namespace fts

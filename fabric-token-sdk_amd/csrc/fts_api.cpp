@@ -1,0 +1,931 @@
+// C-ABI of the MI355X zkatdlog batch verifier (include/fts_gpu.h).
+//
+// Host side of the drop-in boundary: context creation from the public
+// parameters (setup.go:319-372), DER decoding of proofs into device records,
+// orchestration of the HIP kernels in rp_kernels.hip / sigma_kernels.hip, and
+// the reference error-precedence rules (transfer.go:153-197,
+// issue/verifier.go:32-57, rangecorrectness.go:137-162).
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/fts_gpu.h"
+#include "device/rp_kernels.hpp"
+#include "device/sigma.hpp"
+#include "host/bn254_host.hpp"
+#include "host/der.hpp"
+#include "host/pp_parse.hpp"
+#include "host/proofs.hpp"
+#include "host/prover.hpp"
+
+namespace fts {
+// device launchers (rp_kernels.hip)
+
+size_t rp_scratch_words(int B, int n, int k);
+size_t rp_terms_words(int B, int n, int k);
+void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s);
+void launch_rp_verify(const RpBatchDev& d, const uint32_t* tables, const uint8_t* x0_const, hipStream_t s,
+                      hipEvent_t* ev);
+void launch_sig_prep(const SigBatchDev& d, hipStream_t s);
+void launch_sig_finish(const SigBatchDev& d, const uint32_t* tables, int n, hipStream_t s);
+constexpr size_t FB_WORDS = 32 * 128 * 16;
+}  // namespace fts
+
+using namespace fts;
+using namespace fts::host;
+
+#define HIP_OK(x)                                                                         \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess) {                                                               \
+      fprintf(stderr, "fts_gpu: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+      return FTS_API_EDEVICE;                                                             \
+    }                                                                                     \
+  } while (0)
+
+namespace {
+
+// growable device buffer
+struct DBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return 0;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 256);
+    if (hipMalloc(&p, want) != hipSuccess) return -1;
+    cap = want;
+    return 0;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+};
+
+struct Workspace {
+  DBuf pts, ch, small, hpj, hpa, hpbe, com, combe, x0, terms, scratch;
+  // action (transfer / issue) batches
+  DBuf rp_raw, rp_sc, rp_status, rp_ipa;
+  DBuf s_act, s_raw, s_owner, s_pts, s_sc, s_status, s_work, s_terms, s_aff, s_affoff, s_msgs, s_jac, s_scratch;
+  void release() {
+    for (DBuf* b : {&pts, &ch, &small, &hpj, &hpa, &hpbe, &com, &combe, &x0, &terms, &scratch, &rp_raw, &rp_sc,
+                    &rp_status, &rp_ipa, &s_act, &s_raw, &s_owner, &s_pts, &s_sc, &s_status, &s_work, &s_terms, &s_aff,
+                    &s_affoff, &s_msgs, &s_jac, &s_scratch})
+      b->release();
+  }
+};
+
+const int kNumEv = 8;
+const char* kPhaseNames[kNumEv - 1] = {"decode+challenges", "hprime", "normalize+com", "x0", "terms_fixed",
+                                       "terms_var", "check"};
+
+}  // namespace
+
+struct fts_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  PublicParams pp;
+  int n = 0, k = 0;
+  uint32_t* d_tables = nullptr;
+  uint8_t* d_x0const = nullptr;
+  size_t table_bytes = 0;
+  std::mutex mu;
+  Workspace ws;
+  hipEvent_t ev[kNumEv];
+  float timings[kNumEv - 1] = {0};
+  std::once_flag prover_once;
+  ProverTables ptab;
+};
+
+struct fts_rp_batch {
+  int B = 0;
+  int device = 0;
+  uint8_t* raw = nullptr;
+  uint32_t* sc = nullptr;
+  int32_t* status0 = nullptr;  // host-parse verdicts (restored before every run)
+  int32_t* status = nullptr;
+  int32_t* ipa_flag = nullptr;
+};
+
+namespace fts {
+namespace host {
+void build_prover_tables(const PublicParams& pp, int n, ProverTables& t) {
+  t.n = n;
+  std::vector<G1A> bases;
+  for (int i = 0; i < n; i++) bases.push_back(pp.left[i]);
+  for (int i = 0; i < n; i++) bases.push_back(pp.right[i]);
+  for (int i = 0; i < 3; i++) bases.push_back(pp.ped[i]);
+  bases.push_back(pp.P);
+  bases.push_back(pp.Q);
+  t.fb.resize(bases.size());
+  std::atomic<size_t> next{0};
+  unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  for (unsigned w = 0; w < nth; w++)
+    th.emplace_back([&]() {
+      for (size_t i; (i = next++) < bases.size();) t.fb[i].build(bases[i]);
+    });
+  for (auto& x : th) x.join();
+}
+}  // namespace host
+}  // namespace fts
+
+static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int device, fts_ctx** out) {
+  if (!pp_bytes || !out) return FTS_API_EINVAL;
+  *out = nullptr;
+  fts_ctx* c = new fts_ctx();
+  std::string err;
+  if (!parse_public_params(pp_bytes, pp_len, c->pp, err)) {
+    fprintf(stderr, "fts_gpu: public parameters rejected: %s\n", err.c_str());
+    delete c;
+    return FTS_API_EPP;
+  }
+  if (bits) {
+    if (bits > c->pp.bit_length || (bits & (bits - 1)) || bits < 2) {
+      delete c;
+      return FTS_API_ESIZE;
+    }
+    c->pp.left.resize(bits);
+    c->pp.right.resize(bits);
+    c->pp.bit_length = bits;
+    c->pp.rounds = 63 - __builtin_clzll(bits);
+    c->pp.max_token = bits == 64 ? ~0ULL : ((1ULL << bits) - 1);
+    c->pp.precision = bits;
+  }
+  c->n = (int)c->pp.bit_length;
+  c->k = (int)c->pp.rounds;
+  if (device == FTS_DEVICE_NONE) {  // host-only context: parsing + prover, no GPU
+    c->device = FTS_DEVICE_NONE;
+    *out = c;
+    return FTS_API_OK;
+  }
+  if (device < 0) {
+    if (hipGetDevice(&device) != hipSuccess) device = 0;
+  }
+  c->device = device;
+  auto fail = [&](int code) {
+    delete c;
+    return code;
+  };
+  if (hipSetDevice(device) != hipSuccess) return fail(FTS_API_EDEVICE);
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
+  for (int i = 0; i < kNumEv; i++) hipEventCreate(&c->ev[i]);
+  const int n = c->n;
+  // fixed bases in table order (rp_kernels.hpp tb_*)
+  std::vector<G1A> bases;
+  for (int i = 0; i < n; i++) bases.push_back(c->pp.left[i]);
+  for (int i = 0; i < n; i++) bases.push_back(c->pp.right[i]);
+  bases.push_back(c->pp.ped[1]);
+  bases.push_back(c->pp.ped[2]);
+  bases.push_back(c->pp.P);
+  bases.push_back(c->pp.Q);
+  G1J K = jac_identity();
+  for (int i = 0; i < n; i++) {
+    K = jadd_aff(K, c->pp.right[i]);
+    K = jadd_aff(K, aff_neg(c->pp.left[i]));
+  }
+  bases.push_back(to_aff(K));
+  bases.push_back(c->pp.ped[0]);
+  const int nb = (int)bases.size();
+  std::vector<uint32_t> hb((size_t)nb * 16, 0);
+  for (int b = 0; b < nb; b++)
+    if (!bases[b].inf) {
+      memcpy(&hb[b * 16], bases[b].x.v, 32);  // 4x64 LE == 8x32 LE Montgomery form
+      memcpy(&hb[b * 16 + 8], bases[b].y.v, 32);
+    }
+  uint32_t* d_bases = nullptr;
+  uint32_t* d_scr = nullptr;
+  c->table_bytes = (size_t)nb * FB_WORDS * 4;
+  if (hipMalloc(&c->d_tables, c->table_bytes) != hipSuccess) return fail(FTS_API_ENOMEM);
+  if (hipMalloc(&d_bases, hb.size() * 4) != hipSuccess) return fail(FTS_API_ENOMEM);
+  if (hipMalloc(&d_scr, (size_t)nb * 32 * 128 * 32 * 4) != hipSuccess) return fail(FTS_API_ENOMEM);
+  hipMemcpyAsync(d_bases, hb.data(), hb.size() * 4, hipMemcpyHostToDevice, c->stream);
+  launch_build_tables(d_bases, nb, c->d_tables, d_scr, c->stream);
+  // constant part of the x0 transcript: hex(G_i) "||" ... hex(Q) "||"
+  std::string xc;
+  for (int i = 0; i <= n; i++) {
+    uint8_t b[64];
+    g1_to_bytes(i < n ? c->pp.left[i] : c->pp.Q, b);
+    xc += hex_of(b, 64);
+    xc += "||";
+  }
+  if (hipMalloc(&c->d_x0const, xc.size()) != hipSuccess) return fail(FTS_API_ENOMEM);
+  hipMemcpyAsync(c->d_x0const, xc.data(), xc.size(), hipMemcpyHostToDevice, c->stream);
+  hipError_t e = hipStreamSynchronize(c->stream);
+  hipFree(d_bases);
+  hipFree(d_scr);
+  if (e != hipSuccess) {
+    fprintf(stderr, "fts_gpu: table build failed: %s\n", hipGetErrorString(e));
+    return fail(FTS_API_EDEVICE);
+  }
+  *out = c;
+  return FTS_API_OK;
+}
+
+extern "C" {
+
+int fts_ctx_create(const uint8_t* pp, size_t pp_len, int device, fts_ctx** out) {
+  return ctx_create(pp, pp_len, 0, device, out);
+}
+int fts_ctx_create_bits(const uint8_t* pp, size_t pp_len, uint32_t bit_length, int device, fts_ctx** out) {
+  return ctx_create(pp, pp_len, bit_length, device, out);
+}
+
+void fts_ctx_destroy(fts_ctx* c) {
+  if (!c) return;
+  if (c->device == FTS_DEVICE_NONE) {
+    delete c;
+    return;
+  }
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  c->ws.release();
+  if (c->d_tables) hipFree(c->d_tables);
+  if (c->d_x0const) hipFree(c->d_x0const);
+  for (int i = 0; i < kNumEv; i++) hipEventDestroy(c->ev[i]);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int fts_ctx_info(const fts_ctx* c, fts_pp_info* o) {
+  if (!c || !o) return FTS_API_EINVAL;
+  o->bit_length = (uint32_t)c->pp.bit_length;
+  o->rounds = (uint32_t)c->pp.rounds;
+  o->curve_id = (uint32_t)c->pp.curve_id;
+  o->device = c->device;
+  o->max_token = c->pp.max_token;
+  o->table_bytes = c->table_bytes;
+  return FTS_API_OK;
+}
+
+const char* fts_status_str(int32_t s) {
+  switch (s) {
+    case FTS_OK: return "";
+    case FTS_E_MALFORMED: return "failed to deserialize proof";
+    case FTS_E_RP_NIL: return "invalid range proof: nil elements";
+    case FTS_E_RP_INVALID: return "invalid range proof";
+    case FTS_E_IPA_NIL: return "invalid IPA proof: nil elements";
+    case FTS_E_IPA_LEN: return "invalid IPA proof";
+    case FTS_E_IPA_INVALID: return "invalid IPA";
+    case FTS_E_RC_COUNT: return "invalid range proof";
+    case FTS_E_TAS_INVALID: return "invalid sum and type proof";
+    case FTS_E_ST_INVALID: return "invalid same type proof";
+    case FTS_E_NOT_RUN: return "not evaluated";
+    default: return "unknown status";
+  }
+}
+
+int fts_last_timings(const fts_ctx* c, const char** names, float* ms, int cap) {
+  if (!c) return 0;
+  int m = std::min(cap, kNumEv - 1);
+  for (int i = 0; i < m; i++) {
+    if (names) names[i] = kPhaseNames[i];
+    if (ms) ms[i] = c->timings[i];
+  }
+  return m;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------ range proofs
+// host records for B proofs
+struct RpHost {
+  std::vector<uint8_t> raw;
+  std::vector<uint32_t> sc;
+  std::vector<int32_t> status, ipa;
+};
+
+static void parse_rp_batch(int k, size_t B, const uint8_t* const* der_p, const size_t* der_len, const uint8_t* com64,
+                           RpHost& h) {
+  const int npts = rp_npts(k);
+  h.raw.assign(B * npts * 64, 0);
+  h.sc.assign(B * RP_NSC * 8, 0);
+  h.status.assign(B, 0);
+  h.ipa.assign(B, 0);
+  auto work = [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; i++) {
+      uint8_t* pts = &h.raw[i * npts * 64];
+      der::Span s{der_p[i], der_len[i]};
+      if (!der_p[i]) s.n = 0;
+      parse_range_proof(s, k, pts, &h.sc[i * RP_NSC * 8], h.status[i], h.ipa[i]);
+      memcpy(pts + RP_PT_V * 64, com64 + i * 64, 64);
+    }
+  };
+  unsigned nth = B >= 256 ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
+  std::vector<std::thread> th;
+  size_t chunk = (B + nth - 1) / nth;
+  for (unsigned t = 0; t < nth; t++) {
+    size_t lo = t * chunk, hi = std::min(B, lo + chunk);
+    if (lo < hi) th.emplace_back(work, lo, hi);
+  }
+  for (auto& t : th) t.join();
+}
+
+static int launch_rp(fts_ctx* c, int B, uint8_t* d_raw, uint32_t* d_sc, int32_t* d_status, int32_t* d_ipa) {
+  const int n = c->n, k = c->k;
+  Workspace& w = c->ws;
+  if (w.pts.ensure((size_t)B * rp_npts(k) * 64) || w.ch.ensure((size_t)B * rp_nch(k) * 32) ||
+      w.small.ensure((size_t)B * SMALL_SLOT) || w.hpj.ensure((size_t)B * n * 96) || w.hpa.ensure((size_t)B * n * 64) ||
+      w.hpbe.ensure((size_t)B * n * 64) || w.com.ensure((size_t)B * 64) || w.combe.ensure((size_t)B * 64) ||
+      w.x0.ensure((size_t)B * x0_slot_bytes(n)) || w.terms.ensure(rp_terms_words(B, n, k) * 4) ||
+      w.scratch.ensure(std::max(rp_scratch_words(B, n, k), (size_t)B * 10 * 24) * 4))
+    return FTS_API_ENOMEM;
+  RpBatchDev d{B,
+               n,
+               k,
+               d_raw,
+               d_sc,
+               d_status,
+               d_ipa,
+               w.pts.as<uint32_t>(),
+               w.ch.as<uint32_t>(),
+               w.small.as<uint8_t>(),
+               w.hpj.as<uint32_t>(),
+               w.hpa.as<uint32_t>(),
+               w.hpbe.as<uint8_t>(),
+               w.com.as<uint32_t>(),
+               w.combe.as<uint8_t>(),
+               w.x0.as<uint8_t>(),
+               w.terms.as<uint32_t>(),
+               w.scratch.as<uint32_t>()};
+  launch_rp_verify(d, c->d_tables, c->d_x0const, c->stream, c->ev);
+  HIP_OK(hipGetLastError());
+  return FTS_API_OK;
+}
+
+static int run_rp(fts_ctx* c, int B, uint8_t* d_raw, uint32_t* d_sc, int32_t* d_status, int32_t* d_ipa,
+                  int32_t* host_status) {
+  int rc = launch_rp(c, B, d_raw, d_sc, d_status, d_ipa);
+  if (rc != FTS_API_OK) return rc;
+  if (host_status) HIP_OK(hipMemcpyAsync(host_status, d_status, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  for (int i = 0; i + 1 < kNumEv; i++) hipEventElapsedTime(&c->timings[i], c->ev[i], c->ev[i + 1]);
+  return FTS_API_OK;
+}
+
+extern "C" {
+
+// debug/parity hook: intermediates of proof i of the last range-proof run
+//   ch_out: (8 + 2k) x 32 bytes canonical BE Fr  [x, x^2, y, y^-1, z, z^2, polEval, x0, x_j.., x_j^-1..]
+//   com_out: 64 bytes com (BE) ; hp_out: n x 64 bytes H'_i (BE)
+int fts_debug_rp_intermediates(fts_ctx* c, size_t i, uint8_t* ch_out, uint8_t* com_out, uint8_t* hp_out) {
+  if (!c || c->device < 0) return FTS_API_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  const int n = c->n, k = c->k, nch = rp_nch(k);
+  if (ch_out) {
+    std::vector<uint32_t> ch(nch * 8);
+    HIP_OK(hipMemcpy(ch.data(), c->ws.ch.as<uint32_t>() + i * nch * 8, nch * 32, hipMemcpyDeviceToHost));
+    for (int q = 0; q < nch; q++) {
+      Fr m;
+      memcpy(m.v, &ch[q * 8], 32);
+      fr_to_be(m, ch_out + 32 * q);
+    }
+  }
+  if (com_out) HIP_OK(hipMemcpy(com_out, c->ws.combe.as<uint8_t>() + i * 64, 64, hipMemcpyDeviceToHost));
+  if (hp_out) HIP_OK(hipMemcpy(hp_out, c->ws.hpbe.as<uint8_t>() + i * n * 64, n * 64, hipMemcpyDeviceToHost));
+  return FTS_API_OK;
+}
+
+int fts_rp_batch_stage(fts_ctx* c, size_t n, const uint8_t* const* rp_der, const size_t* rp_len, const uint8_t* com64,
+                       fts_rp_batch** out) {
+  if (!c || !out || (n && (!rp_der || !rp_len || !com64))) return FTS_API_EINVAL;
+  if (c->device < 0) return FTS_API_EDEVICE;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  RpHost h;
+  parse_rp_batch(c->k, n, rp_der, rp_len, com64, h);
+  fts_rp_batch* b = new fts_rp_batch();
+  b->B = (int)n;
+  b->device = c->device;
+  size_t nb = std::max<size_t>(n, 1);
+  if (hipMalloc(&b->raw, std::max<size_t>(h.raw.size(), 64)) != hipSuccess ||
+      hipMalloc(&b->sc, std::max<size_t>(h.sc.size() * 4, 32)) != hipSuccess ||
+      hipMalloc(&b->status0, nb * 4) != hipSuccess || hipMalloc(&b->status, nb * 4) != hipSuccess ||
+      hipMalloc(&b->ipa_flag, nb * 4) != hipSuccess) {
+    fts_rp_batch_free(b);
+    return FTS_API_ENOMEM;
+  }
+  if (n) {
+    HIP_OK(hipMemcpyAsync(b->raw, h.raw.data(), h.raw.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(b->sc, h.sc.data(), h.sc.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(b->status0, h.status.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(b->ipa_flag, h.ipa.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+  }
+  HIP_OK(hipStreamSynchronize(c->stream));
+  *out = b;
+  return FTS_API_OK;
+}
+
+int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
+  if (!c || !b) return FTS_API_EINVAL;
+  if (c->device < 0) return FTS_API_EDEVICE;
+  if (b->B == 0) return FTS_API_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  HIP_OK(hipMemcpyAsync(b->status, b->status0, (size_t)b->B * 4, hipMemcpyDeviceToDevice, c->stream));
+  return run_rp(c, b->B, b->raw, b->sc, b->status, b->ipa_flag, status);
+}
+
+void fts_rp_batch_free(fts_rp_batch* b) {
+  if (!b) return;
+  hipSetDevice(b->device);
+  for (void* p : {(void*)b->raw, (void*)b->sc, (void*)b->status0, (void*)b->status, (void*)b->ipa_flag})
+    if (p) hipFree(p);
+  delete b;
+}
+
+int fts_rp_verify_batch(fts_ctx* c, size_t n, const uint8_t* const* rp_der, const size_t* rp_len, const uint8_t* com64,
+                        int32_t* status) {
+  if (!c || !status) return FTS_API_EINVAL;
+  if (n == 0) return FTS_API_OK;
+  fts_rp_batch* b = nullptr;
+  int rc = fts_rp_batch_stage(c, n, rp_der, rp_len, com64, &b);
+  if (rc != FTS_API_OK) {
+    for (size_t i = 0; i < n; i++) status[i] = FTS_E_NOT_RUN;
+    return rc;
+  }
+  rc = fts_rp_batch_verify(c, b, status);
+  fts_rp_batch_free(b);
+  return rc;
+}
+
+
+// ------------------------------------------------------- transfers / issues
+// One action = a transfer (TypeAndSum + RangeCorrectness on Out_j - CT,
+// transfer/transfer.go:49-60,153-197) or an issue (SameType + RangeCorrectness
+// on Tok_i - CT, issue/verifier.go:24-57).
+namespace {
+struct ActionIn {
+  int kind;                    // SIG_TAS / SIG_ST
+  const uint8_t* in;           // n_in * 64
+  size_t n_in;
+  const uint8_t* out;          // n_out * 64 (issue: tokens)
+  size_t n_out;
+  der::Span proof;
+};
+
+struct ActionState {
+  int32_t host_final = -1;     // verdict decided on the host (MALFORMED / TAS_INVALID)
+  bool sig_on_device = false;
+  int sig_index = -1;          // index in the device sigma batch
+  bool rc_applicable = false;
+  int rp_base = -1, rp_count = 0;
+  bool rc_count_bad = false;
+};
+}  // namespace
+
+static int verify_actions(fts_ctx* c, const std::vector<ActionIn>& acts, int32_t* status, int32_t* fail_index) {
+  const int k = c->k, n = c->n, npts_rp = rp_npts(k);
+  const size_t A = acts.size();
+  std::vector<ActionState> st(A);
+  // host-side decoding (parallel over actions)
+  struct Parsed {
+    std::vector<uint8_t> sig_raw;   // CT, in..., out...  (64 B each)
+    std::vector<uint32_t> sig_sc;   // scalars
+    int chal_canonical = 0;
+    std::vector<uint8_t> rp_raw;
+    std::vector<uint32_t> rp_sc;
+    std::vector<int32_t> rp_status, rp_ipa;
+  };
+  std::vector<Parsed> P(A);
+  auto parse_one = [&](size_t i) {
+    const ActionIn& ai = acts[i];
+    ActionState& s = st[i];
+    Parsed& p = P[i];
+    std::vector<der::Span> vals;
+    if (!der::unmarshal_values(ai.proof, vals) || vals.size() != 2) {
+      s.host_final = FTS_E_MALFORMED;
+      return;
+    }
+    s.rc_applicable = ai.kind == SIG_ST || ai.n_in != 1 || ai.n_out != 1;
+    // ---- range proofs (deserialised together with the sigma proof)
+    std::vector<der::Span> rps;
+    if (vals[1].n && !parse_range_correctness(vals[1], rps)) {
+      s.host_final = FTS_E_MALFORMED;
+      return;
+    }
+    s.rp_count = (int)rps.size();
+    p.rp_raw.assign(rps.size() * npts_rp * 64, 0);
+    p.rp_sc.assign(rps.size() * RP_NSC * 8, 0);
+    p.rp_status.assign(rps.size(), 0);
+    p.rp_ipa.assign(rps.size(), 0);
+    for (size_t j = 0; j < rps.size(); j++) {
+      uint8_t* pts = &p.rp_raw[j * npts_rp * 64];
+      parse_range_proof(rps[j], k, pts, &p.rp_sc[j * RP_NSC * 8], p.rp_status[j], p.rp_ipa[j]);
+      filler_point(pts + RP_PT_V * 64);
+      if (p.rp_status[j] == FTS_E_MALFORMED) {
+        s.host_final = FTS_E_MALFORMED;
+        return;
+      }
+      if (!s.rc_applicable) {  // never verified, but must deserialise (points decode)
+        G1A tmp;
+        for (int q = 0; q < npts_rp; q++)
+          if (q != RP_PT_V && !g1_from_bytes(pts + q * 64, 64, tmp)) {
+            s.host_final = FTS_E_MALFORMED;
+            return;
+          }
+      }
+    }
+    if (s.rc_applicable) s.rc_count_bad = rps.size() != ai.n_out;
+    // ---- sigma proof
+    p.sig_raw.assign((1 + ai.n_in + ai.n_out) * 64, 0);
+    for (size_t j = 0; j < ai.n_in; j++) memcpy(&p.sig_raw[(1 + j) * 64], ai.in + 64 * j, 64);
+    for (size_t j = 0; j < ai.n_out; j++) memcpy(&p.sig_raw[(1 + ai.n_in + j) * 64], ai.out + 64 * j, 64);
+    bool nil_fields = false, panic = false;
+    Elem e[7];
+    int ne = ai.kind == SIG_TAS ? 7 : 4;
+    if (vals[0].n) {
+      Unmarshaller u(vals[0]);
+      if (!u.ok) {
+        s.host_final = FTS_E_MALFORMED;
+        return;
+      }
+      for (int f = 0; f < ne; f++)
+        if (!u.next(e[f])) {
+          s.host_final = FTS_E_MALFORMED;
+          return;
+        }
+    }
+    // element kinds: TAS [CT g1, ibf arr, iv arr, Type, TBF, EqSum, Chal]; ST [Type, BF, Chal, CT g1]
+    const int ct_idx = ai.kind == SIG_TAS ? 0 : 3;
+    if (e[ct_idx].present) {
+      if (e[ct_idx].raw.n != 64) {
+        s.host_final = FTS_E_MALFORMED;
+        return;
+      }
+      memcpy(&p.sig_raw[0], e[ct_idx].raw.p, 64);
+    }
+    std::vector<der::Span> ibf, iv;
+    if (ai.kind == SIG_TAS) {
+      if (e[1].present && !der::unmarshal_values(e[1].raw, ibf, true)) return void(s.host_final = FTS_E_MALFORMED);
+      if (e[2].present && !der::unmarshal_values(e[2].raw, iv, true)) return void(s.host_final = FTS_E_MALFORMED);
+      // typeandsum.go:231: nil TBF/Type/CT/EqSum -> "invalid sum and type proof"
+      nil_fields = !e[4].present || !e[3].present || !e[0].present || !e[5].present;
+      if (!nil_fields) {
+        // :242-251 would panic on a nil challenge or short/nil InputValues / InputBlindingFactors
+        if (!e[6].present || !e[2].present || !e[1].present || iv.size() < ai.n_in || ibf.size() < ai.n_in)
+          panic = true;
+      }
+      // transfer.go:175: the range goroutine dereferences CommitmentToType
+      if (s.rc_applicable && !e[0].present) panic = true;
+      if (!nil_fields && !panic) {
+        p.sig_sc.assign((4 + 2 * ai.n_in) * 8, 0);
+        scalar_from_bytes(e[3].raw, &p.sig_sc[TAS_SC_TYPE * 8], nullptr);
+        scalar_from_bytes(e[4].raw, &p.sig_sc[TAS_SC_TBF * 8], nullptr);
+        scalar_from_bytes(e[5].raw, &p.sig_sc[TAS_SC_EQ * 8], nullptr);
+        bool canon;
+        scalar_from_bytes(e[6].raw, &p.sig_sc[TAS_SC_CHAL * 8], &canon);
+        p.chal_canonical = canon;
+        for (size_t j = 0; j < ai.n_in; j++) {
+          scalar_from_bytes(iv[j], &p.sig_sc[(TAS_SC_IV + j) * 8], nullptr);
+          scalar_from_bytes(ibf[j], &p.sig_sc[(TAS_SC_IV + ai.n_in + j) * 8], nullptr);
+        }
+      }
+    } else {
+      // sametype.go:169-171 dereferences every field
+      if (!e[0].present || !e[1].present || !e[2].present || !e[3].present) panic = true;
+      else {
+        p.sig_sc.assign(3 * 8, 0);
+        scalar_from_bytes(e[0].raw, &p.sig_sc[ST_SC_TYPE * 8], nullptr);
+        scalar_from_bytes(e[1].raw, &p.sig_sc[ST_SC_BF * 8], nullptr);
+        bool canon;
+        scalar_from_bytes(e[2].raw, &p.sig_sc[ST_SC_CHAL * 8], &canon);
+        p.chal_canonical = canon;
+      }
+    }
+    if (panic) {
+      s.host_final = FTS_E_MALFORMED;
+      return;
+    }
+    // element arrays / CT must still decode even when the proof is rejected for nil fields
+    if (nil_fields) {
+      G1A tmp;
+      if (e[0].present && !g1_from_bytes(&p.sig_raw[0], 64, tmp)) return void(s.host_final = FTS_E_MALFORMED);
+      s.host_final = FTS_E_TAS_INVALID;
+      // range proofs may still carry malformed points: check them on the host
+      for (size_t j = 0; j < rps.size(); j++)
+        for (int q = 0; q < npts_rp; q++)
+          if (q != RP_PT_V && !g1_from_bytes(&p.rp_raw[(j * npts_rp + q) * 64], 64, tmp))
+            return void(s.host_final = FTS_E_MALFORMED);
+      return;
+    }
+    s.sig_on_device = true;
+  };
+  {
+    unsigned nth = A >= 64 ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nth; t++)
+      th.emplace_back([&]() {
+        for (size_t i; (i = next++) < A;) parse_one(i);
+      });
+    for (auto& t : th) t.join();
+  }
+  // ---- assemble device batches
+  std::vector<SigAction> sact;
+  std::vector<int32_t> s_owner, s_affoff, s_status;
+  std::vector<uint8_t> s_raw;
+  std::vector<uint32_t> s_sc;
+  std::vector<int2> s_work;
+  std::vector<uint8_t> r_raw;
+  std::vector<uint32_t> r_sc;
+  std::vector<int32_t> r_status, r_ipa;
+  int term_off = 0, aff_off = 0, pt_off = 0, sc_off = 0, rp_total = 0;
+  uint32_t msg_off = 0;
+  std::vector<int> sig_of(A, -1);
+  for (size_t i = 0; i < A; i++) {
+    ActionState& s = st[i];
+    if (s.host_final >= 0) continue;
+    const ActionIn& ai = acts[i];
+    Parsed& p = P[i];
+    if (s.rc_applicable && s.rp_count > 0) {
+      s.rp_base = rp_total;
+      rp_total += s.rp_count;
+      r_raw.insert(r_raw.end(), p.rp_raw.begin(), p.rp_raw.end());
+      r_sc.insert(r_sc.end(), p.rp_sc.begin(), p.rp_sc.end());
+      r_status.insert(r_status.end(), p.rp_status.begin(), p.rp_status.end());
+      r_ipa.insert(r_ipa.end(), p.rp_ipa.begin(), p.rp_ipa.end());
+    }
+    SigAction sa{};
+    sa.kind = ai.kind;
+    sa.n_in = ai.kind == SIG_TAS ? (int)ai.n_in : 0;
+    sa.n_out = (int)ai.n_out;
+    sa.pt_off = pt_off;
+    sa.sc_off = sc_off;
+    sa.term_off = term_off;
+    sa.msg_off = (int32_t)msg_off;
+    sa.rp_base = s.rp_base;
+    sa.rp_count = s.rp_count;
+    sa.chal_canonical = p.chal_canonical;
+    const int npt = 1 + sa.n_in + sa.n_out;
+    s_raw.insert(s_raw.end(), p.sig_raw.begin(), p.sig_raw.begin() + npt * 64);
+    for (int q = 0; q < npt; q++) s_owner.push_back((int32_t)sact.size());
+    s_sc.insert(s_sc.end(), p.sig_sc.begin(), p.sig_sc.end());
+    const int nt = sig_nterms(sa.kind, sa.n_in);
+    for (int t = 0; t < nt; t++) s_work.push_back(make_int2((int)sact.size(), t));
+    s_affoff.push_back(aff_off);
+    s_status.push_back(0);
+    pt_off += npt;
+    sc_off += sig_nscalars(sa.kind, sa.n_in);
+    term_off += nt;
+    aff_off += sig_naff(sa.kind, sa.n_in, sa.n_out);
+    msg_off += sig_msg_slot(sa.kind, sa.n_in, sa.n_out);
+    sig_of[i] = (int)sact.size();
+    sact.push_back(sa);
+  }
+  const int SA = (int)sact.size();
+  Workspace& w = c->ws;
+  if (SA) {
+    if (w.s_act.ensure(SA * sizeof(SigAction)) || w.s_raw.ensure(s_raw.size()) || w.s_owner.ensure(s_owner.size() * 4) ||
+        w.s_pts.ensure((size_t)pt_off * 64) || w.s_sc.ensure(std::max<size_t>(s_sc.size(), 1) * 4) ||
+        w.s_status.ensure(SA * 4) || w.s_work.ensure(s_work.size() * sizeof(int2)) ||
+        w.s_terms.ensure((size_t)term_off * 96) || w.s_aff.ensure((size_t)aff_off * 64) ||
+        w.s_affoff.ensure(SA * 4) || w.s_msgs.ensure(msg_off) || w.s_jac.ensure((size_t)aff_off * 96) ||
+        w.s_scratch.ensure(s_work.size() * 10 * 24 * 4))
+      return FTS_API_ENOMEM;
+    HIP_OK(hipMemcpyAsync(w.s_act.p, sact.data(), SA * sizeof(SigAction), hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(w.s_raw.p, s_raw.data(), s_raw.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(w.s_owner.p, s_owner.data(), s_owner.size() * 4, hipMemcpyHostToDevice, c->stream));
+    if (!s_sc.empty())
+      HIP_OK(hipMemcpyAsync(w.s_sc.p, s_sc.data(), s_sc.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(w.s_status.p, s_status.data(), SA * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(w.s_work.p, s_work.data(), s_work.size() * sizeof(int2), hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(w.s_affoff.p, s_affoff.data(), SA * 4, hipMemcpyHostToDevice, c->stream));
+  }
+  if (rp_total) {
+    if (w.rp_raw.ensure(r_raw.size()) || w.rp_sc.ensure(r_sc.size() * 4) || w.rp_status.ensure(rp_total * 4) ||
+        w.rp_ipa.ensure(rp_total * 4))
+      return FTS_API_ENOMEM;
+    HIP_OK(hipMemcpyAsync(w.rp_raw.p, r_raw.data(), r_raw.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(w.rp_sc.p, r_sc.data(), r_sc.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(w.rp_status.p, r_status.data(), rp_total * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(w.rp_ipa.p, r_ipa.data(), rp_total * 4, hipMemcpyHostToDevice, c->stream));
+  }
+  SigBatchDev sd{};
+  if (SA) {
+    sd.A = SA;
+    sd.npts = pt_off;
+    sd.nwork = (int)s_work.size();
+    sd.act = w.s_act.as<SigAction>();
+    sd.raw = w.s_raw.as<uint8_t>();
+    sd.pt_owner = w.s_owner.as<int32_t>();
+    sd.pts = w.s_pts.as<uint32_t>();
+    sd.sc = w.s_sc.as<uint32_t>();
+    sd.status = w.s_status.as<int32_t>();
+    sd.work = w.s_work.as<int2>();
+    sd.terms = w.s_terms.as<uint32_t>();
+    sd.aff = w.s_aff.as<uint32_t>();
+    sd.aff_off = w.s_affoff.as<int32_t>();
+    sd.msgs = w.s_msgs.as<uint8_t>();
+    sd.jac = w.s_jac.as<uint32_t>();
+    sd.scratch = w.s_scratch.as<uint32_t>();
+    sd.rp_raw = rp_total ? w.rp_raw.as<uint8_t>() : nullptr;
+    sd.rp_k = k;
+    launch_sig_prep(sd, c->stream);
+  }
+  if (rp_total) {
+    int rc = launch_rp(c, rp_total, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
+                       w.rp_ipa.as<int32_t>());
+    if (rc != FTS_API_OK) return rc;
+  }
+  if (SA) launch_sig_finish(sd, c->d_tables, n, c->stream);
+  HIP_OK(hipGetLastError());
+  std::vector<int32_t> sig_res(SA), rp_res(rp_total);
+  if (SA) HIP_OK(hipMemcpyAsync(sig_res.data(), w.s_status.p, SA * 4, hipMemcpyDeviceToHost, c->stream));
+  if (rp_total) HIP_OK(hipMemcpyAsync(rp_res.data(), w.rp_status.p, rp_total * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  // ---- combine with the reference's precedence
+  for (size_t i = 0; i < A; i++) {
+    const ActionState& s = st[i];
+    int32_t out = FTS_OK, idx = -1;
+    if (s.host_final >= 0) {
+      out = s.host_final;
+    } else {
+      int32_t sig = sig_res[sig_of[i]];
+      bool malformed = sig == FTS_E_MALFORMED;
+      for (int j = 0; j < s.rp_count && s.rp_base >= 0; j++) malformed |= rp_res[s.rp_base + j] == FTS_E_MALFORMED;
+      if (malformed) {
+        out = FTS_E_MALFORMED;                       // deserialisation precedes verification
+      } else if (sig != FTS_OK) {
+        out = sig;                                   // TypeAndSum / SameType error wins (transfer.go:192-196)
+      } else if (s.rc_applicable) {
+        if (s.rc_count_bad) {
+          out = FTS_E_RC_COUNT;                      // rangecorrectness.go:138-140
+        } else {
+          for (int j = 0; j < s.rp_count; j++)       // first failing index wins (:141-160)
+            if (rp_res[s.rp_base + j] != FTS_OK) {
+              out = rp_res[s.rp_base + j];
+              idx = j;
+              break;
+            }
+        }
+      }
+    }
+    status[i] = out;
+    if (fail_index) fail_index[i] = idx;
+  }
+  return FTS_API_OK;
+}
+
+extern "C" {
+
+int fts_transfer_verify_batch(fts_ctx* c, size_t n, const fts_transfer_item* items, int32_t* status,
+                              int32_t* fail_index) {
+  if (!c || !status || (n && !items)) return FTS_API_EINVAL;
+  if (c->device < 0) return FTS_API_EDEVICE;
+  if (n == 0) return FTS_API_OK;
+  std::vector<ActionIn> acts(n);
+  for (size_t i = 0; i < n; i++)
+    acts[i] = ActionIn{SIG_TAS, items[i].inputs, items[i].n_in, items[i].outputs, items[i].n_out,
+                       der::Span{items[i].proof, items[i].proof ? items[i].proof_len : 0}};
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  int rc = verify_actions(c, acts, status, fail_index);
+  if (rc != FTS_API_OK)
+    for (size_t i = 0; i < n; i++) status[i] = FTS_E_NOT_RUN;
+  return rc;
+}
+
+int fts_issue_verify_batch(fts_ctx* c, size_t n, const fts_issue_item* items, int32_t* status, int32_t* fail_index) {
+  if (!c || !status || (n && !items)) return FTS_API_EINVAL;
+  if (c->device < 0) return FTS_API_EDEVICE;
+  if (n == 0) return FTS_API_OK;
+  std::vector<ActionIn> acts(n);
+  for (size_t i = 0; i < n; i++)
+    acts[i] = ActionIn{SIG_ST, nullptr, 0, items[i].tokens, items[i].n_tok,
+                       der::Span{items[i].proof, items[i].proof ? items[i].proof_len : 0}};
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  int rc = verify_actions(c, acts, status, fail_index);
+  if (rc != FTS_API_OK)
+    for (size_t i = 0; i < n; i++) status[i] = FTS_E_NOT_RUN;
+  return rc;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ prover
+static const ProverTables& prover_tables(const fts_ctx* cc) {
+  fts_ctx* c = const_cast<fts_ctx*>(cc);
+  std::call_once(c->prover_once, [&]() { build_prover_tables(c->pp, c->n, c->ptab); });
+  return c->ptab;
+}
+
+static bool fr_arg(const uint8_t* b32, Fr& out) {
+  if (!b32) return false;
+  out = fr_from_be(b32);
+  return true;
+}
+
+int fts_token_commit(const fts_ctx* c, const uint8_t* type, size_t type_len, uint64_t value, const uint8_t* bf32,
+                     uint8_t* com64_out) {
+  Fr bf;
+  if (!c || !com64_out || !fr_arg(bf32, bf)) return FTS_API_EINVAL;
+  const ProverTables& T = prover_tables(c);
+  G1A t = token_commit(T, type_to_zr(type, type_len), value, bf);
+  g1_to_bytes(t, com64_out);
+  return FTS_API_OK;
+}
+
+int fts_rp_prove(const fts_ctx* c, uint64_t value, const uint8_t* bf32, uint64_t seed, uint8_t* out_der,
+                 size_t out_cap, size_t* out_len, uint8_t* com64_out) {
+  Fr bf;
+  if (!c || !out_der || !out_len || !fr_arg(bf32, bf)) return FTS_API_EINVAL;
+  const ProverTables& T = prover_tables(c);
+  Msm vm;
+  vm.add_fb(T.ped(1), fr_u64(value));
+  vm.add_fb(T.ped(2), bf);
+  G1A V = vm.aff();
+  Rng rng(seed);
+  RangeProofOut rp = prove_range(T, c->pp, c->n, c->k, V, value, bf, rng);
+  std::string s = rp.serialize();
+  *out_len = s.size();
+  if (s.size() > out_cap) return FTS_API_ESIZE;
+  memcpy(out_der, s.data(), s.size());
+  if (com64_out) g1_to_bytes(V, com64_out);
+  return FTS_API_OK;
+}
+
+int fts_rp_prove_batch(const fts_ctx* c, size_t n, const uint64_t* values, const uint8_t* bfs, uint64_t seed,
+                       int threads, uint8_t* out, size_t out_cap, size_t* offsets, size_t* lens,
+                       uint8_t* com64_out) {
+  if (!c || !values || !bfs || !out || !offsets || !lens || !com64_out) return FTS_API_EINVAL;
+  const ProverTables& T = prover_tables(c);
+  std::vector<std::string> res(n);
+  std::atomic<size_t> next{0};
+  int nth = threads > 0 ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  std::vector<std::thread> th;
+  for (int t = 0; t < nth; t++)
+    th.emplace_back([&]() {
+      for (size_t i; (i = next++) < n;) {
+        Fr bf = fr_from_be(bfs + 32 * i);
+        Msm vm;
+        vm.add_fb(T.ped(1), fr_u64(values[i]));
+        vm.add_fb(T.ped(2), bf);
+        G1A V = vm.aff();
+        Rng rng(seed + i);
+        res[i] = prove_range(T, c->pp, c->n, c->k, V, values[i], bf, rng).serialize();
+        g1_to_bytes(V, com64_out + 64 * i);
+      }
+    });
+  for (auto& t : th) t.join();
+  size_t off = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (off + res[i].size() > out_cap) return FTS_API_ESIZE;
+    memcpy(out + off, res[i].data(), res[i].size());
+    offsets[i] = off;
+    lens[i] = res[i].size();
+    off += res[i].size();
+  }
+  return FTS_API_OK;
+}
+
+int fts_transfer_prove(const fts_ctx* c, const uint8_t* type, size_t type_len, size_t n_in, const uint64_t* in_values,
+                       const uint8_t* in_bfs, size_t n_out, const uint64_t* out_values, const uint8_t* out_bfs,
+                       uint64_t seed, uint8_t* out_der, size_t out_cap, size_t* out_len) {
+  if (!c || !out_der || !out_len || !n_in || !n_out) return FTS_API_EINVAL;
+  const ProverTables& T = prover_tables(c);
+  std::vector<uint64_t> iv(in_values, in_values + n_in), ov(out_values, out_values + n_out);
+  std::vector<Fr> ib(n_in), ob(n_out);
+  for (size_t i = 0; i < n_in; i++) ib[i] = fr_from_be(in_bfs + 32 * i);
+  for (size_t i = 0; i < n_out; i++) ob[i] = fr_from_be(out_bfs + 32 * i);
+  Rng rng(seed);
+  std::string s = prove_transfer(T, c->pp, c->n, c->k, type_to_zr(type, type_len), iv, ib, ov, ob, rng);
+  *out_len = s.size();
+  if (s.size() > out_cap) return FTS_API_ESIZE;
+  memcpy(out_der, s.data(), s.size());
+  return FTS_API_OK;
+}
+
+int fts_issue_prove(const fts_ctx* c, const uint8_t* type, size_t type_len, size_t n_tok, const uint64_t* values,
+                    const uint8_t* bfs, uint64_t seed, uint8_t* out_der, size_t out_cap, size_t* out_len) {
+  if (!c || !out_der || !out_len || !n_tok) return FTS_API_EINVAL;
+  const ProverTables& T = prover_tables(c);
+  std::vector<uint64_t> v(values, values + n_tok);
+  std::vector<Fr> b(n_tok);
+  for (size_t i = 0; i < n_tok; i++) b[i] = fr_from_be(bfs + 32 * i);
+  Rng rng(seed);
+  std::string s = prove_issue(T, c->pp, c->n, c->k, type_to_zr(type, type_len), v, b, rng);
+  *out_len = s.size();
+  if (s.size() > out_cap) return FTS_API_ESIZE;
+  memcpy(out_der, s.data(), s.size());
+  return FTS_API_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,472 @@
+// Range-proof (Bulletproof + IPA) batch verification kernels for gfx950.
+//
+// One launch sequence verifies a whole batch of B proofs of bit length n
+// (k = log2 n rounds).  Work is laid out per (proof, item) so a batch of a
+// few thousand proofs fills the 256 CUs:
+//
+//   k_rp_decode        (proof, point)   NewG1FromBytes checks + Montgomery form
+//   k_rp_challenges    proof            x, y, z, x_j transcripts (SHA-256 over hex)
+//                                        + Fr side (polEval, inverses)   bulletproof.go:266-311, ipa.go:229-244
+//   k_rp_hprime        (proof, i)       H'_i = y^-i * H_i  fixed-base    bulletproof.go:483-489
+//   k_rp_hp_normalize  proof            batch affine normalisation (Montgomery trick)
+//   k_rp_com           proof            com = x*D + C + z*K + z^2*W - delta*P   bulletproof.go:477-492
+//                                        (K = sum H_i - sum G_i, W = sum 2^i H'_i: same group element)
+//   k_rp_x0_build      (proof, record)  DER(hex(H'..., G..., Q, com) "||" Zb(ip))   ipa.go:200-212
+//   k_rp_x0_hash       proof            x0 = HashToZr(...)                ipa.go:213
+//   k_rp_terms_fixed   (proof, term)    fixed-base terms of E1 / E2
+//   k_rp_terms_var     (proof, term)    variable-base terms of E1 / E2
+//   k_rp_check         proof            E1 == O ("invalid range proof"), E2 == O ("invalid IPA")
+//
+// E1: (ip - polEval) G + tau H - x T1 - x^2 T2 - z^2 V            (bulletproof.go:314-324)
+// E2: sum a s_i G_i + sum b s_i^-1 y^-i H_i + (ab - ip) x0 Q - com
+//     - sum x_j^2 L_j - sum x_j^-2 R_j                              (ipa.go:214-259 unrolled:
+//     G_fin = sum s_i G_i, H'_fin = sum s_i^-1 H'_i, s_i = prod_j x_j^{+-1} by bit k-1-j of i)
+#include "device/g1.hpp"
+#include "device/rp_kernels.hpp"
+#include "device/transcript.hpp"
+#include "device/helpers.hpp"
+#include "../../include/fts_gpu.h"
+
+namespace fts {
+
+// ---------------------------------------------------------- context tables
+// thread per (base, window w): entries d * 2^(8w) * B for d = 1..128, affine.
+// scratch: [nb*32][128][32] words (Jacobian point + prefix product)
+__global__ void __launch_bounds__(64) k_build_tables(const uint32_t* __restrict__ bases, int nb,
+                                                     uint32_t* __restrict__ tables, uint32_t* __restrict__ scratch) {
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= nb * FB_WINDOWS) return;
+  int b = gid / FB_WINDOWS, w = gid % FB_WINDOWS;
+  G1A B = load_g1a(bases + b * 16);
+  G1J bw = g1j_from_affine(B);
+  for (int i = 0; i < 8 * w; i++) bw = nl_dbl(bw);
+  uint32_t* J = scratch + (size_t)gid * FB_ENTRIES * 32;
+  G1J acc = bw;
+  Fp pre = f_one<FpP>();
+  for (int d = 1; d <= FB_ENTRIES; d++) {
+    if (d > 1) acc = nl_add_mem(acc, J, 0);  // J[0] holds bw
+    store_g1j(J + (d - 1) * 32, acc);
+    store_fp(J + (d - 1) * 32 + 24, pre);
+    if (!f_is_zero(acc.z)) pre = fp_mul(pre, acc.z);
+  }
+  Fp inv = nl_fp_inv(pre);
+  uint32_t* T = tables + (size_t)b * FB_WORDS_PER_BASE + (size_t)w * FB_ENTRIES * 16;
+  for (int d = FB_ENTRIES; d >= 1; d--) {
+    G1J p = load_g1j(J + (d - 1) * 32);
+    G1A a;
+    if (f_is_zero(p.z)) {
+      a.x = f_zero<FpP>();
+      a.y = f_zero<FpP>();
+    } else {
+      Fp pr;
+      load_fp(J + (d - 1) * 32 + 24, pr);
+      Fp zi = fp_mul(inv, pr);
+      inv = fp_mul(inv, p.z);
+      Fp zi2 = fp_sqr(zi);
+      a.x = fp_mul(p.x, zi2);
+      a.y = fp_mul(fp_mul(p.y, zi2), zi);
+    }
+    store_g1a(T + (d - 1) * 16, a);
+  }
+}
+
+// ------------------------------------------------------------------ decode
+// NewG1FromBytes (asn1.go:148 -> gnark SetBytes): 64 bytes, flag bits 00,
+// canonical coordinates, on the curve; 64 zero bytes = identity.
+__global__ void __launch_bounds__(256) k_rp_decode(int B, int npts, const uint8_t* __restrict__ raw,
+                                                   uint32_t* __restrict__ pts, int32_t* __restrict__ status) {
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= B * npts) return;
+  G1A a;
+  if (!decode_point(raw + (size_t)gid * 64, a)) status[gid / npts] = FTS_E_MALFORMED;
+  store_g1a(pts + (size_t)gid * 16, a);
+}
+
+// -------------------------------------------------------------- challenges
+__global__ void __launch_bounds__(64) k_rp_challenges(int B, int n, int k, const uint8_t* __restrict__ raw,
+                                                      const int32_t* __restrict__ status, uint32_t* __restrict__ ch,
+                                                      uint8_t* __restrict__ small_msgs) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B || status[b] != 0) return;
+  const int npts = rp_npts(k);
+  const uint8_t* P = raw + (size_t)b * npts * 64;
+  uint8_t* slot = small_msgs + (size_t)b * SMALL_SLOT;
+  uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
+
+  // x = Hz(Arr(T1, T2))                                  bulletproof.go:266-273
+  const uint8_t* px[2] = {P + RP_PT_T1 * 64, P + RP_PT_T2 * 64};
+  Fr x = f_to_mont(hash_raw_points(slot, px, 2));
+  // y = Hz(Arr(C, D, V)); z = Hz(Zb(y))                  bulletproof.go:276-282
+  const uint8_t* py[3] = {P + RP_PT_C * 64, P + RP_PT_D * 64, P + RP_PT_V * 64};
+  Fr yc = hash_raw_points(slot, py, 3);
+  uint32_t w[16], st[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = yc.v[7 - i];
+  w[8] = 0x80000000u;
+#pragma unroll
+  for (int i = 9; i < 15; i++) w[i] = 0;
+  w[15] = 256;
+  sha256_init(st);
+  sha256_compress(st, w);
+  Fr z = f_to_mont(digest_to_fr(st));
+  Fr y = f_to_mont(yc);
+
+  Fr x2 = fr_sqr(x), z2 = fr_sqr(z), z3 = fr_mul(z2, z);
+  // ipy = sum y^i, ip2 = sum 2^i                           bulletproof.go:287-305
+  Fr yp = f_one<FrP>(), ipy = f_zero<FrP>(), p2 = f_one<FrP>(), ip2 = f_zero<FrP>();
+  for (int i = 0; i < n; i++) {
+    if (i) {
+      yp = fr_mul(yp, y);
+      p2 = f_dbl(p2);
+    }
+    ipy = f_add(ipy, yp);
+    ip2 = f_add(ip2, p2);
+  }
+  Fr pol = f_sub(fr_mul(f_sub(z, z2), ipy), fr_mul(z3, ip2));  // bulletproof.go:307-311
+
+  store_f(C + CH_X * 8, x);
+  store_f(C + CH_X2 * 8, x2);
+  store_f(C + CH_Y * 8, y);
+  store_f(C + CH_YINV * 8, nl_fr_inv(y));
+  store_f(C + CH_Z * 8, z);
+  store_f(C + CH_Z2 * 8, z2);
+  store_f(C + CH_POL * 8, pol);
+  // round challenges x_j = Hz(Arr(L_j, R_j))             ipa.go:229-238
+  for (int j = 0; j < k; j++) {
+    const uint8_t* pl[2] = {P + (RP_PT_L + j) * 64, P + (RP_PT_L + k + j) * 64};
+    Fr xj = f_to_mont(hash_raw_points(slot, pl, 2));
+    store_f(C + (CH_XJ + j) * 8, xj);
+    store_f(C + (CH_XJ + k + j) * 8, nl_fr_inv(xj));
+  }
+}
+
+// --------------------------------------------------------------------- H'
+__global__ void __launch_bounds__(64) k_rp_hprime(int B, int n, int k, const int32_t* __restrict__ status,
+                                                  const uint32_t* __restrict__ ch, const uint32_t* __restrict__ tables,
+                                                  uint32_t* __restrict__ hpj) {
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= B * n) return;
+  int b = gid / n, i = gid % n;
+  if (status[b] != 0) return;
+  Fr yinv;
+  load_f(ch + ((size_t)b * rp_nch(k) + CH_YINV) * 8, yinv);
+  G1J r = fixed_base_mul(tables + (size_t)(n + i) * FB_WORDS_PER_BASE, fr_canon(fr_pow_small(yinv, (uint32_t)i)));
+  store_g1j(hpj + (size_t)gid * 24, r);
+}
+
+// batch affine normalisation of the n H'_i of one proof
+__global__ void __launch_bounds__(64) k_rp_hp_normalize(int B, int n, const int32_t* __restrict__ status,
+                                                        const uint32_t* __restrict__ hpj, uint32_t* __restrict__ hpa,
+                                                        uint8_t* __restrict__ hp_be) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B || status[b] != 0) return;
+  const uint32_t* J = hpj + (size_t)b * n * 24;
+  uint32_t* A = hpa + (size_t)b * n * 16;
+  Fp acc = f_one<FpP>();
+  for (int i = 0; i < n; i++) {
+    store_fp(A + i * 16, acc);  // prefix product
+    Fp z;
+    load_fp(J + i * 24 + 16, z);
+    if (!f_is_zero(z)) acc = fp_mul(acc, z);
+  }
+  Fp inv = nl_fp_inv(acc);
+  for (int i = n - 1; i >= 0; i--) {
+    G1J p = load_g1j(J + i * 24);
+    G1A a;
+    if (f_is_zero(p.z)) {
+      a.x = f_zero<FpP>();
+      a.y = f_zero<FpP>();
+    } else {
+      Fp pr;
+      load_fp(A + i * 16, pr);
+      Fp zi = fp_mul(inv, pr);
+      inv = fp_mul(inv, p.z);
+      Fp zi2 = fp_sqr(zi);
+      a.x = fp_mul(p.x, zi2);
+      a.y = fp_mul(fp_mul(p.y, zi2), zi);
+    }
+    store_g1a(A + i * 16, a);
+    uint32_t pw[16];
+    g1_mont_to_be_words(a.x, a.y, pw);
+    uint4* d = reinterpret_cast<uint4*>(hp_be + ((size_t)b * n + i) * 64);
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      d[q] = make_uint4(__builtin_bswap32(pw[4 * q]), __builtin_bswap32(pw[4 * q + 1]),
+                        __builtin_bswap32(pw[4 * q + 2]), __builtin_bswap32(pw[4 * q + 3]));
+  }
+}
+
+// -------------------------------------------------------------------- com
+__global__ void __launch_bounds__(64) k_rp_com(int B, int n, int k, const int32_t* __restrict__ status,
+                                               const uint32_t* __restrict__ pts, const uint32_t* __restrict__ sc,
+                                               const uint32_t* __restrict__ ch, const uint32_t* __restrict__ hpa,
+                                               const uint32_t* __restrict__ tables, uint32_t* __restrict__ com,
+                                               uint8_t* __restrict__ com_be, uint32_t* __restrict__ scratch) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B || status[b] != 0) return;
+  const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
+  const uint32_t* A = hpa + (size_t)b * n * 16;
+  const uint32_t* Pt = pts + (size_t)b * rp_npts(k) * 16;
+  uint32_t* scr = scratch + (size_t)b * 10 * 24;  // 8 table entries + affine copy + temp
+  uint32_t* tmp = scr + 9 * 24;
+  // W = sum 2^i H'_i (Horner)
+  G1J W = g1j_from_affine(load_g1a(A + (n - 1) * 16));
+  for (int i = n - 2; i >= 0; i--) W = nl_madd_mem(nl_dbl(W), A + i * 16, 0);
+  G1A Wa = nl_to_affine(W);
+  Fr x, z, z2;
+  load_f(C + CH_X * 8, x);
+  load_f(C + CH_Z * 8, z);
+  load_f(C + CH_Z2 * 8, z2);
+  G1J acc = var_base_mul(load_g1a(Pt + RP_PT_D * 16), fr_canon(x), scr);                     // x*D
+  acc = nl_madd_mem(acc, Pt + RP_PT_C * 16, 0);                                                // + C
+  acc = add_via(tmp, acc, fixed_base_mul(tables + (size_t)tb_K(n) * FB_WORDS_PER_BASE, fr_canon(z)));  // + z*K
+  acc = add_via(tmp, acc, var_base_mul(Wa, fr_canon(z2), scr));                               // + z^2*W
+  Scalar s;
+  {
+    Fr d;
+    load_f(sc + ((size_t)b * RP_NSC + RP_SC_DELTA) * 8, d);
+    Fr nd = f_neg(d);  // canonical negation: r - delta
+#pragma unroll
+    for (int i = 0; i < 8; i++) s.v[i] = nd.v[i];
+  }
+  acc = add_via(tmp, acc, fixed_base_mul(tables + (size_t)tb_P(n) * FB_WORDS_PER_BASE, s));  // - delta*P
+  G1A ca = nl_to_affine(acc);
+  store_g1a(com + (size_t)b * 16, ca);
+  uint32_t pw[16];
+  g1_mont_to_be_words(ca.x, ca.y, pw);
+  uint4* d = reinterpret_cast<uint4*>(com_be + (size_t)b * 64);
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+    d[q] = make_uint4(__builtin_bswap32(pw[4 * q]), __builtin_bswap32(pw[4 * q + 1]), __builtin_bswap32(pw[4 * q + 2]),
+                      __builtin_bswap32(pw[4 * q + 3]));
+}
+
+// --------------------------------------------------------- x0 transcript
+// thread per (proof, record r in [0, 2n+2]); record 2n+2 writes DER framing
+__global__ void __launch_bounds__(256) k_rp_x0_build(int B, int n, const int32_t* __restrict__ status,
+                                                     const uint8_t* __restrict__ hp_be, const uint8_t* __restrict__ com_be,
+                                                     const uint8_t* __restrict__ x0_const, const uint32_t* __restrict__ sc,
+                                                     uint8_t* __restrict__ msgs) {
+  const int nrec = 2 * n + 3;
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= B * nrec) return;
+  int b = gid / nrec, r = gid % nrec;
+  if (status[b] != 0) return;
+  uint8_t* m = msgs + (size_t)b * x0_slot_bytes(n);
+  const uint32_t A = x0_array_len(n);
+  if (r < n) {
+    uint32_t pw[16];
+    load_be_words(hp_be + ((size_t)b * n + r) * 64, pw);
+    put_hex_record(m, 8 + 130u * r, pw, true);
+  } else if (r < 2 * n + 1) {
+    const uint16_t* src = reinterpret_cast<const uint16_t*>(x0_const + 130u * (r - n));
+    uint16_t* dst = reinterpret_cast<uint16_t*>(m + 8 + 130u * r);
+    for (int q = 0; q < 65; q++) dst[q] = src[q];
+  } else if (r == 2 * n + 1) {
+    uint32_t pw[16];
+    load_be_words(com_be + (size_t)b * 64, pw);
+    put_hex_record(m, 8 + 130u * r, pw, false);
+  } else {
+    uint16_t* m16 = reinterpret_cast<uint16_t*>(m);
+    const uint32_t L = A + 42u;  // SEQUENCE content
+    m16[0] = 0x8230;
+    m16[1] = (uint16_t)((L >> 8) | ((L & 0xffu) << 8));
+    m16[2] = 0x8204;
+    m16[3] = (uint16_t)((A >> 8) | ((A & 0xffu) << 8));
+    uint16_t* t = reinterpret_cast<uint16_t*>(m + 8 + A);
+    t[0] = 0x0204;
+    t[1] = 0x7c7c;
+    t[2] = 0x2004;
+    const uint32_t* ip = sc + ((size_t)b * RP_NSC + RP_SC_IP) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      uint32_t wd = ip[7 - i];  // BE word i
+      t[3 + 2 * i] = (uint16_t)((wd >> 24) | (((wd >> 16) & 0xffu) << 8));
+      t[4 + 2 * i] = (uint16_t)(((wd >> 8) & 0xffu) | ((wd & 0xffu) << 8));
+    }
+    write_sha_padding_u16(m, x0_msg_len(n));
+  }
+}
+
+__global__ void __launch_bounds__(64) k_rp_x0_hash(int B, int n, int k, const int32_t* __restrict__ status,
+                                                   const uint8_t* __restrict__ msgs, uint32_t* __restrict__ ch) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B || status[b] != 0) return;
+  uint32_t st[8];
+  sha256_blocks(msgs + (size_t)b * x0_slot_bytes(n), sha_blocks(x0_msg_len(n)), st);
+  store_f(ch + ((size_t)b * rp_nch(k) + CH_X0) * 8, f_to_mont(digest_to_fr(st)));
+}
+
+// ------------------------------------------------------------------ terms
+// term slots per proof: [0,1] E1 fixed (G, H); [2,3,4] E1 var (T1, T2, V);
+// [5 .. 5+2n] E2 fixed (G_i, H_i, Q); [6+2n .. 6+2n+2k-1] E2 var (L_j, R_j)
+inline __host__ __device__ int rp_nterms(int n, int k) { return 6 + 2 * n + 2 * k; }
+
+FTS_DEV Fr s_vec(const uint32_t* C, int k, int i) {
+  // s_i = prod_j x_j^{+1 if bit (k-1-j) of i else -1}
+  Fr s = f_one<FrP>();
+  for (int j = 0; j < k; j++) {
+    Fr f;
+    int bit = (i >> (k - 1 - j)) & 1;
+    load_f(C + (CH_XJ + (bit ? 0 : k) + j) * 8, f);
+    s = fr_mul(s, f);
+  }
+  return s;
+}
+
+__global__ void __launch_bounds__(64) k_rp_terms_fixed(int B, int n, int k, const int32_t* __restrict__ status,
+                                                       const int32_t* __restrict__ ipa_flag,
+                                                       const uint32_t* __restrict__ sc, const uint32_t* __restrict__ ch,
+                                                       const uint32_t* __restrict__ tables, uint32_t* __restrict__ terms) {
+  const int nf = 3 + 2 * n;  // 2 (E1) + 2n + 1 (E2)
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= B * nf) return;
+  int b = gid / nf, t = gid % nf;
+  if (status[b] != 0) return;
+  const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
+  const uint32_t* S = sc + (size_t)b * RP_NSC * 8;
+  int slot, base;
+  Fr s;
+  if (t < 2) {
+    slot = t;
+    if (t == 0) {  // (ip - polEval) * G
+      Fr pol;
+      load_f(C + CH_POL * 8, pol);
+      s = f_sub(fr_from_canon(S + RP_SC_IP * 8), pol);
+      base = tb_G(n);
+    } else {  // tau * H
+      s = fr_from_canon(S + RP_SC_TAU * 8);
+      base = tb_H(n);
+    }
+  } else {
+    slot = 5 + (t - 2);
+    if (ipa_flag[b] != 0) {
+      store_g1j(terms + ((size_t)b * rp_nterms(n, k) + slot) * 24, g1j_identity());
+      return;
+    }
+    int e = t - 2;
+    if (e < n) {  // a * s_i * G_i
+      s = fr_mul(fr_from_canon(S + RP_SC_A * 8), s_vec(C, k, e));
+      base = e;
+    } else if (e < 2 * n) {  // b * s_i^-1 * y^-i * H_i   (s_i^-1 = s_{n-1-i})
+      int i = e - n;
+      Fr yinv;
+      load_f(C + CH_YINV * 8, yinv);
+      s = fr_mul(fr_mul(fr_from_canon(S + RP_SC_B * 8), s_vec(C, k, n - 1 - i)), fr_pow_small(yinv, (uint32_t)i));
+      base = n + i;
+    } else {  // (a*b - ip) * x0 * Q
+      Fr x0;
+      load_f(C + CH_X0 * 8, x0);
+      Fr ab = fr_mul(fr_from_canon(S + RP_SC_A * 8), fr_from_canon(S + RP_SC_B * 8));
+      s = fr_mul(f_sub(ab, fr_from_canon(S + RP_SC_IP * 8)), x0);
+      base = tb_Q(n);
+    }
+  }
+  G1J r = fixed_base_mul(tables + (size_t)base * FB_WORDS_PER_BASE, fr_canon(s));
+  store_g1j(terms + ((size_t)b * rp_nterms(n, k) + slot) * 24, r);
+}
+
+__global__ void __launch_bounds__(64) k_rp_terms_var(int B, int n, int k, const int32_t* __restrict__ status,
+                                                     const int32_t* __restrict__ ipa_flag,
+                                                     const uint32_t* __restrict__ pts, const uint32_t* __restrict__ ch,
+                                                     uint32_t* __restrict__ terms, uint32_t* __restrict__ scratch) {
+  const int nv = 3 + 2 * k;
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= B * nv) return;
+  int b = gid / nv, t = gid % nv;
+  if (status[b] != 0) return;
+  const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
+  const uint32_t* Pt = pts + (size_t)b * rp_npts(k) * 16;
+  int slot, pt;
+  Fr s;
+  if (t < 3) {
+    slot = 2 + t;
+    int chi = t == 0 ? CH_X : (t == 1 ? CH_X2 : CH_Z2);
+    load_f(C + chi * 8, s);
+    pt = t == 0 ? RP_PT_T1 : (t == 1 ? RP_PT_T2 : RP_PT_V);
+  } else {
+    slot = 6 + 2 * n + (t - 3);
+    if (ipa_flag[b] != 0) {
+      store_g1j(terms + ((size_t)b * rp_nterms(n, k) + slot) * 24, g1j_identity());
+      return;
+    }
+    int j = t - 3;
+    if (j < k) {  // x_j^2 * L_j
+      load_f(C + (CH_XJ + j) * 8, s);
+      s = fr_sqr(s);
+      pt = RP_PT_L + j;
+    } else {  // x_j^-2 * R_j
+      j -= k;
+      load_f(C + (CH_XJ + k + j) * 8, s);
+      s = fr_sqr(s);
+      pt = RP_PT_L + k + j;
+    }
+  }
+  // all variable terms enter with a minus sign
+  G1J r = var_base_mul(load_g1a(Pt + pt * 16), fr_canon(f_neg(s)), scratch + (size_t)gid * 10 * 24);
+  store_g1j(terms + ((size_t)b * rp_nterms(n, k) + slot) * 24, r);
+}
+
+// ------------------------------------------------------------------ check
+__global__ void __launch_bounds__(64) k_rp_check(int B, int n, int k, int32_t* __restrict__ status,
+                                                 const int32_t* __restrict__ ipa_flag,
+                                                 const uint32_t* __restrict__ terms, const uint32_t* __restrict__ com) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B || status[b] != 0) return;
+  const uint32_t* T = terms + (size_t)b * rp_nterms(n, k) * 24;
+  G1J e1 = load_g1j(T);
+  for (int t = 1; t < 5; t++) e1 = nl_add_mem(e1, T + t * 24, 0);
+  if (!g1j_is_identity(e1)) {
+    status[b] = FTS_E_RP_INVALID;
+    return;
+  }
+  if (ipa_flag[b] != 0) {
+    status[b] = ipa_flag[b];
+    return;
+  }
+  G1J e2 = g1j_from_affine(g1a_neg(load_g1a(com + (size_t)b * 16)));
+  for (int t = 5; t < rp_nterms(n, k); t++) e2 = nl_add_mem(e2, T + t * 24, 0);
+  status[b] = g1j_is_identity(e2) ? FTS_OK : FTS_E_IPA_INVALID;
+}
+
+// ------------------------------------------------------------ host launch
+#define FTS_LAUNCH(kern, nthreads, bs, stream, ...)                                   \
+  do {                                                                                \
+    size_t nt_ = (size_t)(nthreads);                                                  \
+    if (nt_) hipLaunchKernelGGL(kern, dim3((unsigned)((nt_ + (bs)-1) / (bs))), dim3(bs), 0, stream, __VA_ARGS__); \
+  } while (0)
+
+
+
+size_t rp_scratch_words(int B, int n, int k) { return (size_t)B * (3 + 2 * k) * 10 * 24; }
+size_t rp_terms_words(int B, int n, int k) { return (size_t)B * rp_nterms(n, k) * 24; }
+
+void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s) {
+  FTS_LAUNCH(k_build_tables, nb * FB_WINDOWS, 64, s, bases, nb, tables, scratch);
+}
+
+// events: array of at least 8 events to time the phases (may be null)
+void launch_rp_verify(const RpBatchDev& d, const uint32_t* tables, const uint8_t* x0_const, hipStream_t s,
+                      hipEvent_t* ev) {
+  const int B = d.B, n = d.n, k = d.k;
+  if (ev) hipEventRecord(ev[0], s);
+  FTS_LAUNCH(k_rp_decode, B * rp_npts(k), 256, s, B, rp_npts(k), d.raw, d.pts, d.status);
+  FTS_LAUNCH(k_rp_challenges, B, 64, s, B, n, k, d.raw, d.status, d.ch, d.small_msgs);
+  if (ev) hipEventRecord(ev[1], s);
+  FTS_LAUNCH(k_rp_hprime, B * n, 64, s, B, n, k, d.status, d.ch, tables, d.hpj);
+  if (ev) hipEventRecord(ev[2], s);
+  FTS_LAUNCH(k_rp_hp_normalize, B, 64, s, B, n, d.status, d.hpj, d.hpa, d.hp_be);
+  FTS_LAUNCH(k_rp_com, B, 64, s, B, n, k, d.status, d.pts, d.sc, d.ch, d.hpa, tables, d.com, d.com_be, d.scratch);
+  if (ev) hipEventRecord(ev[3], s);
+  FTS_LAUNCH(k_rp_x0_build, B * (2 * n + 3), 256, s, B, n, d.status, d.hp_be, d.com_be, x0_const, d.sc, d.x0_msgs);
+  FTS_LAUNCH(k_rp_x0_hash, B, 64, s, B, n, k, d.status, d.x0_msgs, d.ch);
+  if (ev) hipEventRecord(ev[4], s);
+  FTS_LAUNCH(k_rp_terms_fixed, B * (3 + 2 * n), 64, s, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, tables, d.terms);
+  if (ev) hipEventRecord(ev[5], s);
+  FTS_LAUNCH(k_rp_terms_var, B * (3 + 2 * k), 64, s, B, n, k, d.status, d.ipa_flag, d.pts, d.ch, d.terms, d.scratch);
+  if (ev) hipEventRecord(ev[6], s);
+  FTS_LAUNCH(k_rp_check, B, 64, s, B, n, k, d.status, d.ipa_flag, d.terms, d.com);
+  if (ev) hipEventRecord(ev[7], s);
+}
+
+}  // namespace fts

@@ -1,0 +1,198 @@
+// Sigma-proof kernels: TypeAndSum (transfers) and SameType (issues).
+//
+//   k_sig_decode   (point)         NewG1FromBytes checks on CT / inputs / outputs / tokens
+//   k_sig_prep     (action)        in'_i = In_i - CT, out'_j = Out_j - CT, sum = sum in' - sum out'
+//                                  (transfer/typeandsum.go:241-258); V_j = out'_j feeds the
+//                                  range-proof batch (transfer.go:171-185, issue/verifier.go:44-49)
+//   k_sig_terms    (action, term)  fixed-base (ped0/1/2 tables) and variable-base products
+//   k_sig_finish   (action)        inCom_i, sumCom, typeCom (typeandsum.go:249-265) or
+//                                  com (sametype.go:169-171), exact affine, hex transcript,
+//                                  SHA-256, Zr.Equals against the proof's challenge
+#include "device/g1.hpp"
+#include "device/helpers.hpp"
+#include "device/rp_kernels.hpp"
+#include "device/sigma.hpp"
+#include "device/transcript.hpp"
+#include "../../include/fts_gpu.h"
+
+namespace fts {
+
+__global__ void __launch_bounds__(256) k_sig_decode(int npts, const uint8_t* __restrict__ raw,
+                                                    const int32_t* __restrict__ owner, uint32_t* __restrict__ pts,
+                                                    int32_t* __restrict__ status) {
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= npts) return;
+  G1A a;
+  if (!decode_point(raw + (size_t)gid * 64, a)) status[owner[gid]] = FTS_E_MALFORMED;
+  store_g1a(pts + (size_t)gid * 16, a);
+}
+
+// aff layout per action (from aff_off): TAS [in' (n_in), out' (n_out), sum, inCom (n_in), typeCom, sumCom]
+//                                       ST  [V (n_out), com]
+__global__ void __launch_bounds__(64) k_sig_prep(int A, const SigAction* __restrict__ act,
+                                                 const uint32_t* __restrict__ pts, const int32_t* __restrict__ status,
+                                                 uint32_t* __restrict__ aff, const int32_t* __restrict__ aff_off,
+                                                 uint32_t* __restrict__ jscr, uint8_t* __restrict__ rp_raw, int rp_k) {
+  int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= A || status[a] != 0) return;
+  const SigAction ac = act[a];
+  const uint32_t* P = pts + (size_t)ac.pt_off * 16;
+  uint32_t* J = jscr + (size_t)aff_off[a] * 24;
+  uint32_t* F = aff + (size_t)aff_off[a] * 16;
+  const int nin = ac.kind == SIG_TAS ? ac.n_in : 0;
+  const int m = nin + ac.n_out;
+  G1J sum = g1j_identity();
+  for (int i = 0; i < m; i++) {
+    G1J d = g1j_from_affine(load_g1a(P + (1 + i) * 16));
+    d = nl_madd_mem(d, P, 1);  // - CT
+    store_g1j(J + i * 24, d);
+    if (ac.kind == SIG_TAS) sum = nl_add_mem(sum, J + i * 24, i >= nin);
+  }
+  int mm = m;
+  if (ac.kind == SIG_TAS) {
+    store_g1j(J + m * 24, sum);
+    mm = m + 1;
+  }
+  batch_to_affine(J, F, mm);
+  if (ac.rp_base >= 0 && rp_raw) {
+    const int npts_rp = rp_npts(rp_k);
+    const int nv = ac.n_out < ac.rp_count ? ac.n_out : ac.rp_count;
+    for (int j = 0; j < nv; j++)
+      store_point_be(rp_raw + ((size_t)(ac.rp_base + j) * npts_rp + RP_PT_V) * 64, load_g1a(F + (nin + j) * 16));
+  }
+}
+
+__global__ void __launch_bounds__(64) k_sig_terms(int nwork, const int2* __restrict__ work,
+                                                  const SigAction* __restrict__ act, const uint32_t* __restrict__ pts,
+                                                  const uint32_t* __restrict__ sc, const int32_t* __restrict__ status,
+                                                  const uint32_t* __restrict__ aff, const int32_t* __restrict__ aff_off,
+                                                  const uint32_t* __restrict__ tables, int n,
+                                                  uint32_t* __restrict__ terms, uint32_t* __restrict__ scratch) {
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= nwork) return;
+  const int a = work[gid].x, t = work[gid].y;
+  if (status[a] != 0) return;
+  const SigAction ac = act[a];
+  const uint32_t* S = sc + (size_t)ac.sc_off * 8;
+  const uint32_t* F = aff + (size_t)aff_off[a] * 16;
+  uint32_t* scr = scratch + (size_t)gid * 10 * 24;
+  uint32_t* tmp = scr + 9 * 24;
+  const uint32_t* t_ped0 = tables + (size_t)tb_ped0(n) * FB_WORDS_PER_BASE;
+  const uint32_t* t_ped1 = tables + (size_t)tb_G(n) * FB_WORDS_PER_BASE;
+  const uint32_t* t_ped2 = tables + (size_t)tb_H(n) * FB_WORDS_PER_BASE;
+  auto canon = [](const uint32_t* p) {
+    Scalar s;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s.v[i] = p[i];
+    return s;
+  };
+  G1J r;
+  if (ac.kind == SIG_TAS) {
+    const int N = ac.n_in;
+    const Scalar chal = canon(S + TAS_SC_CHAL * 8);
+    if (t < 2 * N) {
+      int i = t >> 1;
+      if ((t & 1) == 0) {  // iv_i ped1 + ibf_i ped2
+        r = fixed_base_mul(t_ped1, canon(S + (TAS_SC_IV + i) * 8));
+        r = add_via(tmp, r, fixed_base_mul(t_ped2, canon(S + (TAS_SC_IV + N + i) * 8)));
+      } else {  // c in'_i
+        r = var_base_mul(load_g1a(F + i * 16), chal, scr);
+      }
+    } else if (t == 2 * N) {  // EqualityOfSum ped2
+      r = fixed_base_mul(t_ped2, canon(S + TAS_SC_EQ * 8));
+    } else if (t == 2 * N + 1) {  // c sum
+      r = var_base_mul(load_g1a(F + (N + ac.n_out) * 16), chal, scr);
+    } else if (t == 2 * N + 2) {  // Type ped0 + TBF ped2
+      r = fixed_base_mul(t_ped0, canon(S + TAS_SC_TYPE * 8));
+      r = add_via(tmp, r, fixed_base_mul(t_ped2, canon(S + TAS_SC_TBF * 8)));
+    } else {  // c CT
+      r = var_base_mul(load_g1a(pts + (size_t)ac.pt_off * 16), chal, scr);
+    }
+  } else {
+    if (t == 0) {  // Type ped0 + BF ped2
+      r = fixed_base_mul(t_ped0, canon(S + ST_SC_TYPE * 8));
+      r = add_via(tmp, r, fixed_base_mul(t_ped2, canon(S + ST_SC_BF * 8)));
+    } else {  // c CT
+      r = var_base_mul(load_g1a(pts + (size_t)ac.pt_off * 16), canon(S + ST_SC_CHAL * 8), scr);
+    }
+  }
+  store_g1j(terms + (size_t)(ac.term_off + t) * 24, r);
+}
+
+FTS_DEV void put_hex_aff(uint8_t* msg, int idx, const uint32_t* aff_pt, bool sep) {
+  G1A p = load_g1a(aff_pt);
+  uint32_t pw[16];
+  g1_mont_to_be_words(p.x, p.y, pw);
+  put_hex_record(msg, 130u * idx, pw, sep);
+}
+
+__global__ void __launch_bounds__(64) k_sig_finish(int A, const SigAction* __restrict__ act,
+                                                   const uint32_t* __restrict__ pts, const uint32_t* __restrict__ sc,
+                                                   int32_t* __restrict__ status, const uint32_t* __restrict__ terms,
+                                                   uint32_t* __restrict__ aff, const int32_t* __restrict__ aff_off,
+                                                   uint32_t* __restrict__ jscr, uint8_t* __restrict__ msgs) {
+  int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= A || status[a] != 0) return;
+  const SigAction ac = act[a];
+  const uint32_t* T = terms + (size_t)ac.term_off * 24;
+  uint32_t* F = aff + (size_t)aff_off[a] * 16;
+  uint32_t* J = jscr + (size_t)aff_off[a] * 24;
+  const uint32_t* CT = pts + (size_t)ac.pt_off * 16;
+  uint8_t* msg = msgs + ac.msg_off;
+  const uint32_t* S = sc + (size_t)ac.sc_off * 8;
+  int np;
+  const uint32_t* chal;
+  if (ac.kind == SIG_TAS) {
+    const int N = ac.n_in, M = ac.n_out;
+    const int c0 = N + M + 1;  // first commitment slot
+    for (int i = 0; i < N; i++) store_g1j(J + (c0 + i) * 24, nl_add_mem(load_g1j(T + (2 * i) * 24), T + (2 * i + 1) * 24, 1));
+    store_g1j(J + (c0 + N) * 24, nl_add_mem(load_g1j(T + (2 * N + 2) * 24), T + (2 * N + 3) * 24, 1));  // typeCom
+    store_g1j(J + (c0 + N + 1) * 24, nl_add_mem(load_g1j(T + (2 * N) * 24), T + (2 * N + 1) * 24, 1));  // sumCom
+    batch_to_affine(J + c0 * 24, F + c0 * 16, N + 2);
+    // Arr(inComs, typeCom, sumCom, in'..., out'..., CT, sum)     typeandsum.go:267
+    int idx = 0;
+    np = 2 * N + M + 4;
+    for (int i = 0; i < N + 2; i++, idx++) put_hex_aff(msg, idx, F + (c0 + i) * 16, true);
+    for (int i = 0; i < N + M; i++, idx++) put_hex_aff(msg, idx, F + i * 16, true);
+    put_hex_aff(msg, idx++, CT, true);
+    put_hex_aff(msg, idx++, F + (N + M) * 16, false);
+    chal = S + TAS_SC_CHAL * 8;
+  } else {
+    const int M = ac.n_out;
+    store_g1j(J + M * 24, nl_add_mem(load_g1j(T), T + 24, 1));
+    batch_to_affine(J + M * 24, F + M * 16, 1);
+    put_hex_aff(msg, 0, CT, true);  // Arr(CT, com)   sametype.go:174
+    put_hex_aff(msg, 1, F + M * 16, false);
+    np = 2;
+    chal = S + ST_SC_CHAL * 8;
+  }
+  uint32_t len = 130u * np - 2u;
+  write_sha_padding_u16(msg, len);
+  uint32_t st[8];
+  sha256_blocks(msg, sha_blocks(len), st);
+  Fr h = digest_to_fr(st);
+  bool eq = ac.chal_canonical != 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) eq = eq && (h.v[i] == chal[i]);
+  status[a] = eq ? FTS_OK : (ac.kind == SIG_TAS ? FTS_E_TAS_INVALID : FTS_E_ST_INVALID);
+}
+
+#define FTS_LAUNCH(kern, nthreads, bs, stream, ...)                                   \
+  do {                                                                                \
+    size_t nt_ = (size_t)(nthreads);                                                  \
+    if (nt_) hipLaunchKernelGGL(kern, dim3((unsigned)((nt_ + (bs)-1) / (bs))), dim3(bs), 0, stream, __VA_ARGS__); \
+  } while (0)
+
+// phase 1 (before the range-proof batch): decode + primes (writes the rp V slots)
+void launch_sig_prep(const SigBatchDev& d, hipStream_t s) {
+  FTS_LAUNCH(k_sig_decode, d.npts, 256, s, d.npts, d.raw, d.pt_owner, d.pts, d.status);
+  FTS_LAUNCH(k_sig_prep, d.A, 64, s, d.A, d.act, d.pts, d.status, d.aff, d.aff_off, d.jac, d.rp_raw, d.rp_k);
+}
+// phase 2: sigma equations (independent of the range proofs)
+void launch_sig_finish(const SigBatchDev& d, const uint32_t* tables, int n, hipStream_t s) {
+  FTS_LAUNCH(k_sig_terms, d.nwork, 64, s, d.nwork, d.work, d.act, d.pts, d.sc, d.status, d.aff, d.aff_off, tables, n,
+             d.terms, d.scratch);
+  FTS_LAUNCH(k_sig_finish, d.A, 64, s, d.A, d.act, d.pts, d.sc, d.status, d.terms, d.aff, d.aff_off, d.jac, d.msgs);
+}
+
+}  // namespace fts

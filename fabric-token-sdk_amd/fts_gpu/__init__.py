@@ -1,0 +1,278 @@
+"""fts_gpu — MI355X batch verifier for zkatdlog ("nogh" v1) token proofs.
+
+Host-side mirror of the reference verifier API (paths relative to
+token/core/zkatdlog/nogh/v1/crypto/ of fabric-token-sdk):
+
+===========================================  =========================================
+reference                                    here
+===========================================  =========================================
+``PublicParams.Deserialize`` setup.go:319     ``PublicParams(raw, bit_length, device)``
+``rp.NewRangeVerifier(...).Verify``           ``RangeVerifier(pp, com).Verify(rp_bytes)``
+  bulletproof.go:184-205,252-333
+``rp.NewRangeCorrectnessVerifier.Verify``     ``RangeCorrectnessVerifier``
+  rangecorrectness.go:118-162
+``transfer.NewVerifier(in,out,pp).Verify``    ``TransferVerifier(in, out, pp).Verify(proof)``
+  transfer/transfer.go:49-60,153-197
+``issue.NewVerifier(tokens,pp).Verify``       ``IssueVerifier(tokens, pp).Verify(proof)``
+  issue/verifier.go:24-57
+===========================================  =========================================
+
+``Verify`` returns ``None`` on success and raises :class:`VerifyError`
+carrying the reference's error string otherwise.  The batch entry points
+(``PublicParams.verify_range_proofs`` / ``verify_transfers`` /
+``verify_issues`` and :class:`StagedRangeBatch`) are what a validator that
+aggregates many actions calls; every one of them runs the HIP kernels of
+``libfts_gpu.so`` — there is no CPU fallback.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+from ._lib import (FTS_OK, FTS_E_MALFORMED, FTS_E_RP_NIL, FTS_E_RP_INVALID, FTS_E_IPA_NIL, FTS_E_IPA_LEN,  # noqa
+                   FTS_E_IPA_INVALID, FTS_E_RC_COUNT, FTS_E_TAS_INVALID, FTS_E_ST_INVALID, FTS_DEVICE_NONE)
+
+
+class VerifyError(Exception):
+    """Verification failure; ``str(e)`` is the reference's error chain."""
+
+    def __init__(self, msg, status, index=-1):
+        super().__init__(msg)
+        self.status = status
+        self.index = index
+
+
+def _rp_message(status):
+    return L.status_str(status)
+
+
+def transfer_message(status, index):
+    """Error string of transfer.Verify (transfer.go:153-197) for a verdict."""
+    if status == FTS_OK:
+        return None
+    if status == FTS_E_MALFORMED:
+        return "invalid transfer proof: failed to deserialize proof"
+    if status == FTS_E_TAS_INVALID:
+        return "invalid transfer proof: invalid sum and type proof"
+    if status == FTS_E_RC_COUNT:
+        return "invalid range proof"
+    return "invalid range proof at index %d: %s" % (index, _rp_message(status))
+
+
+def issue_message(status, index):
+    """Error string of issue.Verify (issue/verifier.go:32-57) for a verdict."""
+    if status == FTS_OK:
+        return None
+    if status == FTS_E_MALFORMED:
+        return "failed to deserialize proof"
+    if status == FTS_E_ST_INVALID:
+        return "invalid issue proof: invalid same type proof"
+    if status == FTS_E_RC_COUNT:
+        return "invalid issue proof: invalid range proof"
+    return "invalid issue proof: invalid range proof at index %d: %s" % (index, _rp_message(status))
+
+
+def _ptr_array(blobs):
+    bufs = [C.create_string_buffer(b, len(b)) if b else None for b in blobs]
+    ptrs = (C.c_void_p * len(blobs))(*[C.cast(b, C.c_void_p) if b is not None else None for b in bufs])
+    lens = (C.c_size_t * len(blobs))(*[len(b) for b in blobs])
+    return bufs, ptrs, lens
+
+
+class PublicParams:
+    """A verification context: parsed public parameters plus their device
+    tables (fixed-base windows of every generator) on one MI355X."""
+
+    def __init__(self, raw, bit_length=None, device=0):
+        self._ctx = C.c_void_p()
+        if bit_length:
+            rc = L.lib.fts_ctx_create_bits(raw, len(raw), int(bit_length), int(device), C.byref(self._ctx))
+        else:
+            rc = L.lib.fts_ctx_create(raw, len(raw), int(device), C.byref(self._ctx))
+        L.check("fts_ctx_create", rc)
+        info = L.PPInfo()
+        L.check("fts_ctx_info", L.lib.fts_ctx_info(self._ctx, C.byref(info)))
+        self.bit_length, self.rounds, self.device = info.bit_length, info.rounds, info.device
+        self.max_token, self.table_bytes = info.max_token, info.table_bytes
+
+    def close(self):
+        if self._ctx:
+            L.lib.fts_ctx_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------ verify
+    def verify_range_proofs(self, proofs, commitments):
+        """Batch of standalone range proofs -> np.int32 verdicts."""
+        n = len(proofs)
+        assert len(commitments) == n
+        bufs, ptrs, lens = _ptr_array(proofs)
+        coms = b"".join(commitments)
+        st = np.zeros(n, dtype=np.int32)
+        L.check("fts_rp_verify_batch", L.lib.fts_rp_verify_batch(
+            self._ctx, n, ptrs, lens, coms, st.ctypes.data_as(C.POINTER(C.c_int32))))
+        return st
+
+    def verify_transfers(self, transfers):
+        """transfers: list of (inputs[list of 64B], outputs[list], proof bytes) ->
+        (status, fail_index) arrays."""
+        n = len(transfers)
+        items = (L.TransferItem * n)()
+        keep = []
+        for i, (ins, outs, proof) in enumerate(transfers):
+            bi = C.create_string_buffer(b"".join(ins) or b"\0")
+            bo = C.create_string_buffer(b"".join(outs) or b"\0")
+            bp = C.create_string_buffer(proof or b"\0", max(1, len(proof)))
+            keep += [bi, bo, bp]
+            items[i] = L.TransferItem(C.cast(bi, C.c_void_p), len(ins), C.cast(bo, C.c_void_p), len(outs),
+                                      C.cast(bp, C.c_void_p), len(proof))
+        st = np.zeros(n, dtype=np.int32)
+        fi = np.zeros(n, dtype=np.int32)
+        L.check("fts_transfer_verify_batch", L.lib.fts_transfer_verify_batch(
+            self._ctx, n, items, st.ctypes.data_as(C.POINTER(C.c_int32)), fi.ctypes.data_as(C.POINTER(C.c_int32))))
+        return st, fi
+
+    def verify_issues(self, issues):
+        """issues: list of (tokens[list of 64B], proof bytes) -> (status, fail_index)."""
+        n = len(issues)
+        items = (L.IssueItem * n)()
+        keep = []
+        for i, (toks, proof) in enumerate(issues):
+            bt = C.create_string_buffer(b"".join(toks) or b"\0")
+            bp = C.create_string_buffer(proof or b"\0", max(1, len(proof)))
+            keep += [bt, bp]
+            items[i] = L.IssueItem(C.cast(bt, C.c_void_p), len(toks), C.cast(bp, C.c_void_p), len(proof))
+        st = np.zeros(n, dtype=np.int32)
+        fi = np.zeros(n, dtype=np.int32)
+        L.check("fts_issue_verify_batch", L.lib.fts_issue_verify_batch(
+            self._ctx, n, items, st.ctypes.data_as(C.POINTER(C.c_int32)), fi.ctypes.data_as(C.POINTER(C.c_int32))))
+        return st, fi
+
+    def stage_range_proofs(self, proofs, commitments):
+        return StagedRangeBatch(self, proofs, commitments)
+
+    def last_timings(self):
+        names = (C.c_char_p * 16)()
+        ms = (C.c_float * 16)()
+        m = L.lib.fts_last_timings(self._ctx, names, ms, 16)
+        return {names[i].decode(): ms[i] for i in range(m)}
+
+    # ------------------------------------------------------------- prove
+    def token_commit(self, ttype, value, bf32):
+        out = C.create_string_buffer(64)
+        L.check("fts_token_commit", L.lib.fts_token_commit(self._ctx, ttype, len(ttype), value, bf32, out))
+        return out.raw
+
+    def prove_range(self, value, bf32, seed):
+        buf = C.create_string_buffer(1 << 14)
+        ln = C.c_size_t()
+        com = C.create_string_buffer(64)
+        L.check("fts_rp_prove", L.lib.fts_rp_prove(self._ctx, value, bf32, seed, buf, len(buf), C.byref(ln), com))
+        return buf.raw[:ln.value], com.raw
+
+    def prove_range_batch(self, values, bfs, seed, threads=0):
+        n = len(values)
+        vals = (C.c_uint64 * n)(*values)
+        cap = n * (1500 + 150 * self.rounds) + 4096
+        out = C.create_string_buffer(cap)
+        offs = (C.c_size_t * n)()
+        lens = (C.c_size_t * n)()
+        coms = C.create_string_buffer(64 * n)
+        L.check("fts_rp_prove_batch", L.lib.fts_rp_prove_batch(
+            self._ctx, n, vals, b"".join(bfs), seed, threads, out, cap, offs, lens, coms))
+        raw = out.raw
+        return [raw[offs[i]:offs[i] + lens[i]] for i in range(n)], [coms.raw[64 * i:64 * i + 64] for i in range(n)]
+
+    def prove_transfer(self, ttype, in_values, in_bfs, out_values, out_bfs, seed):
+        buf = C.create_string_buffer(1 << 16)
+        ln = C.c_size_t()
+        iv = (C.c_uint64 * len(in_values))(*in_values)
+        ov = (C.c_uint64 * len(out_values))(*out_values)
+        L.check("fts_transfer_prove", L.lib.fts_transfer_prove(
+            self._ctx, ttype, len(ttype), len(in_values), iv, b"".join(in_bfs), len(out_values), ov,
+            b"".join(out_bfs), seed, buf, len(buf), C.byref(ln)))
+        return buf.raw[:ln.value]
+
+    def prove_issue(self, ttype, values, bfs, seed):
+        buf = C.create_string_buffer(1 << 17)
+        ln = C.c_size_t()
+        v = (C.c_uint64 * len(values))(*values)
+        L.check("fts_issue_prove", L.lib.fts_issue_prove(
+            self._ctx, ttype, len(ttype), len(values), v, b"".join(bfs), seed, buf, len(buf), C.byref(ln)))
+        return buf.raw[:ln.value]
+
+
+class StagedRangeBatch:
+    """Range proofs parsed and resident in HBM; ``verify()`` runs only the
+    GPU verification (fts_rp_batch_verify)."""
+
+    def __init__(self, pp, proofs, commitments):
+        self.pp = pp
+        self.n = len(proofs)
+        self._b = C.c_void_p()
+        bufs, ptrs, lens = _ptr_array(proofs)
+        L.check("fts_rp_batch_stage", L.lib.fts_rp_batch_stage(
+            pp._ctx, self.n, ptrs, lens, b"".join(commitments), C.byref(self._b)))
+
+    def verify(self, want_status=True):
+        st = np.zeros(self.n, dtype=np.int32) if want_status else None
+        L.check("fts_rp_batch_verify", L.lib.fts_rp_batch_verify(
+            self.pp._ctx, self._b, st.ctypes.data_as(C.POINTER(C.c_int32)) if want_status else None))
+        return st
+
+    def close(self):
+        if self._b:
+            L.lib.fts_rp_batch_free(self._b)
+            self._b = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ------------------------------------------------ reference-shaped verifiers
+class RangeVerifier:
+    """rp.NewRangeVerifier(com, ...) / Verify (bulletproof.go:184-205,252-333).
+    The generators come from ``pp`` exactly as RangeCorrectnessVerifier passes
+    them (PedersenGenerators[1:], Left/Right, P, Q)."""
+
+    def __init__(self, pp, commitment):
+        self.pp, self.commitment = pp, commitment
+
+    def Verify(self, rp_bytes):
+        s = int(self.pp.verify_range_proofs([rp_bytes], [self.commitment])[0])
+        if s != FTS_OK:
+            raise VerifyError(_rp_message(s), s)
+
+
+class TransferVerifier:
+    """transfer.NewVerifier(inputs, outputs, pp) / Verify (transfer.go:49-60,153-197)."""
+
+    def __init__(self, inputs, outputs, pp):
+        self.inputs, self.outputs, self.pp = list(inputs), list(outputs), pp
+
+    def Verify(self, proof):
+        st, fi = self.pp.verify_transfers([(self.inputs, self.outputs, proof)])
+        msg = transfer_message(int(st[0]), int(fi[0]))
+        if msg:
+            raise VerifyError(msg, int(st[0]), int(fi[0]))
+
+
+class IssueVerifier:
+    """issue.NewVerifier(tokens, pp) / Verify (issue/verifier.go:24-57)."""
+
+    def __init__(self, tokens, pp):
+        self.tokens, self.pp = list(tokens), pp
+
+    def Verify(self, proof):
+        st, fi = self.pp.verify_issues([(self.tokens, proof)])
+        msg = issue_message(int(st[0]), int(fi[0]))
+        if msg:
+            raise VerifyError(msg, int(st[0]), int(fi[0]))

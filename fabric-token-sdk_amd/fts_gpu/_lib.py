@@ -1,0 +1,101 @@
+"""ctypes binding of libfts_gpu.so (include/fts_gpu.h).
+
+The shared library is built in-tree by ``make -C fabric-token-sdk_amd`` (see
+``__graft_entry__.build``).  There is no fallback: if the library is missing
+or fails to load, importing this module raises.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libfts_gpu.so")
+
+# fts_status (include/fts_gpu.h)
+FTS_OK = 0
+FTS_E_MALFORMED = 1
+FTS_E_RP_NIL = 2
+FTS_E_RP_INVALID = 3
+FTS_E_IPA_NIL = 4
+FTS_E_IPA_LEN = 5
+FTS_E_IPA_INVALID = 6
+FTS_E_RC_COUNT = 7
+FTS_E_TAS_INVALID = 8
+FTS_E_ST_INVALID = 9
+FTS_E_NOT_RUN = 10
+
+FTS_API_OK = 0
+FTS_DEVICE_NONE = -2
+
+EXPORTED = [
+    "fts_ctx_create", "fts_ctx_create_bits", "fts_ctx_destroy", "fts_ctx_info",
+    "fts_rp_verify_batch", "fts_transfer_verify_batch", "fts_issue_verify_batch",
+    "fts_rp_batch_stage", "fts_rp_batch_verify", "fts_rp_batch_free", "fts_last_timings",
+    "fts_status_str", "fts_rp_prove", "fts_rp_prove_batch", "fts_token_commit",
+    "fts_transfer_prove", "fts_issue_prove", "fts_debug_rp_intermediates",
+]
+
+
+class PPInfo(C.Structure):
+    _fields_ = [("bit_length", C.c_uint32), ("rounds", C.c_uint32), ("curve_id", C.c_uint32),
+                ("device", C.c_int32), ("max_token", C.c_uint64), ("table_bytes", C.c_uint64)]
+
+
+class TransferItem(C.Structure):
+    _fields_ = [("inputs", C.c_void_p), ("n_in", C.c_size_t), ("outputs", C.c_void_p), ("n_out", C.c_size_t),
+                ("proof", C.c_void_p), ("proof_len", C.c_size_t)]
+
+
+class IssueItem(C.Structure):
+    _fields_ = [("tokens", C.c_void_p), ("n_tok", C.c_size_t), ("proof", C.c_void_p), ("proof_len", C.c_size_t)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libfts_gpu.so not built: run `make -C fabric-token-sdk_amd` (%s)" % LIB_PATH)
+    lib = C.CDLL(LIB_PATH)
+    P, S, U8P, I32P = C.c_void_p, C.c_size_t, C.c_char_p, C.POINTER(C.c_int32)
+    sig = {
+        "fts_ctx_create": ([U8P, S, C.c_int, C.POINTER(P)], C.c_int),
+        "fts_ctx_create_bits": ([U8P, S, C.c_uint32, C.c_int, C.POINTER(P)], C.c_int),
+        "fts_ctx_destroy": ([P], None),
+        "fts_ctx_info": ([P, C.POINTER(PPInfo)], C.c_int),
+        "fts_rp_verify_batch": ([P, S, C.POINTER(C.c_void_p), C.POINTER(S), U8P, I32P], C.c_int),
+        "fts_transfer_verify_batch": ([P, S, C.POINTER(TransferItem), I32P, I32P], C.c_int),
+        "fts_issue_verify_batch": ([P, S, C.POINTER(IssueItem), I32P, I32P], C.c_int),
+        "fts_rp_batch_stage": ([P, S, C.POINTER(C.c_void_p), C.POINTER(S), U8P, C.POINTER(P)], C.c_int),
+        "fts_rp_batch_verify": ([P, P, I32P], C.c_int),
+        "fts_rp_batch_free": ([P], None),
+        "fts_last_timings": ([P, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int], C.c_int),
+        "fts_status_str": ([C.c_int32], C.c_char_p),
+        "fts_rp_prove": ([P, C.c_uint64, U8P, C.c_uint64, P, S, C.POINTER(S), P], C.c_int),
+        "fts_rp_prove_batch": ([P, S, C.POINTER(C.c_uint64), U8P, C.c_uint64, C.c_int, P, S, C.POINTER(S),
+                                C.POINTER(S), P], C.c_int),
+        "fts_token_commit": ([P, U8P, S, C.c_uint64, U8P, P], C.c_int),
+        "fts_transfer_prove": ([P, U8P, S, S, C.POINTER(C.c_uint64), U8P, S, C.POINTER(C.c_uint64), U8P,
+                                C.c_uint64, P, S, C.POINTER(S)], C.c_int),
+        "fts_issue_prove": ([P, U8P, S, S, C.POINTER(C.c_uint64), U8P, C.c_uint64, P, S, C.POINTER(S)], C.c_int),
+        "fts_debug_rp_intermediates": ([P, S, P, P, P], C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = res
+    return lib
+
+
+lib = _load()
+
+
+class FtsError(RuntimeError):
+    def __init__(self, fn, code):
+        super().__init__("%s failed with API code %d" % (fn, code))
+        self.code = code
+
+
+def check(fn, code):
+    if code != FTS_API_OK:
+        raise FtsError(fn, code)
+
+
+def status_str(s):
+    return lib.fts_status_str(int(s)).decode()

@@ -1,0 +1,161 @@
+/*
+ * fts_gpu.h — C-ABI of the MI355X batch verifier for zkatdlog ("nogh" v1)
+ * token proofs on BN254.
+ *
+ * This is the drop-in boundary: a Go validator binds these symbols through
+ * cgo.  Only plain pointers and sizes cross it; the
+ * library owns all device memory, streams and tables per context.
+ *
+ * Reference interfaces each entry point replaces (paths relative to
+ * token/core/zkatdlog/nogh/v1/ in murongshaozong/fabric-token-sdk):
+ *   fts_ctx_create            crypto/setup.go:319-372   PublicParams.Deserialize
+ *                             + driver/base.go:39-46     DefaultValidator (context build)
+ *   fts_rp_verify_batch       crypto/rp/bulletproof.go:184-205,252-333
+ *                                                       NewRangeVerifier + (*rangeVerifier).Verify
+ *                             crypto/rp/ipa.go:190-262  (*ipaVerifier).Verify (called from it)
+ *   fts_transfer_verify_batch crypto/transfer/transfer.go:49-60,153-197
+ *                                                       transfer.NewVerifier + (*Verifier).Verify
+ *                             (validator/validator_transfer.go:96-110 TransferZKProofValidate)
+ *   fts_issue_verify_batch    crypto/issue/verifier.go:24-57 issue.NewVerifier + Verify
+ *                             (validator/validator_issue.go:28-32 IssueValidate)
+ *   fts_status_str            the reference's error strings (bulletproof.go:255-323,
+ *                             ipa.go:193-258, rangecorrectness.go:139-159,
+ *                             typeandsum.go:232-274, sametype.go:180, transfer.go:192-196)
+ *   fts_*_prove               crypto/rp/bulletproof.go:209-249, transfer/transfer.go:69-150,
+ *                             issue/prover.go:46-112 (host prover: synthetic inputs)
+ *
+ * Return values: every function returns FTS_API_OK (0) or a negative
+ * FTS_API_* code for API/driver errors (bad argument, HIP failure).
+ * Per-item verdicts go to caller-owned int32 arrays as fts_status values.
+ * Thread safety: a context serialises concurrent calls internally.
+ */
+#ifndef FTS_GPU_H
+#define FTS_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- per-item verdicts (1:1 with the reference's distinct error strings) ---- */
+enum fts_status {
+  FTS_OK = 0,
+  FTS_E_MALFORMED = 1,      /* deserialization error, or input on which the reference panics */
+  FTS_E_RP_NIL = 2,         /* "invalid range proof: nil elements"   bulletproof.go:255-264 */
+  FTS_E_RP_INVALID = 3,     /* "invalid range proof"                 bulletproof.go:323 */
+  FTS_E_IPA_NIL = 4,        /* "invalid IPA proof: nil elements"     ipa.go:193,227 */
+  FTS_E_IPA_LEN = 5,        /* "invalid IPA proof"                   ipa.go:197 */
+  FTS_E_IPA_INVALID = 6,    /* "invalid IPA"                         ipa.go:258 */
+  FTS_E_RC_COUNT = 7,       /* "invalid range proof" (#proofs != #commitments) rangecorrectness.go:139 */
+  FTS_E_TAS_INVALID = 8,    /* "invalid sum and type proof"          typeandsum.go:232,274 */
+  FTS_E_ST_INVALID = 9,     /* "invalid same type proof"             sametype.go:180 */
+  FTS_E_NOT_RUN = 10        /* item not evaluated (batch aborted by an API error) */
+};
+
+/* ---- API return codes ---- */
+#define FTS_API_OK 0
+#define FTS_API_EINVAL (-1)   /* bad argument / NULL pointer */
+#define FTS_API_EPP (-2)      /* public parameters rejected (setup.go:319-372,444-489) */
+#define FTS_API_EDEVICE (-3)  /* HIP runtime / device failure */
+#define FTS_API_ENOMEM (-4)
+#define FTS_API_ESIZE (-5)    /* unsupported bit length / batch shape */
+
+/* device argument of fts_ctx_create*: host-only context (parsing + prover, no GPU) */
+#define FTS_DEVICE_NONE (-2)
+
+typedef struct fts_ctx fts_ctx;
+typedef struct fts_rp_batch fts_rp_batch;
+
+typedef struct fts_pp_info {
+  uint32_t bit_length;      /* RangeProofParams.BitLength (8/16/32/64) */
+  uint32_t rounds;          /* RangeProofParams.NumberOfRounds */
+  uint32_t curve_id;        /* always 1 (BN254) */
+  int32_t device;           /* HIP device ordinal the context runs on */
+  uint64_t max_token;
+  uint64_t table_bytes;     /* device bytes of fixed-base tables */
+} fts_pp_info;
+
+/* One transfer action: commitments as 64-byte X||Y big-endian (G1.Bytes()). */
+typedef struct fts_transfer_item {
+  const uint8_t* inputs;    /* n_in  * 64 bytes */
+  size_t n_in;
+  const uint8_t* outputs;   /* n_out * 64 bytes */
+  size_t n_out;
+  const uint8_t* proof;     /* transfer.Proof DER (transfer.go:29-40) */
+  size_t proof_len;
+} fts_transfer_item;
+
+/* One issue action. */
+typedef struct fts_issue_item {
+  const uint8_t* tokens;    /* n_tok * 64 bytes */
+  size_t n_tok;
+  const uint8_t* proof;     /* issue.Proof DER (issue/prover.go:27-37) */
+  size_t proof_len;
+} fts_issue_item;
+
+/* ---- context ---- */
+/* pp: PublicParams.Serialize() bytes (JSON container {"identifier","raw"}).
+ * device: HIP device ordinal (-1: current device, FTS_DEVICE_NONE: host-only). */
+int fts_ctx_create(const uint8_t* pp, size_t pp_len, int device, fts_ctx** out);
+/* Same generators, range proofs truncated to bit_length (Setup(bit_length) semantics,
+ * setup.go:388-406: labels do not depend on the bit length). */
+int fts_ctx_create_bits(const uint8_t* pp, size_t pp_len, uint32_t bit_length, int device, fts_ctx** out);
+void fts_ctx_destroy(fts_ctx* ctx);
+int fts_ctx_info(const fts_ctx* ctx, fts_pp_info* out);
+
+/* ---- verification (host buffers in, verdicts out) ---- */
+/* n standalone range proofs: rp_der[i] = RangeProof.Serialize() (bulletproof.go:93-95),
+ * com64 = n * 64-byte commitments V_i.  status[i] <- fts_status. */
+int fts_rp_verify_batch(fts_ctx* ctx, size_t n, const uint8_t* const* rp_der, const size_t* rp_len,
+                        const uint8_t* com64, int32_t* status);
+/* status[i] <- fts_status; fail_index[i] <- index of the failing range proof (-1 if none). */
+int fts_transfer_verify_batch(fts_ctx* ctx, size_t n, const fts_transfer_item* items, int32_t* status,
+                              int32_t* fail_index);
+int fts_issue_verify_batch(fts_ctx* ctx, size_t n, const fts_issue_item* items, int32_t* status,
+                           int32_t* fail_index);
+
+/* ---- device-resident batches (parse + upload once, verify many times) ---- */
+int fts_rp_batch_stage(fts_ctx* ctx, size_t n, const uint8_t* const* rp_der, const size_t* rp_len,
+                       const uint8_t* com64, fts_rp_batch** out);
+/* runs the whole GPU verification of a staged batch; status may be NULL */
+int fts_rp_batch_verify(fts_ctx* ctx, fts_rp_batch* b, int32_t* status);
+void fts_rp_batch_free(fts_rp_batch* b);
+/* device time of the last fts_rp_batch_verify, per kernel class (ms); returns count filled */
+int fts_last_timings(const fts_ctx* ctx, const char** names, float* ms, int cap);
+
+/* parity/debug hook: exact intermediates of proof i of the last range-proof run
+ * (ch_out: (8+2k) x 32-byte BE Fr [x, x^2, y, y^-1, z, z^2, polEval, x0, x_j..., x_j^-1...],
+ *  com_out: 64-byte com, hp_out: n x 64-byte H'_i); any pointer may be NULL */
+int fts_debug_rp_intermediates(fts_ctx* ctx, size_t i, uint8_t* ch_out, uint8_t* com_out, uint8_t* hp_out);
+
+/* ---- error strings ---- */
+const char* fts_status_str(int32_t status);
+
+/* ---- host prover (synthetic inputs; reference prover semantics) ---- */
+/* value < 2^bit_length expected (larger values produce a proof that fails, as in the
+ * reference).  bf32: blinding factor (BE, reduced mod r).  seed: deterministic RNG seed.
+ * out_der: caller buffer of out_cap bytes; *out_len <- bytes written. com64_out: V. */
+int fts_rp_prove(const fts_ctx* ctx, uint64_t value, const uint8_t* bf32, uint64_t seed, uint8_t* out_der,
+                 size_t out_cap, size_t* out_len, uint8_t* com64_out);
+/* batch helper: n proofs with values[i], blinding factors bfs[i*32], seeds seed+i,
+ * written into one buffer (offsets[i], lens[i]); uses `threads` host threads */
+int fts_rp_prove_batch(const fts_ctx* ctx, size_t n, const uint64_t* values, const uint8_t* bfs, uint64_t seed,
+                       int threads, uint8_t* out, size_t out_cap, size_t* offsets, size_t* lens,
+                       uint8_t* com64_out);
+/* Token commitments (token.go:208-217): tok = H(type)*ped0 + value*ped1 + bf*ped2 */
+int fts_token_commit(const fts_ctx* ctx, const uint8_t* type, size_t type_len, uint64_t value,
+                     const uint8_t* bf32, uint8_t* com64_out);
+/* transfer.NewProver(...).Prove(): n_in inputs / n_out outputs with witnesses */
+int fts_transfer_prove(const fts_ctx* ctx, const uint8_t* type, size_t type_len, size_t n_in,
+                       const uint64_t* in_values, const uint8_t* in_bfs, size_t n_out, const uint64_t* out_values,
+                       const uint8_t* out_bfs, uint64_t seed, uint8_t* out_der, size_t out_cap, size_t* out_len);
+/* issue.NewProver(...).Prove() */
+int fts_issue_prove(const fts_ctx* ctx, const uint8_t* type, size_t type_len, size_t n_tok, const uint64_t* values,
+                    const uint8_t* bfs, uint64_t seed, uint8_t* out_der, size_t out_cap, size_t* out_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FTS_GPU_H */

@@ -1,0 +1,65 @@
+"""Developer probe: GPU range-proof verification vs the oracle, with
+intermediates.  Usage: python tools/gpu_probe.py [bits] [count]"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "fabric-token-sdk_amd"))
+
+import ctypes as C  # noqa: E402
+
+import fts_gpu  # noqa: E402
+from fts_gpu import _lib as L  # noqa: E402
+from oracle import bn254 as bn, pp as ppm, zkat  # noqa: E402
+
+bits = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+count = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+raw = open(os.path.join(ROOT, "tests/golden/zkatdlog_pp.json"), "rb").read()
+t = time.time()
+pp = fts_gpu.PublicParams(raw, bit_length=bits, device=0)
+print("ctx %.2fs table %.1f MB" % (time.time() - t, pp.table_bytes / 1e6), flush=True)
+opp = ppm.load_pp(raw).with_bit_length(bits)
+vals = [(i * 0x9E3779B97F4A7C15) % (1 << bits) for i in range(count)]
+bfs = [((i + 1) * 0x1234567).to_bytes(32, "big") for i in range(count)]
+t = time.time()
+proofs, coms = pp.prove_range_batch(vals, bfs, seed=7)
+print("prove %d: %.2fs" % (count, time.time() - t), flush=True)
+t = time.time()
+st = pp.verify_range_proofs(proofs, coms)
+print("verify: %.3fs statuses %s" % (time.time() - t, list(st[:16])), flush=True)
+print("timings", pp.last_timings(), flush=True)
+# intermediates of proof 0
+k = pp.rounds
+ch = C.create_string_buffer(32 * (8 + 2 * k))
+com = C.create_string_buffer(64)
+hp = C.create_string_buffer(64 * bits)
+L.lib.fts_debug_rp_intermediates(pp._ctx, 0, ch, com, hp)
+tr = {}
+V = bn.g1_from_bytes(coms[0])
+err = zkat.rp_verify(V, opp.ped[1:], opp.left, opp.right, opp.P, opp.Q, opp.rounds, bits,
+                     zkat.RangeProof.deserialize(proofs[0]), tr)
+print("oracle verdict proof0:", err, flush=True)
+gch = [int.from_bytes(ch.raw[32 * i:32 * i + 32], "big") for i in range(8 + 2 * k)]
+for name, idx in (("x", 0), ("y", 2), ("z", 4), ("polEval", 6), ("x0", 7)):
+    print("  %-8s %s" % (name, "OK" if gch[idx] == tr.get(name) else "MISMATCH gpu=%x oracle=%x" % (gch[idx], tr.get(name) or 0)))
+for j in range(k):
+    print("  x_%d     %s" % (j, "OK" if gch[8 + j] == tr["xj"][j] else "MISMATCH"))
+print("  com      %s" % ("OK" if com.raw == bn.g1_bytes(tr["com"]) else "MISMATCH"))
+hp_ok = all(hp.raw[64 * i:64 * i + 64] == bn.g1_bytes(tr["Hprime"][i]) for i in range(bits))
+print("  H'       %s" % ("OK" if hp_ok else "MISMATCH"), flush=True)
+# tampering
+bad = list(proofs)
+r0 = zkat.RangeProof.deserialize(proofs[1])
+r0.data.T1 = bn.g1_add(r0.data.T1, opp.ped[1])
+bad[1] = r0.serialize()
+r2 = zkat.RangeProof.deserialize(proofs[2])
+r2.ipa.L[0] = bn.g1_add(r2.ipa.L[0], opp.ped[1])
+bad[2] = r2.serialize()
+r3 = zkat.RangeProof.deserialize(proofs[3])
+r3.ipa.Left = (r3.ipa.Left + 1) % bn.R
+bad[3] = r3.serialize()
+bad[4] = proofs[4][:-3]
+st = pp.verify_range_proofs(bad, coms)
+print("tampered statuses:", [(int(s), L.status_str(s)) for s in st[:6]], flush=True)
