@@ -869,7 +869,7 @@ int fts_rp_prove_batch(const fts_ctx* c, size_t n, const uint64_t* values, const
   const ProverTables& T = prover_tables(c);
   std::vector<std::string> res(n);
   std::atomic<size_t> next{0};
-  int nth = threads > 0 ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  int nth = threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   std::vector<std::thread> th;
   for (int t = 0; t < nth; t++)
     th.emplace_back([&]() {

@@ -1,0 +1,42 @@
+"""GPU: BASELINE config C2 at full size (4,096 standalone 64-bit range proofs
+in one batch) through size-independent properties: every honest proof is
+accepted, exactly the tampered positions are rejected with the reference's
+error class, and re-verifying the staged batch is idempotent."""
+import random
+
+import pytest
+
+from oracle import bn254 as bn, zkat
+
+pytestmark = pytest.mark.gpu
+
+
+def test_full_batch_4096_rp64(gpu_pp):
+    pp = gpu_pp(64)
+    n = 4096
+    rng = random.Random(0xF7A50002)
+    vals = [rng.getrandbits(64) for _ in range(n)]
+    bfs = [rng.randrange(bn.R).to_bytes(32, "big") for _ in range(n)]
+    proofs, coms = pp.prove_range_batch(vals, bfs, seed=0xF7A50002)
+    b = pp.stage_range_proofs(proofs, coms)
+    st = b.verify()
+    assert int((st != 0).sum()) == 0
+    # 1% tampered: random T1 (-> invalid range proof) or L_j (-> invalid IPA)
+    bad = sorted(rng.sample(range(n), 41))
+    kinds = {}
+    for i in bad:
+        r = zkat.RangeProof.deserialize(proofs[i])
+        if rng.random() < 0.5:
+            r.data.T1 = bn.g1_add(r.data.T1, bn.GEN)
+            kinds[i] = 3
+        else:
+            j = rng.randrange(6)
+            r.ipa.L[j] = bn.g1_add(r.ipa.L[j], bn.GEN)
+            kinds[i] = 6
+        proofs[i] = r.serialize()
+    b2 = pp.stage_range_proofs(proofs, coms)
+    st2 = b2.verify()
+    assert {i: int(st2[i]) for i in range(n) if st2[i] != 0} == kinds
+    assert (b2.verify() == st2).all()
+    b.close()
+    b2.close()
