@@ -1,0 +1,188 @@
+"""Benchmark: range-proof verifies/sec (BN254, 64-bit) on MI355X.
+
+Workload (BASELINE.json configs[1]): batches of 4,096
+standalone 64-bit Bulletproof range proofs (synthetic, seeded 0xF7A50002 +
+rank, produced by the library's host prover).  One step = one pass of the
+hot path over one batch: fts_rp_batch_verify on a batch already resident in
+HBM, verdicts delivered to the host; for N > 1 the per-GPU verdict bitmaps
+are all-gathered over RCCL (the only exchange step).  Weak
+scaling: every rank verifies its own 4,096-proof batch.
+
+Prints one JSON line (rank 0).  Usage:
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--bits 64]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "fabric-token-sdk_amd"))
+
+# INT32 VALU peak of one MI355X for v_mad_u64_u32 (quarter rate):
+# 256 CU x 4 SIMD x 32 lanes / 4 x 2.4 GHz (MI355X_MICROARCH.md chip table);
+# tools' int_peak microbenchmark measures >= 88 % of it with the Fp product.
+PEAK_TMAD = 256 * 4 * 32 / 4 * 2.4e9 / 1e12
+MAD_PER_MUL = 136          # 8x32-bit no-carry CIOS / FIPS Montgomery product
+SURVEY_MAD_PER_RP64 = 8.13e6   # SURVEY §8(d) fixed cost model per rp64 verify
+
+
+def kernel_mads(name, B, n, k):
+    """Algorithmic u32 MADs of one launch of `name`:
+    op counts of the algorithm the kernel runs x 136 MAD per Fp/Fr product."""
+    fb = 32 * 11                       # fixed-base product: 32 mixed adds (7M+4S)
+    vb = 7 + 6 * 11 + 64 * (4 * 7) + 60 * 16   # var-base: table + 256 dbl + ~60 full adds
+    inv = 254 + 128                    # Fermat inversion
+    per_unit = {
+        "k_rp_hprime": n * (fb + 9),
+        "k_rp_terms_fixed": (3 + 2 * n) * (fb + 8),
+        "k_rp_terms_var": (3 + 2 * k) * vb,
+        "k_rp_com": (n - 1) * (7 + 11) + 2 * vb + 2 * fb + 2 * (inv + 3) + 3 * 16,
+        "k_rp_hp_normalize": 3 * n + inv + 3 * n,
+        "k_rp_check": (4 + 2 * n + 2 * k + 1) * 16,
+        "k_rp_challenges": 2 * n + (k + 1) * inv + 8,
+    }.get(name)
+    if per_unit is None:
+        return None
+    return B * per_unit * MAD_PER_MUL
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--bits", type=int, default=64)
+    ap.add_argument("--cpu-sample", type=int, default=64, help="proofs verified by the CPU baseline (0: skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import random
+    import numpy as np
+    import fts_gpu
+
+    with open(os.path.join(ROOT, "tests", "golden", "zkatdlog_pp.json"), "rb") as f:
+        pp_raw = f.read()
+    pp = fts_gpu.PublicParams(pp_raw, bit_length=args.bits, device=local)
+    n, k, B = pp.bit_length, pp.rounds, args.batch
+    rng = random.Random(0xF7A50002 + rank)
+    vals = [rng.getrandbits(n) for _ in range(B)]
+    bfs = [rng.randrange(21888242871839275222246405745257275088548364400416034343698204186575808495617)
+           .to_bytes(32, "big") for _ in range(B)]
+    t0 = time.time()
+    proofs, coms = pp.prove_range_batch(vals, bfs, seed=0xF7A50002 + 1000003 * rank)
+    prove_s = time.time() - t0
+    batch = pp.stage_range_proofs(proofs, coms)
+
+    def step():
+        st = batch.verify(want_status=True)
+        if dist is not None:
+            import torch
+            bits = torch.from_numpy(np.packbits(st == 0)).cuda()
+            out = torch.empty(world * bits.numel(), dtype=torch.uint8, device="cuda")
+            dist.all_gather_into_tensor(out, bits)
+        return st
+
+    for _ in range(args.warmup):
+        st = step()
+    ok = int((st == 0).sum())
+    if dist is not None:
+        import torch
+        dist.barrier()
+        torch.cuda.synchronize()
+    kt = {}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        for name, ms in pp.last_timings().items():
+            kt[name] = kt.get(name, 0.0) + ms
+    if dist is not None:
+        torch.cuda.synchronize()
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        okt = torch.tensor([ok], dtype=torch.int64, device="cuda")
+        dist.all_reduce(okt)
+        ok = int(okt.item())
+
+    total = world * B * args.steps
+    value = total / elapsed
+    avg = {kname: v / args.steps for kname, v in kt.items()}
+    dom = max(avg, key=avg.get)
+    dom_ms = avg[dom]
+    mads = kernel_mads(dom, B, n, k)
+    achieved = mads / (dom_ms * 1e-3) / 1e12 if mads else None
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            traffic = json.load(f).get(dom)
+    except (OSError, ValueError):
+        pass
+    roofline = {"bound": "int32_valu", "kernel": dom, "achieved": round(achieved, 3) if achieved else None,
+                "peak": round(PEAK_TMAD, 3), "unit": "TMAD/s",
+                "frac": round(achieved / PEAK_TMAD, 4) if achieved else None,
+                "traffic": traffic, "kernel_ms": round(dom_ms, 4),
+                "pipeline_frac_survey_model": round(value / world * SURVEY_MAD_PER_RP64 / (PEAK_TMAD * 1e12), 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        from oracle import cref, pp as oppm
+        opp = oppm.load_pp(pp_raw).with_bit_length(n)
+        m = args.cpu_sample
+        thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        t0 = time.perf_counter()
+        res = cref.rp_verify_many(opp, coms[:m], proofs[:m], threads=thr)
+        cs = time.perf_counter() - t0
+        assert all(r == 0 for r in res), res
+        cpu = {"value": round(m / cs, 3), "unit": "rp64 verifies/s", "cores": thr, "kind": "port",
+               "sample": "%d of the same rp%d proofs, reference-order C restatement (oracle/c/ref_verify.c, "
+                         "469 affine G1.Mul per proof), %d threads, %.1f s wall" % (m, n, thr, cs)}
+
+    if rank == 0:
+        out = {
+            "metric": "range-proof verifies/sec (BN254, %d-bit)" % n,
+            "value": round(value, 1),
+            "unit": "verifies/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 (BN254 Fp/Fr 8x32-bit Montgomery)",
+            "data": "synthetic: %d seeded %d-bit range proofs per GPU from the library's host prover" % (B, n),
+            "config": {"workload": "C2: batch of %d standalone %d-bit Bulletproof range proofs per GPU "
+                                   "(IPA + RLC-free per-proof equations)" % (B, n),
+                       "batch_per_gpu": B, "bit_length": n, "rounds": k, "parallelism": "shard%d" % world},
+            "accepted": ok,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernel_ms": {kname: round(v, 4) for kname, v in avg.items()},
+            "prove_s": round(prove_s, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

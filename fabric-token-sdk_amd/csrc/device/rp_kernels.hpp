@@ -38,6 +38,10 @@ inline __host__ __device__ uint32_t x0_slot_bytes(int n) { return ((x0_msg_len(n
 // small transcripts slot (x: 258 B, y: 388 B, x_j: 258 B, z: 32 B) -> 512 B scratch each
 constexpr uint32_t SMALL_SLOT = 512;
 
+// per-kernel timing events of launch_rp_verify (names in fts_api.cpp)
+constexpr int RP_NUM_KERNELS = 10;
+constexpr int RP_NUM_EVENTS = RP_NUM_KERNELS + 1;
+
 // device buffers of one range-proof batch (filled by fts_api.cpp)
 struct RpBatchDev {
   int B, n, k;

@@ -90,9 +90,10 @@ struct Workspace {
   }
 };
 
-const int kNumEv = 8;
-const char* kPhaseNames[kNumEv - 1] = {"decode+challenges", "hprime", "normalize+com", "x0", "terms_fixed",
-                                       "terms_var", "check"};
+const int kNumEv = RP_NUM_EVENTS;
+const char* kPhaseNames[RP_NUM_KERNELS] = {"k_rp_decode",   "k_rp_challenges", "k_rp_hprime",      "k_rp_hp_normalize",
+                                           "k_rp_com",      "k_rp_x0_build",   "k_rp_x0_hash",     "k_rp_terms_fixed",
+                                           "k_rp_terms_var", "k_rp_check"};
 
 }  // namespace
 

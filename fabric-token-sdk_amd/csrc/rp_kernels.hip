@@ -445,28 +445,38 @@ void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32
   FTS_LAUNCH(k_build_tables, nb * FB_WINDOWS, 64, s, bases, nb, tables, scratch);
 }
 
-// events: array of at least 8 events to time the phases (may be null)
+// ev: RP_NUM_EVENTS events bracketing every kernel (may be null)
 void launch_rp_verify(const RpBatchDev& d, const uint32_t* tables, const uint8_t* x0_const, hipStream_t s,
                       hipEvent_t* ev) {
   const int B = d.B, n = d.n, k = d.k;
-  if (ev) hipEventRecord(ev[0], s);
+  int e = 0;
+#define FTS_EV()                      \
+  do {                                \
+    if (ev) hipEventRecord(ev[e], s); \
+    e++;                              \
+  } while (0)
+  FTS_EV();
   FTS_LAUNCH(k_rp_decode, B * rp_npts(k), 256, s, B, rp_npts(k), d.raw, d.pts, d.status);
+  FTS_EV();
   FTS_LAUNCH(k_rp_challenges, B, 64, s, B, n, k, d.raw, d.status, d.ch, d.small_msgs);
-  if (ev) hipEventRecord(ev[1], s);
+  FTS_EV();
   FTS_LAUNCH(k_rp_hprime, B * n, 64, s, B, n, k, d.status, d.ch, tables, d.hpj);
-  if (ev) hipEventRecord(ev[2], s);
+  FTS_EV();
   FTS_LAUNCH(k_rp_hp_normalize, B, 64, s, B, n, d.status, d.hpj, d.hpa, d.hp_be);
+  FTS_EV();
   FTS_LAUNCH(k_rp_com, B, 64, s, B, n, k, d.status, d.pts, d.sc, d.ch, d.hpa, tables, d.com, d.com_be, d.scratch);
-  if (ev) hipEventRecord(ev[3], s);
+  FTS_EV();
   FTS_LAUNCH(k_rp_x0_build, B * (2 * n + 3), 256, s, B, n, d.status, d.hp_be, d.com_be, x0_const, d.sc, d.x0_msgs);
+  FTS_EV();
   FTS_LAUNCH(k_rp_x0_hash, B, 64, s, B, n, k, d.status, d.x0_msgs, d.ch);
-  if (ev) hipEventRecord(ev[4], s);
+  FTS_EV();
   FTS_LAUNCH(k_rp_terms_fixed, B * (3 + 2 * n), 64, s, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, tables, d.terms);
-  if (ev) hipEventRecord(ev[5], s);
+  FTS_EV();
   FTS_LAUNCH(k_rp_terms_var, B * (3 + 2 * k), 64, s, B, n, k, d.status, d.ipa_flag, d.pts, d.ch, d.terms, d.scratch);
-  if (ev) hipEventRecord(ev[6], s);
+  FTS_EV();
   FTS_LAUNCH(k_rp_check, B, 64, s, B, n, k, d.status, d.ipa_flag, d.terms, d.com);
-  if (ev) hipEventRecord(ev[7], s);
+  FTS_EV();
+#undef FTS_EV
 }
 
 }  // namespace fts

@@ -1,0 +1,50 @@
+"""ctypes binding of the C oracle (oracle/c/ref_verify.c) — test
+infrastructure and bench.py's cpu_baseline leg only.  Build: make -C oracle/c
+(outputs oracle/_build/libref_verify.so)."""
+import ctypes as C
+import os
+import subprocess
+
+from . import bn254 as bn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "libref_verify.so")
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "c")])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        _lib = C.CDLL(LIB)
+        _lib.oracle_rp_verify.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, C.c_size_t]
+        _lib.oracle_rp_verify.restype = C.c_int
+        _lib.oracle_rp_verify_many.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_char_p, C.POINTER(C.c_char_p),
+                                               C.POINTER(C.c_size_t), C.c_int, C.POINTER(C.c_int32)]
+        _lib.oracle_rp_verify_many.restype = C.c_int
+    return _lib
+
+
+def gens_blob(pp):
+    """[G=ped1, H=ped2, P, Q, L..., R...] as in bulletproof.go's rangeVerifier"""
+    pts = [pp.ped[1], pp.ped[2], pp.P, pp.Q] + list(pp.left) + list(pp.right)
+    return b"".join(bn.g1_bytes(p) for p in pts)
+
+
+def rp_verify(pp, com64, der):
+    return lib().oracle_rp_verify(gens_blob(pp), pp.bit_length, com64, der, len(der))
+
+
+def rp_verify_many(pp, coms, ders, threads=1):
+    n = len(ders)
+    arr = (C.c_char_p * n)(*ders)
+    lens = (C.c_size_t * n)(*[len(d) for d in ders])
+    out = (C.c_int32 * n)()
+    rc = lib().oracle_rp_verify_many(gens_blob(pp), pp.bit_length, n, b"".join(coms), arr, lens, threads, out)
+    assert rc == 0
+    return list(out)
