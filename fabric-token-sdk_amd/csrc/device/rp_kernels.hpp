@@ -38,9 +38,35 @@ inline __host__ __device__ uint32_t x0_slot_bytes(int n) { return ((x0_msg_len(n
 // small transcripts slot (x: 258 B, y: 388 B, x_j: 258 B, z: 32 B) -> 512 B scratch each
 constexpr uint32_t SMALL_SLOT = 512;
 
-// per-kernel timing events of launch_rp_verify (names in fts_api.cpp)
-constexpr int RP_NUM_KERNELS = 10;
-constexpr int RP_NUM_EVENTS = RP_NUM_KERNELS + 1;
+// per-kernel device timeline: events recorded on the launch stream after
+// each kernel; time of mark i = elapsed(mark i-1, mark i)
+struct Timeline {
+  static constexpr int CAP = 40;
+  hipEvent_t ev[CAP + 1];
+  const char* name[CAP];
+  int n = 0;
+  bool created = false;
+  void create() {
+    if (created) return;
+    for (int i = 0; i <= CAP; i++) (void)hipEventCreate(&ev[i]);
+    created = true;
+  }
+  void destroy() {
+    if (!created) return;
+    for (int i = 0; i <= CAP; i++) (void)hipEventDestroy(ev[i]);
+    created = false;
+  }
+  void begin(hipStream_t s) {
+    n = 0;
+    (void)hipEventRecord(ev[0], s);
+  }
+  void mark(const char* nm, hipStream_t s) {
+    if (n >= CAP) return;
+    name[n] = nm;
+    (void)hipEventRecord(ev[n + 1], s);
+    n++;
+  }
+};
 
 // device buffers of one range-proof batch (filled by fts_api.cpp)
 struct RpBatchDev {
@@ -62,4 +88,19 @@ struct RpBatchDev {
   uint32_t* scratch;   // var-base lane tables
 };
 
+}  // namespace fts
+
+#include "msm.hpp"
+namespace fts {
+// device buffers of the random-linear-combination check
+struct RlcDev {
+  uint32_t* key;     // [8] ChaCha20 key (fresh per call)
+  uint32_t* msc;     // [B][5+2k][8] MSM scalars (canonical)
+  uint32_t* coef;    // [B][5][8]
+  uint32_t* colsum;  // [3+2n][8]
+  uint32_t* fixed;   // [3+2n][24]
+  int32_t* flag;     // [1]
+  uint32_t* msm_scratch;
+  MsmPlan plan;
+};
 }  // namespace fts

@@ -14,6 +14,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <sys/random.h>
 #include <vector>
 
 #include "../../include/fts_gpu.h"
@@ -31,8 +32,10 @@ namespace fts {
 size_t rp_scratch_words(int B, int n, int k);
 size_t rp_terms_words(int B, int n, int k);
 void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s);
-void launch_rp_verify(const RpBatchDev& d, const uint32_t* tables, const uint8_t* x0_const, hipStream_t s,
-                      hipEvent_t* ev);
+void launch_rp_exact(const RpBatchDev& d, const uint32_t* tables, const uint8_t* x0_const, hipStream_t s,
+                     Timeline* tl);
+void launch_rp_rlc(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, hipStream_t s, Timeline* tl);
+void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, hipStream_t s, Timeline* tl);
 void launch_sig_prep(const SigBatchDev& d, hipStream_t s);
 void launch_sig_finish(const SigBatchDev& d, const uint32_t* tables, int n, hipStream_t s);
 constexpr size_t FB_WORDS = 32 * 128 * 16;
@@ -79,21 +82,22 @@ struct DBuf {
 
 struct Workspace {
   DBuf pts, ch, small, hpj, hpa, hpbe, com, combe, x0, terms, scratch;
+  // random-linear-combination check + MSM
+  DBuf r_key, r_msc, r_coef, r_colsum, r_fixed, r_flag, m_keys, m_counts, m_offsets, m_cursor, m_sorted, m_buckets,
+      m_segs, m_wins, m_out, m_scratch;
   // action (transfer / issue) batches
   DBuf rp_raw, rp_sc, rp_status, rp_ipa;
   DBuf s_act, s_raw, s_owner, s_pts, s_sc, s_status, s_work, s_terms, s_aff, s_affoff, s_msgs, s_jac, s_scratch;
   void release() {
     for (DBuf* b : {&pts, &ch, &small, &hpj, &hpa, &hpbe, &com, &combe, &x0, &terms, &scratch, &rp_raw, &rp_sc,
                     &rp_status, &rp_ipa, &s_act, &s_raw, &s_owner, &s_pts, &s_sc, &s_status, &s_work, &s_terms, &s_aff,
-                    &s_affoff, &s_msgs, &s_jac, &s_scratch})
+                    &s_affoff, &s_msgs, &s_jac, &s_scratch, &r_key, &r_msc, &r_coef, &r_colsum, &r_fixed, &r_flag,
+                    &m_keys, &m_counts, &m_offsets, &m_cursor, &m_sorted, &m_buckets, &m_segs, &m_wins, &m_out,
+                    &m_scratch})
       b->release();
   }
 };
 
-const int kNumEv = RP_NUM_EVENTS;
-const char* kPhaseNames[RP_NUM_KERNELS] = {"k_rp_decode",   "k_rp_challenges", "k_rp_hprime",      "k_rp_hp_normalize",
-                                           "k_rp_com",      "k_rp_x0_build",   "k_rp_x0_hash",     "k_rp_terms_fixed",
-                                           "k_rp_terms_var", "k_rp_check"};
 
 }  // namespace
 
@@ -107,8 +111,11 @@ struct fts_ctx {
   size_t table_bytes = 0;
   std::mutex mu;
   Workspace ws;
-  hipEvent_t ev[kNumEv];
-  float timings[kNumEv - 1] = {0};
+  Timeline tl;
+  int ntim = 0;
+  const char* tim_name[Timeline::CAP];
+  float tim_ms[Timeline::CAP];
+  int last_fallback = 0;
   std::once_flag prover_once;
   ProverTables ptab;
 };
@@ -185,7 +192,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   };
   if (hipSetDevice(device) != hipSuccess) return fail(FTS_API_EDEVICE);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
-  for (int i = 0; i < kNumEv; i++) hipEventCreate(&c->ev[i]);
+  c->tl.create();
   const int n = c->n;
   // fixed bases in table order (rp_kernels.hpp tb_*)
   std::vector<G1A> bases;
@@ -258,7 +265,7 @@ void fts_ctx_destroy(fts_ctx* c) {
   c->ws.release();
   if (c->d_tables) hipFree(c->d_tables);
   if (c->d_x0const) hipFree(c->d_x0const);
-  for (int i = 0; i < kNumEv; i++) hipEventDestroy(c->ev[i]);
+  c->tl.destroy();
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -293,10 +300,10 @@ const char* fts_status_str(int32_t s) {
 
 int fts_last_timings(const fts_ctx* c, const char** names, float* ms, int cap) {
   if (!c) return 0;
-  int m = std::min(cap, kNumEv - 1);
+  int m = std::min(cap, c->ntim);
   for (int i = 0; i < m; i++) {
-    if (names) names[i] = kPhaseNames[i];
-    if (ms) ms[i] = c->timings[i];
+    if (names) names[i] = c->tim_name[i];
+    if (ms) ms[i] = c->tim_ms[i];
   }
   return m;
 }
@@ -337,14 +344,42 @@ static void parse_rp_batch(int k, size_t B, const uint8_t* const* der_p, const s
   for (auto& t : th) t.join();
 }
 
-static int launch_rp(fts_ctx* c, int B, uint8_t* d_raw, uint32_t* d_sc, int32_t* d_status, int32_t* d_ipa) {
-  const int n = c->n, k = c->k;
+static void collect_timings(fts_ctx* c) {
+  c->ntim = c->tl.n;
+  for (int i = 0; i < c->tl.n; i++) {
+    c->tim_name[i] = c->tl.name[i];
+    hipEventElapsedTime(&c->tim_ms[i], c->tl.ev[i], c->tl.ev[i + 1]);
+  }
+}
+
+// Range-proof pipeline on B proofs already on the device: exact phase, RLC
+// batch check, and the per-proof fallback when the combination fails.
+// `between` (optional) is launched after the RLC check and before the flag
+// sync (the sigma-proof kernels of transfer/issue batches).
+template <class F>
+static int rp_pipeline(fts_ctx* c, int B, uint8_t* d_raw, uint32_t* d_sc, int32_t* d_status, int32_t* d_ipa,
+                       F&& between) {
+  const int n = c->n, k = c->k, npts = rp_npts(k);
   Workspace& w = c->ws;
-  if (w.pts.ensure((size_t)B * rp_npts(k) * 64) || w.ch.ensure((size_t)B * rp_nch(k) * 32) ||
+  const int N = B * npts;
+  MsmPlan mp{};
+  mp.N = N;
+  mp.c = msm_window_bits(N);
+  mp.nw = msm_windows(mp.c);
+  mp.nb = 1 << (mp.c - 1);
+  mp.seg = std::min(16, mp.nb);
+  mp.nseg = mp.nb / mp.seg;
+  if (w.pts.ensure((size_t)B * npts * 64) || w.ch.ensure((size_t)B * rp_nch(k) * 32) ||
       w.small.ensure((size_t)B * SMALL_SLOT) || w.hpj.ensure((size_t)B * n * 96) || w.hpa.ensure((size_t)B * n * 64) ||
       w.hpbe.ensure((size_t)B * n * 64) || w.com.ensure((size_t)B * 64) || w.combe.ensure((size_t)B * 64) ||
       w.x0.ensure((size_t)B * x0_slot_bytes(n)) || w.terms.ensure(rp_terms_words(B, n, k) * 4) ||
-      w.scratch.ensure(std::max(rp_scratch_words(B, n, k), (size_t)B * 10 * 24) * 4))
+      w.scratch.ensure(std::max(rp_scratch_words(B, n, k), (size_t)B * 10 * 24) * 4) || w.r_key.ensure(32) ||
+      w.r_msc.ensure((size_t)N * 32) || w.r_coef.ensure((size_t)B * 5 * 32) || w.r_colsum.ensure((3 + 2 * n) * 32) ||
+      w.r_fixed.ensure((3 + 2 * n) * 96) || w.r_flag.ensure(4) || w.m_keys.ensure((size_t)mp.nw * N * 4) ||
+      w.m_counts.ensure((size_t)mp.nw * mp.nb * 4) || w.m_offsets.ensure((size_t)mp.nw * mp.nb * 4) ||
+      w.m_cursor.ensure((size_t)mp.nw * mp.nb * 4) || w.m_sorted.ensure((size_t)mp.nw * N * 4) ||
+      w.m_buckets.ensure((size_t)mp.nw * mp.nb * 96) || w.m_segs.ensure((size_t)mp.nw * mp.nseg * 96) ||
+      w.m_wins.ensure((size_t)mp.nw * 96) || w.m_out.ensure(96) || w.m_scratch.ensure((size_t)mp.nw * mp.nseg * 96))
     return FTS_API_ENOMEM;
   RpBatchDev d{B,
                n,
@@ -364,18 +399,44 @@ static int launch_rp(fts_ctx* c, int B, uint8_t* d_raw, uint32_t* d_sc, int32_t*
                w.x0.as<uint8_t>(),
                w.terms.as<uint32_t>(),
                w.scratch.as<uint32_t>()};
-  launch_rp_verify(d, c->d_tables, c->d_x0const, c->stream, c->ev);
+  mp.keys = w.m_keys.as<int32_t>();
+  mp.counts = w.m_counts.as<uint32_t>();
+  mp.offsets = w.m_offsets.as<uint32_t>();
+  mp.cursor = w.m_cursor.as<uint32_t>();
+  mp.sorted = w.m_sorted.as<uint32_t>();
+  mp.buckets = w.m_buckets.as<uint32_t>();
+  mp.segs = w.m_segs.as<uint32_t>();
+  mp.wins = w.m_wins.as<uint32_t>();
+  mp.out = w.m_out.as<uint32_t>();
+  RlcDev r{w.r_key.as<uint32_t>(), w.r_msc.as<uint32_t>(),   w.r_coef.as<uint32_t>(), w.r_colsum.as<uint32_t>(),
+           w.r_fixed.as<uint32_t>(), w.r_flag.as<int32_t>(), w.m_scratch.as<uint32_t>(), mp};
+  // fresh RLC weights key (getrandom), unpredictable to the provers
+  uint32_t key[8];
+  if (getrandom(key, sizeof key, 0) != (ssize_t)sizeof key) return FTS_API_EDEVICE;
+  HIP_OK(hipMemcpyAsync(r.key, key, sizeof key, hipMemcpyHostToDevice, c->stream));
+  c->tl.begin(c->stream);
+  launch_rp_exact(d, c->d_tables, c->d_x0const, c->stream, &c->tl);
+  launch_rp_rlc(d, r, c->d_tables, c->stream, &c->tl);
+  between();
   HIP_OK(hipGetLastError());
+  int32_t flag = 0;
+  HIP_OK(hipMemcpyAsync(&flag, r.flag, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  c->last_fallback = flag ? 0 : 1;
+  if (!flag) {
+    launch_rp_fallback(d, c->d_tables, c->stream, &c->tl);
+    HIP_OK(hipGetLastError());
+  }
   return FTS_API_OK;
 }
 
 static int run_rp(fts_ctx* c, int B, uint8_t* d_raw, uint32_t* d_sc, int32_t* d_status, int32_t* d_ipa,
                   int32_t* host_status) {
-  int rc = launch_rp(c, B, d_raw, d_sc, d_status, d_ipa);
+  int rc = rp_pipeline(c, B, d_raw, d_sc, d_status, d_ipa, [] {});
   if (rc != FTS_API_OK) return rc;
   if (host_status) HIP_OK(hipMemcpyAsync(host_status, d_status, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
-  for (int i = 0; i + 1 < kNumEv; i++) hipEventElapsedTime(&c->timings[i], c->ev[i], c->ev[i + 1]);
+  collect_timings(c);
   return FTS_API_OK;
 }
 
@@ -740,12 +801,16 @@ static int verify_actions(fts_ctx* c, const std::vector<ActionIn>& acts, int32_t
     sd.rp_k = k;
     launch_sig_prep(sd, c->stream);
   }
+  auto sig_finish = [&]() {
+    if (SA) launch_sig_finish(sd, c->d_tables, n, c->stream);
+  };
   if (rp_total) {
-    int rc = launch_rp(c, rp_total, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
-                       w.rp_ipa.as<int32_t>());
+    int rc = rp_pipeline(c, rp_total, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
+                         w.rp_ipa.as<int32_t>(), sig_finish);
     if (rc != FTS_API_OK) return rc;
+  } else {
+    sig_finish();
   }
-  if (SA) launch_sig_finish(sd, c->d_tables, n, c->stream);
   HIP_OK(hipGetLastError());
   std::vector<int32_t> sig_res(SA), rp_res(rp_total);
   if (SA) HIP_OK(hipMemcpyAsync(sig_res.data(), w.s_status.p, SA * 4, hipMemcpyDeviceToHost, c->stream));

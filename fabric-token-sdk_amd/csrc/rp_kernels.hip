@@ -25,6 +25,8 @@
 #include "device/rp_kernels.hpp"
 #include "device/transcript.hpp"
 #include "device/helpers.hpp"
+#include "device/msm.hpp"
+#include "common/chacha20.hpp"
 #include "../../include/fts_gpu.h"
 
 namespace fts {
@@ -232,6 +234,7 @@ __global__ void __launch_bounds__(64) k_rp_com(int B, int n, int k, const int32_
   acc = add_via(tmp, acc, fixed_base_mul(tables + (size_t)tb_P(n) * FB_WORDS_PER_BASE, s));  // - delta*P
   G1A ca = nl_to_affine(acc);
   store_g1a(com + (size_t)b * 16, ca);
+  store_g1a(const_cast<uint32_t*>(Pt) + RP_PT_C * 16, ca);  // C is consumed: slot reused by the RLC MSM
   uint32_t pw[16];
   g1_mont_to_be_words(ca.x, ca.y, pw);
   uint4* d = reinterpret_cast<uint4*>(com_be + (size_t)b * 64);
@@ -429,6 +432,139 @@ __global__ void __launch_bounds__(64) k_rp_check(int B, int n, int k, int32_t* _
   status[b] = g1j_is_identity(e2) ? FTS_OK : FTS_E_IPA_INVALID;
 }
 
+// ------------------------------------------------------------ RLC batch check
+// Sum_p rho_p E1_p + rho'_p E2_p == O  (SURVEY Appendix B).  Fixed bases get
+// batch-summed scalars (column reduction), variable points go to one MSM.
+// coef per proof (Montgomery Fr): [rho(ip - polEval), rho tau, rho'(ab - ip)x0, rho' a, rho' b]
+constexpr int RLC_NCOEF = 5;
+
+FTS_DEV Fr fr_from_u128(const uint32_t w[4]) {
+  Fr a = f_zero<FrP>();
+  a.v[0] = w[0];
+  a.v[1] = w[1];
+  a.v[2] = w[2];
+  a.v[3] = w[3];
+  return f_to_mont(a);
+}
+
+__global__ void __launch_bounds__(64) k_rlc_prep(int B, int n, int k, const int32_t* __restrict__ status,
+                                                 const int32_t* __restrict__ ipa_flag, const uint32_t* __restrict__ sc,
+                                                 const uint32_t* __restrict__ ch, const uint32_t* __restrict__ key,
+                                                 uint32_t* __restrict__ msc, uint32_t* __restrict__ coef) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int npts = rp_npts(k);
+  uint32_t* M = msc + (size_t)b * npts * 8;
+  uint32_t* K = coef + (size_t)b * RLC_NCOEF * 8;
+  const bool e1 = status[b] == 0;
+  const bool e2 = e1 && ipa_flag[b] == 0;
+  Fr zero = f_zero<FrP>();
+  for (int q = 0; q < npts; q++) store_f(M + q * 8, zero);
+  for (int q = 0; q < RLC_NCOEF; q++) store_f(K + q * 8, zero);
+  if (!e1) return;
+  uint32_t kk[8], blk[16];
+#pragma unroll
+  for (int q = 0; q < 8; q++) kk[q] = key[q];
+  chacha20_block(kk, (uint32_t)b, blk);
+  Fr rho = fr_from_u128(blk), rho2 = fr_from_u128(blk + 4);
+  const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
+  const uint32_t* S = sc + (size_t)b * RP_NSC * 8;
+  Fr x, x2, z2, pol;
+  load_f(C + CH_X * 8, x);
+  load_f(C + CH_X2 * 8, x2);
+  load_f(C + CH_Z2 * 8, z2);
+  load_f(C + CH_POL * 8, pol);
+  Fr ip = fr_from_canon(S + RP_SC_IP * 8);
+  auto put = [&](int slot, const Fr& v) { store_f(M + slot * 8, f_from_mont(f_neg(v))); };  // canonical, negated
+  put(RP_PT_T1, fr_mul(rho, x));
+  put(RP_PT_T2, fr_mul(rho, x2));
+  put(RP_PT_V, fr_mul(rho, z2));
+  store_f(K + 0 * 8, fr_mul(rho, f_sub(ip, pol)));
+  store_f(K + 1 * 8, fr_mul(rho, fr_from_canon(S + RP_SC_TAU * 8)));
+  if (!e2) return;
+  Fr a = fr_from_canon(S + RP_SC_A * 8), bb = fr_from_canon(S + RP_SC_B * 8), x0;
+  load_f(C + CH_X0 * 8, x0);
+  put(RP_PT_C, rho2);  // slot C holds com
+  for (int j = 0; j < k; j++) {
+    Fr xj, xji;
+    load_f(C + (CH_XJ + j) * 8, xj);
+    load_f(C + (CH_XJ + k + j) * 8, xji);
+    put(RP_PT_L + j, fr_mul(rho2, fr_sqr(xj)));
+    put(RP_PT_L + k + j, fr_mul(rho2, fr_sqr(xji)));
+  }
+  store_f(K + 2 * 8, fr_mul(rho2, fr_mul(f_sub(fr_mul(a, bb), ip), x0)));
+  store_f(K + 3 * 8, fr_mul(rho2, a));
+  store_f(K + 4 * 8, fr_mul(rho2, bb));
+}
+
+// one block per column: col 0 G (ped1), 1 H (ped2), 2 Q, 3+i G_i, 3+n+i H_i
+__global__ void __launch_bounds__(256) k_rlc_columns(int B, int n, int k, const uint32_t* __restrict__ ch,
+                                                     const uint32_t* __restrict__ coef, uint32_t* __restrict__ colsum) {
+  __shared__ uint32_t sh[256 * 8];
+  const int col = blockIdx.x, t = threadIdx.x;
+  Fr acc = f_zero<FrP>();
+  for (int b = t; b < B; b += 256) {
+    const uint32_t* K = coef + (size_t)b * RLC_NCOEF * 8;
+    const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
+    Fr v;
+    if (col < 3) {
+      load_f(K + col * 8, v);
+    } else if (col < 3 + n) {
+      Fr ra;
+      load_f(K + 3 * 8, ra);
+      v = f_is_zero(ra) ? ra : fr_mul(ra, s_vec(C, k, col - 3));
+    } else {
+      int i = col - 3 - n;
+      Fr rb;
+      load_f(K + 4 * 8, rb);
+      if (!f_is_zero(rb)) {
+        Fr yinv;
+        load_f(C + CH_YINV * 8, yinv);
+        v = fr_mul(fr_mul(rb, s_vec(C, k, n - 1 - i)), fr_pow_small(yinv, (uint32_t)i));
+      } else {
+        v = rb;
+      }
+    }
+    acc = f_add(acc, v);
+  }
+  store_f(sh + t * 8, acc);
+  __syncthreads();
+  for (int half = 128; half >= 1; half >>= 1) {
+    if (t < half) {
+      Fr o;
+      load_f(sh + (t + half) * 8, o);
+      acc = f_add(acc, o);
+      store_f(sh + t * 8, acc);
+    }
+    __syncthreads();
+  }
+  if (t == 0) store_f(colsum + col * 8, f_from_mont(acc));
+}
+
+__global__ void __launch_bounds__(64) k_rlc_fixed(int n, const uint32_t* __restrict__ colsum,
+                                                  const uint32_t* __restrict__ tables, uint32_t* __restrict__ out) {
+  int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= 3 + 2 * n) return;
+  int base = col == 0 ? tb_G(n) : col == 1 ? tb_H(n) : col == 2 ? tb_Q(n) : col - 3;
+  Scalar s;
+#pragma unroll
+  for (int q = 0; q < 8; q++) s.v[q] = colsum[col * 8 + q];
+  store_g1j(out + (size_t)col * 24, fixed_base_mul(tables + (size_t)base * FB_WORDS_PER_BASE, s));
+}
+
+// batch verdict: flag = 1 if the combination is the identity; on success the
+// deferred IPA structural verdicts become final (their E1 held)
+__global__ void __launch_bounds__(64) k_rlc_finalize(int B, const uint32_t* __restrict__ msm_out,
+                                                     int32_t* __restrict__ status, const int32_t* __restrict__ ipa_flag,
+                                                     int32_t* __restrict__ flag) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  Fp z;
+  load_fp(msm_out + 16, z);
+  const bool pass = f_is_zero(z);
+  if (b == 0) *flag = pass ? 1 : 0;
+  if (b < B && pass && status[b] == 0 && ipa_flag[b] != 0) status[b] = ipa_flag[b];
+}
+
 // ------------------------------------------------------------ host launch
 #define FTS_LAUNCH(kern, nthreads, bs, stream, ...)                                   \
   do {                                                                                \
@@ -445,38 +581,51 @@ void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32
   FTS_LAUNCH(k_build_tables, nb * FB_WINDOWS, 64, s, bases, nb, tables, scratch);
 }
 
-// ev: RP_NUM_EVENTS events bracketing every kernel (may be null)
-void launch_rp_verify(const RpBatchDev& d, const uint32_t* tables, const uint8_t* x0_const, hipStream_t s,
-                      hipEvent_t* ev) {
+void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
+                uint32_t* scratch, hipStream_t s);
+
+// exact per-proof phase: everything that is hashed (challenges, H'_i, com, x0)
+void launch_rp_exact(const RpBatchDev& d, const uint32_t* tables, const uint8_t* x0_const, hipStream_t s,
+                     Timeline* tl) {
   const int B = d.B, n = d.n, k = d.k;
-  int e = 0;
-#define FTS_EV()                      \
-  do {                                \
-    if (ev) hipEventRecord(ev[e], s); \
-    e++;                              \
-  } while (0)
-  FTS_EV();
   FTS_LAUNCH(k_rp_decode, B * rp_npts(k), 256, s, B, rp_npts(k), d.raw, d.pts, d.status);
-  FTS_EV();
+  if (tl) tl->mark("k_rp_decode", s);
   FTS_LAUNCH(k_rp_challenges, B, 64, s, B, n, k, d.raw, d.status, d.ch, d.small_msgs);
-  FTS_EV();
+  if (tl) tl->mark("k_rp_challenges", s);
   FTS_LAUNCH(k_rp_hprime, B * n, 64, s, B, n, k, d.status, d.ch, tables, d.hpj);
-  FTS_EV();
+  if (tl) tl->mark("k_rp_hprime", s);
   FTS_LAUNCH(k_rp_hp_normalize, B, 64, s, B, n, d.status, d.hpj, d.hpa, d.hp_be);
-  FTS_EV();
+  if (tl) tl->mark("k_rp_hp_normalize", s);
   FTS_LAUNCH(k_rp_com, B, 64, s, B, n, k, d.status, d.pts, d.sc, d.ch, d.hpa, tables, d.com, d.com_be, d.scratch);
-  FTS_EV();
+  if (tl) tl->mark("k_rp_com", s);
   FTS_LAUNCH(k_rp_x0_build, B * (2 * n + 3), 256, s, B, n, d.status, d.hp_be, d.com_be, x0_const, d.sc, d.x0_msgs);
-  FTS_EV();
+  if (tl) tl->mark("k_rp_x0_build", s);
   FTS_LAUNCH(k_rp_x0_hash, B, 64, s, B, n, k, d.status, d.x0_msgs, d.ch);
-  FTS_EV();
+  if (tl) tl->mark("k_rp_x0_hash", s);
+}
+
+// random-linear-combination check of all final equations (one MSM)
+void launch_rp_rlc(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, hipStream_t s, Timeline* tl) {
+  const int B = d.B, n = d.n, k = d.k;
+  FTS_LAUNCH(k_rlc_prep, B, 64, s, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, r.key, r.msc, r.coef);
+  hipLaunchKernelGGL(k_rlc_columns, dim3(3 + 2 * n), dim3(256), 0, s, B, n, k, d.ch, r.coef, r.colsum);
+  FTS_LAUNCH(k_rlc_fixed, 3 + 2 * n, 64, s, n, r.colsum, tables, r.fixed);
+  if (tl) tl->mark("k_rlc_scalars", s);
+  launch_msm(r.plan, d.pts, r.msc, r.fixed, 3 + 2 * n, r.msm_scratch, s);
+  if (tl) tl->mark("k_msm", s);
+  FTS_LAUNCH(k_rlc_finalize, B > 0 ? B : 1, 64, s, B, r.plan.out, d.status, d.ipa_flag, r.flag);
+  if (tl) tl->mark("k_rlc_finalize", s);
+}
+
+// per-proof final equations (fallback when the batch combination fails)
+void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, hipStream_t s, Timeline* tl) {
+  const int B = d.B, n = d.n, k = d.k;
   FTS_LAUNCH(k_rp_terms_fixed, B * (3 + 2 * n), 64, s, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, tables, d.terms);
-  FTS_EV();
+  if (tl) tl->mark("k_rp_terms_fixed", s);
   FTS_LAUNCH(k_rp_terms_var, B * (3 + 2 * k), 64, s, B, n, k, d.status, d.ipa_flag, d.pts, d.ch, d.terms, d.scratch);
-  FTS_EV();
+  if (tl) tl->mark("k_rp_terms_var", s);
   FTS_LAUNCH(k_rp_check, B, 64, s, B, n, k, d.status, d.ipa_flag, d.terms, d.com);
-  FTS_EV();
-#undef FTS_EV
+  if (tl) tl->mark("k_rp_check", s);
 }
 
 }  // namespace fts
