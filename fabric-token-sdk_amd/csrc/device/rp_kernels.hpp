@@ -77,7 +77,7 @@ struct RpBatchDev {
   int32_t* ipa_flag;   // [B] deferred IPA structural verdicts
   uint32_t* pts;       // [B][5+2k][16] affine Montgomery
   uint32_t* ch;        // [B][8+2k][8] challenges (Montgomery Fr)
-  uint8_t* small_msgs; // [B][SMALL_SLOT]
+  uint8_t* small_msgs; // [B][2+k][SMALL_SLOT]
   uint32_t* hpj;       // [B][n][24]
   uint32_t* hpa;       // [B][n][16]
   uint8_t* hp_be;      // [B][n][64]

@@ -84,7 +84,7 @@ struct Workspace {
   DBuf pts, ch, small, hpj, hpa, hpbe, com, combe, x0, terms, scratch;
   // random-linear-combination check + MSM
   DBuf r_key, r_msc, r_coef, r_colsum, r_fixed, r_flag, m_keys, m_counts, m_offsets, m_cursor, m_sorted, m_buckets,
-      m_segs, m_wins, m_out, m_scratch;
+      m_segs, m_wins, m_out, m_scratch, m_win;
   // action (transfer / issue) batches
   DBuf rp_raw, rp_sc, rp_status, rp_ipa;
   DBuf s_act, s_raw, s_owner, s_pts, s_sc, s_status, s_work, s_terms, s_aff, s_affoff, s_msgs, s_jac, s_scratch;
@@ -93,7 +93,7 @@ struct Workspace {
                     &rp_status, &rp_ipa, &s_act, &s_raw, &s_owner, &s_pts, &s_sc, &s_status, &s_work, &s_terms, &s_aff,
                     &s_affoff, &s_msgs, &s_jac, &s_scratch, &r_key, &r_msc, &r_coef, &r_colsum, &r_fixed, &r_flag,
                     &m_keys, &m_counts, &m_offsets, &m_cursor, &m_sorted, &m_buckets, &m_segs, &m_wins, &m_out,
-                    &m_scratch})
+                    &m_scratch, &m_win})
       b->release();
   }
 };
@@ -363,23 +363,19 @@ static int rp_pipeline(fts_ctx* c, int B, uint8_t* d_raw, uint32_t* d_sc, int32_
   Workspace& w = c->ws;
   const int N = B * npts;
   MsmPlan mp{};
-  mp.N = N;
-  mp.c = msm_window_bits(N);
-  mp.nw = msm_windows(mp.c);
-  mp.nb = 1 << (mp.c - 1);
-  mp.seg = std::min(16, mp.nb);
-  mp.nseg = mp.nb / mp.seg;
+  msm_layout(N, mp);
   if (w.pts.ensure((size_t)B * npts * 64) || w.ch.ensure((size_t)B * rp_nch(k) * 32) ||
-      w.small.ensure((size_t)B * SMALL_SLOT) || w.hpj.ensure((size_t)B * n * 96) || w.hpa.ensure((size_t)B * n * 64) ||
+      w.small.ensure((size_t)B * (2 + k) * SMALL_SLOT) || w.hpj.ensure((size_t)B * n * 96) || w.hpa.ensure((size_t)B * n * 64) ||
       w.hpbe.ensure((size_t)B * n * 64) || w.com.ensure((size_t)B * 64) || w.combe.ensure((size_t)B * 64) ||
       w.x0.ensure((size_t)B * x0_slot_bytes(n)) || w.terms.ensure(rp_terms_words(B, n, k) * 4) ||
       w.scratch.ensure(std::max(rp_scratch_words(B, n, k), (size_t)B * 10 * 24) * 4) || w.r_key.ensure(32) ||
       w.r_msc.ensure((size_t)N * 32) || w.r_coef.ensure((size_t)B * 5 * 32) || w.r_colsum.ensure((3 + 2 * n) * 32) ||
       w.r_fixed.ensure((3 + 2 * n) * 96) || w.r_flag.ensure(4) || w.m_keys.ensure((size_t)mp.nw * N * 4) ||
-      w.m_counts.ensure((size_t)mp.nw * mp.nb * 4) || w.m_offsets.ensure((size_t)mp.nw * mp.nb * 4) ||
-      w.m_cursor.ensure((size_t)mp.nw * mp.nb * 4) || w.m_sorted.ensure((size_t)mp.nw * N * 4) ||
-      w.m_buckets.ensure((size_t)mp.nw * mp.nb * 96) || w.m_segs.ensure((size_t)mp.nw * mp.nseg * 96) ||
-      w.m_wins.ensure((size_t)mp.nw * 96) || w.m_out.ensure(96) || w.m_scratch.ensure((size_t)mp.nw * mp.nseg * 96))
+      w.m_counts.ensure((size_t)mp.NB * 4) || w.m_offsets.ensure((size_t)mp.NB * 4) ||
+      w.m_cursor.ensure((size_t)mp.NB * 4) || w.m_sorted.ensure((size_t)mp.nw * N * 4) ||
+      w.m_buckets.ensure((size_t)mp.NB * 96) || w.m_segs.ensure((size_t)mp.NS * 96) ||
+      w.m_wins.ensure((size_t)mp.nw * 96) || w.m_out.ensure(96) || w.m_scratch.ensure((size_t)mp.NS * 96) ||
+      w.m_win.ensure(sizeof(mp.win)))
     return FTS_API_ENOMEM;
   RpBatchDev d{B,
                n,
@@ -399,6 +395,8 @@ static int rp_pipeline(fts_ctx* c, int B, uint8_t* d_raw, uint32_t* d_sc, int32_
                w.x0.as<uint8_t>(),
                w.terms.as<uint32_t>(),
                w.scratch.as<uint32_t>()};
+  mp.d_win = w.m_win.as<MsmWindow>();
+  HIP_OK(hipMemcpyAsync(mp.d_win, mp.win, sizeof(MsmWindow) * mp.nw, hipMemcpyHostToDevice, c->stream));
   mp.keys = w.m_keys.as<int32_t>();
   mp.counts = w.m_counts.as<uint32_t>();
   mp.offsets = w.m_offsets.as<uint32_t>();

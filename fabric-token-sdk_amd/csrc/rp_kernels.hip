@@ -5,12 +5,12 @@
 // few thousand proofs fills the 256 CUs:
 //
 //   k_rp_decode        (proof, point)   NewG1FromBytes checks + Montgomery form
-//   k_rp_challenges    proof            x, y, z, x_j transcripts (SHA-256 over hex)
-//                                        + Fr side (polEval, inverses)   bulletproof.go:266-311, ipa.go:229-244
+//   k_rp_hash_small    (proof, msg)     x, y, x_j transcripts (SHA-256 over hex)  bulletproof.go:266-281, ipa.go:230
+//   k_rp_chal_fr       proof            z, polEval, batch inversion of y, x_j       bulletproof.go:282-311, ipa.go:236-244
 //   k_rp_hprime        (proof, i)       H'_i = y^-i * H_i  fixed-base    bulletproof.go:483-489
 //   k_rp_hp_normalize  proof            batch affine normalisation (Montgomery trick)
-//   k_rp_com           proof            com = x*D + C + z*K + z^2*W - delta*P   bulletproof.go:477-492
-//                                        (K = sum H_i - sum G_i, W = sum 2^i H'_i: same group element)
+//   k_rp_com_terms     (proof, term)    com = x*D + C + z*K + sum (z^2 2^i y^-i) H_i - delta*P
+//   k_rp_com_sum       proof (wave)     LDS tree + normalisation          bulletproof.go:477-492
 //   k_rp_x0_build      (proof, record)  DER(hex(H'..., G..., Q, com) "||" Zb(ip))   ipa.go:200-212
 //   k_rp_x0_hash       proof            x0 = HashToZr(...)                ipa.go:213
 //   k_rp_terms_fixed   (proof, term)    fixed-base terms of E1 / E2
@@ -85,22 +85,50 @@ __global__ void __launch_bounds__(256) k_rp_decode(int B, int npts, const uint8_
 }
 
 // -------------------------------------------------------------- challenges
-__global__ void __launch_bounds__(64) k_rp_challenges(int B, int n, int k, const uint8_t* __restrict__ raw,
+// thread per (proof, message): message 0 = Arr(T1, T2) -> x; 1 = Arr(C, D, V)
+// -> y; 2 + j = Arr(L_j, R_j) -> x_j  (bulletproof.go:266-281, ipa.go:230-235).
+// Digests (canonical Fr) land in the challenge block, converted later.
+__global__ void __launch_bounds__(64) k_rp_hash_small(int B, int n, int k, const uint8_t* __restrict__ raw,
                                                       const int32_t* __restrict__ status, uint32_t* __restrict__ ch,
                                                       uint8_t* __restrict__ small_msgs) {
+  const int nm = 2 + k;
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= B * nm) return;
+  const int b = gid / nm, m = gid % nm;
+  if (status[b] != 0) return;
+  const uint8_t* P = raw + (size_t)b * rp_npts(k) * 64;
+  uint8_t* slot = small_msgs + (size_t)gid * SMALL_SLOT;
+  uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
+  Fr h;
+  int dst;
+  if (m == 0) {
+    const uint8_t* px[2] = {P + RP_PT_T1 * 64, P + RP_PT_T2 * 64};
+    h = hash_raw_points(slot, px, 2);
+    dst = CH_X;
+  } else if (m == 1) {
+    const uint8_t* py[3] = {P + RP_PT_C * 64, P + RP_PT_D * 64, P + RP_PT_V * 64};
+    h = hash_raw_points(slot, py, 3);
+    dst = CH_Y;
+  } else {
+    const int j = m - 2;
+    const uint8_t* pl[2] = {P + (RP_PT_L + j) * 64, P + (RP_PT_L + k + j) * 64};
+    h = hash_raw_points(slot, pl, 2);
+    dst = CH_XJ + j;
+  }
+  store_f(C + dst * 8, h);  // canonical for now
+}
+
+// thread per proof: z = Hz(Zb(y)), Montgomery forms, polEval, and one batch
+// inversion (Montgomery trick) for y and the k round challenges
+__global__ void __launch_bounds__(64) k_rp_chal_fr(int B, int n, int k, const int32_t* __restrict__ status,
+                                                   uint32_t* __restrict__ ch, uint32_t* __restrict__ tmp) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B || status[b] != 0) return;
-  const int npts = rp_npts(k);
-  const uint8_t* P = raw + (size_t)b * npts * 64;
-  uint8_t* slot = small_msgs + (size_t)b * SMALL_SLOT;
   uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
-
-  // x = Hz(Arr(T1, T2))                                  bulletproof.go:266-273
-  const uint8_t* px[2] = {P + RP_PT_T1 * 64, P + RP_PT_T2 * 64};
-  Fr x = f_to_mont(hash_raw_points(slot, px, 2));
-  // y = Hz(Arr(C, D, V)); z = Hz(Zb(y))                  bulletproof.go:276-282
-  const uint8_t* py[3] = {P + RP_PT_C * 64, P + RP_PT_D * 64, P + RP_PT_V * 64};
-  Fr yc = hash_raw_points(slot, py, 3);
+  uint32_t* T = tmp + (size_t)b * (k + 1) * 8;  // prefix products
+  Fr yc, xc;
+  load_f(C + CH_Y * 8, yc);
+  load_f(C + CH_X * 8, xc);
   uint32_t w[16], st[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) w[i] = yc.v[7 - i];
@@ -111,10 +139,8 @@ __global__ void __launch_bounds__(64) k_rp_challenges(int B, int n, int k, const
   sha256_init(st);
   sha256_compress(st, w);
   Fr z = f_to_mont(digest_to_fr(st));
-  Fr y = f_to_mont(yc);
-
+  Fr y = f_to_mont(yc), x = f_to_mont(xc);
   Fr x2 = fr_sqr(x), z2 = fr_sqr(z), z3 = fr_mul(z2, z);
-  // ipy = sum y^i, ip2 = sum 2^i                           bulletproof.go:287-305
   Fr yp = f_one<FrP>(), ipy = f_zero<FrP>(), p2 = f_one<FrP>(), ip2 = f_zero<FrP>();
   for (int i = 0; i < n; i++) {
     if (i) {
@@ -125,20 +151,37 @@ __global__ void __launch_bounds__(64) k_rp_challenges(int B, int n, int k, const
     ip2 = f_add(ip2, p2);
   }
   Fr pol = f_sub(fr_mul(f_sub(z, z2), ipy), fr_mul(z3, ip2));  // bulletproof.go:307-311
-
   store_f(C + CH_X * 8, x);
   store_f(C + CH_X2 * 8, x2);
   store_f(C + CH_Y * 8, y);
-  store_f(C + CH_YINV * 8, nl_fr_inv(y));
   store_f(C + CH_Z * 8, z);
   store_f(C + CH_Z2 * 8, z2);
   store_f(C + CH_POL * 8, pol);
-  // round challenges x_j = Hz(Arr(L_j, R_j))             ipa.go:229-238
-  for (int j = 0; j < k; j++) {
-    const uint8_t* pl[2] = {P + (RP_PT_L + j) * 64, P + (RP_PT_L + k + j) * 64};
-    Fr xj = f_to_mont(hash_raw_points(slot, pl, 2));
-    store_f(C + (CH_XJ + j) * 8, xj);
-    store_f(C + (CH_XJ + k + j) * 8, nl_fr_inv(xj));
+  // batch inversion of v_0 = y, v_{1+j} = x_j (zeros invert to zero, as Fermat does)
+  Fr acc = f_one<FrP>();
+  for (int q = 0; q <= k; q++) {
+    Fr v;
+    if (q == 0) v = y;
+    else {
+      load_f(C + (CH_XJ + q - 1) * 8, v);
+      v = f_to_mont(v);
+      store_f(C + (CH_XJ + q - 1) * 8, v);
+    }
+    store_f(T + q * 8, acc);
+    if (!f_is_zero(v)) acc = fr_mul(acc, v);
+  }
+  Fr inv = nl_fr_inv(acc);
+  for (int q = k; q >= 0; q--) {
+    Fr v, pre;
+    if (q == 0) v = y;
+    else load_f(C + (CH_XJ + q - 1) * 8, v);
+    load_f(T + q * 8, pre);
+    Fr vi = f_zero<FrP>();
+    if (!f_is_zero(v)) {
+      vi = fr_mul(inv, pre);
+      inv = fr_mul(inv, v);
+    }
+    store_f(C + (q == 0 ? CH_YINV : CH_XJ + k + q - 1) * 8, vi);
   }
 }
 
@@ -199,49 +242,88 @@ __global__ void __launch_bounds__(64) k_rp_hp_normalize(int B, int n, const int3
 }
 
 // -------------------------------------------------------------------- com
-__global__ void __launch_bounds__(64) k_rp_com(int B, int n, int k, const int32_t* __restrict__ status,
-                                               const uint32_t* __restrict__ pts, const uint32_t* __restrict__ sc,
-                                               const uint32_t* __restrict__ ch, const uint32_t* __restrict__ hpa,
-                                               const uint32_t* __restrict__ tables, uint32_t* __restrict__ com,
-                                               uint8_t* __restrict__ com_be, uint32_t* __restrict__ scratch) {
-  int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B || status[b] != 0) return;
-  const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
-  const uint32_t* A = hpa + (size_t)b * n * 16;
-  const uint32_t* Pt = pts + (size_t)b * rp_npts(k) * 16;
-  uint32_t* scr = scratch + (size_t)b * 10 * 24;  // 8 table entries + affine copy + temp
-  uint32_t* tmp = scr + 9 * 24;
-  // W = sum 2^i H'_i (Horner)
-  G1J W = g1j_from_affine(load_g1a(A + (n - 1) * 16));
-  for (int i = n - 2; i >= 0; i--) W = nl_madd_mem(nl_dbl(W), A + i * 16, 0);
-  G1A Wa = nl_to_affine(W);
-  Fr x, z, z2;
-  load_f(C + CH_X * 8, x);
-  load_f(C + CH_Z * 8, z);
-  load_f(C + CH_Z2 * 8, z2);
-  G1J acc = var_base_mul(load_g1a(Pt + RP_PT_D * 16), fr_canon(x), scr);                     // x*D
-  acc = nl_madd_mem(acc, Pt + RP_PT_C * 16, 0);                                                // + C
-  acc = add_via(tmp, acc, fixed_base_mul(tables + (size_t)tb_K(n) * FB_WORDS_PER_BASE, fr_canon(z)));  // + z*K
-  acc = add_via(tmp, acc, var_base_mul(Wa, fr_canon(z2), scr));                               // + z^2*W
-  Scalar s;
-  {
-    Fr d;
-    load_f(sc + ((size_t)b * RP_NSC + RP_SC_DELTA) * 8, d);
-    Fr nd = f_neg(d);  // canonical negation: r - delta
-#pragma unroll
-    for (int i = 0; i < 8; i++) s.v[i] = nd.v[i];
+// com = x*D + C - z sum G_i + sum (z y^i + z^2 2^i) H'_i - delta*P   (bulletproof.go:477-492)
+//     = x*D + C + z*K + sum_i (z^2 2^i y^-i) H_i - delta*P,   K = sum H_i - sum G_i
+// (same group element; only the affine result is observable).  Terms per
+// proof: slots 0..n-1 fixed-base on H_i, n: z*K, n+1: -delta*P, n+2: x*D.
+inline __host__ __device__ int com_nterms(int n) { return n + 3; }
+
+__global__ void __launch_bounds__(64) k_rp_com_terms(int B, int n, int k, const int32_t* __restrict__ status,
+                                                     const uint32_t* __restrict__ pts, const uint32_t* __restrict__ sc,
+                                                     const uint32_t* __restrict__ ch, const uint32_t* __restrict__ tables,
+                                                     uint32_t* __restrict__ terms, uint32_t* __restrict__ scratch) {
+  const int nt = com_nterms(n);
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= B * nt) return;
+  // variable-base slots first in the grid so their long chains start early
+  int b, t;
+  if (gid < B) {
+    b = gid;
+    t = n + 2;
+  } else {
+    b = (gid - B) / (nt - 1);
+    t = (gid - B) % (nt - 1);
   }
-  acc = add_via(tmp, acc, fixed_base_mul(tables + (size_t)tb_P(n) * FB_WORDS_PER_BASE, s));  // - delta*P
-  G1A ca = nl_to_affine(acc);
-  store_g1a(com + (size_t)b * 16, ca);
-  store_g1a(const_cast<uint32_t*>(Pt) + RP_PT_C * 16, ca);  // C is consumed: slot reused by the RLC MSM
-  uint32_t pw[16];
-  g1_mont_to_be_words(ca.x, ca.y, pw);
-  uint4* d = reinterpret_cast<uint4*>(com_be + (size_t)b * 64);
+  if (status[b] != 0) return;
+  const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
+  uint32_t* out = terms + ((size_t)b * nt + t) * 24;
+  G1J r;
+  if (t < n) {
+    Fr z2, yinv;
+    load_f(C + CH_Z2 * 8, z2);
+    load_f(C + CH_YINV * 8, yinv);
+    // z^2 2^i y^-i
+    Fr s = fr_mul(z2, fr_pow_small(yinv, (uint32_t)t));
+    for (int q = 0; q < t; q++) s = f_dbl(s);
+    r = fixed_base_mul(tables + (size_t)(n + t) * FB_WORDS_PER_BASE, fr_canon(s));
+  } else if (t == n) {
+    Fr z;
+    load_f(C + CH_Z * 8, z);
+    r = fixed_base_mul(tables + (size_t)tb_K(n) * FB_WORDS_PER_BASE, fr_canon(z));
+  } else if (t == n + 1) {
+    Fr d;
+    load_f(sc + ((size_t)b * RP_NSC + RP_SC_DELTA) * 8, d);  // canonical
+    Fr nd = f_neg(d);
+    Scalar s;
 #pragma unroll
-  for (int q = 0; q < 4; q++)
-    d[q] = make_uint4(__builtin_bswap32(pw[4 * q]), __builtin_bswap32(pw[4 * q + 1]), __builtin_bswap32(pw[4 * q + 2]),
-                      __builtin_bswap32(pw[4 * q + 3]));
+    for (int q = 0; q < 8; q++) s.v[q] = nd.v[q];
+    r = fixed_base_mul(tables + (size_t)tb_P(n) * FB_WORDS_PER_BASE, s);
+  } else {
+    Fr x;
+    load_f(C + CH_X * 8, x);
+    r = var_base_mul(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_D) * 16), fr_canon(x),
+                     scratch + (size_t)b * 10 * 24);
+  }
+  store_g1j(out, r);
+}
+
+// one wave per proof: LDS tree over the n + 3 terms, + C, normalise
+__global__ void __launch_bounds__(64) k_rp_com_sum(int B, int n, int k, const int32_t* __restrict__ status,
+                                                   uint32_t* __restrict__ pts, const uint32_t* __restrict__ terms,
+                                                   uint32_t* __restrict__ com, uint8_t* __restrict__ com_be) {
+  __shared__ uint32_t sh[64 * 24];
+  const int b = blockIdx.x, t = threadIdx.x;
+  if (status[b] != 0) return;  // uniform per block
+  const int nt = com_nterms(n);
+  const uint32_t* T = terms + (size_t)b * nt * 24;
+  uint32_t* Pt = pts + (size_t)b * rp_npts(k) * 16;
+  G1J acc = g1j_identity();
+  for (int q = t; q < nt; q += 64) acc = nl_add_mem(acc, T + q * 24, 0);
+  if (t == 0) acc = nl_madd_mem(acc, Pt + RP_PT_C * 16, 0);  // + C
+  store_g1j(sh + t * 24, acc);
+  __syncthreads();
+  for (int half = 32; half >= 1; half >>= 1) {
+    if (t < half) acc = nl_add_mem(acc, sh + (t + half) * 24, 0);
+    __syncthreads();
+    if (t < half) store_g1j(sh + t * 24, acc);
+    __syncthreads();
+  }
+  if (t == 0) {
+    G1A ca = nl_to_affine(acc);
+    store_g1a(com + (size_t)b * 16, ca);
+    store_g1a(Pt + RP_PT_C * 16, ca);  // C is consumed: slot reused by the RLC MSM
+    store_point_be(com_be + (size_t)b * 64, ca);
+  }
 }
 
 // --------------------------------------------------------- x0 transcript
@@ -590,14 +672,19 @@ void launch_rp_exact(const RpBatchDev& d, const uint32_t* tables, const uint8_t*
   const int B = d.B, n = d.n, k = d.k;
   FTS_LAUNCH(k_rp_decode, B * rp_npts(k), 256, s, B, rp_npts(k), d.raw, d.pts, d.status);
   if (tl) tl->mark("k_rp_decode", s);
-  FTS_LAUNCH(k_rp_challenges, B, 64, s, B, n, k, d.raw, d.status, d.ch, d.small_msgs);
-  if (tl) tl->mark("k_rp_challenges", s);
+  FTS_LAUNCH(k_rp_hash_small, B * (2 + k), 64, s, B, n, k, d.raw, d.status, d.ch, d.small_msgs);
+  if (tl) tl->mark("k_rp_hash_small", s);
+  FTS_LAUNCH(k_rp_chal_fr, B, 64, s, B, n, k, d.status, d.ch, d.scratch);
+  if (tl) tl->mark("k_rp_chal_fr", s);
   FTS_LAUNCH(k_rp_hprime, B * n, 64, s, B, n, k, d.status, d.ch, tables, d.hpj);
   if (tl) tl->mark("k_rp_hprime", s);
   FTS_LAUNCH(k_rp_hp_normalize, B, 64, s, B, n, d.status, d.hpj, d.hpa, d.hp_be);
   if (tl) tl->mark("k_rp_hp_normalize", s);
-  FTS_LAUNCH(k_rp_com, B, 64, s, B, n, k, d.status, d.pts, d.sc, d.ch, d.hpa, tables, d.com, d.com_be, d.scratch);
-  if (tl) tl->mark("k_rp_com", s);
+  FTS_LAUNCH(k_rp_com_terms, B * com_nterms(n), 64, s, B, n, k, d.status, d.pts, d.sc, d.ch, tables, d.terms,
+             d.scratch);
+  if (tl) tl->mark("k_rp_com_terms", s);
+  if (B) hipLaunchKernelGGL(k_rp_com_sum, dim3(B), dim3(64), 0, s, B, n, k, d.status, d.pts, d.terms, d.com, d.com_be);
+  if (tl) tl->mark("k_rp_com_sum", s);
   FTS_LAUNCH(k_rp_x0_build, B * (2 * n + 3), 256, s, B, n, d.status, d.hp_be, d.com_be, x0_const, d.sc, d.x0_msgs);
   if (tl) tl->mark("k_rp_x0_build", s);
   FTS_LAUNCH(k_rp_x0_hash, B, 64, s, B, n, k, d.status, d.x0_msgs, d.ch);
