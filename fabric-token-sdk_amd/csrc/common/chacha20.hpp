@@ -4,7 +4,7 @@
 // the host draws a fresh 256-bit key per verification call from getrandom(),
 // and proof p takes block (key, counter = p) on the device, so the weights
 // are unpredictable to whoever produced the proofs (batch soundness error
-// <= 2^-128 per call with 128-bit weights).
+// ~2^-253 per call with full-width weights).
 #pragma once
 #include <stdint.h>
 #ifdef __HIPCC__

@@ -214,6 +214,48 @@ FTS_DEV Field<P> f_mul_fips(const Field<P>& a, const Field<P>& b) {
   return r;
 }
 
+// FIPS with two independent 96-bit accumulators per column (a*b products in
+// one, m*M products in the other): halves the dependent mad chain, which is
+// what bounds the latency-critical per-proof kernels.
+FTS_DEV void add96(uint64_t& acc, uint32_t& ovf, uint64_t acc2, uint32_t ovf2) {
+  uint32_t lo = (uint32_t)acc, hi = (uint32_t)(acc >> 32), c;
+  lo = addc(lo, (uint32_t)acc2, 0, c);
+  hi = addc(hi, (uint32_t)(acc2 >> 32), c, c);
+  ovf = ovf + ovf2 + c;
+  acc = ((uint64_t)hi << 32) | lo;
+}
+
+template <class P>
+FTS_DEV Field<P> f_mul_fips2(const Field<P>& a, const Field<P>& b) {
+  uint32_t m[8], t[8];
+  uint64_t acc = 0, acc2;
+  uint32_t ovf = 0, ovf2;
+#pragma unroll
+  for (int k = 0; k < 15; k++) {
+    acc2 = 0;
+    ovf2 = 0;
+#pragma unroll
+    for (int i = (k > 7 ? k - 7 : 0); i <= (k < 7 ? k : 7); i++) mac96(acc, ovf, a.v[i], b.v[k - i]);
+#pragma unroll
+    for (int i = (k > 7 ? k - 7 : 0); i < (k < 8 ? k : 8); i++) mac96s(acc2, ovf2, m[i], P::M[k - i]);
+    add96(acc, ovf, acc2, ovf2);
+    if (k < 8) {
+      m[k] = (uint32_t)acc * P::INV;
+      mac96s(acc, ovf, m[k], P::M[0]);
+    } else {
+      t[k - 8] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)ovf << 32);
+    ovf = 0;
+  }
+  t[7] = (uint32_t)acc;
+  Field<P> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = t[i];
+  f_reduce_once(r);
+  return r;
+}
+
 template <class P>
 FTS_DEV Field<P> f_sqr(const Field<P>& a) {
   return f_mul(a, a);

@@ -462,6 +462,26 @@ int fts_debug_rp_intermediates(fts_ctx* c, size_t i, uint8_t* ch_out, uint8_t* c
   return FTS_API_OK;
 }
 
+// debug: bucket-occupancy statistics of the last RLC MSM
+// out[0] = max bucket count, out[1] = its bucket index, out[2] = NB, out[3] = #nonzero buckets
+int fts_debug_msm_stats(fts_ctx* c, int64_t* out) {
+  if (!c || c->device < 0 || !out) return FTS_API_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  size_t nb = c->ws.m_counts.cap / 4;
+  std::vector<uint32_t> cnt(nb);
+  HIP_OK(hipMemcpy(cnt.data(), c->ws.m_counts.p, nb * 4, hipMemcpyDeviceToHost));
+  size_t arg = 0, nz = 0;
+  for (size_t i = 0; i < nb; i++) {
+    if (cnt[i] > cnt[arg]) arg = i;
+    nz += cnt[i] != 0;
+  }
+  out[0] = cnt[arg];
+  out[1] = (int64_t)arg;
+  out[2] = (int64_t)nb;
+  out[3] = (int64_t)nz;
+  return FTS_API_OK;
+}
+
 int fts_rp_batch_stage(fts_ctx* c, size_t n, const uint8_t* const* rp_der, const size_t* rp_len, const uint8_t* com64,
                        fts_rp_batch** out) {
   if (!c || !out || (n && (!rp_der || !rp_len || !com64))) return FTS_API_EINVAL;

@@ -8,6 +8,7 @@
 #include "device/g1.hpp"
 #include "device/helpers.hpp"
 #include "device/msm.hpp"
+#include "device/rp_kernels.hpp"
 
 namespace fts {
 
@@ -195,15 +196,22 @@ __global__ void k_msm_final(int nw, const MsmWindow* __restrict__ win, const uin
 
 // scratch: NS * 24 words.  p.d_win must already hold p.win (uploaded by the caller).
 void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
-                uint32_t* scratch, hipStream_t s) {
+                uint32_t* scratch, hipStream_t s, Timeline* tl) {
   (void)hipMemsetAsync(p.counts, 0, (size_t)p.NB * 4, s);
   FTS_LAUNCH(k_msm_digits, p.N, 256, s, p.N, p.nw, p.d_win, scalars, p.keys, p.counts);
+  if (tl) tl->mark("k_msm_digits", s);
   hipLaunchKernelGGL(k_msm_scan, dim3(p.nw), dim3(256), 0, s, p.d_win, p.counts, p.offsets, p.cursor);
+  if (tl) tl->mark("k_msm_scan", s);
   FTS_LAUNCH(k_msm_scatter, p.N, 256, s, p.N, p.nw, p.keys, p.cursor, p.sorted);
+  if (tl) tl->mark("k_msm_scatter", s);
   FTS_LAUNCH(k_msm_buckets, p.NB, 64, s, p.N, p.nw, p.NB, p.d_win, points, p.offsets, p.counts, p.sorted, p.buckets);
+  if (tl) tl->mark("k_msm_buckets", s);
   FTS_LAUNCH(k_msm_segments, p.NS, 64, s, p.nw, p.NS, p.d_win, p.buckets, p.segs, scratch);
+  if (tl) tl->mark("k_msm_segments", s);
   hipLaunchKernelGGL(k_msm_windows, dim3(p.nw), dim3(64), 0, s, p.d_win, p.segs, p.wins);
+  if (tl) tl->mark("k_msm_windows", s);
   hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, s, p.nw, p.d_win, p.wins, extra, nextra, p.out);
+  if (tl) tl->mark("k_msm_final", s);
 }
 
 }  // namespace fts

@@ -321,7 +321,8 @@ __global__ void __launch_bounds__(64) k_rp_com_sum(int B, int n, int k, const in
   if (t == 0) {
     G1A ca = nl_to_affine(acc);
     store_g1a(com + (size_t)b * 16, ca);
-    store_g1a(Pt + RP_PT_C * 16, ca);  // C is consumed: slot reused by the RLC MSM
+    // C is consumed: the slot now holds -com for the RLC MSM (scalar rho')
+    store_g1a(Pt + RP_PT_C * 16, g1a_neg(ca));
     store_point_be(com_be + (size_t)b * 64, ca);
   }
 }
@@ -520,13 +521,14 @@ __global__ void __launch_bounds__(64) k_rp_check(int B, int n, int k, int32_t* _
 // coef per proof (Montgomery Fr): [rho(ip - polEval), rho tau, rho'(ab - ip)x0, rho' a, rho' b]
 constexpr int RLC_NCOEF = 5;
 
-FTS_DEV Fr fr_from_u128(const uint32_t w[4]) {
-  Fr a = f_zero<FrP>();
-  a.v[0] = w[0];
-  a.v[1] = w[1];
-  a.v[2] = w[2];
-  a.v[3] = w[3];
-  return f_to_mont(a);
+// full-width weight: 256 random bits reduced mod r (Montgomery form).  Full
+// width keeps every MSM window's digits uniform (a 128-bit weight would put
+// all proofs' top-digit entries into a few buckets of one window).
+FTS_DEV Fr fr_from_u256(const uint32_t w[8]) {
+  uint32_t be[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) be[i] = w[7 - i];
+  return f_to_mont(digest_to_fr(be));
 }
 
 __global__ void __launch_bounds__(64) k_rlc_prep(int B, int n, int k, const int32_t* __restrict__ status,
@@ -548,7 +550,7 @@ __global__ void __launch_bounds__(64) k_rlc_prep(int B, int n, int k, const int3
 #pragma unroll
   for (int q = 0; q < 8; q++) kk[q] = key[q];
   chacha20_block(kk, (uint32_t)b, blk);
-  Fr rho = fr_from_u128(blk), rho2 = fr_from_u128(blk + 4);
+  Fr rho = fr_from_u256(blk), rho2 = fr_from_u256(blk + 8);
   const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
   const uint32_t* S = sc + (size_t)b * RP_NSC * 8;
   Fr x, x2, z2, pol;
@@ -566,7 +568,7 @@ __global__ void __launch_bounds__(64) k_rlc_prep(int B, int n, int k, const int3
   if (!e2) return;
   Fr a = fr_from_canon(S + RP_SC_A * 8), bb = fr_from_canon(S + RP_SC_B * 8), x0;
   load_f(C + CH_X0 * 8, x0);
-  put(RP_PT_C, rho2);  // slot C holds com
+  store_f(M + RP_PT_C * 8, f_from_mont(rho2));  // slot C holds -com: scalar +rho' 
   for (int j = 0; j < k; j++) {
     Fr xj, xji;
     load_f(C + (CH_XJ + j) * 8, xj);
@@ -664,7 +666,7 @@ void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32
 }
 
 void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
-                uint32_t* scratch, hipStream_t s);
+                uint32_t* scratch, hipStream_t s, Timeline* tl);
 
 // exact per-proof phase: everything that is hashed (challenges, H'_i, com, x0)
 void launch_rp_exact(const RpBatchDev& d, const uint32_t* tables, const uint8_t* x0_const, hipStream_t s,
@@ -698,8 +700,7 @@ void launch_rp_rlc(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables,
   hipLaunchKernelGGL(k_rlc_columns, dim3(3 + 2 * n), dim3(256), 0, s, B, n, k, d.ch, r.coef, r.colsum);
   FTS_LAUNCH(k_rlc_fixed, 3 + 2 * n, 64, s, n, r.colsum, tables, r.fixed);
   if (tl) tl->mark("k_rlc_scalars", s);
-  launch_msm(r.plan, d.pts, r.msc, r.fixed, 3 + 2 * n, r.msm_scratch, s);
-  if (tl) tl->mark("k_msm", s);
+  launch_msm(r.plan, d.pts, r.msc, r.fixed, 3 + 2 * n, r.msm_scratch, s, tl);
   FTS_LAUNCH(k_rlc_finalize, B > 0 ? B : 1, 64, s, B, r.plan.out, d.status, d.ipa_flag, r.flag);
   if (tl) tl->mark("k_rlc_finalize", s);
 }

@@ -88,6 +88,46 @@ __global__ void __launch_bounds__(256) k_fpmul_fips(const uint32_t* in, uint32_t
   out[tid] = s;
 }
 
+template <int V>
+__device__ __forceinline__ fts::Fp mulv(const fts::Fp& a, const fts::Fp& b) {
+  if constexpr (V == 0) return fts::f_mul(a, b);
+  else if constexpr (V == 1) return fts::f_mul_fips(a, b);
+  else return fts::f_mul_fips2(a, b);
+}
+// dependent chain: latency per product when few waves are resident
+template <int V>
+__global__ void __launch_bounds__(256) k_lat(const uint32_t* in, uint32_t* out, int iters) {
+  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  fts::Fp a, b;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a.v[i] = in[(tid * 8 + i) & 1023];
+    b.v[i] = in[(tid * 8 + i + 5) & 1023];
+  }
+  a.v[7] &= 0x0fffffffu;
+  b.v[7] &= 0x0fffffffu;
+  for (int i = 0; i < iters; i++) a = mulv<V>(a, b);
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) s ^= a.v[i];
+  out[tid] = s;
+}
+template <int V>
+double time_lat(const uint32_t* d_in, uint32_t* d_out, int blocks, int threads, int iters) {
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  k_lat<V><<<blocks, threads>>>(d_in, d_out, 16);
+  hipDeviceSynchronize();
+  hipEventRecord(e0);
+  k_lat<V><<<blocks, threads>>>(d_in, d_out, iters);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms;
+  hipEventElapsedTime(&ms, e0, e1);
+  return ms * 1e-3 / iters;  // seconds per dependent product
+}
+
 int main() {
   hipDeviceProp_t prop;
   CK(hipGetDeviceProperties(&prop, 0));
@@ -148,6 +188,35 @@ int main() {
   CK(hipEventElapsedTime(&ms, e0, e1));
   double fips_rate = 5.0 * n * MUL_ITERS * 2 / (ms * 1e-3);
   printf("{\"fips_fp_mul_per_s\": %.4e, \"fips_mismatch\": %d}\n", fips_rate, mism);
+  // latency regime: 1 wave per SIMD (256 blocks x 256 threads) and 1 wave per 16 SIMDs
+  for (int cfg = 0; cfg < 2; cfg++) {
+    int blocks = cfg == 0 ? cus : cus / 4, threads = cfg == 0 ? 256 : 64;
+    double l0 = time_lat<0>(d_in, (uint32_t*)d_out, blocks, threads, 2000);
+    double l1 = time_lat<1>(d_in, (uint32_t*)d_out, blocks, threads, 2000);
+    double l2 = time_lat<2>(d_in, (uint32_t*)d_out, blocks, threads, 2000);
+    printf("{\"latency_cfg\": \"%dx%d\", \"cios_cycles\": %.0f, \"fips_cycles\": %.0f, \"fips2_cycles\": %.0f}\n",
+           blocks, threads, l0 * 2.4e9, l1 * 2.4e9, l2 * 2.4e9);
+  }
+  // throughput of fips2 (full occupancy, same shape as k_fpmul)
+  {
+    hipEvent_t a0, a1;
+    hipEventCreate(&a0);
+    hipEventCreate(&a1);
+    hipEventRecord(a0);
+    k_lat<2><<<cus * 8, 256>>>(d_in, (uint32_t*)d_out, 512);
+    hipEventRecord(a1);
+    hipEventSynchronize(a1);
+    float m2;
+    hipEventElapsedTime(&m2, a0, a1);
+    hipEventRecord(a0);
+    k_lat<1><<<cus * 8, 256>>>(d_in, (uint32_t*)d_out, 512);
+    hipEventRecord(a1);
+    hipEventSynchronize(a1);
+    float m1;
+    hipEventElapsedTime(&m1, a0, a1);
+    printf("{\"throughput_fips_per_s\": %.4e, \"throughput_fips2_per_s\": %.4e}\n", (double)cus * 8 * 256 * 512 / (m1 * 1e-3),
+           (double)cus * 8 * 256 * 512 / (m2 * 1e-3));
+  }
   printf("{\"device\": \"%s\", \"cus\": %d, \"clock_khz\": %d, \"mad_u64_u32_per_s\": %.4e, "
          "\"u32_ops_per_s\": %.4e, \"fp_mul_per_s\": %.4e, \"fp_mul_mad_equiv_per_s\": %.4e}\n",
          prop.gcnArchName, cus, prop.clockRate, mad_rate, add_rate, fpmul_rate, fpmul_rate * 136.0);

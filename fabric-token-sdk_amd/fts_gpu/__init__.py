@@ -157,9 +157,9 @@ class PublicParams:
         return StagedRangeBatch(self, proofs, commitments)
 
     def last_timings(self):
-        names = (C.c_char_p * 16)()
-        ms = (C.c_float * 16)()
-        m = L.lib.fts_last_timings(self._ctx, names, ms, 16)
+        names = (C.c_char_p * 64)()
+        ms = (C.c_float * 64)()
+        m = L.lib.fts_last_timings(self._ctx, names, ms, 64)
         return {names[i].decode(): ms[i] for i in range(m)}
 
     # ------------------------------------------------------------- prove

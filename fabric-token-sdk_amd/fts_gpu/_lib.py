@@ -32,6 +32,7 @@ EXPORTED = [
     "fts_rp_batch_stage", "fts_rp_batch_verify", "fts_rp_batch_free", "fts_last_timings",
     "fts_status_str", "fts_rp_prove", "fts_rp_prove_batch", "fts_token_commit",
     "fts_transfer_prove", "fts_issue_prove", "fts_debug_rp_intermediates",
+    "fts_debug_msm_stats",
 ]
 
 
@@ -75,6 +76,7 @@ def _load():
                                 C.c_uint64, P, S, C.POINTER(S)], C.c_int),
         "fts_issue_prove": ([P, U8P, S, S, C.POINTER(C.c_uint64), U8P, C.c_uint64, P, S, C.POINTER(S)], C.c_int),
         "fts_debug_rp_intermediates": ([P, S, P, P, P], C.c_int),
+        "fts_debug_msm_stats": ([P, C.POINTER(C.c_int64)], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

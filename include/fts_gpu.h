@@ -130,6 +130,10 @@ int fts_last_timings(const fts_ctx* ctx, const char** names, float* ms, int cap)
  *  com_out: 64-byte com, hp_out: n x 64-byte H'_i); any pointer may be NULL */
 int fts_debug_rp_intermediates(fts_ctx* ctx, size_t i, uint8_t* ch_out, uint8_t* com_out, uint8_t* hp_out);
 
+/* debug: bucket occupancy of the last RLC MSM: out[0] max bucket count, out[1] its index,
+ * out[2] total buckets, out[3] non-empty buckets */
+int fts_debug_msm_stats(fts_ctx* ctx, int64_t* out);
+
 /* ---- error strings ---- */
 const char* fts_status_str(int32_t status);
 

@@ -63,3 +63,9 @@ bad[3] = r3.serialize()
 bad[4] = proofs[4][:-3]
 st = pp.verify_range_proofs(bad, coms)
 print("tampered statuses:", [(int(s), L.status_str(s)) for s in st[:6]], flush=True)
+st = C.c_int64 * 4
+o = st()
+
+pp.verify_range_proofs(proofs, coms)
+L.lib.fts_debug_msm_stats(pp._ctx, o)
+print("msm stats (max count, bucket, NB, nonzero):", list(o), flush=True)
