@@ -30,7 +30,7 @@ MAD_PER_MUL = 136          # 8x32-bit no-carry CIOS / FIPS Montgomery product
 SURVEY_MAD_PER_RP64 = 8.13e6   # SURVEY §8(d) fixed cost model per rp64 verify
 
 
-def kernel_mads(name, B, n, k):
+def kernel_mads(name, B, n, k, nw=18):
     """Algorithmic u32 MADs of one launch of `name`:
     op counts of the algorithm the kernel runs x 136 MAD per Fp/Fr product."""
     fb = 32 * 11                       # fixed-base product: 32 mixed adds (7M+4S)
@@ -38,12 +38,14 @@ def kernel_mads(name, B, n, k):
     inv = 254 + 128                    # Fermat inversion
     per_unit = {
         "k_rp_hprime": n * (fb + 9),
+        "k_rp_com_terms": (n + 2) * (fb + 9) + vb,
+        "k_rp_com_sum": (n + 3) * 16 + 11 + inv + 3,
+        "k_rp_hp_normalize": 8 * n + inv,
+        "k_rp_chal_fr": 2 * n + inv + 3 * (k + 1) + 8,
+        "k_msm_buckets": 16 * nw * 11,
         "k_rp_terms_fixed": (3 + 2 * n) * (fb + 8),
         "k_rp_terms_var": (3 + 2 * k) * vb,
-        "k_rp_com": (n - 1) * (7 + 11) + 2 * vb + 2 * fb + 2 * (inv + 3) + 3 * 16,
-        "k_rp_hp_normalize": 3 * n + inv + 3 * n,
         "k_rp_check": (4 + 2 * n + 2 * k + 1) * 16,
-        "k_rp_challenges": 2 * n + (k + 1) * inv + 8,
     }.get(name)
     if per_unit is None:
         return None
@@ -171,7 +173,7 @@ def main():
             "dtype": "u32 (BN254 Fp/Fr 8x32-bit Montgomery)",
             "data": "synthetic: %d seeded %d-bit range proofs per GPU from the library's host prover" % (B, n),
             "config": {"workload": "C2: batch of %d standalone %d-bit Bulletproof range proofs per GPU "
-                                   "(IPA + RLC-free per-proof equations)" % (B, n),
+                                   "(exact transcripts per proof + RLC batch check via one Pippenger MSM)" % (B, n),
                        "batch_per_gpu": B, "bit_length": n, "rounds": k, "parallelism": "shard%d" % world},
             "accepted": ok,
             "roofline": roofline,
