@@ -30,28 +30,6 @@ MAD_PER_MUL = 136          # 8x32-bit no-carry CIOS / FIPS Montgomery product
 SURVEY_MAD_PER_RP64 = 8.13e6   # SURVEY §8(d) fixed cost model per rp64 verify
 
 
-def kernel_mads(name, B, n, k, nw=18):
-    """Algorithmic u32 MADs of one launch of `name`:
-    op counts of the algorithm the kernel runs x 136 MAD per Fp/Fr product."""
-    fb = 32 * 11                       # fixed-base product: 32 mixed adds (7M+4S)
-    vb = 7 + 6 * 11 + 64 * (4 * 7) + 60 * 16   # var-base: table + 256 dbl + ~60 full adds
-    inv = 254 + 128                    # Fermat inversion
-    per_unit = {
-        "k_rp_hprime": n * (fb + 9),
-        "k_rp_com_terms": (n + 2) * (fb + 9) + vb,
-        "k_rp_com_sum": (n + 3) * 16 + 11 + inv + 3,
-        "k_rp_hp_normalize": 8 * n + inv,
-        "k_rp_chal_fr": 2 * n + inv + 3 * (k + 1) + 8,
-        "k_msm_buckets": 16 * nw * 11,
-        "k_rp_terms_fixed": (3 + 2 * n) * (fb + 8),
-        "k_rp_terms_var": (3 + 2 * k) * vb,
-        "k_rp_check": (4 + 2 * n + 2 * k + 1) * 16,
-    }.get(name)
-    if per_unit is None:
-        return None
-    return B * per_unit * MAD_PER_MUL
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -59,8 +37,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--bits", type=int, default=64)
-    ap.add_argument("--cpu-sample", type=int, default=64, help="proofs verified by the CPU baseline (0: skip)")
+    ap.add_argument("--cpu-sample", type=int, default=256, help="CPU baseline chunk size (0: skip the CPU baseline)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall-time bound of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     args = ap.parse_args()
 
@@ -111,8 +90,9 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        for name, ms in pp.last_timings().items():
-            kt[name] = kt.get(name, 0.0) + ms
+        for name, (ms, mads) in pp.last_timings_ex().items():
+            o = kt.get(name, (0.0, 0.0))
+            kt[name] = (o[0] + ms, mads)
     if dist is not None:
         torch.cuda.synchronize()
         dist.barrier()
@@ -127,10 +107,10 @@ def main():
 
     total = world * B * args.steps
     value = total / elapsed
-    avg = {kname: v / args.steps for kname, v in kt.items()}
+    avg = {kname: v[0] / args.steps for kname, v in kt.items()}
     dom = max(avg, key=avg.get)
     dom_ms = avg[dom]
-    mads = kernel_mads(dom, B, n, k)
+    mads = kt[dom][1]  # algorithmic u32 MADs of one launch (library cost model)
     achieved = mads / (dom_ms * 1e-3) / 1e12 if mads else None
     traffic = None
     try:
@@ -146,17 +126,21 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
+        # bounded sample: chunks of the same proofs until ~cpu_seconds of wall time
         from oracle import cref, pp as oppm
         opp = oppm.load_pp(pp_raw).with_bit_length(n)
-        m = args.cpu_sample
         thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        t0 = time.perf_counter()
-        res = cref.rp_verify_many(opp, coms[:m], proofs[:m], threads=thr)
-        cs = time.perf_counter() - t0
-        assert all(r == 0 for r in res), res
-        cpu = {"value": round(m / cs, 3), "unit": "rp64 verifies/s", "cores": thr, "kind": "port",
+        done, cs, chunk = 0, 0.0, max(thr, args.cpu_sample)
+        while cs < args.cpu_seconds and done < B:
+            m = min(chunk, B - done)
+            t0 = time.perf_counter()
+            res = cref.rp_verify_many(opp, coms[done:done + m], proofs[done:done + m], threads=thr)
+            cs += time.perf_counter() - t0
+            assert all(r == 0 for r in res), res
+            done += m
+        cpu = {"value": round(done / cs, 3), "unit": "rp%d verifies/s" % n, "cores": thr, "kind": "port",
                "sample": "%d of the same rp%d proofs, reference-order C restatement (oracle/c/ref_verify.c, "
-                         "469 affine G1.Mul per proof), %d threads, %.1f s wall" % (m, n, thr, cs)}
+                         "%d affine G1.Mul per proof), %d threads, %.1f s wall" % (done, n, 7 * n + 2 * k + 9, thr, cs)}
 
     if rank == 0:
         out = {

@@ -26,6 +26,8 @@ struct FpP {
                                       0x7879462cu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
   static constexpr uint32_t R2[8] = {0x538afa89u, 0xf32cfc5bu, 0xd44501fbu, 0xb5e71911u,
                                      0x0a417ff6u, 0x47ab1effu, 0xcab8351fu, 0x06d89f71u};
+  static constexpr uint32_t R3[8] = {0xda1530dfu, 0xb1cd6dafu, 0xa7283db6u, 0x62f210e6u,
+                                     0x0ada0afbu, 0xef7f0b0cu, 0x2d592544u, 0x20fd6e90u};
 };
 
 struct FrP {
@@ -36,6 +38,8 @@ struct FrP {
                                       0x7879462eu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
   static constexpr uint32_t R2[8] = {0xae216da7u, 0x1bb8e645u, 0xe35c59e3u, 0x53fe3ab1u,
                                      0x53bb8085u, 0x8c49833du, 0x7f4e44a5u, 0x0216d0b1u};
+  static constexpr uint32_t R3[8] = {0xb4bf0040u, 0x5e94d8e1u, 0x1cfbb6b8u, 0x2a489cbeu,
+                                     0xa19fcfedu, 0x893cc664u, 0x7fcc657cu, 0x0cf8594bu};
 };
 
 template <class P>
@@ -302,6 +306,96 @@ FTS_DEV Field<P> f_inv(const Field<P>& a) {
 #pragma unroll
   for (int i = 1; i < 8; i++) e[i] = subb(P::M[i], 0u, bw, bw);
   return f_pow(a, e);
+}
+
+// Inverse by the binary extended Euclidean algorithm (variable time: every
+// value inverted on the verification path is public).  Invariants
+// x1 * A == u, x2 * A == v (mod M) for the Montgomery representative A = aR;
+// each step halves u or v, so at most ~2*254 steps.  The result A^-1 is
+// mapped back to Montgomery form with one product by R^3:
+// mont(A^-1, R^3) = a^-1 R.  inv(0) = 0 (as Fermat gives).
+// Latency: ~500 steps of 8-limb add/shift (full-rate VALU) instead of the
+// ~380 dependent 136-MAD products of a^(M-2).
+template <class P>
+FTS_DEV void limbs_half_mod(uint32_t x[8]) {  // x <- x/2 mod M  (x < M)
+  const uint32_t mask = 0u - (x[0] & 1u);
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x[i] = addc(x[i], P::M[i] & mask, c, c);
+  // x + M < 2^255: no carry out
+#pragma unroll
+  for (int i = 0; i < 7; i++) x[i] = (x[i] >> 1) | (x[i + 1] << 31);
+  x[7] >>= 1;
+}
+template <class P>
+FTS_DEV void limbs_sub_mod(uint32_t x[8], const uint32_t y[8]) {  // x <- x - y mod M
+  uint32_t bw = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x[i] = subb(x[i], y[i], bw, bw);
+  const uint32_t mask = 0u - bw;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x[i] = addc(x[i], P::M[i] & mask, c, c);
+}
+FTS_DEV bool limbs_is_one(const uint32_t u[8]) {
+  uint32_t o = u[0] ^ 1u;
+#pragma unroll
+  for (int i = 1; i < 8; i++) o |= u[i];
+  return o == 0;
+}
+template <class P>
+FTS_DEV Field<P> f_inv_bin(const Field<P>& a) {
+  if (f_is_zero(a)) return a;
+  uint32_t u[8], v[8], x1[8], x2[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    u[i] = a.v[i];
+    v[i] = P::M[i];
+    x1[i] = 0;
+    x2[i] = 0;
+  }
+  x1[0] = 1;
+  while (!limbs_is_one(u) && !limbs_is_one(v)) {
+    if ((u[0] & 1u) == 0) {
+#pragma unroll
+      for (int i = 0; i < 7; i++) u[i] = (u[i] >> 1) | (u[i + 1] << 31);
+      u[7] >>= 1;
+      limbs_half_mod<P>(x1);
+    } else if ((v[0] & 1u) == 0) {
+#pragma unroll
+      for (int i = 0; i < 7; i++) v[i] = (v[i] >> 1) | (v[i + 1] << 31);
+      v[7] >>= 1;
+      limbs_half_mod<P>(x2);
+    } else {
+      uint32_t t[8], bw = 0;
+#pragma unroll
+      for (int i = 0; i < 8; i++) t[i] = subb(u[i], v[i], bw, bw);
+      if (!bw) {  // u >= v: u <- (u - v)/2, x1 <- (x1 - x2)/2
+#pragma unroll
+        for (int i = 0; i < 7; i++) u[i] = (t[i] >> 1) | (t[i + 1] << 31);
+        u[7] = t[7] >> 1;
+        limbs_sub_mod<P>(x1, x2);
+        limbs_half_mod<P>(x1);
+      } else {  // v <- (v - u)/2, x2 <- (x2 - x1)/2
+        uint32_t b2 = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) t[i] = subb(v[i], u[i], b2, b2);
+#pragma unroll
+        for (int i = 0; i < 7; i++) v[i] = (t[i] >> 1) | (t[i + 1] << 31);
+        v[7] = t[7] >> 1;
+        limbs_sub_mod<P>(x2, x1);
+        limbs_half_mod<P>(x2);
+      }
+    }
+  }
+  Field<P> r, r3;
+  const bool one_u = limbs_is_one(u);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    r.v[i] = one_u ? x1[i] : x2[i];
+    r3.v[i] = P::R3[i];
+  }
+  return f_mul(r, r3);
 }
 
 // canonical (non-Montgomery) limbs < M ?

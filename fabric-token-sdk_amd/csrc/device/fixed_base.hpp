@@ -1,0 +1,109 @@
+// Fixed-base scalar multiplication over device-resident window tables.
+//
+// Every public generator the verifier multiplies (H_i, G_i, ped0..2, P, Q,
+// K = sum H_i - sum G_i) gets a table
+//     T[w][d-1] = d * 2^(FB_W * w) * B,   d = 1 .. 2^(FB_W-1),  w < FB_NW
+// of affine Montgomery points (16 words).  A canonical scalar k < r < 2^254
+// is recoded into FB_NW signed FB_W-bit digits, so k*B costs FB_NW mixed
+// additions and no doublings.  With FB_W = 16 that is 16 additions per
+// product (32 with byte windows) for 32 MiB of table per base: the
+// 134 bases of a 64-bit context take 4.3 GiB of HBM, which the 288 GB part
+// affords; every lookup is one 64-byte gather.
+//
+// The multiplication loop is fully inlined (no out-of-line calls: the call
+// ABI would spill the accumulator to scratch on every addition) and
+// prefetches the next table entry while the current addition runs.
+#pragma once
+#include "g1.hpp"
+
+namespace fts {
+
+constexpr int FB_W = 16;                                   // window bits
+constexpr int FB_NW = (255 + FB_W - 1) / FB_W;             // windows (covers 255 bits)
+constexpr int FB_E = 1 << (FB_W - 1);                      // entries per window
+constexpr size_t FB_WORDS_PER_BASE = (size_t)FB_NW * FB_E * 16;
+// two-level construction of a window: d - 1 = hi * FB_S + lo
+constexpr int FB_S = 1 << ((FB_W) / 2);                    // small multiples per window
+constexpr int FB_L = FB_E / FB_S;                          // large multiples per window
+
+// next signed digit of k (LSB first): consumes FB_W bits of s (shifted in
+// place: constant register indices, no scratch), carry in/out via `carry`
+FTS_DEV int fb_next_digit(uint32_t s[8], int& carry) {
+  int d = (int)(s[0] & (uint32_t)(2 * FB_E - 1)) + carry;
+#pragma unroll
+  for (int i = 0; i < 7; i++) s[i] = (s[i] >> FB_W) | (s[i + 1] << (32 - FB_W));
+  s[7] >>= FB_W;
+  carry = d > FB_E;
+  return carry ? d - 2 * FB_E : d;
+}
+
+// p += q (q affine, not the identity): madd-2007-bl, inlined
+FTS_DEV void madd_inl(G1J& p, const G1A& q) {
+  if (f_is_zero(p.z)) {
+    p.x = q.x;
+    p.y = q.y;
+    p.z = f_one<FpP>();
+    return;
+  }
+  Fp z1z1 = fp_sqr(p.z);
+  Fp u2 = fp_mul(q.x, z1z1);
+  Fp s2 = fp_mul(fp_mul(q.y, p.z), z1z1);
+  Fp h = f_sub(u2, p.x);
+  Fp rr = f_sub(s2, p.y);
+  if (f_is_zero(h)) {  // P == +-Q: exceptional, out of line
+    p = f_is_zero(rr) ? g1j_dbl(p) : g1j_identity();
+    return;
+  }
+  Fp hh = fp_sqr(h);
+  Fp i = f_dbl(f_dbl(hh));
+  Fp j = fp_mul(h, i);
+  rr = f_dbl(rr);
+  Fp v = fp_mul(p.x, i);
+  Fp x3 = f_sub(f_sub(fp_sqr(rr), j), f_dbl(v));
+  Fp y3 = f_sub(fp_mul(rr, f_sub(v, x3)), f_dbl(fp_mul(p.y, j)));
+  p.z = f_sub(f_sub(fp_sqr(f_add(p.z, h)), z1z1), hh);
+  p.x = x3;
+  p.y = y3;
+}
+
+FTS_DEV G1A fb_entry(const uint32_t* __restrict__ table, int w, int d) {
+  const int ad = d < 0 ? -d : d;
+  G1A q = load_g1a(table + ((size_t)w * FB_E + (ad - 1)) * 16);
+  if (d < 0) q.y = f_neg(q.y);
+  return q;
+}
+
+// k * B for a canonical scalar k (8 LE limbs)
+FTS_DEV G1J fb_mul(const uint32_t* __restrict__ table, const Scalar& k) {
+  uint32_t s[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = k.v[i];
+  G1J acc = g1j_identity();
+  int carry = 0, w = 0, d = 0;
+  // first nonzero digit
+  for (; w < FB_NW; w++) {
+    d = fb_next_digit(s, carry);
+    if (d != 0) break;
+  }
+  if (w == FB_NW) return acc;
+  G1A cur = fb_entry(table, w, d);
+  for (;;) {
+    int wn = w + 1, dn = 0;
+    for (; wn < FB_NW; wn++) {
+      dn = fb_next_digit(s, carry);
+      if (dn != 0) break;
+    }
+    G1A nxt;
+    if (wn < FB_NW) nxt = fb_entry(table, wn, dn);  // in flight during the addition
+    madd_inl(acc, cur);
+    if (wn >= FB_NW) break;
+    cur = nxt;
+    w = wn;
+  }
+  return acc;
+}
+
+// out-of-line copy for cold call sites (keeps their kernels small)
+__device__ __noinline__ G1J nl_fb_mul(const uint32_t* __restrict__ table, Scalar k) { return fb_mul(table, k); }
+
+}  // namespace fts

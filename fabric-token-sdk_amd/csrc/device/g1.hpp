@@ -131,8 +131,8 @@ FTS_DEV G1J g1j_add(const G1J& p, const G1J& q) {
   return r;
 }
 
-__device__ __noinline__ Fp nl_fp_inv(Fp a) { return f_inv(a); }
-__device__ __noinline__ Fr nl_fr_inv(Fr a) { return f_inv(a); }
+__device__ __noinline__ Fp nl_fp_inv(Fp a) { return f_inv_bin(a); }
+__device__ __noinline__ Fr nl_fr_inv(Fr a) { return f_inv_bin(a); }
 
 // equality of two Jacobian points (as group elements)
 FTS_DEV bool g1j_eq(const G1J& p, const G1J& q) {
@@ -230,33 +230,6 @@ __device__ __noinline__ G1J nl_add_mem(G1J p, const uint32_t* q_ptr, uint32_t ne
 __device__ __noinline__ G1A nl_to_affine(G1J p) { return g1j_to_affine(p); }
 
 // --------------------------------------------------- scalar multiplication
-// Fixed-base: table[w][d-1] = d * 2^(8w) * B, d in 1..128, affine (16 words),
-// 32 windows.  Signed 8-bit digits of a canonical scalar k < r < 2^254.
-constexpr int FB_WINDOWS = 32;
-constexpr int FB_ENTRIES = 128;
-constexpr int FB_WORDS_PER_BASE = FB_WINDOWS * FB_ENTRIES * 16;
-
-__device__ __noinline__ G1J fixed_base_mul(const uint32_t* __restrict__ table, Scalar k) {
-  uint32_t s[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) s[i] = k.v[i];
-  G1J acc = g1j_identity();
-  int carry = 0;
-  for (int w = 0; w < FB_WINDOWS; w++) {
-    int d = (int)(s[0] & 0xffu) + carry;
-#pragma unroll
-    for (int i = 0; i < 7; i++) s[i] = (s[i] >> 8) | (s[i + 1] << 24);
-    s[7] >>= 8;
-    carry = d > 128;
-    d = carry ? d - 256 : d;
-    if (d != 0) {
-      int ad = d < 0 ? -d : d;
-      acc = nl_madd_mem(acc, table + ((size_t)(w * FB_ENTRIES + (ad - 1)) * 16), d < 0);
-    }
-  }
-  return acc;
-}
-
 // Variable-base: signed 4-bit windows, per-lane table of 1..8 * P kept in
 // `scratch` (8 x 24 words, lane-private global memory; L1/L2 resident).
 __device__ __noinline__ G1J var_base_mul(G1A p, Scalar k, uint32_t* __restrict__ scratch) {

@@ -1,0 +1,228 @@
+// GLV endomorphism of BN254 G1 (y^2 = x^3 + 3, j-invariant 0):
+//   phi(x, y) = (beta x, y) = lambda * (x, y),   beta^3 = 1 in Fp, lambda^3 = 1 in Fr.
+// A scalar k < r splits as k = k1 + k2 * lambda (mod r) with |k1|, |k2| < 2^126
+// (lattice basis v1 = (a1, b1), v2 = (a2, b2) of {(x, y): x + y lambda = 0 mod r},
+// Babai rounding with precomputed g_i = floor(2^384 * b_i / r); the rounding
+// error only changes which short vector is found, never k1 + k2 lambda).
+// This halves the doubling chain of every variable-base product: the
+// per-proof x*D, the sigma proofs' challenge products and the RLC MSM's
+// Horner (254 -> 127 doublings).  gnark-crypto uses the same endomorphism
+// (ecc/bn254 G1 ScalarMultiplication); the values here are derived from the
+// curve (tools/glv_constants.py), not copied.
+#pragma once
+#include "g1.hpp"
+
+namespace fts {
+
+struct Glv {
+  // beta in Montgomery form (Fp), paired with lambda = 0xb3c4d79d...c90dd
+  static constexpr uint32_t BETA[8] = {0xd782e155u, 0x71930c11u, 0xffbe3323u, 0xa6bb947cu,
+                                       0xd4741444u, 0xaa303344u, 0x26594943u, 0x2c3b3f0du};
+  static constexpr uint32_t G1[7] = {0x2fafba64u, 0x8fa7d32du, 0x773a6ef2u, 0x6eb9c714u,
+                                     0xc7e0b3d7u, 0xd91d232eu, 0x00000002u};
+  static constexpr uint32_t G2[9] = {0x9b9bdffau, 0x86937516u, 0x5eaa26d9u, 0xa5e38cfbu, 0x391eb18du,
+                                     0x7a7bd9d4u, 0xa773d2cfu, 0x4ccef014u, 0x00000002u};
+  static constexpr uint32_t A1[2] = {0x94d213e3u, 0x89d32568u};                          // a1 (= b2)
+  static constexpr uint32_t A2[4] = {0x1221250bu, 0x0be4e154u, 0xeeb859fdu, 0x6f4d8248u};  // a2
+  static constexpr uint32_t NB1[4] = {0x7d4f1128u, 0x8211bbebu, 0xeeb859fcu, 0x6f4d8248u}; // -b1
+};
+
+// c = round(k * g / 2^384) for a G-limb constant g; returns the low 5 limbs
+template <int G>
+FTS_DEV void glv_round(const uint32_t k[8], const uint32_t (&g)[G], uint32_t c[5]) {
+  // full product limbs 11 .. 8+G-1 are needed (limb 11 for the rounding bit)
+  uint32_t t[8 + G];
+#pragma unroll
+  for (int i = 0; i < 8 + G; i++) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < G; j++) {
+      uint64_t v = (uint64_t)k[i] * g[j] + t[i + j] + carry;
+      t[i + j] = (uint32_t)v;
+      carry = v >> 32;
+    }
+    t[i + G] = (uint32_t)carry;
+  }
+  // + 2^383 (rounding), then >> 384 (limb 12)
+  uint32_t cy = (t[11] >> 31);
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    uint32_t v = (12 + i) < 8 + G ? t[12 + i] : 0u;
+    c[i] = addc(v, 0u, cy, cy);
+  }
+}
+
+// r -= a * b (mod 2^256), a: NA limbs, b: NB limbs
+template <int NA, int NB>
+FTS_DEV void sub_mul_256(uint32_t r[8], const uint32_t* a, const uint32_t* b) {
+  uint32_t p[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) p[i] = 0;
+#pragma unroll
+  for (int i = 0; i < NA; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+      if (i + j < 8) {
+        uint64_t v = (uint64_t)a[i] * b[j] + p[i + j] + carry;
+        p[i + j] = (uint32_t)v;
+        carry = v >> 32;
+      }
+    }
+    if (i + NB < 8) p[i + NB] = (uint32_t)carry;
+  }
+  uint32_t bw = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r[i] = subb(r[i], p[i], bw, bw);
+}
+
+// two's-complement 256-bit -> (|v| low 4 limbs, sign)
+FTS_DEV uint32_t glv_abs(const uint32_t v[8], uint32_t out[4]) {
+  const uint32_t neg = v[7] >> 31;
+  uint32_t c = neg;
+#pragma unroll
+  for (int i = 0; i < 4; i++) out[i] = addc(neg ? ~v[i] : v[i], 0u, c, c);
+  return neg;
+}
+
+// k (canonical, 8 limbs) -> k1, k2 (|.| in 4 limbs) with signs: k = k1 + k2 lambda mod r
+FTS_DEV void glv_decompose(const uint32_t k[8], uint32_t k1[4], uint32_t& s1, uint32_t k2[4], uint32_t& s2) {
+  uint32_t c1[5], c2[5];
+  glv_round<7>(k, Glv::G1, c1);
+  glv_round<9>(k, Glv::G2, c2);
+  uint32_t r1[8], r2[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    r1[i] = k[i];
+    r2[i] = 0;
+  }
+  // k1 = k - c1 a1 - c2 a2
+  sub_mul_256<3, 2>(r1, c1, Glv::A1);
+  sub_mul_256<5, 4>(r1, c2, Glv::A2);
+  // k2 = c1 (-b1) - c2 b2 = -( c2 b2 - c1 (-b1) )   (b2 = a1)
+  sub_mul_256<5, 2>(r2, c2, Glv::A1);  // r2 = -c2 b2
+  {
+    uint32_t p[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) p[i] = 0;
+    sub_mul_256<3, 4>(p, c1, Glv::NB1);  // p = -c1 (-b1)
+    uint32_t bw = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r2[i] = subb(r2[i], p[i], bw, bw);  // r2 = -c2 b2 + c1 (-b1)
+  }
+  s1 = glv_abs(r1, k1);
+  s2 = glv_abs(r2, k2);
+}
+
+FTS_DEV Fp glv_beta() {
+  Fp b;
+#pragma unroll
+  for (int i = 0; i < 8; i++) b.v[i] = Glv::BETA[i];
+  return b;
+}
+
+// p += q (both Jacobian): add-2007-bl, inlined (exceptional cases inline too,
+// so the caller's loop never makes an out-of-line call)
+FTS_DEV void add_inl(G1J& p, const G1J& q) {
+  if (f_is_zero(q.z)) return;
+  if (f_is_zero(p.z)) {
+    p = q;
+    return;
+  }
+  Fp z1z1 = fp_sqr(p.z);
+  Fp z2z2 = fp_sqr(q.z);
+  Fp u1 = fp_mul(p.x, z2z2);
+  Fp u2 = fp_mul(q.x, z1z1);
+  Fp s1 = fp_mul(fp_mul(p.y, q.z), z2z2);
+  Fp s2 = fp_mul(fp_mul(q.y, p.z), z1z1);
+  Fp h = f_sub(u2, u1);
+  Fp rr = f_sub(s2, s1);
+  if (f_is_zero(h)) {
+    p = f_is_zero(rr) ? g1j_dbl(p) : g1j_identity();
+    return;
+  }
+  Fp i = fp_sqr(f_dbl(h));
+  Fp j = fp_mul(h, i);
+  rr = f_dbl(rr);
+  Fp v = fp_mul(u1, i);
+  Fp x3 = f_sub(f_sub(fp_sqr(rr), j), f_dbl(v));
+  Fp y3 = f_sub(fp_mul(rr, f_sub(v, x3)), f_dbl(fp_mul(s1, j)));
+  p.z = fp_mul(f_sub(f_sub(fp_sqr(f_add(p.z, q.z)), z1z1), z2z2), h);
+  p.x = x3;
+  p.y = y3;
+}
+
+// LDS-resident per-lane table of 1..8 * P: [entry][word][64 lanes] (one bank
+// column per lane, conflict-free).  `tab` points at this wave's 8*24*64 words.
+FTS_DEV void vtab_store(uint32_t* tab, int lane, int e, const G1J& p) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    tab[((e * 24) + i) * 64 + lane] = p.x.v[i];
+    tab[((e * 24) + 8 + i) * 64 + lane] = p.y.v[i];
+    tab[((e * 24) + 16 + i) * 64 + lane] = p.z.v[i];
+  }
+}
+FTS_DEV G1J vtab_load(const uint32_t* tab, int lane, int e) {
+  G1J p;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    p.x.v[i] = tab[((e * 24) + i) * 64 + lane];
+    p.y.v[i] = tab[((e * 24) + 8 + i) * 64 + lane];
+    p.z.v[i] = tab[((e * 24) + 16 + i) * 64 + lane];
+  }
+  return p;
+}
+
+// k * P for a 128-bit magnitude k (4 LE limbs, < 2^127): signed 4-bit
+// windows (32 windows), 1 + 6 table additions, 128 doublings, <= 32 additions.
+FTS_DEV G1J vb128(const G1A& p, const uint32_t kk[4], uint32_t* tab, int lane) {
+  if (g1a_is_identity(p)) return g1j_identity();
+  {
+    G1J t = g1j_from_affine(p);
+    vtab_store(tab, lane, 0, t);
+    G1J cur = g1j_dbl(t);
+    vtab_store(tab, lane, 1, cur);
+    for (int e = 2; e < 8; e++) {
+      add_inl(cur, t);
+      vtab_store(tab, lane, e, cur);
+    }
+  }
+  uint32_t s[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) s[i] = kk[i];
+  // carries of the signed recoding (LSB first), one bit per window
+  uint32_t cm = 0;
+  {
+    int carry = 0;
+#pragma unroll
+    for (int w = 0; w < 32; w++) {
+      cm |= (uint32_t)carry << w;
+      int d = (int)((s[w >> 3] >> (4 * (w & 7))) & 0xfu) + carry;
+      carry = d > 8;
+    }
+  }
+  G1J acc = g1j_identity();
+  for (int w = 31; w >= 0; w--) {
+    if (w != 31)
+      for (int q = 0; q < 4; q++) acc = g1j_dbl(acc);
+    // window w raw nibble (s shifted left by 4 each step: MSB nibble of s[3])
+    int raw = (int)(s[3] >> 28);
+    s[3] = (s[3] << 4) | (s[2] >> 28);
+    s[2] = (s[2] << 4) | (s[1] >> 28);
+    s[1] = (s[1] << 4) | (s[0] >> 28);
+    s[0] <<= 4;
+    int cin = (int)((cm >> w) & 1u);
+    int cout = w < 31 ? (int)((cm >> (w + 1)) & 1u) : 0;
+    int d = raw + cin - 16 * cout;
+    if (d != 0) {
+      G1J q = vtab_load(tab, lane, (d < 0 ? -d : d) - 1);
+      if (d < 0) q.y = f_neg(q.y);
+      add_inl(acc, q);
+    }
+  }
+  return acc;
+}
+
+}  // namespace fts

@@ -2,19 +2,27 @@
 //
 // sum_i k_i * P_i over N affine points (Montgomery, 16 words each, identity =
 // (0,0)) and canonical scalars (8 LE words each, < r < 2^254).
+// GLV (device/glv.hpp): every scalar is split as k = k1 + k2 lambda with
+// |k1|, |k2| < 2^126, so the MSM runs over NV = 2N virtual points
+// (P_i with k1, phi(P_i) with k2; signs folded into the digit signs) with
+// 127-bit scalars: half the windows and half the final doubling chain.
 // Signed windows: window w covers bits [off_w, off_w + width_w); digit d in
-// [-2^(width-1), 2^(width-1)] and bucket |d|-1 collects +-P_i.  Widths are c
-// except the top window, which is widened (merged) when the leftover bits
-// would leave it with a handful of huge buckets: every window then has
-// ~N / 2^(c-1) points per bucket for uniform scalars.
-// Kernels (msm.hip):
-//   k_msm_digits   (point)            recode + bucket histogram (atomics)
-//   k_msm_scan     (window)           exclusive prefix sum of bucket counts
-//   k_msm_scatter  (point)            counting-sort scatter of (index|sign)
-//   k_msm_buckets  (bucket)           bucket sums, mixed additions from HBM
-//   k_msm_segments (segment)          running-sum reduction of SEG buckets
-//   k_msm_windows  (window)           LDS tree over the window's segments
-//   k_msm_final    (1 thread)         Horner over windows (+ extra points)
+// [-2^(width-1), 2^(width-1)] and bucket |d|-1 collects +-P.  The 127
+// covered bits are split into nw windows of width c or c-1 (balanced), so
+// every window has ~NV / 2^(c-1) points per bucket.
+// Bucket accumulation is chunked (<= MSM_CH points per lane) so a bucket that
+// attracts many points (adversarial or low-entropy scalars) is summed by
+// several lanes instead of one long dependent chain.
+// Kernels (msm.hip), all on one stream:
+//   k_msm_digits      (point)          recode + bucket histogram (atomics)
+//   k_msm_scan        (window)         prefix sums: bucket offsets + chunk map
+//   k_msm_scatter     (point)          counting-sort scatter of (index|sign)
+//   k_msm_chunks      (chunk)          <= MSM_CH mixed additions from HBM
+//   k_msm_bucket_sum  (bucket)         sum of the bucket's chunk partials
+//   k_msm_segments    (segment)        running-sum reduction of MSM_SEG buckets
+//   k_msm_windows     (window + 1)     LDS tree over the window's segments;
+//                                      block nw sums the extra (fixed) points
+//   k_msm_final       (1 lane)         Horner over the windows + extras
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -22,67 +30,75 @@
 namespace fts {
 
 constexpr int MSM_MAX_WINDOWS = 64;
-constexpr int MSM_SEG = 16;  // buckets per running-sum segment
+constexpr int MSM_SEG = 8;   // buckets per running-sum segment
+constexpr int MSM_CH = 8;    // points per bucket-accumulation chunk
 
 struct MsmWindow {
   int32_t width;   // bits
   int32_t off;     // first bit
   int32_t bbase;   // first bucket (global index)
   int32_t sbase;   // first segment (global index)
+  int32_t cbase;   // first chunk slot (global index); NV/MSM_CH + nb slots reserved
+  int32_t pad[3];
 };
 
+constexpr int MSM_BITS = 127;  // magnitude < 2^126 + sign-recoding carry
+
 struct MsmPlan {
-  int N;
+  int N;           // real points
+  int NV;          // virtual points (2N)
   int nw;
   int NB;          // total buckets
   int NS;          // total segments
+  int NC;          // total chunk slots
   MsmWindow win[MSM_MAX_WINDOWS];  // host copy
   MsmWindow* d_win;                // device copy
-  int32_t* keys;     // [nw][N] bucket (global) index | sign<<31, or -1
-  uint32_t* counts;  // [NB]
-  uint32_t* offsets; // [NB] (within the window's sorted range)
-  uint32_t* cursor;  // [NB]
-  uint32_t* sorted;  // [nw][N] index | sign << 31
-  uint32_t* buckets; // [NB][24] Jacobian
-  uint32_t* segs;    // [NS][24]
-  uint32_t* wins;    // [nw][24]
-  uint32_t* out;     // [24] result (Jacobian)
+  int32_t* keys;      // [nw][NV] bucket (global) index | sign<<31, or -1
+  uint32_t* counts;   // [NB]
+  uint32_t* offsets;  // [NB] (within the window's sorted range)
+  uint32_t* cursor;   // [NB]
+  uint32_t* chunk_off;// [NB] first chunk slot of the bucket (global)
+  int32_t* chunk_bkt; // [NC] bucket of a chunk slot, -1 if unused
+  uint32_t* sorted;   // [nw][NV] virtual index | sign << 31
+  uint32_t* partials; // [NC][24] Jacobian
+  uint32_t* buckets;  // [NB][24] Jacobian
+  uint32_t* segs;     // [NS][24]
+  uint32_t* wins;     // [nw + 1][24] (slot nw: sum of the extra points)
+  uint32_t* out;      // [24] result (Jacobian)
 };
 
-// window layout for N points: base width c ~ log2(N) - 3; leftover top bits
-// are merged into the previous window when <= 3, widths whose leftover
-// would be unbalanced are skipped
+// Field-product count of the bucket phase for window width c (host cost model)
+inline double msm_cost(int N, int c) {
+  int nw = (MSM_BITS + c - 1) / c;
+  return (double)nw * ((double)N * 11.0 + (double)(1 << c) * 16.0);
+}
+
 inline void msm_layout(int N, MsmPlan& p) {
-  int c = 4;
-  while ((1 << (c + 3)) < N && c < 17) c++;
-  for (;; c++) {
-    int nw = (255 + c - 1) / c;
-    int t = 255 - c * (nw - 1);
-    if (t <= 3 || t >= c - 1 || c >= 17) break;
-  }
-  int nw = (255 + c - 1) / c;
-  int t = 255 - c * (nw - 1);
-  int widths[MSM_MAX_WINDOWS];
-  for (int w = 0; w < nw; w++) widths[w] = c;
-  if (t <= 3 && nw > 1) {
-    nw -= 1;
-    widths[nw - 1] = c + t;
-  } else {
-    widths[nw - 1] = t;
-  }
+  const int NV = 2 * N;
+  int best = 4;
+  for (int c = 5; c <= 16; c++)
+    if (msm_cost(NV, c) < msm_cost(NV, best)) best = c;
+  const int c = best;
+  const int nw = (MSM_BITS + c - 1) / c;
+  // balanced widths: (MSM_BITS mod nw) windows of ceil, the rest floor
+  const int lo = MSM_BITS / nw, extra = MSM_BITS - lo * nw;
   p.nw = nw;
-  int off = 0, bb = 0, sb = 0;
+  int off = 0, bb = 0, sb = 0, cb = 0;
   for (int w = 0; w < nw; w++) {
-    int nb = 1 << (widths[w] - 1);
-    int ns = (nb + MSM_SEG - 1) / MSM_SEG;
-    p.win[w] = MsmWindow{widths[w], off, bb, sb};
-    off += widths[w];
+    const int width = lo + (w < extra ? 1 : 0);
+    const int nb = 1 << (width - 1);
+    const int ns = (nb + MSM_SEG - 1) / MSM_SEG;
+    p.win[w] = MsmWindow{width, off, bb, sb, cb, {0, 0, 0}};
+    off += width;
     bb += nb;
     sb += ns;
+    cb += NV / MSM_CH + nb;
   }
   p.NB = bb;
   p.NS = sb;
+  p.NC = cb;
   p.N = N;
+  p.NV = NV;
 }
 
 }  // namespace fts

@@ -38,13 +38,34 @@ inline __host__ __device__ uint32_t x0_slot_bytes(int n) { return ((x0_msg_len(n
 // small transcripts slot (x: 258 B, y: 388 B, x_j: 258 B, z: 32 B) -> 512 B scratch each
 constexpr uint32_t SMALL_SLOT = 512;
 
-// per-kernel device timeline: events recorded on the launch stream after
-// each kernel; time of mark i = elapsed(mark i-1, mark i)
+// Algorithmic cost model, in Fp/Fr Montgomery products; one
+// product = 136 u32 MADs (8x32-bit FIPS/CIOS).  Every kernel launch is marked
+// with the products its algorithm needs, so bench.py can report
+// achieved MAD/s = products * 136 / measured kernel time.
+constexpr double MADS_PER_MUL = 136.0;
+constexpr double COST_MADD = 11.0;    // madd-2007-bl 7M + 4S
+constexpr double COST_ADD = 16.0;     // add-2007-bl 11M + 5S
+constexpr double COST_DBL = 7.0;      // dbl-2009-l 2M + 5S
+constexpr double COST_FB = 16.0 * COST_MADD;   // fixed-base, 16 signed 16-bit windows (fixed_base.hpp)
+constexpr double COST_VB4 = 7.0 + 6.0 * COST_MADD + 256.0 * COST_DBL + 60.0 * COST_ADD;  // 4-bit var-base
+constexpr double COST_VB128 = 7.0 + 6.0 * COST_ADD + 124.0 * COST_DBL + 30.0 * COST_ADD;  // GLV half (glv.hpp)
+constexpr double COST_NORM = 7.0;     // batched affine normalisation, per point
+
+// Per-kernel device timeline: an event is recorded on the launching stream
+// after each kernel; the time of mark i is elapsed(previous event on the same
+// stream, mark i).  fork()/join() record the cross-stream dependencies (their
+// events start the next kernel's interval on the waiting stream).
 struct Timeline {
-  static constexpr int CAP = 40;
+  static constexpr int CAP = 48;
+  static constexpr int MAXS = 4;
   hipEvent_t ev[CAP + 1];
   const char* name[CAP];
+  double work[CAP];
+  int start[CAP];
   int n = 0;
+  hipStream_t sl[MAXS];
+  int last[MAXS];
+  int ns = 0;
   bool created = false;
   void create() {
     if (created) return;
@@ -56,15 +77,41 @@ struct Timeline {
     for (int i = 0; i <= CAP; i++) (void)hipEventDestroy(ev[i]);
     created = false;
   }
+  int& last_of(hipStream_t s) {
+    for (int i = 0; i < ns; i++)
+      if (sl[i] == s) return last[i];
+    sl[ns] = s;
+    last[ns] = 0;
+    return last[ns++];
+  }
   void begin(hipStream_t s) {
     n = 0;
+    ns = 0;
     (void)hipEventRecord(ev[0], s);
+    last_of(s) = 0;
   }
-  void mark(const char* nm, hipStream_t s) {
+  void mark(const char* nm, hipStream_t s, double w) {
     if (n >= CAP) return;
+    int& l = last_of(s);
     name[n] = nm;
+    work[n] = w;
+    start[n] = l;
     (void)hipEventRecord(ev[n + 1], s);
-    n++;
+    l = ++n;
+  }
+  // `to` waits for everything issued so far on `from`
+  void fork(hipStream_t from, hipStream_t to) {
+    if (n >= CAP) {
+      hipEvent_t e;
+      (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+      (void)hipEventRecord(e, from);
+      (void)hipStreamWaitEvent(to, e, 0);
+      (void)hipEventDestroy(e);
+      return;
+    }
+    mark(nullptr, from, 0);
+    (void)hipStreamWaitEvent(to, ev[n], 0);
+    mark(nullptr, to, 0);  // completes once `to` has also drained its own work
   }
 };
 
@@ -78,11 +125,9 @@ struct RpBatchDev {
   uint32_t* pts;       // [B][5+2k][16] affine Montgomery
   uint32_t* ch;        // [B][8+2k][8] challenges (Montgomery Fr)
   uint8_t* small_msgs; // [B][2+k][SMALL_SLOT]
-  uint32_t* hpj;       // [B][n][24]
-  uint32_t* hpa;       // [B][n][16]
-  uint8_t* hp_be;      // [B][n][64]
-  uint32_t* com;       // [B][16]
-  uint8_t* com_be;     // [B][64]
+  uint32_t* hpj;       // [B][n+1][24] Jacobian H'_0..H'_{n-1}, com
+  uint32_t* hpa;       // [B][n+1][16] affine Montgomery
+  uint8_t* hp_be;      // [B][n+1][64] canonical big-endian encodings
   uint8_t* x0_msgs;    // [B][x0_slot_bytes(n)]
   uint32_t* terms;     // [B][6+2n+2k][24]
   uint32_t* scratch;   // var-base lane tables

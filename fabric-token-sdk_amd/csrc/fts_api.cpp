@@ -32,13 +32,13 @@ namespace fts {
 size_t rp_scratch_words(int B, int n, int k);
 size_t rp_terms_words(int B, int n, int k);
 void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s);
-void launch_rp_exact(const RpBatchDev& d, const uint32_t* tables, const uint8_t* x0_const, hipStream_t s,
-                     Timeline* tl);
-void launch_rp_rlc(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, hipStream_t s, Timeline* tl);
+void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const uint8_t* x0_const,
+                     hipStream_t s, hipStream_t s2, Timeline* tl);
 void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, hipStream_t s, Timeline* tl);
 void launch_sig_prep(const SigBatchDev& d, hipStream_t s);
 void launch_sig_finish(const SigBatchDev& d, const uint32_t* tables, int n, hipStream_t s);
-constexpr size_t FB_WORDS = 32 * 128 * 16;
+size_t table_build_scratch_bytes(int nb);
+size_t fb_words_per_base();
 }  // namespace fts
 
 using namespace fts;
@@ -81,15 +81,15 @@ struct DBuf {
 };
 
 struct Workspace {
-  DBuf pts, ch, small, hpj, hpa, hpbe, com, combe, x0, terms, scratch;
+  DBuf pts, ch, small, hpj, hpa, hpbe, x0, terms, scratch;
   // random-linear-combination check + MSM
   DBuf r_key, r_msc, r_coef, r_colsum, r_fixed, r_flag, m_keys, m_counts, m_offsets, m_cursor, m_sorted, m_buckets,
-      m_segs, m_wins, m_out, m_scratch, m_win;
+      m_segs, m_wins, m_out, m_scratch, m_win, m_choff, m_chbkt, m_partials;
   // action (transfer / issue) batches
   DBuf rp_raw, rp_sc, rp_status, rp_ipa;
   DBuf s_act, s_raw, s_owner, s_pts, s_sc, s_status, s_work, s_terms, s_aff, s_affoff, s_msgs, s_jac, s_scratch;
   void release() {
-    for (DBuf* b : {&pts, &ch, &small, &hpj, &hpa, &hpbe, &com, &combe, &x0, &terms, &scratch, &rp_raw, &rp_sc,
+    for (DBuf* b : {&pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &terms, &scratch, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
                     &rp_status, &rp_ipa, &s_act, &s_raw, &s_owner, &s_pts, &s_sc, &s_status, &s_work, &s_terms, &s_aff,
                     &s_affoff, &s_msgs, &s_jac, &s_scratch, &r_key, &r_msc, &r_coef, &r_colsum, &r_fixed, &r_flag,
                     &m_keys, &m_counts, &m_offsets, &m_cursor, &m_sorted, &m_buckets, &m_segs, &m_wins, &m_out,
@@ -103,7 +103,7 @@ struct Workspace {
 
 struct fts_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr, stream2 = nullptr;
   PublicParams pp;
   int n = 0, k = 0;
   uint32_t* d_tables = nullptr;
@@ -115,6 +115,7 @@ struct fts_ctx {
   int ntim = 0;
   const char* tim_name[Timeline::CAP];
   float tim_ms[Timeline::CAP];
+  double tim_work[Timeline::CAP];
   int last_fallback = 0;
   std::once_flag prover_once;
   ProverTables ptab;
@@ -192,6 +193,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   };
   if (hipSetDevice(device) != hipSuccess) return fail(FTS_API_EDEVICE);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
+  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
   c->tl.create();
   const int n = c->n;
   // fixed bases in table order (rp_kernels.hpp tb_*)
@@ -218,12 +220,18 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
     }
   uint32_t* d_bases = nullptr;
   uint32_t* d_scr = nullptr;
-  c->table_bytes = (size_t)nb * FB_WORDS * 4;
+  c->table_bytes = (size_t)nb * fb_words_per_base() * 4;
   if (hipMalloc(&c->d_tables, c->table_bytes) != hipSuccess) return fail(FTS_API_ENOMEM);
   if (hipMalloc(&d_bases, hb.size() * 4) != hipSuccess) return fail(FTS_API_ENOMEM);
-  if (hipMalloc(&d_scr, (size_t)nb * 32 * 128 * 32 * 4) != hipSuccess) return fail(FTS_API_ENOMEM);
+  const int chunk = std::min(nb, 16);  // bases per build pass (bounds the Jacobian scratch)
+  if (hipMalloc(&d_scr, table_build_scratch_bytes(chunk)) != hipSuccess) {
+    hipFree(d_bases);
+    return fail(FTS_API_ENOMEM);
+  }
   hipMemcpyAsync(d_bases, hb.data(), hb.size() * 4, hipMemcpyHostToDevice, c->stream);
-  launch_build_tables(d_bases, nb, c->d_tables, d_scr, c->stream);
+  for (int b0 = 0; b0 < nb; b0 += chunk)
+    launch_build_tables(d_bases + (size_t)b0 * 16, std::min(chunk, nb - b0), c->d_tables + (size_t)b0 * fb_words_per_base(),
+                        d_scr, c->stream);
   // constant part of the x0 transcript: hex(G_i) "||" ... hex(Q) "||"
   std::string xc;
   for (int i = 0; i <= n; i++) {
@@ -267,6 +275,7 @@ void fts_ctx_destroy(fts_ctx* c) {
   if (c->d_x0const) hipFree(c->d_x0const);
   c->tl.destroy();
   if (c->stream) hipStreamDestroy(c->stream);
+  if (c->stream2) hipStreamDestroy(c->stream2);
   delete c;
 }
 
@@ -299,11 +308,16 @@ const char* fts_status_str(int32_t s) {
 }
 
 int fts_last_timings(const fts_ctx* c, const char** names, float* ms, int cap) {
+  return fts_last_timings_ex(c, names, ms, nullptr, cap);
+}
+
+int fts_last_timings_ex(const fts_ctx* c, const char** names, float* ms, double* mads, int cap) {
   if (!c) return 0;
   int m = std::min(cap, c->ntim);
   for (int i = 0; i < m; i++) {
     if (names) names[i] = c->tim_name[i];
     if (ms) ms[i] = c->tim_ms[i];
+    if (mads) mads[i] = c->tim_work[i] * MADS_PER_MUL;
   }
   return m;
 }
@@ -345,10 +359,13 @@ static void parse_rp_batch(int k, size_t B, const uint8_t* const* der_p, const s
 }
 
 static void collect_timings(fts_ctx* c) {
-  c->ntim = c->tl.n;
+  c->ntim = 0;
   for (int i = 0; i < c->tl.n; i++) {
-    c->tim_name[i] = c->tl.name[i];
-    hipEventElapsedTime(&c->tim_ms[i], c->tl.ev[i], c->tl.ev[i + 1]);
+    if (!c->tl.name[i]) continue;  // fork/join markers
+    const int j = c->ntim++;
+    c->tim_name[j] = c->tl.name[i];
+    c->tim_work[j] = c->tl.work[i];
+    hipEventElapsedTime(&c->tim_ms[j], c->tl.ev[c->tl.start[i]], c->tl.ev[i + 1]);
   }
 }
 
@@ -365,16 +382,18 @@ static int rp_pipeline(fts_ctx* c, int B, uint8_t* d_raw, uint32_t* d_sc, int32_
   MsmPlan mp{};
   msm_layout(N, mp);
   if (w.pts.ensure((size_t)B * npts * 64) || w.ch.ensure((size_t)B * rp_nch(k) * 32) ||
-      w.small.ensure((size_t)B * (2 + k) * SMALL_SLOT) || w.hpj.ensure((size_t)B * n * 96) || w.hpa.ensure((size_t)B * n * 64) ||
-      w.hpbe.ensure((size_t)B * n * 64) || w.com.ensure((size_t)B * 64) || w.combe.ensure((size_t)B * 64) ||
+      w.small.ensure((size_t)B * (2 + k) * SMALL_SLOT) || w.hpj.ensure((size_t)B * (n + 1) * 96) ||
+      w.hpa.ensure((size_t)B * (n + 1) * 64) || w.hpbe.ensure((size_t)B * (n + 1) * 64) ||
+      w.m_choff.ensure((size_t)mp.NB * 4) || w.m_chbkt.ensure((size_t)mp.NC * 4) ||
+      w.m_partials.ensure((size_t)mp.NC * 96) ||
       w.x0.ensure((size_t)B * x0_slot_bytes(n)) || w.terms.ensure(rp_terms_words(B, n, k) * 4) ||
       w.scratch.ensure(std::max(rp_scratch_words(B, n, k), (size_t)B * 10 * 24) * 4) || w.r_key.ensure(32) ||
       w.r_msc.ensure((size_t)N * 32) || w.r_coef.ensure((size_t)B * 5 * 32) || w.r_colsum.ensure((3 + 2 * n) * 32) ||
-      w.r_fixed.ensure((3 + 2 * n) * 96) || w.r_flag.ensure(4) || w.m_keys.ensure((size_t)mp.nw * N * 4) ||
+      w.r_fixed.ensure((3 + 2 * n) * 96) || w.r_flag.ensure(4) || w.m_keys.ensure((size_t)mp.nw * mp.NV * 4) ||
       w.m_counts.ensure((size_t)mp.NB * 4) || w.m_offsets.ensure((size_t)mp.NB * 4) ||
-      w.m_cursor.ensure((size_t)mp.NB * 4) || w.m_sorted.ensure((size_t)mp.nw * N * 4) ||
+      w.m_cursor.ensure((size_t)mp.NB * 4) || w.m_sorted.ensure((size_t)mp.nw * mp.NV * 4) ||
       w.m_buckets.ensure((size_t)mp.NB * 96) || w.m_segs.ensure((size_t)mp.NS * 96) ||
-      w.m_wins.ensure((size_t)mp.nw * 96) || w.m_out.ensure(96) || w.m_scratch.ensure((size_t)mp.NS * 96) ||
+      w.m_wins.ensure((size_t)(mp.nw + 1) * 96) || w.m_out.ensure(96) || w.m_scratch.ensure((size_t)mp.NS * 96) ||
       w.m_win.ensure(sizeof(mp.win)))
     return FTS_API_ENOMEM;
   RpBatchDev d{B,
@@ -390,8 +409,6 @@ static int rp_pipeline(fts_ctx* c, int B, uint8_t* d_raw, uint32_t* d_sc, int32_
                w.hpj.as<uint32_t>(),
                w.hpa.as<uint32_t>(),
                w.hpbe.as<uint8_t>(),
-               w.com.as<uint32_t>(),
-               w.combe.as<uint8_t>(),
                w.x0.as<uint8_t>(),
                w.terms.as<uint32_t>(),
                w.scratch.as<uint32_t>()};
@@ -406,6 +423,9 @@ static int rp_pipeline(fts_ctx* c, int B, uint8_t* d_raw, uint32_t* d_sc, int32_
   mp.segs = w.m_segs.as<uint32_t>();
   mp.wins = w.m_wins.as<uint32_t>();
   mp.out = w.m_out.as<uint32_t>();
+  mp.chunk_off = w.m_choff.as<uint32_t>();
+  mp.chunk_bkt = w.m_chbkt.as<int32_t>();
+  mp.partials = w.m_partials.as<uint32_t>();
   RlcDev r{w.r_key.as<uint32_t>(), w.r_msc.as<uint32_t>(),   w.r_coef.as<uint32_t>(), w.r_colsum.as<uint32_t>(),
            w.r_fixed.as<uint32_t>(), w.r_flag.as<int32_t>(), w.m_scratch.as<uint32_t>(), mp};
   // fresh RLC weights key (getrandom), unpredictable to the provers
@@ -413,8 +433,7 @@ static int rp_pipeline(fts_ctx* c, int B, uint8_t* d_raw, uint32_t* d_sc, int32_
   if (getrandom(key, sizeof key, 0) != (ssize_t)sizeof key) return FTS_API_EDEVICE;
   HIP_OK(hipMemcpyAsync(r.key, key, sizeof key, hipMemcpyHostToDevice, c->stream));
   c->tl.begin(c->stream);
-  launch_rp_exact(d, c->d_tables, c->d_x0const, c->stream, &c->tl);
-  launch_rp_rlc(d, r, c->d_tables, c->stream, &c->tl);
+  launch_rp_batch(d, r, c->d_tables, c->d_x0const, c->stream, c->stream2, &c->tl);
   between();
   HIP_OK(hipGetLastError());
   int32_t flag = 0;
@@ -457,8 +476,8 @@ int fts_debug_rp_intermediates(fts_ctx* c, size_t i, uint8_t* ch_out, uint8_t* c
       fr_to_be(m, ch_out + 32 * q);
     }
   }
-  if (com_out) HIP_OK(hipMemcpy(com_out, c->ws.combe.as<uint8_t>() + i * 64, 64, hipMemcpyDeviceToHost));
-  if (hp_out) HIP_OK(hipMemcpy(hp_out, c->ws.hpbe.as<uint8_t>() + i * n * 64, n * 64, hipMemcpyDeviceToHost));
+  if (com_out) HIP_OK(hipMemcpy(com_out, c->ws.hpbe.as<uint8_t>() + (i * (n + 1) + n) * 64, 64, hipMemcpyDeviceToHost));
+  if (hp_out) HIP_OK(hipMemcpy(hp_out, c->ws.hpbe.as<uint8_t>() + i * (n + 1) * 64, n * 64, hipMemcpyDeviceToHost));
   return FTS_API_OK;
 }
 

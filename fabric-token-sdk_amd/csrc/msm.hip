@@ -6,22 +6,29 @@
 // bulletproof.go:314-324 and ipa.go:254-259.  Also exposed as fts_msm_g1
 // (BASELINE config C3 microbenchmark).
 #include "device/g1.hpp"
+#include "device/glv.hpp"
+#include "device/fixed_base.hpp"
 #include "device/helpers.hpp"
 #include "device/msm.hpp"
 #include "device/rp_kernels.hpp"
 
 namespace fts {
 
-// bits [off, off+width) of a 256-bit LE scalar (width <= 20)
-FTS_DEV uint32_t scalar_bits(const uint32_t s[8], int off, int width) {
+// bits [off, off+width) of a 128-bit LE magnitude (width <= 20)
+FTS_DEV uint32_t scalar_bits4(const uint32_t s[4], int off, int width) {
   int q = off >> 5, r = off & 31;
-  uint64_t lo = s[q < 8 ? q : 7];
-  uint64_t hi = (q + 1 < 8) ? s[q + 1] : 0;
-  if (q >= 8) return 0;
+  uint64_t lo = 0, hi = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    if (i == q) lo = s[i];
+    if (i == q + 1) hi = s[i];
+  }
   uint64_t v = (lo | (hi << 32)) >> r;
   return (uint32_t)(v & ((1ull << width) - 1));
 }
 
+// lane per real point i: GLV split, then the signed digits of both halves
+// (virtual points i and N + i) for every window
 __global__ void __launch_bounds__(256) k_msm_digits(int N, int nw, const MsmWindow* __restrict__ win,
                                                     const uint32_t* __restrict__ scalars, int32_t* __restrict__ keys,
                                                     uint32_t* __restrict__ counts) {
@@ -30,66 +37,85 @@ __global__ void __launch_bounds__(256) k_msm_digits(int N, int nw, const MsmWind
   uint32_t s[8];
 #pragma unroll
   for (int q = 0; q < 8; q++) s[q] = scalars[(size_t)i * 8 + q];
-  int carry = 0;
-  for (int w = 0; w < nw; w++) {
-    const MsmWindow W = win[w];
-    int d = (int)scalar_bits(s, W.off, W.width) + carry;
-    const int half = 1 << (W.width - 1);
-    carry = d > half;
-    d = carry ? d - (1 << W.width) : d;
-    int key = -1;
-    if (d != 0) {
-      int b = W.bbase + (d < 0 ? -d : d) - 1;
-      key = d < 0 ? (b | (int)0x80000000) : b;
-      atomicAdd(&counts[b], 1u);
+  uint32_t k[2][4], sg[2];
+  glv_decompose(s, k[0], sg[0], k[1], sg[1]);
+  const int NV = 2 * N;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    int carry = 0;
+    for (int w = 0; w < nw; w++) {
+      const MsmWindow W = win[w];
+      int d = (int)scalar_bits4(k[h], W.off, W.width) + carry;
+      const int half = 1 << (W.width - 1);
+      carry = d > half;
+      d = carry ? d - (1 << W.width) : d;
+      int key = -1;
+      if (d != 0) {
+        int b = W.bbase + (d < 0 ? -d : d) - 1;
+        key = ((d < 0) != (sg[h] != 0)) ? (b | (int)0x80000000) : b;
+        atomicAdd(&counts[b], 1u);
+      }
+      keys[(size_t)w * NV + h * N + i] = key;
     }
-    keys[(size_t)w * N + i] = key;
   }
 }
 
-// exclusive scan of the window's bucket counts -> offsets, cursor (block per window)
+// Prefix sums of one window (block per window): entry offsets of the buckets
+// in the window's sorted range, and the chunk map (bucket b owns chunk slots
+// [chunk_off[b], chunk_off[b] + ceil(cnt_b / MSM_CH)) inside the window's
+// reserved slot range; unused slots keep chunk_bkt = -1 from the memset).
 __global__ void __launch_bounds__(256) k_msm_scan(const MsmWindow* __restrict__ win, const uint32_t* __restrict__ counts,
-                                                  uint32_t* __restrict__ offsets, uint32_t* __restrict__ cursor) {
-  __shared__ uint32_t part[256];
+                                                  uint32_t* __restrict__ offsets, uint32_t* __restrict__ cursor,
+                                                  uint32_t* __restrict__ chunk_off, int32_t* __restrict__ chunk_bkt) {
+  __shared__ uint32_t pe[256], pc[256];
   const int t = threadIdx.x;
   const MsmWindow W = win[blockIdx.x];
   const int nb = 1 << (W.width - 1);
   const uint32_t* C = counts + W.bbase;
   const int per = (nb + 255) / 256;
-  uint32_t loc = 0;
-  for (int j = 0; j < per; j++) {
-    int b = t * per + j;
-    if (b < nb) loc += C[b];
-  }
-  part[t] = loc;
-  __syncthreads();
-  for (int off = 1; off < 256; off <<= 1) {
-    uint32_t v = t >= off ? part[t - off] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  uint32_t run = part[t] - loc;
+  uint32_t le = 0, lc = 0;
   for (int j = 0; j < per; j++) {
     int b = t * per + j;
     if (b < nb) {
-      offsets[W.bbase + b] = run;
-      cursor[W.bbase + b] = run;
-      run += C[b];
+      le += C[b];
+      lc += (C[b] + MSM_CH - 1) / MSM_CH;
+    }
+  }
+  pe[t] = le;
+  pc[t] = lc;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    uint32_t ve = t >= off ? pe[t - off] : 0, vc = t >= off ? pc[t - off] : 0;
+    __syncthreads();
+    pe[t] += ve;
+    pc[t] += vc;
+    __syncthreads();
+  }
+  uint32_t re = pe[t] - le, rc = (uint32_t)W.cbase + pc[t] - lc;
+  for (int j = 0; j < per; j++) {
+    int b = t * per + j;
+    if (b < nb) {
+      const uint32_t cnt = C[b], nch = (cnt + MSM_CH - 1) / MSM_CH;
+      offsets[W.bbase + b] = re;
+      cursor[W.bbase + b] = re;
+      chunk_off[W.bbase + b] = rc;
+      for (uint32_t q = 0; q < nch; q++) chunk_bkt[rc + q] = W.bbase + b;
+      re += cnt;
+      rc += nch;
     }
   }
 }
 
-__global__ void __launch_bounds__(256) k_msm_scatter(int N, int nw, const int32_t* __restrict__ keys,
+__global__ void __launch_bounds__(256) k_msm_scatter(int NV, int nw, const int32_t* __restrict__ keys,
                                                      uint32_t* __restrict__ cursor, uint32_t* __restrict__ sorted) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
+  if (i >= NV) return;
   for (int w = 0; w < nw; w++) {
-    int key = keys[(size_t)w * N + i];
+    int key = keys[(size_t)w * NV + i];
     if (key == -1) continue;
     uint32_t b = (uint32_t)key & 0x7fffffffu;
     uint32_t pos = atomicAdd(&cursor[b], 1u);
-    sorted[(size_t)w * N + pos] = (uint32_t)i | ((uint32_t)key & 0x80000000u);
+    sorted[(size_t)w * NV + pos] = (uint32_t)i | ((uint32_t)key & 0x80000000u);
   }
 }
 
@@ -100,21 +126,48 @@ FTS_DEV int window_of_bucket(const MsmWindow* win, int nw, int b) {
   return w;
 }
 
-__global__ void __launch_bounds__(64) k_msm_buckets(int N, int nw, int NB, const MsmWindow* __restrict__ win,
-                                                    const uint32_t* __restrict__ points,
-                                                    const uint32_t* __restrict__ offsets,
-                                                    const uint32_t* __restrict__ counts,
-                                                    const uint32_t* __restrict__ sorted, uint32_t* __restrict__ buckets) {
+// one lane per chunk slot: <= MSM_CH mixed additions of sorted virtual points
+// (index >= N: phi(P_{index-N}) = (beta x, y))
+__global__ void __launch_bounds__(64) k_msm_chunks(int N, int nw, int NC, const MsmWindow* __restrict__ win,
+                                                   const uint32_t* __restrict__ points,
+                                                   const uint32_t* __restrict__ offsets,
+                                                   const uint32_t* __restrict__ counts,
+                                                   const uint32_t* __restrict__ chunk_off,
+                                                   const int32_t* __restrict__ chunk_bkt,
+                                                   const uint32_t* __restrict__ sorted, uint32_t* __restrict__ partials) {
+  int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= NC) return;
+  const int b = chunk_bkt[g];
+  if (b < 0) return;
+  const int w = window_of_bucket(win, nw, b);
+  const uint32_t j = (uint32_t)g - chunk_off[b], cnt = counts[b];
+  const uint32_t lo = j * MSM_CH, hi = min(cnt, lo + MSM_CH);
+  const uint32_t* S = sorted + (size_t)w * 2 * N + offsets[b];
+  const Fp beta = glv_beta();
+  G1J acc = g1j_identity();
+  for (uint32_t t = lo; t < hi; t++) {
+    const uint32_t e = S[t], v = e & 0x7fffffffu;
+    const bool ph = v >= (uint32_t)N;
+    G1A q = load_g1a(points + (size_t)(ph ? v - N : v) * 16);
+    if (g1a_is_identity(q)) continue;
+    if (ph) q.x = fp_mul(q.x, beta);
+    if (e >> 31) q.y = f_neg(q.y);
+    madd_inl(acc, q);
+  }
+  store_g1j(partials + (size_t)g * 24, acc);
+}
+
+// one lane per bucket: sum of its chunk partials (usually 1..4)
+__global__ void __launch_bounds__(64) k_msm_bucket_sum(int NB, const uint32_t* __restrict__ counts,
+                                                       const uint32_t* __restrict__ chunk_off,
+                                                       const uint32_t* __restrict__ partials,
+                                                       uint32_t* __restrict__ buckets) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= NB) return;
-  const int w = window_of_bucket(win, nw, b);
-  const uint32_t off = offsets[b], cnt = counts[b];
-  const uint32_t* S = sorted + (size_t)w * N;
+  const uint32_t nch = (counts[b] + MSM_CH - 1) / MSM_CH, c0 = chunk_off[b];
   G1J acc = g1j_identity();
-  for (uint32_t t = 0; t < cnt; t++) {
-    uint32_t e = S[off + t];
-    acc = nl_madd_mem(acc, points + (size_t)(e & 0x7fffffffu) * 16, e >> 31);
-  }
+  if (nch) acc = load_g1j(partials + (size_t)c0 * 24);
+  for (uint32_t q = 1; q < nch; q++) add_inl(acc, load_g1j(partials + (size_t)(c0 + q) * 24));
   store_g1j(buckets + (size_t)b * 24, acc);
 }
 
@@ -132,41 +185,46 @@ __global__ void __launch_bounds__(64) k_msm_segments(int nw, int NS, const MsmWi
   const int s = g - W.sbase;
   const int lo = s * MSM_SEG, cnt = (nb - lo) < MSM_SEG ? (nb - lo) : MSM_SEG;
   const uint32_t* Bk = buckets + ((size_t)W.bbase + lo) * 24;
-  uint32_t* scr = scratch + (size_t)g * 24;
   G1J sum = g1j_identity(), acc = g1j_identity();
   for (int j = cnt - 1; j >= 0; j--) {
-    sum = nl_add_mem(sum, Bk + j * 24, 0);
-    store_g1j(scr, sum);
-    acc = nl_add_mem(acc, scr, 0);
+    add_inl(sum, load_g1j(Bk + j * 24));
+    add_inl(acc, sum);
   }
   uint32_t m = (uint32_t)lo;  // bucket lo+j carries multiplier lo + j + 1
   if (m) {
-    store_g1j(scr, sum);
     G1J t = g1j_identity();
     for (int bit = 31 - __builtin_clz(m); bit >= 0; bit--) {
-      t = nl_dbl(t);
-      if ((m >> bit) & 1u) t = nl_add_mem(t, scr, 0);
+      t = g1j_dbl(t);
+      if ((m >> bit) & 1u) add_inl(t, sum);
     }
-    store_g1j(scr, t);
-    acc = nl_add_mem(acc, scr, 0);
+    add_inl(acc, t);
   }
   store_g1j(segs + (size_t)g * 24, acc);
 }
 
-// tree over the segments of one window (block per window, 64 threads)
-__global__ void __launch_bounds__(64) k_msm_windows(const MsmWindow* __restrict__ win, const uint32_t* __restrict__ segs,
-                                                    uint32_t* __restrict__ wins) {
-  __shared__ uint32_t sh[64 * 24];
+// LDS tree (block of 256 lanes): block w < nw sums the segments of window w;
+// block nw sums the nextra extra Jacobian points (the fixed-base part)
+__global__ void __launch_bounds__(256) k_msm_windows(int nw, const MsmWindow* __restrict__ win,
+                                                     const uint32_t* __restrict__ segs, const uint32_t* __restrict__ extra,
+                                                     int nextra, uint32_t* __restrict__ wins) {
+  __shared__ uint32_t sh[256 * 24];
   const int t = threadIdx.x;
-  const MsmWindow W = win[blockIdx.x];
-  const int nseg = ((1 << (W.width - 1)) + MSM_SEG - 1) / MSM_SEG;
-  const uint32_t* S = segs + (size_t)W.sbase * 24;
+  const uint32_t* S;
+  int cnt;
+  if ((int)blockIdx.x < nw) {
+    const MsmWindow W = win[blockIdx.x];
+    cnt = ((1 << (W.width - 1)) + MSM_SEG - 1) / MSM_SEG;
+    S = segs + (size_t)W.sbase * 24;
+  } else {
+    cnt = nextra;
+    S = extra;
+  }
   G1J acc = g1j_identity();
-  for (int s = t; s < nseg; s += 64) acc = nl_add_mem(acc, S + s * 24, 0);
+  for (int s = t; s < cnt; s += 256) add_inl(acc, load_g1j(S + (size_t)s * 24));
   store_g1j(sh + t * 24, acc);
   __syncthreads();
-  for (int half = 32; half >= 1; half >>= 1) {
-    if (t < half) acc = nl_add_mem(acc, sh + (t + half) * 24, 0);
+  for (int half = 128; half >= 1; half >>= 1) {
+    if (t < half) add_inl(acc, load_g1j(sh + (t + half) * 24));
     __syncthreads();
     if (t < half) store_g1j(sh + t * 24, acc);
     __syncthreads();
@@ -174,17 +232,17 @@ __global__ void __launch_bounds__(64) k_msm_windows(const MsmWindow* __restrict_
   if (t == 0) store_g1j(wins + (size_t)blockIdx.x * 24, acc);
 }
 
-// result = sum_w 2^off_w W_w (+ extra Jacobian points, e.g. the fixed-base part)
+// result = sum_w 2^off_w W_w + (sum of the extra points, slot nw)
 __global__ void k_msm_final(int nw, const MsmWindow* __restrict__ win, const uint32_t* __restrict__ wins,
-                            const uint32_t* __restrict__ extra, int nextra, uint32_t* __restrict__ out) {
+                            uint32_t* __restrict__ out) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   G1J acc = load_g1j(wins + (size_t)(nw - 1) * 24);
   for (int w = nw - 2; w >= 0; w--) {
     const int shift = win[w + 1].off - win[w].off;
-    for (int q = 0; q < shift; q++) acc = nl_dbl(acc);
-    acc = nl_add_mem(acc, wins + (size_t)w * 24, 0);
+    for (int q = 0; q < shift; q++) acc = g1j_dbl(acc);
+    add_inl(acc, load_g1j(wins + (size_t)w * 24));
   }
-  for (int e = 0; e < nextra; e++) acc = nl_add_mem(acc, extra + (size_t)e * 24, 0);
+  add_inl(acc, load_g1j(wins + (size_t)nw * 24));
   store_g1j(out, acc);
 }
 
@@ -195,23 +253,32 @@ __global__ void k_msm_final(int nw, const MsmWindow* __restrict__ win, const uin
   } while (0)
 
 // scratch: NS * 24 words.  p.d_win must already hold p.win (uploaded by the caller).
+// `extra` (nextra Jacobian points) is produced on stream s_extra: joined
+// before the window reduction that sums it.
 void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
-                uint32_t* scratch, hipStream_t s, Timeline* tl) {
+                uint32_t* scratch, hipStream_t s, hipStream_t s_extra, Timeline* tl) {
   (void)hipMemsetAsync(p.counts, 0, (size_t)p.NB * 4, s);
+  (void)hipMemsetAsync(p.chunk_bkt, 0xff, (size_t)p.NC * 4, s);
   FTS_LAUNCH(k_msm_digits, p.N, 256, s, p.N, p.nw, p.d_win, scalars, p.keys, p.counts);
-  if (tl) tl->mark("k_msm_digits", s);
-  hipLaunchKernelGGL(k_msm_scan, dim3(p.nw), dim3(256), 0, s, p.d_win, p.counts, p.offsets, p.cursor);
-  if (tl) tl->mark("k_msm_scan", s);
-  FTS_LAUNCH(k_msm_scatter, p.N, 256, s, p.N, p.nw, p.keys, p.cursor, p.sorted);
-  if (tl) tl->mark("k_msm_scatter", s);
-  FTS_LAUNCH(k_msm_buckets, p.NB, 64, s, p.N, p.nw, p.NB, p.d_win, points, p.offsets, p.counts, p.sorted, p.buckets);
-  if (tl) tl->mark("k_msm_buckets", s);
+  tl->mark("k_msm_digits", s, 0);
+  hipLaunchKernelGGL(k_msm_scan, dim3(p.nw), dim3(256), 0, s, p.d_win, p.counts, p.offsets, p.cursor, p.chunk_off,
+                     p.chunk_bkt);
+  tl->mark("k_msm_scan", s, 0);
+  FTS_LAUNCH(k_msm_scatter, p.NV, 256, s, p.NV, p.nw, p.keys, p.cursor, p.sorted);
+  tl->mark("k_msm_scatter", s, 0);
+  FTS_LAUNCH(k_msm_chunks, p.NC, 64, s, p.N, p.nw, p.NC, p.d_win, points, p.offsets, p.counts, p.chunk_off,
+             p.chunk_bkt, p.sorted, p.partials);
+  // expected nonzero digits: N * nw * (1 - 2^-c) ~ N * nw mixed additions
+  tl->mark("k_msm_chunks", s, (double)p.NV * p.nw * (COST_MADD + 0.5));
+  FTS_LAUNCH(k_msm_bucket_sum, p.NB, 64, s, p.NB, p.counts, p.chunk_off, p.partials, p.buckets);
+  tl->mark("k_msm_bucket_sum", s, 0);
   FTS_LAUNCH(k_msm_segments, p.NS, 64, s, p.nw, p.NS, p.d_win, p.buckets, p.segs, scratch);
-  if (tl) tl->mark("k_msm_segments", s);
-  hipLaunchKernelGGL(k_msm_windows, dim3(p.nw), dim3(64), 0, s, p.d_win, p.segs, p.wins);
-  if (tl) tl->mark("k_msm_windows", s);
-  hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, s, p.nw, p.d_win, p.wins, extra, nextra, p.out);
-  if (tl) tl->mark("k_msm_final", s);
+  tl->mark("k_msm_segments", s, (double)p.NB * 2 * COST_ADD);
+  if (s_extra != s) tl->fork(s_extra, s);
+  hipLaunchKernelGGL(k_msm_windows, dim3(p.nw + 1), dim3(256), 0, s, p.nw, p.d_win, p.segs, extra, nextra, p.wins);
+  tl->mark("k_msm_windows", s, (double)(p.NS + nextra) * COST_ADD);
+  hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, s, p.nw, p.d_win, p.wins, p.out);
+  tl->mark("k_msm_final", s, (double)MSM_BITS * COST_DBL + p.nw * COST_ADD);
 }
 
 }  // namespace fts

@@ -2,26 +2,25 @@
 //
 // One launch sequence verifies a whole batch of B proofs of bit length n
 // (k = log2 n rounds).  Work is laid out per (proof, item) so a batch of a
-// few thousand proofs fills the 256 CUs:
+// few thousand proofs fills the 256 CUs.  Stream S is the batch's main
+// stream, S2 its side stream (fork/join through events):
 //
-//   k_rp_decode        (proof, point)   NewG1FromBytes checks + Montgomery form
-//   k_rp_hash_small    (proof, msg)     x, y, x_j transcripts (SHA-256 over hex)  bulletproof.go:266-281, ipa.go:230
-//   k_rp_chal_fr       proof            z, polEval, batch inversion of y, x_j       bulletproof.go:282-311, ipa.go:236-244
-//   k_rp_hprime        (proof, i)       H'_i = y^-i * H_i  fixed-base    bulletproof.go:483-489
-//   k_rp_hp_normalize  proof            batch affine normalisation (Montgomery trick)
-//   k_rp_com_terms     (proof, term)    com = x*D + C + z*K + sum (z^2 2^i y^-i) H_i - delta*P
-//   k_rp_com_sum       proof (wave)     LDS tree + normalisation          bulletproof.go:477-492
-//   k_rp_x0_build      (proof, record)  DER(hex(H'..., G..., Q, com) "||" Zb(ip))   ipa.go:200-212
-//   k_rp_x0_hash       proof            x0 = HashToZr(...)                ipa.go:213
-//   k_rp_terms_fixed   (proof, term)    fixed-base terms of E1 / E2
-//   k_rp_terms_var     (proof, term)    variable-base terms of E1 / E2
-//   k_rp_check         proof            E1 == O ("invalid range proof"), E2 == O ("invalid IPA")
+//   S   k_rp_decode        (proof, point)   NewG1FromBytes checks + Montgomery form
+//   S   k_rp_hash_small    (proof, msg)     x, y, x_j transcripts (SHA-256 over hex)  bulletproof.go:266-281, ipa.go:230
+//   S   k_rp_chal_fr       proof            z, polEval, batch inversion of y, x_j       bulletproof.go:282-311, ipa.go:236-244
+//   S2  k_rp_xd            proof            x*D (variable base)                         bulletproof.go:478
+//   S   k_rp_fixed_exact   (proof, item)    H'_i = y^-i H_i; com terms (z^2 2^i y^-i) H_i, z K, -delta P
+//   S   k_rp_com_sum       proof (wave)     LDS tree of the com terms + x*D + C         bulletproof.go:477-492
+//   S   k_rp_normalize     point (block)    batch affine normalisation of H'_i and com (one inversion per 256 points)
+//   S2  k_rp_x0_build      (proof, record)  DER(hex(H'..., G..., Q, com) "||" Zb(ip))   ipa.go:200-212
+//   S2  k_rp_x0_hash       proof            x0 = HashToZr(...)                          ipa.go:213
+//   S2  k_rlc_columns/fixed                 fixed-base columns of the batch equation (need x0)
+//   S   k_rlc_prep + MSM                    variable points of the batch equation (no x0)
+//   k_rp_terms_fixed / k_rp_terms_var / k_rp_check: per-proof fallback
 //
-// E1: (ip - polEval) G + tau H - x T1 - x^2 T2 - z^2 V            (bulletproof.go:314-324)
-// E2: sum a s_i G_i + sum b s_i^-1 y^-i H_i + (ab - ip) x0 Q - com
-//     - sum x_j^2 L_j - sum x_j^-2 R_j                              (ipa.go:214-259 unrolled:
-//     G_fin = sum s_i G_i, H'_fin = sum s_i^-1 H'_i, s_i = prod_j x_j^{+-1} by bit k-1-j of i)
 #include "device/g1.hpp"
+#include "device/fixed_base.hpp"
+#include "device/glv.hpp"
 #include "device/rp_kernels.hpp"
 #include "device/transcript.hpp"
 #include "device/helpers.hpp"
@@ -31,45 +30,59 @@
 
 namespace fts {
 
+constexpr int NORM_BS = 256;
+__global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, const int32_t* __restrict__ status,
+                                                          const uint32_t* __restrict__ jac, uint32_t* __restrict__ aff,
+                                                          uint8_t* __restrict__ be);
+
 // ---------------------------------------------------------- context tables
-// thread per (base, window w): entries d * 2^(8w) * B for d = 1..128, affine.
-// scratch: [nb*32][128][32] words (Jacobian point + prefix product)
-__global__ void __launch_bounds__(64) k_build_tables(const uint32_t* __restrict__ bases, int nb,
-                                                     uint32_t* __restrict__ tables, uint32_t* __restrict__ scratch) {
+// Built once per context (device/fixed_base.hpp layout), for nb bases:
+//   kt_window_bases  lane per (base, window)   B_w = 2^(FB_W w) B            (Jacobian)
+//   kt_small_large   lane per (base, window)   small[lo] = (lo+1) B_w, large[hi] = hi FB_S B_w
+//   kt_entries       lane per entry            T[w][d-1] = large[hi] + small[lo], d-1 = hi FB_S + lo
+//   k_rp_normalize   block per 256 entries     affine (one inversion per block)
+__global__ void __launch_bounds__(64) kt_window_bases(const uint32_t* __restrict__ bases, int nb,
+                                                      uint32_t* __restrict__ bw) {
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= nb * FB_WINDOWS) return;
-  int b = gid / FB_WINDOWS, w = gid % FB_WINDOWS;
-  G1A B = load_g1a(bases + b * 16);
-  G1J bw = g1j_from_affine(B);
-  for (int i = 0; i < 8 * w; i++) bw = nl_dbl(bw);
-  uint32_t* J = scratch + (size_t)gid * FB_ENTRIES * 32;
-  G1J acc = bw;
-  Fp pre = f_one<FpP>();
-  for (int d = 1; d <= FB_ENTRIES; d++) {
-    if (d > 1) acc = nl_add_mem(acc, J, 0);  // J[0] holds bw
-    store_g1j(J + (d - 1) * 32, acc);
-    store_fp(J + (d - 1) * 32 + 24, pre);
-    if (!f_is_zero(acc.z)) pre = fp_mul(pre, acc.z);
+  if (gid >= nb * FB_NW) return;
+  int b = gid / FB_NW, w = gid % FB_NW;
+  G1J p = g1j_from_affine(load_g1a(bases + b * 16));
+  for (int i = 0; i < FB_W * w; i++) p = nl_dbl(p);
+  store_g1j(bw + (size_t)gid * 24, p);
+}
+
+__global__ void __launch_bounds__(64) kt_small_large(int nb, const uint32_t* __restrict__ bw,
+                                                     uint32_t* __restrict__ small, uint32_t* __restrict__ large) {
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= nb * FB_NW) return;
+  const uint32_t* Bw = bw + (size_t)gid * 24;
+  uint32_t* S = small + (size_t)gid * FB_S * 24;
+  uint32_t* L = large + (size_t)gid * FB_L * 24;
+  G1J acc = load_g1j(Bw);
+  store_g1j(S, acc);
+  for (int lo = 1; lo < FB_S; lo++) {
+    acc = nl_add_mem(acc, Bw, 0);
+    store_g1j(S + lo * 24, acc);
   }
-  Fp inv = nl_fp_inv(pre);
-  uint32_t* T = tables + (size_t)b * FB_WORDS_PER_BASE + (size_t)w * FB_ENTRIES * 16;
-  for (int d = FB_ENTRIES; d >= 1; d--) {
-    G1J p = load_g1j(J + (d - 1) * 32);
-    G1A a;
-    if (f_is_zero(p.z)) {
-      a.x = f_zero<FpP>();
-      a.y = f_zero<FpP>();
-    } else {
-      Fp pr;
-      load_fp(J + (d - 1) * 32 + 24, pr);
-      Fp zi = fp_mul(inv, pr);
-      inv = fp_mul(inv, p.z);
-      Fp zi2 = fp_sqr(zi);
-      a.x = fp_mul(p.x, zi2);
-      a.y = fp_mul(fp_mul(p.y, zi2), zi);
-    }
-    store_g1a(T + (d - 1) * 16, a);
+  // acc = FB_S * B_w
+  store_g1j(L, g1j_identity());
+  G1J big = g1j_identity();
+  for (int hi = 1; hi < FB_L; hi++) {
+    big = nl_add_mem(big, S + (FB_S - 1) * 24, 0);
+    store_g1j(L + hi * 24, big);
   }
+}
+
+__global__ void __launch_bounds__(64) kt_entries(int nb, const uint32_t* __restrict__ small,
+                                                 const uint32_t* __restrict__ large, uint32_t* __restrict__ jac) {
+  size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (size_t)nb * FB_NW * FB_E) return;
+  const size_t bw = gid / FB_E;
+  const int e = (int)(gid % FB_E);  // d - 1
+  const int hi = e / FB_S, lo = e % FB_S;
+  G1J p = load_g1j(small + (bw * FB_S + lo) * 24);
+  if (hi) p = nl_add_mem(p, large + (bw * FB_L + hi) * 24, 0);
+  store_g1j(jac + gid * 24, p);
 }
 
 // ------------------------------------------------------------------ decode
@@ -141,15 +154,18 @@ __global__ void __launch_bounds__(64) k_rp_chal_fr(int B, int n, int k, const in
   Fr z = f_to_mont(digest_to_fr(st));
   Fr y = f_to_mont(yc), x = f_to_mont(xc);
   Fr x2 = fr_sqr(x), z2 = fr_sqr(z), z3 = fr_mul(z2, z);
-  Fr yp = f_one<FrP>(), ipy = f_zero<FrP>(), p2 = f_one<FrP>(), ip2 = f_zero<FrP>();
-  for (int i = 0; i < n; i++) {
-    if (i) {
-      yp = fr_mul(yp, y);
-      p2 = f_dbl(p2);
-    }
-    ipy = f_add(ipy, yp);
-    ip2 = f_add(ip2, p2);
+  // sum_{i<n} y^i by doubling (n = 2^k): S_2m = S_m (1 + y^m), y^2m = (y^m)^2
+  // (same field element as the reference's loop, bulletproof.go:287-305)
+  Fr ipy = f_one<FrP>(), ym = y;
+  for (int m = 1; m < n; m <<= 1) {
+    ipy = fr_mul(ipy, f_add(f_one<FrP>(), ym));
+    ym = fr_sqr(ym);
   }
+  // sum_{i<n} 2^i = 2^n - 1 (< r for n <= 64)
+  Fr ip2 = f_zero<FrP>();
+  ip2.v[0] = n >= 32 ? 0xffffffffu : (1u << n) - 1u;
+  ip2.v[1] = n >= 64 ? 0xffffffffu : (n > 32 ? (1u << (n - 32)) - 1u : 0u);
+  ip2 = f_to_mont(ip2);
   Fr pol = f_sub(fr_mul(f_sub(z, z2), ipy), fr_mul(z3, ip2));  // bulletproof.go:307-311
   store_f(C + CH_X * 8, x);
   store_f(C + CH_X2 * 8, x2);
@@ -185,152 +201,178 @@ __global__ void __launch_bounds__(64) k_rp_chal_fr(int B, int n, int k, const in
   }
 }
 
-// --------------------------------------------------------------------- H'
-__global__ void __launch_bounds__(64) k_rp_hprime(int B, int n, int k, const int32_t* __restrict__ status,
-                                                  const uint32_t* __restrict__ ch, const uint32_t* __restrict__ tables,
-                                                  uint32_t* __restrict__ hpj) {
-  int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= B * n) return;
-  int b = gid / n, i = gid % n;
-  if (status[b] != 0) return;
-  Fr yinv;
-  load_f(ch + ((size_t)b * rp_nch(k) + CH_YINV) * 8, yinv);
-  G1J r = fixed_base_mul(tables + (size_t)(n + i) * FB_WORDS_PER_BASE, fr_canon(fr_pow_small(yinv, (uint32_t)i)));
-  store_g1j(hpj + (size_t)gid * 24, r);
-}
-
-// batch affine normalisation of the n H'_i of one proof
-__global__ void __launch_bounds__(64) k_rp_hp_normalize(int B, int n, const int32_t* __restrict__ status,
-                                                        const uint32_t* __restrict__ hpj, uint32_t* __restrict__ hpa,
-                                                        uint8_t* __restrict__ hp_be) {
-  int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B || status[b] != 0) return;
-  const uint32_t* J = hpj + (size_t)b * n * 24;
-  uint32_t* A = hpa + (size_t)b * n * 16;
-  Fp acc = f_one<FpP>();
-  for (int i = 0; i < n; i++) {
-    store_fp(A + i * 16, acc);  // prefix product
-    Fp z;
-    load_fp(J + i * 24 + 16, z);
-    if (!f_is_zero(z)) acc = fp_mul(acc, z);
-  }
-  Fp inv = nl_fp_inv(acc);
-  for (int i = n - 1; i >= 0; i--) {
-    G1J p = load_g1j(J + i * 24);
-    G1A a;
-    if (f_is_zero(p.z)) {
-      a.x = f_zero<FpP>();
-      a.y = f_zero<FpP>();
-    } else {
-      Fp pr;
-      load_fp(A + i * 16, pr);
-      Fp zi = fp_mul(inv, pr);
-      inv = fp_mul(inv, p.z);
-      Fp zi2 = fp_sqr(zi);
-      a.x = fp_mul(p.x, zi2);
-      a.y = fp_mul(fp_mul(p.y, zi2), zi);
-    }
-    store_g1a(A + i * 16, a);
-    uint32_t pw[16];
-    g1_mont_to_be_words(a.x, a.y, pw);
-    uint4* d = reinterpret_cast<uint4*>(hp_be + ((size_t)b * n + i) * 64);
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-      d[q] = make_uint4(__builtin_bswap32(pw[4 * q]), __builtin_bswap32(pw[4 * q + 1]),
-                        __builtin_bswap32(pw[4 * q + 2]), __builtin_bswap32(pw[4 * q + 3]));
-  }
-}
-
-// -------------------------------------------------------------------- com
+// ------------------------------------------------------------ H' and com
 // com = x*D + C - z sum G_i + sum (z y^i + z^2 2^i) H'_i - delta*P   (bulletproof.go:477-492)
 //     = x*D + C + z*K + sum_i (z^2 2^i y^-i) H_i - delta*P,   K = sum H_i - sum G_i
 // (same group element; only the affine result is observable).  Terms per
-// proof: slots 0..n-1 fixed-base on H_i, n: z*K, n+1: -delta*P, n+2: x*D.
-inline __host__ __device__ int com_nterms(int n) { return n + 3; }
+// proof: slots 0..n-1 fixed-base on H_i, n: z*K, n+1: -delta*P,
+// n+2, n+3: the GLV halves x1*D and x2*phi(D) of x*D (x = x1 + x2 lambda).
+inline __host__ __device__ int com_nterms(int n) { return n + 4; }
 
-__global__ void __launch_bounds__(64) k_rp_com_terms(int B, int n, int k, const int32_t* __restrict__ status,
-                                                     const uint32_t* __restrict__ pts, const uint32_t* __restrict__ sc,
-                                                     const uint32_t* __restrict__ ch, const uint32_t* __restrict__ tables,
-                                                     uint32_t* __restrict__ terms, uint32_t* __restrict__ scratch) {
-  const int nt = com_nterms(n);
+// lane per (proof, item): items 0..n-1: H'_i = y^-i H_i (-> hpj[b][i]);
+// n..2n-1: (z^2 2^(i) y^-i) H_i; 2n: z K; 2n+1: -delta P (-> terms[b][.])
+__global__ void __launch_bounds__(64) k_rp_fixed_exact(int B, int n, int k, const int32_t* __restrict__ status,
+                                                       const uint32_t* __restrict__ sc, const uint32_t* __restrict__ ch,
+                                                       const uint32_t* __restrict__ tables, uint32_t* __restrict__ hpj,
+                                                       uint32_t* __restrict__ terms) {
+  const int ni = 2 * n + 2;
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= B * nt) return;
-  // variable-base slots first in the grid so their long chains start early
-  int b, t;
-  if (gid < B) {
-    b = gid;
-    t = n + 2;
-  } else {
-    b = (gid - B) / (nt - 1);
-    t = (gid - B) % (nt - 1);
-  }
+  if (gid >= B * ni) return;
+  const int b = gid / ni, t = gid % ni;
   if (status[b] != 0) return;
   const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
-  uint32_t* out = terms + ((size_t)b * nt + t) * 24;
-  G1J r;
-  if (t < n) {
-    Fr z2, yinv;
-    load_f(C + CH_Z2 * 8, z2);
+  uint32_t* out;
+  const uint32_t* tab;
+  Scalar sk;
+  if (t < 2 * n) {
+    const int i = t < n ? t : t - n;
+    Fr yinv;
     load_f(C + CH_YINV * 8, yinv);
-    // z^2 2^i y^-i
-    Fr s = fr_mul(z2, fr_pow_small(yinv, (uint32_t)t));
-    for (int q = 0; q < t; q++) s = f_dbl(s);
-    r = fixed_base_mul(tables + (size_t)(n + t) * FB_WORDS_PER_BASE, fr_canon(s));
-  } else if (t == n) {
+    Fr s = fr_pow_small(yinv, (uint32_t)i);
+    if (t >= n) {  // z^2 2^i y^-i
+      Fr z2;
+      load_f(C + CH_Z2 * 8, z2);
+      s = fr_mul(z2, s);
+      for (int q = 0; q < i; q++) s = f_dbl(s);
+    }
+    tab = tables + (size_t)(n + i) * FB_WORDS_PER_BASE;
+    sk = fr_canon(s);
+    out = t < n ? hpj + ((size_t)b * (n + 1) + i) * 24 : terms + ((size_t)b * com_nterms(n) + i) * 24;
+  } else if (t == 2 * n) {
     Fr z;
     load_f(C + CH_Z * 8, z);
-    r = fixed_base_mul(tables + (size_t)tb_K(n) * FB_WORDS_PER_BASE, fr_canon(z));
-  } else if (t == n + 1) {
+    tab = tables + (size_t)tb_K(n) * FB_WORDS_PER_BASE;
+    sk = fr_canon(z);
+    out = terms + ((size_t)b * com_nterms(n) + n) * 24;
+  } else {
     Fr d;
     load_f(sc + ((size_t)b * RP_NSC + RP_SC_DELTA) * 8, d);  // canonical
     Fr nd = f_neg(d);
-    Scalar s;
 #pragma unroll
-    for (int q = 0; q < 8; q++) s.v[q] = nd.v[q];
-    r = fixed_base_mul(tables + (size_t)tb_P(n) * FB_WORDS_PER_BASE, s);
-  } else {
-    Fr x;
-    load_f(C + CH_X * 8, x);
-    r = var_base_mul(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_D) * 16), fr_canon(x),
-                     scratch + (size_t)b * 10 * 24);
+    for (int q = 0; q < 8; q++) sk.v[q] = nd.v[q];
+    tab = tables + (size_t)tb_P(n) * FB_WORDS_PER_BASE;
+    out = terms + ((size_t)b * com_nterms(n) + n + 1) * 24;
   }
+  G1J r = fb_mul(tab, sk);
   store_g1j(out, r);
 }
 
-// one wave per proof: LDS tree over the n + 3 terms, + C, normalise
+// two lanes per proof: the GLV halves of x*D (variable base), on the side stream
+__global__ void __launch_bounds__(64) k_rp_xd(int B, int n, int k, const int32_t* __restrict__ status,
+                                              const uint32_t* __restrict__ pts, const uint32_t* __restrict__ ch,
+                                              uint32_t* __restrict__ terms) {
+  __shared__ uint32_t tab[8 * 24 * 64];
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = gid >> 1, h = gid & 1;
+  if (b >= B || status[b] != 0) return;
+  Fr x;
+  load_f(ch + ((size_t)b * rp_nch(k) + CH_X) * 8, x);
+  const Scalar xs = fr_canon(x);
+  uint32_t k1[4], k2[4], s1, s2;
+  glv_decompose(xs.v, k1, s1, k2, s2);
+  G1A D = load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_D) * 16);
+  if (h) D.x = fp_mul(D.x, glv_beta());  // phi(D)
+  if (h ? s2 : s1) D = g1a_neg(D);
+  G1J r = vb128(D, h ? k2 : k1, tab, threadIdx.x);
+  store_g1j(terms + ((size_t)b * com_nterms(n) + n + 2 + h) * 24, r);
+}
+
+// one wave per proof: LDS tree over the n + 4 terms, + C -> hpj[b][n] (Jacobian)
 __global__ void __launch_bounds__(64) k_rp_com_sum(int B, int n, int k, const int32_t* __restrict__ status,
-                                                   uint32_t* __restrict__ pts, const uint32_t* __restrict__ terms,
-                                                   uint32_t* __restrict__ com, uint8_t* __restrict__ com_be) {
+                                                   const uint32_t* __restrict__ pts, const uint32_t* __restrict__ terms,
+                                                   uint32_t* __restrict__ hpj) {
   __shared__ uint32_t sh[64 * 24];
   const int b = blockIdx.x, t = threadIdx.x;
   if (status[b] != 0) return;  // uniform per block
   const int nt = com_nterms(n);
   const uint32_t* T = terms + (size_t)b * nt * 24;
-  uint32_t* Pt = pts + (size_t)b * rp_npts(k) * 16;
+  const uint32_t* Pt = pts + (size_t)b * rp_npts(k) * 16;
   G1J acc = g1j_identity();
-  for (int q = t; q < nt; q += 64) acc = nl_add_mem(acc, T + q * 24, 0);
-  if (t == 0) acc = nl_madd_mem(acc, Pt + RP_PT_C * 16, 0);  // + C
+  for (int q = t; q < nt; q += 64) add_inl(acc, load_g1j(T + q * 24));
+  if (t == 0) add_inl(acc, g1j_from_affine(load_g1a(Pt + RP_PT_C * 16)));  // + C
   store_g1j(sh + t * 24, acc);
   __syncthreads();
   for (int half = 32; half >= 1; half >>= 1) {
-    if (t < half) acc = nl_add_mem(acc, sh + (t + half) * 24, 0);
+    if (t < half) add_inl(acc, load_g1j(sh + (t + half) * 24));
     __syncthreads();
     if (t < half) store_g1j(sh + t * 24, acc);
     __syncthreads();
   }
-  if (t == 0) {
-    G1A ca = nl_to_affine(acc);
-    store_g1a(com + (size_t)b * 16, ca);
-    // C is consumed: the slot now holds -com for the RLC MSM (scalar rho')
-    store_g1a(Pt + RP_PT_C * 16, g1a_neg(ca));
-    store_point_be(com_be + (size_t)b * 64, ca);
+  if (t == 0) store_g1j(hpj + ((size_t)b * (n + 1) + n) * 24, acc);
+}
+
+// Batch affine normalisation, block of 256 lanes = 256 consecutive points
+// ([B][per] Jacobian, points of proofs with status != 0 are skipped): prefix
+// and suffix products of the z's in LDS, ONE inversion per block, then
+// z_i^-1 = inv * prefix_{i-1} * suffix_{i+1}.  Writes affine Montgomery
+// (aff, 16 words) and the canonical 64-byte BE encoding (be).
+__global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, const int32_t* __restrict__ status,
+                                                          const uint32_t* __restrict__ jac, uint32_t* __restrict__ aff,
+                                                          uint8_t* __restrict__ be) {
+  __shared__ uint32_t pre[NORM_BS * 8], suf[NORM_BS * 8];
+  __shared__ uint32_t invs[8];
+  const int t = threadIdx.x;
+  const int g = blockIdx.x * NORM_BS + t;
+  const bool live = g < total && (!status || status[g / per] == 0);
+  G1J p;
+  Fp z = f_one<FpP>();
+  if (live) {
+    p = load_g1j(jac + (size_t)g * 24);
+    if (!f_is_zero(p.z)) z = p.z;
   }
+  store_fp(pre + t * 8, z);
+  store_fp(suf + t * 8, z);
+  __syncthreads();
+  // inclusive scans (Hillis-Steele): pre_t = z_0..z_t, suf_t = z_t..z_255
+  Fp a = z, c = z;
+  for (int off = 1; off < NORM_BS; off <<= 1) {
+    Fp o1, o2;
+    const bool h1 = t >= off, h2 = t + off < NORM_BS;
+    if (h1) load_fp(pre + (t - off) * 8, o1);
+    if (h2) load_fp(suf + (t + off) * 8, o2);
+    __syncthreads();
+    if (h1) {
+      a = fp_mul(a, o1);
+      store_fp(pre + t * 8, a);
+    }
+    if (h2) {
+      c = fp_mul(c, o2);
+      store_fp(suf + t * 8, c);
+    }
+    __syncthreads();
+  }
+  if (t == 0) store_fp(invs, nl_fp_inv(c));  // suf_0 = product of all
+  __syncthreads();
+  if (!live) return;
+  const bool ident = f_is_zero(p.z);
+  G1A r;
+  if (ident) {
+    r.x = f_zero<FpP>();
+    r.y = f_zero<FpP>();
+  } else {
+    Fp zi;
+    load_fp(invs, zi);
+    Fp o;
+    if (t > 0) {
+      load_fp(pre + (t - 1) * 8, o);
+      zi = fp_mul(zi, o);
+    }
+    if (t + 1 < NORM_BS) {
+      load_fp(suf + (t + 1) * 8, o);
+      zi = fp_mul(zi, o);
+    }
+    Fp zi2 = fp_sqr(zi);
+    r.x = fp_mul(p.x, zi2);
+    r.y = fp_mul(fp_mul(p.y, zi2), zi);
+  }
+  store_g1a(aff + (size_t)g * 16, r);
+  if (be) store_point_be(be + (size_t)g * 64, r);
 }
 
 // --------------------------------------------------------- x0 transcript
 // thread per (proof, record r in [0, 2n+2]); record 2n+2 writes DER framing
 __global__ void __launch_bounds__(256) k_rp_x0_build(int B, int n, const int32_t* __restrict__ status,
-                                                     const uint8_t* __restrict__ hp_be, const uint8_t* __restrict__ com_be,
+                                                     const uint8_t* __restrict__ hp_be,
                                                      const uint8_t* __restrict__ x0_const, const uint32_t* __restrict__ sc,
                                                      uint8_t* __restrict__ msgs) {
   const int nrec = 2 * n + 3;
@@ -342,7 +384,7 @@ __global__ void __launch_bounds__(256) k_rp_x0_build(int B, int n, const int32_t
   const uint32_t A = x0_array_len(n);
   if (r < n) {
     uint32_t pw[16];
-    load_be_words(hp_be + ((size_t)b * n + r) * 64, pw);
+    load_be_words(hp_be + ((size_t)b * (n + 1) + r) * 64, pw);
     put_hex_record(m, 8 + 130u * r, pw, true);
   } else if (r < 2 * n + 1) {
     const uint16_t* src = reinterpret_cast<const uint16_t*>(x0_const + 130u * (r - n));
@@ -350,7 +392,7 @@ __global__ void __launch_bounds__(256) k_rp_x0_build(int B, int n, const int32_t
     for (int q = 0; q < 65; q++) dst[q] = src[q];
   } else if (r == 2 * n + 1) {
     uint32_t pw[16];
-    load_be_words(com_be + (size_t)b * 64, pw);
+    load_be_words(hp_be + ((size_t)b * (n + 1) + n) * 64, pw);
     put_hex_record(m, 8 + 130u * r, pw, false);
   } else {
     uint16_t* m16 = reinterpret_cast<uint16_t*>(m);
@@ -448,7 +490,7 @@ __global__ void __launch_bounds__(64) k_rp_terms_fixed(int B, int n, int k, cons
       base = tb_Q(n);
     }
   }
-  G1J r = fixed_base_mul(tables + (size_t)base * FB_WORDS_PER_BASE, fr_canon(s));
+  G1J r = nl_fb_mul(tables + (size_t)base * FB_WORDS_PER_BASE, fr_canon(s));
   store_g1j(terms + ((size_t)b * rp_nterms(n, k) + slot) * 24, r);
 }
 
@@ -496,7 +538,7 @@ __global__ void __launch_bounds__(64) k_rp_terms_var(int B, int n, int k, const 
 // ------------------------------------------------------------------ check
 __global__ void __launch_bounds__(64) k_rp_check(int B, int n, int k, int32_t* __restrict__ status,
                                                  const int32_t* __restrict__ ipa_flag,
-                                                 const uint32_t* __restrict__ terms, const uint32_t* __restrict__ com) {
+                                                 const uint32_t* __restrict__ terms, const uint32_t* __restrict__ hpa) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B || status[b] != 0) return;
   const uint32_t* T = terms + (size_t)b * rp_nterms(n, k) * 24;
@@ -510,7 +552,7 @@ __global__ void __launch_bounds__(64) k_rp_check(int B, int n, int k, int32_t* _
     status[b] = ipa_flag[b];
     return;
   }
-  G1J e2 = g1j_from_affine(g1a_neg(load_g1a(com + (size_t)b * 16)));
+  G1J e2 = g1j_from_affine(g1a_neg(load_g1a(hpa + ((size_t)b * (n + 1) + n) * 16)));
   for (int t = 5; t < rp_nterms(n, k); t++) e2 = nl_add_mem(e2, T + t * 24, 0);
   status[b] = g1j_is_identity(e2) ? FTS_OK : FTS_E_IPA_INVALID;
 }
@@ -518,7 +560,9 @@ __global__ void __launch_bounds__(64) k_rp_check(int B, int n, int k, int32_t* _
 // ------------------------------------------------------------ RLC batch check
 // Sum_p rho_p E1_p + rho'_p E2_p == O  (SURVEY Appendix B).  Fixed bases get
 // batch-summed scalars (column reduction), variable points go to one MSM.
-// coef per proof (Montgomery Fr): [rho(ip - polEval), rho tau, rho'(ab - ip)x0, rho' a, rho' b]
+// coef per proof (Montgomery Fr): [rho(ip - polEval), rho tau, rho'(ab - ip), rho' a, rho' b]
+// (column Q is rho'(ab - ip) x0: x0 is applied by k_rlc_columns, so the MSM
+// side does not wait for the x0 transcript)
 constexpr int RLC_NCOEF = 5;
 
 // full-width weight: 256 random bits reduced mod r (Montgomery form).  Full
@@ -534,10 +578,13 @@ FTS_DEV Fr fr_from_u256(const uint32_t w[8]) {
 __global__ void __launch_bounds__(64) k_rlc_prep(int B, int n, int k, const int32_t* __restrict__ status,
                                                  const int32_t* __restrict__ ipa_flag, const uint32_t* __restrict__ sc,
                                                  const uint32_t* __restrict__ ch, const uint32_t* __restrict__ key,
+                                                 const uint32_t* __restrict__ hpa, uint32_t* __restrict__ pts,
                                                  uint32_t* __restrict__ msc, uint32_t* __restrict__ coef) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const int npts = rp_npts(k);
+  // C is consumed by com: the slot now holds -com for the MSM (scalar rho')
+  if (status[b] == 0) store_g1a(pts + ((size_t)b * npts + RP_PT_C) * 16, g1a_neg(load_g1a(hpa + ((size_t)b * (n + 1) + n) * 16)));
   uint32_t* M = msc + (size_t)b * npts * 8;
   uint32_t* K = coef + (size_t)b * RLC_NCOEF * 8;
   const bool e1 = status[b] == 0;
@@ -566,8 +613,7 @@ __global__ void __launch_bounds__(64) k_rlc_prep(int B, int n, int k, const int3
   store_f(K + 0 * 8, fr_mul(rho, f_sub(ip, pol)));
   store_f(K + 1 * 8, fr_mul(rho, fr_from_canon(S + RP_SC_TAU * 8)));
   if (!e2) return;
-  Fr a = fr_from_canon(S + RP_SC_A * 8), bb = fr_from_canon(S + RP_SC_B * 8), x0;
-  load_f(C + CH_X0 * 8, x0);
+  Fr a = fr_from_canon(S + RP_SC_A * 8), bb = fr_from_canon(S + RP_SC_B * 8);
   store_f(M + RP_PT_C * 8, f_from_mont(rho2));  // slot C holds -com: scalar +rho' 
   for (int j = 0; j < k; j++) {
     Fr xj, xji;
@@ -576,7 +622,7 @@ __global__ void __launch_bounds__(64) k_rlc_prep(int B, int n, int k, const int3
     put(RP_PT_L + j, fr_mul(rho2, fr_sqr(xj)));
     put(RP_PT_L + k + j, fr_mul(rho2, fr_sqr(xji)));
   }
-  store_f(K + 2 * 8, fr_mul(rho2, fr_mul(f_sub(fr_mul(a, bb), ip), x0)));
+  store_f(K + 2 * 8, fr_mul(rho2, f_sub(fr_mul(a, bb), ip)));
   store_f(K + 3 * 8, fr_mul(rho2, a));
   store_f(K + 4 * 8, fr_mul(rho2, bb));
 }
@@ -593,6 +639,11 @@ __global__ void __launch_bounds__(256) k_rlc_columns(int B, int n, int k, const 
     Fr v;
     if (col < 3) {
       load_f(K + col * 8, v);
+      if (col == 2 && !f_is_zero(v)) {
+        Fr x0;
+        load_f(C + CH_X0 * 8, x0);
+        v = fr_mul(v, x0);
+      }
     } else if (col < 3 + n) {
       Fr ra;
       load_f(K + 3 * 8, ra);
@@ -633,7 +684,7 @@ __global__ void __launch_bounds__(64) k_rlc_fixed(int n, const uint32_t* __restr
   Scalar s;
 #pragma unroll
   for (int q = 0; q < 8; q++) s.v[q] = colsum[col * 8 + q];
-  store_g1j(out + (size_t)col * 24, fixed_base_mul(tables + (size_t)base * FB_WORDS_PER_BASE, s));
+  store_g1j(out + (size_t)col * 24, nl_fb_mul(tables + (size_t)base * FB_WORDS_PER_BASE, s));
 }
 
 // batch verdict: flag = 1 if the combination is the identity; on success the
@@ -661,59 +712,81 @@ __global__ void __launch_bounds__(64) k_rlc_finalize(int B, const uint32_t* __re
 size_t rp_scratch_words(int B, int n, int k) { return (size_t)B * (3 + 2 * k) * 10 * 24; }
 size_t rp_terms_words(int B, int n, int k) { return (size_t)B * rp_nterms(n, k) * 24; }
 
+size_t fb_words_per_base() { return FB_WORDS_PER_BASE; }
+size_t table_build_scratch_bytes(int nb) {
+  const size_t nbw = (size_t)nb * FB_NW;
+  return nbw * 24 * 4 + nbw * (FB_S + FB_L) * 24 * 4 + nbw * FB_E * 24 * 4;
+}
+// tables: nb * FB_WORDS_PER_BASE words; scratch: table_build_scratch_bytes(nb)
 void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s) {
-  FTS_LAUNCH(k_build_tables, nb * FB_WINDOWS, 64, s, bases, nb, tables, scratch);
+  const size_t nbw = (size_t)nb * FB_NW;
+  uint32_t* bw = scratch;
+  uint32_t* small = bw + nbw * 24;
+  uint32_t* large = small + nbw * FB_S * 24;
+  uint32_t* jac = large + nbw * FB_L * 24;
+  FTS_LAUNCH(kt_window_bases, nbw, 64, s, bases, nb, bw);
+  FTS_LAUNCH(kt_small_large, nbw, 64, s, nb, bw, small, large);
+  FTS_LAUNCH(kt_entries, nbw * FB_E, 64, s, nb, small, large, jac);
+  const size_t tot = nbw * FB_E;
+  FTS_LAUNCH(k_rp_normalize, tot, NORM_BS, s, (int)tot, 1, (const int32_t*)nullptr, jac, tables, (uint8_t*)nullptr);
 }
 
 void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
-                uint32_t* scratch, hipStream_t s, Timeline* tl);
+                uint32_t* scratch, hipStream_t s, hipStream_t s_extra, Timeline* tl);
 
-// exact per-proof phase: everything that is hashed (challenges, H'_i, com, x0)
-void launch_rp_exact(const RpBatchDev& d, const uint32_t* tables, const uint8_t* x0_const, hipStream_t s,
-                     Timeline* tl) {
+// Whole range-proof pipeline up to the batch verdict (flag): exact per-proof
+// phase (everything that is hashed: challenges, H'_i, com, x0) and the
+// random-linear-combination check of all final equations (one MSM).
+// s = main stream, s2 = side stream.
+void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const uint8_t* x0_const,
+                     hipStream_t s, hipStream_t s2, Timeline* tl) {
   const int B = d.B, n = d.n, k = d.k;
+  if (!B) return;
   FTS_LAUNCH(k_rp_decode, B * rp_npts(k), 256, s, B, rp_npts(k), d.raw, d.pts, d.status);
-  if (tl) tl->mark("k_rp_decode", s);
+  tl->mark("k_rp_decode", s, 0);
   FTS_LAUNCH(k_rp_hash_small, B * (2 + k), 64, s, B, n, k, d.raw, d.status, d.ch, d.small_msgs);
-  if (tl) tl->mark("k_rp_hash_small", s);
+  tl->mark("k_rp_hash_small", s, 0);
   FTS_LAUNCH(k_rp_chal_fr, B, 64, s, B, n, k, d.status, d.ch, d.scratch);
-  if (tl) tl->mark("k_rp_chal_fr", s);
-  FTS_LAUNCH(k_rp_hprime, B * n, 64, s, B, n, k, d.status, d.ch, tables, d.hpj);
-  if (tl) tl->mark("k_rp_hprime", s);
-  FTS_LAUNCH(k_rp_hp_normalize, B, 64, s, B, n, d.status, d.hpj, d.hpa, d.hp_be);
-  if (tl) tl->mark("k_rp_hp_normalize", s);
-  FTS_LAUNCH(k_rp_com_terms, B * com_nterms(n), 64, s, B, n, k, d.status, d.pts, d.sc, d.ch, tables, d.terms,
-             d.scratch);
-  if (tl) tl->mark("k_rp_com_terms", s);
-  if (B) hipLaunchKernelGGL(k_rp_com_sum, dim3(B), dim3(64), 0, s, B, n, k, d.status, d.pts, d.terms, d.com, d.com_be);
-  if (tl) tl->mark("k_rp_com_sum", s);
-  FTS_LAUNCH(k_rp_x0_build, B * (2 * n + 3), 256, s, B, n, d.status, d.hp_be, d.com_be, x0_const, d.sc, d.x0_msgs);
-  if (tl) tl->mark("k_rp_x0_build", s);
-  FTS_LAUNCH(k_rp_x0_hash, B, 64, s, B, n, k, d.status, d.x0_msgs, d.ch);
-  if (tl) tl->mark("k_rp_x0_hash", s);
-}
-
-// random-linear-combination check of all final equations (one MSM)
-void launch_rp_rlc(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, hipStream_t s, Timeline* tl) {
-  const int B = d.B, n = d.n, k = d.k;
-  FTS_LAUNCH(k_rlc_prep, B, 64, s, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, r.key, r.msc, r.coef);
-  hipLaunchKernelGGL(k_rlc_columns, dim3(3 + 2 * n), dim3(256), 0, s, B, n, k, d.ch, r.coef, r.colsum);
-  FTS_LAUNCH(k_rlc_fixed, 3 + 2 * n, 64, s, n, r.colsum, tables, r.fixed);
-  if (tl) tl->mark("k_rlc_scalars", s);
-  launch_msm(r.plan, d.pts, r.msc, r.fixed, 3 + 2 * n, r.msm_scratch, s, tl);
-  FTS_LAUNCH(k_rlc_finalize, B > 0 ? B : 1, 64, s, B, r.plan.out, d.status, d.ipa_flag, r.flag);
-  if (tl) tl->mark("k_rlc_finalize", s);
+  tl->mark("k_rp_chal_fr", s, (double)B * (3 * k + 4 * (k + 1) + 12));
+  // side: x*D while the main stream runs the fixed-base products
+  tl->fork(s, s2);
+  FTS_LAUNCH(k_rp_xd, 2 * B, 64, s2, B, n, k, d.status, d.pts, d.ch, d.terms);
+  tl->mark("k_rp_xd", s2, (double)B * 2 * COST_VB128);
+  FTS_LAUNCH(k_rp_fixed_exact, B * (2 * n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, tables, d.hpj, d.terms);
+  tl->mark("k_rp_fixed_exact", s, (double)B * (2 * n + 2) * COST_FB);
+  tl->fork(s2, s);
+  hipLaunchKernelGGL(k_rp_com_sum, dim3(B), dim3(64), 0, s, B, n, k, d.status, d.pts, d.terms, d.hpj);
+  tl->mark("k_rp_com_sum", s, (double)B * (com_nterms(n) + 1) * COST_ADD);
+  const int npt = B * (n + 1);
+  FTS_LAUNCH(k_rp_normalize, npt, NORM_BS, s, npt, n + 1, d.status, d.hpj, d.hpa, d.hp_be);
+  tl->mark("k_rp_normalize", s, (double)npt * (2 * 8.0 / 1.0 + 6.0));
+  // side: x0 transcript + hash, then the fixed-base columns (need x0)
+  tl->fork(s, s2);
+  FTS_LAUNCH(k_rp_x0_build, B * (2 * n + 3), 256, s2, B, n, d.status, d.hp_be, x0_const, d.sc, d.x0_msgs);
+  tl->mark("k_rp_x0_build", s2, 0);
+  FTS_LAUNCH(k_rp_x0_hash, B, 64, s2, B, n, k, d.status, d.x0_msgs, d.ch);
+  tl->mark("k_rp_x0_hash", s2, 0);
+  // main: variable points of the batch equation -> MSM
+  FTS_LAUNCH(k_rlc_prep, B, 64, s, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, r.key, d.hpa, d.pts, r.msc, r.coef);
+  tl->mark("k_rlc_prep", s, (double)B * (3 * k + 30));
+  hipLaunchKernelGGL(k_rlc_columns, dim3(3 + 2 * n), dim3(256), 0, s2, B, n, k, d.ch, r.coef, r.colsum);
+  tl->mark("k_rlc_columns", s2, (double)B * 2 * n * (k + 2));
+  FTS_LAUNCH(k_rlc_fixed, 3 + 2 * n, 64, s2, n, r.colsum, tables, r.fixed);
+  tl->mark("k_rlc_fixed", s2, (double)(3 + 2 * n) * COST_FB);
+  launch_msm(r.plan, d.pts, r.msc, r.fixed, 3 + 2 * n, r.msm_scratch, s, s2, tl);
+  FTS_LAUNCH(k_rlc_finalize, B, 64, s, B, r.plan.out, d.status, d.ipa_flag, r.flag);
+  tl->mark("k_rlc_finalize", s, 0);
 }
 
 // per-proof final equations (fallback when the batch combination fails)
 void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, hipStream_t s, Timeline* tl) {
   const int B = d.B, n = d.n, k = d.k;
   FTS_LAUNCH(k_rp_terms_fixed, B * (3 + 2 * n), 64, s, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, tables, d.terms);
-  if (tl) tl->mark("k_rp_terms_fixed", s);
+  tl->mark("k_rp_terms_fixed", s, (double)B * (3 + 2 * n) * COST_FB);
   FTS_LAUNCH(k_rp_terms_var, B * (3 + 2 * k), 64, s, B, n, k, d.status, d.ipa_flag, d.pts, d.ch, d.terms, d.scratch);
-  if (tl) tl->mark("k_rp_terms_var", s);
-  FTS_LAUNCH(k_rp_check, B, 64, s, B, n, k, d.status, d.ipa_flag, d.terms, d.com);
-  if (tl) tl->mark("k_rp_check", s);
+  tl->mark("k_rp_terms_var", s, (double)B * (3 + 2 * k) * COST_VB4);
+  FTS_LAUNCH(k_rp_check, B, 64, s, B, n, k, d.status, d.ipa_flag, d.terms, d.hpa);
+  tl->mark("k_rp_check", s, (double)B * rp_nterms(n, k) * COST_ADD);
 }
 
 }  // namespace fts

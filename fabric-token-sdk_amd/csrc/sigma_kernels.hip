@@ -9,6 +9,7 @@
 //                                  com (sametype.go:169-171), exact affine, hex transcript,
 //                                  SHA-256, Zr.Equals against the proof's challenge
 #include "device/g1.hpp"
+#include "device/fixed_base.hpp"
 #include "device/helpers.hpp"
 #include "device/rp_kernels.hpp"
 #include "device/sigma.hpp"
@@ -93,25 +94,25 @@ __global__ void __launch_bounds__(64) k_sig_terms(int nwork, const int2* __restr
     if (t < 2 * N) {
       int i = t >> 1;
       if ((t & 1) == 0) {  // iv_i ped1 + ibf_i ped2
-        r = fixed_base_mul(t_ped1, canon(S + (TAS_SC_IV + i) * 8));
-        r = add_via(tmp, r, fixed_base_mul(t_ped2, canon(S + (TAS_SC_IV + N + i) * 8)));
+        r = nl_fb_mul(t_ped1, canon(S + (TAS_SC_IV + i) * 8));
+        r = add_via(tmp, r, nl_fb_mul(t_ped2, canon(S + (TAS_SC_IV + N + i) * 8)));
       } else {  // c in'_i
         r = var_base_mul(load_g1a(F + i * 16), chal, scr);
       }
     } else if (t == 2 * N) {  // EqualityOfSum ped2
-      r = fixed_base_mul(t_ped2, canon(S + TAS_SC_EQ * 8));
+      r = nl_fb_mul(t_ped2, canon(S + TAS_SC_EQ * 8));
     } else if (t == 2 * N + 1) {  // c sum
       r = var_base_mul(load_g1a(F + (N + ac.n_out) * 16), chal, scr);
     } else if (t == 2 * N + 2) {  // Type ped0 + TBF ped2
-      r = fixed_base_mul(t_ped0, canon(S + TAS_SC_TYPE * 8));
-      r = add_via(tmp, r, fixed_base_mul(t_ped2, canon(S + TAS_SC_TBF * 8)));
+      r = nl_fb_mul(t_ped0, canon(S + TAS_SC_TYPE * 8));
+      r = add_via(tmp, r, nl_fb_mul(t_ped2, canon(S + TAS_SC_TBF * 8)));
     } else {  // c CT
       r = var_base_mul(load_g1a(pts + (size_t)ac.pt_off * 16), chal, scr);
     }
   } else {
     if (t == 0) {  // Type ped0 + BF ped2
-      r = fixed_base_mul(t_ped0, canon(S + ST_SC_TYPE * 8));
-      r = add_via(tmp, r, fixed_base_mul(t_ped2, canon(S + ST_SC_BF * 8)));
+      r = nl_fb_mul(t_ped0, canon(S + ST_SC_TYPE * 8));
+      r = add_via(tmp, r, nl_fb_mul(t_ped2, canon(S + ST_SC_BF * 8)));
     } else {  // c CT
       r = var_base_mul(load_g1a(pts + (size_t)ac.pt_off * 16), canon(S + ST_SC_CHAL * 8), scr);
     }

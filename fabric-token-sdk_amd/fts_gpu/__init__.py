@@ -157,10 +157,21 @@ class PublicParams:
         return StagedRangeBatch(self, proofs, commitments)
 
     def last_timings(self):
+        """{kernel: ms} of the last range-proof run (device time per launch class)"""
+        return {name: ms for name, (ms, _) in self.last_timings_ex().items()}
+
+    def last_timings_ex(self):
+        """{kernel: (ms, algorithmic u32 MADs)} of the last range-proof run"""
         names = (C.c_char_p * 64)()
         ms = (C.c_float * 64)()
-        m = L.lib.fts_last_timings(self._ctx, names, ms, 64)
-        return {names[i].decode(): ms[i] for i in range(m)}
+        mads = (C.c_double * 64)()
+        m = L.lib.fts_last_timings_ex(self._ctx, names, ms, mads, 64)
+        out = {}
+        for i in range(m):
+            k = names[i].decode()
+            o = out.get(k, (0.0, 0.0))
+            out[k] = (o[0] + ms[i], o[1] + mads[i])
+        return out
 
     # ------------------------------------------------------------- prove
     def token_commit(self, ttype, value, bf32):

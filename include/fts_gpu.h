@@ -124,6 +124,9 @@ int fts_rp_batch_verify(fts_ctx* ctx, fts_rp_batch* b, int32_t* status);
 void fts_rp_batch_free(fts_rp_batch* b);
 /* device time of the last fts_rp_batch_verify, per kernel class (ms); returns count filled */
 int fts_last_timings(const fts_ctx* ctx, const char** names, float* ms, int cap);
+/* same, plus the algorithmic u32 MAD count of each launch (DESIGN.md cost model; 0 for
+ * kernels without field products, e.g. SHA-256) */
+int fts_last_timings_ex(const fts_ctx* ctx, const char** names, float* ms, double* mads, int cap);
 
 /* parity/debug hook: exact intermediates of proof i of the last range-proof run
  * (ch_out: (8+2k) x 32-byte BE Fr [x, x^2, y, y^-1, z, z^2, polEval, x0, x_j..., x_j^-1...],

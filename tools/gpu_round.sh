@@ -1,10 +1,39 @@
 #!/bin/bash
-# one GPU session: smoke, bench, rocprof kernel-trace stats (run from the repo root)
+# One GPU session (run from the repo root on the gpurun box):
+#   smoke -> [pytest -m gpu] -> bench -> INT-peak microbench -> rocprofv3
+#   kernel-trace stats (CSV) -> PMC passes (one counter group per run).
+# Every GPU step has its own time limit; the first failure ends the script.
+# Env: STEPS (bench steps), TESTS=1 (run pytest -m gpu), PMC=0 (skip counters),
+#      TAG (suffix of the output directory names).
 set -o pipefail
-mkdir -p gpurun_out/prof
+TAG=${TAG:-r01}
+OUT=gpurun_out
+mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo SMOKE FAILED; cat gpurun_out/smoke.log; exit 1; }
-timeout -k 10 300 python3 -u bench.py --steps ${STEPS:-10} --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo BENCH FAILED; tail -20 gpurun_out/bench.err; exit 1; }
-cat gpurun_out/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --cpu-sample 0 > gpurun_out/prof.log 2>&1 || { echo PROF FAILED; tail -20 gpurun_out/prof.log; exit 1; }
-find gpurun_out/prof -name "*stats*" | head
+step() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  echo "== $name"
+  timeout -k 10 "$lim" "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  if [ $rc -ne 0 ]; then echo "$name FAILED rc=$rc"; tail -30 $OUT/$name.log; exit 1; fi
+}
+step smoke 240 python3 -c "import __graft_entry__ as g; g.smoke()"
+if [ "${TESTS:-0}" = 1 ]; then
+  step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+  tail -3 $OUT/pytest_gpu.log
+fi
+step bench 400 python3 -u bench.py --steps ${STEPS:-20} --warmup 3
+grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json
+cat $OUT/bench.json
+step int_peak 120 fabric-token-sdk_amd/lib/int_peak
+cat $OUT/int_peak.log
+rm -rf $OUT/prof_$TAG
+step rocprof 300 rocprofv3 --kernel-trace --stats -T -f csv -d $OUT/prof_$TAG -o run -- python3 bench.py --steps 5 --warmup 1 --cpu-sample 0
+find $OUT/prof_$TAG -name "*kernel_stats.csv" | head -3
+if [ "${PMC:-1}" = 1 ]; then
+  # separate passes (TCC: FETCH_SIZE uses 3 slots, WRITE_SIZE 2)
+  step pmc_fetch 90 rocprofv3 --pmc FETCH_SIZE -T -f csv -d $OUT/pmc_fetch_$TAG -o run -- python3 bench.py --steps 1 --warmup 1 --cpu-sample 0
+  step pmc_write 90 rocprofv3 --pmc WRITE_SIZE -T -f csv -d $OUT/pmc_write_$TAG -o run -- python3 bench.py --steps 1 --warmup 1 --cpu-sample 0
+  step pmc_valu 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE -T -f csv -d $OUT/pmc_valu_$TAG -o run -- python3 bench.py --steps 1 --warmup 1 --cpu-sample 0
+fi
+echo "== done"
