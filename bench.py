@@ -16,6 +16,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -26,6 +27,7 @@ sys.path.insert(0, os.path.join(ROOT, "fabric-token-sdk_amd"))
 # 256 CU x 4 SIMD x 32 lanes / 4 x 2.4 GHz (MI355X_MICROARCH.md chip table);
 # tools' int_peak microbenchmark measures >= 88 % of it with the Fp product.
 PEAK_TMAD = 256 * 4 * 32 / 4 * 2.4e9 / 1e12
+R_ORDER = 21888242871839275222246405745257275088548364400416034343698204186575808495617
 MAD_PER_MUL = 136          # 8x32-bit no-carry CIOS / FIPS Montgomery product
 SURVEY_MAD_PER_RP64 = 8.13e6   # SURVEY §8(d) fixed cost model per rp64 verify
 
@@ -37,6 +39,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--bits", type=int, default=64)
+    ap.add_argument("--lanes", type=int, default=int(os.environ.get("FTS_LANES", "3")),
+                    help="batches in flight (host threads / device lanes; FTS_LANES)")
     ap.add_argument("--cpu-sample", type=int, default=256, help="CPU baseline chunk size (0: skip the CPU baseline)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall-time bound of the CPU baseline sample")
@@ -61,42 +65,61 @@ def main():
         pp_raw = f.read()
     pp = fts_gpu.PublicParams(pp_raw, bit_length=args.bits, device=local)
     n, k, B = pp.bit_length, pp.rounds, args.batch
-    rng = random.Random(0xF7A50002 + rank)
-    vals = [rng.getrandbits(n) for _ in range(B)]
-    bfs = [rng.randrange(21888242871839275222246405745257275088548364400416034343698204186575808495617)
-           .to_bytes(32, "big") for _ in range(B)]
+    # one staged batch per lane (distinct proofs); lanes run concurrently
+    lanes = max(1, args.lanes)
     t0 = time.time()
-    proofs, coms = pp.prove_range_batch(vals, bfs, seed=0xF7A50002 + 1000003 * rank)
+    batches, proofs0, coms0 = [], None, None
+    for ln in range(lanes):
+        rng = random.Random(0xF7A50002 + 7919 * rank + 104729 * ln)
+        vals = [rng.getrandbits(n) for _ in range(B)]
+        bfs = [rng.randrange(R_ORDER).to_bytes(32, "big") for _ in range(B)]
+        proofs, coms = pp.prove_range_batch(vals, bfs, seed=0xF7A50002 + 1000003 * rank + 7777 * ln)
+        if ln == 0:
+            proofs0, coms0 = proofs, coms
+        batches.append(pp.stage_range_proofs(proofs, coms))
     prove_s = time.time() - t0
-    batch = pp.stage_range_proofs(proofs, coms)
 
-    def step():
-        st = batch.verify(want_status=True)
+    def run(ln, nsteps, sink):
+        for _ in range(nsteps):
+            st = batches[ln].verify(want_status=True)
+            sink.append((st, batches[ln].timings()))
+
+    def pipelined(nsteps):
+        """nsteps batch verifications spread over the lanes (one host thread
+        per lane); for N > 1 every step's verdict bitmap is all-gathered."""
+        per = [nsteps // lanes + (1 if i < nsteps % lanes else 0) for i in range(lanes)]
+        sinks = [[] for _ in range(lanes)]
+        th = [threading.Thread(target=run, args=(i, per[i], sinks[i])) for i in range(lanes)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        res = [x for s in sinks for x in s]
         if dist is not None:
             import torch
-            bits = torch.from_numpy(np.packbits(st == 0)).cuda()
-            out = torch.empty(world * bits.numel(), dtype=torch.uint8, device="cuda")
-            dist.all_gather_into_tensor(out, bits)
-        return st
+            for st, _ in res:
+                bits = torch.from_numpy(np.packbits(st == 0)).cuda()
+                out = torch.empty(world * bits.numel(), dtype=torch.uint8, device="cuda")
+                dist.all_gather_into_tensor(out, bits)
+        return res
 
-    for _ in range(args.warmup):
-        st = step()
-    ok = int((st == 0).sum())
+    pipelined(max(args.warmup, lanes))
     if dist is not None:
         import torch
         dist.barrier()
         torch.cuda.synchronize()
-    kt = {}
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        for name, (ms, mads) in pp.last_timings_ex().items():
-            o = kt.get(name, (0.0, 0.0))
-            kt[name] = (o[0] + ms, mads)
+    res = pipelined(args.steps)
     if dist is not None:
         torch.cuda.synchronize()
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ok = int(sum(int((st == 0).sum()) for st, _ in res))  # verdicts of the timed steps
+    kt = {}
+    for _, tm in res:
+        for name, (ms, mads) in tm.items():
+            o = kt.get(name, (0.0, 0.0))
+            kt[name] = (o[0] + ms, mads)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -134,7 +157,7 @@ def main():
         while cs < args.cpu_seconds and done < B:
             m = min(chunk, B - done)
             t0 = time.perf_counter()
-            res = cref.rp_verify_many(opp, coms[done:done + m], proofs[done:done + m], threads=thr)
+            res = cref.rp_verify_many(opp, coms0[done:done + m], proofs0[done:done + m], threads=thr)
             cs += time.perf_counter() - t0
             assert all(r == 0 for r in res), res
             done += m
@@ -160,6 +183,8 @@ def main():
                                    "(exact transcripts per proof + RLC batch check via one Pippenger MSM)" % (B, n),
                        "batch_per_gpu": B, "bit_length": n, "rounds": k, "parallelism": "shard%d" % world},
             "accepted": ok,
+            "verified": world * B * args.steps,
+            "lanes": lanes,
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernel_ms": {kname: round(v, 4) for kname, v in avg.items()},

@@ -11,6 +11,7 @@
 #include <string.h>
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -101,29 +102,73 @@ struct Workspace {
 
 }  // namespace
 
+// One execution lane: a main + side stream pair with its own workspace and
+// timeline.  Independent batches submitted concurrently (e.g. by the Go shim's
+// aggregation goroutines, or bench.py's pipeline) run on different lanes, so
+// one batch's latency-bound phases (transcript hashing, doubling chains)
+// overlap another batch's throughput-bound kernels.
+struct Lane {
+  int id = 0;
+  hipStream_t s = nullptr, s2 = nullptr;
+  Workspace ws;
+  Timeline tl;
+};
+
 struct fts_ctx {
   int device = 0;
-  hipStream_t stream = nullptr, stream2 = nullptr;
   PublicParams pp;
   int n = 0, k = 0;
   uint32_t* d_tables = nullptr;
   uint8_t* d_x0const = nullptr;
   size_t table_bytes = 0;
+  // lane pool
+  std::vector<Lane*> lanes;
+  std::vector<int> free_lanes;
   std::mutex mu;
-  Workspace ws;
-  Timeline tl;
+  std::condition_variable cv;
+  int last_lane = 0;
+  // timings of the most recently completed range-proof run
+  std::mutex tim_mu;
   int ntim = 0;
   const char* tim_name[Timeline::CAP];
   float tim_ms[Timeline::CAP];
   double tim_work[Timeline::CAP];
-  int last_fallback = 0;
+  std::atomic<int> last_fallback{0};
   std::once_flag prover_once;
   ProverTables ptab;
+};
+
+// RAII lane acquisition (want < 0: any free lane)
+struct LaneGuard {
+  fts_ctx* c;
+  Lane* L;
+  LaneGuard(fts_ctx* cc, int want = -1) : c(cc), L(nullptr) {
+    std::unique_lock<std::mutex> lk(c->mu);
+    c->cv.wait(lk, [&] {
+      if (want < 0) return !c->free_lanes.empty();
+      return std::find(c->free_lanes.begin(), c->free_lanes.end(), want) != c->free_lanes.end();
+    });
+    auto it = want < 0 ? c->free_lanes.end() - 1 : std::find(c->free_lanes.begin(), c->free_lanes.end(), want);
+    L = c->lanes[*it];
+    c->free_lanes.erase(it);
+  }
+  ~LaneGuard() {
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      c->free_lanes.push_back(L->id);
+    }
+    c->cv.notify_all();
+  }
 };
 
 struct fts_rp_batch {
   int B = 0;
   int device = 0;
+  // timings of this batch's last verification
+  int ntim = 0;
+  const char* tim_name[Timeline::CAP];
+  float tim_ms[Timeline::CAP];
+  double tim_work[Timeline::CAP];
   uint8_t* raw = nullptr;
   uint32_t* sc = nullptr;
   int32_t* status0 = nullptr;  // host-parse verdicts (restored before every run)
@@ -188,13 +233,30 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   }
   c->device = device;
   auto fail = [&](int code) {
+    for (Lane* L : c->lanes) {
+      if (L->s) hipStreamDestroy(L->s);
+      if (L->s2) hipStreamDestroy(L->s2);
+      L->tl.destroy();
+      delete L;
+    }
+    if (c->d_tables) hipFree(c->d_tables);
     delete c;
     return code;
   };
   if (hipSetDevice(device) != hipSuccess) return fail(FTS_API_EDEVICE);
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
-  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
-  c->tl.create();
+  int nl = 3;
+  if (const char* e = getenv("FTS_LANES")) nl = std::max(1, std::min(8, atoi(e)));
+  for (int i = 0; i < nl; i++) {
+    Lane* L = new Lane();
+    L->id = i;
+    c->lanes.push_back(L);
+    c->free_lanes.push_back(i);
+    if (hipStreamCreateWithFlags(&L->s, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&L->s2, hipStreamNonBlocking) != hipSuccess)
+      return fail(FTS_API_EDEVICE);
+    L->tl.create();
+  }
+  hipStream_t s0 = c->lanes[0]->s;
   const int n = c->n;
   // fixed bases in table order (rp_kernels.hpp tb_*)
   std::vector<G1A> bases;
@@ -228,10 +290,10 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
     hipFree(d_bases);
     return fail(FTS_API_ENOMEM);
   }
-  hipMemcpyAsync(d_bases, hb.data(), hb.size() * 4, hipMemcpyHostToDevice, c->stream);
+  hipMemcpyAsync(d_bases, hb.data(), hb.size() * 4, hipMemcpyHostToDevice, s0);
   for (int b0 = 0; b0 < nb; b0 += chunk)
     launch_build_tables(d_bases + (size_t)b0 * 16, std::min(chunk, nb - b0), c->d_tables + (size_t)b0 * fb_words_per_base(),
-                        d_scr, c->stream);
+                        d_scr, s0);
   // constant part of the x0 transcript: hex(G_i) "||" ... hex(Q) "||"
   std::string xc;
   for (int i = 0; i <= n; i++) {
@@ -241,8 +303,8 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
     xc += "||";
   }
   if (hipMalloc(&c->d_x0const, xc.size()) != hipSuccess) return fail(FTS_API_ENOMEM);
-  hipMemcpyAsync(c->d_x0const, xc.data(), xc.size(), hipMemcpyHostToDevice, c->stream);
-  hipError_t e = hipStreamSynchronize(c->stream);
+  hipMemcpyAsync(c->d_x0const, xc.data(), xc.size(), hipMemcpyHostToDevice, s0);
+  hipError_t e = hipStreamSynchronize(s0);
   hipFree(d_bases);
   hipFree(d_scr);
   if (e != hipSuccess) {
@@ -269,13 +331,17 @@ void fts_ctx_destroy(fts_ctx* c) {
     return;
   }
   hipSetDevice(c->device);
-  if (c->stream) hipStreamSynchronize(c->stream);
-  c->ws.release();
+  for (Lane* L : c->lanes) {
+    if (L->s) hipStreamSynchronize(L->s);
+    if (L->s2) hipStreamSynchronize(L->s2);
+    L->ws.release();
+    L->tl.destroy();
+    if (L->s) hipStreamDestroy(L->s);
+    if (L->s2) hipStreamDestroy(L->s2);
+    delete L;
+  }
   if (c->d_tables) hipFree(c->d_tables);
   if (c->d_x0const) hipFree(c->d_x0const);
-  c->tl.destroy();
-  if (c->stream) hipStreamDestroy(c->stream);
-  if (c->stream2) hipStreamDestroy(c->stream2);
   delete c;
 }
 
@@ -311,8 +377,10 @@ int fts_last_timings(const fts_ctx* c, const char** names, float* ms, int cap) {
   return fts_last_timings_ex(c, names, ms, nullptr, cap);
 }
 
-int fts_last_timings_ex(const fts_ctx* c, const char** names, float* ms, double* mads, int cap) {
-  if (!c) return 0;
+int fts_last_timings_ex(const fts_ctx* cc, const char** names, float* ms, double* mads, int cap) {
+  if (!cc) return 0;
+  fts_ctx* c = const_cast<fts_ctx*>(cc);
+  std::lock_guard<std::mutex> g(c->tim_mu);
   int m = std::min(cap, c->ntim);
   for (int i = 0; i < m; i++) {
     if (names) names[i] = c->tim_name[i];
@@ -358,14 +426,24 @@ static void parse_rp_batch(int k, size_t B, const uint8_t* const* der_p, const s
   for (auto& t : th) t.join();
 }
 
-static void collect_timings(fts_ctx* c) {
+static void collect_timings(fts_ctx* c, Lane& L, fts_rp_batch* b) {
+  std::lock_guard<std::mutex> g(c->tim_mu);
   c->ntim = 0;
-  for (int i = 0; i < c->tl.n; i++) {
-    if (!c->tl.name[i]) continue;  // fork/join markers
+  c->last_lane = L.id;
+  for (int i = 0; i < L.tl.n; i++) {
+    if (!L.tl.name[i]) continue;  // fork/join markers
     const int j = c->ntim++;
-    c->tim_name[j] = c->tl.name[i];
-    c->tim_work[j] = c->tl.work[i];
-    hipEventElapsedTime(&c->tim_ms[j], c->tl.ev[c->tl.start[i]], c->tl.ev[i + 1]);
+    c->tim_name[j] = L.tl.name[i];
+    c->tim_work[j] = L.tl.work[i];
+    hipEventElapsedTime(&c->tim_ms[j], L.tl.ev[L.tl.start[i]], L.tl.ev[i + 1]);
+  }
+  if (b) {
+    b->ntim = c->ntim;
+    for (int j = 0; j < c->ntim; j++) {
+      b->tim_name[j] = c->tim_name[j];
+      b->tim_ms[j] = c->tim_ms[j];
+      b->tim_work[j] = c->tim_work[j];
+    }
   }
 }
 
@@ -374,10 +452,10 @@ static void collect_timings(fts_ctx* c) {
 // `between` (optional) is launched after the RLC check and before the flag
 // sync (the sigma-proof kernels of transfer/issue batches).
 template <class F>
-static int rp_pipeline(fts_ctx* c, int B, uint8_t* d_raw, uint32_t* d_sc, int32_t* d_status, int32_t* d_ipa,
+static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc, int32_t* d_status, int32_t* d_ipa,
                        F&& between) {
   const int n = c->n, k = c->k, npts = rp_npts(k);
-  Workspace& w = c->ws;
+  Workspace& w = L.ws;
   const int N = B * npts;
   MsmPlan mp{};
   msm_layout(N, mp);
@@ -413,7 +491,7 @@ static int rp_pipeline(fts_ctx* c, int B, uint8_t* d_raw, uint32_t* d_sc, int32_
                w.terms.as<uint32_t>(),
                w.scratch.as<uint32_t>()};
   mp.d_win = w.m_win.as<MsmWindow>();
-  HIP_OK(hipMemcpyAsync(mp.d_win, mp.win, sizeof(MsmWindow) * mp.nw, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipMemcpyAsync(mp.d_win, mp.win, sizeof(MsmWindow) * mp.nw, hipMemcpyHostToDevice, L.s));
   mp.keys = w.m_keys.as<int32_t>();
   mp.counts = w.m_counts.as<uint32_t>();
   mp.offsets = w.m_offsets.as<uint32_t>();
@@ -431,29 +509,29 @@ static int rp_pipeline(fts_ctx* c, int B, uint8_t* d_raw, uint32_t* d_sc, int32_
   // fresh RLC weights key (getrandom), unpredictable to the provers
   uint32_t key[8];
   if (getrandom(key, sizeof key, 0) != (ssize_t)sizeof key) return FTS_API_EDEVICE;
-  HIP_OK(hipMemcpyAsync(r.key, key, sizeof key, hipMemcpyHostToDevice, c->stream));
-  c->tl.begin(c->stream);
-  launch_rp_batch(d, r, c->d_tables, c->d_x0const, c->stream, c->stream2, &c->tl);
+  HIP_OK(hipMemcpyAsync(r.key, key, sizeof key, hipMemcpyHostToDevice, L.s));
+  L.tl.begin(L.s);
+  launch_rp_batch(d, r, c->d_tables, c->d_x0const, L.s, L.s2, &L.tl);
   between();
   HIP_OK(hipGetLastError());
   int32_t flag = 0;
-  HIP_OK(hipMemcpyAsync(&flag, r.flag, 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
+  HIP_OK(hipMemcpyAsync(&flag, r.flag, 4, hipMemcpyDeviceToHost, L.s));
+  HIP_OK(hipStreamSynchronize(L.s));
   c->last_fallback = flag ? 0 : 1;
   if (!flag) {
-    launch_rp_fallback(d, c->d_tables, c->stream, &c->tl);
+    launch_rp_fallback(d, c->d_tables, L.s, &L.tl);
     HIP_OK(hipGetLastError());
   }
   return FTS_API_OK;
 }
 
-static int run_rp(fts_ctx* c, int B, uint8_t* d_raw, uint32_t* d_sc, int32_t* d_status, int32_t* d_ipa,
-                  int32_t* host_status) {
-  int rc = rp_pipeline(c, B, d_raw, d_sc, d_status, d_ipa, [] {});
+static int run_rp(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc, int32_t* d_status, int32_t* d_ipa,
+                  int32_t* host_status, fts_rp_batch* batch) {
+  int rc = rp_pipeline(c, L, B, d_raw, d_sc, d_status, d_ipa, [] {});
   if (rc != FTS_API_OK) return rc;
-  if (host_status) HIP_OK(hipMemcpyAsync(host_status, d_status, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
-  collect_timings(c);
+  if (host_status) HIP_OK(hipMemcpyAsync(host_status, d_status, (size_t)B * 4, hipMemcpyDeviceToHost, L.s));
+  HIP_OK(hipStreamSynchronize(L.s));
+  collect_timings(c, L, batch);
   return FTS_API_OK;
 }
 
@@ -464,20 +542,26 @@ extern "C" {
 //   com_out: 64 bytes com (BE) ; hp_out: n x 64 bytes H'_i (BE)
 int fts_debug_rp_intermediates(fts_ctx* c, size_t i, uint8_t* ch_out, uint8_t* com_out, uint8_t* hp_out) {
   if (!c || c->device < 0) return FTS_API_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
+  int want;
+  {
+    std::lock_guard<std::mutex> g(c->tim_mu);
+    want = c->last_lane;
+  }
+  LaneGuard lg(c, want);
+  Workspace& ws = lg.L->ws;
   HIP_OK(hipSetDevice(c->device));
   const int n = c->n, k = c->k, nch = rp_nch(k);
   if (ch_out) {
     std::vector<uint32_t> ch(nch * 8);
-    HIP_OK(hipMemcpy(ch.data(), c->ws.ch.as<uint32_t>() + i * nch * 8, nch * 32, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(ch.data(), ws.ch.as<uint32_t>() + i * nch * 8, nch * 32, hipMemcpyDeviceToHost));
     for (int q = 0; q < nch; q++) {
       Fr m;
       memcpy(m.v, &ch[q * 8], 32);
       fr_to_be(m, ch_out + 32 * q);
     }
   }
-  if (com_out) HIP_OK(hipMemcpy(com_out, c->ws.hpbe.as<uint8_t>() + (i * (n + 1) + n) * 64, 64, hipMemcpyDeviceToHost));
-  if (hp_out) HIP_OK(hipMemcpy(hp_out, c->ws.hpbe.as<uint8_t>() + i * (n + 1) * 64, n * 64, hipMemcpyDeviceToHost));
+  if (com_out) HIP_OK(hipMemcpy(com_out, ws.hpbe.as<uint8_t>() + (i * (n + 1) + n) * 64, 64, hipMemcpyDeviceToHost));
+  if (hp_out) HIP_OK(hipMemcpy(hp_out, ws.hpbe.as<uint8_t>() + i * (n + 1) * 64, n * 64, hipMemcpyDeviceToHost));
   return FTS_API_OK;
 }
 
@@ -485,10 +569,16 @@ int fts_debug_rp_intermediates(fts_ctx* c, size_t i, uint8_t* ch_out, uint8_t* c
 // out[0] = max bucket count, out[1] = its bucket index, out[2] = NB, out[3] = #nonzero buckets
 int fts_debug_msm_stats(fts_ctx* c, int64_t* out) {
   if (!c || c->device < 0 || !out) return FTS_API_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  size_t nb = c->ws.m_counts.cap / 4;
+  int want;
+  {
+    std::lock_guard<std::mutex> g(c->tim_mu);
+    want = c->last_lane;
+  }
+  LaneGuard lg(c, want);
+  Workspace& ws = lg.L->ws;
+  size_t nb = ws.m_counts.cap / 4;
   std::vector<uint32_t> cnt(nb);
-  HIP_OK(hipMemcpy(cnt.data(), c->ws.m_counts.p, nb * 4, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(cnt.data(), ws.m_counts.p, nb * 4, hipMemcpyDeviceToHost));
   size_t arg = 0, nz = 0;
   for (size_t i = 0; i < nb; i++) {
     if (cnt[i] > cnt[arg]) arg = i;
@@ -505,7 +595,6 @@ int fts_rp_batch_stage(fts_ctx* c, size_t n, const uint8_t* const* rp_der, const
                        fts_rp_batch** out) {
   if (!c || !out || (n && (!rp_der || !rp_len || !com64))) return FTS_API_EINVAL;
   if (c->device < 0) return FTS_API_EDEVICE;
-  std::lock_guard<std::mutex> g(c->mu);
   HIP_OK(hipSetDevice(c->device));
   RpHost h;
   parse_rp_batch(c->k, n, rp_der, rp_len, com64, h);
@@ -521,12 +610,11 @@ int fts_rp_batch_stage(fts_ctx* c, size_t n, const uint8_t* const* rp_der, const
     return FTS_API_ENOMEM;
   }
   if (n) {
-    HIP_OK(hipMemcpyAsync(b->raw, h.raw.data(), h.raw.size(), hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(b->sc, h.sc.data(), h.sc.size() * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(b->status0, h.status.data(), n * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(b->ipa_flag, h.ipa.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpy(b->raw, h.raw.data(), h.raw.size(), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(b->sc, h.sc.data(), h.sc.size() * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(b->status0, h.status.data(), n * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(b->ipa_flag, h.ipa.data(), n * 4, hipMemcpyHostToDevice));
   }
-  HIP_OK(hipStreamSynchronize(c->stream));
   *out = b;
   return FTS_API_OK;
 }
@@ -535,10 +623,22 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
   if (!c || !b) return FTS_API_EINVAL;
   if (c->device < 0) return FTS_API_EDEVICE;
   if (b->B == 0) return FTS_API_OK;
-  std::lock_guard<std::mutex> g(c->mu);
   HIP_OK(hipSetDevice(c->device));
-  HIP_OK(hipMemcpyAsync(b->status, b->status0, (size_t)b->B * 4, hipMemcpyDeviceToDevice, c->stream));
-  return run_rp(c, b->B, b->raw, b->sc, b->status, b->ipa_flag, status);
+  LaneGuard lg(c);
+  Lane& L = *lg.L;
+  HIP_OK(hipMemcpyAsync(b->status, b->status0, (size_t)b->B * 4, hipMemcpyDeviceToDevice, L.s));
+  return run_rp(c, L, b->B, b->raw, b->sc, b->status, b->ipa_flag, status, b);
+}
+
+int fts_rp_batch_timings(const fts_rp_batch* b, const char** names, float* ms, double* mads, int cap) {
+  if (!b) return 0;
+  int m = std::min(cap, b->ntim);
+  for (int i = 0; i < m; i++) {
+    if (names) names[i] = b->tim_name[i];
+    if (ms) ms[i] = b->tim_ms[i];
+    if (mads) mads[i] = b->tim_work[i] * MADS_PER_MUL;
+  }
+  return m;
 }
 
 void fts_rp_batch_free(fts_rp_batch* b) {
@@ -589,7 +689,7 @@ struct ActionState {
 };
 }  // namespace
 
-static int verify_actions(fts_ctx* c, const std::vector<ActionIn>& acts, int32_t* status, int32_t* fail_index) {
+static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts, int32_t* status, int32_t* fail_index) {
   const int k = c->k, n = c->n, npts_rp = rp_npts(k);
   const size_t A = acts.size();
   std::vector<ActionState> st(A);
@@ -789,7 +889,7 @@ static int verify_actions(fts_ctx* c, const std::vector<ActionIn>& acts, int32_t
     sact.push_back(sa);
   }
   const int SA = (int)sact.size();
-  Workspace& w = c->ws;
+  Workspace& w = L.ws;
   if (SA) {
     if (w.s_act.ensure(SA * sizeof(SigAction)) || w.s_raw.ensure(s_raw.size()) || w.s_owner.ensure(s_owner.size() * 4) ||
         w.s_pts.ensure((size_t)pt_off * 64) || w.s_sc.ensure(std::max<size_t>(s_sc.size(), 1) * 4) ||
@@ -798,23 +898,23 @@ static int verify_actions(fts_ctx* c, const std::vector<ActionIn>& acts, int32_t
         w.s_affoff.ensure(SA * 4) || w.s_msgs.ensure(msg_off) || w.s_jac.ensure((size_t)aff_off * 96) ||
         w.s_scratch.ensure(s_work.size() * 10 * 24 * 4))
       return FTS_API_ENOMEM;
-    HIP_OK(hipMemcpyAsync(w.s_act.p, sact.data(), SA * sizeof(SigAction), hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(w.s_raw.p, s_raw.data(), s_raw.size(), hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(w.s_owner.p, s_owner.data(), s_owner.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(w.s_act.p, sact.data(), SA * sizeof(SigAction), hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.s_raw.p, s_raw.data(), s_raw.size(), hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.s_owner.p, s_owner.data(), s_owner.size() * 4, hipMemcpyHostToDevice, L.s));
     if (!s_sc.empty())
-      HIP_OK(hipMemcpyAsync(w.s_sc.p, s_sc.data(), s_sc.size() * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(w.s_status.p, s_status.data(), SA * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(w.s_work.p, s_work.data(), s_work.size() * sizeof(int2), hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(w.s_affoff.p, s_affoff.data(), SA * 4, hipMemcpyHostToDevice, c->stream));
+      HIP_OK(hipMemcpyAsync(w.s_sc.p, s_sc.data(), s_sc.size() * 4, hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.s_status.p, s_status.data(), SA * 4, hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.s_work.p, s_work.data(), s_work.size() * sizeof(int2), hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.s_affoff.p, s_affoff.data(), SA * 4, hipMemcpyHostToDevice, L.s));
   }
   if (rp_total) {
     if (w.rp_raw.ensure(r_raw.size()) || w.rp_sc.ensure(r_sc.size() * 4) || w.rp_status.ensure(rp_total * 4) ||
         w.rp_ipa.ensure(rp_total * 4))
       return FTS_API_ENOMEM;
-    HIP_OK(hipMemcpyAsync(w.rp_raw.p, r_raw.data(), r_raw.size(), hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(w.rp_sc.p, r_sc.data(), r_sc.size() * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(w.rp_status.p, r_status.data(), rp_total * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(w.rp_ipa.p, r_ipa.data(), rp_total * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(w.rp_raw.p, r_raw.data(), r_raw.size(), hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.rp_sc.p, r_sc.data(), r_sc.size() * 4, hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.rp_status.p, r_status.data(), rp_total * 4, hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.rp_ipa.p, r_ipa.data(), rp_total * 4, hipMemcpyHostToDevice, L.s));
   }
   SigBatchDev sd{};
   if (SA) {
@@ -836,13 +936,13 @@ static int verify_actions(fts_ctx* c, const std::vector<ActionIn>& acts, int32_t
     sd.scratch = w.s_scratch.as<uint32_t>();
     sd.rp_raw = rp_total ? w.rp_raw.as<uint8_t>() : nullptr;
     sd.rp_k = k;
-    launch_sig_prep(sd, c->stream);
+    launch_sig_prep(sd, L.s);
   }
   auto sig_finish = [&]() {
-    if (SA) launch_sig_finish(sd, c->d_tables, n, c->stream);
+    if (SA) launch_sig_finish(sd, c->d_tables, n, L.s);
   };
   if (rp_total) {
-    int rc = rp_pipeline(c, rp_total, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
+    int rc = rp_pipeline(c, L, rp_total, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
                          w.rp_ipa.as<int32_t>(), sig_finish);
     if (rc != FTS_API_OK) return rc;
   } else {
@@ -850,9 +950,9 @@ static int verify_actions(fts_ctx* c, const std::vector<ActionIn>& acts, int32_t
   }
   HIP_OK(hipGetLastError());
   std::vector<int32_t> sig_res(SA), rp_res(rp_total);
-  if (SA) HIP_OK(hipMemcpyAsync(sig_res.data(), w.s_status.p, SA * 4, hipMemcpyDeviceToHost, c->stream));
-  if (rp_total) HIP_OK(hipMemcpyAsync(rp_res.data(), w.rp_status.p, rp_total * 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
+  if (SA) HIP_OK(hipMemcpyAsync(sig_res.data(), w.s_status.p, SA * 4, hipMemcpyDeviceToHost, L.s));
+  if (rp_total) HIP_OK(hipMemcpyAsync(rp_res.data(), w.rp_status.p, rp_total * 4, hipMemcpyDeviceToHost, L.s));
+  HIP_OK(hipStreamSynchronize(L.s));
   // ---- combine with the reference's precedence
   for (size_t i = 0; i < A; i++) {
     const ActionState& s = st[i];
@@ -897,9 +997,9 @@ int fts_transfer_verify_batch(fts_ctx* c, size_t n, const fts_transfer_item* ite
   for (size_t i = 0; i < n; i++)
     acts[i] = ActionIn{SIG_TAS, items[i].inputs, items[i].n_in, items[i].outputs, items[i].n_out,
                        der::Span{items[i].proof, items[i].proof ? items[i].proof_len : 0}};
-  std::lock_guard<std::mutex> g(c->mu);
   HIP_OK(hipSetDevice(c->device));
-  int rc = verify_actions(c, acts, status, fail_index);
+  LaneGuard lg(c);
+  int rc = verify_actions(c, *lg.L, acts, status, fail_index);
   if (rc != FTS_API_OK)
     for (size_t i = 0; i < n; i++) status[i] = FTS_E_NOT_RUN;
   return rc;
@@ -913,9 +1013,9 @@ int fts_issue_verify_batch(fts_ctx* c, size_t n, const fts_issue_item* items, in
   for (size_t i = 0; i < n; i++)
     acts[i] = ActionIn{SIG_ST, nullptr, 0, items[i].tokens, items[i].n_tok,
                        der::Span{items[i].proof, items[i].proof ? items[i].proof_len : 0}};
-  std::lock_guard<std::mutex> g(c->mu);
   HIP_OK(hipSetDevice(c->device));
-  int rc = verify_actions(c, acts, status, fail_index);
+  LaneGuard lg(c);
+  int rc = verify_actions(c, *lg.L, acts, status, fail_index);
   if (rc != FTS_API_OK)
     for (size_t i = 0; i < n; i++) status[i] = FTS_E_NOT_RUN;
   return rc;

@@ -236,6 +236,19 @@ class StagedRangeBatch:
             self.pp._ctx, self._b, st.ctypes.data_as(C.POINTER(C.c_int32)) if want_status else None))
         return st
 
+    def timings(self):
+        """{kernel: (ms, algorithmic u32 MADs)} of this batch's last verify()"""
+        names = (C.c_char_p * 64)()
+        ms = (C.c_float * 64)()
+        mads = (C.c_double * 64)()
+        m = L.lib.fts_rp_batch_timings(self._b, names, ms, mads, 64)
+        out = {}
+        for i in range(m):
+            k = names[i].decode()
+            o = out.get(k, (0.0, 0.0))
+            out[k] = (o[0] + ms[i], o[1] + mads[i])
+        return out
+
     def close(self):
         if self._b:
             L.lib.fts_rp_batch_free(self._b)
