@@ -11,7 +11,7 @@ imports it and fails loudly when its HIP library is missing.
 
 Pinning: ``oracle.bn254.hash_to_g1`` reproduces all 130 range-proof generators
 of the reference fixture ``cmd/tokengen/testdata/zkatdlog_pp.json`` (KAT-1,
-``tests/test_oracle_kat.py``).  Everything above the curve arithmetic
+``tests/test_oracle.py``).  Everything above the curve arithmetic
 (HashToZr, Zr byte encoding, transcripts) has no golden vector in the
 reference and is "parity unpinned" beyond the KAT — see DESIGN.md §Oracle.
 """
