@@ -15,6 +15,11 @@ Prints one JSON line (rank 0).  Usage:
 import argparse
 import json
 import os
+
+# Hardware queues per process: every lane uses two streams, and streams that
+# share a HIP hardware queue serialise.  Read once at HIP runtime init, so set
+# before anything initialises the GPU (lane sweep).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 import sys
 import threading
 import time
@@ -39,8 +44,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--bits", type=int, default=64)
-    ap.add_argument("--lanes", type=int, default=int(os.environ.get("FTS_LANES", "3")),
+    ap.add_argument("--lanes", type=int, default=int(os.environ.get("FTS_LANES", "8")),
                     help="batches in flight (host threads / device lanes; FTS_LANES)")
+    ap.add_argument("--reuse-proofs", action="store_true", help="stage lane 0's proofs on every lane (faster setup)")
     ap.add_argument("--cpu-sample", type=int, default=256, help="CPU baseline chunk size (0: skip the CPU baseline)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall-time bound of the CPU baseline sample")
@@ -70,6 +76,9 @@ def main():
     t0 = time.time()
     batches, proofs0, coms0 = [], None, None
     for ln in range(lanes):
+        if ln > 0 and args.reuse_proofs:
+            batches.append(pp.stage_range_proofs(proofs0, coms0))
+            continue
         rng = random.Random(0xF7A50002 + 7919 * rank + 104729 * ln)
         vals = [rng.getrandbits(n) for _ in range(B)]
         bfs = [rng.randrange(R_ORDER).to_bytes(32, "big") for _ in range(B)]

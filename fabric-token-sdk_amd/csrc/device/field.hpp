@@ -186,6 +186,51 @@ FTS_DEV void mac96s(uint64_t& acc, uint32_t& ovf, uint32_t x, uint32_t y_uniform
       : "vcc");
 }
 
+// Runs of 2 / 4 MACs on one 96-bit accumulator inside one asm block.  The
+// hazard recognizer pads every inline-asm boundary with an s_nop; grouping
+// removes most of those pads from the dependent chain (the mad -> addc VCC
+// dependency is interlocked, as in mac96).
+#define FTS_MAC_LINE(X, Y) "v_mad_u64_u32 %0, vcc, %" #X ", %" #Y ", %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc\n\t"
+FTS_DEV void mac96_2v(uint64_t& acc, uint32_t& ovf, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
+  asm(FTS_MAC_LINE(2, 3) FTS_MAC_LINE(4, 5) : "+v"(acc), "+v"(ovf) : "v"(x0), "v"(y0), "v"(x1), "v"(y1) : "vcc");
+}
+FTS_DEV void mac96_4v(uint64_t& acc, uint32_t& ovf, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1, uint32_t x2,
+                      uint32_t y2, uint32_t x3, uint32_t y3) {
+  asm(FTS_MAC_LINE(2, 3) FTS_MAC_LINE(4, 5) FTS_MAC_LINE(6, 7) FTS_MAC_LINE(8, 9)
+      : "+v"(acc), "+v"(ovf)
+      : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(x2), "v"(y2), "v"(x3), "v"(y3)
+      : "vcc");
+}
+FTS_DEV void mac96_2s(uint64_t& acc, uint32_t& ovf, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
+  asm(FTS_MAC_LINE(2, 3) FTS_MAC_LINE(4, 5) : "+v"(acc), "+v"(ovf) : "v"(x0), "s"(y0), "v"(x1), "s"(y1) : "vcc");
+}
+FTS_DEV void mac96_4s(uint64_t& acc, uint32_t& ovf, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1, uint32_t x2,
+                      uint32_t y2, uint32_t x3, uint32_t y3) {
+  asm(FTS_MAC_LINE(2, 3) FTS_MAC_LINE(4, 5) FTS_MAC_LINE(6, 7) FTS_MAC_LINE(8, 9)
+      : "+v"(acc), "+v"(ovf)
+      : "v"(x0), "s"(y0), "v"(x1), "s"(y1), "v"(x2), "s"(y2), "v"(x3), "s"(y3)
+      : "vcc");
+}
+// sum_{q < cnt} x[q] * y[q] into (acc, ovf); cnt is a compile-time constant after unrolling
+template <bool UNIFORM_Y>
+FTS_DEV void mac_run(uint64_t& acc, uint32_t& ovf, const uint32_t* x, const uint32_t* y, int cnt) {
+  int q = 0;
+#pragma unroll
+  for (; q + 4 <= cnt; q += 4) {
+    if (UNIFORM_Y) mac96_4s(acc, ovf, x[q], y[q], x[q + 1], y[q + 1], x[q + 2], y[q + 2], x[q + 3], y[q + 3]);
+    else mac96_4v(acc, ovf, x[q], y[q], x[q + 1], y[q + 1], x[q + 2], y[q + 2], x[q + 3], y[q + 3]);
+  }
+  if (q + 2 <= cnt) {
+    if (UNIFORM_Y) mac96_2s(acc, ovf, x[q], y[q], x[q + 1], y[q + 1]);
+    else mac96_2v(acc, ovf, x[q], y[q], x[q + 1], y[q + 1]);
+    q += 2;
+  }
+  if (q < cnt) {
+    if (UNIFORM_Y) mac96s(acc, ovf, x[q], y[q]);
+    else mac96(acc, ovf, x[q], y[q]);
+  }
+}
+
 // Montgomery product, finely-integrated product scanning (FIPS): column k of
 // a*b and of m*M are summed in a 96-bit accumulator, m[k] is produced as soon
 // as column k < 8 is complete.  Same 136 multiplies as CIOS, but the
@@ -260,9 +305,304 @@ FTS_DEV Field<P> f_mul_fips2(const Field<P>& a, const Field<P>& b) {
   return r;
 }
 
+// The carry of v_mad_u64_u32 in an SGPR pair instead of VCC, and the mad and
+// its carry-add as separate asm statements: the compiler can interleave
+// independent accumulator chains (with VCC every mad/addc pair of every chain
+// serialises on the one flag register).
+FTS_DEV void mad_sc(uint64_t& acc, uint64_t& c, uint32_t x, uint32_t y) {
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(c) : "v"(x), "v"(y));
+}
+FTS_DEV void mad_scs(uint64_t& acc, uint64_t& c, uint32_t x, uint32_t y_uniform) {
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(c) : "v"(x), "s"(y_uniform));
+}
+FTS_DEV void addc_sc(uint32_t& ovf, uint64_t c) {
+  uint64_t d;
+  asm("v_addc_co_u32 %0, %1, 0, %0, %2" : "+v"(ovf), "=s"(d) : "s"(c));
+}
+
+// Experimental variants kept for lib/int_peak only (measured on MI355X,
+// profiles/r01_int_peak.log): a single wave already fills its SIMD's
+// quarter-rate MAD issue, so extra ILP does not shorten a product
+// (fips 1,840 cycles; sc 2,180; x2 2,050).
+// two independent 96-bit accumulations in one asm block: both mads issue
+// before either carry-add, carries in two distinct SGPR pairs
+FTS_DEV void mac96x2(uint64_t& a0, uint32_t& o0, uint32_t x0, uint32_t y0, uint64_t& a1, uint32_t& o1, uint32_t x1,
+                     uint32_t y1_uniform) {
+  uint64_t c0, c1;
+  asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\t"
+      "v_mad_u64_u32 %2, %5, %8, %9, %2\n\t"
+      "v_addc_co_u32 %1, %4, 0, %1, %4\n\t"
+      "v_addc_co_u32 %3, %5, 0, %3, %5"
+      : "+v"(a0), "+v"(o0), "+v"(a1), "+v"(o1), "=&s"(c0), "=&s"(c1)
+      : "v"(x0), "v"(y0), "v"(x1), "s"(y1_uniform));
+}
+
+// FIPS with the a*b and m*M products of each column in two accumulators,
+// issued pairwise (mac96x2): half the dependent-chain length of f_mul_fips.
+template <class P>
+FTS_DEV Field<P> f_mul_x2(const Field<P>& a, const Field<P>& b) {
+  uint32_t m[8], t[8];
+  uint64_t acc = 0;
+  uint32_t ovf = 0;
+#pragma unroll
+  for (int k = 0; k < 15; k++) {
+    uint64_t acc2 = 0;
+    uint32_t ovf2 = 0;
+    const int lo = k > 7 ? k - 7 : 0, hi = k < 7 ? k : 7;  // a_i b_{k-i}, i in [lo, hi]
+    const int mhi = k < 8 ? k : 8;                          // m_j M_{k-j}, j in [lo, mhi)
+    const int na = hi - lo + 1, nm = mhi - lo;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const bool ha = q < na, hm = q < nm;
+      if (ha && hm) {
+        mac96x2(acc, ovf, a.v[lo + q], b.v[k - lo - q], acc2, ovf2, m[lo + q], P::M[k - lo - q]);
+      } else if (ha) {
+        mac96(acc, ovf, a.v[lo + q], b.v[k - lo - q]);
+      } else if (hm) {
+        mac96s(acc2, ovf2, m[lo + q], P::M[k - lo - q]);
+      }
+    }
+    add96(acc, ovf, acc2, ovf2);
+    if (k < 8) {
+      m[k] = (uint32_t)acc * P::INV;
+      mac96s(acc, ovf, m[k], P::M[0]);
+    } else {
+      t[k - 8] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)ovf << 32);
+    ovf = 0;
+  }
+  t[7] = (uint32_t)acc;
+  Field<P> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = t[i];
+  f_reduce_once(r);
+  return r;
+}
+
+// FIPS with two independent 96-bit accumulators per column (a*b and m*M),
+// SGPR carries: the two chains overlap in the pipeline.
+template <class P>
+FTS_DEV Field<P> f_mul_sc2(const Field<P>& a, const Field<P>& b) {
+  uint32_t m[8], t[8];
+  uint64_t acc = 0;
+  uint32_t ovf = 0;
+#pragma unroll
+  for (int k = 0; k < 15; k++) {
+    uint64_t acc2 = 0;
+    uint32_t ovf2 = 0;
+    const int lo = k > 7 ? k - 7 : 0, hi = k < 7 ? k : 7;
+    const int mhi = k < 8 ? k : 8;
+    // interleave the two chains product by product
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int i = lo + q, j = lo + q;
+      if (i <= hi) {
+        uint64_t c;
+        mad_sc(acc, c, a.v[i], b.v[k - i]);
+        addc_sc(ovf, c);
+      }
+      if (j < mhi) {
+        uint64_t c;
+        mad_scs(acc2, c, m[j], P::M[k - j]);
+        addc_sc(ovf2, c);
+      }
+    }
+    add96(acc, ovf, acc2, ovf2);
+    if (k < 8) {
+      m[k] = (uint32_t)acc * P::INV;
+      uint64_t c;
+      mad_scs(acc, c, m[k], P::M[0]);
+      addc_sc(ovf, c);
+    } else {
+      t[k - 8] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)ovf << 32);
+    ovf = 0;
+  }
+  t[7] = (uint32_t)acc;
+  Field<P> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = t[i];
+  f_reduce_once(r);
+  return r;
+}
+
+// FIPS, single accumulator, SGPR carries (same dependency chain as
+// f_mul_fips, but the mad/addc pairs are no longer fused in one asm block)
+template <class P>
+FTS_DEV Field<P> f_mul_sc(const Field<P>& a, const Field<P>& b) {
+  uint32_t m[8], t[8];
+  uint64_t acc = 0;
+  uint32_t ovf = 0;
+#pragma unroll
+  for (int k = 0; k < 15; k++) {
+#pragma unroll
+    for (int i = (k > 7 ? k - 7 : 0); i <= (k < 7 ? k : 7); i++) {
+      uint64_t c;
+      mad_sc(acc, c, a.v[i], b.v[k - i]);
+      addc_sc(ovf, c);
+    }
+#pragma unroll
+    for (int i = (k > 7 ? k - 7 : 0); i < (k < 8 ? k : 8); i++) {
+      uint64_t c;
+      mad_scs(acc, c, m[i], P::M[k - i]);
+      addc_sc(ovf, c);
+    }
+    if (k < 8) {
+      m[k] = (uint32_t)acc * P::INV;
+      uint64_t c;
+      mad_scs(acc, c, m[k], P::M[0]);
+      addc_sc(ovf, c);
+    } else {
+      t[k - 8] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)ovf << 32);
+    ovf = 0;
+  }
+  t[7] = (uint32_t)acc;
+  Field<P> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = t[i];
+  f_reduce_once(r);
+  return r;
+}
+
+// FIPS product with the column MACs grouped (mac_run): same 136 MADs as
+// f_mul_fips, ~1/3 of the inline-asm boundary pads.
+template <class P>
+FTS_DEV Field<P> f_mul_g(const Field<P>& a, const Field<P>& b) {
+  uint32_t m[8], t[8];
+  uint64_t acc = 0;
+  uint32_t ovf = 0;
+#pragma unroll
+  for (int k = 0; k < 15; k++) {
+    const int lo = k > 7 ? k - 7 : 0, hi = k < 7 ? k : 7;
+    uint32_t xs[8], ys[8];
+#pragma unroll
+    for (int i = lo; i <= hi; i++) {
+      xs[i - lo] = a.v[i];
+      ys[i - lo] = b.v[k - i];
+    }
+    mac_run<false>(acc, ovf, xs, ys, hi - lo + 1);
+    const int mhi = k < 8 ? k : 8;
+    uint32_t ms[8], cs[8];
+#pragma unroll
+    for (int i = lo; i < mhi; i++) {
+      ms[i - lo] = m[i];
+      cs[i - lo] = P::M[k - i];
+    }
+    mac_run<true>(acc, ovf, ms, cs, mhi - lo);
+    if (k < 8) {
+      m[k] = (uint32_t)acc * P::INV;
+      mac96s(acc, ovf, m[k], P::M[0]);
+    } else {
+      t[k - 8] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)ovf << 32);
+    ovf = 0;
+  }
+  t[7] = (uint32_t)acc;
+  Field<P> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = t[i];
+  f_reduce_once(r);
+  return r;
+}
+
+// Montgomery square with grouped MACs: 36 products + 64 reduction MADs.
+template <class P>
+FTS_DEV Field<P> f_sqr_g(const Field<P>& a) {
+  uint32_t m[8], t[8];
+  uint64_t acc = 0;
+  uint32_t ovf = 0;
+#pragma unroll
+  for (int k = 0; k < 15; k++) {
+    uint64_t x = 0;
+    uint32_t xo = 0;
+    const int lo = k > 7 ? k - 7 : 0;
+    uint32_t xs[4], ys[4];
+    int nc = 0;
+#pragma unroll
+    for (int i = lo; 2 * i < k; i++) {
+      xs[nc] = a.v[i];
+      ys[nc] = a.v[k - i];
+      nc++;
+    }
+    mac_run<false>(x, xo, xs, ys, nc);
+    xo = (xo << 1) | (uint32_t)(x >> 63);
+    x <<= 1;
+    if ((k & 1) == 0) mac96(x, xo, a.v[k / 2], a.v[k / 2]);
+    add96(acc, ovf, x, xo);
+    const int mhi = k < 8 ? k : 8;
+    uint32_t ms[8], cs[8];
+#pragma unroll
+    for (int i = lo; i < mhi; i++) {
+      ms[i - lo] = m[i];
+      cs[i - lo] = P::M[k - i];
+    }
+    mac_run<true>(acc, ovf, ms, cs, mhi - lo);
+    if (k < 8) {
+      m[k] = (uint32_t)acc * P::INV;
+      mac96s(acc, ovf, m[k], P::M[0]);
+    } else {
+      t[k - 8] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)ovf << 32);
+    ovf = 0;
+  }
+  t[7] = (uint32_t)acc;
+  Field<P> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = t[i];
+  f_reduce_once(r);
+  return r;
+}
+
 template <class P>
 FTS_DEV Field<P> f_sqr(const Field<P>& a) {
   return f_mul(a, a);
+}
+
+// Montgomery square, FIPS: column k of a^2 = 2 * sum_{i<j, i+j=k} a_i a_j
+// (+ a_{k/2}^2 for even k).  The cross products go to their own 96-bit
+// accumulator, doubled by a 1-bit shift before the square term and the
+// running column value are added: 36 products + 64 for the reduction
+// = 100 MADs instead of 136.
+template <class P>
+FTS_DEV Field<P> f_sqr_fips(const Field<P>& a) {
+  uint32_t m[8], t[8];
+  uint64_t acc = 0;
+  uint32_t ovf = 0;
+#pragma unroll
+  for (int k = 0; k < 15; k++) {
+    uint64_t x = 0;
+    uint32_t xo = 0;
+    const int lo = k > 7 ? k - 7 : 0;
+#pragma unroll
+    for (int i = lo; 2 * i < k; i++) mac96(x, xo, a.v[i], a.v[k - i]);
+    // x <<= 1 (96-bit)
+    xo = (xo << 1) | (uint32_t)(x >> 63);
+    x <<= 1;
+    if ((k & 1) == 0) mac96(x, xo, a.v[k / 2], a.v[k / 2]);
+    add96(acc, ovf, x, xo);
+#pragma unroll
+    for (int i = lo; i < (k < 8 ? k : 8); i++) mac96s(acc, ovf, m[i], P::M[k - i]);
+    if (k < 8) {
+      m[k] = (uint32_t)acc * P::INV;
+      mac96s(acc, ovf, m[k], P::M[0]);
+    } else {
+      t[k - 8] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)ovf << 32);
+    ovf = 0;
+  }
+  t[7] = (uint32_t)acc;
+  Field<P> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = t[i];
+  f_reduce_once(r);
+  return r;
 }
 
 // Montgomery form <-> canonical integer (both as 8 little-endian limbs)

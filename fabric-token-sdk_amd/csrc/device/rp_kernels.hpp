@@ -101,6 +101,7 @@ struct Timeline {
   }
   // `to` waits for everything issued so far on `from`
   void fork(hipStream_t from, hipStream_t to) {
+    if (from == to) return;
     if (n >= CAP) {
       hipEvent_t e;
       (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);

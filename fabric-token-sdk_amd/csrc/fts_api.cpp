@@ -234,8 +234,8 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   c->device = device;
   auto fail = [&](int code) {
     for (Lane* L : c->lanes) {
+      if (L->s2 && L->s2 != L->s) hipStreamDestroy(L->s2);
       if (L->s) hipStreamDestroy(L->s);
-      if (L->s2) hipStreamDestroy(L->s2);
       L->tl.destroy();
       delete L;
     }
@@ -244,16 +244,19 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
     return code;
   };
   if (hipSetDevice(device) != hipSuccess) return fail(FTS_API_EDEVICE);
-  int nl = 3;
-  if (const char* e = getenv("FTS_LANES")) nl = std::max(1, std::min(8, atoi(e)));
+  int nl = 8;
+  if (const char* e = getenv("FTS_LANES")) nl = std::max(1, std::min(16, atoi(e)));
+  // FTS_SIDE_STREAM=0: run each lane's side work on its main stream
+  bool side = true;
+  if (const char* e = getenv("FTS_SIDE_STREAM")) side = atoi(e) != 0;
   for (int i = 0; i < nl; i++) {
     Lane* L = new Lane();
     L->id = i;
     c->lanes.push_back(L);
     c->free_lanes.push_back(i);
-    if (hipStreamCreateWithFlags(&L->s, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&L->s2, hipStreamNonBlocking) != hipSuccess)
-      return fail(FTS_API_EDEVICE);
+    if (hipStreamCreateWithFlags(&L->s, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
+    if (!side) L->s2 = L->s;
+    else if (hipStreamCreateWithFlags(&L->s2, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
     L->tl.create();
   }
   hipStream_t s0 = c->lanes[0]->s;
@@ -333,11 +336,11 @@ void fts_ctx_destroy(fts_ctx* c) {
   hipSetDevice(c->device);
   for (Lane* L : c->lanes) {
     if (L->s) hipStreamSynchronize(L->s);
-    if (L->s2) hipStreamSynchronize(L->s2);
+    if (L->s2 && L->s2 != L->s) hipStreamSynchronize(L->s2);
     L->ws.release();
     L->tl.destroy();
+    if (L->s2 && L->s2 != L->s) hipStreamDestroy(L->s2);
     if (L->s) hipStreamDestroy(L->s);
-    if (L->s2) hipStreamDestroy(L->s2);
     delete L;
   }
   if (c->d_tables) hipFree(c->d_tables);

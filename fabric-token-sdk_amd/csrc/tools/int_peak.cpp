@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <vector>
 #include "../device/field.hpp"
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1);} } while (0)
@@ -92,7 +93,10 @@ template <int V>
 __device__ __forceinline__ fts::Fp mulv(const fts::Fp& a, const fts::Fp& b) {
   if constexpr (V == 0) return fts::f_mul(a, b);
   else if constexpr (V == 1) return fts::f_mul_fips(a, b);
-  else return fts::f_mul_fips2(a, b);
+  else if constexpr (V == 2) return fts::f_mul_g(a, b);
+  else if constexpr (V == 3) return fts::f_sqr_fips(a);
+  else if constexpr (V == 4) return fts::f_sqr_g(a);
+  else return fts::f_mul_x2(a, b);
 }
 // dependent chain: latency per product when few waves are resident
 template <int V>
@@ -106,7 +110,7 @@ __global__ void __launch_bounds__(256) k_lat(const uint32_t* in, uint32_t* out, 
   }
   a.v[7] &= 0x0fffffffu;
   b.v[7] &= 0x0fffffffu;
-  for (int i = 0; i < iters; i++) a = mulv<V>(a, b);
+  for (int i = 0; i < iters; i++) a = (V == 3 || V == 4) ? mulv<V>(a, a) : (V == 5 ? fts::f_mul(a, a) : mulv<V>(a, b));
   uint32_t s = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) s ^= a.v[i];
@@ -194,8 +198,11 @@ int main() {
     double l0 = time_lat<0>(d_in, (uint32_t*)d_out, blocks, threads, 2000);
     double l1 = time_lat<1>(d_in, (uint32_t*)d_out, blocks, threads, 2000);
     double l2 = time_lat<2>(d_in, (uint32_t*)d_out, blocks, threads, 2000);
-    printf("{\"latency_cfg\": \"%dx%d\", \"cios_cycles\": %.0f, \"fips_cycles\": %.0f, \"fips2_cycles\": %.0f}\n",
-           blocks, threads, l0 * 2.4e9, l1 * 2.4e9, l2 * 2.4e9);
+    double l3 = time_lat<3>(d_in, (uint32_t*)d_out, blocks, threads, 2000);
+    double l4 = time_lat<4>(d_in, (uint32_t*)d_out, blocks, threads, 2000);
+    printf("{\"latency_cfg\": \"%dx%d\", \"cios_cycles\": %.0f, \"fips_cycles\": %.0f, \"g_cycles\": %.0f, "
+           "\"sqr_cycles\": %.0f, \"sqr_g_cycles\": %.0f}\n",
+           blocks, threads, l0 * 2.4e9, l1 * 2.4e9, l2 * 2.4e9, l3 * 2.4e9, l4 * 2.4e9);
   }
   // throughput of fips2 (full occupancy, same shape as k_fpmul)
   {
@@ -214,8 +221,36 @@ int main() {
     hipEventSynchronize(a1);
     float m1;
     hipEventElapsedTime(&m1, a0, a1);
-    printf("{\"throughput_fips_per_s\": %.4e, \"throughput_fips2_per_s\": %.4e}\n", (double)cus * 8 * 256 * 512 / (m1 * 1e-3),
-           (double)cus * 8 * 256 * 512 / (m2 * 1e-3));
+    float m3, m4;
+    hipEventRecord(a0);
+    k_lat<3><<<cus * 8, 256>>>(d_in, (uint32_t*)d_out, 512);
+    hipEventRecord(a1);
+    hipEventSynchronize(a1);
+    hipEventElapsedTime(&m3, a0, a1);
+    hipEventRecord(a0);
+    k_lat<4><<<cus * 8, 256>>>(d_in, (uint32_t*)d_out, 512);
+    hipEventRecord(a1);
+    hipEventSynchronize(a1);
+    hipEventElapsedTime(&m4, a0, a1);
+    const double nm = (double)cus * 8 * 256 * 512;
+    printf("{\"throughput_fips_per_s\": %.4e, \"throughput_g_per_s\": %.4e, \"throughput_sqr_per_s\": %.4e, "
+           "\"throughput_sqr_g_per_s\": %.4e}\n", nm / (m1 * 1e-3), nm / (m2 * 1e-3), nm / (m3 * 1e-3), nm / (m4 * 1e-3));
+    // correctness of the new variants against CIOS
+    std::vector<uint32_t> r0(cus * 256), r3(cus * 256), r4(cus * 256), r5(cus * 256);
+    k_lat<5><<<cus, 256>>>(d_in, (uint32_t*)d_out, 64);
+    hipMemcpy(r5.data(), d_out, r5.size() * 4, hipMemcpyDeviceToHost);
+    k_lat<0><<<cus, 256>>>(d_in, (uint32_t*)d_out, 64);
+    hipMemcpy(r0.data(), d_out, r0.size() * 4, hipMemcpyDeviceToHost);
+    k_lat<3><<<cus, 256>>>(d_in, (uint32_t*)d_out, 64);
+    hipMemcpy(r3.data(), d_out, r3.size() * 4, hipMemcpyDeviceToHost);
+    k_lat<4><<<cus, 256>>>(d_in, (uint32_t*)d_out, 64);
+    hipMemcpy(r4.data(), d_out, r4.size() * 4, hipMemcpyDeviceToHost);
+    int bad3 = 0, bad4 = 0;
+    for (size_t i = 0; i < r0.size(); i++) {
+      bad3 += r5[i] != r3[i];
+      bad4 += r5[i] != r4[i];
+    }
+    printf("{\"sqr_mismatch\": %d, \"sqr_g_mismatch\": %d}\n", bad3, bad4);
   }
   printf("{\"device\": \"%s\", \"cus\": %d, \"clock_khz\": %d, \"mad_u64_u32_per_s\": %.4e, "
          "\"u32_ops_per_s\": %.4e, \"fp_mul_per_s\": %.4e, \"fp_mul_mad_equiv_per_s\": %.4e}\n",

@@ -27,7 +27,7 @@
  * Return values: every function returns FTS_API_OK (0) or a negative
  * FTS_API_* code for API/driver errors (bad argument, HIP failure).
  * Per-item verdicts go to caller-owned int32 arrays as fts_status values.
- * Thread safety: a context runs up to FTS_LANES (default 3) calls concurrently,
+ * Thread safety: a context runs up to FTS_LANES (default 8) calls concurrently,
  * each on its own pair of HIP streams and workspace; further callers wait.
  */
 #ifndef FTS_GPU_H
@@ -122,7 +122,7 @@ int fts_rp_batch_stage(fts_ctx* ctx, size_t n, const uint8_t* const* rp_der, con
                        const uint8_t* com64, fts_rp_batch** out);
 /* runs the whole GPU verification of a staged batch; status may be NULL.
  * Thread-safe: concurrent calls on DIFFERENT batches run on different lanes
- * (stream pairs, FTS_LANES env, default 3) and overlap on the device. */
+ * (stream pairs, FTS_LANES env, default 8) and overlap on the device. */
 int fts_rp_batch_verify(fts_ctx* ctx, fts_rp_batch* b, int32_t* status);
 /* per-kernel device time (ms) and algorithmic u32 MADs of b's last verification */
 int fts_rp_batch_timings(const fts_rp_batch* b, const char** names, float* ms, double* mads, int cap);
