@@ -128,7 +128,7 @@ FTS_DEV int window_of_bucket(const MsmWindow* win, int nw, int b) {
 
 // one lane per chunk slot: <= MSM_CH mixed additions of sorted virtual points
 // (index >= N: phi(P_{index-N}) = (beta x, y))
-__global__ void __launch_bounds__(64) k_msm_chunks(int N, int nw, int NC, const MsmWindow* __restrict__ win,
+__global__ void __launch_bounds__(64, 4) k_msm_chunks(int N, int nw, int NC, const MsmWindow* __restrict__ win,
                                                    const uint32_t* __restrict__ points,
                                                    const uint32_t* __restrict__ offsets,
                                                    const uint32_t* __restrict__ counts,

@@ -211,7 +211,7 @@ inline __host__ __device__ int com_nterms(int n) { return n + 4; }
 
 // lane per (proof, item): items 0..n-1: H'_i = y^-i H_i (-> hpj[b][i]);
 // n..2n-1: (z^2 2^(i) y^-i) H_i; 2n: z K; 2n+1: -delta P (-> terms[b][.])
-__global__ void __launch_bounds__(64) k_rp_fixed_exact(int B, int n, int k, const int32_t* __restrict__ status,
+__global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, const int32_t* __restrict__ status,
                                                        const uint32_t* __restrict__ sc, const uint32_t* __restrict__ ch,
                                                        const uint32_t* __restrict__ tables, uint32_t* __restrict__ hpj,
                                                        uint32_t* __restrict__ terms) {
@@ -277,28 +277,34 @@ __global__ void __launch_bounds__(64) k_rp_xd(int B, int n, int k, const int32_t
   store_g1j(terms + ((size_t)b * com_nterms(n) + n + 2 + h) * 24, r);
 }
 
-// one wave per proof: LDS tree over the n + 4 terms, + C -> hpj[b][n] (Jacobian)
+// 8 lanes per proof (8 proofs per 64-lane block): lane j sums terms j, j+8,
+// ... sequentially, then a 3-level LDS tree; lane 0 adds C.  -> hpj[b][n]
+// (Jacobian).  A wave-wide tree per proof would run 7 levels of additions
+// with most lanes masked off: 7x the wave instructions for the same sums.
+constexpr int COMSUM_LANES = 8;
 __global__ void __launch_bounds__(64) k_rp_com_sum(int B, int n, int k, const int32_t* __restrict__ status,
                                                    const uint32_t* __restrict__ pts, const uint32_t* __restrict__ terms,
                                                    uint32_t* __restrict__ hpj) {
   __shared__ uint32_t sh[64 * 24];
-  const int b = blockIdx.x, t = threadIdx.x;
-  if (status[b] != 0) return;  // uniform per block
+  const int t = threadIdx.x, p = t / COMSUM_LANES, j = t % COMSUM_LANES;
+  const int b = blockIdx.x * (64 / COMSUM_LANES) + p;
+  const bool live = b < B && status[b] == 0;
   const int nt = com_nterms(n);
-  const uint32_t* T = terms + (size_t)b * nt * 24;
-  const uint32_t* Pt = pts + (size_t)b * rp_npts(k) * 16;
   G1J acc = g1j_identity();
-  for (int q = t; q < nt; q += 64) add_inl(acc, load_g1j(T + q * 24));
-  if (t == 0) add_inl(acc, g1j_from_affine(load_g1a(Pt + RP_PT_C * 16)));  // + C
+  if (live) {
+    const uint32_t* T = terms + (size_t)b * nt * 24;
+    for (int q = j; q < nt; q += COMSUM_LANES) add_inl(acc, load_g1j(T + q * 24));
+    if (j == 0) add_inl(acc, g1j_from_affine(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_C) * 16)));  // + C
+  }
   store_g1j(sh + t * 24, acc);
   __syncthreads();
-  for (int half = 32; half >= 1; half >>= 1) {
-    if (t < half) add_inl(acc, load_g1j(sh + (t + half) * 24));
+  for (int half = COMSUM_LANES / 2; half >= 1; half >>= 1) {
+    if (live && j < half) add_inl(acc, load_g1j(sh + (t + half) * 24));
     __syncthreads();
-    if (t < half) store_g1j(sh + t * 24, acc);
+    if (j < half) store_g1j(sh + t * 24, acc);
     __syncthreads();
   }
-  if (t == 0) store_g1j(hpj + ((size_t)b * (n + 1) + n) * 24, acc);
+  if (live && j == 0) store_g1j(hpj + ((size_t)b * (n + 1) + n) * 24, acc);
 }
 
 // Batch affine normalisation, block of 256 lanes = 256 consecutive points
@@ -755,7 +761,8 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   FTS_LAUNCH(k_rp_fixed_exact, B * (2 * n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, tables, d.hpj, d.terms);
   tl->mark("k_rp_fixed_exact", s, (double)B * (2 * n + 2) * COST_FB);
   tl->fork(s2, s);
-  hipLaunchKernelGGL(k_rp_com_sum, dim3(B), dim3(64), 0, s, B, n, k, d.status, d.pts, d.terms, d.hpj);
+  hipLaunchKernelGGL(k_rp_com_sum, dim3((B + 64 / COMSUM_LANES - 1) / (64 / COMSUM_LANES)), dim3(64), 0, s, B, n, k,
+                     d.status, d.pts, d.terms, d.hpj);
   tl->mark("k_rp_com_sum", s, (double)B * (com_nterms(n) + 1) * COST_ADD);
   const int npt = B * (n + 1);
   FTS_LAUNCH(k_rp_normalize, npt, NORM_BS, s, npt, n + 1, d.status, d.hpj, d.hpa, d.hp_be);
