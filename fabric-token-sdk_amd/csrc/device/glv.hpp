@@ -177,10 +177,14 @@ FTS_DEV G1J vtab_load(const uint32_t* tab, int lane, int e) {
 
 // k * P for a 128-bit magnitude k (4 LE limbs, < 2^127): signed 4-bit
 // windows (32 windows), 1 + 6 table additions, 128 doublings, <= 32 additions.
+FTS_DEV G1J vb128j(const G1J& t, const uint32_t kk[4], uint32_t* tab, int lane);
 FTS_DEV G1J vb128(const G1A& p, const uint32_t kk[4], uint32_t* tab, int lane) {
   if (g1a_is_identity(p)) return g1j_identity();
+  return vb128j(g1j_from_affine(p), kk, tab, lane);
+}
+FTS_DEV G1J vb128j(const G1J& t, const uint32_t kk[4], uint32_t* tab, int lane) {
+  if (f_is_zero(t.z)) return g1j_identity();
   {
-    G1J t = g1j_from_affine(p);
     vtab_store(tab, lane, 0, t);
     G1J cur = g1j_dbl(t);
     vtab_store(tab, lane, 1, cur);

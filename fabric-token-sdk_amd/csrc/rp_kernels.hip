@@ -8,9 +8,11 @@
 //   S   k_rp_decode        (proof, point)   NewG1FromBytes checks + Montgomery form
 //   S   k_rp_hash_small    (proof, msg)     x, y, x_j transcripts (SHA-256 over hex)  bulletproof.go:266-281, ipa.go:230
 //   S   k_rp_chal_fr       proof            z, polEval, batch inversion of y, x_j       bulletproof.go:282-311, ipa.go:236-244
-//   S2  k_rp_xd            proof            x*D (variable base)                         bulletproof.go:478
-//   S   k_rp_fixed_exact   (proof, item)    H'_i = y^-i H_i; com terms (z^2 2^i y^-i) H_i, z K, -delta P
-//   S   k_rp_com_sum       proof (wave)     LDS tree of the com terms + x*D + C         bulletproof.go:477-492
+//   S2  k_rp_glv_terms     2 lanes/proof    x*D (GLV, variable base)                    bulletproof.go:478
+//   S   k_rp_fixed_exact   (proof, item)    H'_i = y^-i H_i, z K, -delta P (fixed base) bulletproof.go:483-489
+//   S   k_rp_hsum_chunks   (proof, chunk)   S_c = sum_j 2^j H'_{8c+j} (Horner)
+//   S   k_rp_glv_terms     2 lanes/proof    z^2 * S, S = sum_c 2^(8c) S_c
+//   S   k_rp_com_sum       proof            com = C + z K - delta P + x D + z^2 S       bulletproof.go:477-492
 //   S   k_rp_normalize     point (block)    batch affine normalisation of H'_i and com (one inversion per 256 points)
 //   S2  k_rp_x0_build      (proof, record)  DER(hex(H'..., G..., Q, com) "||" Zb(ip))   ipa.go:200-212
 //   S2  k_rp_x0_hash       proof            x0 = HashToZr(...)                          ipa.go:213
@@ -203,19 +205,23 @@ __global__ void __launch_bounds__(64) k_rp_chal_fr(int B, int n, int k, const in
 
 // ------------------------------------------------------------ H' and com
 // com = x*D + C - z sum G_i + sum (z y^i + z^2 2^i) H'_i - delta*P   (bulletproof.go:477-492)
-//     = x*D + C + z*K + sum_i (z^2 2^i y^-i) H_i - delta*P,   K = sum H_i - sum G_i
-// (same group element; only the affine result is observable).  Terms per
-// proof: slots 0..n-1 fixed-base on H_i, n: z*K, n+1: -delta*P,
-// n+2, n+3: the GLV halves x1*D and x2*phi(D) of x*D (x = x1 + x2 lambda).
-inline __host__ __device__ int com_nterms(int n) { return n + 4; }
+//     = x*D + C + z*K - delta*P + z^2 * S,   K = sum H_i - sum G_i,  S = sum_i 2^i H'_i
+// (z y^i H'_i = z H_i folds into z K; the same group element, and only its
+// affine form is observable).  S is a Horner sum over the exact H'_i, so
+// the n fixed-base products of the com terms become one variable-base product.
+// Terms per proof (com_terms): 0 z*K, 1 -delta*P, 2,3 the GLV halves of x*D,
+// 4,5 the GLV halves of z^2*S.
+constexpr int COM_NTERMS = 6;
+constexpr int HS_CHUNK = 8;  // H' per Horner chunk of S
+inline __host__ __device__ int com_nterms(int n) { return COM_NTERMS; }
 
 // lane per (proof, item): items 0..n-1: H'_i = y^-i H_i (-> hpj[b][i]);
-// n..2n-1: (z^2 2^(i) y^-i) H_i; 2n: z K; 2n+1: -delta P (-> terms[b][.])
+// n: z K; n+1: -delta P (-> terms[b][0..1])
 __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, const int32_t* __restrict__ status,
-                                                       const uint32_t* __restrict__ sc, const uint32_t* __restrict__ ch,
-                                                       const uint32_t* __restrict__ tables, uint32_t* __restrict__ hpj,
-                                                       uint32_t* __restrict__ terms) {
-  const int ni = 2 * n + 2;
+                                                          const uint32_t* __restrict__ sc, const uint32_t* __restrict__ ch,
+                                                          const uint32_t* __restrict__ tables, uint32_t* __restrict__ hpj,
+                                                          uint32_t* __restrict__ terms) {
+  const int ni = n + 2;
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * ni) return;
   const int b = gid / ni, t = gid % ni;
@@ -224,26 +230,18 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, c
   uint32_t* out;
   const uint32_t* tab;
   Scalar sk;
-  if (t < 2 * n) {
-    const int i = t < n ? t : t - n;
+  if (t < n) {
     Fr yinv;
     load_f(C + CH_YINV * 8, yinv);
-    Fr s = fr_pow_small(yinv, (uint32_t)i);
-    if (t >= n) {  // z^2 2^i y^-i
-      Fr z2;
-      load_f(C + CH_Z2 * 8, z2);
-      s = fr_mul(z2, s);
-      for (int q = 0; q < i; q++) s = f_dbl(s);
-    }
-    tab = tables + (size_t)(n + i) * FB_WORDS_PER_BASE;
-    sk = fr_canon(s);
-    out = t < n ? hpj + ((size_t)b * (n + 1) + i) * 24 : terms + ((size_t)b * com_nterms(n) + i) * 24;
-  } else if (t == 2 * n) {
+    tab = tables + (size_t)(n + t) * FB_WORDS_PER_BASE;
+    sk = fr_canon(fr_pow_small(yinv, (uint32_t)t));
+    out = hpj + ((size_t)b * (n + 1) + t) * 24;
+  } else if (t == n) {
     Fr z;
     load_f(C + CH_Z * 8, z);
     tab = tables + (size_t)tb_K(n) * FB_WORDS_PER_BASE;
     sk = fr_canon(z);
-    out = terms + ((size_t)b * com_nterms(n) + n) * 24;
+    out = terms + ((size_t)b * COM_NTERMS + 0) * 24;
   } else {
     Fr d;
     load_f(sc + ((size_t)b * RP_NSC + RP_SC_DELTA) * 8, d);  // canonical
@@ -251,60 +249,75 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, c
 #pragma unroll
     for (int q = 0; q < 8; q++) sk.v[q] = nd.v[q];
     tab = tables + (size_t)tb_P(n) * FB_WORDS_PER_BASE;
-    out = terms + ((size_t)b * com_nterms(n) + n + 1) * 24;
+    out = terms + ((size_t)b * COM_NTERMS + 1) * 24;
   }
   G1J r = fb_mul(tab, sk);
   store_g1j(out, r);
 }
 
-// two lanes per proof: the GLV halves of x*D (variable base), on the side stream
-__global__ void __launch_bounds__(64) k_rp_xd(int B, int n, int k, const int32_t* __restrict__ status,
-                                              const uint32_t* __restrict__ pts, const uint32_t* __restrict__ ch,
-                                              uint32_t* __restrict__ terms) {
+// lane per (proof, chunk c): S_c = sum_{j < 8} 2^j H'_{8c+j} (Horner, Jacobian H')
+__global__ void __launch_bounds__(64) k_rp_hsum_chunks(int B, int n, const int32_t* __restrict__ status,
+                                                       const uint32_t* __restrict__ hpj, uint32_t* __restrict__ chunks) {
+  const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= B * nc) return;
+  const int b = gid / nc, c = gid % nc;
+  if (status[b] != 0) return;
+  const int lo = c * HS_CHUNK, hi = min(n, lo + HS_CHUNK);
+  const uint32_t* H = hpj + (size_t)b * (n + 1) * 24;
+  G1J acc = load_g1j(H + (hi - 1) * 24);
+  for (int i = hi - 2; i >= lo; i--) {
+    acc = g1j_dbl(acc);
+    add_inl(acc, load_g1j(H + i * 24));
+  }
+  store_g1j(chunks + (size_t)gid * 24, acc);
+}
+
+// Variable-base GLV products, two lanes per proof (h = 0: k1*P, h = 1: k2*phi(P)):
+//   which = 0: x*D   (terms 2, 3)      bulletproof.go:478
+//   which = 1: z^2*S (terms 4, 5), S = sum_c 2^(8c) S_c assembled by Horner first
+__global__ void __launch_bounds__(64) k_rp_glv_terms(int B, int n, int k, int which, const int32_t* __restrict__ status,
+                                                     const uint32_t* __restrict__ pts, const uint32_t* __restrict__ ch,
+                                                     const uint32_t* __restrict__ chunks, uint32_t* __restrict__ terms) {
   __shared__ uint32_t tab[8 * 24 * 64];
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = gid >> 1, h = gid & 1;
   if (b >= B || status[b] != 0) return;
-  Fr x;
-  load_f(ch + ((size_t)b * rp_nch(k) + CH_X) * 8, x);
-  const Scalar xs = fr_canon(x);
+  const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
+  Fr s;
+  G1J P;
+  if (which == 0) {
+    load_f(C + CH_X * 8, s);
+    P = g1j_from_affine(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_D) * 16));
+  } else {
+    load_f(C + CH_Z2 * 8, s);
+    const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
+    const uint32_t* S = chunks + (size_t)b * nc * 24;
+    P = load_g1j(S + (nc - 1) * 24);
+    for (int c = nc - 2; c >= 0; c--) {
+      for (int q = 0; q < HS_CHUNK; q++) P = g1j_dbl(P);
+      add_inl(P, load_g1j(S + c * 24));
+    }
+  }
+  const Scalar sk = fr_canon(s);
   uint32_t k1[4], k2[4], s1, s2;
-  glv_decompose(xs.v, k1, s1, k2, s2);
-  G1A D = load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_D) * 16);
-  if (h) D.x = fp_mul(D.x, glv_beta());  // phi(D)
-  if (h ? s2 : s1) D = g1a_neg(D);
-  G1J r = vb128(D, h ? k2 : k1, tab, threadIdx.x);
-  store_g1j(terms + ((size_t)b * com_nterms(n) + n + 2 + h) * 24, r);
+  glv_decompose(sk.v, k1, s1, k2, s2);
+  if (h) P.x = fp_mul(P.x, glv_beta());  // phi
+  if (h ? s2 : s1) P.y = f_neg(P.y);
+  G1J r = vb128j(P, h ? k2 : k1, tab, threadIdx.x);
+  store_g1j(terms + ((size_t)b * COM_NTERMS + 2 + 2 * which + h) * 24, r);
 }
 
-// 8 lanes per proof (8 proofs per 64-lane block): lane j sums terms j, j+8,
-// ... sequentially, then a 3-level LDS tree; lane 0 adds C.  -> hpj[b][n]
-// (Jacobian).  A wave-wide tree per proof would run 7 levels of additions
-// with most lanes masked off: 7x the wave instructions for the same sums.
-constexpr int COMSUM_LANES = 8;
+// lane per proof: com = C + the 6 terms -> hpj[b][n] (Jacobian)
 __global__ void __launch_bounds__(64) k_rp_com_sum(int B, int n, int k, const int32_t* __restrict__ status,
                                                    const uint32_t* __restrict__ pts, const uint32_t* __restrict__ terms,
                                                    uint32_t* __restrict__ hpj) {
-  __shared__ uint32_t sh[64 * 24];
-  const int t = threadIdx.x, p = t / COMSUM_LANES, j = t % COMSUM_LANES;
-  const int b = blockIdx.x * (64 / COMSUM_LANES) + p;
-  const bool live = b < B && status[b] == 0;
-  const int nt = com_nterms(n);
-  G1J acc = g1j_identity();
-  if (live) {
-    const uint32_t* T = terms + (size_t)b * nt * 24;
-    for (int q = j; q < nt; q += COMSUM_LANES) add_inl(acc, load_g1j(T + q * 24));
-    if (j == 0) add_inl(acc, g1j_from_affine(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_C) * 16)));  // + C
-  }
-  store_g1j(sh + t * 24, acc);
-  __syncthreads();
-  for (int half = COMSUM_LANES / 2; half >= 1; half >>= 1) {
-    if (live && j < half) add_inl(acc, load_g1j(sh + (t + half) * 24));
-    __syncthreads();
-    if (j < half) store_g1j(sh + t * 24, acc);
-    __syncthreads();
-  }
-  if (live && j == 0) store_g1j(hpj + ((size_t)b * (n + 1) + n) * 24, acc);
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B || status[b] != 0) return;
+  const uint32_t* T = terms + (size_t)b * COM_NTERMS * 24;
+  G1J acc = g1j_from_affine(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_C) * 16));
+  for (int q = 0; q < COM_NTERMS; q++) add_inl(acc, load_g1j(T + q * 24));
+  store_g1j(hpj + ((size_t)b * (n + 1) + n) * 24, acc);
 }
 
 // Batch affine normalisation, block of 256 lanes = 256 consecutive points
@@ -756,14 +769,18 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   tl->mark("k_rp_chal_fr", s, (double)B * (3 * k + 4 * (k + 1) + 12));
   // side: x*D while the main stream runs the fixed-base products
   tl->fork(s, s2);
-  FTS_LAUNCH(k_rp_xd, 2 * B, 64, s2, B, n, k, d.status, d.pts, d.ch, d.terms);
+  FTS_LAUNCH(k_rp_glv_terms, 2 * B, 64, s2, B, n, k, 0, d.status, d.pts, d.ch, d.scratch, d.terms);
   tl->mark("k_rp_xd", s2, (double)B * 2 * COST_VB128);
-  FTS_LAUNCH(k_rp_fixed_exact, B * (2 * n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, tables, d.hpj, d.terms);
-  tl->mark("k_rp_fixed_exact", s, (double)B * (2 * n + 2) * COST_FB);
+  FTS_LAUNCH(k_rp_fixed_exact, B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, tables, d.hpj, d.terms);
+  tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FB);
+  const int nch = (n + HS_CHUNK - 1) / HS_CHUNK;
+  FTS_LAUNCH(k_rp_hsum_chunks, B * nch, 64, s, B, n, d.status, d.hpj, d.scratch);
+  tl->mark("k_rp_hsum_chunks", s, (double)B * (n - nch) * (COST_DBL + COST_ADD));
+  FTS_LAUNCH(k_rp_glv_terms, 2 * B, 64, s, B, n, k, 1, d.status, d.pts, d.ch, d.scratch, d.terms);
+  tl->mark("k_rp_zs", s, (double)B * (2 * COST_VB128 + 2 * (nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD)));
   tl->fork(s2, s);
-  hipLaunchKernelGGL(k_rp_com_sum, dim3((B + 64 / COMSUM_LANES - 1) / (64 / COMSUM_LANES)), dim3(64), 0, s, B, n, k,
-                     d.status, d.pts, d.terms, d.hpj);
-  tl->mark("k_rp_com_sum", s, (double)B * (com_nterms(n) + 1) * COST_ADD);
+  FTS_LAUNCH(k_rp_com_sum, B, 64, s, B, n, k, d.status, d.pts, d.terms, d.hpj);
+  tl->mark("k_rp_com_sum", s, (double)B * COM_NTERMS * COST_ADD);
   const int npt = B * (n + 1);
   FTS_LAUNCH(k_rp_normalize, npt, NORM_BS, s, npt, n + 1, d.status, d.hpj, d.hpa, d.hp_be);
   tl->mark("k_rp_normalize", s, (double)npt * (2 * 8.0 / 1.0 + 6.0));
