@@ -17,9 +17,11 @@ import json
 import os
 
 # Hardware queues per process: every lane uses two streams, and streams that
-# share a HIP hardware queue serialise.  Read once at HIP runtime init, so set
-# before anything initialises the GPU (lane sweep).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# share a HIP hardware queue serialise (the box's default is 4).  Read once at
+# HIP runtime load, so raised here before anything loads HIP (DESIGN.md §5,
+# lane sweep: 8 lanes run 2.4x faster with 16 queues than with 4).
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 import sys
 import threading
 import time
@@ -143,7 +145,7 @@ def main():
     # roofline kernel: the largest share of the algorithmic work (MADs/launch);
     # the longest (latency-bound) kernel is reported beside it
     dom = max(kt, key=lambda kname: kt[kname][1])
-    longest = max(avg, key=avg.get)
+    longest = max((kn for kn in avg if not kn.startswith("host_")), key=avg.get)
 
     def kernel_roof(kname):
         ms, mads = avg[kname], kt[kname][1]

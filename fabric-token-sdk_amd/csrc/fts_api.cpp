@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <condition_variable>
 #include <mutex>
@@ -112,7 +113,36 @@ struct Lane {
   hipStream_t s = nullptr, s2 = nullptr;
   Workspace ws;
   Timeline tl;
+  float host_prep_ms = 0, host_enqueue_ms = 0, host_wait_ms = 0;  // host wall time of the last run
+  // pinned host staging (pageable async copies would block the enqueue)
+  struct Pinned {
+    uint32_t key[8];
+    MsmWindow win[MSM_MAX_WINDOWS];
+    int32_t flag;
+  }* pin = nullptr;
+  int32_t* pin_status = nullptr;
+  size_t pin_status_cap = 0;
+  int32_t* status_buf(size_t n) {
+    if (n > pin_status_cap) {
+      if (pin_status) (void)hipHostFree(pin_status);
+      pin_status = nullptr;
+      pin_status_cap = 0;
+      if (hipHostMalloc((void**)&pin_status, std::max<size_t>(n, 4096) * 4, 0) != hipSuccess) return nullptr;
+      pin_status_cap = std::max<size_t>(n, 4096);
+    }
+    return pin_status;
+  }
+  void free_pinned() {
+    if (pin) (void)hipHostFree(pin);
+    if (pin_status) (void)hipHostFree(pin_status);
+    pin = nullptr;
+    pin_status = nullptr;
+    pin_status_cap = 0;
+  }
 };
+static inline double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 struct fts_ctx {
   int device = 0;
@@ -237,6 +267,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
       if (L->s2 && L->s2 != L->s) hipStreamDestroy(L->s2);
       if (L->s) hipStreamDestroy(L->s);
       L->tl.destroy();
+      L->free_pinned();
       delete L;
     }
     if (c->d_tables) hipFree(c->d_tables);
@@ -255,6 +286,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
     c->lanes.push_back(L);
     c->free_lanes.push_back(i);
     if (hipStreamCreateWithFlags(&L->s, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
+    if (hipHostMalloc((void**)&L->pin, sizeof(Lane::Pinned), 0) != hipSuccess) return fail(FTS_API_ENOMEM);
     if (!side) L->s2 = L->s;
     else if (hipStreamCreateWithFlags(&L->s2, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
     L->tl.create();
@@ -341,6 +373,7 @@ void fts_ctx_destroy(fts_ctx* c) {
     L->tl.destroy();
     if (L->s2 && L->s2 != L->s) hipStreamDestroy(L->s2);
     if (L->s) hipStreamDestroy(L->s);
+    L->free_pinned();
     delete L;
   }
   if (c->d_tables) hipFree(c->d_tables);
@@ -440,6 +473,14 @@ static void collect_timings(fts_ctx* c, Lane& L, fts_rp_batch* b) {
     c->tim_work[j] = L.tl.work[i];
     hipEventElapsedTime(&c->tim_ms[j], L.tl.ev[L.tl.start[i]], L.tl.ev[i + 1]);
   }
+  const char* hn[3] = {"host_prep", "host_enqueue", "host_wait_flag"};
+  const float hv[3] = {L.host_prep_ms, L.host_enqueue_ms, L.host_wait_ms};
+  for (int q = 0; q < 3 && c->ntim < Timeline::CAP; q++) {
+    c->tim_name[c->ntim] = hn[q];
+    c->tim_ms[c->ntim] = hv[q];
+    c->tim_work[c->ntim] = 0;
+    c->ntim++;
+  }
   if (b) {
     b->ntim = c->ntim;
     for (int j = 0; j < c->ntim; j++) {
@@ -460,6 +501,7 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   const int n = c->n, k = c->k, npts = rp_npts(k);
   Workspace& w = L.ws;
   const int N = B * npts;
+  const double t_start = now_ms();
   MsmPlan mp{};
   msm_layout(N, mp);
   if (w.pts.ensure((size_t)B * npts * 64) || w.ch.ensure((size_t)B * rp_nch(k) * 32) ||
@@ -494,7 +536,8 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
                w.terms.as<uint32_t>(),
                w.scratch.as<uint32_t>()};
   mp.d_win = w.m_win.as<MsmWindow>();
-  HIP_OK(hipMemcpyAsync(mp.d_win, mp.win, sizeof(MsmWindow) * mp.nw, hipMemcpyHostToDevice, L.s));
+  memcpy(L.pin->win, mp.win, sizeof(MsmWindow) * mp.nw);
+  HIP_OK(hipMemcpyAsync(mp.d_win, L.pin->win, sizeof(MsmWindow) * mp.nw, hipMemcpyHostToDevice, L.s));
   mp.keys = w.m_keys.as<int32_t>();
   mp.counts = w.m_counts.as<uint32_t>();
   mp.offsets = w.m_offsets.as<uint32_t>();
@@ -510,16 +553,21 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   RlcDev r{w.r_key.as<uint32_t>(), w.r_msc.as<uint32_t>(),   w.r_coef.as<uint32_t>(), w.r_colsum.as<uint32_t>(),
            w.r_fixed.as<uint32_t>(), w.r_flag.as<int32_t>(), w.m_scratch.as<uint32_t>(), mp};
   // fresh RLC weights key (getrandom), unpredictable to the provers
-  uint32_t key[8];
-  if (getrandom(key, sizeof key, 0) != (ssize_t)sizeof key) return FTS_API_EDEVICE;
-  HIP_OK(hipMemcpyAsync(r.key, key, sizeof key, hipMemcpyHostToDevice, L.s));
+  if (getrandom(L.pin->key, sizeof L.pin->key, 0) != (ssize_t)sizeof L.pin->key) return FTS_API_EDEVICE;
+  HIP_OK(hipMemcpyAsync(r.key, L.pin->key, sizeof L.pin->key, hipMemcpyHostToDevice, L.s));
+  const double t_prep = now_ms();
   L.tl.begin(L.s);
   launch_rp_batch(d, r, c->d_tables, c->d_x0const, L.s, L.s2, &L.tl);
   between();
   HIP_OK(hipGetLastError());
-  int32_t flag = 0;
-  HIP_OK(hipMemcpyAsync(&flag, r.flag, 4, hipMemcpyDeviceToHost, L.s));
+  HIP_OK(hipMemcpyAsync(&L.pin->flag, r.flag, 4, hipMemcpyDeviceToHost, L.s));
+  const double t_enq = now_ms();
   HIP_OK(hipStreamSynchronize(L.s));
+  const double t_wait = now_ms();
+  L.host_prep_ms = (float)(t_prep - t_start);
+  L.host_enqueue_ms = (float)(t_enq - t_prep);
+  L.host_wait_ms = (float)(t_wait - t_enq);
+  const int32_t flag = L.pin->flag;
   c->last_fallback = flag ? 0 : 1;
   if (!flag) {
     launch_rp_fallback(d, c->d_tables, L.s, &L.tl);
@@ -532,8 +580,11 @@ static int run_rp(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc, in
                   int32_t* host_status, fts_rp_batch* batch) {
   int rc = rp_pipeline(c, L, B, d_raw, d_sc, d_status, d_ipa, [] {});
   if (rc != FTS_API_OK) return rc;
-  if (host_status) HIP_OK(hipMemcpyAsync(host_status, d_status, (size_t)B * 4, hipMemcpyDeviceToHost, L.s));
+  int32_t* pst = host_status ? L.status_buf((size_t)B) : nullptr;
+  if (host_status && !pst) return FTS_API_ENOMEM;
+  if (host_status) HIP_OK(hipMemcpyAsync(pst, d_status, (size_t)B * 4, hipMemcpyDeviceToHost, L.s));
   HIP_OK(hipStreamSynchronize(L.s));
+  if (host_status) memcpy(host_status, pst, (size_t)B * 4);
   collect_timings(c, L, batch);
   return FTS_API_OK;
 }
