@@ -8,7 +8,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libfts_gpu.so")
+# FTS_LIB: alternative in-tree build of the same library (A/B experiments)
+LIB_PATH = os.environ.get("FTS_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libfts_gpu.so")
 
 # fts_status (include/fts_gpu.h)
 FTS_OK = 0
