@@ -46,9 +46,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--bits", type=int, default=64)
-    ap.add_argument("--lanes", type=int, default=int(os.environ.get("FTS_LANES", "8")),
-                    help="batches in flight (host threads / device lanes; FTS_LANES)")
-    ap.add_argument("--reuse-proofs", action="store_true", help="stage lane 0's proofs on every lane (faster setup)")
+    ap.add_argument("--inflight", type=int, default=16,
+                    help="batches in flight: host threads, each submitting its own staged batch")
+    ap.add_argument("--lanes", type=int, default=int(os.environ.get("FTS_LANES", "4")),
+                    help="device lanes (stream pairs) of the library (FTS_LANES); batches submitted while "
+                         "all lanes are busy are coalesced into one device pass (FTS_COALESCE_MAX proofs)")
+    ap.add_argument("--distinct", type=int, default=4,
+                    help="batches with distinct proofs; the other in-flight batches re-stage them (setup time)")
+    ap.add_argument("--roofline-steps", type=int, default=6,
+                    help="isolated steps (one batch alone on the GPU) for the per-kernel roofline")
     ap.add_argument("--cpu-sample", type=int, default=256, help="CPU baseline chunk size (0: skip the CPU baseline)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall-time bound of the CPU baseline sample")
@@ -65,6 +71,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    os.environ["FTS_LANES"] = str(max(1, args.lanes))
     import random
     import numpy as np
     import fts_gpu
@@ -73,34 +80,35 @@ def main():
         pp_raw = f.read()
     pp = fts_gpu.PublicParams(pp_raw, bit_length=args.bits, device=local)
     n, k, B = pp.bit_length, pp.rounds, args.batch
-    # one staged batch per lane (distinct proofs); lanes run concurrently
-    lanes = max(1, args.lanes)
+    # one staged batch per in-flight slot; the first `distinct` hold distinct
+    # proofs, the rest re-stage them (verification work does not depend on it)
+    inflight = max(1, args.inflight)
     t0 = time.time()
-    batches, proofs0, coms0 = [], None, None
-    for ln in range(lanes):
-        if ln > 0 and args.reuse_proofs:
-            batches.append(pp.stage_range_proofs(proofs0, coms0))
-            continue
-        rng = random.Random(0xF7A50002 + 7919 * rank + 104729 * ln)
-        vals = [rng.getrandbits(n) for _ in range(B)]
-        bfs = [rng.randrange(R_ORDER).to_bytes(32, "big") for _ in range(B)]
-        proofs, coms = pp.prove_range_batch(vals, bfs, seed=0xF7A50002 + 1000003 * rank + 7777 * ln)
-        if ln == 0:
-            proofs0, coms0 = proofs, coms
+    batches, sets = [], []
+    for ln in range(inflight):
+        if ln >= max(1, args.distinct):
+            proofs, coms = sets[ln % len(sets)]
+        else:
+            rng = random.Random(0xF7A50002 + 7919 * rank + 104729 * ln)
+            vals = [rng.getrandbits(n) for _ in range(B)]
+            bfs = [rng.randrange(R_ORDER).to_bytes(32, "big") for _ in range(B)]
+            proofs, coms = pp.prove_range_batch(vals, bfs, seed=0xF7A50002 + 1000003 * rank + 7777 * ln)
+            sets.append((proofs, coms))
         batches.append(pp.stage_range_proofs(proofs, coms))
+    proofs0, coms0 = sets[0]
     prove_s = time.time() - t0
 
     def run(ln, nsteps, sink):
         for _ in range(nsteps):
             st = batches[ln].verify(want_status=True)
-            sink.append((st, batches[ln].timings()))
+            sink.append((st, batches[ln].merged()))
 
     def pipelined(nsteps):
-        """nsteps batch verifications spread over the lanes (one host thread
-        per lane); for N > 1 every step's verdict bitmap is all-gathered."""
-        per = [nsteps // lanes + (1 if i < nsteps % lanes else 0) for i in range(lanes)]
-        sinks = [[] for _ in range(lanes)]
-        th = [threading.Thread(target=run, args=(i, per[i], sinks[i])) for i in range(lanes)]
+        """nsteps batch verifications spread over the in-flight slots (one host
+        thread each); for N > 1 every step's verdict bitmap is all-gathered."""
+        per = [nsteps // inflight + (1 if i < nsteps % inflight else 0) for i in range(inflight)]
+        sinks = [[] for _ in range(inflight)]
+        th = [threading.Thread(target=run, args=(i, per[i], sinks[i])) for i in range(inflight)]
         for t in th:
             t.start()
         for t in th:
@@ -114,7 +122,7 @@ def main():
                 dist.all_gather_into_tensor(out, bits)
         return res
 
-    pipelined(max(args.warmup, lanes))
+    pipelined(max(args.warmup, inflight))
     if dist is not None:
         import torch
         dist.barrier()
@@ -126,11 +134,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ok = int(sum(int((st == 0).sum()) for st, _ in res))  # verdicts of the timed steps
-    kt = {}
-    for _, tm in res:
-        for name, (ms, mads) in tm.items():
-            o = kt.get(name, (0.0, 0.0))
-            kt[name] = (o[0] + ms, mads)
+    merged_avg = sum(m for _, m in res) / max(1, len(res))
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -141,7 +145,19 @@ def main():
 
     total = world * B * args.steps
     value = total / elapsed
-    avg = {kname: v[0] / args.steps for kname, v in kt.items()}
+
+    # Roofline pass (after the timed region): one batch alone on the GPU, so
+    # each kernel's HIP-event time is its own (in the pipelined region kernels
+    # of several passes share the CUs and their event spans overlap).
+    kt = {}
+    R = max(1, args.roofline_steps)
+    for _ in range(R):
+        st = batches[0].verify(want_status=True)
+        assert int((st != 0).sum()) == 0
+        for name, (ms, mads) in batches[0].timings().items():
+            o = kt.get(name, (0.0, 0.0))
+            kt[name] = (o[0] + ms, mads)
+    avg = {kname: v[0] / R for kname, v in kt.items()}
     # roofline kernel: the largest share of the algorithmic work (MADs/launch);
     # the longest (latency-bound) kernel is reported beside it
     dom = max(kt, key=lambda kname: kt[kname][1])
@@ -163,6 +179,7 @@ def main():
     roofline = {"bound": "int32_valu (v_mad_u64_u32)", "kernel": dom, "achieved": rd["achieved"],
                 "peak": round(PEAK_TMAD, 3), "unit": "TMAD/s", "frac": rd["frac"], "traffic": traffic,
                 "kernel_ms": rd["kernel_ms"], "mads_per_launch": rd["mads_per_launch"],
+                "measured": "HIP events, %d isolated steps of one %d-proof batch after the timed region" % (R, B),
                 "pipeline_frac_survey_model": round(value / world * SURVEY_MAD_PER_RP64 / (PEAK_TMAD * 1e12), 4)}
     longest_kernel = kernel_roof(longest)
 
@@ -203,11 +220,13 @@ def main():
                        "batch_per_gpu": B, "bit_length": n, "rounds": k, "parallelism": "shard%d" % world},
             "accepted": ok,
             "verified": world * B * args.steps,
-            "lanes": lanes,
+            "inflight": inflight,
+            "device_lanes": args.lanes,
+            "merged_batches_avg": round(merged_avg, 2),
             "roofline": roofline,
             "longest_kernel": longest_kernel,
             "cpu_baseline": cpu,
-            "kernel_ms": {kname: round(v, 4) for kname, v in avg.items()},
+            "kernel_ms_isolated": {kname: round(v, 4) for kname, v in avg.items()},
             "prove_s": round(prove_s, 2),
         }
         print(json.dumps(out), flush=True)

@@ -13,6 +13,7 @@
 #include <chrono>
 #include <atomic>
 #include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -144,6 +145,14 @@ static inline double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// One fts_rp_batch_verify call waiting for (or being served by) a device pass.
+struct RpReq {
+  fts_rp_batch* b;
+  int32_t* status;  // caller's host status array (may be null)
+  int rc = 0;
+  bool done = false;
+};
+
 struct fts_ctx {
   int device = 0;
   PublicParams pp;
@@ -164,6 +173,10 @@ struct fts_ctx {
   float tim_ms[Timeline::CAP];
   double tim_work[Timeline::CAP];
   std::atomic<int> last_fallback{0};
+  // batch coalescing (fts_rp_batch_verify): staged batches submitted
+  // concurrently are merged into one device pass of up to coalesce_max proofs
+  std::deque<RpReq*> rp_pending;
+  size_t coalesce_max = 16384;
   std::once_flag prover_once;
   ProverTables ptab;
 };
@@ -194,6 +207,7 @@ struct LaneGuard {
 struct fts_rp_batch {
   int B = 0;
   int device = 0;
+  int merged = 1;  // batches in the device pass that verified it last
   // timings of this batch's last verification
   int ntim = 0;
   const char* tim_name[Timeline::CAP];
@@ -275,8 +289,9 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
     return code;
   };
   if (hipSetDevice(device) != hipSuccess) return fail(FTS_API_EDEVICE);
-  int nl = 8;
+  int nl = 4;
   if (const char* e = getenv("FTS_LANES")) nl = std::max(1, std::min(16, atoi(e)));
+  if (const char* e = getenv("FTS_COALESCE_MAX")) c->coalesce_max = (size_t)std::max(0L, atol(e));
   // FTS_SIDE_STREAM=0: run each lane's side work on its main stream
   bool side = true;
   if (const char* e = getenv("FTS_SIDE_STREAM")) side = atoi(e) != 0;
@@ -589,6 +604,55 @@ static int run_rp(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc, in
   return FTS_API_OK;
 }
 
+// One device pass over a group of staged batches: a single batch runs in
+// place; several are gathered (D2D) into the lane's contiguous input buffers,
+// verified as one batch, and their verdicts scattered back.
+static int run_rp_group(fts_ctx* c, Lane& L, const std::vector<RpReq*>& grp) {
+  if (grp.size() == 1) {
+    fts_rp_batch* b = grp[0]->b;
+    HIP_OK(hipMemcpyAsync(b->status, b->status0, (size_t)b->B * 4, hipMemcpyDeviceToDevice, L.s));
+    b->merged = 1;
+    return run_rp(c, L, b->B, b->raw, b->sc, b->status, b->ipa_flag, grp[0]->status, b);
+  }
+  const int npts = rp_npts(c->k);
+  size_t B = 0;
+  for (RpReq* q : grp) B += (size_t)q->b->B;
+  Workspace& w = L.ws;
+  if (w.rp_raw.ensure(B * npts * 64) || w.rp_sc.ensure(B * RP_NSC * 32) || w.rp_status.ensure(B * 4) ||
+      w.rp_ipa.ensure(B * 4))
+    return FTS_API_ENOMEM;
+  size_t off = 0;
+  for (RpReq* q : grp) {
+    const fts_rp_batch* b = q->b;
+    const size_t m = (size_t)b->B;
+    HIP_OK(hipMemcpyAsync(w.rp_raw.as<uint8_t>() + off * npts * 64, b->raw, m * npts * 64, hipMemcpyDeviceToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.rp_sc.as<uint8_t>() + off * RP_NSC * 32, b->sc, m * RP_NSC * 32, hipMemcpyDeviceToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.rp_status.as<int32_t>() + off, b->status0, m * 4, hipMemcpyDeviceToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.rp_ipa.as<int32_t>() + off, b->ipa_flag, m * 4, hipMemcpyDeviceToDevice, L.s));
+    off += m;
+  }
+  int rc = rp_pipeline(c, L, (int)B, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
+                       w.rp_ipa.as<int32_t>(), [] {});
+  if (rc != FTS_API_OK) return rc;
+  int32_t* pst = L.status_buf(B);
+  if (!pst) return FTS_API_ENOMEM;
+  HIP_OK(hipMemcpyAsync(pst, w.rp_status.as<int32_t>(), B * 4, hipMemcpyDeviceToHost, L.s));
+  off = 0;
+  for (RpReq* q : grp) {  // device verdicts of each batch, as a lone run leaves them
+    HIP_OK(hipMemcpyAsync(q->b->status, w.rp_status.as<int32_t>() + off, (size_t)q->b->B * 4, hipMemcpyDeviceToDevice, L.s));
+    off += (size_t)q->b->B;
+  }
+  HIP_OK(hipStreamSynchronize(L.s));
+  off = 0;
+  for (RpReq* q : grp) {
+    if (q->status) memcpy(q->status, pst + off, (size_t)q->b->B * 4);
+    off += (size_t)q->b->B;
+    collect_timings(c, L, q->b);
+    q->b->merged = (int)grp.size();
+  }
+  return FTS_API_OK;
+}
+
 extern "C" {
 
 // debug/parity hook: intermediates of proof i of the last range-proof run
@@ -678,10 +742,42 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
   if (c->device < 0) return FTS_API_EDEVICE;
   if (b->B == 0) return FTS_API_OK;
   HIP_OK(hipSetDevice(c->device));
-  LaneGuard lg(c);
-  Lane& L = *lg.L;
-  HIP_OK(hipMemcpyAsync(b->status, b->status0, (size_t)b->B * 4, hipMemcpyDeviceToDevice, L.s));
-  return run_rp(c, L, b->B, b->raw, b->sc, b->status, b->ipa_flag, status, b);
+  // Work-sharing dispatcher: the request joins the pending queue; any waiting
+  // caller that finds a free lane takes the queue's head group (FIFO, up to
+  // coalesce_max proofs) and runs it as ONE device pass, so batches submitted
+  // while the lanes are busy are merged (a 4,096-proof batch alone fills only
+  // 64 waves in the per-proof chain kernels).  Verdicts stay per proof.
+  RpReq me{b, status};
+  std::unique_lock<std::mutex> lk(c->mu);
+  c->rp_pending.push_back(&me);
+  c->cv.notify_all();
+  while (!me.done) {
+    if (c->free_lanes.empty() || c->rp_pending.empty()) {
+      c->cv.wait(lk);
+      continue;
+    }
+    Lane* L = c->lanes[c->free_lanes.back()];
+    c->free_lanes.pop_back();
+    std::vector<RpReq*> grp;
+    size_t tot = 0;
+    while (!c->rp_pending.empty()) {
+      RpReq* q = c->rp_pending.front();
+      if (!grp.empty() && tot + (size_t)q->b->B > c->coalesce_max) break;
+      grp.push_back(q);
+      tot += (size_t)q->b->B;
+      c->rp_pending.pop_front();
+    }
+    lk.unlock();
+    const int rc = run_rp_group(c, *L, grp);
+    lk.lock();
+    for (RpReq* q : grp) {
+      q->rc = rc;
+      q->done = true;
+    }
+    c->free_lanes.push_back(L->id);
+    c->cv.notify_all();
+  }
+  return me.rc;
 }
 
 int fts_rp_batch_timings(const fts_rp_batch* b, const char** names, float* ms, double* mads, int cap) {
@@ -694,6 +790,8 @@ int fts_rp_batch_timings(const fts_rp_batch* b, const char** names, float* ms, d
   }
   return m;
 }
+
+int fts_rp_batch_merged(const fts_rp_batch* b) { return b ? b->merged : 0; }
 
 void fts_rp_batch_free(fts_rp_batch* b) {
   if (!b) return;

@@ -236,6 +236,10 @@ class StagedRangeBatch:
             self.pp._ctx, self._b, st.ctypes.data_as(C.POINTER(C.c_int32)) if want_status else None))
         return st
 
+    def merged(self):
+        """staged batches in the device pass that verified this one last (coalescing)"""
+        return int(L.lib.fts_rp_batch_merged(self._b))
+
     def timings(self):
         """{kernel: (ms, algorithmic u32 MADs)} of this batch's last verify()"""
         names = (C.c_char_p * 64)()

@@ -79,3 +79,65 @@ def test_concurrent_lanes_rp32(gpu_pp):
         for st in out[t]:
             assert st == expect[t]
         batches[t].close()
+
+
+def test_coalesced_batches_keep_their_verdicts(pp_raw):
+    """With ONE device lane, batches submitted concurrently are coalesced into
+    shared device passes (fts_rp_batch_verify's dispatcher).  Each caller must
+    still get exactly its own per-proof verdicts, including the per-proof
+    fallback (tampered proofs make the merged combination fail)."""
+    import os
+    import threading
+
+    import fts_gpu
+
+    old = os.environ.get("FTS_LANES")
+    os.environ["FTS_LANES"] = "1"
+    try:
+        pp = fts_gpu.PublicParams(pp_raw, bit_length=16, device=0)
+    finally:
+        if old is None:
+            del os.environ["FTS_LANES"]
+        else:
+            os.environ["FTS_LANES"] = old
+    rng = random.Random(0xC0A1E5CE)
+    sizes = [1, 7, 64, 200, 33, 128, 5, 90]
+    batches, expect = [], []
+    for t, m in enumerate(sizes):
+        vals = [rng.getrandbits(16) for _ in range(m)]
+        bfs = [rng.randrange(bn.R).to_bytes(32, "big") for _ in range(m)]
+        proofs, coms = pp.prove_range_batch(vals, bfs, seed=5000 + t)
+        exp = [0] * m
+        if t % 2 == 1:  # odd batches carry tampered proofs of both classes
+            for i in rng.sample(range(m), min(m, 2 + t // 2)):
+                r = zkat.RangeProof.deserialize(proofs[i])
+                if rng.random() < 0.5:
+                    r.data.T1 = bn.g1_add(r.data.T1, bn.GEN)
+                    exp[i] = 3
+                else:
+                    r.ipa.R[rng.randrange(4)] = bn.g1_add(r.ipa.R[0], bn.GEN)
+                    exp[i] = 6
+                proofs[i] = r.serialize()
+        batches.append(pp.stage_range_proofs(proofs, coms))
+        expect.append(exp)
+    out = [[] for _ in batches]
+    merged = []
+
+    def work(t):
+        for _ in range(4):
+            out[t].append([int(s) for s in batches[t].verify()])
+            merged.append(batches[t].merged())
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(len(batches))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    for t in range(len(batches)):
+        assert len(out[t]) == 4
+        for st in out[t]:
+            assert st == expect[t], t
+    assert max(merged) > 1, merged  # the dispatcher did merge batches
+    for b in batches:
+        b.close()
+    pp.close()

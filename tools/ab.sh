@@ -9,7 +9,7 @@ for lib in $LIBS; do
   echo "== $lib"
   FTS_LIB=$lib TAG=$(basename $lib) timeout -k 10 120 python3 tools/kernel_times.py 4096 5 || exit 1
   for ln in ${BENCH_LANES:-8}; do
-    r=$(FTS_LIB=$lib timeout -k 10 150 python3 bench.py --steps ${STEPS:-64} --warmup 8 --lanes $ln --cpu-sample 0 --reuse-proofs 2>/dev/null | grep '^{' | python3 -c "import json,sys; d=json.load(sys.stdin); print(round(d['value']), d['ms_per_step'])") || exit 1
+    r=$(FTS_LIB=$lib timeout -k 10 150 python3 bench.py --steps ${STEPS:-64} --warmup 8 --lanes $ln --distinct 1 --cpu-sample 0 --roofline-steps 1 2>/dev/null | grep '^{' | python3 -c "import json,sys; d=json.load(sys.stdin); print(round(d['value']), d['ms_per_step'])") || exit 1
     echo "bench lanes=$ln -> $r"
   done
 done
