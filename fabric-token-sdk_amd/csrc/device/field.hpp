@@ -28,6 +28,9 @@ struct FpP {
                                      0x0a417ff6u, 0x47ab1effu, 0xcab8351fu, 0x06d89f71u};
   static constexpr uint32_t R3[8] = {0xda1530dfu, 0xb1cd6dafu, 0xa7283db6u, 0x62f210e6u,
                                      0x0ada0afbu, 0xef7f0b0cu, 0x2d592544u, 0x20fd6e90u};
+  // 2^34 R^3 mod M: final factor of f_inv_gcd (17 outer steps x (32 - 30) bits)
+  static constexpr uint32_t GCDC[8] = {0x13bd45e1u, 0x31d6a0d9u, 0x382c59a2u, 0x45fbf2bcu,
+                                       0x1ab31dfbu, 0x5b5fa369u, 0xb36fd339u, 0x24811383u};
 };
 
 struct FrP {
@@ -40,6 +43,8 @@ struct FrP {
                                      0x53bb8085u, 0x8c49833du, 0x7f4e44a5u, 0x0216d0b1u};
   static constexpr uint32_t R3[8] = {0xb4bf0040u, 0x5e94d8e1u, 0x1cfbb6b8u, 0x2a489cbeu,
                                      0xa19fcfedu, 0x893cc664u, 0x7fcc657cu, 0x0cf8594bu};
+  static constexpr uint32_t GCDC[8] = {0xdd8b6d21u, 0x352ff640u, 0x331ce10au, 0x011e8bd1u,
+                                       0x55d392c2u, 0x438150aeu, 0x73335b20u, 0x21fe9388u};
 };
 
 template <class P>
@@ -736,6 +741,173 @@ FTS_DEV Field<P> f_inv_bin(const Field<P>& a) {
     r3.v[i] = P::R3[i];
   }
   return f_mul(r, r3);
+}
+
+
+// Constant-time inverse by the optimised binary GCD (T. Pornin, "Optimized
+// Binary GCD for Modular Inversion", 2020, Alg. 2), branch-free so the 64
+// lanes of a wave never diverge (f_inv_bin's three-way branch serialises
+// them).  Each of 17 outer steps runs 30 divsteps on 64-bit approximations
+// of a, b (low 31 bits exact + top 33 bits), collecting the transition
+// matrix (f0 g0; f1 g1), |f|,|g| <= 2^30; then applies it exactly to the
+// 256-bit a, b and, divided by 2^32 (one Montgomery word step), to the
+// Bezout coefficients u, v.  Invariant: b == v * y * 4^i (mod M) after i
+// steps, ending at a = 0, b = 1, so y^-1 = v * 2^34.  With y = A = aR the
+// Montgomery product by GCDC = 2^34 R^3 yields a^-1 R.  inv(0) = 0.
+// 2 * 254 - 1 = 507 <= 17 * 30 divsteps suffice (Pornin, Thm. 1).
+FTS_DEV uint32_t gcd_sel(bool c, uint32_t x, uint32_t y) { return c ? x : y; }
+
+// r (9 limbs, two's complement) = a * f + b * g   (a, b < 2^256 unsigned; f, g signed, |.| <= 2^30)
+FTS_DEV void gcd_lincomb(const uint32_t a[8], int32_t f, const uint32_t b[8], int32_t g, uint32_t r[9]) {
+  const uint32_t fa = (uint32_t)(f < 0 ? -f : f), ga = (uint32_t)(g < 0 ? -g : g);
+  uint32_t pa[9], pb[9];
+  uint64_t ca = 0, cb = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    ca = (uint64_t)a[i] * fa + (ca >> 32);
+    cb = (uint64_t)b[i] * ga + (cb >> 32);
+    pa[i] = (uint32_t)ca;
+    pb[i] = (uint32_t)cb;
+  }
+  pa[8] = (uint32_t)(ca >> 32);
+  pb[8] = (uint32_t)(cb >> 32);
+  // conditional negation: x -> (x ^ m) - m with m = all-ones if negative
+  const uint32_t ma = f < 0 ? 0xffffffffu : 0u, mb = g < 0 ? 0xffffffffu : 0u;
+  uint32_t c1 = ma & 1u, c2 = mb & 1u, c3 = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint32_t x = addc(pa[i] ^ ma, 0u, c1, c1);
+    const uint32_t y = addc(pb[i] ^ mb, 0u, c2, c2);
+    r[i] = addc(x, y, c3, c3);
+  }
+}
+
+template <class P>
+FTS_DEV Field<P> f_inv_gcd(const Field<P>& y) {
+  if (f_is_zero(y)) return y;
+  uint32_t a[8], b[8], u[8], v[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a[i] = y.v[i];
+    b[i] = P::M[i];
+    u[i] = 0;
+    v[i] = 0;
+  }
+  u[0] = 1;
+  for (int it = 0; it < 17; it++) {
+    // n = max(len a, len b, 64); approximations: low 31 bits | top 33 bits << 31
+    uint32_t top = 0;
+    int ti = 1;
+#pragma unroll
+    for (int i = 1; i < 8; i++) {
+      const uint32_t o = a[i] | b[i];
+      ti = o ? i : ti;
+      top = o ? o : top;
+    }
+    const int n = max(32 * ti + 32 - __clz(top | 1u), 64);
+    const int sh = n - 33, wi = sh >> 5, bo = sh & 31;
+    uint32_t al = 0, ah = 0, bl = 0, bh = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      al = gcd_sel(i == wi, a[i], al);
+      ah = gcd_sel(i == wi + 1, a[i], ah);
+      bl = gcd_sel(i == wi, b[i], bl);
+      bh = gcd_sel(i == wi + 1, b[i], bh);
+    }
+    const uint64_t atop = ((((uint64_t)ah << 32) | al) >> bo) & 0x1ffffffffull;
+    const uint64_t btop = ((((uint64_t)bh << 32) | bl) >> bo) & 0x1ffffffffull;
+    uint64_t xa = (atop << 31) | (a[0] & 0x7fffffffu);
+    uint64_t xb = (btop << 31) | (b[0] & 0x7fffffffu);
+    int32_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+#pragma unroll
+    for (int j = 0; j < 30; j++) {
+      const bool odd = (xa & 1u) != 0;
+      const bool sw = odd && xa < xb;
+      const uint64_t ta = sw ? xb : xa, tb = sw ? xa : xb;
+      const int32_t tf0 = sw ? f1 : f0, tg0 = sw ? g1 : g0, tf1 = sw ? f0 : f1, tg1 = sw ? g0 : g1;
+      xb = tb;
+      f1 = tf1;
+      g1 = tg1;
+      xa = odd ? ta - tb : ta;
+      f0 = odd ? tf0 - tf1 : tf0;
+      g0 = odd ? tg0 - tg1 : tg0;
+      xa >>= 1;
+      f1 *= 2;
+      g1 *= 2;
+    }
+    // (a, b) <- ((a f0 + b g0), (a f1 + b g1)) / 2^30, made non-negative
+    uint32_t na[9], nb[9];
+    gcd_lincomb(a, f0, b, g0, na);
+    gcd_lincomb(a, f1, b, g1, nb);
+    const bool nega = (int32_t)na[8] < 0, negb = (int32_t)nb[8] < 0;
+    {
+      const uint32_t m1 = nega ? 0xffffffffu : 0u, m2 = negb ? 0xffffffffu : 0u;
+      uint32_t c1 = m1 & 1u, c2 = m2 & 1u;
+#pragma unroll
+      for (int i = 0; i < 9; i++) {
+        na[i] = addc(na[i] ^ m1, 0u, c1, c1);
+        nb[i] = addc(nb[i] ^ m2, 0u, c2, c2);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        a[i] = (na[i] >> 30) | (na[i + 1] << 2);
+        b[i] = (nb[i] >> 30) | (nb[i + 1] << 2);
+      }
+    }
+    if (nega) {
+      f0 = -f0;
+      g0 = -g0;
+    }
+    if (negb) {
+      f1 = -f1;
+      g1 = -g1;
+    }
+    // (u, v) <- ((u f0 + v g0), (u f1 + v g1)) / 2^32 mod M
+    uint32_t wu[9], wv[9];
+    gcd_lincomb(u, f0, v, g0, wu);
+    gcd_lincomb(u, f1, v, g1, wv);
+    uint32_t* ws[2] = {wu, wv};
+    uint32_t* outs[2] = {u, v};
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      uint32_t* w = ws[q];
+      // w + m * M, m = w0 * (-M^-1) mod 2^32: low word cancels; (w + m M) / 2^32 in (-M/2, 3M/2)
+      const uint32_t mq = w[0] * P::INV;
+      uint64_t c = 0;
+      uint32_t t[10];
+      const uint32_t sgn = (int32_t)w[8] < 0 ? 0xffffffffu : 0u;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        c = (uint64_t)mq * P::M[i] + w[i] + (c >> 32);
+        t[i] = (uint32_t)c;
+      }
+      uint32_t cc = 0;
+      t[8] = addc(w[8], (uint32_t)(c >> 32), 0u, cc);
+      t[9] = sgn + cc;  // sign extension + carry
+      // r = t >> 32 (9 limbs: t[1..9]); add M if negative, subtract M if >= M
+      const bool neg = (int32_t)t[9] < 0;
+      uint32_t r[8], bw = 0, ce = 0;
+      const uint32_t madd = neg ? 0xffffffffu : 0u;
+#pragma unroll
+      for (int i = 0; i < 8; i++) r[i] = addc(t[i + 1], P::M[i] & madd, ce, ce);
+      uint32_t s2[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) s2[i] = subb(r[i], P::M[i], bw, bw);
+      // r >= M iff no borrow (when r was non-negative; after +M a negative r is < M)
+      const bool ge = !bw && !neg;
+      // top word of the 9-limb value when positive can carry into limb 8 (t[9]) -> treat as >= M
+      const bool big = !neg && t[9] != 0;
+#pragma unroll
+      for (int i = 0; i < 8; i++) outs[q][i] = (ge || big) ? s2[i] : r[i];
+    }
+  }
+  Field<P> r, c;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    r.v[i] = v[i];
+    c.v[i] = P::GCDC[i];
+  }
+  return f_mul(r, c);
 }
 
 // canonical (non-Montgomery) limbs < M ?

@@ -138,8 +138,8 @@ FTS_DEV G1J g1j_add(const G1J& p, const G1J& q) {
   return r;
 }
 
-__device__ __noinline__ Fp nl_fp_inv(Fp a) { return f_inv_bin(a); }
-__device__ __noinline__ Fr nl_fr_inv(Fr a) { return f_inv_bin(a); }
+__device__ __noinline__ Fp nl_fp_inv(Fp a) { return f_inv_gcd(a); }
+__device__ __noinline__ Fr nl_fr_inv(Fr a) { return f_inv_gcd(a); }
 
 // equality of two Jacobian points (as group elements)
 FTS_DEV bool g1j_eq(const G1J& p, const G1J& q) {

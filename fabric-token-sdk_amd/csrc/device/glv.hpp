@@ -154,43 +154,43 @@ FTS_DEV void add_inl(G1J& p, const G1J& q) {
   p.y = y3;
 }
 
-// LDS-resident per-lane table of 1..8 * P: [entry][word][64 lanes] (one bank
-// column per lane, conflict-free).  `tab` points at this wave's 8*24*64 words.
-FTS_DEV void vtab_store(uint32_t* tab, int lane, int e, const G1J& p) {
+// Per-lane table of 1..8 * P in global memory, [entry][word][stride] with
+// stride = lanes of the launch and idx = the lane's global id (coalesced when
+// neighbouring lanes use the same entry; 768 B per lane, L2/MALL-resident).
+// Kept out of LDS: a 48 KB LDS table per 64-lane block capped the kernel at
+// 3 waves per CU.
+FTS_DEV void vtab_store(uint32_t* __restrict__ tab, size_t stride, size_t idx, int e, const G1J& p) {
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    tab[((e * 24) + i) * 64 + lane] = p.x.v[i];
-    tab[((e * 24) + 8 + i) * 64 + lane] = p.y.v[i];
-    tab[((e * 24) + 16 + i) * 64 + lane] = p.z.v[i];
+    tab[((size_t)(e * 24) + i) * stride + idx] = p.x.v[i];
+    tab[((size_t)(e * 24) + 8 + i) * stride + idx] = p.y.v[i];
+    tab[((size_t)(e * 24) + 16 + i) * stride + idx] = p.z.v[i];
   }
 }
-FTS_DEV G1J vtab_load(const uint32_t* tab, int lane, int e) {
+FTS_DEV G1J vtab_load(const uint32_t* __restrict__ tab, size_t stride, size_t idx, int e) {
   G1J p;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    p.x.v[i] = tab[((e * 24) + i) * 64 + lane];
-    p.y.v[i] = tab[((e * 24) + 8 + i) * 64 + lane];
-    p.z.v[i] = tab[((e * 24) + 16 + i) * 64 + lane];
+    p.x.v[i] = tab[((size_t)(e * 24) + i) * stride + idx];
+    p.y.v[i] = tab[((size_t)(e * 24) + 8 + i) * stride + idx];
+    p.z.v[i] = tab[((size_t)(e * 24) + 16 + i) * stride + idx];
   }
   return p;
 }
 
 // k * P for a 128-bit magnitude k (4 LE limbs, < 2^127): signed 4-bit
-// windows (32 windows), 1 + 6 table additions, 128 doublings, <= 32 additions.
-FTS_DEV G1J vb128j(const G1J& t, const uint32_t kk[4], uint32_t* tab, int lane);
-FTS_DEV G1J vb128(const G1A& p, const uint32_t kk[4], uint32_t* tab, int lane) {
-  if (g1a_is_identity(p)) return g1j_identity();
-  return vb128j(g1j_from_affine(p), kk, tab, lane);
-}
-FTS_DEV G1J vb128j(const G1J& t, const uint32_t kk[4], uint32_t* tab, int lane) {
+// windows (32 windows), 1 + 6 table additions, 124 doublings, <= 32 additions.
+// The table entry of a window is loaded before that window's 4 doublings, so
+// its latency hides behind them.
+FTS_DEV G1J vb128j(const G1J& t, const uint32_t kk[4], uint32_t* __restrict__ tab, size_t stride, size_t idx) {
   if (f_is_zero(t.z)) return g1j_identity();
   {
-    vtab_store(tab, lane, 0, t);
+    vtab_store(tab, stride, idx, 0, t);
     G1J cur = g1j_dbl(t);
-    vtab_store(tab, lane, 1, cur);
+    vtab_store(tab, stride, idx, 1, cur);
     for (int e = 2; e < 8; e++) {
       add_inl(cur, t);
-      vtab_store(tab, lane, e, cur);
+      vtab_store(tab, stride, idx, e, cur);
     }
   }
   uint32_t s[4];
@@ -209,8 +209,6 @@ FTS_DEV G1J vb128j(const G1J& t, const uint32_t kk[4], uint32_t* tab, int lane) 
   }
   G1J acc = g1j_identity();
   for (int w = 31; w >= 0; w--) {
-    if (w != 31)
-      for (int q = 0; q < 4; q++) acc = g1j_dbl(acc);
     // window w raw nibble (s shifted left by 4 each step: MSB nibble of s[3])
     int raw = (int)(s[3] >> 28);
     s[3] = (s[3] << 4) | (s[2] >> 28);
@@ -220,10 +218,73 @@ FTS_DEV G1J vb128j(const G1J& t, const uint32_t kk[4], uint32_t* tab, int lane) 
     int cin = (int)((cm >> w) & 1u);
     int cout = w < 31 ? (int)((cm >> (w + 1)) & 1u) : 0;
     int d = raw + cin - 16 * cout;
+    G1J q;
+    if (d != 0) q = vtab_load(tab, stride, idx, (d < 0 ? -d : d) - 1);
+    if (w != 31)
+      for (int r = 0; r < 4; r++) acc = g1j_dbl(acc);
     if (d != 0) {
-      G1J q = vtab_load(tab, lane, (d < 0 ? -d : d) - 1);
       if (d < 0) q.y = f_neg(q.y);
       add_inl(acc, q);
+    }
+  }
+  return acc;
+}
+
+// Joint GLV/Straus half: a * P + b * Q for 127-bit magnitudes a, b (4 LE
+// limbs each, signs already folded into P, Q): ONE chain of 124 doublings
+// with <= 2 x 32 additions (two separate products double 2 x 124 times).
+// Tables 1..8 * P (entries 0..7) and 1..8 * Q (8..15) in global memory as
+// vtab_*; both window entries are loaded before the window's doublings.
+FTS_DEV uint32_t recode_carries(const uint32_t s[4]) {
+  uint32_t cm = 0;
+  int carry = 0;
+#pragma unroll
+  for (int w = 0; w < 32; w++) {
+    cm |= (uint32_t)carry << w;
+    int d = (int)((s[w >> 3] >> (4 * (w & 7))) & 0xfu) + carry;
+    carry = d > 8;
+  }
+  return cm;
+}
+FTS_DEV int window_digit(const uint32_t s[4], uint32_t cm, int w) {
+  const int raw = (int)((s[w >> 3] >> (4 * (w & 7))) & 0xfu);
+  const int cin = (int)((cm >> w) & 1u);
+  const int cout = w < 31 ? (int)((cm >> (w + 1)) & 1u) : 0;
+  return raw + cin - 16 * cout;
+}
+FTS_DEV void vtab_build(const G1J& t, uint32_t* __restrict__ tab, size_t stride, size_t idx, int e0) {
+  vtab_store(tab, stride, idx, e0, t);
+  if (f_is_zero(t.z)) {  // identity: every multiple is the identity
+    for (int e = 1; e < 8; e++) vtab_store(tab, stride, idx, e0 + e, t);
+    return;
+  }
+  G1J cur = g1j_dbl(t);
+  vtab_store(tab, stride, idx, e0 + 1, cur);
+  for (int e = 2; e < 8; e++) {
+    add_inl(cur, t);
+    vtab_store(tab, stride, idx, e0 + e, cur);
+  }
+}
+FTS_DEV G1J straus2_128(const G1J& P, const uint32_t a[4], const G1J& Q, const uint32_t b[4], uint32_t* __restrict__ tab,
+                        size_t stride, size_t idx) {
+  vtab_build(P, tab, stride, idx, 0);
+  vtab_build(Q, tab, stride, idx, 8);
+  const uint32_t ca = recode_carries(a), cb = recode_carries(b);
+  G1J acc = g1j_identity();
+  for (int w = 31; w >= 0; w--) {
+    const int da = window_digit(a, ca, w), db = window_digit(b, cb, w);
+    G1J qa, qb;
+    if (da != 0) qa = vtab_load(tab, stride, idx, (da < 0 ? -da : da) - 1);
+    if (db != 0) qb = vtab_load(tab, stride, idx, 8 + (db < 0 ? -db : db) - 1);
+    if (w != 31)
+      for (int r = 0; r < 4; r++) acc = g1j_dbl(acc);
+    if (da != 0) {
+      if (da < 0) qa.y = f_neg(qa.y);
+      add_inl(acc, qa);
+    }
+    if (db != 0) {
+      if (db < 0) qb.y = f_neg(qb.y);
+      add_inl(acc, qb);
     }
   }
   return acc;

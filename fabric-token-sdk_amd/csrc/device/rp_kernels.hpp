@@ -49,6 +49,7 @@ constexpr double COST_DBL = 7.0;      // dbl-2009-l 2M + 5S
 constexpr double COST_FB = 16.0 * COST_MADD;   // fixed-base, 16 signed 16-bit windows (fixed_base.hpp)
 constexpr double COST_VB4 = 7.0 + 6.0 * COST_MADD + 256.0 * COST_DBL + 60.0 * COST_ADD;  // 4-bit var-base
 constexpr double COST_VB128 = 7.0 + 6.0 * COST_ADD + 124.0 * COST_DBL + 30.0 * COST_ADD;  // GLV half (glv.hpp)
+constexpr double COST_STRAUS2 = 2.0 * (7.0 + 6.0 * COST_ADD) + 124.0 * COST_DBL + 60.0 * COST_ADD;  // glv.hpp straus2_128
 constexpr double COST_NORM = 7.0;     // batched affine normalisation, per point
 
 // Per-kernel device timeline: an event is recorded on the launching stream

@@ -8,10 +8,9 @@
 //   S   k_rp_decode        (proof, point)   NewG1FromBytes checks + Montgomery form
 //   S   k_rp_hash_small    (proof, msg)     x, y, x_j transcripts (SHA-256 over hex)  bulletproof.go:266-281, ipa.go:230
 //   S   k_rp_chal_fr       proof            z, polEval, batch inversion of y, x_j       bulletproof.go:282-311, ipa.go:236-244
-//   S2  k_rp_glv_terms     2 lanes/proof    x*D (GLV, variable base)                    bulletproof.go:478
 //   S   k_rp_fixed_exact   (proof, item)    H'_i = y^-i H_i, z K, -delta P (fixed base) bulletproof.go:483-489
 //   S   k_rp_hsum_chunks   (proof, chunk)   S_c = sum_j 2^j H'_{8c+j} (Horner)
-//   S   k_rp_glv_terms     2 lanes/proof    z^2 * S, S = sum_c 2^(8c) S_c
+//   S   k_rp_com_var       2 lanes/proof    x*D + z^2*S (joint GLV/Straus), S = sum_c 2^(8c) S_c
 //   S   k_rp_com_sum       proof            com = C + z K - delta P + x D + z^2 S       bulletproof.go:477-492
 //   S   k_rp_normalize     point (block)    batch affine normalisation of H'_i and com (one inversion per 256 points)
 //   S2  k_rp_x0_build      (proof, record)  DER(hex(H'..., G..., Q, com) "||" Zb(ip))   ipa.go:200-212
@@ -33,6 +32,7 @@
 namespace fts {
 
 constexpr int NORM_BS = 256;
+constexpr int NORM_E = 4;  // points per lane of k_rp_normalize
 __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, const int32_t* __restrict__ status,
                                                           const uint32_t* __restrict__ jac, uint32_t* __restrict__ aff,
                                                           uint8_t* __restrict__ be);
@@ -211,8 +211,9 @@ __global__ void __launch_bounds__(64) k_rp_chal_fr(int B, int n, int k, const in
 // the n fixed-base products of the com terms become one variable-base product.
 // Terms per proof (com_terms): 0 z*K, 1 -delta*P, 2,3 the GLV halves of x*D,
 // 4,5 the GLV halves of z^2*S.
-constexpr int COM_NTERMS = 6;
+constexpr int COM_NTERMS = 4;  // z K, -delta P, the two joint GLV halves
 constexpr int HS_CHUNK = 8;  // H' per Horner chunk of S
+constexpr int HS_SCRATCH = 8 * 24;  // scratch words per proof for the chunks (n <= 64)
 inline __host__ __device__ int com_nterms(int n) { return COM_NTERMS; }
 
 // lane per (proof, item): items 0..n-1: H'_i = y^-i H_i (-> hpj[b][i]);
@@ -273,42 +274,44 @@ __global__ void __launch_bounds__(64) k_rp_hsum_chunks(int B, int n, const int32
   store_g1j(chunks + (size_t)gid * 24, acc);
 }
 
-// Variable-base GLV products, two lanes per proof (h = 0: k1*P, h = 1: k2*phi(P)):
-//   which = 0: x*D   (terms 2, 3)      bulletproof.go:478
-//   which = 1: z^2*S (terms 4, 5), S = sum_c 2^(8c) S_c assembled by Horner first
-__global__ void __launch_bounds__(64) k_rp_glv_terms(int B, int n, int k, int which, const int32_t* __restrict__ status,
-                                                     const uint32_t* __restrict__ pts, const uint32_t* __restrict__ ch,
-                                                     const uint32_t* __restrict__ chunks, uint32_t* __restrict__ terms) {
-  __shared__ uint32_t tab[8 * 24 * 64];
+// x*D + z^2*S (bulletproof.go:478, 486-489 via S), two lanes per proof:
+// with x = x1 + x2 lambda and z^2 = w1 + w2 lambda (GLV), lane h computes
+// x_h phi^h(D) + w_h phi^h(S) in one joint Straus chain (glv.hpp), where
+// S = sum_c 2^(8c) S_c is assembled by Horner first -> terms[b][2 + h]
+__global__ void __launch_bounds__(64) k_rp_com_var(int B, int n, int k, const int32_t* __restrict__ status,
+                                                   const uint32_t* __restrict__ pts, const uint32_t* __restrict__ ch,
+                                                   const uint32_t* __restrict__ chunks, uint32_t* __restrict__ vtab,
+                                                   uint32_t* __restrict__ terms) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = gid >> 1, h = gid & 1;
   if (b >= B || status[b] != 0) return;
   const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
-  Fr s;
-  G1J P;
-  if (which == 0) {
-    load_f(C + CH_X * 8, s);
-    P = g1j_from_affine(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_D) * 16));
-  } else {
-    load_f(C + CH_Z2 * 8, s);
-    const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
-    const uint32_t* S = chunks + (size_t)b * nc * 24;
-    P = load_g1j(S + (nc - 1) * 24);
-    for (int c = nc - 2; c >= 0; c--) {
-      for (int q = 0; q < HS_CHUNK; q++) P = g1j_dbl(P);
-      add_inl(P, load_g1j(S + c * 24));
-    }
+  Fr x, z2;
+  load_f(C + CH_X * 8, x);
+  load_f(C + CH_Z2 * 8, z2);
+  const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
+  const uint32_t* Sc = chunks + (size_t)b * nc * 24;
+  G1J S = load_g1j(Sc + (nc - 1) * 24);
+  for (int c = nc - 2; c >= 0; c--) {
+    for (int q = 0; q < HS_CHUNK; q++) S = g1j_dbl(S);
+    add_inl(S, load_g1j(Sc + c * 24));
   }
-  const Scalar sk = fr_canon(s);
-  uint32_t k1[4], k2[4], s1, s2;
-  glv_decompose(sk.v, k1, s1, k2, s2);
-  if (h) P.x = fp_mul(P.x, glv_beta());  // phi
-  if (h ? s2 : s1) P.y = f_neg(P.y);
-  G1J r = vb128j(P, h ? k2 : k1, tab, threadIdx.x);
-  store_g1j(terms + ((size_t)b * COM_NTERMS + 2 + 2 * which + h) * 24, r);
+  G1J D = g1j_from_affine(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_D) * 16));
+  uint32_t xk[2][4], xs[2], wk[2][4], ws[2];
+  glv_decompose(fr_canon(x).v, xk[0], xs[0], xk[1], xs[1]);
+  glv_decompose(fr_canon(z2).v, wk[0], ws[0], wk[1], ws[1]);
+  if (h) {  // phi
+    const Fp beta = glv_beta();
+    D.x = fp_mul(D.x, beta);
+    S.x = fp_mul(S.x, beta);
+  }
+  if (xs[h]) D.y = f_neg(D.y);
+  if (ws[h]) S.y = f_neg(S.y);
+  G1J r = straus2_128(D, xk[h], S, wk[h], vtab, (size_t)2 * B, (size_t)gid);
+  store_g1j(terms + ((size_t)b * COM_NTERMS + 2 + h) * 24, r);
 }
 
-// lane per proof: com = C + the 6 terms -> hpj[b][n] (Jacobian)
+// lane per proof: com = C + the 4 terms -> hpj[b][n] (Jacobian)
 __global__ void __launch_bounds__(64) k_rp_com_sum(int B, int n, int k, const int32_t* __restrict__ status,
                                                    const uint32_t* __restrict__ pts, const uint32_t* __restrict__ terms,
                                                    uint32_t* __restrict__ hpj) {
@@ -320,30 +323,49 @@ __global__ void __launch_bounds__(64) k_rp_com_sum(int B, int n, int k, const in
   store_g1j(hpj + ((size_t)b * (n + 1) + n) * 24, acc);
 }
 
-// Batch affine normalisation, block of 256 lanes = 256 consecutive points
-// ([B][per] Jacobian, points of proofs with status != 0 are skipped): prefix
-// and suffix products of the z's in LDS, ONE inversion per block, then
-// z_i^-1 = inv * prefix_{i-1} * suffix_{i+1}.  Writes affine Montgomery
-// (aff, 16 words) and the canonical 64-byte BE encoding (be).
+// Batch affine normalisation (Montgomery's trick), NORM_E points per lane and
+// NORM_BS * NORM_E points per block ([B][per] Jacobian; points of proofs with
+// status != 0 are skipped, identities map to (0, 0)):
+//   1. lane-local prefix products of its NORM_E z's (strided by NORM_BS, so
+//      every load/store is coalesced),
+//   2. Hillis-Steele prefix + suffix scans of the lane totals in LDS,
+//   3. ONE inversion per block (f_inv_gcd, branch-free),
+//   4. lane-local back-sweep: z_j^-1, then x z^-2, y z^-3.
+// ~9 products per point (the scans cost 16 / NORM_E per point).  Writes affine
+// Montgomery (aff, 16 words) and the canonical 64-byte BE encoding (be).
 __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, const int32_t* __restrict__ status,
                                                           const uint32_t* __restrict__ jac, uint32_t* __restrict__ aff,
                                                           uint8_t* __restrict__ be) {
   __shared__ uint32_t pre[NORM_BS * 8], suf[NORM_BS * 8];
   __shared__ uint32_t invs[8];
   const int t = threadIdx.x;
-  const int g = blockIdx.x * NORM_BS + t;
-  const bool live = g < total && (!status || status[g / per] == 0);
-  G1J p;
-  Fp z = f_one<FpP>();
-  if (live) {
-    p = load_g1j(jac + (size_t)g * 24);
-    if (!f_is_zero(p.z)) z = p.z;
+  const size_t g0 = (size_t)blockIdx.x * NORM_BS * NORM_E + t;
+  auto zload = [&](int j, Fp& z) -> bool {  // z of point j (1 if absent/skipped/identity); live?
+    const size_t g = g0 + (size_t)j * NORM_BS;
+    z = f_one<FpP>();
+    if (g >= (size_t)total || (status && status[g / per] != 0)) return false;
+    Fp zz;
+    load_fp(jac + g * 24 + 16, zz);
+    if (!f_is_zero(zz)) z = zz;
+    return true;
+  };
+  Fp acc[NORM_E];
+  {
+    Fp run = f_one<FpP>();
+#pragma unroll
+    for (int j = 0; j < NORM_E; j++) {
+      Fp z;
+      zload(j, z);
+      run = j ? fp_mul(run, z) : z;
+      acc[j] = run;
+    }
   }
-  store_fp(pre + t * 8, z);
-  store_fp(suf + t * 8, z);
+  const Fp tot = acc[NORM_E - 1];
+  store_fp(pre + t * 8, tot);
+  store_fp(suf + t * 8, tot);
   __syncthreads();
-  // inclusive scans (Hillis-Steele): pre_t = z_0..z_t, suf_t = z_t..z_255
-  Fp a = z, c = z;
+  // inclusive scans (Hillis-Steele): pre_t = T_0..T_t, suf_t = T_t..T_255
+  Fp a = tot, c = tot;
   for (int off = 1; off < NORM_BS; off <<= 1) {
     Fp o1, o2;
     const bool h1 = t >= off, h2 = t + off < NORM_BS;
@@ -362,30 +384,41 @@ __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, co
   }
   if (t == 0) store_fp(invs, nl_fp_inv(c));  // suf_0 = product of all
   __syncthreads();
-  if (!live) return;
-  const bool ident = f_is_zero(p.z);
-  G1A r;
-  if (ident) {
-    r.x = f_zero<FpP>();
-    r.y = f_zero<FpP>();
-  } else {
-    Fp zi;
-    load_fp(invs, zi);
+  // inverse of this lane's total: inv(all) * pre_{t-1} * suf_{t+1}
+  Fp inv;
+  load_fp(invs, inv);
+  {
     Fp o;
     if (t > 0) {
       load_fp(pre + (t - 1) * 8, o);
-      zi = fp_mul(zi, o);
+      inv = fp_mul(inv, o);
     }
     if (t + 1 < NORM_BS) {
       load_fp(suf + (t + 1) * 8, o);
-      zi = fp_mul(zi, o);
+      inv = fp_mul(inv, o);
     }
-    Fp zi2 = fp_sqr(zi);
-    r.x = fp_mul(p.x, zi2);
-    r.y = fp_mul(fp_mul(p.y, zi2), zi);
   }
-  store_g1a(aff + (size_t)g * 16, r);
-  if (be) store_point_be(be + (size_t)g * 64, r);
+#pragma unroll
+  for (int j = NORM_E - 1; j >= 0; j--) {
+    Fp z;
+    const bool live = zload(j, z);
+    Fp zi = j ? fp_mul(inv, acc[j - 1]) : inv;  // z_j^-1
+    if (j) inv = fp_mul(inv, z);
+    if (!live) continue;
+    const size_t g = g0 + (size_t)j * NORM_BS;
+    const G1J p = load_g1j(jac + g * 24);
+    G1A r;
+    if (f_is_zero(p.z)) {
+      r.x = f_zero<FpP>();
+      r.y = f_zero<FpP>();
+    } else {
+      Fp zi2 = fp_sqr(zi);
+      r.x = fp_mul(p.x, zi2);
+      r.y = fp_mul(fp_mul(p.y, zi2), zi);
+    }
+    store_g1a(aff + g * 16, r);
+    if (be) store_point_be(be + g * 64, r);
+  }
 }
 
 // --------------------------------------------------------- x0 transcript
@@ -728,7 +761,9 @@ __global__ void __launch_bounds__(64) k_rlc_finalize(int B, const uint32_t* __re
 
 
 
-size_t rp_scratch_words(int B, int n, int k) { return (size_t)B * (3 + 2 * k) * 10 * 24; }
+size_t rp_scratch_words(int B, int n, int k) {
+  return std::max((size_t)B * (3 + 2 * k) * 10 * 24, (size_t)B * (HS_SCRATCH + 2 * 16 * 24));
+}
 size_t rp_terms_words(int B, int n, int k) { return (size_t)B * rp_nterms(n, k) * 24; }
 
 size_t fb_words_per_base() { return FB_WORDS_PER_BASE; }
@@ -747,7 +782,8 @@ void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32
   FTS_LAUNCH(kt_small_large, nbw, 64, s, nb, bw, small, large);
   FTS_LAUNCH(kt_entries, nbw * FB_E, 64, s, nb, small, large, jac);
   const size_t tot = nbw * FB_E;
-  FTS_LAUNCH(k_rp_normalize, tot, NORM_BS, s, (int)tot, 1, (const int32_t*)nullptr, jac, tables, (uint8_t*)nullptr);
+  FTS_LAUNCH(k_rp_normalize, (tot + NORM_E - 1) / NORM_E, NORM_BS, s, (int)tot, 1, (const int32_t*)nullptr, jac, tables,
+             (uint8_t*)nullptr);
 }
 
 void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
@@ -767,23 +803,20 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   tl->mark("k_rp_hash_small", s, 0);
   FTS_LAUNCH(k_rp_chal_fr, B, 64, s, B, n, k, d.status, d.ch, d.scratch);
   tl->mark("k_rp_chal_fr", s, (double)B * (3 * k + 4 * (k + 1) + 12));
-  // side: x*D while the main stream runs the fixed-base products
-  tl->fork(s, s2);
-  FTS_LAUNCH(k_rp_glv_terms, 2 * B, 64, s2, B, n, k, 0, d.status, d.pts, d.ch, d.scratch, d.terms);
-  tl->mark("k_rp_xd", s2, (double)B * 2 * COST_VB128);
   FTS_LAUNCH(k_rp_fixed_exact, B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, tables, d.hpj, d.terms);
   tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FB);
   const int nch = (n + HS_CHUNK - 1) / HS_CHUNK;
   FTS_LAUNCH(k_rp_hsum_chunks, B * nch, 64, s, B, n, d.status, d.hpj, d.scratch);
   tl->mark("k_rp_hsum_chunks", s, (double)B * (n - nch) * (COST_DBL + COST_ADD));
-  FTS_LAUNCH(k_rp_glv_terms, 2 * B, 64, s, B, n, k, 1, d.status, d.pts, d.ch, d.scratch, d.terms);
-  tl->mark("k_rp_zs", s, (double)B * (2 * COST_VB128 + 2 * (nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD)));
-  tl->fork(s2, s);
+  // scratch: [0, B*192) Horner chunks of S, then the 2B lanes' joint tables
+  FTS_LAUNCH(k_rp_com_var, 2 * B, 64, s, B, n, k, d.status, d.pts, d.ch, d.scratch, d.scratch + (size_t)B * HS_SCRATCH,
+             d.terms);
+  tl->mark("k_rp_com_var", s, (double)B * 2 * (COST_STRAUS2 + (nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD)));
   FTS_LAUNCH(k_rp_com_sum, B, 64, s, B, n, k, d.status, d.pts, d.terms, d.hpj);
   tl->mark("k_rp_com_sum", s, (double)B * COM_NTERMS * COST_ADD);
   const int npt = B * (n + 1);
-  FTS_LAUNCH(k_rp_normalize, npt, NORM_BS, s, npt, n + 1, d.status, d.hpj, d.hpa, d.hp_be);
-  tl->mark("k_rp_normalize", s, (double)npt * (2 * 8.0 / 1.0 + 6.0));
+  FTS_LAUNCH(k_rp_normalize, (npt + NORM_E - 1) / NORM_E, NORM_BS, s, npt, n + 1, d.status, d.hpj, d.hpa, d.hp_be);
+  tl->mark("k_rp_normalize", s, (double)npt * (2.0 * 8.0 / NORM_E + 9.0));
   // side: x0 transcript + hash, then the fixed-base columns (need x0)
   tl->fork(s, s2);
   FTS_LAUNCH(k_rp_x0_build, B * (2 * n + 3), 256, s2, B, n, d.status, d.hp_be, x0_const, d.sc, d.x0_msgs);
