@@ -15,14 +15,17 @@
 // several lanes instead of one long dependent chain.
 // Kernels (msm.hip), all on one stream:
 //   k_msm_digits      (point)          recode + bucket histogram (atomics)
-//   k_msm_scan        (window)         prefix sums: bucket offsets + chunk map
+//   k_msm_scan1/2/3   (bucket)         global exclusive scans over all buckets:
+//                                      entry offsets into one flat sorted array
+//                                      and the chunk map (3-pass block scan)
 //   k_msm_scatter     (point)          counting-sort scatter of (index|sign)
 //   k_msm_chunks      (chunk)          <= MSM_CH mixed additions from HBM
 //   k_msm_bucket_sum  (bucket)         sum of the bucket's chunk partials
 //   k_msm_segments    (segment)        running-sum reduction of MSM_SEG buckets
-//   k_msm_windows     (window + 1)     LDS tree over the window's segments;
-//                                      block nw sums the extra (fixed) points
-//   k_msm_final       (1 lane)         Horner over the windows + extras
+//   k_msm_windows     (window+1, part) LDS tree over <= MSM_WIN_ITEMS segments
+//                                      (window nw: the extra fixed points)
+//   k_msm_final       (1 wave)         per-window sum of the parts, then
+//                                      Horner over the windows + extras
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -32,6 +35,8 @@ namespace fts {
 constexpr int MSM_MAX_WINDOWS = 64;
 constexpr int MSM_SEG = 8;   // buckets per running-sum segment
 constexpr int MSM_CH = 8;    // points per bucket-accumulation chunk
+constexpr int MSM_SCAN_ITEMS = 1024;  // buckets per block of the scan passes
+constexpr int MSM_WIN_ITEMS = 1024;   // segments per block of k_msm_windows
 
 struct MsmWindow {
   int32_t width;   // bits
@@ -51,6 +56,8 @@ struct MsmPlan {
   int NB;          // total buckets
   int NS;          // total segments
   int NC;          // total chunk slots
+  int NBLK;        // scan blocks (ceil(NB / MSM_SCAN_ITEMS))
+  int WB;          // k_msm_windows blocks per window
   MsmWindow win[MSM_MAX_WINDOWS];  // host copy
   MsmWindow* d_win;                // device copy
   int32_t* keys;      // [nw][NV] bucket (global) index | sign<<31, or -1
@@ -65,7 +72,10 @@ struct MsmPlan {
   uint32_t* segs;     // [NS][24]
   uint32_t* wins;     // [nw + 1][24] (slot nw: sum of the extra points)
   uint32_t* out;      // [24] result (Jacobian)
+  uint32_t* scratch;  // >= msm_scratch_words(p): scan block sums + window parts
 };
+
+inline size_t msm_scratch_words(const MsmPlan& p) { return (size_t)2 * p.NBLK + (size_t)(p.nw + 1) * p.WB * 24; }
 
 // Field-product count of the bucket phase for window width c (host cost model)
 inline double msm_cost(int N, int c) {
@@ -97,6 +107,14 @@ inline void msm_layout(int N, MsmPlan& p) {
   p.NB = bb;
   p.NS = sb;
   p.NC = cb;
+  p.NBLK = (bb + MSM_SCAN_ITEMS - 1) / MSM_SCAN_ITEMS;
+  int maxs = 0;
+  for (int w = 0; w < nw; w++) {
+    const int ns = ((1 << (p.win[w].width - 1)) + MSM_SEG - 1) / MSM_SEG;
+    maxs = ns > maxs ? ns : maxs;
+  }
+  p.WB = (maxs + MSM_WIN_ITEMS - 1) / MSM_WIN_ITEMS;
+  if (p.WB < 1) p.WB = 1;
   p.N = N;
   p.NV = NV;
 }

@@ -133,6 +133,8 @@ struct RpBatchDev {
   uint8_t* x0_msgs;    // [B][x0_slot_bytes(n)]
   uint32_t* terms;     // [B][6+2n+2k][24]
   uint32_t* scratch;   // var-base lane tables
+  uint32_t* ypow;      // [n][B][8] y^-i (Montgomery Fr), i-major (coalesced over proofs)
+  uint32_t* svec;      // [n][B][8] s_i = prod_j x_j^(+-1) (ipa.go:343-356 unrolled), i-major
 };
 
 }  // namespace fts

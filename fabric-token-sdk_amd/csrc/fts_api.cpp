@@ -84,7 +84,7 @@ struct DBuf {
 };
 
 struct Workspace {
-  DBuf pts, ch, small, hpj, hpa, hpbe, x0, terms, scratch;
+  DBuf pts, ch, small, hpj, hpa, hpbe, x0, terms, scratch, ypow, svec;
   // random-linear-combination check + MSM
   DBuf r_key, r_msc, r_coef, r_colsum, r_fixed, r_flag, m_keys, m_counts, m_offsets, m_cursor, m_sorted, m_buckets,
       m_segs, m_wins, m_out, m_scratch, m_win, m_choff, m_chbkt, m_partials;
@@ -92,7 +92,7 @@ struct Workspace {
   DBuf rp_raw, rp_sc, rp_status, rp_ipa;
   DBuf s_act, s_raw, s_owner, s_pts, s_sc, s_status, s_work, s_terms, s_aff, s_affoff, s_msgs, s_jac, s_scratch;
   void release() {
-    for (DBuf* b : {&pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &terms, &scratch, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
+    for (DBuf* b : {&pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &terms, &scratch, &ypow, &svec, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
                     &rp_status, &rp_ipa, &s_act, &s_raw, &s_owner, &s_pts, &s_sc, &s_status, &s_work, &s_terms, &s_aff,
                     &s_affoff, &s_msgs, &s_jac, &s_scratch, &r_key, &r_msc, &r_coef, &r_colsum, &r_fixed, &r_flag,
                     &m_keys, &m_counts, &m_offsets, &m_cursor, &m_sorted, &m_buckets, &m_segs, &m_wins, &m_out,
@@ -531,8 +531,8 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
       w.m_counts.ensure((size_t)mp.NB * 4) || w.m_offsets.ensure((size_t)mp.NB * 4) ||
       w.m_cursor.ensure((size_t)mp.NB * 4) || w.m_sorted.ensure((size_t)mp.nw * mp.NV * 4) ||
       w.m_buckets.ensure((size_t)mp.NB * 96) || w.m_segs.ensure((size_t)mp.NS * 96) ||
-      w.m_wins.ensure((size_t)(mp.nw + 1) * 96) || w.m_out.ensure(96) || w.m_scratch.ensure((size_t)mp.NS * 96) ||
-      w.m_win.ensure(sizeof(mp.win)))
+      w.m_wins.ensure((size_t)(mp.nw + 1) * 96) || w.m_out.ensure(96) || w.m_scratch.ensure(std::max((size_t)mp.NS * 96, msm_scratch_words(mp) * 4)) ||
+      w.m_win.ensure(sizeof(mp.win)) || w.ypow.ensure((size_t)B * n * 32) || w.svec.ensure((size_t)B * n * 32))
     return FTS_API_ENOMEM;
   RpBatchDev d{B,
                n,
@@ -549,7 +549,9 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
                w.hpbe.as<uint8_t>(),
                w.x0.as<uint8_t>(),
                w.terms.as<uint32_t>(),
-               w.scratch.as<uint32_t>()};
+               w.scratch.as<uint32_t>(),
+               w.ypow.as<uint32_t>(),
+               w.svec.as<uint32_t>()};
   mp.d_win = w.m_win.as<MsmWindow>();
   memcpy(L.pin->win, mp.win, sizeof(MsmWindow) * mp.nw);
   HIP_OK(hipMemcpyAsync(mp.d_win, L.pin->win, sizeof(MsmWindow) * mp.nw, hipMemcpyHostToDevice, L.s));
@@ -565,6 +567,7 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   mp.chunk_off = w.m_choff.as<uint32_t>();
   mp.chunk_bkt = w.m_chbkt.as<int32_t>();
   mp.partials = w.m_partials.as<uint32_t>();
+  mp.scratch = w.m_scratch.as<uint32_t>();
   RlcDev r{w.r_key.as<uint32_t>(), w.r_msc.as<uint32_t>(),   w.r_coef.as<uint32_t>(), w.r_colsum.as<uint32_t>(),
            w.r_fixed.as<uint32_t>(), w.r_flag.as<int32_t>(), w.m_scratch.as<uint32_t>(), mp};
   // fresh RLC weights key (getrandom), unpredictable to the provers

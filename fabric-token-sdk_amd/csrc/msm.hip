@@ -60,50 +60,99 @@ __global__ void __launch_bounds__(256) k_msm_digits(int N, int nw, const MsmWind
   }
 }
 
-// Prefix sums of one window (block per window): entry offsets of the buckets
-// in the window's sorted range, and the chunk map (bucket b owns chunk slots
-// [chunk_off[b], chunk_off[b] + ceil(cnt_b / MSM_CH)) inside the window's
-// reserved slot range; unused slots keep chunk_bkt = -1 from the memset).
-__global__ void __launch_bounds__(256) k_msm_scan(const MsmWindow* __restrict__ win, const uint32_t* __restrict__ counts,
-                                                  uint32_t* __restrict__ offsets, uint32_t* __restrict__ cursor,
-                                                  uint32_t* __restrict__ chunk_off, int32_t* __restrict__ chunk_bkt) {
+// Global exclusive scans over all NB buckets (windows are consecutive bucket
+// ranges): offsets[b] = position of bucket b's first entry in the flat sorted
+// array, chunk_off[b] = its first chunk slot.  Pass 1: block-local scans of
+// MSM_SCAN_ITEMS buckets (4 per lane) + block totals; pass 2: one block scans
+// the totals; pass 3: adds the block offsets, copies the cursor and fills the
+// chunk map (unused slots keep chunk_bkt = -1 from the memset).
+__global__ void __launch_bounds__(256) k_msm_scan1(int NB, const uint32_t* __restrict__ counts,
+                                                   uint32_t* __restrict__ offsets, uint32_t* __restrict__ chunk_off,
+                                                   uint32_t* __restrict__ blk) {
   __shared__ uint32_t pe[256], pc[256];
   const int t = threadIdx.x;
-  const MsmWindow W = win[blockIdx.x];
-  const int nb = 1 << (W.width - 1);
-  const uint32_t* C = counts + W.bbase;
-  const int per = (nb + 255) / 256;
+  const int base = blockIdx.x * MSM_SCAN_ITEMS + t * 4;
+  uint32_t cnt[4], le = 0, lc = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    cnt[j] = base + j < NB ? counts[base + j] : 0u;
+    le += cnt[j];
+    lc += (cnt[j] + MSM_CH - 1) / MSM_CH;
+  }
+  pe[t] = le;
+  pc[t] = lc;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    const uint32_t ve = t >= off ? pe[t - off] : 0, vc = t >= off ? pc[t - off] : 0;
+    __syncthreads();
+    pe[t] += ve;
+    pc[t] += vc;
+    __syncthreads();
+  }
+  uint32_t re = pe[t] - le, rc = pc[t] - lc;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    if (base + j < NB) {
+      offsets[base + j] = re;
+      chunk_off[base + j] = rc;
+    }
+    re += cnt[j];
+    rc += (cnt[j] + MSM_CH - 1) / MSM_CH;
+  }
+  if (t == 255) {
+    blk[2 * blockIdx.x] = pe[255];
+    blk[2 * blockIdx.x + 1] = pc[255];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_msm_scan2(int nblk, uint32_t* __restrict__ blk) {
+  __shared__ uint32_t pe[256], pc[256];
+  const int t = threadIdx.x;
+  const int per = (nblk + 255) / 256;
   uint32_t le = 0, lc = 0;
   for (int j = 0; j < per; j++) {
-    int b = t * per + j;
-    if (b < nb) {
-      le += C[b];
-      lc += (C[b] + MSM_CH - 1) / MSM_CH;
+    const int q = t * per + j;
+    if (q < nblk) {
+      le += blk[2 * q];
+      lc += blk[2 * q + 1];
     }
   }
   pe[t] = le;
   pc[t] = lc;
   __syncthreads();
   for (int off = 1; off < 256; off <<= 1) {
-    uint32_t ve = t >= off ? pe[t - off] : 0, vc = t >= off ? pc[t - off] : 0;
+    const uint32_t ve = t >= off ? pe[t - off] : 0, vc = t >= off ? pc[t - off] : 0;
     __syncthreads();
     pe[t] += ve;
     pc[t] += vc;
     __syncthreads();
   }
-  uint32_t re = pe[t] - le, rc = (uint32_t)W.cbase + pc[t] - lc;
+  uint32_t re = pe[t] - le, rc = pc[t] - lc;
   for (int j = 0; j < per; j++) {
-    int b = t * per + j;
-    if (b < nb) {
-      const uint32_t cnt = C[b], nch = (cnt + MSM_CH - 1) / MSM_CH;
-      offsets[W.bbase + b] = re;
-      cursor[W.bbase + b] = re;
-      chunk_off[W.bbase + b] = rc;
-      for (uint32_t q = 0; q < nch; q++) chunk_bkt[rc + q] = W.bbase + b;
-      re += cnt;
-      rc += nch;
+    const int q = t * per + j;
+    if (q < nblk) {
+      const uint32_t e = blk[2 * q], c = blk[2 * q + 1];
+      blk[2 * q] = re;
+      blk[2 * q + 1] = rc;
+      re += e;
+      rc += c;
     }
   }
+}
+
+__global__ void __launch_bounds__(256) k_msm_scan3(int NB, const uint32_t* __restrict__ counts,
+                                                   uint32_t* __restrict__ offsets, uint32_t* __restrict__ cursor,
+                                                   uint32_t* __restrict__ chunk_off, int32_t* __restrict__ chunk_bkt,
+                                                   const uint32_t* __restrict__ blk) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= NB) return;
+  const int q = b / MSM_SCAN_ITEMS;
+  const uint32_t o = offsets[b] + blk[2 * q], oc = chunk_off[b] + blk[2 * q + 1];
+  offsets[b] = o;
+  cursor[b] = o;
+  chunk_off[b] = oc;
+  const uint32_t nch = (counts[b] + MSM_CH - 1) / MSM_CH;
+  for (uint32_t c = 0; c < nch; c++) chunk_bkt[oc + c] = b;
 }
 
 __global__ void __launch_bounds__(256) k_msm_scatter(int NV, int nw, const int32_t* __restrict__ keys,
@@ -114,16 +163,9 @@ __global__ void __launch_bounds__(256) k_msm_scatter(int NV, int nw, const int32
     int key = keys[(size_t)w * NV + i];
     if (key == -1) continue;
     uint32_t b = (uint32_t)key & 0x7fffffffu;
-    uint32_t pos = atomicAdd(&cursor[b], 1u);
-    sorted[(size_t)w * NV + pos] = (uint32_t)i | ((uint32_t)key & 0x80000000u);
+    uint32_t pos = atomicAdd(&cursor[b], 1u);  // global position (flat sorted array)
+    sorted[pos] = (uint32_t)i | ((uint32_t)key & 0x80000000u);
   }
-}
-
-// window of a global bucket index (nw is small; linear scan over the table)
-FTS_DEV int window_of_bucket(const MsmWindow* win, int nw, int b) {
-  int w = 0;
-  while (w + 1 < nw && win[w + 1].bbase <= b) w++;
-  return w;
 }
 
 // one lane per chunk slot: <= MSM_CH mixed additions of sorted virtual points
@@ -139,10 +181,9 @@ __global__ void __launch_bounds__(64, 4) k_msm_chunks(int N, int nw, int NC, con
   if (g >= NC) return;
   const int b = chunk_bkt[g];
   if (b < 0) return;
-  const int w = window_of_bucket(win, nw, b);
   const uint32_t j = (uint32_t)g - chunk_off[b], cnt = counts[b];
   const uint32_t lo = j * MSM_CH, hi = min(cnt, lo + MSM_CH);
-  const uint32_t* S = sorted + (size_t)w * 2 * N + offsets[b];
+  const uint32_t* S = sorted + offsets[b];
   const Fp beta = glv_beta();
   G1J acc = g1j_identity();
   for (uint32_t t = lo; t < hi; t++) {
@@ -202,25 +243,27 @@ __global__ void __launch_bounds__(64) k_msm_segments(int nw, int NS, const MsmWi
   store_g1j(segs + (size_t)g * 24, acc);
 }
 
-// LDS tree (block of 256 lanes): block w < nw sums the segments of window w;
-// block nw sums the nextra extra Jacobian points (the fixed-base part)
-__global__ void __launch_bounds__(256) k_msm_windows(int nw, const MsmWindow* __restrict__ win,
+// LDS tree (block of 256 lanes) over <= MSM_WIN_ITEMS consecutive segments:
+// block (w, j) with w < nw sums part j of window w's segments; w = nw sums
+// part j of the nextra extra Jacobian points (the fixed-base part)
+__global__ void __launch_bounds__(256) k_msm_windows(int nw, int WB, const MsmWindow* __restrict__ win,
                                                      const uint32_t* __restrict__ segs, const uint32_t* __restrict__ extra,
-                                                     int nextra, uint32_t* __restrict__ wins) {
+                                                     int nextra, uint32_t* __restrict__ parts) {
   __shared__ uint32_t sh[256 * 24];
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, w = blockIdx.x, j = blockIdx.y;
   const uint32_t* S;
   int cnt;
-  if ((int)blockIdx.x < nw) {
-    const MsmWindow W = win[blockIdx.x];
+  if (w < nw) {
+    const MsmWindow W = win[w];
     cnt = ((1 << (W.width - 1)) + MSM_SEG - 1) / MSM_SEG;
     S = segs + (size_t)W.sbase * 24;
   } else {
     cnt = nextra;
     S = extra;
   }
+  const int lo = j * MSM_WIN_ITEMS, hi = min(cnt, lo + MSM_WIN_ITEMS);
   G1J acc = g1j_identity();
-  for (int s = t; s < cnt; s += 256) add_inl(acc, load_g1j(S + (size_t)s * 24));
+  for (int s = lo + t; s < hi; s += 256) add_inl(acc, load_g1j(S + (size_t)s * 24));
   store_g1j(sh + t * 24, acc);
   __syncthreads();
   for (int half = 128; half >= 1; half >>= 1) {
@@ -229,13 +272,22 @@ __global__ void __launch_bounds__(256) k_msm_windows(int nw, const MsmWindow* __
     if (t < half) store_g1j(sh + t * 24, acc);
     __syncthreads();
   }
-  if (t == 0) store_g1j(wins + (size_t)blockIdx.x * 24, acc);
+  if (t == 0) store_g1j(parts + ((size_t)w * WB + j) * 24, acc);
 }
 
-// result = sum_w 2^off_w W_w + (sum of the extra points, slot nw)
-__global__ void k_msm_final(int nw, const MsmWindow* __restrict__ win, const uint32_t* __restrict__ wins,
-                            uint32_t* __restrict__ out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// lane w <= nw: W_w = sum of window w's parts; then lane 0:
+// result = sum_w 2^off_w W_w (Horner) + W_nw (the extra points)
+__global__ void __launch_bounds__(64) k_msm_final(int nw, int WB, const MsmWindow* __restrict__ win,
+                                                  const uint32_t* __restrict__ parts, uint32_t* __restrict__ wins,
+                                                  uint32_t* __restrict__ out) {
+  const int t = threadIdx.x;
+  for (int w = t; w <= nw; w += 64) {
+    G1J acc = load_g1j(parts + (size_t)w * WB * 24);
+    for (int j = 1; j < WB; j++) add_inl(acc, load_g1j(parts + ((size_t)w * WB + j) * 24));
+    store_g1j(wins + (size_t)w * 24, acc);
+  }
+  __syncthreads();
+  if (t != 0) return;
   G1J acc = load_g1j(wins + (size_t)(nw - 1) * 24);
   for (int w = nw - 2; w >= 0; w--) {
     const int shift = win[w + 1].off - win[w].off;
@@ -261,8 +313,9 @@ void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalar
   (void)hipMemsetAsync(p.chunk_bkt, 0xff, (size_t)p.NC * 4, s);
   FTS_LAUNCH(k_msm_digits, p.N, 256, s, p.N, p.nw, p.d_win, scalars, p.keys, p.counts);
   tl->mark("k_msm_digits", s, 0);
-  hipLaunchKernelGGL(k_msm_scan, dim3(p.nw), dim3(256), 0, s, p.d_win, p.counts, p.offsets, p.cursor, p.chunk_off,
-                     p.chunk_bkt);
+  FTS_LAUNCH(k_msm_scan1, (size_t)p.NBLK * 256, 256, s, p.NB, p.counts, p.offsets, p.chunk_off, p.scratch);
+  hipLaunchKernelGGL(k_msm_scan2, dim3(1), dim3(256), 0, s, p.NBLK, p.scratch);
+  FTS_LAUNCH(k_msm_scan3, p.NB, 256, s, p.NB, p.counts, p.offsets, p.cursor, p.chunk_off, p.chunk_bkt, p.scratch);
   tl->mark("k_msm_scan", s, 0);
   FTS_LAUNCH(k_msm_scatter, p.NV, 256, s, p.NV, p.nw, p.keys, p.cursor, p.sorted);
   tl->mark("k_msm_scatter", s, 0);
@@ -275,9 +328,11 @@ void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalar
   FTS_LAUNCH(k_msm_segments, p.NS, 64, s, p.nw, p.NS, p.d_win, p.buckets, p.segs, scratch);
   tl->mark("k_msm_segments", s, (double)p.NB * 2 * COST_ADD);
   if (s_extra != s) tl->fork(s_extra, s);
-  hipLaunchKernelGGL(k_msm_windows, dim3(p.nw + 1), dim3(256), 0, s, p.nw, p.d_win, p.segs, extra, nextra, p.wins);
+  uint32_t* parts = p.scratch + 2 * (size_t)p.NBLK;
+  hipLaunchKernelGGL(k_msm_windows, dim3(p.nw + 1, p.WB), dim3(256), 0, s, p.nw, p.WB, p.d_win, p.segs, extra, nextra,
+                     parts);
   tl->mark("k_msm_windows", s, (double)(p.NS + nextra) * COST_ADD);
-  hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, s, p.nw, p.d_win, p.wins, p.out);
+  hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, s, p.nw, p.WB, p.d_win, parts, p.wins, p.out);
   tl->mark("k_msm_final", s, (double)MSM_BITS * COST_DBL + p.nw * COST_ADD);
 }
 

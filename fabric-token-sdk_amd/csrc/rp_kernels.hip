@@ -203,6 +203,68 @@ __global__ void __launch_bounds__(64) k_rp_chal_fr(int B, int n, int k, const in
   }
 }
 
+// lane per (chunk c of PW_CH indices, proof b), chunk-major: for i in the chunk
+//   ypow[i][b] = y^-i                                 (bulletproof.go:483-485)
+//   svec[i][b] = s_i = prod_j x_j^(+1 if bit k-1-j of i else -1)
+// (the generator folding of ipa.go:343-356 unrolled: G_fin = sum s_i G_i,
+// H'_fin = sum s_i^-1 H'_i = sum s_{n-1-i} H'_i).  The chunk's high index
+// bits give a common prefix product; the low bits expand as a binary tree.
+constexpr int PW_LC = 3, PW_CH = 1 << PW_LC;
+__global__ void __launch_bounds__(64) k_rp_powers(int B, int n, int k, const int32_t* __restrict__ status,
+                                                  const uint32_t* __restrict__ ch, uint32_t* __restrict__ ypow,
+                                                  uint32_t* __restrict__ svec) {
+  const int lc = min(PW_LC, k), cs = 1 << lc, nch = n >> lc;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= B * nch) return;
+  const int c = gid / B, b = gid % B;
+  if (status[b] != 0) return;
+  const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
+  const int i0 = c * cs;
+  Fr yinv;
+  load_f(C + CH_YINV * 8, yinv);
+  Fr yp = fr_pow_small(yinv, (uint32_t)i0);
+  for (int q = 0; q < cs; q++) {
+    if (q) yp = fr_mul(yp, yinv);
+    store_f(ypow + ((size_t)(i0 + q) * B + b) * 8, yp);
+  }
+  // prefix over the high bits: j = 0 .. k-1-lc  (bit k-1-j of i0)
+  Fr pre = f_one<FrP>();
+  for (int j = 0; j < k - lc; j++) {
+    Fr f;
+    load_f(C + (CH_XJ + (((i0 >> (k - 1 - j)) & 1) ? 0 : k) + j) * 8, f);
+    pre = j ? fr_mul(pre, f) : f;
+  }
+  if (lc == PW_LC) {
+    Fr v[PW_CH];
+    v[0] = pre;
+#pragma unroll
+    for (int l = 0; l < PW_LC; l++) {  // low bits, MSB first: index 2t + bit
+      const int j = k - PW_LC + l;
+      Fr xj, xji;
+      load_f(C + (CH_XJ + j) * 8, xj);
+      load_f(C + (CH_XJ + k + j) * 8, xji);
+#pragma unroll
+      for (int t = (1 << l) - 1; t >= 0; t--) {
+        const Fr base = v[t];
+        v[2 * t + 1] = fr_mul(base, xj);
+        v[2 * t] = fr_mul(base, xji);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PW_CH; q++) store_f(svec + ((size_t)(i0 + q) * B + b) * 8, v[q]);
+  } else {  // n < 8: one chunk, direct products
+    for (int q = 0; q < cs; q++) {
+      Fr sv = f_one<FrP>();
+      for (int j = 0; j < k; j++) {
+        Fr f;
+        load_f(C + (CH_XJ + (((q >> (k - 1 - j)) & 1) ? 0 : k) + j) * 8, f);
+        sv = fr_mul(sv, f);
+      }
+      store_f(svec + ((size_t)q * B + b) * 8, sv);
+    }
+  }
+}
+
 // ------------------------------------------------------------ H' and com
 // com = x*D + C - z sum G_i + sum (z y^i + z^2 2^i) H'_i - delta*P   (bulletproof.go:477-492)
 //     = x*D + C + z*K - delta*P + z^2 * S,   K = sum H_i - sum G_i,  S = sum_i 2^i H'_i
@@ -220,6 +282,7 @@ inline __host__ __device__ int com_nterms(int n) { return COM_NTERMS; }
 // n: z K; n+1: -delta P (-> terms[b][0..1])
 __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, const int32_t* __restrict__ status,
                                                           const uint32_t* __restrict__ sc, const uint32_t* __restrict__ ch,
+                                                          const uint32_t* __restrict__ ypow,
                                                           const uint32_t* __restrict__ tables, uint32_t* __restrict__ hpj,
                                                           uint32_t* __restrict__ terms) {
   const int ni = n + 2;
@@ -232,10 +295,10 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, c
   const uint32_t* tab;
   Scalar sk;
   if (t < n) {
-    Fr yinv;
-    load_f(C + CH_YINV * 8, yinv);
+    Fr yp;
+    load_f(ypow + ((size_t)t * B + b) * 8, yp);
     tab = tables + (size_t)(n + t) * FB_WORDS_PER_BASE;
-    sk = fr_canon(fr_pow_small(yinv, (uint32_t)t));
+    sk = fr_canon(yp);
     out = hpj + ((size_t)b * (n + 1) + t) * 24;
   } else if (t == n) {
     Fr z;
@@ -680,34 +743,42 @@ __global__ void __launch_bounds__(64) k_rlc_prep(int B, int n, int k, const int3
 }
 
 // one block per column: col 0 G (ped1), 1 H (ped2), 2 Q, 3+i G_i, 3+n+i H_i
+// (s_i and y^-i come precomputed, i-major, from k_rp_powers)
 __global__ void __launch_bounds__(256) k_rlc_columns(int B, int n, int k, const uint32_t* __restrict__ ch,
-                                                     const uint32_t* __restrict__ coef, uint32_t* __restrict__ colsum) {
+                                                     const uint32_t* __restrict__ coef, const uint32_t* __restrict__ ypow,
+                                                     const uint32_t* __restrict__ svec, uint32_t* __restrict__ colsum) {
   __shared__ uint32_t sh[256 * 8];
   const int col = blockIdx.x, t = threadIdx.x;
   Fr acc = f_zero<FrP>();
   for (int b = t; b < B; b += 256) {
     const uint32_t* K = coef + (size_t)b * RLC_NCOEF * 8;
-    const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
     Fr v;
     if (col < 3) {
       load_f(K + col * 8, v);
       if (col == 2 && !f_is_zero(v)) {
         Fr x0;
-        load_f(C + CH_X0 * 8, x0);
+        load_f(ch + ((size_t)b * rp_nch(k) + CH_X0) * 8, x0);
         v = fr_mul(v, x0);
       }
     } else if (col < 3 + n) {
       Fr ra;
       load_f(K + 3 * 8, ra);
-      v = f_is_zero(ra) ? ra : fr_mul(ra, s_vec(C, k, col - 3));
+      if (!f_is_zero(ra)) {
+        Fr sv;
+        load_f(svec + ((size_t)(col - 3) * B + b) * 8, sv);
+        v = fr_mul(ra, sv);
+      } else {
+        v = ra;
+      }
     } else {
-      int i = col - 3 - n;
+      const int i = col - 3 - n;
       Fr rb;
       load_f(K + 4 * 8, rb);
       if (!f_is_zero(rb)) {
-        Fr yinv;
-        load_f(C + CH_YINV * 8, yinv);
-        v = fr_mul(fr_mul(rb, s_vec(C, k, n - 1 - i)), fr_pow_small(yinv, (uint32_t)i));
+        Fr sv, yp;
+        load_f(svec + ((size_t)(n - 1 - i) * B + b) * 8, sv);
+        load_f(ypow + ((size_t)i * B + b) * 8, yp);
+        v = fr_mul(fr_mul(rb, sv), yp);
       } else {
         v = rb;
       }
@@ -803,7 +874,9 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   tl->mark("k_rp_hash_small", s, 0);
   FTS_LAUNCH(k_rp_chal_fr, B, 64, s, B, n, k, d.status, d.ch, d.scratch);
   tl->mark("k_rp_chal_fr", s, (double)B * (3 * k + 4 * (k + 1) + 12));
-  FTS_LAUNCH(k_rp_fixed_exact, B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, tables, d.hpj, d.terms);
+  FTS_LAUNCH(k_rp_powers, B * (n >> std::min(PW_LC, k)), 64, s, B, n, k, d.status, d.ch, d.ypow, d.svec);
+  tl->mark("k_rp_powers", s, (double)B * (2.0 * n + 2.0 * k));
+  FTS_LAUNCH(k_rp_fixed_exact, B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, tables, d.hpj, d.terms);
   tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FB);
   const int nch = (n + HS_CHUNK - 1) / HS_CHUNK;
   FTS_LAUNCH(k_rp_hsum_chunks, B * nch, 64, s, B, n, d.status, d.hpj, d.scratch);
@@ -826,8 +899,8 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   // main: variable points of the batch equation -> MSM
   FTS_LAUNCH(k_rlc_prep, B, 64, s, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, r.key, d.hpa, d.pts, r.msc, r.coef);
   tl->mark("k_rlc_prep", s, (double)B * (3 * k + 30));
-  hipLaunchKernelGGL(k_rlc_columns, dim3(3 + 2 * n), dim3(256), 0, s2, B, n, k, d.ch, r.coef, r.colsum);
-  tl->mark("k_rlc_columns", s2, (double)B * 2 * n * (k + 2));
+  hipLaunchKernelGGL(k_rlc_columns, dim3(3 + 2 * n), dim3(256), 0, s2, B, n, k, d.ch, r.coef, d.ypow, d.svec, r.colsum);
+  tl->mark("k_rlc_columns", s2, (double)B * 3 * n);
   FTS_LAUNCH(k_rlc_fixed, 3 + 2 * n, 64, s2, n, r.colsum, tables, r.fixed);
   tl->mark("k_rlc_fixed", s2, (double)(3 + 2 * n) * COST_FB);
   launch_msm(r.plan, d.pts, r.msc, r.fixed, 3 + 2 * n, r.msm_scratch, s, s2, tl);
