@@ -46,9 +46,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--bits", type=int, default=64)
-    ap.add_argument("--inflight", type=int, default=16,
+    ap.add_argument("--inflight", type=int, default=32,
                     help="batches in flight: host threads, each submitting its own staged batch")
-    ap.add_argument("--lanes", type=int, default=int(os.environ.get("FTS_LANES", "4")),
+    ap.add_argument("--lanes", type=int, default=int(os.environ.get("FTS_LANES", "3")),
                     help="device lanes (stream pairs) of the library (FTS_LANES); batches submitted while "
                          "all lanes are busy are coalesced into one device pass (FTS_COALESCE_MAX proofs)")
     ap.add_argument("--distinct", type=int, default=4,
@@ -151,12 +151,14 @@ def main():
     # of several passes share the CUs and their event spans overlap).
     kt = {}
     R = max(1, args.roofline_steps)
+    t_iso = time.perf_counter()
     for _ in range(R):
         st = batches[0].verify(want_status=True)
         assert int((st != 0).sum()) == 0
         for name, (ms, mads) in batches[0].timings().items():
             o = kt.get(name, (0.0, 0.0))
             kt[name] = (o[0] + ms, mads)
+    iso_ms = (time.perf_counter() - t_iso) * 1e3 / R
     avg = {kname: v[0] / R for kname, v in kt.items()}
     # roofline kernel: the largest share of the algorithmic work (MADs/launch);
     # the longest (latency-bound) kernel is reported beside it
@@ -223,6 +225,8 @@ def main():
             "inflight": inflight,
             "device_lanes": args.lanes,
             "merged_batches_avg": round(merged_avg, 2),
+            "isolated_batch": {"ms": round(iso_ms, 3), "verifies_per_s": round(B / iso_ms * 1e3, 1),
+                               "note": "one %d-proof batch alone on the GPU (latency; no coalescing)" % B},
             "roofline": roofline,
             "longest_kernel": longest_kernel,
             "cpu_baseline": cpu,

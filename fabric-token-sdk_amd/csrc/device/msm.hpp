@@ -63,7 +63,7 @@ struct MsmPlan {
   int32_t* keys;      // [nw][NV] bucket (global) index | sign<<31, or -1
   uint32_t* counts;   // [NB]
   uint32_t* offsets;  // [NB] (within the window's sorted range)
-  uint32_t* cursor;   // [NB]
+  uint32_t* cursor;   // [nw][NV] rank of each (window, virtual point) entry within its bucket
   uint32_t* chunk_off;// [NB] first chunk slot of the bucket (global)
   int32_t* chunk_bkt; // [NC] bucket of a chunk slot, -1 if unused
   uint32_t* sorted;   // [nw][NV] virtual index | sign << 31
@@ -75,7 +75,7 @@ struct MsmPlan {
   uint32_t* scratch;  // >= msm_scratch_words(p): scan block sums + window parts
 };
 
-inline size_t msm_scratch_words(const MsmPlan& p) { return (size_t)2 * p.NBLK + (size_t)(p.nw + 1) * p.WB * 24; }
+inline size_t msm_scratch_words(const MsmPlan& p) { return (size_t)2 * p.NBLK + 2 + (size_t)(p.nw + 1) * p.WB * 24; }
 
 // Field-product count of the bucket phase for window width c (host cost model)
 inline double msm_cost(int N, int c) {

@@ -50,7 +50,8 @@ constexpr double COST_FB = 16.0 * COST_MADD;   // fixed-base, 16 signed 16-bit w
 constexpr double COST_VB4 = 7.0 + 6.0 * COST_MADD + 256.0 * COST_DBL + 60.0 * COST_ADD;  // 4-bit var-base
 constexpr double COST_VB128 = 7.0 + 6.0 * COST_ADD + 124.0 * COST_DBL + 30.0 * COST_ADD;  // GLV half (glv.hpp)
 constexpr double COST_STRAUS2 = 2.0 * (7.0 + 6.0 * COST_ADD) + 124.0 * COST_DBL + 60.0 * COST_ADD;  // glv.hpp straus2_128
-constexpr double COST_NORM = 7.0;     // batched affine normalisation, per point
+constexpr double COST_NORM = 7.0;
+     // batched affine normalisation, per point
 
 // Per-kernel device timeline: an event is recorded on the launching stream
 // after each kernel; the time of mark i is elapsed(previous event on the same
@@ -118,6 +119,17 @@ struct Timeline {
 };
 
 // device buffers of one range-proof batch (filled by fts_api.cpp)
+// staged batches gathered into one device pass (fts_rp_batch_verify coalescing)
+constexpr int RP_GATHER_MAX = 32;
+struct RpGather {
+  const uint8_t* raw[RP_GATHER_MAX];
+  const uint32_t* sc[RP_GATHER_MAX];
+  const int32_t* status0[RP_GATHER_MAX];
+  const int32_t* ipa[RP_GATHER_MAX];
+  int off[RP_GATHER_MAX + 1];  // first proof of each batch in the merged pass; off[G] = B
+  int G;
+};
+
 struct RpBatchDev {
   int B, n, k;
   uint8_t* raw;        // [B][5+2k][64] raw BE points (slot V from the caller)

@@ -38,6 +38,7 @@ void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32
 void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const uint8_t* x0_const,
                      hipStream_t s, hipStream_t s2, Timeline* tl);
 void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, hipStream_t s, Timeline* tl);
+void launch_rp_gather(const RpGather& g, int k, uint8_t* raw, uint32_t* sc, int32_t* status, int32_t* ipa, hipStream_t s);
 void launch_sig_prep(const SigBatchDev& d, hipStream_t s);
 void launch_sig_finish(const SigBatchDev& d, const uint32_t* tables, int n, hipStream_t s);
 size_t table_build_scratch_bytes(int nb);
@@ -176,7 +177,7 @@ struct fts_ctx {
   // batch coalescing (fts_rp_batch_verify): staged batches submitted
   // concurrently are merged into one device pass of up to coalesce_max proofs
   std::deque<RpReq*> rp_pending;
-  size_t coalesce_max = 16384;
+  size_t coalesce_max = 32768;
   std::once_flag prover_once;
   ProverTables ptab;
 };
@@ -289,7 +290,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
     return code;
   };
   if (hipSetDevice(device) != hipSuccess) return fail(FTS_API_EDEVICE);
-  int nl = 4;
+  int nl = 3;
   if (const char* e = getenv("FTS_LANES")) nl = std::max(1, std::min(16, atoi(e)));
   if (const char* e = getenv("FTS_COALESCE_MAX")) c->coalesce_max = (size_t)std::max(0L, atol(e));
   // FTS_SIDE_STREAM=0: run each lane's side work on its main stream
@@ -529,7 +530,7 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
       w.r_msc.ensure((size_t)N * 32) || w.r_coef.ensure((size_t)B * 5 * 32) || w.r_colsum.ensure((3 + 2 * n) * 32) ||
       w.r_fixed.ensure((3 + 2 * n) * 96) || w.r_flag.ensure(4) || w.m_keys.ensure((size_t)mp.nw * mp.NV * 4) ||
       w.m_counts.ensure((size_t)mp.NB * 4) || w.m_offsets.ensure((size_t)mp.NB * 4) ||
-      w.m_cursor.ensure((size_t)mp.NB * 4) || w.m_sorted.ensure((size_t)mp.nw * mp.NV * 4) ||
+      w.m_cursor.ensure((size_t)mp.nw * mp.NV * 4) || w.m_sorted.ensure((size_t)mp.nw * mp.NV * 4) ||
       w.m_buckets.ensure((size_t)mp.NB * 96) || w.m_segs.ensure((size_t)mp.NS * 96) ||
       w.m_wins.ensure((size_t)(mp.nw + 1) * 96) || w.m_out.ensure(96) || w.m_scratch.ensure(std::max((size_t)mp.NS * 96, msm_scratch_words(mp) * 4)) ||
       w.m_win.ensure(sizeof(mp.win)) || w.ypow.ensure((size_t)B * n * 32) || w.svec.ensure((size_t)B * n * 32))
@@ -624,27 +625,27 @@ static int run_rp_group(fts_ctx* c, Lane& L, const std::vector<RpReq*>& grp) {
   if (w.rp_raw.ensure(B * npts * 64) || w.rp_sc.ensure(B * RP_NSC * 32) || w.rp_status.ensure(B * 4) ||
       w.rp_ipa.ensure(B * 4))
     return FTS_API_ENOMEM;
+  RpGather g{};
+  g.G = (int)grp.size();
   size_t off = 0;
-  for (RpReq* q : grp) {
-    const fts_rp_batch* b = q->b;
-    const size_t m = (size_t)b->B;
-    HIP_OK(hipMemcpyAsync(w.rp_raw.as<uint8_t>() + off * npts * 64, b->raw, m * npts * 64, hipMemcpyDeviceToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(w.rp_sc.as<uint8_t>() + off * RP_NSC * 32, b->sc, m * RP_NSC * 32, hipMemcpyDeviceToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(w.rp_status.as<int32_t>() + off, b->status0, m * 4, hipMemcpyDeviceToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(w.rp_ipa.as<int32_t>() + off, b->ipa_flag, m * 4, hipMemcpyDeviceToDevice, L.s));
-    off += m;
+  for (int i = 0; i < g.G; i++) {
+    const fts_rp_batch* b = grp[i]->b;
+    g.raw[i] = b->raw;
+    g.sc[i] = b->sc;
+    g.status0[i] = b->status0;
+    g.ipa[i] = b->ipa_flag;
+    g.off[i] = (int)off;
+    off += (size_t)b->B;
   }
+  g.off[g.G] = (int)off;
+  launch_rp_gather(g, c->k, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
+                   w.rp_ipa.as<int32_t>(), L.s);
   int rc = rp_pipeline(c, L, (int)B, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
                        w.rp_ipa.as<int32_t>(), [] {});
   if (rc != FTS_API_OK) return rc;
   int32_t* pst = L.status_buf(B);
   if (!pst) return FTS_API_ENOMEM;
   HIP_OK(hipMemcpyAsync(pst, w.rp_status.as<int32_t>(), B * 4, hipMemcpyDeviceToHost, L.s));
-  off = 0;
-  for (RpReq* q : grp) {  // device verdicts of each batch, as a lone run leaves them
-    HIP_OK(hipMemcpyAsync(q->b->status, w.rp_status.as<int32_t>() + off, (size_t)q->b->B * 4, hipMemcpyDeviceToDevice, L.s));
-    off += (size_t)q->b->B;
-  }
   HIP_OK(hipStreamSynchronize(L.s));
   off = 0;
   for (RpReq* q : grp) {
@@ -765,7 +766,7 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
     size_t tot = 0;
     while (!c->rp_pending.empty()) {
       RpReq* q = c->rp_pending.front();
-      if (!grp.empty() && tot + (size_t)q->b->B > c->coalesce_max) break;
+      if (!grp.empty() && (tot + (size_t)q->b->B > c->coalesce_max || (int)grp.size() == RP_GATHER_MAX)) break;
       grp.push_back(q);
       tot += (size_t)q->b->B;
       c->rp_pending.pop_front();

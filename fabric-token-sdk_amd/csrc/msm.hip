@@ -31,7 +31,7 @@ FTS_DEV uint32_t scalar_bits4(const uint32_t s[4], int off, int width) {
 // (virtual points i and N + i) for every window
 __global__ void __launch_bounds__(256) k_msm_digits(int N, int nw, const MsmWindow* __restrict__ win,
                                                     const uint32_t* __restrict__ scalars, int32_t* __restrict__ keys,
-                                                    uint32_t* __restrict__ counts) {
+                                                    uint32_t* __restrict__ ranks, uint32_t* __restrict__ counts) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
   uint32_t s[8];
@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(256) k_msm_digits(int N, int nw, const MsmWind
       if (d != 0) {
         int b = W.bbase + (d < 0 ? -d : d) - 1;
         key = ((d < 0) != (sg[h] != 0)) ? (b | (int)0x80000000) : b;
-        atomicAdd(&counts[b], 1u);
+        ranks[(size_t)w * NV + h * N + i] = atomicAdd(&counts[b], 1u);  // rank within the bucket
       }
       keys[(size_t)w * NV + h * N + i] = key;
     }
@@ -65,7 +65,7 @@ __global__ void __launch_bounds__(256) k_msm_digits(int N, int nw, const MsmWind
 // array, chunk_off[b] = its first chunk slot.  Pass 1: block-local scans of
 // MSM_SCAN_ITEMS buckets (4 per lane) + block totals; pass 2: one block scans
 // the totals; pass 3: adds the block offsets, copies the cursor and fills the
-// chunk map (unused slots keep chunk_bkt = -1 from the memset).
+// chunk map; k_msm_chunks ignores slots past the chunk total (blk[2 NBLK + 1]).
 __global__ void __launch_bounds__(256) k_msm_scan1(int NB, const uint32_t* __restrict__ counts,
                                                    uint32_t* __restrict__ offsets, uint32_t* __restrict__ chunk_off,
                                                    uint32_t* __restrict__ blk) {
@@ -138,6 +138,10 @@ __global__ void __launch_bounds__(256) k_msm_scan2(int nblk, uint32_t* __restric
       rc += c;
     }
   }
+  if (t == 255) {  // totals: entries, chunk slots in use
+    blk[2 * nblk] = pe[255];
+    blk[2 * nblk + 1] = pc[255];
+  }
 }
 
 __global__ void __launch_bounds__(256) k_msm_scan3(int NB, const uint32_t* __restrict__ counts,
@@ -149,28 +153,30 @@ __global__ void __launch_bounds__(256) k_msm_scan3(int NB, const uint32_t* __res
   const int q = b / MSM_SCAN_ITEMS;
   const uint32_t o = offsets[b] + blk[2 * q], oc = chunk_off[b] + blk[2 * q + 1];
   offsets[b] = o;
-  cursor[b] = o;
   chunk_off[b] = oc;
   const uint32_t nch = (counts[b] + MSM_CH - 1) / MSM_CH;
   for (uint32_t c = 0; c < nch; c++) chunk_bkt[oc + c] = b;
 }
 
+// counting-sort scatter without atomics: position = bucket offset + the
+// rank the histogram atomic returned in k_msm_digits
 __global__ void __launch_bounds__(256) k_msm_scatter(int NV, int nw, const int32_t* __restrict__ keys,
-                                                     uint32_t* __restrict__ cursor, uint32_t* __restrict__ sorted) {
+                                                     const uint32_t* __restrict__ ranks,
+                                                     const uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= NV) return;
   for (int w = 0; w < nw; w++) {
     int key = keys[(size_t)w * NV + i];
     if (key == -1) continue;
     uint32_t b = (uint32_t)key & 0x7fffffffu;
-    uint32_t pos = atomicAdd(&cursor[b], 1u);  // global position (flat sorted array)
-    sorted[pos] = (uint32_t)i | ((uint32_t)key & 0x80000000u);
+    sorted[offsets[b] + ranks[(size_t)w * NV + i]] = (uint32_t)i | ((uint32_t)key & 0x80000000u);
   }
 }
 
 // one lane per chunk slot: <= MSM_CH mixed additions of sorted virtual points
 // (index >= N: phi(P_{index-N}) = (beta x, y))
-__global__ void __launch_bounds__(64, 4) k_msm_chunks(int N, int nw, int NC, const MsmWindow* __restrict__ win,
+__global__ void __launch_bounds__(64, 4) k_msm_chunks(int N, int nw, const uint32_t* __restrict__ nc_total,
+                                                   const MsmWindow* __restrict__ win,
                                                    const uint32_t* __restrict__ points,
                                                    const uint32_t* __restrict__ offsets,
                                                    const uint32_t* __restrict__ counts,
@@ -178,9 +184,8 @@ __global__ void __launch_bounds__(64, 4) k_msm_chunks(int N, int nw, int NC, con
                                                    const int32_t* __restrict__ chunk_bkt,
                                                    const uint32_t* __restrict__ sorted, uint32_t* __restrict__ partials) {
   int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= NC) return;
+  if (g >= (int)*nc_total) return;
   const int b = chunk_bkt[g];
-  if (b < 0) return;
   const uint32_t j = (uint32_t)g - chunk_off[b], cnt = counts[b];
   const uint32_t lo = j * MSM_CH, hi = min(cnt, lo + MSM_CH);
   const uint32_t* S = sorted + offsets[b];
@@ -310,16 +315,16 @@ __global__ void __launch_bounds__(64) k_msm_final(int nw, int WB, const MsmWindo
 void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
                 uint32_t* scratch, hipStream_t s, hipStream_t s_extra, Timeline* tl) {
   (void)hipMemsetAsync(p.counts, 0, (size_t)p.NB * 4, s);
-  (void)hipMemsetAsync(p.chunk_bkt, 0xff, (size_t)p.NC * 4, s);
-  FTS_LAUNCH(k_msm_digits, p.N, 256, s, p.N, p.nw, p.d_win, scalars, p.keys, p.counts);
+  FTS_LAUNCH(k_msm_digits, p.N, 256, s, p.N, p.nw, p.d_win, scalars, p.keys, p.cursor, p.counts);
   tl->mark("k_msm_digits", s, 0);
   FTS_LAUNCH(k_msm_scan1, (size_t)p.NBLK * 256, 256, s, p.NB, p.counts, p.offsets, p.chunk_off, p.scratch);
   hipLaunchKernelGGL(k_msm_scan2, dim3(1), dim3(256), 0, s, p.NBLK, p.scratch);
   FTS_LAUNCH(k_msm_scan3, p.NB, 256, s, p.NB, p.counts, p.offsets, p.cursor, p.chunk_off, p.chunk_bkt, p.scratch);
   tl->mark("k_msm_scan", s, 0);
-  FTS_LAUNCH(k_msm_scatter, p.NV, 256, s, p.NV, p.nw, p.keys, p.cursor, p.sorted);
+  FTS_LAUNCH(k_msm_scatter, p.NV, 256, s, p.NV, p.nw, p.keys, p.cursor, p.offsets, p.sorted);
   tl->mark("k_msm_scatter", s, 0);
-  FTS_LAUNCH(k_msm_chunks, p.NC, 64, s, p.N, p.nw, p.NC, p.d_win, points, p.offsets, p.counts, p.chunk_off,
+  FTS_LAUNCH(k_msm_chunks, p.NC, 64, s, p.N, p.nw, p.scratch + 2 * (size_t)p.NBLK + 1, p.d_win, points, p.offsets,
+             p.counts, p.chunk_off,
              p.chunk_bkt, p.sorted, p.partials);
   // expected nonzero digits: N * nw * (1 - 2^-c) ~ N * nw mixed additions
   tl->mark("k_msm_chunks", s, (double)p.NV * p.nw * (COST_MADD + 0.5));
@@ -328,7 +333,7 @@ void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalar
   FTS_LAUNCH(k_msm_segments, p.NS, 64, s, p.nw, p.NS, p.d_win, p.buckets, p.segs, scratch);
   tl->mark("k_msm_segments", s, (double)p.NB * 2 * COST_ADD);
   if (s_extra != s) tl->fork(s_extra, s);
-  uint32_t* parts = p.scratch + 2 * (size_t)p.NBLK;
+  uint32_t* parts = p.scratch + 2 * (size_t)p.NBLK + 2;
   hipLaunchKernelGGL(k_msm_windows, dim3(p.nw + 1, p.WB), dim3(256), 0, s, p.nw, p.WB, p.d_win, p.segs, extra, nextra,
                      parts);
   tl->mark("k_msm_windows", s, (double)(p.NS + nextra) * COST_ADD);

@@ -33,7 +33,8 @@ namespace fts {
 
 constexpr int NORM_BS = 256;
 constexpr int NORM_E = 4;  // points per lane of k_rp_normalize
-__global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, const int32_t* __restrict__ status,
+__global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, int stride, int first,
+                                                          const int32_t* __restrict__ status,
                                                           const uint32_t* __restrict__ jac, uint32_t* __restrict__ aff,
                                                           uint8_t* __restrict__ be);
 
@@ -85,6 +86,31 @@ __global__ void __launch_bounds__(64) kt_entries(int nb, const uint32_t* __restr
   G1J p = load_g1j(small + (bw * FB_S + lo) * 24);
   if (hi) p = nl_add_mem(p, large + (bw * FB_L + hi) * 24, 0);
   store_g1j(jac + gid * 24, p);
+}
+
+// ------------------------------------------------------------------ gather
+// thread per (proof, 16-byte chunk) of the merged pass: raw points
+// (npts x 64 B), canonical scalars (RP_NSC x 32 B), host verdicts, IPA flags
+__global__ void __launch_bounds__(256) k_rp_gather(RpGather g, int npts, uint8_t* __restrict__ raw,
+                                                   uint32_t* __restrict__ sc, int32_t* __restrict__ status,
+                                                   int32_t* __restrict__ ipa) {
+  const int per = npts * 4 + RP_NSC * 2 + 1;  // uint4 chunks of raw, sc, + 1 lane for the two flags
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int B = g.off[g.G];
+  if (gid >= (size_t)B * per) return;
+  const int p = (int)(gid / per), c = (int)(gid % per);
+  int q = 0;
+  while (q + 1 < g.G && g.off[q + 1] <= p) q++;
+  const int i = p - g.off[q];
+  if (c < npts * 4) {
+    reinterpret_cast<uint4*>(raw)[(size_t)p * npts * 4 + c] = reinterpret_cast<const uint4*>(g.raw[q])[(size_t)i * npts * 4 + c];
+  } else if (c < npts * 4 + RP_NSC * 2) {
+    const int cc = c - npts * 4;
+    reinterpret_cast<uint4*>(sc)[(size_t)p * RP_NSC * 2 + cc] = reinterpret_cast<const uint4*>(g.sc[q])[(size_t)i * RP_NSC * 2 + cc];
+  } else {
+    status[p] = g.status0[q][i];
+    ipa[p] = g.ipa[q][i];
+  }
 }
 
 // ------------------------------------------------------------------ decode
@@ -387,8 +413,8 @@ __global__ void __launch_bounds__(64) k_rp_com_sum(int B, int n, int k, const in
 }
 
 // Batch affine normalisation (Montgomery's trick), NORM_E points per lane and
-// NORM_BS * NORM_E points per block ([B][per] Jacobian; points of proofs with
-// status != 0 are skipped, identities map to (0, 0)):
+// NORM_BS * NORM_E points per block (point g lives at index g * stride + first;
+// points of proofs with status[g / per] != 0 are skipped, identities map to (0, 0)):
 //   1. lane-local prefix products of its NORM_E z's (strided by NORM_BS, so
 //      every load/store is coalesced),
 //   2. Hillis-Steele prefix + suffix scans of the lane totals in LDS,
@@ -396,7 +422,8 @@ __global__ void __launch_bounds__(64) k_rp_com_sum(int B, int n, int k, const in
 //   4. lane-local back-sweep: z_j^-1, then x z^-2, y z^-3.
 // ~9 products per point (the scans cost 16 / NORM_E per point).  Writes affine
 // Montgomery (aff, 16 words) and the canonical 64-byte BE encoding (be).
-__global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, const int32_t* __restrict__ status,
+__global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, int stride, int first,
+                                                          const int32_t* __restrict__ status,
                                                           const uint32_t* __restrict__ jac, uint32_t* __restrict__ aff,
                                                           uint8_t* __restrict__ be) {
   __shared__ uint32_t pre[NORM_BS * 8], suf[NORM_BS * 8];
@@ -408,7 +435,7 @@ __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, co
     z = f_one<FpP>();
     if (g >= (size_t)total || (status && status[g / per] != 0)) return false;
     Fp zz;
-    load_fp(jac + g * 24 + 16, zz);
+    load_fp(jac + (g * stride + first) * 24 + 16, zz);
     if (!f_is_zero(zz)) z = zz;
     return true;
   };
@@ -468,7 +495,7 @@ __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, co
     Fp zi = j ? fp_mul(inv, acc[j - 1]) : inv;  // z_j^-1
     if (j) inv = fp_mul(inv, z);
     if (!live) continue;
-    const size_t g = g0 + (size_t)j * NORM_BS;
+    const size_t g = (g0 + (size_t)j * NORM_BS) * stride + first;
     const G1J p = load_g1j(jac + g * 24);
     G1A r;
     if (f_is_zero(p.z)) {
@@ -485,50 +512,71 @@ __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, co
 }
 
 // --------------------------------------------------------- x0 transcript
-// thread per (proof, record r in [0, 2n+2]); record 2n+2 writes DER framing
+// The x0 message DER(SEQUENCE{OCTET(Arr(H'_0..H'_{n-1}, G_0..G_{n-1}, Q, com)),
+// OCTET("||"), OCTET(Zb(ip))}) + SHA-256 padding (ipa.go:200-213) as 16-bit
+// units (2 hex chars, "||", DER bytes, padding; first byte in the low half).
+struct X0Src {
+  const uint8_t* hp;     // this proof's n+1 canonical BE points (H'..., com)
+  const uint16_t* cst;   // hex(G_0) "||" ... hex(Q) "||"
+  const uint32_t* ip;    // Zb(ip): canonical LE limbs
+  uint32_t A, len, end;  // array length, message length, padded length (bytes)
+  int n;
+};
+FTS_DEV uint32_t x0_unit(const X0Src& m, uint32_t u) {
+  const uint32_t pos = 2u * u;
+  if (pos < 8) {  // 30 82 L L 04 82 A A
+    const uint32_t L = m.A + 42u;
+    return pos == 0 ? 0x8230u : pos == 2 ? ((L >> 8) | ((L & 0xffu) << 8)) : pos == 4 ? 0x8204u
+                                                                           : ((m.A >> 8) | ((m.A & 0xffu) << 8));
+  }
+  uint32_t off = pos - 8u;
+  if (off < m.A) {
+    const uint32_t r = off / 130u, o = off - 130u * r;
+    if (r >= (uint32_t)m.n && r <= 2u * m.n) return m.cst[(130u * (r - m.n) + o) >> 1];
+    if (o == 128u) return 0x7c7cu;
+    return hex2(m.hp[(r < (uint32_t)m.n ? r : (uint32_t)m.n) * 64u + (o >> 1)]);
+  }
+  off -= m.A;
+  if (off < 38u) {  // 04 02 "||" 04 20 Zb(ip)
+    if (off < 6u) return off == 0 ? 0x0204u : off == 2 ? 0x7c7cu : 0x2004u;
+    const uint32_t k = off - 6u;  // even byte index into Zb(ip)
+    const uint32_t wd = m.ip[7 - (k >> 2)];
+    return (k & 2u) ? (((wd >> 8) & 0xffu) | ((wd & 0xffu) << 8)) : ((wd >> 24) | (((wd >> 16) & 0xffu) << 8));
+  }
+  if (pos == m.len) return 0x0080u;
+  if (pos >= m.end - 8u) {  // 64-bit big-endian bit length
+    const uint64_t bits = (uint64_t)m.len * 8u;
+    const uint32_t k = pos - (m.end - 8u);  // 0, 2, 4, 6
+    const uint32_t b0 = (uint32_t)(bits >> (56 - 8 * k)) & 0xffu, b1 = (uint32_t)(bits >> (48 - 8 * k)) & 0xffu;
+    return b0 | (b1 << 8);
+  }
+  return 0u;
+}
+
+// thread per (16-byte chunk, proof): each writes one uint4 of the padded
+// message, so a wave's stores cover 1 KB of one proof's message contiguously
 __global__ void __launch_bounds__(256) k_rp_x0_build(int B, int n, const int32_t* __restrict__ status,
                                                      const uint8_t* __restrict__ hp_be,
                                                      const uint8_t* __restrict__ x0_const, const uint32_t* __restrict__ sc,
                                                      uint8_t* __restrict__ msgs) {
-  const int nrec = 2 * n + 3;
-  int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= B * nrec) return;
-  int b = gid / nrec, r = gid % nrec;
+  const uint32_t nchk = x0_slot_bytes(n) / 16u;
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (size_t)B * nchk) return;
+  const int b = (int)(gid / nchk);
+  const uint32_t c = (uint32_t)(gid % nchk);
   if (status[b] != 0) return;
-  uint8_t* m = msgs + (size_t)b * x0_slot_bytes(n);
-  const uint32_t A = x0_array_len(n);
-  if (r < n) {
-    uint32_t pw[16];
-    load_be_words(hp_be + ((size_t)b * (n + 1) + r) * 64, pw);
-    put_hex_record(m, 8 + 130u * r, pw, true);
-  } else if (r < 2 * n + 1) {
-    const uint16_t* src = reinterpret_cast<const uint16_t*>(x0_const + 130u * (r - n));
-    uint16_t* dst = reinterpret_cast<uint16_t*>(m + 8 + 130u * r);
-    for (int q = 0; q < 65; q++) dst[q] = src[q];
-  } else if (r == 2 * n + 1) {
-    uint32_t pw[16];
-    load_be_words(hp_be + ((size_t)b * (n + 1) + n) * 64, pw);
-    put_hex_record(m, 8 + 130u * r, pw, false);
-  } else {
-    uint16_t* m16 = reinterpret_cast<uint16_t*>(m);
-    const uint32_t L = A + 42u;  // SEQUENCE content
-    m16[0] = 0x8230;
-    m16[1] = (uint16_t)((L >> 8) | ((L & 0xffu) << 8));
-    m16[2] = 0x8204;
-    m16[3] = (uint16_t)((A >> 8) | ((A & 0xffu) << 8));
-    uint16_t* t = reinterpret_cast<uint16_t*>(m + 8 + A);
-    t[0] = 0x0204;
-    t[1] = 0x7c7c;
-    t[2] = 0x2004;
-    const uint32_t* ip = sc + ((size_t)b * RP_NSC + RP_SC_IP) * 8;
+  X0Src m;
+  m.hp = hp_be + (size_t)b * (n + 1) * 64;
+  m.cst = reinterpret_cast<const uint16_t*>(x0_const);
+  m.ip = sc + ((size_t)b * RP_NSC + RP_SC_IP) * 8;
+  m.A = x0_array_len(n);
+  m.len = x0_msg_len(n);
+  m.end = x0_slot_bytes(n);
+  m.n = n;
+  uint32_t v[4];
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      uint32_t wd = ip[7 - i];  // BE word i
-      t[3 + 2 * i] = (uint16_t)((wd >> 24) | (((wd >> 16) & 0xffu) << 8));
-      t[4 + 2 * i] = (uint16_t)(((wd >> 8) & 0xffu) | ((wd & 0xffu) << 8));
-    }
-    write_sha_padding_u16(m, x0_msg_len(n));
-  }
+  for (int q = 0; q < 4; q++) v[q] = x0_unit(m, 8u * c + 2u * q) | (x0_unit(m, 8u * c + 2u * q + 1u) << 16);
+  reinterpret_cast<uint4*>(msgs + (size_t)b * m.end)[c] = make_uint4(v[0], v[1], v[2], v[3]);
 }
 
 __global__ void __launch_bounds__(64) k_rp_x0_hash(int B, int n, int k, const int32_t* __restrict__ status,
@@ -853,8 +901,8 @@ void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32
   FTS_LAUNCH(kt_small_large, nbw, 64, s, nb, bw, small, large);
   FTS_LAUNCH(kt_entries, nbw * FB_E, 64, s, nb, small, large, jac);
   const size_t tot = nbw * FB_E;
-  FTS_LAUNCH(k_rp_normalize, (tot + NORM_E - 1) / NORM_E, NORM_BS, s, (int)tot, 1, (const int32_t*)nullptr, jac, tables,
-             (uint8_t*)nullptr);
+  FTS_LAUNCH(k_rp_normalize, (tot + NORM_E - 1) / NORM_E, NORM_BS, s, (int)tot, 1, 1, 0, (const int32_t*)nullptr, jac,
+             tables, (uint8_t*)nullptr);
 }
 
 void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
@@ -888,11 +936,12 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   FTS_LAUNCH(k_rp_com_sum, B, 64, s, B, n, k, d.status, d.pts, d.terms, d.hpj);
   tl->mark("k_rp_com_sum", s, (double)B * COM_NTERMS * COST_ADD);
   const int npt = B * (n + 1);
-  FTS_LAUNCH(k_rp_normalize, (npt + NORM_E - 1) / NORM_E, NORM_BS, s, npt, n + 1, d.status, d.hpj, d.hpa, d.hp_be);
+  FTS_LAUNCH(k_rp_normalize, (npt + NORM_E - 1) / NORM_E, NORM_BS, s, npt, n + 1, 1, 0, d.status, d.hpj, d.hpa, d.hp_be);
   tl->mark("k_rp_normalize", s, (double)npt * (2.0 * 8.0 / NORM_E + 9.0));
   // side: x0 transcript + hash, then the fixed-base columns (need x0)
   tl->fork(s, s2);
-  FTS_LAUNCH(k_rp_x0_build, B * (2 * n + 3), 256, s2, B, n, d.status, d.hp_be, x0_const, d.sc, d.x0_msgs);
+  FTS_LAUNCH(k_rp_x0_build, (size_t)B * (x0_slot_bytes(n) / 16), 256, s2, B, n, d.status, d.hp_be, x0_const, d.sc,
+             d.x0_msgs);
   tl->mark("k_rp_x0_build", s2, 0);
   FTS_LAUNCH(k_rp_x0_hash, B, 64, s2, B, n, k, d.status, d.x0_msgs, d.ch);
   tl->mark("k_rp_x0_hash", s2, 0);
@@ -909,6 +958,11 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
 }
 
 // per-proof final equations (fallback when the batch combination fails)
+void launch_rp_gather(const RpGather& g, int k, uint8_t* raw, uint32_t* sc, int32_t* status, int32_t* ipa, hipStream_t s) {
+  const int per = rp_npts(k) * 4 + RP_NSC * 2 + 1;
+  FTS_LAUNCH(k_rp_gather, (size_t)g.off[g.G] * per, 256, s, g, rp_npts(k), raw, sc, status, ipa);
+}
+
 void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, hipStream_t s, Timeline* tl) {
   const int B = d.B, n = d.n, k = d.k;
   FTS_LAUNCH(k_rp_terms_fixed, B * (3 + 2 * n), 64, s, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, tables, d.terms);

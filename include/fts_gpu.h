@@ -122,9 +122,9 @@ int fts_rp_batch_stage(fts_ctx* ctx, size_t n, const uint8_t* const* rp_der, con
                        const uint8_t* com64, fts_rp_batch** out);
 /* runs the whole GPU verification of a staged batch; status may be NULL.
  * Thread-safe: concurrent calls on DIFFERENT batches run on different lanes
- * (stream pairs, FTS_LANES env, default 4) and overlap on the device; batches
+ * (stream pairs, FTS_LANES env, default 3) and overlap on the device; batches
  * submitted while every lane is busy are coalesced into one device pass of
- * up to FTS_COALESCE_MAX proofs (default 16384).  Verdicts are per proof and
+ * up to FTS_COALESCE_MAX proofs (default 32768).  Verdicts are per proof and
  * independent of the grouping. */
 int fts_rp_batch_verify(fts_ctx* ctx, fts_rp_batch* b, int32_t* status);
 /* number of staged batches (including b) in the device pass that verified b last */
