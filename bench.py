@@ -8,8 +8,16 @@ HBM, verdicts delivered to the host; for N > 1 the per-GPU verdict bitmaps
 are all-gathered over RCCL (the only exchange step).  Weak
 scaling: every rank verifies its own 4,096-proof batch.
 
+Other BASELINE.json configs as extra workloads (not the default line):
+  --workload msm       configs[2] / C3: one BN254 G1 MSM over 2^--msm-log points
+                       (fts_msm_run on staged inputs), terms/s
+  --workload transfer  configs[3] / C4 per GPU: --transfers 2-in/2-out 64-bit
+                       transfers (TypeAndSum + 2 rp64 each) per step through
+                       fts_transfer_verify_batch, transfers/s
+
 Prints one JSON line (rank 0).  Usage:
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--bits 64]
+  python bench.py --workload msm --msm-log 20
   torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
@@ -59,7 +67,14 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall-time bound of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--workload", choices=["rp", "msm", "transfer"], default="rp")
+    ap.add_argument("--msm-log", type=int, default=20, help="msm workload: log2 of the point count")
+    ap.add_argument("--transfers", type=int, default=8192, help="transfer workload: transfers per GPU per step")
     args = ap.parse_args()
+    if args.workload == "msm":
+        return bench_msm(args)
+    if args.workload == "transfer":
+        return bench_transfer(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -234,6 +249,202 @@ def main():
             "prove_s": round(prove_s, 2),
         }
         print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+# ------------------------------------------------------------- extra workloads
+def _dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local, dist
+
+
+def _max_over_ranks(dist, x):
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _seq_points(m):
+    """P_i = (i+1) G for i < m (affine, successive additions; synthetic input)"""
+    p, G = 21888242871839275222246405745257275088696311157297823662689037894645226208583, (1, 2)
+    out, (x, y) = [], G
+    out.append((x, y))
+    for _ in range(m - 1):
+        if x == G[0]:
+            lam = 3 * x * x * pow(2 * y, -1, p) % p
+        else:
+            lam = (y - G[1]) * pow(x - G[0], -1, p) % p
+        x3 = (lam * lam - x - G[0]) % p
+        y = (lam * (x - x3) - y) % p
+        x = x3
+        out.append((x, y))
+    return out
+
+
+def _mul_g(k):
+    """k G (double-and-add, affine; used once to check the MSM result)"""
+    p = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+    acc, base = None, (1, 2)
+    while k:
+        if k & 1:
+            acc = base if acc is None else _add(acc, base, p)
+        base = _add(base, base, p)
+        k >>= 1
+    return acc
+
+
+def _add(a, b, p):
+    if a[0] == b[0]:
+        if (a[1] + b[1]) % p == 0:
+            return None
+        lam = 3 * a[0] * a[0] * pow(2 * a[1], -1, p) % p
+    else:
+        lam = (b[1] - a[1]) * pow(b[0] - a[0], -1, p) % p
+    x3 = (lam * lam - a[0] - b[0]) % p
+    return (x3, (lam * (a[0] - x3) - a[1]) % p)
+
+
+def _roofline_from(timings, steps):
+    """dominant kernel (largest algorithmic MAD count) of the per-kernel timings"""
+    dom = max(timings, key=lambda k: timings[k][1])
+    ms, mads = timings[dom][0] / steps, timings[dom][1]
+    ach = mads / (ms * 1e-3) / 1e12 if mads and ms > 0 else None
+    return {"bound": "int32_valu (v_mad_u64_u32)", "kernel": dom, "achieved": round(ach, 3) if ach else None,
+            "peak": round(PEAK_TMAD, 3), "unit": "TMAD/s", "frac": round(ach / PEAK_TMAD, 4) if ach else None,
+            "traffic": None, "kernel_ms": round(ms, 4), "mads_per_launch": mads}
+
+
+def bench_msm(args):
+    world, rank, local, dist = _dist_setup()
+    import random
+    import fts_gpu
+    with open(os.path.join(ROOT, "tests", "golden", "zkatdlog_pp.json"), "rb") as f:
+        pp_raw = f.read()
+    pp = fts_gpu.PublicParams(pp_raw, bit_length=args.bits, device=local)
+    n = 1 << args.msm_log
+    t0 = time.time()
+    m = min(n, 1 << 16)
+    base = b"".join(x.to_bytes(32, "big") + y.to_bytes(32, "big") for x, y in _seq_points(m))
+    pts = base * (n // m)
+    rng = random.Random(0xF7A50003 + rank)
+    ks = [rng.randrange(R_ORDER) for _ in range(n)]
+    scs = b"".join(k.to_bytes(32, "big") for k in ks)
+    st = pp.stage_msm(pts, scs)
+    setup_s = time.time() - t0
+    for _ in range(max(1, args.warmup)):
+        res = st.run()
+    e = _mul_g(sum(k * (i % m + 1) for i, k in enumerate(ks)) % R_ORDER)
+    assert res == (bytes(64) if e is None else e[0].to_bytes(32, "big") + e[1].to_bytes(32, "big")), "MSM mismatch"
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    kt = {}
+    for _ in range(args.steps):
+        st.run()
+        for name, (ms, mads) in st.timings().items():
+            o = kt.get(name, (0.0, 0.0))
+            kt[name] = (o[0] + ms, mads)
+    elapsed = _max_over_ranks(dist, time.perf_counter() - t0)
+    value = world * n * args.steps / elapsed
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        from oracle import cref
+        thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        done, cs = 0, 0.0
+        while cs < args.cpu_seconds and done < n:
+            c = min(1024, n - done)
+            t1 = time.perf_counter()
+            cref.msm(pts[64 * done:64 * (done + c)], scs[32 * done:32 * (done + c)], threads=thr)
+            cs += time.perf_counter() - t1
+            done += c
+        cpu = {"value": round(done / cs, 1), "unit": "terms/s", "cores": thr, "kind": "port",
+               "sample": "%d terms of the same MSM, term-by-term G1.Mul + Add (oracle/c/ref_verify.c oracle_msm, "
+                         "no Pippenger), %d threads, %.1f s wall" % (done, thr, cs)}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "BN254 G1 MSM terms/sec (2^%d points)" % args.msm_log, "value": round(value, 1),
+            "unit": "terms/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32 (BN254 Fp 8x32-bit Montgomery)",
+            "data": "synthetic: P_i = (i mod 2^16 + 1) G, uniform scalars mod r (seed 0xF7A50003 + rank)",
+            "config": {"workload": "C3: standalone G1 MSM, 2^%d points per GPU (fts_msm_run, inputs resident in HBM)"
+                                   % args.msm_log, "points": n, "parallelism": "shard%d" % world},
+            "roofline": _roofline_from(kt, args.steps), "cpu_baseline": cpu,
+            "kernel_ms": {k: round(v[0] / args.steps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),
+            flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_transfer(args):
+    world, rank, local, dist = _dist_setup()
+    import random
+    import numpy as np
+    import fts_gpu
+    with open(os.path.join(ROOT, "tests", "golden", "zkatdlog_pp.json"), "rb") as f:
+        pp_raw = f.read()
+    pp = fts_gpu.PublicParams(pp_raw, bit_length=args.bits, device=local)
+    T = b"ABC"
+    rng = random.Random(0xF7A50004 + rank)
+    t0 = time.time()
+    distinct = min(args.transfers, 512)
+    base = []
+    for i in range(distinct):
+        a, b_ = rng.getrandbits(args.bits - 2), rng.getrandbits(args.bits - 2)
+        c = rng.randrange(a + b_ + 1)
+        inv, outv = [a, b_], [c, a + b_ - c]
+        ib = [rng.randrange(R_ORDER).to_bytes(32, "big") for _ in range(2)]
+        ob = [rng.randrange(R_ORDER).to_bytes(32, "big") for _ in range(2)]
+        ins = [pp.token_commit(T, v, bf) for v, bf in zip(inv, ib)]
+        outs = [pp.token_commit(T, v, bf) for v, bf in zip(outv, ob)]
+        base.append((ins, outs, pp.prove_transfer(T, inv, ib, outv, ob, 0xF7A50004 + i)))
+    batch = pp.prepare_transfers([base[i % distinct] for i in range(args.transfers)])
+    setup_s = time.time() - t0
+    for _ in range(max(1, args.warmup)):
+        st, fi = batch.verify()
+    assert int((st != 0).sum()) == 0, "honest transfers rejected"
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    kt = {}
+    for _ in range(args.steps):
+        st, fi = batch.verify()  # host buffers in (the C-ABI parses the DER proofs), verdicts out
+        for name, (ms, mads) in pp.last_timings_ex().items():
+            o = kt.get(name, (0.0, 0.0))
+            kt[name] = (o[0] + ms, mads)
+        if dist is not None:
+            import torch
+            bits = torch.from_numpy(np.packbits(st == 0)).cuda()
+            out = torch.empty(world * bits.numel(), dtype=torch.uint8, device="cuda")
+            dist.all_gather_into_tensor(out, bits)
+    elapsed = _max_over_ranks(dist, time.perf_counter() - t0)
+    value = world * args.transfers * args.steps / elapsed
+    if rank == 0:
+        print(json.dumps({
+            "metric": "2-in/2-out transfer verifies/sec (BN254, %d-bit range proofs)" % args.bits,
+            "value": round(value, 1), "unit": "transfers/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32 (BN254 Fp/Fr 8x32-bit Montgomery)",
+            "data": "synthetic: %d distinct 2-in/2-out transfers (type ABC) from the library's host prover, tiled"
+                    % distinct,
+            "config": {"workload": "C4 per GPU: %d transfers (TypeAndSum + 2 rp%d each) per step via "
+                                   "fts_transfer_verify_batch" % (args.transfers, args.bits),
+                       "transfers_per_gpu": args.transfers, "parallelism": "shard%d" % world},
+            "roofline": _roofline_from(kt, args.steps),
+            "kernel_ms": {k: round(v[0] / args.steps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),
+            flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -290,4 +290,20 @@ FTS_DEV G1J straus2_128(const G1J& P, const uint32_t a[4], const G1J& Q, const u
   return acc;
 }
 
+// k * P for a canonical scalar k < r in one lane: GLV split k = k1 + k2 lambda,
+// then the joint chain k1 P + k2 phi(P) (124 doublings instead of 252);
+// tab/stride/idx: the lane's 16-entry table (straus2_128).  Keep it inlined
+// at ONE call site per kernel: an out-of-line (__noinline__) build of this
+// function never terminated on gfx950 (tools/glv_check reproduces it).
+FTS_DEV G1J glv_mul(const G1A& p, const Scalar& k, uint32_t* __restrict__ tab, size_t stride, size_t idx) {
+  if (g1a_is_identity(p)) return g1j_identity();
+  uint32_t k1[4], k2[4], s1, s2;
+  glv_decompose(k.v, k1, s1, k2, s2);
+  G1J P = g1j_from_affine(p), Q = P;
+  Q.x = fp_mul(Q.x, glv_beta());  // phi(P)
+  if (s1) P.y = f_neg(P.y);
+  if (s2) Q.y = f_neg(Q.y);
+  return straus2_128(P, k1, Q, k2, tab, stride, idx);
+}
+
 }  // namespace fts

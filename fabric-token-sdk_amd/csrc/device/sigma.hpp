@@ -27,6 +27,10 @@ struct SigAction {
 constexpr int TAS_SC_TYPE = 0, TAS_SC_TBF = 1, TAS_SC_EQ = 2, TAS_SC_CHAL = 3, TAS_SC_IV = 4;
 constexpr int ST_SC_TYPE = 0, ST_SC_BF = 1, ST_SC_CHAL = 2;
 
+// k_sig_terms scratch per work item: a 16-entry GLV/Straus table + one point
+constexpr int SIG_VTAB_WORDS = 16 * 24;
+inline __host__ __device__ size_t sig_scratch_words(size_t nwork) { return nwork * (SIG_VTAB_WORDS + 24); }
+
 inline __host__ __device__ int sig_nterms(int kind, int n_in) { return kind == SIG_TAS ? 2 * n_in + 4 : 2; }
 inline __host__ __device__ int sig_nscalars(int kind, int n_in) { return kind == SIG_TAS ? 4 + 2 * n_in : 3; }
 // transcript points: TAS inComs(n_in), typeCom, sumCom, in'(n_in), out'(n_out), CT, sum ; ST CT, com
@@ -58,7 +62,7 @@ struct SigBatchDev {
   int32_t* aff_off;   // [A] first affine scratch slot
   uint8_t* msgs;      // transcript slots
   uint32_t* jac;      // per-action Jacobian scratch [sum naff][24] (same offsets as aff)
-  uint32_t* scratch;  // var-base lane tables [nwork][10*24]
+  uint32_t* scratch;  // sig_scratch_words(nwork): GLV lane tables + add_via temporaries
   uint8_t* rp_raw;    // rp batch raw points (V slots are written here), may be null
   int rp_k;           // rounds of the rp batch
 };

@@ -39,6 +39,11 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
                      hipStream_t s, hipStream_t s2, Timeline* tl);
 void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, hipStream_t s, Timeline* tl);
 void launch_rp_gather(const RpGather& g, int k, uint8_t* raw, uint32_t* sc, int32_t* status, int32_t* ipa, hipStream_t s);
+void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
+                uint32_t* scratch, hipStream_t s, hipStream_t s_extra, Timeline* tl);
+void launch_msm_load(int N, const uint8_t* raw_pts, const uint8_t* raw_sc, uint32_t* pts, uint32_t* sc, uint32_t* bad,
+                     hipStream_t s);
+void launch_msm_to_bytes(const uint32_t* jac, uint8_t* out, hipStream_t s);
 void launch_sig_prep(const SigBatchDev& d, hipStream_t s);
 void launch_sig_finish(const SigBatchDev& d, const uint32_t* tables, int n, hipStream_t s);
 size_t table_build_scratch_bytes(int nb);
@@ -507,6 +512,40 @@ static void collect_timings(fts_ctx* c, Lane& L, fts_rp_batch* b) {
   }
 }
 
+// MSM plan for N real points on lane L's workspace (buffers grown as needed,
+// window table uploaded on L.s).  Returns 0 or FTS_API_ENOMEM.
+static int msm_prepare(Lane& L, int N, MsmPlan& mp) {
+  Workspace& w = L.ws;
+  mp = MsmPlan{};
+  msm_layout(N, mp);
+  if (w.m_choff.ensure((size_t)mp.NB * 4) || w.m_chbkt.ensure((size_t)mp.NC * 4) ||
+      w.m_partials.ensure((size_t)mp.NC * 96) || w.m_keys.ensure((size_t)mp.nw * mp.NV * 4) ||
+      w.m_counts.ensure((size_t)mp.NB * 4) || w.m_offsets.ensure((size_t)mp.NB * 4) ||
+      w.m_cursor.ensure((size_t)mp.nw * mp.NV * 4) || w.m_sorted.ensure((size_t)mp.nw * mp.NV * 4) ||
+      w.m_buckets.ensure((size_t)mp.NB * 96) || w.m_segs.ensure((size_t)mp.NS * 96) ||
+      w.m_wins.ensure((size_t)(mp.nw + 1) * 96) || w.m_out.ensure(96) ||
+      w.m_scratch.ensure(std::max((size_t)mp.NS * 96, msm_scratch_words(mp) * 4)) || w.m_win.ensure(sizeof(mp.win)))
+    return FTS_API_ENOMEM;
+  mp.d_win = w.m_win.as<MsmWindow>();
+  memcpy(L.pin->win, mp.win, sizeof(MsmWindow) * mp.nw);
+  if (hipMemcpyAsync(mp.d_win, L.pin->win, sizeof(MsmWindow) * mp.nw, hipMemcpyHostToDevice, L.s) != hipSuccess)
+    return FTS_API_EDEVICE;
+  mp.keys = w.m_keys.as<int32_t>();
+  mp.counts = w.m_counts.as<uint32_t>();
+  mp.offsets = w.m_offsets.as<uint32_t>();
+  mp.cursor = w.m_cursor.as<uint32_t>();
+  mp.sorted = w.m_sorted.as<uint32_t>();
+  mp.buckets = w.m_buckets.as<uint32_t>();
+  mp.segs = w.m_segs.as<uint32_t>();
+  mp.wins = w.m_wins.as<uint32_t>();
+  mp.out = w.m_out.as<uint32_t>();
+  mp.chunk_off = w.m_choff.as<uint32_t>();
+  mp.chunk_bkt = w.m_chbkt.as<int32_t>();
+  mp.partials = w.m_partials.as<uint32_t>();
+  mp.scratch = w.m_scratch.as<uint32_t>();
+  return FTS_API_OK;
+}
+
 // Range-proof pipeline on B proofs already on the device: exact phase, RLC
 // batch check, and the per-proof fallback when the combination fails.
 // `between` (optional) is launched after the RLC check and before the flag
@@ -519,21 +558,15 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   const int N = B * npts;
   const double t_start = now_ms();
   MsmPlan mp{};
-  msm_layout(N, mp);
+  if (int rc = msm_prepare(L, N, mp)) return rc;
   if (w.pts.ensure((size_t)B * npts * 64) || w.ch.ensure((size_t)B * rp_nch(k) * 32) ||
       w.small.ensure((size_t)B * (2 + k) * SMALL_SLOT) || w.hpj.ensure((size_t)B * (n + 1) * 96) ||
       w.hpa.ensure((size_t)B * (n + 1) * 64) || w.hpbe.ensure((size_t)B * (n + 1) * 64) ||
-      w.m_choff.ensure((size_t)mp.NB * 4) || w.m_chbkt.ensure((size_t)mp.NC * 4) ||
-      w.m_partials.ensure((size_t)mp.NC * 96) ||
       w.x0.ensure((size_t)B * x0_slot_bytes(n)) || w.terms.ensure(rp_terms_words(B, n, k) * 4) ||
       w.scratch.ensure(std::max(rp_scratch_words(B, n, k), (size_t)B * 10 * 24) * 4) || w.r_key.ensure(32) ||
       w.r_msc.ensure((size_t)N * 32) || w.r_coef.ensure((size_t)B * 5 * 32) || w.r_colsum.ensure((3 + 2 * n) * 32) ||
-      w.r_fixed.ensure((3 + 2 * n) * 96) || w.r_flag.ensure(4) || w.m_keys.ensure((size_t)mp.nw * mp.NV * 4) ||
-      w.m_counts.ensure((size_t)mp.NB * 4) || w.m_offsets.ensure((size_t)mp.NB * 4) ||
-      w.m_cursor.ensure((size_t)mp.nw * mp.NV * 4) || w.m_sorted.ensure((size_t)mp.nw * mp.NV * 4) ||
-      w.m_buckets.ensure((size_t)mp.NB * 96) || w.m_segs.ensure((size_t)mp.NS * 96) ||
-      w.m_wins.ensure((size_t)(mp.nw + 1) * 96) || w.m_out.ensure(96) || w.m_scratch.ensure(std::max((size_t)mp.NS * 96, msm_scratch_words(mp) * 4)) ||
-      w.m_win.ensure(sizeof(mp.win)) || w.ypow.ensure((size_t)B * n * 32) || w.svec.ensure((size_t)B * n * 32))
+      w.r_fixed.ensure((3 + 2 * n) * 96) || w.r_flag.ensure(4) || w.ypow.ensure((size_t)B * n * 32) ||
+      w.svec.ensure((size_t)B * n * 32))
     return FTS_API_ENOMEM;
   RpBatchDev d{B,
                n,
@@ -553,22 +586,6 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
                w.scratch.as<uint32_t>(),
                w.ypow.as<uint32_t>(),
                w.svec.as<uint32_t>()};
-  mp.d_win = w.m_win.as<MsmWindow>();
-  memcpy(L.pin->win, mp.win, sizeof(MsmWindow) * mp.nw);
-  HIP_OK(hipMemcpyAsync(mp.d_win, L.pin->win, sizeof(MsmWindow) * mp.nw, hipMemcpyHostToDevice, L.s));
-  mp.keys = w.m_keys.as<int32_t>();
-  mp.counts = w.m_counts.as<uint32_t>();
-  mp.offsets = w.m_offsets.as<uint32_t>();
-  mp.cursor = w.m_cursor.as<uint32_t>();
-  mp.sorted = w.m_sorted.as<uint32_t>();
-  mp.buckets = w.m_buckets.as<uint32_t>();
-  mp.segs = w.m_segs.as<uint32_t>();
-  mp.wins = w.m_wins.as<uint32_t>();
-  mp.out = w.m_out.as<uint32_t>();
-  mp.chunk_off = w.m_choff.as<uint32_t>();
-  mp.chunk_bkt = w.m_chbkt.as<int32_t>();
-  mp.partials = w.m_partials.as<uint32_t>();
-  mp.scratch = w.m_scratch.as<uint32_t>();
   RlcDev r{w.r_key.as<uint32_t>(), w.r_msc.as<uint32_t>(),   w.r_coef.as<uint32_t>(), w.r_colsum.as<uint32_t>(),
            w.r_fixed.as<uint32_t>(), w.r_flag.as<int32_t>(), w.m_scratch.as<uint32_t>(), mp};
   // fresh RLC weights key (getrandom), unpredictable to the provers
@@ -796,6 +813,119 @@ int fts_rp_batch_timings(const fts_rp_batch* b, const char** names, float* ms, d
 }
 
 int fts_rp_batch_merged(const fts_rp_batch* b) { return b ? b->merged : 0; }
+
+// ------------------------------------------------- standalone G1 MSM (C3)
+}  // extern "C"
+struct fts_msm_batch {
+  int N = 0;
+  int device = 0;
+  uint32_t* pts = nullptr;  // [N][16] affine Montgomery
+  uint32_t* sc = nullptr;   // [N][8] canonical scalars
+  uint8_t* out = nullptr;   // 64-byte result
+  int ntim = 0;
+  const char* tim_name[Timeline::CAP];
+  float tim_ms[Timeline::CAP];
+  double tim_work[Timeline::CAP];
+};
+extern "C" {
+
+void fts_msm_free(fts_msm_batch* b) {
+  if (!b) return;
+  hipSetDevice(b->device);
+  for (void* p : {(void*)b->pts, (void*)b->sc, (void*)b->out})
+    if (p) hipFree(p);
+  delete b;
+}
+
+int fts_msm_stage(fts_ctx* c, size_t n, const uint8_t* points64, const uint8_t* scalars32, fts_msm_batch** out) {
+  if (!c || !out || !n || !points64 || !scalars32 || n > (size_t)(1u << 26)) return FTS_API_EINVAL;
+  if (c->device < 0) return FTS_API_EDEVICE;
+  HIP_OK(hipSetDevice(c->device));
+  fts_msm_batch* b = new fts_msm_batch();
+  b->N = (int)n;
+  b->device = c->device;
+  uint8_t *rp = nullptr, *rs = nullptr;
+  uint32_t* bad = nullptr;
+  if (hipMalloc(&b->pts, n * 64) != hipSuccess || hipMalloc(&b->sc, n * 32) != hipSuccess ||
+      hipMalloc(&b->out, 64) != hipSuccess || hipMalloc(&rp, n * 64) != hipSuccess || hipMalloc(&rs, n * 32) != hipSuccess ||
+      hipMalloc(&bad, 4) != hipSuccess) {
+    for (void* p : {(void*)rp, (void*)rs, (void*)bad})
+      if (p) hipFree(p);
+    fts_msm_free(b);
+    return FTS_API_ENOMEM;
+  }
+  uint32_t nbad = 0;
+  hipError_t e = hipMemcpy(rp, points64, n * 64, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(rs, scalars32, n * 32, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemset(bad, 0, 4);
+  if (e == hipSuccess) {
+    launch_msm_load((int)n, rp, rs, b->pts, b->sc, bad, 0);
+    e = hipMemcpy(&nbad, bad, 4, hipMemcpyDeviceToHost);
+  }
+  hipFree(rp);
+  hipFree(rs);
+  hipFree(bad);
+  if (e != hipSuccess) {
+    fts_msm_free(b);
+    return FTS_API_EDEVICE;
+  }
+  if (nbad) {  // a point failed NewG1FromBytes (flags, range, on-curve)
+    fts_msm_free(b);
+    return FTS_API_EINVAL;
+  }
+  *out = b;
+  return FTS_API_OK;
+}
+
+int fts_msm_run(fts_ctx* c, fts_msm_batch* b, uint8_t* out64) {
+  if (!c || !b || !out64) return FTS_API_EINVAL;
+  if (c->device < 0) return FTS_API_EDEVICE;
+  HIP_OK(hipSetDevice(c->device));
+  LaneGuard lg(c);
+  Lane& L = *lg.L;
+  MsmPlan mp{};
+  if (int rc = msm_prepare(L, b->N, mp)) return rc;
+  L.tl.begin(L.s);
+  launch_msm(mp, b->pts, b->sc, nullptr, 0, L.ws.m_scratch.as<uint32_t>(), L.s, L.s, &L.tl);
+  launch_msm_to_bytes(mp.out, b->out, L.s);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(out64, b->out, 64, hipMemcpyDeviceToHost, L.s));
+  HIP_OK(hipStreamSynchronize(L.s));
+  b->ntim = 0;
+  for (int i = 0; i < L.tl.n && b->ntim < Timeline::CAP; i++) {
+    if (!L.tl.name[i]) continue;
+    const int j = b->ntim++;
+    b->tim_name[j] = L.tl.name[i];
+    b->tim_work[j] = L.tl.work[i];
+    hipEventElapsedTime(&b->tim_ms[j], L.tl.ev[L.tl.start[i]], L.tl.ev[i + 1]);
+  }
+  return FTS_API_OK;
+}
+
+int fts_msm_timings(const fts_msm_batch* b, const char** names, float* ms, double* mads, int cap) {
+  if (!b) return 0;
+  int m = std::min(cap, b->ntim);
+  for (int i = 0; i < m; i++) {
+    if (names) names[i] = b->tim_name[i];
+    if (ms) ms[i] = b->tim_ms[i];
+    if (mads) mads[i] = b->tim_work[i] * MADS_PER_MUL;
+  }
+  return m;
+}
+
+int fts_msm_g1(fts_ctx* c, size_t n, const uint8_t* points64, const uint8_t* scalars32, uint8_t* out64) {
+  if (!out64) return FTS_API_EINVAL;
+  if (n == 0) {
+    memset(out64, 0, 64);
+    return FTS_API_OK;
+  }
+  fts_msm_batch* b = nullptr;
+  int rc = fts_msm_stage(c, n, points64, scalars32, &b);
+  if (rc != FTS_API_OK) return rc;
+  rc = fts_msm_run(c, b, out64);
+  fts_msm_free(b);
+  return rc;
+}
 
 void fts_rp_batch_free(fts_rp_batch* b) {
   if (!b) return;
@@ -1052,7 +1182,7 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
         w.s_status.ensure(SA * 4) || w.s_work.ensure(s_work.size() * sizeof(int2)) ||
         w.s_terms.ensure((size_t)term_off * 96) || w.s_aff.ensure((size_t)aff_off * 64) ||
         w.s_affoff.ensure(SA * 4) || w.s_msgs.ensure(msg_off) || w.s_jac.ensure((size_t)aff_off * 96) ||
-        w.s_scratch.ensure(s_work.size() * 10 * 24 * 4))
+        w.s_scratch.ensure(sig_scratch_words(s_work.size()) * 4))
       return FTS_API_ENOMEM;
     HIP_OK(hipMemcpyAsync(w.s_act.p, sact.data(), SA * sizeof(SigAction), hipMemcpyHostToDevice, L.s));
     HIP_OK(hipMemcpyAsync(w.s_raw.p, s_raw.data(), s_raw.size(), hipMemcpyHostToDevice, L.s));
@@ -1096,6 +1226,7 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
   }
   auto sig_finish = [&]() {
     if (SA) launch_sig_finish(sd, c->d_tables, n, L.s);
+    if (SA && rp_total) L.tl.mark("k_sig_finish", L.s, 0);
   };
   if (rp_total) {
     int rc = rp_pipeline(c, L, rp_total, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
@@ -1109,6 +1240,7 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
   if (SA) HIP_OK(hipMemcpyAsync(sig_res.data(), w.s_status.p, SA * 4, hipMemcpyDeviceToHost, L.s));
   if (rp_total) HIP_OK(hipMemcpyAsync(rp_res.data(), w.rp_status.p, rp_total * 4, hipMemcpyDeviceToHost, L.s));
   HIP_OK(hipStreamSynchronize(L.s));
+  if (rp_total) collect_timings(c, L, nullptr);
   // ---- combine with the reference's precedence
   for (size_t i = 0; i < A; i++) {
     const ActionState& s = st[i];

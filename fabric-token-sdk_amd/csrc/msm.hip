@@ -303,6 +303,43 @@ __global__ void __launch_bounds__(64) k_msm_final(int nw, int WB, const MsmWindo
   store_g1j(out, acc);
 }
 
+// ------------------------------------------------ standalone MSM (fts_msm_*)
+// Inputs of fts_msm_stage: N raw points (64-byte X||Y BE, NewG1FromBytes
+// checks; 64 zero bytes = identity) and N 32-byte BE scalars (any 256-bit
+// integer, reduced mod r as G1.Mul does).  bad counts rejected points.
+__global__ void __launch_bounds__(256) k_msm_load(int N, const uint8_t* __restrict__ raw_pts,
+                                                  const uint8_t* __restrict__ raw_sc, uint32_t* __restrict__ pts,
+                                                  uint32_t* __restrict__ sc, uint32_t* __restrict__ bad) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  G1A a;
+  if (!decode_point(raw_pts + (size_t)i * 64, a)) {
+    atomicAdd(bad, 1u);
+    a.x = f_zero<FpP>();
+    a.y = f_zero<FpP>();
+  }
+  store_g1a(pts + (size_t)i * 16, a);
+  uint32_t w[8];
+  const uint4* s4 = reinterpret_cast<const uint4*>(raw_sc + (size_t)i * 32);
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const uint4 u = s4[q];
+    w[4 * q + 0] = __builtin_bswap32(u.x);
+    w[4 * q + 1] = __builtin_bswap32(u.y);
+    w[4 * q + 2] = __builtin_bswap32(u.z);
+    w[4 * q + 3] = __builtin_bswap32(u.w);
+  }
+  const Fr k = digest_to_fr(w);  // BE integer mod r (canonical limbs)
+#pragma unroll
+  for (int q = 0; q < 8; q++) sc[(size_t)i * 8 + q] = k.v[q];
+}
+
+// Jacobian result -> 64-byte BE affine (identity -> 64 zero bytes)
+__global__ void k_msm_to_bytes(const uint32_t* __restrict__ jac, uint8_t* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  store_point_be(out, g1j_to_affine(load_g1j(jac)));
+}
+
 #define FTS_LAUNCH(kern, nthreads, bs, stream, ...)                                   \
   do {                                                                                \
     size_t nt_ = (size_t)(nthreads);                                                  \
@@ -339,6 +376,14 @@ void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalar
   tl->mark("k_msm_windows", s, (double)(p.NS + nextra) * COST_ADD);
   hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, s, p.nw, p.WB, p.d_win, parts, p.wins, p.out);
   tl->mark("k_msm_final", s, (double)MSM_BITS * COST_DBL + p.nw * COST_ADD);
+}
+
+void launch_msm_load(int N, const uint8_t* raw_pts, const uint8_t* raw_sc, uint32_t* pts, uint32_t* sc, uint32_t* bad,
+                     hipStream_t s) {
+  FTS_LAUNCH(k_msm_load, N, 256, s, N, raw_pts, raw_sc, pts, sc, bad);
+}
+void launch_msm_to_bytes(const uint32_t* jac, uint8_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_msm_to_bytes, dim3(1), dim3(64), 0, s, jac, out);
 }
 
 }  // namespace fts

@@ -10,6 +10,7 @@
 //                                  SHA-256, Zr.Equals against the proof's challenge
 #include "device/g1.hpp"
 #include "device/fixed_base.hpp"
+#include "device/glv.hpp"
 #include "device/helpers.hpp"
 #include "device/rp_kernels.hpp"
 #include "device/sigma.hpp"
@@ -76,8 +77,8 @@ __global__ void __launch_bounds__(64) k_sig_terms(int nwork, const int2* __restr
   const SigAction ac = act[a];
   const uint32_t* S = sc + (size_t)ac.sc_off * 8;
   const uint32_t* F = aff + (size_t)aff_off[a] * 16;
-  uint32_t* scr = scratch + (size_t)gid * 10 * 24;
-  uint32_t* tmp = scr + 9 * 24;
+  // lane tables of glv_mul: [16 entries][24 words][nwork lanes] (coalesced)
+  uint32_t* tmp = scratch + (size_t)nwork * SIG_VTAB_WORDS + (size_t)gid * 24;
   const uint32_t* t_ped0 = tables + (size_t)tb_ped0(n) * FB_WORDS_PER_BASE;
   const uint32_t* t_ped1 = tables + (size_t)tb_G(n) * FB_WORDS_PER_BASE;
   const uint32_t* t_ped2 = tables + (size_t)tb_H(n) * FB_WORDS_PER_BASE;
@@ -88,6 +89,9 @@ __global__ void __launch_bounds__(64) k_sig_terms(int nwork, const int2* __restr
     return s;
   };
   G1J r;
+  bool var = false;  // variable-base term: r = vk * vp (one inlined GLV chain below)
+  G1A vp;
+  Scalar vk;
   if (ac.kind == SIG_TAS) {
     const int N = ac.n_in;
     const Scalar chal = canon(S + TAS_SC_CHAL * 8);
@@ -97,26 +101,35 @@ __global__ void __launch_bounds__(64) k_sig_terms(int nwork, const int2* __restr
         r = nl_fb_mul(t_ped1, canon(S + (TAS_SC_IV + i) * 8));
         r = add_via(tmp, r, nl_fb_mul(t_ped2, canon(S + (TAS_SC_IV + N + i) * 8)));
       } else {  // c in'_i
-        r = var_base_mul(load_g1a(F + i * 16), chal, scr);
+        var = true;
+        vp = load_g1a(F + i * 16);
+        vk = chal;
       }
     } else if (t == 2 * N) {  // EqualityOfSum ped2
       r = nl_fb_mul(t_ped2, canon(S + TAS_SC_EQ * 8));
     } else if (t == 2 * N + 1) {  // c sum
-      r = var_base_mul(load_g1a(F + (N + ac.n_out) * 16), chal, scr);
+      var = true;
+      vp = load_g1a(F + (N + ac.n_out) * 16);
+      vk = chal;
     } else if (t == 2 * N + 2) {  // Type ped0 + TBF ped2
       r = nl_fb_mul(t_ped0, canon(S + TAS_SC_TYPE * 8));
       r = add_via(tmp, r, nl_fb_mul(t_ped2, canon(S + TAS_SC_TBF * 8)));
     } else {  // c CT
-      r = var_base_mul(load_g1a(pts + (size_t)ac.pt_off * 16), chal, scr);
+      var = true;
+      vp = load_g1a(pts + (size_t)ac.pt_off * 16);
+      vk = chal;
     }
   } else {
     if (t == 0) {  // Type ped0 + BF ped2
       r = nl_fb_mul(t_ped0, canon(S + ST_SC_TYPE * 8));
       r = add_via(tmp, r, nl_fb_mul(t_ped2, canon(S + ST_SC_BF * 8)));
     } else {  // c CT
-      r = var_base_mul(load_g1a(pts + (size_t)ac.pt_off * 16), canon(S + ST_SC_CHAL * 8), scr);
+      var = true;
+      vp = load_g1a(pts + (size_t)ac.pt_off * 16);
+      vk = canon(S + ST_SC_CHAL * 8);
     }
   }
+  if (var) r = glv_mul(vp, vk, scratch, nwork, gid);
   store_g1j(terms + (size_t)(ac.term_off + t) * 24, r);
 }
 

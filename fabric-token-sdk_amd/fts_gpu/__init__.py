@@ -15,6 +15,7 @@ reference                                    here
   transfer/transfer.go:49-60,153-197
 ``issue.NewVerifier(tokens,pp).Verify``       ``IssueVerifier(tokens, pp).Verify(proof)``
   issue/verifier.go:24-57
+gnark-crypto G1 ``MultiExp`` (config C3)      ``PublicParams.msm`` / :class:`StagedMsm`
 ===========================================  =========================================
 
 ``Verify`` returns ``None`` on success and raises :class:`VerifyError`
@@ -30,7 +31,8 @@ import numpy as np
 
 from . import _lib as L
 from ._lib import (FTS_OK, FTS_E_MALFORMED, FTS_E_RP_NIL, FTS_E_RP_INVALID, FTS_E_IPA_NIL, FTS_E_IPA_LEN,  # noqa
-                   FTS_E_IPA_INVALID, FTS_E_RC_COUNT, FTS_E_TAS_INVALID, FTS_E_ST_INVALID, FTS_DEVICE_NONE)
+                   FTS_E_IPA_INVALID, FTS_E_RC_COUNT, FTS_E_TAS_INVALID, FTS_E_ST_INVALID, FTS_DEVICE_NONE,
+                   FtsError)
 
 
 class VerifyError(Exception):
@@ -118,24 +120,29 @@ class PublicParams:
             self._ctx, n, ptrs, lens, coms, st.ctypes.data_as(C.POINTER(C.c_int32))))
         return st
 
+    def msm(self, points, scalars):
+        """sum_i k_i P_i (fts_msm_g1): points = 64-byte X||Y BE each (or one
+        joined bytes object), scalars = 32-byte BE each -> 64-byte result"""
+        pts = points if isinstance(points, (bytes, bytearray)) else b"".join(points)
+        scs = scalars if isinstance(scalars, (bytes, bytearray)) else b"".join(scalars)
+        n = len(pts) // 64
+        assert len(pts) == 64 * n and len(scs) == 32 * n
+        out = C.create_string_buffer(64)
+        L.check("fts_msm_g1", L.lib.fts_msm_g1(self._ctx, n, pts, scs, out))
+        return out.raw
+
+    def stage_msm(self, points, scalars):
+        return StagedMsm(self, points, scalars)
+
     def verify_transfers(self, transfers):
         """transfers: list of (inputs[list of 64B], outputs[list], proof bytes) ->
         (status, fail_index) arrays."""
-        n = len(transfers)
-        items = (L.TransferItem * n)()
-        keep = []
-        for i, (ins, outs, proof) in enumerate(transfers):
-            bi = C.create_string_buffer(b"".join(ins) or b"\0")
-            bo = C.create_string_buffer(b"".join(outs) or b"\0")
-            bp = C.create_string_buffer(proof or b"\0", max(1, len(proof)))
-            keep += [bi, bo, bp]
-            items[i] = L.TransferItem(C.cast(bi, C.c_void_p), len(ins), C.cast(bo, C.c_void_p), len(outs),
-                                      C.cast(bp, C.c_void_p), len(proof))
-        st = np.zeros(n, dtype=np.int32)
-        fi = np.zeros(n, dtype=np.int32)
-        L.check("fts_transfer_verify_batch", L.lib.fts_transfer_verify_batch(
-            self._ctx, n, items, st.ctypes.data_as(C.POINTER(C.c_int32)), fi.ctypes.data_as(C.POINTER(C.c_int32))))
-        return st, fi
+        return self.prepare_transfers(transfers).verify()
+
+    def prepare_transfers(self, transfers):
+        """the fts_transfer_item array of a batch (host buffers the C-ABI borrows),
+        reusable across verify() calls"""
+        return TransferBatch(self, transfers)
 
     def verify_issues(self, issues):
         """issues: list of (tokens[list of 64B], proof bytes) -> (status, fail_index)."""
@@ -266,6 +273,71 @@ class StagedRangeBatch:
 
 
 # ------------------------------------------------ reference-shaped verifiers
+class TransferBatch:
+    """Host-side fts_transfer_item array (what the Go shim hands over per batch)."""
+
+    def __init__(self, pp, transfers):
+        self.pp = pp
+        self.n = len(transfers)
+        self.items = (L.TransferItem * self.n)()
+        self._keep = []
+        for i, (ins, outs, proof) in enumerate(transfers):
+            bi = C.create_string_buffer(b"".join(ins) or b"\0")
+            bo = C.create_string_buffer(b"".join(outs) or b"\0")
+            bp = C.create_string_buffer(proof or b"\0", max(1, len(proof)))
+            self._keep += [bi, bo, bp]
+            self.items[i] = L.TransferItem(C.cast(bi, C.c_void_p), len(ins), C.cast(bo, C.c_void_p), len(outs),
+                                           C.cast(bp, C.c_void_p), len(proof))
+
+    def verify(self):
+        st = np.zeros(self.n, dtype=np.int32)
+        fi = np.zeros(self.n, dtype=np.int32)
+        L.check("fts_transfer_verify_batch", L.lib.fts_transfer_verify_batch(
+            self.pp._ctx, self.n, self.items, st.ctypes.data_as(C.POINTER(C.c_int32)),
+            fi.ctypes.data_as(C.POINTER(C.c_int32))))
+        return st, fi
+
+
+class StagedMsm:
+    """MSM inputs validated and resident in HBM; ``run()`` is the device MSM only."""
+
+    def __init__(self, pp, points, scalars):
+        self.pp = pp
+        pts = points if isinstance(points, (bytes, bytearray)) else b"".join(points)
+        scs = scalars if isinstance(scalars, (bytes, bytearray)) else b"".join(scalars)
+        self.n = len(pts) // 64
+        self._b = C.c_void_p()
+        L.check("fts_msm_stage", L.lib.fts_msm_stage(pp._ctx, self.n, pts, scs, C.byref(self._b)))
+
+    def run(self):
+        out = C.create_string_buffer(64)
+        L.check("fts_msm_run", L.lib.fts_msm_run(self.pp._ctx, self._b, out))
+        return out.raw
+
+    def timings(self):
+        names = (C.c_char_p * 64)()
+        ms = (C.c_float * 64)()
+        mads = (C.c_double * 64)()
+        m = L.lib.fts_msm_timings(self._b, names, ms, mads, 64)
+        out = {}
+        for i in range(m):
+            k = names[i].decode()
+            o = out.get(k, (0.0, 0.0))
+            out[k] = (o[0] + ms[i], o[1] + mads[i])
+        return out
+
+    def close(self):
+        if self._b:
+            L.lib.fts_msm_free(self._b)
+            self._b = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class RangeVerifier:
     """rp.NewRangeVerifier(com, ...) / Verify (bulletproof.go:184-205,252-333).
     The generators come from ``pp`` exactly as RangeCorrectnessVerifier passes

@@ -147,6 +147,23 @@ int fts_debug_rp_intermediates(fts_ctx* ctx, size_t i, uint8_t* ch_out, uint8_t*
  * out[2] total buckets, out[3] non-empty buckets */
 int fts_debug_msm_stats(fts_ctx* ctx, int64_t* out);
 
+/* ---- standalone BN254 G1 multi-scalar multiplication (BASELINE config C3) ----
+ * out64 <- sum_i k_i P_i as 64-byte X||Y BE (identity: 64 zero bytes), the value
+ * gnark-crypto's G1 MultiExp / mathlib G1.Mul + Add return.
+ * points64: n x 64-byte X||Y BE, each checked like NewG1FromBytes (asn1.go:148): flag
+ * bits, canonical coordinates, on the curve; 64 zero bytes = identity.  A rejected
+ * point makes the call return FTS_API_EINVAL.
+ * scalars32: n x 32-byte BE integers, used mod r (G1.Mul semantics).
+ * Device Pippenger MSM (GLV split, signed windows, counting-sort buckets; msm.hip). */
+typedef struct fts_msm_batch fts_msm_batch;
+int fts_msm_g1(fts_ctx* ctx, size_t n, const uint8_t* points64, const uint8_t* scalars32, uint8_t* out64);
+/* device-resident variant: upload + validate once, run many times */
+int fts_msm_stage(fts_ctx* ctx, size_t n, const uint8_t* points64, const uint8_t* scalars32, fts_msm_batch** out);
+int fts_msm_run(fts_ctx* ctx, fts_msm_batch* b, uint8_t* out64);
+/* per-kernel device time (ms) and algorithmic u32 MADs of b's last run */
+int fts_msm_timings(const fts_msm_batch* b, const char** names, float* ms, double* mads, int cap);
+void fts_msm_free(fts_msm_batch* b);
+
 /* ---- error strings ---- */
 const char* fts_status_str(int32_t status);
 

@@ -695,3 +695,61 @@ int oracle_rp_verify_many(const uint8_t* gens, int n, int count, const uint8_t* 
   free(pp.R);
   return 0;
 }
+
+/* ------------------------------------------------ MSM baseline (config C3)
+ * int oracle_msm(const uint8_t* pts, const uint8_t* scs, size_t n, int threads, uint8_t* out64)
+ * sum_i (k_i mod r) P_i term by term with the reference's G1.Mul + Add (no
+ * Pippenger): the CPU baseline of the MSM microbenchmark, and an oracle for
+ * it.  pts: n x 64-byte BE points, scs: n x 32-byte BE scalars.
+ * Return 0, or -1 if a point fails NewG1FromBytes. */
+typedef struct {
+  const uint8_t *pts, *scs;
+  size_t n, next;
+  g1j acc;
+  int bad;
+  pthread_mutex_t mu;
+} msm_job;
+static void* msm_worker(void* arg) {
+  msm_job* j = (msm_job*)arg;
+  g1j acc = jid();
+  int bad = 0;
+  for (;;) {
+    pthread_mutex_lock(&j->mu);
+    size_t lo = j->next;
+    j->next += 64;
+    pthread_mutex_unlock(&j->mu);
+    if (lo >= j->n) break;
+    size_t hi = lo + 64 < j->n ? lo + 64 : j->n;
+    for (size_t i = lo; i < hi; i++) {
+      g1 p;
+      if (!g1_from_bytes(j->pts + 64 * i, 64, &p)) {
+        bad = 1;
+        continue;
+      }
+      acc = jadd(acc, tojac(g1_mul(p, be_to_fe(j->scs + 32 * i))));
+    }
+  }
+  pthread_mutex_lock(&j->mu);
+  j->acc = jadd(j->acc, acc);
+  j->bad |= bad;
+  pthread_mutex_unlock(&j->mu);
+  return NULL;
+}
+int oracle_msm(const uint8_t* pts, const uint8_t* scs, size_t n, int threads, uint8_t* out64) {
+  init_consts();
+  msm_job j;
+  j.pts = pts;
+  j.scs = scs;
+  j.n = n;
+  j.next = 0;
+  j.acc = jid();
+  j.bad = 0;
+  pthread_mutex_init(&j.mu, NULL);
+  if (threads < 1) threads = 1;
+  pthread_t* th = malloc(sizeof(pthread_t) * threads);
+  for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, msm_worker, &j);
+  for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+  free(th);
+  g1_bytes(toaff(j.acc), out64);
+  return j.bad ? -1 : 0;
+}

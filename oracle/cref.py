@@ -27,6 +27,8 @@ def lib():
         _lib.oracle_rp_verify_many.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_char_p, C.POINTER(C.c_char_p),
                                                C.POINTER(C.c_size_t), C.c_int, C.POINTER(C.c_int32)]
         _lib.oracle_rp_verify_many.restype = C.c_int
+        _lib.oracle_msm.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t, C.c_int, C.c_char_p]
+        _lib.oracle_msm.restype = C.c_int
     return _lib
 
 
@@ -48,3 +50,12 @@ def rp_verify_many(pp, coms, ders, threads=1):
     rc = lib().oracle_rp_verify_many(gens_blob(pp), pp.bit_length, n, b"".join(coms), arr, lens, threads, out)
     assert rc == 0
     return list(out)
+
+
+def msm(points64, scalars32, threads=1):
+    """sum (k_i mod r) P_i term by term (G1.Mul + Add) -> 64-byte BE result"""
+    n = len(points64) // 64
+    out = C.create_string_buffer(64)
+    rc = lib().oracle_msm(points64, scalars32, n, threads, out)
+    assert rc == 0
+    return out.raw

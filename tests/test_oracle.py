@@ -104,3 +104,20 @@ def test_oracle_issue_golden(case, oracle_pp):
     toks = [bn.g1_from_bytes(bytes.fromhex(h)) for h in case["tokens"]]
     err, idx = zkat.issue_verify(pp, toks, bytes.fromhex(case["proof"]))
     assert (err, idx) == (case["expect"], case["index"])
+
+
+def test_c_oracle_msm_matches_python_oracle():
+    """The C MSM baseline (bench.py --workload msm cpu_baseline) equals the
+    Python restatement of sum (k mod r) P (G1.Mul + Add), incl. identities."""
+    import random
+
+    from oracle import bn254 as bn, cref
+
+    rng = random.Random(0xC3C)
+    pts = [bn.g1_mul(bn.GEN, rng.randrange(1, bn.R)) for _ in range(12)] + [None]
+    sc = [rng.getrandbits(256) for _ in range(12)] + [5]
+    blob = b"".join(bn.g1_bytes(p) for p in pts)
+    sblob = b"".join(k.to_bytes(32, "big") for k in sc)
+    assert cref.msm(blob, sblob, threads=3) == bn.g1_bytes(bn.g1_msm(pts, sc))
+    P = pts[0]
+    assert cref.msm(bn.g1_bytes(P) * 2, (7).to_bytes(32, "big") + (bn.R - 7).to_bytes(32, "big")) == bytes(64)
