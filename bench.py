@@ -50,8 +50,8 @@ SURVEY_MAD_PER_RP64 = 8.13e6   # SURVEY §8(d) fixed cost model per rp64 verify
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=256)
+    ap.add_argument("--warmup", type=int, default=32)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--bits", type=int, default=64)
     ap.add_argument("--inflight", type=int, default=32,
@@ -90,6 +90,7 @@ def main():
     import random
     import numpy as np
     import fts_gpu
+    from fts_gpu import dist as fdist
 
     with open(os.path.join(ROOT, "tests", "golden", "zkatdlog_pp.json"), "rb") as f:
         pp_raw = f.read()
@@ -104,7 +105,7 @@ def main():
         if ln >= max(1, args.distinct):
             proofs, coms = sets[ln % len(sets)]
         else:
-            rng = random.Random(0xF7A50002 + 7919 * rank + 104729 * ln)
+            rng = random.Random(fdist.shard_seed(0xF7A50002, rank, ln))
             vals = [rng.getrandbits(n) for _ in range(B)]
             bfs = [rng.randrange(R_ORDER).to_bytes(32, "big") for _ in range(B)]
             proofs, coms = pp.prove_range_batch(vals, bfs, seed=0xF7A50002 + 1000003 * rank + 7777 * ln)
@@ -130,11 +131,8 @@ def main():
             t.join()
         res = [x for s in sinks for x in s]
         if dist is not None:
-            import torch
             for st, _ in res:
-                bits = torch.from_numpy(np.packbits(st == 0)).cuda()
-                out = torch.empty(world * bits.numel(), dtype=torch.uint8, device="cuda")
-                dist.all_gather_into_tensor(out, bits)
+                fdist.allgather_verdicts(dist, st)
         return res
 
     pipelined(max(args.warmup, inflight))
@@ -151,12 +149,8 @@ def main():
     ok = int(sum(int((st == 0).sum()) for st, _ in res))  # verdicts of the timed steps
     merged_avg = sum(m for _, m in res) / max(1, len(res))
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        okt = torch.tensor([ok], dtype=torch.int64, device="cuda")
-        dist.all_reduce(okt)
-        ok = int(okt.item())
+        elapsed = fdist.reduce_scalar(dist, elapsed, "max")
+        ok = int(fdist.reduce_scalar(dist, ok, "sum"))
 
     total = world * B * args.steps
     value = total / elapsed
@@ -186,10 +180,13 @@ def main():
         return {"kernel": kname, "kernel_ms": round(ms, 4), "mads_per_launch": mads,
                 "achieved": round(ach, 3) if ach else None, "frac": round(ach / PEAK_TMAD, 4) if ach else None}
 
+    # this pipeline's own cost model: algorithmic MADs of every kernel of one batch / B
+    own_mads = sum(v[1] for v in kt.values()) / B
     traffic = None
     try:
         with open(args.traffic_json) as f:
-            traffic = json.load(f).get(dom, {}).get("fetch_bytes_corrected")
+            tj = json.load(f)
+            traffic = tj.get(dom + "@isolated", tj.get(dom, {})).get("fetch_bytes_corrected")
     except (OSError, ValueError, AttributeError):
         pass
     rd = kernel_roof(dom)
@@ -197,7 +194,9 @@ def main():
                 "peak": round(PEAK_TMAD, 3), "unit": "TMAD/s", "frac": rd["frac"], "traffic": traffic,
                 "kernel_ms": rd["kernel_ms"], "mads_per_launch": rd["mads_per_launch"],
                 "measured": "HIP events, %d isolated steps of one %d-proof batch after the timed region" % (R, B),
-                "pipeline_frac_survey_model": round(value / world * SURVEY_MAD_PER_RP64 / (PEAK_TMAD * 1e12), 4)}
+                "pipeline_frac_survey_model": round(value / world * SURVEY_MAD_PER_RP64 / (PEAK_TMAD * 1e12), 4),
+                "pipeline_mads_per_rp64": round(own_mads),
+                "pipeline_frac_own_model": round(value / world * own_mads / (PEAK_TMAD * 1e12), 4)}
     longest_kernel = kernel_roof(longest)
 
     cpu = None
@@ -270,10 +269,8 @@ def _dist_setup():
 def _max_over_ranks(dist, x):
     if dist is None:
         return x
-    import torch
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    from fts_gpu import dist as fdist
+    return fdist.reduce_scalar(dist, x, "max")
 
 
 def _seq_points(m):
@@ -425,10 +422,8 @@ def bench_transfer(args):
             o = kt.get(name, (0.0, 0.0))
             kt[name] = (o[0] + ms, mads)
         if dist is not None:
-            import torch
-            bits = torch.from_numpy(np.packbits(st == 0)).cuda()
-            out = torch.empty(world * bits.numel(), dtype=torch.uint8, device="cuda")
-            dist.all_gather_into_tensor(out, bits)
+            from fts_gpu import dist as fdist
+            fdist.allgather_verdicts(dist, st)
     elapsed = _max_over_ranks(dist, time.perf_counter() - t0)
     value = world * args.transfers * args.steps / elapsed
     if rank == 0:
