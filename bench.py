@@ -47,16 +47,25 @@ MAD_PER_MUL = 136          # 8x32-bit no-carry CIOS / FIPS Montgomery product
 SURVEY_MAD_PER_RP64 = 8.13e6   # SURVEY §8(d) fixed cost model per rp64 verify
 
 
+def _cg_throttle():
+    """(nr_throttled, throttled_usec) of this process's cgroup (v2), if readable"""
+    try:
+        d = dict(l.split() for l in open("/sys/fs/cgroup/cpu.stat"))
+        return int(d["nr_throttled"]), int(d["throttled_usec"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=256)
-    ap.add_argument("--warmup", type=int, default=32)
+    ap.add_argument("--steps", type=int, default=512)
+    ap.add_argument("--warmup", type=int, default=64)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--bits", type=int, default=64)
-    ap.add_argument("--inflight", type=int, default=32,
+    ap.add_argument("--inflight", type=int, default=64,
                     help="batches in flight: host threads, each submitting its own staged batch")
-    ap.add_argument("--lanes", type=int, default=int(os.environ.get("FTS_LANES", "3")),
+    ap.add_argument("--lanes", type=int, default=int(os.environ.get("FTS_LANES", "5")),
                     help="device lanes (stream pairs) of the library (FTS_LANES); batches submitted while "
                          "all lanes are busy are coalesced into one device pass (FTS_COALESCE_MAX proofs)")
     ap.add_argument("--distinct", type=int, default=4,
@@ -95,6 +104,7 @@ def main():
     with open(os.path.join(ROOT, "tests", "golden", "zkatdlog_pp.json"), "rb") as f:
         pp_raw = f.read()
     pp = fts_gpu.PublicParams(pp_raw, bit_length=args.bits, device=local)
+    pp.reserve()  # every lane's workspace sized for the largest coalesced pass, before the clock
     n, k, B = pp.bit_length, pp.rounds, args.batch
     # one staged batch per in-flight slot; the first `distinct` hold distinct
     # proofs, the rest re-stage them (verification work does not depend on it)
@@ -140,12 +150,18 @@ def main():
         import torch
         dist.barrier()
         torch.cuda.synchronize()
+    cg0, cpu0 = _cg_throttle(), time.process_time()
     t0 = time.perf_counter()
     res = pipelined(args.steps)
     if dist is not None:
         torch.cuda.synchronize()
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    host = {"cpu_s": round(time.process_time() - cpu0, 3), "wall_s": round(elapsed, 3)}
+    cg1 = _cg_throttle()
+    if cg0 and cg1:
+        host["cgroup_throttled_periods"] = cg1[0] - cg0[0]
+        host["cgroup_throttled_ms"] = round((cg1[1] - cg0[1]) / 1e3, 1)
     ok = int(sum(int((st == 0).sum()) for st, _ in res))  # verdicts of the timed steps
     merged_avg = sum(m for _, m in res) / max(1, len(res))
     if dist is not None:
@@ -239,6 +255,7 @@ def main():
             "inflight": inflight,
             "device_lanes": args.lanes,
             "merged_batches_avg": round(merged_avg, 2),
+            "host": host,
             "isolated_batch": {"ms": round(iso_ms, 3), "verifies_per_s": round(B / iso_ms * 1e3, 1),
                                "note": "one %d-proof batch alone on the GPU (latency; no coalescing)" % B},
             "roofline": roofline,

@@ -68,12 +68,15 @@ namespace {
 struct DBuf {
   void* p = nullptr;
   size_t cap = 0;
+  // grows geometrically: hipFree synchronises the whole device, so a buffer
+  // must not be re-allocated on every slightly larger batch
   int ensure(size_t bytes) {
     if (bytes <= cap) return 0;
     if (p) hipFree(p);
     p = nullptr;
+    const size_t grown = cap + cap / 2;
     cap = 0;
-    size_t want = std::max<size_t>(bytes, 256);
+    size_t want = std::max<size_t>(std::max(bytes, grown), 256);
     if (hipMalloc(&p, want) != hipSuccess) return -1;
     cap = want;
     return 0;
@@ -117,6 +120,16 @@ struct Workspace {
 // overlap another batch's throughput-bound kernels.
 struct Lane {
   int id = 0;
+  // completion event created with hipEventBlockingSync: waiting on it sleeps
+  // instead of spinning (a spinning waiter per lane burns the process's CPU
+  // quota; on a CFS-throttled box that stalls every host thread for ~50 ms
+  // out of each 100 ms period)
+  hipEvent_t done = nullptr;
+  hipError_t sync() {
+    hipError_t e = hipEventRecord(done, s);
+    return e == hipSuccess ? hipEventSynchronize(done) : e;
+  }
+  bool presized = false;  // workspace sized for the context's largest coalesced pass
   hipStream_t s = nullptr, s2 = nullptr;
   Workspace ws;
   Timeline tl;
@@ -157,6 +170,8 @@ struct RpReq {
   int32_t* status;  // caller's host status array (may be null)
   int rc = 0;
   bool done = false;
+  std::condition_variable cv;  // this caller's wake-up (targeted, no thundering herd)
+  RpReq(fts_rp_batch* bb, int32_t* st) : b(bb), status(st) {}
 };
 
 struct fts_ctx {
@@ -183,6 +198,12 @@ struct fts_ctx {
   // concurrently are merged into one device pass of up to coalesce_max proofs
   std::deque<RpReq*> rp_pending;
   size_t coalesce_max = 32768;
+  // a lane was freed (call with mu held): the head pending range-proof request
+  // becomes the next leader; LaneGuard waiters re-check too
+  void wake_lane_waiters() {
+    if (!rp_pending.empty()) rp_pending.front()->cv.notify_one();
+    cv.notify_all();
+  }
   std::once_flag prover_once;
   ProverTables ptab;
 };
@@ -202,11 +223,9 @@ struct LaneGuard {
     c->free_lanes.erase(it);
   }
   ~LaneGuard() {
-    {
-      std::lock_guard<std::mutex> lk(c->mu);
-      c->free_lanes.push_back(L->id);
-    }
-    c->cv.notify_all();
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->free_lanes.push_back(L->id);
+    c->wake_lane_waiters();
   }
 };
 
@@ -287,6 +306,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
       if (L->s2 && L->s2 != L->s) hipStreamDestroy(L->s2);
       if (L->s) hipStreamDestroy(L->s);
       L->tl.destroy();
+      if (L->done) hipEventDestroy(L->done);
       L->free_pinned();
       delete L;
     }
@@ -295,7 +315,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
     return code;
   };
   if (hipSetDevice(device) != hipSuccess) return fail(FTS_API_EDEVICE);
-  int nl = 3;
+  int nl = 5;
   if (const char* e = getenv("FTS_LANES")) nl = std::max(1, std::min(16, atoi(e)));
   if (const char* e = getenv("FTS_COALESCE_MAX")) c->coalesce_max = (size_t)std::max(0L, atol(e));
   // FTS_SIDE_STREAM=0: run each lane's side work on its main stream
@@ -307,6 +327,8 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
     c->lanes.push_back(L);
     c->free_lanes.push_back(i);
     if (hipStreamCreateWithFlags(&L->s, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
+    if (hipEventCreateWithFlags(&L->done, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)
+      return fail(FTS_API_EDEVICE);
     if (hipHostMalloc((void**)&L->pin, sizeof(Lane::Pinned), 0) != hipSuccess) return fail(FTS_API_ENOMEM);
     if (!side) L->s2 = L->s;
     else if (hipStreamCreateWithFlags(&L->s2, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
@@ -392,6 +414,7 @@ void fts_ctx_destroy(fts_ctx* c) {
     if (L->s2 && L->s2 != L->s) hipStreamSynchronize(L->s2);
     L->ws.release();
     L->tl.destroy();
+    if (L->done) hipEventDestroy(L->done);
     if (L->s2 && L->s2 != L->s) hipStreamDestroy(L->s2);
     if (L->s) hipStreamDestroy(L->s);
     L->free_pinned();
@@ -546,6 +569,40 @@ static int msm_prepare(Lane& L, int N, MsmPlan& mp) {
   return FTS_API_OK;
 }
 
+// workspace of a range-proof pass of B proofs (grow-only).  The pass's INPUT
+// buffers (w.rp_* for gathered/action batches) belong to the caller, which
+// fills them before rp_pipeline runs: they are never re-allocated here.
+static int rp_buffers(fts_ctx* c, Lane& L, int B) {
+  const int n = c->n, k = c->k, npts = rp_npts(k), N = B * npts;
+  Workspace& w = L.ws;
+  if (w.pts.ensure((size_t)B * npts * 64) || w.ch.ensure((size_t)B * rp_nch(k) * 32) ||
+      w.small.ensure((size_t)B * (2 + k) * SMALL_SLOT) || w.hpj.ensure((size_t)B * (n + 1) * 96) ||
+      w.hpa.ensure((size_t)B * (n + 1) * 64) || w.hpbe.ensure((size_t)B * (n + 1) * 64) ||
+      w.x0.ensure((size_t)B * x0_slot_bytes(n)) || w.terms.ensure(rp_terms_words(B, n, k) * 4) ||
+      w.scratch.ensure(std::max(rp_scratch_words(B, n, k), (size_t)B * 10 * 24) * 4) || w.r_key.ensure(32) ||
+      w.r_msc.ensure((size_t)N * 32) || w.r_coef.ensure((size_t)B * 5 * 32) || w.r_colsum.ensure((3 + 2 * n) * 32) ||
+      w.r_fixed.ensure((3 + 2 * n) * 96) || w.r_flag.ensure(4) || w.ypow.ensure((size_t)B * n * 32) ||
+      w.svec.ensure((size_t)B * n * 32) || !L.status_buf((size_t)B))
+    return FTS_API_ENOMEM;
+  return FTS_API_OK;
+}
+
+// size lane L's workspace for range-proof passes of up to B proofs; with
+// inputs, also the pass-input buffers (w.rp_*) -- never from inside a pass,
+// whose caller has already filled them
+static int lane_reserve(fts_ctx* c, Lane& L, int B, bool inputs) {
+  const int npts = rp_npts(c->k);
+  MsmPlan big{};
+  if (int rc = msm_prepare(L, B * npts, big)) return rc;
+  if (int rc = rp_buffers(c, L, B)) return rc;
+  Workspace& w = L.ws;
+  if (inputs && (w.rp_raw.ensure((size_t)B * npts * 64) || w.rp_sc.ensure((size_t)B * RP_NSC * 32) ||
+                 w.rp_status.ensure((size_t)B * 4) || w.rp_ipa.ensure((size_t)B * 4)))
+    return FTS_API_ENOMEM;
+  L.presized = true;
+  return FTS_API_OK;
+}
+
 // Range-proof pipeline on B proofs already on the device: exact phase, RLC
 // batch check, and the per-proof fallback when the combination fails.
 // `between` (optional) is launched after the RLC check and before the flag
@@ -557,17 +614,13 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   Workspace& w = L.ws;
   const int N = B * npts;
   const double t_start = now_ms();
+  // first range-proof pass of this lane: size the workspace for the largest
+  // coalesced pass at once (no re-allocation, i.e. no device-wide sync, later)
+  if (!L.presized && c->coalesce_max > (size_t)B && c->coalesce_max <= (1u << 20))
+    if (int rc = lane_reserve(c, L, (int)c->coalesce_max, false)) return rc;
   MsmPlan mp{};
   if (int rc = msm_prepare(L, N, mp)) return rc;
-  if (w.pts.ensure((size_t)B * npts * 64) || w.ch.ensure((size_t)B * rp_nch(k) * 32) ||
-      w.small.ensure((size_t)B * (2 + k) * SMALL_SLOT) || w.hpj.ensure((size_t)B * (n + 1) * 96) ||
-      w.hpa.ensure((size_t)B * (n + 1) * 64) || w.hpbe.ensure((size_t)B * (n + 1) * 64) ||
-      w.x0.ensure((size_t)B * x0_slot_bytes(n)) || w.terms.ensure(rp_terms_words(B, n, k) * 4) ||
-      w.scratch.ensure(std::max(rp_scratch_words(B, n, k), (size_t)B * 10 * 24) * 4) || w.r_key.ensure(32) ||
-      w.r_msc.ensure((size_t)N * 32) || w.r_coef.ensure((size_t)B * 5 * 32) || w.r_colsum.ensure((3 + 2 * n) * 32) ||
-      w.r_fixed.ensure((3 + 2 * n) * 96) || w.r_flag.ensure(4) || w.ypow.ensure((size_t)B * n * 32) ||
-      w.svec.ensure((size_t)B * n * 32))
-    return FTS_API_ENOMEM;
+  if (int rc = rp_buffers(c, L, B)) return rc;
   RpBatchDev d{B,
                n,
                k,
@@ -598,7 +651,7 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(&L.pin->flag, r.flag, 4, hipMemcpyDeviceToHost, L.s));
   const double t_enq = now_ms();
-  HIP_OK(hipStreamSynchronize(L.s));
+  HIP_OK(L.sync());
   const double t_wait = now_ms();
   L.host_prep_ms = (float)(t_prep - t_start);
   L.host_enqueue_ms = (float)(t_enq - t_prep);
@@ -619,7 +672,7 @@ static int run_rp(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc, in
   int32_t* pst = host_status ? L.status_buf((size_t)B) : nullptr;
   if (host_status && !pst) return FTS_API_ENOMEM;
   if (host_status) HIP_OK(hipMemcpyAsync(pst, d_status, (size_t)B * 4, hipMemcpyDeviceToHost, L.s));
-  HIP_OK(hipStreamSynchronize(L.s));
+  HIP_OK(L.sync());
   if (host_status) memcpy(host_status, pst, (size_t)B * 4);
   collect_timings(c, L, batch);
   return FTS_API_OK;
@@ -639,8 +692,9 @@ static int run_rp_group(fts_ctx* c, Lane& L, const std::vector<RpReq*>& grp) {
   size_t B = 0;
   for (RpReq* q : grp) B += (size_t)q->b->B;
   Workspace& w = L.ws;
-  if (w.rp_raw.ensure(B * npts * 64) || w.rp_sc.ensure(B * RP_NSC * 32) || w.rp_status.ensure(B * 4) ||
-      w.rp_ipa.ensure(B * 4))
+  const size_t Bal = std::max(B, std::min(c->coalesce_max, (size_t)1 << 20));  // sized once for the largest pass
+  if (w.rp_raw.ensure(Bal * npts * 64) || w.rp_sc.ensure(Bal * RP_NSC * 32) || w.rp_status.ensure(Bal * 4) ||
+      w.rp_ipa.ensure(Bal * 4))
     return FTS_API_ENOMEM;
   RpGather g{};
   g.G = (int)grp.size();
@@ -663,7 +717,7 @@ static int run_rp_group(fts_ctx* c, Lane& L, const std::vector<RpReq*>& grp) {
   int32_t* pst = L.status_buf(B);
   if (!pst) return FTS_API_ENOMEM;
   HIP_OK(hipMemcpyAsync(pst, w.rp_status.as<int32_t>(), B * 4, hipMemcpyDeviceToHost, L.s));
-  HIP_OK(hipStreamSynchronize(L.s));
+  HIP_OK(L.sync());
   off = 0;
   for (RpReq* q : grp) {
     if (q->status) memcpy(q->status, pst + off, (size_t)q->b->B * 4);
@@ -768,13 +822,12 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
   // coalesce_max proofs) and runs it as ONE device pass, so batches submitted
   // while the lanes are busy are merged (a 4,096-proof batch alone fills only
   // 64 waves in the per-proof chain kernels).  Verdicts stay per proof.
-  RpReq me{b, status};
+  RpReq me(b, status);
   std::unique_lock<std::mutex> lk(c->mu);
   c->rp_pending.push_back(&me);
-  c->cv.notify_all();
   while (!me.done) {
     if (c->free_lanes.empty() || c->rp_pending.empty()) {
-      c->cv.wait(lk);
+      me.cv.wait(lk);
       continue;
     }
     Lane* L = c->lanes[c->free_lanes.back()];
@@ -794,9 +847,10 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
     for (RpReq* q : grp) {
       q->rc = rc;
       q->done = true;
+      if (q != &me) q->cv.notify_one();
     }
     c->free_lanes.push_back(L->id);
-    c->cv.notify_all();
+    c->wake_lane_waiters();
   }
   return me.rc;
 }
@@ -813,6 +867,20 @@ int fts_rp_batch_timings(const fts_rp_batch* b, const char** names, float* ms, d
 }
 
 int fts_rp_batch_merged(const fts_rp_batch* b) { return b ? b->merged : 0; }
+
+int fts_ctx_reserve(fts_ctx* c, size_t max_pass_proofs) {
+  if (!c) return FTS_API_EINVAL;
+  if (c->device < 0) return FTS_API_EDEVICE;
+  const size_t B = max_pass_proofs ? max_pass_proofs : c->coalesce_max;
+  if (B == 0 || B > (1u << 20)) return FTS_API_ESIZE;
+  HIP_OK(hipSetDevice(c->device));
+  for (size_t i = 0; i < c->lanes.size(); i++) {
+    LaneGuard lg(c, (int)i);
+    if (int rc = lane_reserve(c, *lg.L, (int)B, true)) return rc;
+    HIP_OK(lg.L->sync());
+  }
+  return FTS_API_OK;
+}
 
 // ------------------------------------------------- standalone G1 MSM (C3)
 }  // extern "C"
@@ -890,7 +958,7 @@ int fts_msm_run(fts_ctx* c, fts_msm_batch* b, uint8_t* out64) {
   launch_msm_to_bytes(mp.out, b->out, L.s);
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(out64, b->out, 64, hipMemcpyDeviceToHost, L.s));
-  HIP_OK(hipStreamSynchronize(L.s));
+  HIP_OK(L.sync());
   b->ntim = 0;
   for (int i = 0; i < L.tl.n && b->ntim < Timeline::CAP; i++) {
     if (!L.tl.name[i]) continue;
@@ -1239,7 +1307,7 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
   std::vector<int32_t> sig_res(SA), rp_res(rp_total);
   if (SA) HIP_OK(hipMemcpyAsync(sig_res.data(), w.s_status.p, SA * 4, hipMemcpyDeviceToHost, L.s));
   if (rp_total) HIP_OK(hipMemcpyAsync(rp_res.data(), w.rp_status.p, rp_total * 4, hipMemcpyDeviceToHost, L.s));
-  HIP_OK(hipStreamSynchronize(L.s));
+  HIP_OK(L.sync());
   if (rp_total) collect_timings(c, L, nullptr);
   // ---- combine with the reference's precedence
   for (size_t i = 0; i < A; i++) {

@@ -108,6 +108,11 @@ class PublicParams:
         except Exception:
             pass
 
+    def reserve(self, max_pass_proofs=0):
+        """pre-allocate every device lane for passes of up to max_pass_proofs
+        (0: the coalescing cap) -- no allocation once batches flow"""
+        L.check("fts_ctx_reserve", L.lib.fts_ctx_reserve(self._ctx, max_pass_proofs))
+
     # ------------------------------------------------------------ verify
     def verify_range_proofs(self, proofs, commitments):
         """Batch of standalone range proofs -> np.int32 verdicts."""

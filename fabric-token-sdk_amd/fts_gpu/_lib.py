@@ -30,7 +30,7 @@ FTS_DEVICE_NONE = -2
 EXPORTED = [
     "fts_ctx_create", "fts_ctx_create_bits", "fts_ctx_destroy", "fts_ctx_info",
     "fts_rp_verify_batch", "fts_transfer_verify_batch", "fts_issue_verify_batch",
-    "fts_rp_batch_stage", "fts_rp_batch_verify", "fts_rp_batch_free", "fts_rp_batch_merged", "fts_last_timings", "fts_last_timings_ex", "fts_rp_batch_timings",
+    "fts_rp_batch_stage", "fts_rp_batch_verify", "fts_rp_batch_free", "fts_rp_batch_merged", "fts_ctx_reserve", "fts_last_timings", "fts_last_timings_ex", "fts_rp_batch_timings",
     "fts_status_str", "fts_rp_prove", "fts_rp_prove_batch", "fts_token_commit",
     "fts_transfer_prove", "fts_issue_prove", "fts_debug_rp_intermediates",
     "fts_debug_msm_stats", "fts_msm_g1", "fts_msm_stage", "fts_msm_run", "fts_msm_timings", "fts_msm_free",
@@ -68,6 +68,7 @@ def _load():
         "fts_rp_batch_verify": ([P, P, I32P], C.c_int),
         "fts_rp_batch_free": ([P], None),
         "fts_rp_batch_merged": ([P], C.c_int),
+        "fts_ctx_reserve": ([P, S], C.c_int),
         "fts_last_timings": ([P, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int], C.c_int),
         "fts_last_timings_ex": ([P, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.POINTER(C.c_double), C.c_int],
                                 C.c_int),

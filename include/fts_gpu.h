@@ -122,11 +122,15 @@ int fts_rp_batch_stage(fts_ctx* ctx, size_t n, const uint8_t* const* rp_der, con
                        const uint8_t* com64, fts_rp_batch** out);
 /* runs the whole GPU verification of a staged batch; status may be NULL.
  * Thread-safe: concurrent calls on DIFFERENT batches run on different lanes
- * (stream pairs, FTS_LANES env, default 3) and overlap on the device; batches
+ * (stream pairs, FTS_LANES env, default 5) and overlap on the device; batches
  * submitted while every lane is busy are coalesced into one device pass of
  * up to FTS_COALESCE_MAX proofs (default 32768).  Verdicts are per proof and
  * independent of the grouping. */
 int fts_rp_batch_verify(fts_ctx* ctx, fts_rp_batch* b, int32_t* status);
+/* pre-allocate every lane's workspace for device passes of up to max_pass_proofs
+ * range proofs (0: FTS_COALESCE_MAX) so that no allocation -- and no device-wide
+ * synchronisation -- happens once batches flow; call once after fts_ctx_create */
+int fts_ctx_reserve(fts_ctx* ctx, size_t max_pass_proofs);
 /* number of staged batches (including b) in the device pass that verified b last */
 int fts_rp_batch_merged(const fts_rp_batch* b);
 /* per-kernel device time (ms) and algorithmic u32 MADs of b's last verification */
