@@ -26,6 +26,21 @@ constexpr size_t FB_WORDS_PER_BASE = (size_t)FB_NW * FB_E * 16;
 constexpr int FB_S = 1 << ((FB_W) / 2);                    // small multiples per window
 constexpr int FB_L = FB_E / FB_S;                          // large multiples per window
 
+// The same layout for any window width W.  The per-proof bases of the
+// range-proof pipeline (H_i, K, P: the n + 2 fixed-base products of every
+// proof) use FBW_W = 20-bit windows: 13 mixed additions per product instead
+// of 16, for 436 MiB per base (28.8 GiB at n = 64 -- the 288 GB part holds it).
+template <int W>
+struct FbCfg {
+  static constexpr int NW = (255 + W - 1) / W;
+  static constexpr int E = 1 << (W - 1);
+  static constexpr size_t WORDS_PER_BASE = (size_t)NW * E * 16;
+  static constexpr int S = 1 << (W / 2);
+  static constexpr int L = E / S;
+};
+constexpr int FBW_W = 20;
+using FbWide = FbCfg<FBW_W>;
+
 // next signed digit of k (LSB first): consumes FB_W bits of s (shifted in
 // place: constant register indices, no scratch), carry in/out via `carry`
 FTS_DEV int fb_next_digit(uint32_t s[8], int& carry) {
@@ -97,6 +112,54 @@ FTS_DEV G1J fb_mul(const uint32_t* __restrict__ table, const Scalar& k) {
     if (wn < FB_NW) nxt = fb_entry(table, wn, dn);  // in flight during the addition
     madd_inl(acc, cur);
     if (wn >= FB_NW) break;
+    cur = nxt;
+    w = wn;
+  }
+  return acc;
+}
+
+// k * B over a width-W table (FbCfg<W> layout)
+template <int W>
+FTS_DEV int fb_next_digit_w(uint32_t s[8], int& carry) {
+  constexpr int E = FbCfg<W>::E;
+  int d = (int)(s[0] & (uint32_t)(2 * E - 1)) + carry;
+#pragma unroll
+  for (int i = 0; i < 7; i++) s[i] = (s[i] >> W) | (s[i + 1] << (32 - W));
+  s[7] >>= W;
+  carry = d > E;
+  return carry ? d - 2 * E : d;
+}
+template <int W>
+FTS_DEV G1A fb_entry_w(const uint32_t* __restrict__ table, int w, int d) {
+  const int ad = d < 0 ? -d : d;
+  G1A q = load_g1a(table + ((size_t)w * FbCfg<W>::E + (ad - 1)) * 16);
+  if (d < 0) q.y = f_neg(q.y);
+  return q;
+}
+template <int W>
+FTS_DEV G1J fb_mul_w(const uint32_t* __restrict__ table, const Scalar& k) {
+  constexpr int NW = FbCfg<W>::NW;
+  uint32_t s[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = k.v[i];
+  G1J acc = g1j_identity();
+  int carry = 0, w = 0, d = 0;
+  for (; w < NW; w++) {
+    d = fb_next_digit_w<W>(s, carry);
+    if (d != 0) break;
+  }
+  if (w == NW) return acc;
+  G1A cur = fb_entry_w<W>(table, w, d);
+  for (;;) {
+    int wn = w + 1, dn = 0;
+    for (; wn < NW; wn++) {
+      dn = fb_next_digit_w<W>(s, carry);
+      if (dn != 0) break;
+    }
+    G1A nxt;
+    if (wn < NW) nxt = fb_entry_w<W>(table, wn, dn);  // in flight during the addition
+    madd_inl(acc, cur);
+    if (wn >= NW) break;
     cur = nxt;
     w = wn;
   }

@@ -35,8 +35,11 @@ namespace fts {
 size_t rp_scratch_words(int B, int n, int k);
 size_t rp_terms_words(int B, int n, int k);
 void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s);
-void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const uint8_t* x0_const,
-                     hipStream_t s, hipStream_t s2, Timeline* tl);
+void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const uint32_t* wtables,
+                     const uint8_t* x0_const, hipStream_t s, hipStream_t s2, Timeline* tl);
+void launch_build_wide_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s);
+size_t wide_build_scratch_bytes(int nb);
+size_t fbw_words_per_base();
 void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, hipStream_t s, Timeline* tl);
 void launch_rp_gather(const RpGather& g, int k, uint8_t* raw, uint32_t* sc, int32_t* status, int32_t* ipa, hipStream_t s);
 void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
@@ -179,6 +182,7 @@ struct fts_ctx {
   PublicParams pp;
   int n = 0, k = 0;
   uint32_t* d_tables = nullptr;
+  uint32_t* d_wtables = nullptr;  // 20-bit tables of [H_0 .. H_{n-1}, K, P] (k_rp_fixed_exact)
   uint8_t* d_x0const = nullptr;
   size_t table_bytes = 0;
   // lane pool
@@ -311,6 +315,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
       delete L;
     }
     if (c->d_tables) hipFree(c->d_tables);
+    if (c->d_wtables) hipFree(c->d_wtables);
     delete c;
     return code;
   };
@@ -372,6 +377,37 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   for (int b0 = 0; b0 < nb; b0 += chunk)
     launch_build_tables(d_bases + (size_t)b0 * 16, std::min(chunk, nb - b0), c->d_tables + (size_t)b0 * fb_words_per_base(),
                         d_scr, s0);
+  // 20-bit tables of the per-proof bases H_i, K, P (same build, wider windows)
+  {
+    const int nw = n + 2;
+    std::vector<uint32_t> hw((size_t)nw * 16, 0);
+    for (int i = 0; i < nw; i++) {
+      const int src = i < n ? n + i : (i == n ? 2 * n + 4 : 2 * n + 2);  // H_i, K, P in `bases`
+      memcpy(&hw[(size_t)i * 16], &hb[(size_t)src * 16], 64);
+    }
+    uint32_t* d_wb = nullptr;
+    uint32_t* d_wscr = nullptr;
+    const int wchunk = std::min(nw, 4);
+    if (hipMalloc(&c->d_wtables, (size_t)nw * fbw_words_per_base() * 4) != hipSuccess ||
+        hipMalloc(&d_wb, hw.size() * 4) != hipSuccess || hipMalloc(&d_wscr, wide_build_scratch_bytes(wchunk)) != hipSuccess) {
+      if (d_wb) hipFree(d_wb);
+      hipFree(d_bases);
+      hipFree(d_scr);
+      return fail(FTS_API_ENOMEM);
+    }
+    hipMemcpyAsync(d_wb, hw.data(), hw.size() * 4, hipMemcpyHostToDevice, s0);
+    for (int b0 = 0; b0 < nw; b0 += wchunk)
+      launch_build_wide_tables(d_wb + (size_t)b0 * 16, std::min(wchunk, nw - b0),
+                               c->d_wtables + (size_t)b0 * fbw_words_per_base(), d_wscr, s0);
+    hipError_t we = hipStreamSynchronize(s0);
+    hipFree(d_wb);
+    hipFree(d_wscr);
+    if (we != hipSuccess) {
+      hipFree(d_bases);
+      hipFree(d_scr);
+      return fail(FTS_API_EDEVICE);
+    }
+  }
   // constant part of the x0 transcript: hex(G_i) "||" ... hex(Q) "||"
   std::string xc;
   for (int i = 0; i <= n; i++) {
@@ -421,6 +457,7 @@ void fts_ctx_destroy(fts_ctx* c) {
     delete L;
   }
   if (c->d_tables) hipFree(c->d_tables);
+  if (c->d_wtables) hipFree(c->d_wtables);
   if (c->d_x0const) hipFree(c->d_x0const);
   delete c;
 }
@@ -646,7 +683,7 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   HIP_OK(hipMemcpyAsync(r.key, L.pin->key, sizeof L.pin->key, hipMemcpyHostToDevice, L.s));
   const double t_prep = now_ms();
   L.tl.begin(L.s);
-  launch_rp_batch(d, r, c->d_tables, c->d_x0const, L.s, L.s2, &L.tl);
+  launch_rp_batch(d, r, c->d_tables, c->d_wtables, c->d_x0const, L.s, L.s2, &L.tl);
   between();
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(&L.pin->flag, r.flag, 4, hipMemcpyDeviceToHost, L.s));

@@ -40,51 +40,58 @@ __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, in
 
 // ---------------------------------------------------------- context tables
 // Built once per context (device/fixed_base.hpp layout), for nb bases:
-//   kt_window_bases  lane per (base, window)   B_w = 2^(FB_W w) B            (Jacobian)
-//   kt_small_large   lane per (base, window)   small[lo] = (lo+1) B_w, large[hi] = hi FB_S B_w
-//   kt_entries       lane per entry            T[w][d-1] = large[hi] + small[lo], d-1 = hi FB_S + lo
+//   kt_window_bases  lane per (base, window)   B_w = 2^(W w) B            (Jacobian)
+//   kt_small_large   lane per (base, window)   small[lo] = (lo+1) B_w, large[hi] = hi S B_w
+//   kt_entries       lane per entry            T[w][d-1] = large[hi] + small[lo], d-1 = hi S + lo
+// for window width W (FbCfg<W>: 16-bit for every base, 20-bit for H_i, K, P)
 //   k_rp_normalize   block per 256 entries     affine (one inversion per block)
+template <int W>
 __global__ void __launch_bounds__(64) kt_window_bases(const uint32_t* __restrict__ bases, int nb,
                                                       uint32_t* __restrict__ bw) {
+  using C = FbCfg<W>;
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= nb * FB_NW) return;
-  int b = gid / FB_NW, w = gid % FB_NW;
+  if (gid >= nb * C::NW) return;
+  int b = gid / C::NW, w = gid % C::NW;
   G1J p = g1j_from_affine(load_g1a(bases + b * 16));
-  for (int i = 0; i < FB_W * w; i++) p = nl_dbl(p);
+  for (int i = 0; i < W * w; i++) p = nl_dbl(p);
   store_g1j(bw + (size_t)gid * 24, p);
 }
 
+template <int W>
 __global__ void __launch_bounds__(64) kt_small_large(int nb, const uint32_t* __restrict__ bw,
                                                      uint32_t* __restrict__ small, uint32_t* __restrict__ large) {
+  using C = FbCfg<W>;
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= nb * FB_NW) return;
+  if (gid >= nb * C::NW) return;
   const uint32_t* Bw = bw + (size_t)gid * 24;
-  uint32_t* S = small + (size_t)gid * FB_S * 24;
-  uint32_t* L = large + (size_t)gid * FB_L * 24;
+  uint32_t* S = small + (size_t)gid * C::S * 24;
+  uint32_t* L = large + (size_t)gid * C::L * 24;
   G1J acc = load_g1j(Bw);
   store_g1j(S, acc);
-  for (int lo = 1; lo < FB_S; lo++) {
+  for (int lo = 1; lo < C::S; lo++) {
     acc = nl_add_mem(acc, Bw, 0);
     store_g1j(S + lo * 24, acc);
   }
-  // acc = FB_S * B_w
+  // acc = S * B_w
   store_g1j(L, g1j_identity());
   G1J big = g1j_identity();
-  for (int hi = 1; hi < FB_L; hi++) {
-    big = nl_add_mem(big, S + (FB_S - 1) * 24, 0);
+  for (int hi = 1; hi < C::L; hi++) {
+    big = nl_add_mem(big, S + (C::S - 1) * 24, 0);
     store_g1j(L + hi * 24, big);
   }
 }
 
+template <int W>
 __global__ void __launch_bounds__(64) kt_entries(int nb, const uint32_t* __restrict__ small,
                                                  const uint32_t* __restrict__ large, uint32_t* __restrict__ jac) {
+  using C = FbCfg<W>;
   size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (size_t)nb * FB_NW * FB_E) return;
-  const size_t bw = gid / FB_E;
-  const int e = (int)(gid % FB_E);  // d - 1
-  const int hi = e / FB_S, lo = e % FB_S;
-  G1J p = load_g1j(small + (bw * FB_S + lo) * 24);
-  if (hi) p = nl_add_mem(p, large + (bw * FB_L + hi) * 24, 0);
+  if (gid >= (size_t)nb * C::NW * C::E) return;
+  const size_t bw = gid / C::E;
+  const int e = (int)(gid % C::E);  // d - 1
+  const int hi = e / C::S, lo = e % C::S;
+  G1J p = load_g1j(small + (bw * C::S + lo) * 24);
+  if (hi) p = nl_add_mem(p, large + (bw * C::L + hi) * 24, 0);
   store_g1j(jac + gid * 24, p);
 }
 
@@ -306,10 +313,11 @@ inline __host__ __device__ int com_nterms(int n) { return COM_NTERMS; }
 
 // lane per (proof, item): items 0..n-1: H'_i = y^-i H_i (-> hpj[b][i]);
 // n: z K; n+1: -delta P (-> terms[b][0..1])
+// wtables: the 20-bit tables of [H_0 .. H_{n-1}, K, P] (FbWide layout)
 __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, const int32_t* __restrict__ status,
                                                           const uint32_t* __restrict__ sc, const uint32_t* __restrict__ ch,
                                                           const uint32_t* __restrict__ ypow,
-                                                          const uint32_t* __restrict__ tables, uint32_t* __restrict__ hpj,
+                                                          const uint32_t* __restrict__ wtables, uint32_t* __restrict__ hpj,
                                                           uint32_t* __restrict__ terms) {
   const int ni = n + 2;
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -323,13 +331,13 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, c
   if (t < n) {
     Fr yp;
     load_f(ypow + ((size_t)t * B + b) * 8, yp);
-    tab = tables + (size_t)(n + t) * FB_WORDS_PER_BASE;
+    tab = wtables + (size_t)t * FbWide::WORDS_PER_BASE;
     sk = fr_canon(yp);
     out = hpj + ((size_t)b * (n + 1) + t) * 24;
   } else if (t == n) {
     Fr z;
     load_f(C + CH_Z * 8, z);
-    tab = tables + (size_t)tb_K(n) * FB_WORDS_PER_BASE;
+    tab = wtables + (size_t)n * FbWide::WORDS_PER_BASE;
     sk = fr_canon(z);
     out = terms + ((size_t)b * COM_NTERMS + 0) * 24;
   } else {
@@ -338,10 +346,10 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, c
     Fr nd = f_neg(d);
 #pragma unroll
     for (int q = 0; q < 8; q++) sk.v[q] = nd.v[q];
-    tab = tables + (size_t)tb_P(n) * FB_WORDS_PER_BASE;
+    tab = wtables + (size_t)(n + 1) * FbWide::WORDS_PER_BASE;
     out = terms + ((size_t)b * COM_NTERMS + 1) * 24;
   }
-  G1J r = fb_mul(tab, sk);
+  G1J r = fb_mul_w<FBW_W>(tab, sk);
   store_g1j(out, r);
 }
 
@@ -886,23 +894,36 @@ size_t rp_scratch_words(int B, int n, int k) {
 size_t rp_terms_words(int B, int n, int k) { return (size_t)B * rp_nterms(n, k) * 24; }
 
 size_t fb_words_per_base() { return FB_WORDS_PER_BASE; }
-size_t table_build_scratch_bytes(int nb) {
-  const size_t nbw = (size_t)nb * FB_NW;
-  return nbw * 24 * 4 + nbw * (FB_S + FB_L) * 24 * 4 + nbw * FB_E * 24 * 4;
+size_t fbw_words_per_base() { return FbWide::WORDS_PER_BASE; }
+template <int W>
+static size_t build_scratch_bytes(int nb) {
+  using C = FbCfg<W>;
+  const size_t nbw = (size_t)nb * C::NW;
+  return nbw * 24 * 4 + nbw * (C::S + C::L) * 24 * 4 + nbw * C::E * 24 * 4;
 }
-// tables: nb * FB_WORDS_PER_BASE words; scratch: table_build_scratch_bytes(nb)
-void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s) {
-  const size_t nbw = (size_t)nb * FB_NW;
+size_t table_build_scratch_bytes(int nb) { return build_scratch_bytes<FB_W>(nb); }
+size_t wide_build_scratch_bytes(int nb) { return build_scratch_bytes<FBW_W>(nb); }
+// tables: nb * WORDS_PER_BASE words; scratch: build_scratch_bytes<W>(nb)
+template <int W>
+static void build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s) {
+  using C = FbCfg<W>;
+  const size_t nbw = (size_t)nb * C::NW;
   uint32_t* bw = scratch;
   uint32_t* small = bw + nbw * 24;
-  uint32_t* large = small + nbw * FB_S * 24;
-  uint32_t* jac = large + nbw * FB_L * 24;
-  FTS_LAUNCH(kt_window_bases, nbw, 64, s, bases, nb, bw);
-  FTS_LAUNCH(kt_small_large, nbw, 64, s, nb, bw, small, large);
-  FTS_LAUNCH(kt_entries, nbw * FB_E, 64, s, nb, small, large, jac);
-  const size_t tot = nbw * FB_E;
+  uint32_t* large = small + nbw * C::S * 24;
+  uint32_t* jac = large + nbw * C::L * 24;
+  FTS_LAUNCH(kt_window_bases<W>, nbw, 64, s, bases, nb, bw);
+  FTS_LAUNCH(kt_small_large<W>, nbw, 64, s, nb, bw, small, large);
+  FTS_LAUNCH(kt_entries<W>, nbw * C::E, 64, s, nb, small, large, jac);
+  const size_t tot = nbw * C::E;
   FTS_LAUNCH(k_rp_normalize, (tot + NORM_E - 1) / NORM_E, NORM_BS, s, (int)tot, 1, 1, 0, (const int32_t*)nullptr, jac,
              tables, (uint8_t*)nullptr);
+}
+void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s) {
+  build_tables<FB_W>(bases, nb, tables, scratch, s);
+}
+void launch_build_wide_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s) {
+  build_tables<FBW_W>(bases, nb, tables, scratch, s);
 }
 
 void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
@@ -912,8 +933,8 @@ void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalar
 // phase (everything that is hashed: challenges, H'_i, com, x0) and the
 // random-linear-combination check of all final equations (one MSM).
 // s = main stream, s2 = side stream.
-void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const uint8_t* x0_const,
-                     hipStream_t s, hipStream_t s2, Timeline* tl) {
+void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const uint32_t* wtables,
+                     const uint8_t* x0_const, hipStream_t s, hipStream_t s2, Timeline* tl) {
   const int B = d.B, n = d.n, k = d.k;
   if (!B) return;
   FTS_LAUNCH(k_rp_decode, B * rp_npts(k), 256, s, B, rp_npts(k), d.raw, d.pts, d.status);
@@ -924,8 +945,8 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   tl->mark("k_rp_chal_fr", s, (double)B * (3 * k + 4 * (k + 1) + 12));
   FTS_LAUNCH(k_rp_powers, B * (n >> std::min(PW_LC, k)), 64, s, B, n, k, d.status, d.ch, d.ypow, d.svec);
   tl->mark("k_rp_powers", s, (double)B * (2.0 * n + 2.0 * k));
-  FTS_LAUNCH(k_rp_fixed_exact, B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, tables, d.hpj, d.terms);
-  tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FB);
+  FTS_LAUNCH(k_rp_fixed_exact, B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, wtables, d.hpj, d.terms);
+  tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FBW);
   const int nch = (n + HS_CHUNK - 1) / HS_CHUNK;
   FTS_LAUNCH(k_rp_hsum_chunks, B * nch, 64, s, B, n, d.status, d.hpj, d.scratch);
   tl->mark("k_rp_hsum_chunks", s, (double)B * (n - nch) * (COST_DBL + COST_ADD));
