@@ -10,7 +10,8 @@
 //   S   k_rp_chal_fr       proof            z, polEval, batch inversion of y, x_j       bulletproof.go:282-311, ipa.go:236-244
 //   S   k_rp_fixed_exact   (proof, item)    H'_i = y^-i H_i, z K, -delta P (fixed base) bulletproof.go:483-489
 //   S   k_rp_hsum_chunks   (proof, chunk)   S_c = sum_j 2^j H'_{8c+j} (Horner)
-//   S   k_rp_com_var       2 lanes/proof    x*D + z^2*S (joint GLV/Straus), S = sum_c 2^(8c) S_c
+//   S   k_rp_hsum_join     proof            S = sum_c 2^(8c) S_c (Horner)
+//   S   k_rp_com_var       2 lanes/proof    x*D + z^2*S (joint GLV/Straus)
 //   S   k_rp_com_sum       proof            com = C + z K - delta P + x D + z^2 S       bulletproof.go:477-492
 //   S   k_rp_normalize     point (block)    batch affine normalisation of H'_i and com (one inversion per 256 points)
 //   S2  k_rp_x0_build      (proof, record)  DER(hex(H'..., G..., Q, com) "||" Zb(ip))   ipa.go:200-212
@@ -353,22 +354,39 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, c
   store_g1j(out, r);
 }
 
-// lane per (proof, chunk c): S_c = sum_{j < 8} 2^j H'_{8c+j} (Horner, Jacobian H')
+// lane per (proof, chunk c): S_c = sum_{j < 8} 2^j H'_{8c+j} (Horner over the affine H')
 __global__ void __launch_bounds__(64) k_rp_hsum_chunks(int B, int n, const int32_t* __restrict__ status,
-                                                       const uint32_t* __restrict__ hpj, uint32_t* __restrict__ chunks) {
+                                                       const uint32_t* __restrict__ hpa, uint32_t* __restrict__ chunks) {
   const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * nc) return;
   const int b = gid / nc, c = gid % nc;
   if (status[b] != 0) return;
   const int lo = c * HS_CHUNK, hi = min(n, lo + HS_CHUNK);
-  const uint32_t* H = hpj + (size_t)b * (n + 1) * 24;
-  G1J acc = load_g1j(H + (hi - 1) * 24);
+  const uint32_t* H = hpa + (size_t)b * (n + 1) * 16;  // affine H' (mixed additions)
+  G1J acc = g1j_from_affine(load_g1a(H + (hi - 1) * 16));
   for (int i = hi - 2; i >= lo; i--) {
     acc = g1j_dbl(acc);
-    add_inl(acc, load_g1j(H + i * 24));
+    const G1A q = load_g1a(H + i * 16);
+    if (!g1a_is_identity(q)) madd_inl(acc, q);
   }
   store_g1j(chunks + (size_t)gid * 24, acc);
+}
+
+// lane per proof: S = sum_c 2^(8c) S_c (Horner over the chunk sums), written
+// over chunk 0 -- once per proof instead of in both GLV lanes of k_rp_com_var
+__global__ void __launch_bounds__(64) k_rp_hsum_join(int B, int n, const int32_t* __restrict__ status,
+                                                     uint32_t* __restrict__ chunks) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B || status[b] != 0) return;
+  const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
+  uint32_t* Sc = chunks + (size_t)b * nc * 24;
+  G1J S = load_g1j(Sc + (nc - 1) * 24);
+  for (int c = nc - 2; c >= 0; c--) {
+    for (int q = 0; q < HS_CHUNK; q++) S = g1j_dbl(S);
+    add_inl(S, load_g1j(Sc + c * 24));
+  }
+  store_g1j(Sc, S);
 }
 
 // x*D + z^2*S (bulletproof.go:478, 486-489 via S), two lanes per proof:
@@ -387,12 +405,7 @@ __global__ void __launch_bounds__(64) k_rp_com_var(int B, int n, int k, const in
   load_f(C + CH_X * 8, x);
   load_f(C + CH_Z2 * 8, z2);
   const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
-  const uint32_t* Sc = chunks + (size_t)b * nc * 24;
-  G1J S = load_g1j(Sc + (nc - 1) * 24);
-  for (int c = nc - 2; c >= 0; c--) {
-    for (int q = 0; q < HS_CHUNK; q++) S = g1j_dbl(S);
-    add_inl(S, load_g1j(Sc + c * 24));
-  }
+  G1J S = load_g1j(chunks + (size_t)b * nc * 24);  // assembled by k_rp_hsum_join
   G1J D = g1j_from_affine(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_D) * 16));
   uint32_t xk[2][4], xs[2], wk[2][4], ws[2];
   glv_decompose(fr_canon(x).v, xk[0], xs[0], xk[1], xs[1]);
@@ -421,7 +434,8 @@ __global__ void __launch_bounds__(64) k_rp_com_sum(int B, int n, int k, const in
 }
 
 // Batch affine normalisation (Montgomery's trick), NORM_E points per lane and
-// NORM_BS * NORM_E points per block (point g lives at index g * stride + first;
+// NORM_BS * NORM_E points per block (point g of group g / per lives at index
+// (g / per) * stride + g % per + first;
 // points of proofs with status[g / per] != 0 are skipped, identities map to (0, 0)):
 //   1. lane-local prefix products of its NORM_E z's (strided by NORM_BS, so
 //      every load/store is coalesced),
@@ -443,7 +457,7 @@ __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, in
     z = f_one<FpP>();
     if (g >= (size_t)total || (status && status[g / per] != 0)) return false;
     Fp zz;
-    load_fp(jac + (g * stride + first) * 24 + 16, zz);
+    load_fp(jac + ((g / per) * stride + g % per + first) * 24 + 16, zz);
     if (!f_is_zero(zz)) z = zz;
     return true;
   };
@@ -503,7 +517,8 @@ __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, in
     Fp zi = j ? fp_mul(inv, acc[j - 1]) : inv;  // z_j^-1
     if (j) inv = fp_mul(inv, z);
     if (!live) continue;
-    const size_t g = (g0 + (size_t)j * NORM_BS) * stride + first;
+    const size_t gg = g0 + (size_t)j * NORM_BS;
+    const size_t g = (gg / per) * stride + gg % per + first;
     const G1J p = load_g1j(jac + g * 24);
     G1A r;
     if (f_is_zero(p.z)) {
@@ -947,18 +962,23 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   tl->mark("k_rp_powers", s, (double)B * (2.0 * n + 2.0 * k));
   FTS_LAUNCH(k_rp_fixed_exact, B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, wtables, d.hpj, d.terms);
   tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FBW);
+  // H'_i -> affine + BE bytes (x0 transcript) now; com is normalised after com_sum
+  const int nhp = B * n;
+  FTS_LAUNCH(k_rp_normalize, (nhp + NORM_E - 1) / NORM_E, NORM_BS, s, nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be);
+  tl->mark("k_rp_normalize", s, (double)nhp * (2.0 * 8.0 / NORM_E + 9.0));
   const int nch = (n + HS_CHUNK - 1) / HS_CHUNK;
-  FTS_LAUNCH(k_rp_hsum_chunks, B * nch, 64, s, B, n, d.status, d.hpj, d.scratch);
-  tl->mark("k_rp_hsum_chunks", s, (double)B * (n - nch) * (COST_DBL + COST_ADD));
+  FTS_LAUNCH(k_rp_hsum_chunks, B * nch, 64, s, B, n, d.status, d.hpa, d.scratch);
+  tl->mark("k_rp_hsum_chunks", s, (double)B * (n - nch) * (COST_DBL + COST_MADD));
+  FTS_LAUNCH(k_rp_hsum_join, B, 64, s, B, n, d.status, d.scratch);
+  tl->mark("k_rp_hsum_join", s, (double)B * (nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD));
   // scratch: [0, B*192) Horner chunks of S, then the 2B lanes' joint tables
   FTS_LAUNCH(k_rp_com_var, 2 * B, 64, s, B, n, k, d.status, d.pts, d.ch, d.scratch, d.scratch + (size_t)B * HS_SCRATCH,
              d.terms);
-  tl->mark("k_rp_com_var", s, (double)B * 2 * (COST_STRAUS2 + (nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD)));
+  tl->mark("k_rp_com_var", s, (double)B * 2 * COST_STRAUS2);
   FTS_LAUNCH(k_rp_com_sum, B, 64, s, B, n, k, d.status, d.pts, d.terms, d.hpj);
   tl->mark("k_rp_com_sum", s, (double)B * COM_NTERMS * COST_ADD);
-  const int npt = B * (n + 1);
-  FTS_LAUNCH(k_rp_normalize, (npt + NORM_E - 1) / NORM_E, NORM_BS, s, npt, n + 1, 1, 0, d.status, d.hpj, d.hpa, d.hp_be);
-  tl->mark("k_rp_normalize", s, (double)npt * (2.0 * 8.0 / NORM_E + 9.0));
+  FTS_LAUNCH(k_rp_normalize, (B + NORM_E - 1) / NORM_E, NORM_BS, s, B, 1, n + 1, n, d.status, d.hpj, d.hpa, d.hp_be);
+  tl->mark("k_rp_normalize_com", s, (double)B * (2.0 * 8.0 / NORM_E + 9.0));
   // side: x0 transcript + hash, then the fixed-base columns (need x0)
   tl->fork(s, s2);
   FTS_LAUNCH(k_rp_x0_build, (size_t)B * (x0_slot_bytes(n) / 16), 256, s2, B, n, d.status, d.hp_be, x0_const, d.sc,
