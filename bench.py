@@ -14,6 +14,9 @@ Other BASELINE.json configs as extra workloads (not the default line):
   --workload transfer  configs[3] / C4 per GPU: --transfers 2-in/2-out 64-bit
                        transfers (TypeAndSum + 2 rp64 each) per step through
                        fts_transfer_verify_batch, transfers/s
+  --workload mixed     configs[4] / C5 per GPU: issues with 16 outputs and
+                       2-in/2-out transfers (1 : 4) at 32-bit range, 1 % tampered,
+                       one fts_actions_verify_batch per step, actions/s
 
 Prints one JSON line (rank 0).  Usage:
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--bits 64]
@@ -76,7 +79,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall-time bound of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    ap.add_argument("--workload", choices=["rp", "msm", "transfer"], default="rp")
+    ap.add_argument("--workload", choices=["rp", "msm", "transfer", "mixed"], default="rp")
     ap.add_argument("--msm-log", type=int, default=20, help="msm workload: log2 of the point count")
     ap.add_argument("--transfers", type=int, default=8192, help="transfer workload: transfers per GPU per step")
     args = ap.parse_args()
@@ -84,6 +87,8 @@ def main():
         return bench_msm(args)
     if args.workload == "transfer":
         return bench_transfer(args)
+    if args.workload == "mixed":
+        return bench_mixed(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -454,6 +459,88 @@ def bench_transfer(args):
             "config": {"workload": "C4 per GPU: %d transfers (TypeAndSum + 2 rp%d each) per step via "
                                    "fts_transfer_verify_batch" % (args.transfers, args.bits),
                        "transfers_per_gpu": args.transfers, "parallelism": "shard%d" % world},
+            "roofline": _roofline_from(kt, args.steps),
+            "kernel_ms": {k: round(v[0] / args.steps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),
+            flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_mixed(args):
+    """C5: issue(16 outputs) : transfer(2-in/2-out) = 1 : 4 at 32-bit range,
+    1 % of the actions tampered (wrong committed value), one pass per step"""
+    world, rank, local, dist = _dist_setup()
+    import random
+    import numpy as np
+    import fts_gpu
+    bits = 32
+    with open(os.path.join(ROOT, "tests", "golden", "zkatdlog_pp.json"), "rb") as f:
+        pp_raw = f.read()
+    pp = fts_gpu.PublicParams(pp_raw, bit_length=bits, device=local)
+    T = b"ABC"
+    rng = random.Random(0xF7A50005 + rank)
+    n_tr = args.transfers
+    n_is = n_tr // 4
+    t0 = time.time()
+
+    def bf():
+        return rng.randrange(R_ORDER).to_bytes(32, "big")
+
+    def transfer(bad):
+        a, b_ = rng.getrandbits(bits - 2), rng.getrandbits(bits - 2)
+        c = rng.randrange(a + b_ + 1)
+        inv, outv = [a, b_], [c, a + b_ - c]
+        ib, ob = [bf(), bf()], [bf(), bf()]
+        ins = [pp.token_commit(T, v, x) for v, x in zip(inv, ib)]
+        outs = [pp.token_commit(T, v + (1 if bad and j == 0 else 0), x) for j, (v, x) in enumerate(zip(outv, ob))]
+        return ins, outs, pp.prove_transfer(T, inv, ib, outv, ob, rng.getrandbits(63))
+
+    def issue(bad):
+        vals = [rng.getrandbits(bits) for _ in range(16)]
+        bfs = [bf() for _ in range(16)]
+        toks = [pp.token_commit(T, v, x) for v, x in zip(vals, bfs)]
+        if bad:
+            toks[rng.randrange(16)] = pp.token_commit(T, vals[0] ^ 1, bfs[0])
+        return toks, pp.prove_issue(T, vals, bfs, rng.getrandbits(63))
+
+    dt, di = min(n_tr, 256), min(n_is, 64)
+    tr_base = [transfer(False) for _ in range(dt)]
+    is_base = [issue(False) for _ in range(di)]
+    bad_tr = set(rng.sample(range(n_tr), max(1, n_tr // 100)))
+    bad_is = set(rng.sample(range(n_is), max(1, n_is // 100)))
+    tr_bad = {i: transfer(True) for i in bad_tr}
+    is_bad = {i: issue(True) for i in bad_is}
+    transfers = [tr_bad.get(i, tr_base[i % dt]) for i in range(n_tr)]
+    issues = [is_bad.get(i, is_base[i % di]) for i in range(n_is)]
+    batch = pp.prepare_actions(transfers, issues)
+    setup_s = time.time() - t0
+    for _ in range(max(1, args.warmup)):
+        st_t, _, st_i, _ = batch.verify()
+    assert set(np.nonzero(st_t)[0]) == bad_tr and set(np.nonzero(st_i)[0]) == bad_is, "verdict mismatch"
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    kt = {}
+    for _ in range(args.steps):
+        st_t, _, st_i, _ = batch.verify()
+        for name, (ms, mads) in pp.last_timings_ex().items():
+            o = kt.get(name, (0.0, 0.0))
+            kt[name] = (o[0] + ms, mads)
+        if dist is not None:
+            from fts_gpu import dist as fdist
+            fdist.allgather_verdicts(dist, np.concatenate([st_t, st_i]))
+    elapsed = _max_over_ranks(dist, time.perf_counter() - t0)
+    value = world * (n_tr + n_is) * args.steps / elapsed
+    if rank == 0:
+        print(json.dumps({
+            "metric": "mixed action verifies/sec (issue-16 + 2-in/2-out transfers, BN254, 32-bit)",
+            "value": round(value, 1), "unit": "actions/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32 (BN254 Fp/Fr 8x32-bit Montgomery)",
+            "data": "synthetic: %d transfers + %d issues (16 outputs) per GPU, 1 %% tampered, host prover" % (n_tr, n_is),
+            "config": {"workload": "C5 per GPU: 1 issue-16 : 4 transfers at 32-bit, one fts_actions_verify_batch "
+                                   "per step (%d range proofs)" % (2 * n_tr + 16 * n_is),
+                       "transfers_per_gpu": n_tr, "issues_per_gpu": n_is, "parallelism": "shard%d" % world},
             "roofline": _roofline_from(kt, args.steps),
             "kernel_ms": {k: round(v[0] / args.steps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),
             flush=True)

@@ -1414,6 +1414,41 @@ int fts_issue_verify_batch(fts_ctx* c, size_t n, const fts_issue_item* items, in
   return rc;
 }
 
+// mixed batch (BASELINE config C5): the transfers and issues of many token
+// requests verified in ONE device pass (one range-proof batch + one sigma batch)
+int fts_actions_verify_batch(fts_ctx* c, size_t n_tr, const fts_transfer_item* transfers, size_t n_is,
+                             const fts_issue_item* issues, int32_t* status_tr, int32_t* fail_tr, int32_t* status_is,
+                             int32_t* fail_is) {
+  if (!c || (n_tr && (!transfers || !status_tr)) || (n_is && (!issues || !status_is))) return FTS_API_EINVAL;
+  if (c->device < 0) return FTS_API_EDEVICE;
+  const size_t n = n_tr + n_is;
+  if (n == 0) return FTS_API_OK;
+  std::vector<ActionIn> acts(n);
+  for (size_t i = 0; i < n_tr; i++)
+    acts[i] = ActionIn{SIG_TAS, transfers[i].inputs, transfers[i].n_in, transfers[i].outputs, transfers[i].n_out,
+                       der::Span{transfers[i].proof, transfers[i].proof ? transfers[i].proof_len : 0}};
+  for (size_t i = 0; i < n_is; i++)
+    acts[n_tr + i] = ActionIn{SIG_ST, nullptr, 0, issues[i].tokens, issues[i].n_tok,
+                              der::Span{issues[i].proof, issues[i].proof ? issues[i].proof_len : 0}};
+  std::vector<int32_t> st(n, FTS_E_NOT_RUN), fi(n, -1);
+  HIP_OK(hipSetDevice(c->device));
+  int rc;
+  {
+    LaneGuard lg(c);
+    rc = verify_actions(c, *lg.L, acts, st.data(), fi.data());
+  }
+  if (rc != FTS_API_OK) std::fill(st.begin(), st.end(), FTS_E_NOT_RUN);
+  for (size_t i = 0; i < n_tr; i++) {
+    status_tr[i] = st[i];
+    if (fail_tr) fail_tr[i] = fi[i];
+  }
+  for (size_t i = 0; i < n_is; i++) {
+    status_is[i] = st[n_tr + i];
+    if (fail_is) fail_is[i] = fi[n_tr + i];
+  }
+  return rc;
+}
+
 }  // extern "C"
 
 // ------------------------------------------------------------------ prover

@@ -144,6 +144,13 @@ class PublicParams:
         (status, fail_index) arrays."""
         return self.prepare_transfers(transfers).verify()
 
+    def verify_actions(self, transfers, issues):
+        """mixed batch in one device pass -> (st_transfers, fail_transfers, st_issues, fail_issues)"""
+        return self.prepare_actions(transfers, issues).verify()
+
+    def prepare_actions(self, transfers, issues):
+        return ActionBatch(self, transfers, issues)
+
     def prepare_transfers(self, transfers):
         """the fts_transfer_item array of a batch (host buffers the C-ABI borrows),
         reusable across verify() calls"""
@@ -284,7 +291,7 @@ class TransferBatch:
     def __init__(self, pp, transfers):
         self.pp = pp
         self.n = len(transfers)
-        self.items = (L.TransferItem * self.n)()
+        self.items = (L.TransferItem * max(1, self.n))()
         self._keep = []
         for i, (ins, outs, proof) in enumerate(transfers):
             bi = C.create_string_buffer(b"".join(ins) or b"\0")
@@ -301,6 +308,39 @@ class TransferBatch:
             self.pp._ctx, self.n, self.items, st.ctypes.data_as(C.POINTER(C.c_int32)),
             fi.ctypes.data_as(C.POINTER(C.c_int32))))
         return st, fi
+
+
+class IssueBatch:
+    """Host-side fts_issue_item array."""
+
+    def __init__(self, pp, issues):
+        self.pp = pp
+        self.n = len(issues)
+        self.items = (L.IssueItem * max(1, self.n))()
+        self._keep = []
+        for i, (toks, proof) in enumerate(issues):
+            bt = C.create_string_buffer(b"".join(toks) or b"\0")
+            bp = C.create_string_buffer(proof or b"\0", max(1, len(proof)))
+            self._keep += [bt, bp]
+            self.items[i] = L.IssueItem(C.cast(bt, C.c_void_p), len(toks), C.cast(bp, C.c_void_p), len(proof))
+
+
+class ActionBatch:
+    """Transfers + issues verified together (fts_actions_verify_batch)."""
+
+    def __init__(self, pp, transfers, issues):
+        self.pp = pp
+        self.tr = TransferBatch(pp, transfers)
+        self.iss = IssueBatch(pp, issues)
+
+    def verify(self):
+        nt, ni = self.tr.n, self.iss.n
+        st_t, fi_t = np.zeros(max(1, nt), dtype=np.int32), np.zeros(max(1, nt), dtype=np.int32)
+        st_i, fi_i = np.zeros(max(1, ni), dtype=np.int32), np.zeros(max(1, ni), dtype=np.int32)
+        ptr = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32))  # noqa: E731
+        L.check("fts_actions_verify_batch", L.lib.fts_actions_verify_batch(
+            self.pp._ctx, nt, self.tr.items, ni, self.iss.items, ptr(st_t), ptr(fi_t), ptr(st_i), ptr(fi_i)))
+        return st_t[:nt], fi_t[:nt], st_i[:ni], fi_i[:ni]
 
 
 class StagedMsm:

@@ -29,7 +29,7 @@ FTS_DEVICE_NONE = -2
 
 EXPORTED = [
     "fts_ctx_create", "fts_ctx_create_bits", "fts_ctx_destroy", "fts_ctx_info",
-    "fts_rp_verify_batch", "fts_transfer_verify_batch", "fts_issue_verify_batch",
+    "fts_rp_verify_batch", "fts_transfer_verify_batch", "fts_issue_verify_batch", "fts_actions_verify_batch",
     "fts_rp_batch_stage", "fts_rp_batch_verify", "fts_rp_batch_free", "fts_rp_batch_merged", "fts_ctx_reserve", "fts_last_timings", "fts_last_timings_ex", "fts_rp_batch_timings",
     "fts_status_str", "fts_rp_prove", "fts_rp_prove_batch", "fts_token_commit",
     "fts_transfer_prove", "fts_issue_prove", "fts_debug_rp_intermediates",
@@ -64,6 +64,8 @@ def _load():
         "fts_rp_verify_batch": ([P, S, C.POINTER(C.c_void_p), C.POINTER(S), U8P, I32P], C.c_int),
         "fts_transfer_verify_batch": ([P, S, C.POINTER(TransferItem), I32P, I32P], C.c_int),
         "fts_issue_verify_batch": ([P, S, C.POINTER(IssueItem), I32P, I32P], C.c_int),
+        "fts_actions_verify_batch": ([P, S, C.POINTER(TransferItem), S, C.POINTER(IssueItem), I32P, I32P, I32P, I32P],
+                                     C.c_int),
         "fts_rp_batch_stage": ([P, S, C.POINTER(C.c_void_p), C.POINTER(S), U8P, C.POINTER(P)], C.c_int),
         "fts_rp_batch_verify": ([P, P, I32P], C.c_int),
         "fts_rp_batch_free": ([P], None),

@@ -117,6 +117,13 @@ int fts_transfer_verify_batch(fts_ctx* ctx, size_t n, const fts_transfer_item* i
 int fts_issue_verify_batch(fts_ctx* ctx, size_t n, const fts_issue_item* items, int32_t* status,
                            int32_t* fail_index);
 
+/* Transfers and issues of many token requests in ONE device pass (BASELINE config C5):
+ * verdicts identical to fts_transfer_verify_batch / fts_issue_verify_batch on the same
+ * items.  fail_tr / fail_is may be NULL. */
+int fts_actions_verify_batch(fts_ctx* ctx, size_t n_tr, const fts_transfer_item* transfers, size_t n_is,
+                             const fts_issue_item* issues, int32_t* status_tr, int32_t* fail_tr, int32_t* status_is,
+                             int32_t* fail_is);
+
 /* ---- device-resident batches (parse + upload once, verify many times) ---- */
 int fts_rp_batch_stage(fts_ctx* ctx, size_t n, const uint8_t* const* rp_der, const size_t* rp_len,
                        const uint8_t* com64, fts_rp_batch** out);

@@ -160,3 +160,45 @@ def test_reference_shaped_transfer_api(gpu_pp):
     with pytest.raises(fts_gpu.VerifyError) as e:
         fts_gpu.TransferVerifier(ins, outs, pp).Verify(pp.prove_transfer(b"ABC", [220, 60], ib, [261, 20], ob, 1))
     assert "invalid transfer proof: invalid sum and type proof" in str(e.value)
+
+
+def test_mixed_actions_one_pass(gpu_pp, oracle_pp):
+    """BASELINE config C5 shape: issues with 16 outputs at 32-bit range plus
+    2-in/2-out transfers, verified in ONE device pass
+    (fts_actions_verify_batch).  Every verdict equals the oracle's
+    (reference) verdict and the separate transfer / issue calls."""
+    bits = 32
+    pp = gpu_pp(bits)
+    opp = oracle_pp.with_bit_length(bits)
+    T = b"USD"
+    transfers, t_expect = [], []
+    for seed in range(1, 5):
+        inv = [1000 * seed + 7, 50 * seed]
+        outv = [inv[0] - seed, inv[1] + seed] if seed != 3 else [inv[0], inv[1] + 1]  # seed 3: wrong sum
+        ib = [_bf(seed * 10 + j) for j in range(2)]
+        ob = [_bf(seed * 10 + 5 + j) for j in range(2)]
+        ins = [pp.token_commit(T, v, b) for v, b in zip(inv, ib)]
+        outs = [pp.token_commit(T, v, b) for v, b in zip(outv, ob)]
+        proof = pp.prove_transfer(T, inv, ib, outv, ob, seed)
+        transfers.append((ins, outs, proof))
+        err, idx = zkat.transfer_verify(opp, [bn.g1_from_bytes(x) for x in ins], [bn.g1_from_bytes(x) for x in outs],
+                                        proof)
+        t_expect.append(oracle_status(err, idx))
+    issues, i_expect = [], []
+    for seed in (21, 22):
+        vals = [(seed * 7919 + 104729 * j) % (1 << 32) for j in range(16)]
+        bfs = [_bf(seed * 100 + j) for j in range(16)]
+        toks = [pp.token_commit(T, v, b) for v, b in zip(vals, bfs)]
+        proof = pp.prove_issue(T, vals, bfs, seed)
+        if seed == 22:  # token 5 committed to another value -> its range proof fails
+            toks[5] = pp.token_commit(T, vals[5] + 1, bfs[5])
+        issues.append((toks, proof))
+        err, idx = zkat.issue_verify(opp, [bn.g1_from_bytes(x) for x in toks], proof)
+        i_expect.append(oracle_status(err, idx, "invalid issue proof: "))
+    st_t, fi_t, st_i, fi_i = pp.verify_actions(transfers, issues)
+    assert [(int(s), int(i)) for s, i in zip(st_t, fi_t)] == t_expect
+    assert [(int(s), int(i)) for s, i in zip(st_i, fi_i)] == i_expect
+    assert t_expect[2][0] == 8 and t_expect[0] == (0, -1) and i_expect[0] == (0, -1) and i_expect[1][0] != 0
+    s2, f2 = pp.verify_transfers(transfers)
+    s3, f3 = pp.verify_issues(issues)
+    assert (s2 == st_t).all() and (f2 == fi_t).all() and (s3 == st_i).all() and (f3 == fi_i).all()
