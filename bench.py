@@ -81,7 +81,9 @@ def main():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     ap.add_argument("--workload", choices=["rp", "msm", "transfer", "mixed"], default="rp")
     ap.add_argument("--msm-log", type=int, default=20, help="msm workload: log2 of the point count")
-    ap.add_argument("--transfers", type=int, default=8192, help="transfer workload: transfers per GPU per step")
+    ap.add_argument("--transfers", type=int, default=8192, help="transfer/mixed workloads: transfers per GPU per step")
+    ap.add_argument("--action-inflight", type=int, default=3,
+                    help="transfer/mixed workloads: concurrent verify calls (host threads)")
     args = ap.parse_args()
     if args.workload == "msm":
         return bench_msm(args)
@@ -345,6 +347,31 @@ def _roofline_from(timings, steps):
             "traffic": None, "kernel_ms": round(ms, 4), "mads_per_launch": mads}
 
 
+def _run_action_steps(batches, steps, dist, gather):
+    """`steps` verify() calls spread over one host thread per prepared batch
+    (concurrent calls run on different device lanes, so one call's host DER
+    parsing overlaps another's kernels); returns (elapsed, per-kernel timings)"""
+    per = [steps // len(batches) + (1 if i < steps % len(batches) else 0) for i in range(len(batches))]
+    outs = [[] for _ in batches]
+
+    def run(i):
+        for _ in range(per[i]):
+            outs[i].append(batches[i].verify())
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(len(batches))]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        for o in outs:
+            for r in o:
+                gather(r)
+    return elapsed, outs
+
+
 def bench_msm(args):
     world, rank, local, dist = _dist_setup()
     import random
@@ -429,24 +456,21 @@ def bench_transfer(args):
         ins = [pp.token_commit(T, v, bf) for v, bf in zip(inv, ib)]
         outs = [pp.token_commit(T, v, bf) for v, bf in zip(outv, ob)]
         base.append((ins, outs, pp.prove_transfer(T, inv, ib, outv, ob, 0xF7A50004 + i)))
-    batch = pp.prepare_transfers([base[i % distinct] for i in range(args.transfers)])
+    items = [base[i % distinct] for i in range(args.transfers)]
+    nb = max(1, min(args.action_inflight, args.steps))
+    batches = [pp.prepare_transfers(items) for _ in range(nb)]
     setup_s = time.time() - t0
     for _ in range(max(1, args.warmup)):
-        st, fi = batch.verify()
+        st, fi = batches[0].verify()
     assert int((st != 0).sum()) == 0, "honest transfers rejected"
+    _run_action_steps(batches, nb, None, None)
     if dist is not None:
         dist.barrier()
-    t0 = time.perf_counter()
-    kt = {}
-    for _ in range(args.steps):
-        st, fi = batch.verify()  # host buffers in (the C-ABI parses the DER proofs), verdicts out
-        for name, (ms, mads) in pp.last_timings_ex().items():
-            o = kt.get(name, (0.0, 0.0))
-            kt[name] = (o[0] + ms, mads)
-        if dist is not None:
-            from fts_gpu import dist as fdist
-            fdist.allgather_verdicts(dist, st)
-    elapsed = _max_over_ranks(dist, time.perf_counter() - t0)
+    from fts_gpu import dist as fdist
+    # host buffers in (the C-ABI parses the DER proofs), verdicts out
+    elapsed, _ = _run_action_steps(batches, args.steps, dist, lambda r: fdist.allgather_verdicts(dist, r[0]))
+    elapsed = _max_over_ranks(dist, elapsed)
+    kt = {k: (v[0] * args.steps, v[1]) for k, v in pp.last_timings_ex().items()}
     value = world * args.transfers * args.steps / elapsed
     if rank == 0:
         print(json.dumps({
@@ -457,7 +481,7 @@ def bench_transfer(args):
             "data": "synthetic: %d distinct 2-in/2-out transfers (type ABC) from the library's host prover, tiled"
                     % distinct,
             "config": {"workload": "C4 per GPU: %d transfers (TypeAndSum + 2 rp%d each) per step via "
-                                   "fts_transfer_verify_batch" % (args.transfers, args.bits),
+                                   "fts_transfer_verify_batch, %d calls in flight" % (args.transfers, args.bits, nb),
                        "transfers_per_gpu": args.transfers, "parallelism": "shard%d" % world},
             "roofline": _roofline_from(kt, args.steps),
             "kernel_ms": {k: round(v[0] / args.steps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),
@@ -512,24 +536,23 @@ def bench_mixed(args):
     is_bad = {i: issue(True) for i in bad_is}
     transfers = [tr_bad.get(i, tr_base[i % dt]) for i in range(n_tr)]
     issues = [is_bad.get(i, is_base[i % di]) for i in range(n_is)]
-    batch = pp.prepare_actions(transfers, issues)
+    nb = max(1, min(args.action_inflight, args.steps))
+    batches = [pp.prepare_actions(transfers, issues) for _ in range(nb)]
     setup_s = time.time() - t0
     for _ in range(max(1, args.warmup)):
-        st_t, _, st_i, _ = batch.verify()
+        st_t, _, st_i, _ = batches[0].verify()
     assert set(np.nonzero(st_t)[0]) == bad_tr and set(np.nonzero(st_i)[0]) == bad_is, "verdict mismatch"
+    _run_action_steps(batches, nb, None, None)
     if dist is not None:
         dist.barrier()
-    t0 = time.perf_counter()
-    kt = {}
-    for _ in range(args.steps):
-        st_t, _, st_i, _ = batch.verify()
-        for name, (ms, mads) in pp.last_timings_ex().items():
-            o = kt.get(name, (0.0, 0.0))
-            kt[name] = (o[0] + ms, mads)
-        if dist is not None:
-            from fts_gpu import dist as fdist
-            fdist.allgather_verdicts(dist, np.concatenate([st_t, st_i]))
-    elapsed = _max_over_ranks(dist, time.perf_counter() - t0)
+    from fts_gpu import dist as fdist
+    elapsed, outs = _run_action_steps(batches, args.steps, dist,
+                                      lambda r: fdist.allgather_verdicts(dist, np.concatenate([r[0], r[2]])))
+    elapsed = _max_over_ranks(dist, elapsed)
+    for o in outs:
+        for r in o:
+            assert set(np.nonzero(r[0])[0]) == bad_tr and set(np.nonzero(r[2])[0]) == bad_is
+    kt = {k: (v[0] * args.steps, v[1]) for k, v in pp.last_timings_ex().items()}
     value = world * (n_tr + n_is) * args.steps / elapsed
     if rank == 0:
         print(json.dumps({
@@ -539,7 +562,7 @@ def bench_mixed(args):
             "scaling": "weak", "vs_baseline": None, "dtype": "u32 (BN254 Fp/Fr 8x32-bit Montgomery)",
             "data": "synthetic: %d transfers + %d issues (16 outputs) per GPU, 1 %% tampered, host prover" % (n_tr, n_is),
             "config": {"workload": "C5 per GPU: 1 issue-16 : 4 transfers at 32-bit, one fts_actions_verify_batch "
-                                   "per step (%d range proofs)" % (2 * n_tr + 16 * n_is),
+                                   "per step (%d range proofs), %d calls in flight" % (2 * n_tr + 16 * n_is, nb),
                        "transfers_per_gpu": n_tr, "issues_per_gpu": n_is, "parallelism": "shard%d" % world},
             "roofline": _roofline_from(kt, args.steps),
             "kernel_ms": {k: round(v[0] / args.steps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),

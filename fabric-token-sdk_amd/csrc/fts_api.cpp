@@ -137,6 +137,7 @@ struct Lane {
   Workspace ws;
   Timeline tl;
   float host_prep_ms = 0, host_enqueue_ms = 0, host_wait_ms = 0;  // host wall time of the last run
+  float host_parse_ms = 0, host_stage_ms = 0;  // action batches: DER parsing, assembly + upload
   // pinned host staging (pageable async copies would block the enqueue)
   struct Pinned {
     uint32_t key[8];
@@ -163,6 +164,23 @@ struct Lane {
     pin_status_cap = 0;
   }
 };
+// host worker threads for batch parsing: the CPUs this process may actually
+// use (cgroup v2 cpu.max quota, else the hardware count), at most 16
+static unsigned host_threads() {
+  static const unsigned n = [] {
+    unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {0};
+      long long period = 0;
+      if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0)
+        hw = std::min<unsigned>(hw, (unsigned)std::max(1LL, atoll(q) / period));
+      fclose(f);
+    }
+    return std::min(16u, hw);
+  }();
+  return n;
+}
+
 static inline double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -261,7 +279,7 @@ void build_prover_tables(const PublicParams& pp, int n, ProverTables& t) {
   bases.push_back(pp.Q);
   t.fb.resize(bases.size());
   std::atomic<size_t> next{0};
-  unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  unsigned nth = host_threads();
   std::vector<std::thread> th;
   for (unsigned w = 0; w < nth; w++)
     th.emplace_back([&]() {
@@ -533,7 +551,7 @@ static void parse_rp_batch(int k, size_t B, const uint8_t* const* der_p, const s
       memcpy(pts + RP_PT_V * 64, com64 + i * 64, 64);
     }
   };
-  unsigned nth = B >= 256 ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
+  unsigned nth = B >= 256 ? host_threads() : 1u;
   std::vector<std::thread> th;
   size_t chunk = (B + nth - 1) / nth;
   for (unsigned t = 0; t < nth; t++) {
@@ -554,9 +572,9 @@ static void collect_timings(fts_ctx* c, Lane& L, fts_rp_batch* b) {
     c->tim_work[j] = L.tl.work[i];
     hipEventElapsedTime(&c->tim_ms[j], L.tl.ev[L.tl.start[i]], L.tl.ev[i + 1]);
   }
-  const char* hn[3] = {"host_prep", "host_enqueue", "host_wait_flag"};
-  const float hv[3] = {L.host_prep_ms, L.host_enqueue_ms, L.host_wait_ms};
-  for (int q = 0; q < 3 && c->ntim < Timeline::CAP; q++) {
+  const char* hn[5] = {"host_prep", "host_enqueue", "host_wait_flag", "host_parse", "host_stage"};
+  const float hv[5] = {L.host_prep_ms, L.host_enqueue_ms, L.host_wait_ms, L.host_parse_ms, L.host_stage_ms};
+  for (int q = 0; q < 5 && c->ntim < Timeline::CAP; q++) {
     c->tim_name[c->ntim] = hn[q];
     c->tim_ms[c->ntim] = hv[q];
     c->tim_work[c->ntim] = 0;
@@ -1094,6 +1112,7 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
     std::vector<int32_t> rp_status, rp_ipa;
   };
   std::vector<Parsed> P(A);
+  const double t_parse0 = now_ms();
   auto parse_one = [&](size_t i) {
     const ActionIn& ai = acts[i];
     ActionState& s = st[i];
@@ -1218,7 +1237,7 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
     s.sig_on_device = true;
   };
   {
-    unsigned nth = A >= 64 ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
+    unsigned nth = A >= 64 ? host_threads() : 1u;
     std::atomic<size_t> next{0};
     std::vector<std::thread> th;
     for (unsigned t = 0; t < nth; t++)
@@ -1227,6 +1246,8 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
       });
     for (auto& t : th) t.join();
   }
+  const double t_parse1 = now_ms();
+  L.host_parse_ms = (float)(t_parse1 - t_parse0);
   // ---- assemble device batches
   std::vector<SigAction> sact;
   std::vector<int32_t> s_owner, s_affoff, s_status;
@@ -1328,6 +1349,7 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
     sd.rp_raw = rp_total ? w.rp_raw.as<uint8_t>() : nullptr;
     sd.rp_k = k;
     launch_sig_prep(sd, L.s);
+    L.host_stage_ms = (float)(now_ms() - t_parse1);
   }
   auto sig_finish = [&]() {
     if (SA) launch_sig_finish(sd, c->d_tables, n, L.s);
@@ -1500,7 +1522,7 @@ int fts_rp_prove_batch(const fts_ctx* c, size_t n, const uint64_t* values, const
   const ProverTables& T = prover_tables(c);
   std::vector<std::string> res(n);
   std::atomic<size_t> next{0};
-  int nth = threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  int nth = threads > 0 ? threads : (int)host_threads();
   std::vector<std::thread> th;
   for (int t = 0; t < nth; t++)
     th.emplace_back([&]() {
