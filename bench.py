@@ -96,11 +96,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # FTS_DIST_BACKEND=gloo + FTS_DEVICE=0 rehearse the N > 1 path with every
+    # rank on one GPU (the exchange then runs over CPU tensors)
+    backend = os.environ.get("FTS_DIST_BACKEND", "nccl")
+    local = int(os.environ.get("FTS_DEVICE", str(local)))
     if world > 1:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     os.environ["FTS_LANES"] = str(max(1, args.lanes))
     import random
@@ -282,11 +289,18 @@ def _dist_setup():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # FTS_DIST_BACKEND=gloo + FTS_DEVICE=0 rehearse the N > 1 path with every
+    # rank on one GPU (the exchange then runs over CPU tensors)
+    backend = os.environ.get("FTS_DIST_BACKEND", "nccl")
+    local = int(os.environ.get("FTS_DEVICE", str(local)))
     if world > 1:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local, dist
 
 
