@@ -73,6 +73,8 @@ def main():
                          "all lanes are busy are coalesced into one device pass (FTS_COALESCE_MAX proofs)")
     ap.add_argument("--distinct", type=int, default=4,
                     help="batches with distinct proofs; the other in-flight batches re-stage them (setup time)")
+    ap.add_argument("--pass-batches", type=int, default=0,
+                    help="batches in the isolated roofline pass (0: the timed region's average pass size)")
     ap.add_argument("--roofline-steps", type=int, default=6,
                     help="isolated steps (one batch alone on the GPU) for the per-kernel roofline")
     ap.add_argument("--cpu-sample", type=int, default=256, help="CPU baseline chunk size (0: skip the CPU baseline)")
@@ -185,20 +187,34 @@ def main():
     total = world * B * args.steps
     value = total / elapsed
 
-    # Roofline pass (after the timed region): one batch alone on the GPU, so
-    # each kernel's HIP-event time is its own (in the pipelined region kernels
-    # of several passes share the CUs and their event spans overlap).
-    kt = {}
+    # Isolated passes (after the timed region), so each kernel's HIP-event
+    # time is its own (in the pipelined region kernels of several passes share
+    # the CUs and their event spans overlap):
+    #  1. one 4,096-proof batch alone: the single-batch latency view;
+    #  2. one pass of the size the timed region ran (merged_batches_avg
+    #     batches, coalesced), alone: the ROOFLINE launch -- run last, so the
+    #     last R dispatches of a rocprofv3 trace / PMC pass are exactly these.
     R = max(1, args.roofline_steps)
-    t_iso = time.perf_counter()
-    for _ in range(R):
-        st = batches[0].verify(want_status=True)
-        assert int((st != 0).sum()) == 0
-        for name, (ms, mads) in batches[0].timings().items():
-            o = kt.get(name, (0.0, 0.0))
-            kt[name] = (o[0] + ms, mads)
-    iso_ms = (time.perf_counter() - t_iso) * 1e3 / R
+
+    def isolated(batch, reps):
+        acc = {}
+        t = time.perf_counter()
+        for _ in range(reps):
+            st = batch.verify(want_status=True)
+            assert int((st != 0).sum()) == 0
+            for name, (ms, mads) in batch.timings().items():
+                o = acc.get(name, (0.0, 0.0))
+                acc[name] = (o[0] + ms, mads)
+        return acc, (time.perf_counter() - t) * 1e3 / reps
+
+    kt1, iso_ms = isolated(batches[0], R)
+    m = args.pass_batches or max(1, min(int(round(merged_avg)), 32768 // B))
+    pass_proofs = [sets[i % len(sets)] for i in range(m)]
+    big = pp.stage_range_proofs([p for ps, _ in pass_proofs for p in ps], [c for _, cs in pass_proofs for c in cs])
+    kt, pass_ms = isolated(big, R)
+    big.close()
     avg = {kname: v[0] / R for kname, v in kt.items()}
+    avg1 = {kname: v[0] / R for kname, v in kt1.items()}
     # roofline kernel: the largest share of the algorithmic work (MADs/launch);
     # the longest (latency-bound) kernel is reported beside it
     dom = max(kt, key=lambda kname: kt[kname][1])
@@ -210,8 +226,8 @@ def main():
         return {"kernel": kname, "kernel_ms": round(ms, 4), "mads_per_launch": mads,
                 "achieved": round(ach, 3) if ach else None, "frac": round(ach / PEAK_TMAD, 4) if ach else None}
 
-    # this pipeline's own cost model: algorithmic MADs of every kernel of one batch / B
-    own_mads = sum(v[1] for v in kt.values()) / B
+    # this pipeline's own cost model: algorithmic MADs of every kernel of one pass / proofs
+    own_mads = sum(v[1] for v in kt.values()) / (m * B)
     traffic = None
     try:
         with open(args.traffic_json) as f:
@@ -223,7 +239,8 @@ def main():
     roofline = {"bound": "int32_valu (v_mad_u64_u32)", "kernel": dom, "achieved": rd["achieved"],
                 "peak": round(PEAK_TMAD, 3), "unit": "TMAD/s", "frac": rd["frac"], "traffic": traffic,
                 "kernel_ms": rd["kernel_ms"], "mads_per_launch": rd["mads_per_launch"],
-                "measured": "HIP events, %d isolated steps of one %d-proof batch after the timed region" % (R, B),
+                "measured": "HIP events, %d isolated passes of %d proofs (%d coalesced batches, the timed region's "
+                            "pass size) alone on the GPU after the timed region" % (R, m * B, m),
                 "pipeline_frac_survey_model": round(value / world * SURVEY_MAD_PER_RP64 / (PEAK_TMAD * 1e12), 4),
                 "pipeline_mads_per_rp64": round(own_mads),
                 "pipeline_frac_own_model": round(value / world * own_mads / (PEAK_TMAD * 1e12), 4)}
@@ -271,7 +288,11 @@ def main():
             "merged_batches_avg": round(merged_avg, 2),
             "host": host,
             "isolated_batch": {"ms": round(iso_ms, 3), "verifies_per_s": round(B / iso_ms * 1e3, 1),
-                               "note": "one %d-proof batch alone on the GPU (latency; no coalescing)" % B},
+                               "note": "one %d-proof batch alone on the GPU (latency; no coalescing)" % B,
+                               "roofline_kernel_ms": round(avg1.get(dom, 0.0), 4),
+                               "roofline_frac": round(kt1[dom][1] / (avg1[dom] * 1e-3) / 1e12 / PEAK_TMAD, 4)
+                               if avg1.get(dom) else None},
+            "isolated_pass": {"proofs": m * B, "ms": round(pass_ms, 3), "verifies_per_s": round(m * B / pass_ms * 1e3, 1)},
             "roofline": roofline,
             "longest_kernel": longest_kernel,
             "cpu_baseline": cpu,

@@ -22,18 +22,18 @@ if [ "${TESTS:-0}" = 1 ]; then
   step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
   tail -3 $OUT/pytest_gpu.log
 fi
-step bench 400 python3 -u bench.py --steps ${STEPS:-256} --warmup 32
+step bench 400 python3 -u bench.py --steps ${STEPS:-512} --warmup 64
 grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json
 cat $OUT/bench.json
 step int_peak 120 fabric-token-sdk_amd/lib/int_peak
 cat $OUT/int_peak.log
 rm -rf $OUT/prof_$TAG
-step rocprof 300 rocprofv3 --kernel-trace --stats -T -f csv -d $OUT/prof_$TAG -o run -- python3 bench.py --steps 64 --warmup 16 --distinct 1 --roofline-steps 6 --cpu-sample 0
+step rocprof 300 rocprofv3 --kernel-trace --stats -T -f csv -d $OUT/prof_$TAG -o run -- python3 bench.py --steps 256 --warmup 64 --distinct 1 --roofline-steps 6 --pass-batches 8 --cpu-sample 0
 grep '^{' $OUT/rocprof.log | tail -1 > $OUT/bench_rocprof.json
 python3 tools/prof_summary.py $(find $OUT/prof_$TAG -name "*kernel_trace.csv" | head -1) 6 $OUT/prof_$TAG/isolated.json
 if [ "${PMC:-1}" = 1 ]; then
   # separate passes (TCC: FETCH_SIZE uses 3 slots, WRITE_SIZE 2)
-  PB="python3 bench.py --steps 4 --warmup 4 --inflight 4 --distinct 1 --roofline-steps 2 --cpu-sample 0"
+  PB="python3 bench.py --steps 4 --warmup 4 --inflight 4 --distinct 1 --roofline-steps 2 --pass-batches 8 --cpu-sample 0"
   step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE -T -f csv -d $OUT/pmc_fetch_$TAG -o run -- $PB
   step pmc_write 120 rocprofv3 --pmc WRITE_SIZE -T -f csv -d $OUT/pmc_write_$TAG -o run -- $PB
   step pmc_valu 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE -T -f csv -d $OUT/pmc_valu_$TAG -o run -- $PB
