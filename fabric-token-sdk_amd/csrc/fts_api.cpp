@@ -26,6 +26,7 @@
 #include "host/bn254_host.hpp"
 #include "host/der.hpp"
 #include "host/pp_parse.hpp"
+#include "host/request_parse.hpp"
 #include "host/proofs.hpp"
 #include "host/prover.hpp"
 
@@ -504,6 +505,7 @@ const char* fts_status_str(int32_t s) {
     case FTS_E_TAS_INVALID: return "invalid sum and type proof";
     case FTS_E_ST_INVALID: return "invalid same type proof";
     case FTS_E_NOT_RUN: return "not evaluated";
+    case FTS_E_ACTION_INVALID: return "invalid action";
     default: return "unknown status";
   }
 }
@@ -1469,6 +1471,95 @@ int fts_actions_verify_batch(fts_ctx* c, size_t n_tr, const fts_transfer_item* t
     if (fail_is) fail_is[i] = fi[n_tr + i];
   }
   return rc;
+}
+
+// Raw TokenRequest ingest: decode n requests on the host threads, verify the
+// proofs of every action of every request in one device pass, then fold each
+// request's action verdicts in the reference's order (issues, then transfers).
+int fts_request_verify_batch(fts_ctx* c, size_t n, const uint8_t* const* req, const size_t* req_len,
+                             int32_t* status, int32_t* fail_action, int32_t* fail_index) {
+  if (!c || !status || (n && (!req || !req_len))) return FTS_API_EINVAL;
+  if (c->device < 0) return FTS_API_EDEVICE;
+  if (n == 0) return FTS_API_OK;
+  namespace rq = fts::host::req;
+  std::vector<rq::Request> R(n);
+  {
+    unsigned nth = n >= 64 ? host_threads() : 1u;
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nth; t++)
+      th.emplace_back([&]() {
+        for (size_t i; (i = next++) < n;)
+          rq::parse_request(req[i], req[i] ? req_len[i] : 0, SIG_TAS, SIG_ST, R[i]);
+      });
+    for (auto& t : th) t.join();
+  }
+  // actions that reach the verifier: those before (and excluding) the request's
+  // first structurally invalid action
+  std::vector<ActionIn> acts;
+  std::vector<std::pair<uint32_t, uint32_t>> owner;  // (request, position in acts order)
+  for (size_t i = 0; i < n; i++) {
+    if (R[i].deser_failed) continue;
+    for (size_t j = 0; j < R[i].acts.size(); j++) {
+      const rq::Action& a = R[i].acts[j];
+      if (a.pre >= 0) break;
+      acts.push_back(ActionIn{a.kind, (const uint8_t*)a.in.data(), a.n_in, (const uint8_t*)a.out.data(), a.n_out,
+                              der::Span{(const uint8_t*)a.proof.data(), a.proof.size()}});
+      owner.emplace_back((uint32_t)i, (uint32_t)j);
+    }
+  }
+  std::vector<int32_t> st(acts.size(), FTS_OK), fi(acts.size(), -1);
+  int rc = FTS_API_OK;
+  if (!acts.empty()) {
+    HIP_OK(hipSetDevice(c->device));
+    LaneGuard lg(c);
+    rc = verify_actions(c, *lg.L, acts, st.data(), fi.data());
+  }
+  // fold: first failing verified action, else the first structural verdict
+  std::vector<int32_t> first(n, -1);  // index into acts of the request's first failing action
+  for (size_t q = acts.size(); q-- > 0;)
+    if (st[q] != FTS_OK) first[owner[q].first] = (int32_t)q;
+  for (size_t i = 0; i < n; i++) {
+    const rq::Request& r = R[i];
+    int32_t s = r.status, fa = r.fail_action, fx = -1;
+    if (rc != FTS_API_OK) {
+      s = FTS_E_NOT_RUN, fa = -1;
+    } else if (!r.deser_failed) {
+      if (first[i] >= 0) {
+        const int q = first[i];
+        s = st[q], fx = fi[q], fa = r.acts[owner[q].second].index;
+      } else {
+        for (const rq::Action& a : r.acts)
+          if (a.pre >= 0) {
+            s = a.pre, fa = a.index;
+            break;
+          }
+      }
+    }
+    status[i] = s;
+    if (fail_action) fail_action[i] = fa;
+    if (fail_index) fail_index[i] = fx;
+  }
+  return rc;
+}
+
+int fts_request_inspect(const uint8_t* req, size_t req_len, int32_t* status, int32_t* fail_action, int32_t* n_issue,
+                        int32_t* n_transfer, int32_t* pre_status, int32_t* pre_action) {
+  if (!status || (req_len && !req)) return FTS_API_EINVAL;
+  fts::host::req::Request r;
+  fts::host::req::parse_request(req, req ? req_len : 0, SIG_TAS, SIG_ST, r);
+  int32_t ni = 0, nt = 0, ps = FTS_OK, pa = -1;
+  for (const auto& a : r.acts) {
+    (a.transfer ? nt : ni)++;
+    if (a.pre >= 0 && pa < 0) ps = a.pre, pa = a.index;
+  }
+  *status = r.status;
+  if (fail_action) *fail_action = r.fail_action;
+  if (n_issue) *n_issue = ni;
+  if (n_transfer) *n_transfer = nt;
+  if (pre_status) *pre_status = ps;
+  if (pre_action) *pre_action = pa;
+  return FTS_API_OK;
 }
 
 }  // extern "C"

@@ -63,14 +63,16 @@ inline bool json_int_field(const std::string& js, const std::string& key, long l
 }
 
 inline bool b64_decode(const std::string& in, std::string& out) {
-  static int8_t tbl[256];
-  static bool init = false;
-  if (!init) {
-    for (int i = 0; i < 256; i++) tbl[i] = -1;
-    const char* a = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
-    for (int i = 0; i < 64; i++) tbl[(uint8_t)a[i]] = (int8_t)i;
-    init = true;
-  }
+  struct Tbl {
+    int8_t v[256];
+    Tbl() {
+      for (int i = 0; i < 256; i++) v[i] = -1;
+      const char* a = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+      for (int i = 0; i < 64; i++) v[(uint8_t)a[i]] = (int8_t)i;
+    }
+  };
+  static const Tbl T;  // thread-safe one-time init (request ingest decodes on many threads)
+  const int8_t* tbl = T.v;
   out.clear();
   uint32_t acc = 0;
   int bits = 0;

@@ -32,7 +32,8 @@ import numpy as np
 from . import _lib as L
 from ._lib import (FTS_OK, FTS_E_MALFORMED, FTS_E_RP_NIL, FTS_E_RP_INVALID, FTS_E_IPA_NIL, FTS_E_IPA_LEN,  # noqa
                    FTS_E_IPA_INVALID, FTS_E_RC_COUNT, FTS_E_TAS_INVALID, FTS_E_ST_INVALID, FTS_DEVICE_NONE,
-                   FtsError)
+                   FTS_E_ACTION_INVALID, FtsError)
+from . import request  # noqa: F401  (TokenRequest writers)
 
 
 class VerifyError(Exception):
@@ -72,6 +73,15 @@ def issue_message(status, index):
     if status == FTS_E_RC_COUNT:
         return "invalid issue proof: invalid range proof"
     return "invalid issue proof: invalid range proof at index %d: %s" % (index, _rp_message(status))
+
+
+def inspect_request(raw):
+    """host-only decode of one serialized TokenRequest (fts_request_inspect):
+    dict(status, fail_action, n_issue, n_transfer, pre_status, pre_action)"""
+    out = [C.c_int32() for _ in range(6)]
+    L.check("fts_request_inspect", L.lib.fts_request_inspect(raw, len(raw), *[C.byref(o) for o in out]))
+    keys = ("status", "fail_action", "n_issue", "n_transfer", "pre_status", "pre_action")
+    return {k: o.value for k, o in zip(keys, out)}
 
 
 def _ptr_array(blobs):
@@ -171,6 +181,20 @@ class PublicParams:
         L.check("fts_issue_verify_batch", L.lib.fts_issue_verify_batch(
             self._ctx, n, items, st.ctypes.data_as(C.POINTER(C.c_int32)), fi.ctypes.data_as(C.POINTER(C.c_int32))))
         return st, fi
+
+    def verify_requests(self, requests):
+        """serialized TokenRequests -> (status, fail_action, fail_index) arrays
+        (fts_request_verify_batch: every action's proofs in one device pass)"""
+        n = len(requests)
+        keep, ptrs, lens = _ptr_array(requests)
+        st = np.zeros(n, dtype=np.int32)
+        fa = np.zeros(n, dtype=np.int32)
+        fi = np.zeros(n, dtype=np.int32)
+        I32 = C.POINTER(C.c_int32)
+        L.check("fts_request_verify_batch", L.lib.fts_request_verify_batch(
+            self._ctx, n, ptrs, lens, st.ctypes.data_as(I32), fa.ctypes.data_as(I32), fi.ctypes.data_as(I32)))
+        del keep
+        return st, fa, fi
 
     def stage_range_proofs(self, proofs, commitments):
         return StagedRangeBatch(self, proofs, commitments)

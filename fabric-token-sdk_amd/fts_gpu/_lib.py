@@ -23,6 +23,7 @@ FTS_E_RC_COUNT = 7
 FTS_E_TAS_INVALID = 8
 FTS_E_ST_INVALID = 9
 FTS_E_NOT_RUN = 10
+FTS_E_ACTION_INVALID = 11
 
 FTS_API_OK = 0
 FTS_DEVICE_NONE = -2
@@ -34,6 +35,7 @@ EXPORTED = [
     "fts_status_str", "fts_rp_prove", "fts_rp_prove_batch", "fts_token_commit",
     "fts_transfer_prove", "fts_issue_prove", "fts_debug_rp_intermediates",
     "fts_debug_msm_stats", "fts_msm_g1", "fts_msm_stage", "fts_msm_run", "fts_msm_timings", "fts_msm_free",
+    "fts_request_verify_batch", "fts_request_inspect",
 ]
 
 
@@ -91,6 +93,8 @@ def _load():
         "fts_msm_run": ([P, P, P], C.c_int),
         "fts_msm_timings": ([P, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.POINTER(C.c_double), C.c_int], C.c_int),
         "fts_msm_free": ([P], None),
+        "fts_request_verify_batch": ([P, S, C.POINTER(C.c_void_p), C.POINTER(S), I32P, I32P, I32P], C.c_int),
+        "fts_request_inspect": ([U8P, S, I32P, I32P, I32P, I32P, I32P, I32P], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

@@ -52,7 +52,9 @@ enum fts_status {
   FTS_E_RC_COUNT = 7,       /* "invalid range proof" (#proofs != #commitments) rangecorrectness.go:139 */
   FTS_E_TAS_INVALID = 8,    /* "invalid sum and type proof"          typeandsum.go:232,274 */
   FTS_E_ST_INVALID = 9,     /* "invalid same type proof"             sametype.go:180 */
-  FTS_E_NOT_RUN = 10        /* item not evaluated (batch aborted by an API error) */
+  FTS_E_NOT_RUN = 10,       /* item not evaluated (batch aborted by an API error) */
+  FTS_E_ACTION_INVALID = 11 /* action fails its structural Validate() before the ZK proof:
+                               issue/action.go:161-185,273-282; transfer/action.go:244-283 */
 };
 
 /* ---- API return codes ---- */
@@ -123,6 +125,30 @@ int fts_issue_verify_batch(fts_ctx* ctx, size_t n, const fts_issue_item* items, 
 int fts_actions_verify_batch(fts_ctx* ctx, size_t n_tr, const fts_transfer_item* transfers, size_t n_is,
                              const fts_issue_item* issues, int32_t* status_tr, int32_t* fail_tr, int32_t* status_is,
                              int32_t* fail_is);
+
+/* ---- raw TokenRequest ingest (replaces the deserialisation + ZK half of
+ * Validator.VerifyTokenRequestFromRaw, core/common/validator.go:78-130) ----
+ * req[i] = TokenRequest.Bytes() (driver/request.go:38-53, protos request.proto:95-100).
+ * Every request is decoded on the host (TokenRequest.FromBytes, DeserializeActions:
+ * validator/validator.go:27-47, the actions' Deserialize + Validate), then the ZK proofs
+ * of ALL actions of ALL n requests are verified in ONE device pass.
+ *   status[i]      <- FTS_OK, or the verdict of the request's first failing action in
+ *                     the reference's order (every issue, then every transfer), or
+ *                     FTS_E_MALFORMED when the request / an action does not deserialise
+ *   fail_action[i] <- index in TokenRequest.actions of that action (-1: request level
+ *                     or OK)
+ *   fail_index[i]  <- index of the failing range proof inside that action (-1 if none)
+ * Not evaluated here (stay with the caller's Go code): signatures, auditor signature,
+ * issuer allow-list, upgrade-witness commitment, HTLC scripts, ledger lookups.
+ * fail_action / fail_index may be NULL. */
+int fts_request_verify_batch(fts_ctx* ctx, size_t n, const uint8_t* const* req, const size_t* req_len,
+                             int32_t* status, int32_t* fail_action, int32_t* fail_index);
+/* Host-only decode of one request (no device, ctx not needed): the deserialisation verdict
+ * (status, fail_action as above), the action counts, and the first action (reference order)
+ * whose structural check fails before its proof (pre_status FTS_E_ACTION_INVALID /
+ * FTS_E_MALFORMED, pre_action its index; FTS_OK / -1 if none). */
+int fts_request_inspect(const uint8_t* req, size_t req_len, int32_t* status, int32_t* fail_action,
+                        int32_t* n_issue, int32_t* n_transfer, int32_t* pre_status, int32_t* pre_action);
 
 /* ---- device-resident batches (parse + upload once, verify many times) ---- */
 int fts_rp_batch_stage(fts_ctx* ctx, size_t n, const uint8_t* const* rp_der, const size_t* rp_len,
