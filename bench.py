@@ -81,7 +81,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall-time bound of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    ap.add_argument("--workload", choices=["rp", "msm", "transfer", "mixed"], default="rp")
+    ap.add_argument("--workload", choices=["rp", "msm", "transfer", "mixed", "request"], default="rp")
     ap.add_argument("--msm-log", type=int, default=20, help="msm workload: log2 of the point count")
     ap.add_argument("--transfers", type=int, default=8192, help="transfer/mixed workloads: transfers per GPU per step")
     ap.add_argument("--action-inflight", type=int, default=3,
@@ -93,6 +93,8 @@ def main():
         return bench_transfer(args)
     if args.workload == "mixed":
         return bench_mixed(args)
+    if args.workload == "request":
+        return bench_transfer(args, raw_requests=True)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -232,7 +234,10 @@ def main():
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-            traffic = tj.get(dom + "@isolated", tj.get(dom, {})).get("fetch_bytes_corrected")
+            # HBM bytes per launch = corrected FETCH_SIZE + WRITE_SIZE of the isolated pass (PMC runs)
+            e = tj.get(dom + "@isolated", tj.get(dom, {}))
+            if e.get("fetch_bytes_corrected") is not None:
+                traffic = int(e["fetch_bytes_corrected"] + e.get("write_bytes", 0))
     except (OSError, ValueError, AttributeError):
         pass
     rd = kernel_roof(dom)
@@ -469,7 +474,11 @@ def bench_msm(args):
         dist.destroy_process_group()
 
 
-def bench_transfer(args):
+def bench_transfer(args, raw_requests=False):
+    """C4: 2-in/2-out transfers.  raw_requests: the same transfers, each wrapped in
+    its own serialized TokenRequest (1 transfer action, signatures attached) and
+    verified through fts_request_verify_batch -- protobuf decode, structural checks
+    and G1 JSON decoding included in the timed region"""
     world, rank, local, dist = _dist_setup()
     import random
     import numpy as np
@@ -493,10 +502,19 @@ def bench_transfer(args):
         base.append((ins, outs, pp.prove_transfer(T, inv, ib, outv, ob, 0xF7A50004 + i)))
     items = [base[i % distinct] for i in range(args.transfers)]
     nb = max(1, min(args.action_inflight, args.steps))
-    batches = [pp.prepare_transfers(items) for _ in range(nb)]
+    if raw_requests:
+        R = fts_gpu.request
+        reqs = []
+        for i, (ins, outs, proof) in enumerate(items):
+            ta = R.transfer_action([("%064x" % (i * 2 + k), k, b"owner-%d" % i, c) for k, c in enumerate(ins)],
+                                   [(b"recipient-%d" % i, c) for c in outs], proof)
+            reqs.append(R.token_request([(R.TRANSFER, ta)], [b"\x30" * 72, b"\x30" * 72]))
+        batches = [pp.prepare_requests(reqs) for _ in range(nb)]
+    else:
+        batches = [pp.prepare_transfers(items) for _ in range(nb)]
     setup_s = time.time() - t0
     for _ in range(max(1, args.warmup)):
-        st, fi = batches[0].verify()
+        st, fi = batches[0].verify()[0], None
     assert int((st != 0).sum()) == 0, "honest transfers rejected"
     _run_action_steps(batches, nb, None, None)
     if dist is not None:
@@ -507,16 +525,22 @@ def bench_transfer(args):
     elapsed = _max_over_ranks(dist, elapsed)
     kt = {k: (v[0] * args.steps, v[1]) for k, v in pp.last_timings_ex().items()}
     value = world * args.transfers * args.steps / elapsed
+    if raw_requests:
+        metric = "raw TokenRequest verifies/sec (1 transfer 2-in/2-out each, BN254, %d-bit range proofs)" % args.bits
+        unit, entry = "requests/s", "fts_request_verify_batch (protobuf + G1 JSON decode in the timed region)"
+    else:
+        metric = "2-in/2-out transfer verifies/sec (BN254, %d-bit range proofs)" % args.bits
+        unit, entry = "transfers/s", "fts_transfer_verify_batch"
     if rank == 0:
         print(json.dumps({
-            "metric": "2-in/2-out transfer verifies/sec (BN254, %d-bit range proofs)" % args.bits,
-            "value": round(value, 1), "unit": "transfers/s", "n_gpus": world, "steps": args.steps,
+            "metric": metric,
+            "value": round(value, 1), "unit": unit, "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32 (BN254 Fp/Fr 8x32-bit Montgomery)",
             "data": "synthetic: %d distinct 2-in/2-out transfers (type ABC) from the library's host prover, tiled"
                     % distinct,
             "config": {"workload": "C4 per GPU: %d transfers (TypeAndSum + 2 rp%d each) per step via "
-                                   "fts_transfer_verify_batch, %d calls in flight" % (args.transfers, args.bits, nb),
+                                   "%s, %d calls in flight" % (args.transfers, args.bits, entry, nb),
                        "transfers_per_gpu": args.transfers, "parallelism": "shard%d" % world},
             "roofline": _roofline_from(kt, args.steps),
             "kernel_ms": {k: round(v[0] / args.steps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),

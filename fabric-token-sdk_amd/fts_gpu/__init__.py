@@ -185,16 +185,11 @@ class PublicParams:
     def verify_requests(self, requests):
         """serialized TokenRequests -> (status, fail_action, fail_index) arrays
         (fts_request_verify_batch: every action's proofs in one device pass)"""
-        n = len(requests)
-        keep, ptrs, lens = _ptr_array(requests)
-        st = np.zeros(n, dtype=np.int32)
-        fa = np.zeros(n, dtype=np.int32)
-        fi = np.zeros(n, dtype=np.int32)
-        I32 = C.POINTER(C.c_int32)
-        L.check("fts_request_verify_batch", L.lib.fts_request_verify_batch(
-            self._ctx, n, ptrs, lens, st.ctypes.data_as(I32), fa.ctypes.data_as(I32), fi.ctypes.data_as(I32)))
-        del keep
-        return st, fa, fi
+        return self.prepare_requests(requests).verify()
+
+    def prepare_requests(self, requests):
+        """the request pointer / length arrays the C-ABI borrows, reusable across verify() calls"""
+        return RequestBatch(self, requests)
 
     def stage_range_proofs(self, proofs, commitments):
         return StagedRangeBatch(self, proofs, commitments)
@@ -332,6 +327,25 @@ class TransferBatch:
             self.pp._ctx, self.n, self.items, st.ctypes.data_as(C.POINTER(C.c_int32)),
             fi.ctypes.data_as(C.POINTER(C.c_int32))))
         return st, fi
+
+
+class RequestBatch:
+    """Serialized TokenRequests as the host hands them over (pointer + length per request)."""
+
+    def __init__(self, pp, requests):
+        self.pp = pp
+        self.n = len(requests)
+        self._keep, self.ptrs, self.lens = _ptr_array(requests)
+
+    def verify(self):
+        st = np.zeros(self.n, dtype=np.int32)
+        fa = np.zeros(self.n, dtype=np.int32)
+        fi = np.zeros(self.n, dtype=np.int32)
+        I32 = C.POINTER(C.c_int32)
+        L.check("fts_request_verify_batch", L.lib.fts_request_verify_batch(
+            self.pp._ctx, self.n, self.ptrs, self.lens, st.ctypes.data_as(I32), fa.ctypes.data_as(I32),
+            fi.ctypes.data_as(I32)))
+        return st, fa, fi
 
 
 class IssueBatch:

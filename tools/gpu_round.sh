@@ -4,7 +4,7 @@
 #   kernel-trace stats (CSV) -> PMC passes (one counter group per run).
 # Every GPU step has its own time limit; the first failure ends the script.
 # Env: STEPS (bench steps), TESTS=1 (run pytest -m gpu), PMC=0 (skip counters),
-#      TAG (suffix of the output directory names).
+#      EXTRA=0 (skip the action-level benches), TAG (suffix of the output directory names).
 set -o pipefail
 TAG=${TAG:-r01}
 OUT=gpurun_out
@@ -38,5 +38,12 @@ if [ "${PMC:-1}" = 1 ]; then
   step pmc_write 120 rocprofv3 --pmc WRITE_SIZE -T -f csv -d $OUT/pmc_write_$TAG -o run -- $PB
   step pmc_valu 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE -T -f csv -d $OUT/pmc_valu_$TAG -o run -- $PB
   python3 tools/pmc_summary.py $OUT $TAG $OUT/traffic_$TAG.json 2
+fi
+if [ "${EXTRA:-1}" = 1 ]; then
+  # action-level workloads: C4 transfers through the typed batch and as raw TokenRequests, C5 mixed
+  step bench_transfer 300 python3 -u bench.py --workload transfer --steps 96 --warmup 4
+  step bench_request 300 python3 -u bench.py --workload request --steps 96 --warmup 4
+  step bench_mixed 300 python3 -u bench.py --workload mixed --transfers 4096 --steps 48 --warmup 4
+  for w in transfer request mixed; do grep '^{' $OUT/bench_$w.log | tail -1 > $OUT/bench_$w.json; done
 fi
 echo "== done"
