@@ -147,6 +147,20 @@ struct Lane {
   }* pin = nullptr;
   int32_t* pin_status = nullptr;
   size_t pin_status_cap = 0;
+  // action batches: pinned staging of the assembled sigma / range-proof inputs
+  uint8_t* stage = nullptr;
+  size_t stage_cap = 0;
+  uint8_t* stage_buf(size_t bytes) {
+    if (bytes > stage_cap) {
+      if (stage) (void)hipHostFree(stage);
+      stage = nullptr;
+      const size_t want = std::max<size_t>(std::max(bytes, stage_cap + stage_cap / 2), 1 << 20);
+      stage_cap = 0;
+      if (hipHostMalloc((void**)&stage, want, 0) != hipSuccess) return nullptr;
+      stage_cap = want;
+    }
+    return stage;
+  }
   int32_t* status_buf(size_t n) {
     if (n > pin_status_cap) {
       if (pin_status) (void)hipHostFree(pin_status);
@@ -160,9 +174,12 @@ struct Lane {
   void free_pinned() {
     if (pin) (void)hipHostFree(pin);
     if (pin_status) (void)hipHostFree(pin_status);
+    if (stage) (void)hipHostFree(stage);
     pin = nullptr;
     pin_status = nullptr;
     pin_status_cap = 0;
+    stage = nullptr;
+    stage_cap = 0;
   }
 };
 // host worker threads for batch parsing: the CPUs this process may actually
@@ -180,6 +197,23 @@ static unsigned host_threads() {
     return std::min(16u, hw);
   }();
   return n;
+}
+
+// run f(i) for i in [0, n) on up to host_threads() threads (inline when small)
+template <class F>
+static void parallel_for(size_t n, size_t min_parallel, F&& f) {
+  const unsigned nth = n >= min_parallel ? host_threads() : 1u;
+  if (nth <= 1) {
+    for (size_t i = 0; i < n; i++) f(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nth; t++)
+    th.emplace_back([&]() {
+      for (size_t i; (i = next++) < n;) f(i);
+    });
+  for (auto& t : th) t.join();
 }
 
 static inline double now_ms() {
@@ -1250,16 +1284,16 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
   }
   const double t_parse1 = now_ms();
   L.host_parse_ms = (float)(t_parse1 - t_parse0);
-  // ---- assemble device batches
+  // ---- assemble device batches: offsets on one thread (integer sums), then a
+  // parallel fill of the lane's pinned staging buffer and async uploads from it
+  struct Off {
+    int sig = -1;               // index in the device sigma batch
+    size_t scw = 0;             // word offset in s_sc
+  };
+  std::vector<Off> off(A);
   std::vector<SigAction> sact;
-  std::vector<int32_t> s_owner, s_affoff, s_status;
-  std::vector<uint8_t> s_raw;
-  std::vector<uint32_t> s_sc;
-  std::vector<int2> s_work;
-  std::vector<uint8_t> r_raw;
-  std::vector<uint32_t> r_sc;
-  std::vector<int32_t> r_status, r_ipa;
   int term_off = 0, aff_off = 0, pt_off = 0, sc_off = 0, rp_total = 0;
+  size_t scw_total = 0;
   uint32_t msg_off = 0;
   std::vector<int> sig_of(A, -1);
   for (size_t i = 0; i < A; i++) {
@@ -1270,10 +1304,6 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
     if (s.rc_applicable && s.rp_count > 0) {
       s.rp_base = rp_total;
       rp_total += s.rp_count;
-      r_raw.insert(r_raw.end(), p.rp_raw.begin(), p.rp_raw.end());
-      r_sc.insert(r_sc.end(), p.rp_sc.begin(), p.rp_sc.end());
-      r_status.insert(r_status.end(), p.rp_status.begin(), p.rp_status.end());
-      r_ipa.insert(r_ipa.end(), p.rp_ipa.begin(), p.rp_ipa.end());
     }
     SigAction sa{};
     sa.kind = ai.kind;
@@ -1286,55 +1316,94 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
     sa.rp_base = s.rp_base;
     sa.rp_count = s.rp_count;
     sa.chal_canonical = p.chal_canonical;
-    const int npt = 1 + sa.n_in + sa.n_out;
-    s_raw.insert(s_raw.end(), p.sig_raw.begin(), p.sig_raw.begin() + npt * 64);
-    for (int q = 0; q < npt; q++) s_owner.push_back((int32_t)sact.size());
-    s_sc.insert(s_sc.end(), p.sig_sc.begin(), p.sig_sc.end());
-    const int nt = sig_nterms(sa.kind, sa.n_in);
-    for (int t = 0; t < nt; t++) s_work.push_back(make_int2((int)sact.size(), t));
-    s_affoff.push_back(aff_off);
-    s_status.push_back(0);
-    pt_off += npt;
+    off[i].sig = (int)sact.size();
+    off[i].scw = scw_total;
+    scw_total += p.sig_sc.size();
+    pt_off += 1 + sa.n_in + sa.n_out;
     sc_off += sig_nscalars(sa.kind, sa.n_in);
-    term_off += nt;
+    term_off += sig_nterms(sa.kind, sa.n_in);
     aff_off += sig_naff(sa.kind, sa.n_in, sa.n_out);
     msg_off += sig_msg_slot(sa.kind, sa.n_in, sa.n_out);
     sig_of[i] = (int)sact.size();
     sact.push_back(sa);
   }
   const int SA = (int)sact.size();
+  const size_t nwork = (size_t)term_off;
+  // staging layout (256-byte aligned regions)
+  size_t o = 0;
+  auto region = [&](size_t bytes) {
+    size_t r = o;
+    o += (bytes + 255) & ~size_t(255);
+    return r;
+  };
+  const size_t o_act = region((size_t)SA * sizeof(SigAction)), o_raw = region((size_t)pt_off * 64),
+               o_owner = region((size_t)pt_off * 4), o_sc = region(scw_total * 4),
+               o_work = region(nwork * sizeof(int2)), o_affoff = region((size_t)SA * 4),
+               o_rraw = region((size_t)rp_total * npts_rp * 64), o_rsc = region((size_t)rp_total * RP_NSC * 8 * 4),
+               o_rst = region((size_t)rp_total * 4), o_ripa = region((size_t)rp_total * 4);
+  uint8_t* hs = L.stage_buf(std::max<size_t>(o, 1));
+  if (!hs) return FTS_API_ENOMEM;
+  if (SA) memcpy(hs + o_act, sact.data(), (size_t)SA * sizeof(SigAction));
+  parallel_for(A, 64, [&](size_t i) {
+    if (sig_of[i] < 0) return;
+    const SigAction& sa = sact[sig_of[i]];
+    const Parsed& p = P[i];
+    const ActionState& s = st[i];
+    const int npt = 1 + sa.n_in + sa.n_out, g = sig_of[i];
+    memcpy(hs + o_raw + (size_t)sa.pt_off * 64, p.sig_raw.data(), (size_t)npt * 64);
+    int32_t* own = (int32_t*)(hs + o_owner) + sa.pt_off;
+    for (int q = 0; q < npt; q++) own[q] = g;
+    if (!p.sig_sc.empty()) memcpy(hs + o_sc + off[i].scw * 4, p.sig_sc.data(), p.sig_sc.size() * 4);
+    int2* wk = (int2*)(hs + o_work) + sa.term_off;
+    for (int t = 0, nt = sig_nterms(sa.kind, sa.n_in); t < nt; t++) wk[t] = make_int2(g, t);
+    ((int32_t*)(hs + o_affoff))[g] = 0;
+    if (s.rp_base >= 0) {
+      const size_t rb = (size_t)s.rp_base, rc = (size_t)s.rp_count;
+      memcpy(hs + o_rraw + rb * npts_rp * 64, p.rp_raw.data(), rc * npts_rp * 64);
+      memcpy(hs + o_rsc + rb * RP_NSC * 8 * 4, p.rp_sc.data(), rc * RP_NSC * 8 * 4);
+      memcpy(hs + o_rst + rb * 4, p.rp_status.data(), rc * 4);
+      memcpy(hs + o_ripa + rb * 4, p.rp_ipa.data(), rc * 4);
+    }
+  });
+  {  // affine-table offsets: prefix sum in sigma-batch order
+    int32_t* ao = (int32_t*)(hs + o_affoff);
+    int acc = 0;
+    for (int g = 0; g < SA; g++) {
+      ao[g] = acc;
+      acc += sig_naff(sact[g].kind, sact[g].n_in, sact[g].n_out);
+    }
+  }
   Workspace& w = L.ws;
   if (SA) {
-    if (w.s_act.ensure(SA * sizeof(SigAction)) || w.s_raw.ensure(s_raw.size()) || w.s_owner.ensure(s_owner.size() * 4) ||
-        w.s_pts.ensure((size_t)pt_off * 64) || w.s_sc.ensure(std::max<size_t>(s_sc.size(), 1) * 4) ||
-        w.s_status.ensure(SA * 4) || w.s_work.ensure(s_work.size() * sizeof(int2)) ||
-        w.s_terms.ensure((size_t)term_off * 96) || w.s_aff.ensure((size_t)aff_off * 64) ||
-        w.s_affoff.ensure(SA * 4) || w.s_msgs.ensure(msg_off) || w.s_jac.ensure((size_t)aff_off * 96) ||
-        w.s_scratch.ensure(sig_scratch_words(s_work.size()) * 4))
+    if (w.s_act.ensure(SA * sizeof(SigAction)) || w.s_raw.ensure((size_t)pt_off * 64) ||
+        w.s_owner.ensure((size_t)pt_off * 4) || w.s_pts.ensure((size_t)pt_off * 64) ||
+        w.s_sc.ensure(std::max<size_t>(scw_total, 1) * 4) || w.s_status.ensure(SA * 4) ||
+        w.s_work.ensure(nwork * sizeof(int2)) || w.s_terms.ensure((size_t)term_off * 96) ||
+        w.s_aff.ensure((size_t)aff_off * 64) || w.s_affoff.ensure(SA * 4) || w.s_msgs.ensure(msg_off) ||
+        w.s_jac.ensure((size_t)aff_off * 96) || w.s_scratch.ensure(sig_scratch_words(nwork) * 4))
       return FTS_API_ENOMEM;
-    HIP_OK(hipMemcpyAsync(w.s_act.p, sact.data(), SA * sizeof(SigAction), hipMemcpyHostToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(w.s_raw.p, s_raw.data(), s_raw.size(), hipMemcpyHostToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(w.s_owner.p, s_owner.data(), s_owner.size() * 4, hipMemcpyHostToDevice, L.s));
-    if (!s_sc.empty())
-      HIP_OK(hipMemcpyAsync(w.s_sc.p, s_sc.data(), s_sc.size() * 4, hipMemcpyHostToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(w.s_status.p, s_status.data(), SA * 4, hipMemcpyHostToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(w.s_work.p, s_work.data(), s_work.size() * sizeof(int2), hipMemcpyHostToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(w.s_affoff.p, s_affoff.data(), SA * 4, hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.s_act.p, hs + o_act, SA * sizeof(SigAction), hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.s_raw.p, hs + o_raw, (size_t)pt_off * 64, hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.s_owner.p, hs + o_owner, (size_t)pt_off * 4, hipMemcpyHostToDevice, L.s));
+    if (scw_total) HIP_OK(hipMemcpyAsync(w.s_sc.p, hs + o_sc, scw_total * 4, hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemsetAsync(w.s_status.p, 0, SA * 4, L.s));
+    HIP_OK(hipMemcpyAsync(w.s_work.p, hs + o_work, nwork * sizeof(int2), hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.s_affoff.p, hs + o_affoff, SA * 4, hipMemcpyHostToDevice, L.s));
   }
   if (rp_total) {
-    if (w.rp_raw.ensure(r_raw.size()) || w.rp_sc.ensure(r_sc.size() * 4) || w.rp_status.ensure(rp_total * 4) ||
-        w.rp_ipa.ensure(rp_total * 4))
+    if (w.rp_raw.ensure((size_t)rp_total * npts_rp * 64) || w.rp_sc.ensure((size_t)rp_total * RP_NSC * 8 * 4) ||
+        w.rp_status.ensure(rp_total * 4) || w.rp_ipa.ensure(rp_total * 4))
       return FTS_API_ENOMEM;
-    HIP_OK(hipMemcpyAsync(w.rp_raw.p, r_raw.data(), r_raw.size(), hipMemcpyHostToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(w.rp_sc.p, r_sc.data(), r_sc.size() * 4, hipMemcpyHostToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(w.rp_status.p, r_status.data(), rp_total * 4, hipMemcpyHostToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(w.rp_ipa.p, r_ipa.data(), rp_total * 4, hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.rp_raw.p, hs + o_rraw, (size_t)rp_total * npts_rp * 64, hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.rp_sc.p, hs + o_rsc, (size_t)rp_total * RP_NSC * 8 * 4, hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.rp_status.p, hs + o_rst, rp_total * 4, hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(w.rp_ipa.p, hs + o_ripa, rp_total * 4, hipMemcpyHostToDevice, L.s));
   }
   SigBatchDev sd{};
   if (SA) {
     sd.A = SA;
     sd.npts = pt_off;
-    sd.nwork = (int)s_work.size();
+    sd.nwork = (int)nwork;
     sd.act = w.s_act.as<SigAction>();
     sd.raw = w.s_raw.as<uint8_t>();
     sd.pt_owner = w.s_owner.as<int32_t>();
@@ -1503,8 +1572,7 @@ int fts_request_verify_batch(fts_ctx* c, size_t n, const uint8_t* const* req, co
     for (size_t j = 0; j < R[i].acts.size(); j++) {
       const rq::Action& a = R[i].acts[j];
       if (a.pre >= 0) break;
-      acts.push_back(ActionIn{a.kind, (const uint8_t*)a.in.data(), a.n_in, (const uint8_t*)a.out.data(), a.n_out,
-                              der::Span{(const uint8_t*)a.proof.data(), a.proof.size()}});
+      acts.push_back(ActionIn{a.kind, R[i].in(a), a.n_in, R[i].out(a), a.n_out, der::Span{a.proof, a.proof_len}});
       owner.emplace_back((uint32_t)i, (uint32_t)j);
     }
   }

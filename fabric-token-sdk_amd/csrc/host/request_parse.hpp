@@ -27,6 +27,8 @@
 // callable without a device (fts_request_inspect).
 #pragma once
 #include <stdint.h>
+#include <string.h>
+#include <deque>
 #include <string>
 #include <vector>
 #include "../../../include/fts_gpu.h"
@@ -43,9 +45,10 @@ struct Field {
   size_t n;
 };
 
-// one protobuf message -> its fields in wire order (protobuf-go's decoder errors)
-inline bool fields(const uint8_t* b, size_t len, std::vector<Field>& out) {
-  out.clear();
+// Walk one protobuf message field by field (protobuf-go's decoder errors):
+// fn(const Field&) -> bool; false from fn or a wire error ends the walk with false.
+template <class Fn>
+inline bool each(const uint8_t* b, size_t len, Fn&& fn) {
   size_t i = 0;
   while (i < len) {
     uint64_t key;
@@ -70,7 +73,7 @@ inline bool fields(const uint8_t* b, size_t len, std::vector<Field>& out) {
     } else {
       return false;  // groups (3/4) and reserved wire types
     }
-    out.push_back(f);
+    if (!fn(f)) return false;
   }
   return true;
 }
@@ -101,8 +104,9 @@ inline bool utf8_valid(const uint8_t* s, size_t n) {
   return true;
 }
 
-// A singular sub-message: every occurrence of field `no` with wire type 2,
-// merged (protobuf-go MergeFrom == parsing the concatenation).
+// A singular sub-message: every occurrence (wire type 2) merged -- protobuf-go
+// MergeFrom == parsing the concatenation; the bytes are copied only when the
+// field occurs more than once.
 struct Sub {
   Sub() = default;
   Sub(const Sub&) = delete;  // p may point into merged
@@ -133,10 +137,43 @@ struct Bytes {
 
 // message with `bytes raw = 1` (G1, Zr, Identity, Signature, Proof{proof=1})
 inline bool raw_field(const uint8_t* b, size_t n, Bytes& raw) {
-  std::vector<Field> f;
-  if (!fields(b, n, f)) return false;
-  for (auto& x : f)
+  return each(b, n, [&](const Field& x) {
     if (x.no == 1 && x.wt == 2) raw.set(x);
+    return true;
+  });
+}
+
+// mathlib's own encoding of a G1 (json.Marshal of {Curve, Element []byte}):
+// {"curve":1,"element":"<88 base64 chars>"} -- decoded without allocations;
+// any other spelling goes through the general JSON path below.
+inline bool g1_json_fast(const uint8_t* s, size_t n, uint8_t out[64], bool& ok) {
+  static const char pre[] = "{\"curve\":1,\"element\":\"";
+  const size_t lp = sizeof(pre) - 1;
+  if (n != lp + 88 + 2 || memcmp(s, pre, lp) || s[n - 2] != '"' || s[n - 1] != '}') return false;
+  static const struct T {
+    int8_t v[256];
+    T() {
+      for (int i = 0; i < 256; i++) v[i] = -1;
+      const char* a = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+      for (int i = 0; i < 64; i++) v[(uint8_t)a[i]] = (int8_t)i;
+    }
+  } t;
+  const uint8_t* e = s + lp;
+  if (e[86] != '=' || e[87] != '=') return false;
+  uint32_t acc = 0;
+  int bits = 0, o = 0;
+  for (int i = 0; i < 86; i++) {
+    int v = t.v[e[i]];
+    if (v < 0) return false;  // general path decides
+    acc = (acc << 6) | (uint32_t)v;
+    bits += 6;
+    if (bits >= 8) {
+      bits -= 8;
+      out[o++] = (uint8_t)(acc >> bits);
+    }
+  }
+  G1A a;
+  ok = o == 64 && g1_from_bytes(out, 64, a);
   return true;
 }
 
@@ -148,6 +185,8 @@ inline bool g1_field(const Sub& g, bool& has, uint8_t out[64]) {
   Bytes raw;
   if (!raw_field(g.p, g.n, raw)) return false;
   if (!raw.n) return true;
+  bool ok;
+  if (g1_json_fast(raw.p, raw.n, out, ok)) return has = ok;
   std::string js((const char*)raw.p, raw.n), el, bin;
   long long curve = -1;
   if (!json_int_field(js, "curve", curve) || curve != 1) return false;
@@ -175,31 +214,26 @@ inline bool zr_field(const Sub& z) {
 inline bool token_id_ok(const Sub& id, bool& txid_nonempty) {
   txid_nonempty = false;
   if (!id.present) return true;
-  std::vector<Field> f;
-  if (!fields(id.p, id.n, f)) return false;
   Bytes s;
-  for (auto& x : f)
-    if (x.no == 1 && x.wt == 2) {
-      if (!utf8_valid(x.p, x.n)) return false;
-      s.set(x);
-    }
+  if (!each(id.p, id.n, [&](const Field& x) {
+        if (x.no == 1 && x.wt == 2) {
+          if (!utf8_valid(x.p, x.n)) return false;
+          s.set(x);
+        }
+        return true;
+      }))
+    return false;
   txid_nonempty = s.n > 0;
   return true;
 }
 inline bool map_entry_ok(const Field& e) {  // map<string, bytes>: key = 1
-  std::vector<Field> f;
-  if (!fields(e.p, e.n, f)) return false;
-  for (auto& x : f)
-    if (x.no == 1 && x.wt == 2 && !utf8_valid(x.p, x.n)) return false;
-  return true;
+  return each(e.p, e.n, [](const Field& x) { return !(x.no == 1 && x.wt == 2 && !utf8_valid(x.p, x.n)); });
 }
 inline bool fabtoken_ok(const Sub& t) {  // fabtoken.Token{owner=1 bytes, type=2 string, quantity=3 string}
   if (!t.present) return true;
-  std::vector<Field> f;
-  if (!fields(t.p, t.n, f)) return false;
-  for (auto& x : f)
-    if ((x.no == 2 || x.no == 3) && x.wt == 2 && !utf8_valid(x.p, x.n)) return false;
-  return true;
+  return each(t.p, t.n, [](const Field& x) {
+    return !((x.no == 2 || x.no == 3) && x.wt == 2 && !utf8_valid(x.p, x.n));
+  });
 }
 
 // nogh.Token{owner=1, data=2}
@@ -209,18 +243,20 @@ struct Tok {
   uint8_t data[64];
 };
 inline bool token_msg(const Sub& s, Tok& t) {
-  t = Tok{};
+  t.present = t.has_data = false;
+  t.owner_len = 0;
   if (!s.present) return true;
   t.present = true;
-  std::vector<Field> f;
-  if (!fields(s.p, s.n, f)) return false;
   Bytes owner;
   Sub data;
-  for (auto& x : f) {
-    if (x.wt != 2) continue;
-    if (x.no == 1) owner.set(x);
-    else if (x.no == 2) data.add(x);
-  }
+  if (!each(s.p, s.n, [&](const Field& x) {
+        if (x.wt == 2) {
+          if (x.no == 1) owner.set(x);
+          else if (x.no == 2) data.add(x);
+        }
+        return true;
+      }))
+    return false;
   t.owner_len = owner.n;
   return g1_field(data, t.has_data, t.data);
 }
@@ -232,134 +268,156 @@ struct Action {
   int kind = 0;                 // SIG_TAS (transfer) / SIG_ST (issue) numbering of the caller
   int index = -1;               // position in TokenRequest.actions
   bool transfer = false;
-  std::string in, out;          // input / output commitments, 64-byte raw points
-  size_t n_in = 0, n_out = 0;
-  std::string proof;            // Proof.proof bytes (owned: a merged Proof message is a temporary)
+  uint32_t in_off = 0, out_off = 0;  // byte offsets of the commitments in Request::pts
+  uint32_t n_in = 0, n_out = 0;
+  const uint8_t* proof = nullptr;    // Proof.proof: into the caller's request bytes, or Request::owned
+  size_t proof_len = 0;
   int32_t pre = -1;             // verdict decided before the ZK proof (FTS_E_ACTION_INVALID / FTS_E_MALFORMED)
 };
 
 struct Request {
-  int32_t status = FTS_OK;      // request-level verdict (FTS_E_MALFORMED) when fail_action < 0 or deserialisation
+  int32_t status = FTS_OK;      // request-level verdict (FTS_E_MALFORMED) when deserialisation fails
   int32_t fail_action = -1;
   bool deser_failed = false;
   std::vector<Action> acts;     // issues (request order), then transfers (request order)
+  std::string pts;              // 64-byte raw commitments of every action (inputs, then outputs)
+  std::deque<std::string> owned;  // proof bytes of merged Proof messages (stable addresses)
+  void reset() {
+    status = FTS_OK, fail_action = -1, deser_failed = false;
+    acts.clear(), pts.clear(), owned.clear();
+  }
+  const uint8_t* in(const Action& a) const { return (const uint8_t*)pts.data() + a.in_off; }
+  const uint8_t* out(const Action& a) const { return (const uint8_t*)pts.data() + a.out_off; }
 };
 
-// transfer Action.Deserialize + Validate (transfer/action.go:326-362, 244-283)
-inline bool transfer_action(const uint8_t* b, size_t n, Action& a) {
-  std::vector<Field> f;
-  if (!fields(b, n, f)) return false;
+// Proof{proof = 1}: the last proof bytes of the (merged) message
+inline bool proof_msg(const Sub& proof, Request& r, Action& a) {
+  if (!proof.present) return true;
+  Bytes pb;
+  if (!raw_field(proof.p, proof.n, pb)) return false;
+  if (proof.count > 1 && pb.n) {  // points into the Sub's temporary merge buffer
+    r.owned.emplace_back((const char*)pb.p, pb.n);
+    pb.p = (const uint8_t*)r.owned.back().data();
+  }
+  a.proof = pb.p, a.proof_len = pb.n;
+  return true;
+}
+
+// transfer Action.Deserialize + Validate (transfer/action.go:326-362, 244-283).
+// Inputs are written to r.pts first, outputs after (two walks of the message).
+inline bool transfer_action(const uint8_t* b, size_t n, Request& r, Action& a) {
   Sub proof;
   bool invalid = false;
-  for (auto& x : f) {
-    if (x.wt != 2) continue;
-    if (x.no == 1) {  // TransferActionInput
-      std::vector<Field> g;
-      if (!fields(x.p, x.n, g)) return false;
-      Sub id, input, wit;
-      for (auto& y : g) {
-        if (y.wt != 2) continue;
-        if (y.no == 1) id.add(y);
-        else if (y.no == 2) input.add(y);
-        else if (y.no == 3) wit.add(y);
-      }
-      bool txid;
-      if (!token_id_ok(id, txid)) return false;
-      Tok t;
-      if (!token_msg(input, t)) return false;
-      if (wit.present) {  // FromZrProto on the blinding factor; fabtoken strings
-        std::vector<Field> w;
-        if (!fields(wit.p, wit.n, w)) return false;
-        Sub out, bf;
-        for (auto& y : w) {
-          if (y.wt != 2) continue;
-          if (y.no == 1) out.add(y);
-          else if (y.no == 2) bf.add(y);
+  a.in_off = (uint32_t)r.pts.size();
+  Tok t;
+  if (!each(b, n, [&](const Field& x) {
+        if (x.wt != 2) return true;
+        if (x.no == 1) {  // TransferActionInput
+          Sub id, input, wit;
+          if (!each(x.p, x.n, [&](const Field& y) {
+                if (y.wt == 2) {
+                  if (y.no == 1) id.add(y);
+                  else if (y.no == 2) input.add(y);
+                  else if (y.no == 3) wit.add(y);
+                }
+                return true;
+              }))
+            return false;
+          bool txid;
+          if (!token_id_ok(id, txid) || !token_msg(input, t)) return false;
+          if (wit.present) {  // FromZrProto on the blinding factor; fabtoken strings
+            Sub out, bf;
+            if (!each(wit.p, wit.n, [&](const Field& y) {
+                  if (y.wt == 2) {
+                    if (y.no == 1) out.add(y);
+                    else if (y.no == 2) bf.add(y);
+                  }
+                  return true;
+                }))
+              return false;
+            if (!fabtoken_ok(out) || !zr_field(bf)) return false;
+          }
+          // Validate: ID set, tx id non-empty, token set, owner non-empty, data set (:248-263)
+          if (!id.present || !txid || !t.present || !t.owner_len || !t.has_data) invalid = true;
+          r.pts.append((const char*)(t.has_data ? t.data : kZero64), 64);
+          a.n_in++;
+        } else if (x.no == 3) {
+          proof.add(x);
+        } else if (x.no == 4) {
+          return map_entry_ok(x);
         }
-        if (!fabtoken_ok(out) || !zr_field(bf)) return false;
-      }
-      // Validate: ID set, tx id non-empty, token set, owner non-empty, data set (:248-263)
-      if (!id.present || !txid || !t.present || !t.owner_len || !t.has_data) invalid = true;
-      a.in.append((const char*)(t.has_data ? t.data : kZero64), 64);
-      a.n_in++;
-    } else if (x.no == 2) {  // TransferActionOutput{token=1}
-      std::vector<Field> g;
-      if (!fields(x.p, x.n, g)) return false;
-      Sub tok;
-      for (auto& y : g)
-        if (y.no == 1 && y.wt == 2) tok.add(y);
-      Tok t;
-      if (!token_msg(tok, t)) return false;
-      if (!t.present || !t.has_data) invalid = true;  // nil output / Token.Validate(false) (:274-280)
-      a.out.append((const char*)(t.has_data ? t.data : kZero64), 64);
-      a.n_out++;
-    } else if (x.no == 3) {
-      proof.add(x);
-    } else if (x.no == 4) {
-      if (!map_entry_ok(x)) return false;
-    }
-  }
-  if (proof.present) {
-    Bytes pb;
-    std::vector<Field> g;
-    if (!fields(proof.p, proof.n, g)) return false;
-    for (auto& y : g)
-      if (y.no == 1 && y.wt == 2) pb.set(y);
-    a.proof.assign((const char*)pb.p, pb.n);
-  }
+        return true;
+      }))
+    return false;
+  a.out_off = (uint32_t)r.pts.size();
+  if (!each(b, n, [&](const Field& x) {
+        if (x.wt != 2 || x.no != 2) return true;  // TransferActionOutput{token=1}
+        Sub tok;
+        if (!each(x.p, x.n, [&](const Field& y) {
+              if (y.no == 1 && y.wt == 2) tok.add(y);
+              return true;
+            }))
+          return false;
+        if (!token_msg(tok, t)) return false;
+        if (!t.present || !t.has_data) invalid = true;  // nil output / Token.Validate(false) (:274-280)
+        r.pts.append((const char*)(t.has_data ? t.data : kZero64), 64);
+        a.n_out++;
+        return true;
+      }))
+    return false;
+  if (!proof_msg(proof, r, a)) return false;
   if (a.n_in == 0 || a.n_out == 0) invalid = true;  // (:245-247, :271-273)
   if (invalid) a.pre = FTS_E_ACTION_INVALID;
   return true;
 }
 
 // issue Action.Deserialize + Validate + GetCommitments (issue/action.go:231-270, 161-185, 273-282)
-inline bool issue_action(const uint8_t* b, size_t n, Action& a) {
-  std::vector<Field> f;
-  if (!fields(b, n, f)) return false;
+inline bool issue_action(const uint8_t* b, size_t n, Request& r, Action& a) {
   Sub issuer, proof;
   bool invalid = false, nil_data = false;
-  for (auto& x : f) {
-    if (x.wt != 2) continue;
-    if (x.no == 1) {
-      issuer.add(x);
-    } else if (x.no == 2) {  // IssueActionInput{id=1 TokenID, token=2 bytes}
-      std::vector<Field> g;
-      if (!fields(x.p, x.n, g)) return false;
-      Sub id;
-      Bytes tok;
-      for (auto& y : g) {
-        if (y.wt != 2) continue;
-        if (y.no == 1) id.add(y);
-        else if (y.no == 2) tok.set(y);
-      }
-      bool txid;
-      if (!token_id_ok(id, txid)) return false;
-      if (!tok.n || !txid) invalid = true;  // (:169-174)
-    } else if (x.no == 3) {  // IssueActionOutput{token=1}
-      std::vector<Field> g;
-      if (!fields(x.p, x.n, g)) return false;
-      Sub tok;
-      for (auto& y : g)
-        if (y.no == 1 && y.wt == 2) tok.add(y);
-      Tok t;
-      if (!token_msg(tok, t)) return false;
-      if (!t.present) invalid = true;  // nil output (:179-183)
-      else if (!t.has_data) nil_data = true;
-      a.out.append((const char*)(t.has_data ? t.data : kZero64), 64);
-      a.n_out++;
-    } else if (x.no == 4) {
-      proof.add(x);
-    } else if (x.no == 5) {
-      if (!map_entry_ok(x)) return false;
-    }
-  }
+  a.in_off = a.out_off = (uint32_t)r.pts.size();
+  Tok t;
+  if (!each(b, n, [&](const Field& x) {
+        if (x.wt != 2) return true;
+        if (x.no == 1) {
+          issuer.add(x);
+        } else if (x.no == 2) {  // IssueActionInput{id=1 TokenID, token=2 bytes}
+          Sub id;
+          Bytes tok;
+          if (!each(x.p, x.n, [&](const Field& y) {
+                if (y.wt == 2) {
+                  if (y.no == 1) id.add(y);
+                  else if (y.no == 2) tok.set(y);
+                }
+                return true;
+              }))
+            return false;
+          bool txid;
+          if (!token_id_ok(id, txid)) return false;
+          if (!tok.n || !txid) invalid = true;  // (:169-174)
+        } else if (x.no == 3) {  // IssueActionOutput{token=1}
+          Sub tok;
+          if (!each(x.p, x.n, [&](const Field& y) {
+                if (y.no == 1 && y.wt == 2) tok.add(y);
+                return true;
+              }))
+            return false;
+          if (!token_msg(tok, t)) return false;
+          if (!t.present) invalid = true;  // nil output (:179-183)
+          else if (!t.has_data) nil_data = true;
+          r.pts.append((const char*)(t.has_data ? t.data : kZero64), 64);
+          a.n_out++;
+        } else if (x.no == 4) {
+          proof.add(x);
+        } else if (x.no == 5) {
+          return map_entry_ok(x);
+        }
+        return true;
+      }))
+    return false;
   Bytes iraw;
   if (issuer.present && !raw_field(issuer.p, issuer.n, iraw)) return false;
-  if (proof.present) {
-    Bytes pb;
-    if (!raw_field(proof.p, proof.n, pb)) return false;
-    a.proof.assign((const char*)pb.p, pb.n);
-  }
+  if (!proof_msg(proof, r, a)) return false;
   if (!iraw.n || a.n_out == 0) invalid = true;  // issuer not set (:162-164), no outputs (:176-178)
   if (invalid) a.pre = FTS_E_ACTION_INVALID;
   // a nil commitment reaches the verifier, which dereferences it (issue/verifier.go): a panic
@@ -368,11 +426,11 @@ inline bool issue_action(const uint8_t* b, size_t n, Action& a) {
 }
 
 // TokenRequest.FromBytes + DeserializeActions + the per-action structural checks.
-// The returned Request either carries a final verdict (status != FTS_OK, e.g.
-// MALFORMED with the failing action's index), or the action list whose ZK
-// proofs decide the verdict (first failing action in acts order).
+// The returned Request either carries a final verdict (deser_failed: MALFORMED,
+// with the failing action's index when one is to blame), or the action list
+// whose structural verdicts and ZK proofs decide (first failing action in acts order).
 inline void parse_request(const uint8_t* b, size_t n, int kind_transfer, int kind_issue, Request& r) {
-  r = Request{};
+  r.reset();
   auto fail = [&](int32_t st, int32_t idx) {
     r.status = st;
     r.fail_action = idx;
@@ -380,53 +438,69 @@ inline void parse_request(const uint8_t* b, size_t n, int kind_transfer, int kin
     r.acts.clear();
   };
   if (n == 0) return fail(FTS_E_MALFORMED, -1);  // "empty token request" (validator.go:79-81)
-  std::vector<Field> f;
-  if (!fields(b, n, f)) return fail(FTS_E_MALFORMED, -1);
   struct Raw {
     int index;
     bool transfer;
     const uint8_t* p;
     size_t n;
   };
-  std::vector<Raw> issues, transfers;
+  Raw stack_raw[8];
+  std::vector<Raw> heap_raw;
+  int n_act = 0, n_iss = 0;
   // proto.Unmarshal of the request (Action / Signature messages included) fails first ...
-  int idx = 0, unknown = -1;
+  int unknown = -1;
   bool nil_sig = false;
-  for (auto& x : f) {
-    if (x.wt != 2) continue;
+  bool wire_ok = each(b, n, [&](const Field& x) {
+    if (x.wt != 2) return true;
     if (x.no == 2) {  // Action{type=1 enum, raw=2 bytes}
-      std::vector<Field> g;
-      if (!fields(x.p, x.n, g)) return fail(FTS_E_MALFORMED, -1);
       int32_t type = 0;
       Bytes raw;
-      for (auto& y : g) {
-        if (y.no == 1 && y.wt == 0) type = (int32_t)(uint32_t)y.v;
-        else if (y.no == 2 && y.wt == 2) raw.set(y);
+      if (!each(x.p, x.n, [&](const Field& y) {
+            if (y.no == 1 && y.wt == 0) type = (int32_t)(uint32_t)y.v;
+            else if (y.no == 2 && y.wt == 2) raw.set(y);
+            return true;
+          }))
+        return false;
+      if (type == 0 || type == 1) {
+        Raw w{n_act, type == 1, raw.p, raw.n};
+        n_iss += type == 0;
+        if (heap_raw.empty() && n_act < 8) {
+          stack_raw[n_act] = w;
+        } else {
+          if (heap_raw.empty()) heap_raw.assign(stack_raw, stack_raw + n_act);
+          heap_raw.push_back(w);
+        }
+      } else if (unknown < 0) {
+        unknown = n_act;
       }
-      if (type == 0) issues.push_back(Raw{idx, false, raw.p, raw.n});
-      else if (type == 1) transfers.push_back(Raw{idx, true, raw.p, raw.n});
-      else if (unknown < 0) unknown = idx;
-      idx++;
+      n_act++;
     } else if (x.no == 3 || x.no == 4) {  // Signature{raw=1}
       Bytes raw;
-      if (!raw_field(x.p, x.n, raw)) return fail(FTS_E_MALFORMED, -1);
+      if (!raw_field(x.p, x.n, raw)) return false;
       nil_sig |= !raw.n;
     }
-  }
+    return true;
+  });
+  if (!wire_ok) return fail(FTS_E_MALFORMED, -1);
   // ... then FromProtos: unknown action type (request.go:73-80), nil / empty signature (:82-93)
   if (unknown >= 0) return fail(FTS_E_MALFORMED, unknown);
   if (nil_sig) return fail(FTS_E_MALFORMED, -1);
-  r.acts.reserve(issues.size() + transfers.size());
-  for (int pass = 0; pass < 2; pass++)
-    for (const Raw& w : pass == 0 ? issues : transfers) {
-      Action a;
+  const Raw* raws = heap_raw.empty() ? stack_raw : heap_raw.data();
+  const int n_known = heap_raw.empty() ? n_act : (int)heap_raw.size();
+  r.acts.reserve(n_known);
+  for (int pass = 0; pass < 2; pass++)  // every issue, then every transfer
+    for (int k = 0; k < n_known; k++) {
+      const Raw& w = raws[k];
+      if (w.transfer != (pass == 1)) continue;
+      r.acts.emplace_back();
+      Action& a = r.acts.back();
       a.index = w.index;
       a.transfer = w.transfer;
       a.kind = w.transfer ? kind_transfer : kind_issue;
-      bool ok = w.transfer ? transfer_action(w.p, w.n, a) : issue_action(w.p, w.n, a);
+      bool ok = w.transfer ? transfer_action(w.p, w.n, r, a) : issue_action(w.p, w.n, r, a);
       if (!ok) return fail(FTS_E_MALFORMED, w.index);  // "failed to unmarshal actions"
-      r.acts.push_back(std::move(a));
     }
+  (void)n_iss;
 }
 
 }  // namespace req
