@@ -81,7 +81,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall-time bound of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    ap.add_argument("--workload", choices=["rp", "msm", "transfer", "mixed", "request"], default="rp")
+    ap.add_argument("--workload", choices=["rp", "msm", "transfer", "mixed", "request", "audit"], default="rp")
+    ap.add_argument("--tokens", type=int, default=65536, help="audit workload: token openings per GPU per step")
     ap.add_argument("--msm-log", type=int, default=20, help="msm workload: log2 of the point count")
     ap.add_argument("--transfers", type=int, default=8192, help="transfer/mixed workloads: transfers per GPU per step")
     ap.add_argument("--action-inflight", type=int, default=3,
@@ -93,6 +94,8 @@ def main():
         return bench_transfer(args)
     if args.workload == "mixed":
         return bench_mixed(args)
+    if args.workload == "audit":
+        return bench_audit(args)
     if args.workload == "request":
         return bench_transfer(args, raw_requests=True)
 
@@ -469,6 +472,96 @@ def bench_msm(args):
                                    % args.msm_log, "points": n, "parallelism": "shard%d" % world},
             "roofline": _roofline_from(kt, args.steps), "cpu_baseline": cpu,
             "kernel_ms": {k: round(v[0] / args.steps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),
+            flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_audit(args):
+    """the auditor's / wallet's token opening checks
+    (auditor.go:226-238, token.go:69-83).  One step = one fts_token_open_batch
+    over --tokens openings (host structs in: HashToZr of the type, scalar
+    reduction and upload included), --action-inflight calls concurrently."""
+    world, rank, local, dist = _dist_setup()
+    import random
+    import numpy as np
+    import fts_gpu
+    with open(os.path.join(ROOT, "tests", "golden", "zkatdlog_pp.json"), "rb") as f:
+        pp_raw = f.read()
+    pp = fts_gpu.PublicParams(pp_raw, bit_length=args.bits, device=local)
+    t0 = time.time()
+    rng = random.Random(0xF7A500A0 + rank)
+    distinct = []
+    for i in range(1024):
+        v, bf = rng.randrange(2**64), rng.randrange(R_ORDER)
+        t = b"TOK%d" % (i % 8)
+        distinct.append((pp.token_commit(t, v, bf.to_bytes(32, "big")), t, v.to_bytes(32, "big"),
+                         bf.to_bytes(32, "big")))
+    n = args.tokens
+    ops = (distinct * (n // len(distinct) + 1))[:n]
+    bad = set(range(7, n, 101))  # ~1 % tampered values
+    for j in bad:
+        com, t, v, bf = ops[j]
+        ops[j] = (com, t, (int.from_bytes(v, "big") ^ 1).to_bytes(32, "big"), bf)
+    batches = [pp.prepare_openings(ops) for _ in range(max(1, args.action_inflight))]
+    setup_s = time.time() - t0
+    want = np.zeros(n, dtype=np.int32)
+    want[sorted(bad)] = fts_gpu.FTS_E_OPEN_MISMATCH
+
+    class Step:
+        def __init__(self, b):
+            self.b = b
+
+        def verify(self):
+            st = pp.check_openings(self.b)
+            assert (st == want).all(), "opening verdicts differ"
+            return st
+
+    steps_objs = [Step(b) for b in batches]
+    for _ in range(max(1, args.warmup)):
+        steps_objs[0].verify()
+    if dist is not None:
+        dist.barrier()
+    elapsed, _ = _run_action_steps(steps_objs, args.steps, None, None)
+    elapsed = _max_over_ranks(dist, elapsed)
+    value = world * n * args.steps / elapsed
+    # isolated kernel time (one call alone on the GPU)
+    kt = {}
+    reps = 4
+    for _ in range(reps):
+        steps_objs[0].verify()
+        for name, (ms, mads) in pp.last_timings_ex().items():
+            o = kt.get(name, (0.0, 0.0))
+            kt[name] = (o[0] + ms, mads)
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        from oracle import cref, pp as oppm
+        opp = oppm.load_pp(pp_raw)
+        thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        done, cs = 0, 0.0
+        while cs < args.cpu_seconds and done < n:
+            c = min(2048, n - done)
+            t1 = time.perf_counter()
+            got = cref.open_check_many(opp, ops[done:done + c], threads=thr)
+            cs += time.perf_counter() - t1
+            assert got == [int(w) for w in want[done:done + c]], "CPU oracle verdicts differ"
+            done += c
+        cpu = {"value": round(done / cs, 1), "unit": "openings/s", "cores": thr, "kind": "port",
+               "sample": "%d of the same openings, reference-order commit() (3 G1.Mul + 2 Add + Equals; "
+                         "oracle/c/ref_verify.c oracle_open_check_many), %d threads, %.1f s wall" % (done, thr, cs)}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "token opening checks/sec (auditor InspectOutput, BN254)", "value": round(value, 1),
+            "unit": "openings/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32 (BN254 Fp/Fr 8x32-bit Montgomery)",
+            "data": "synthetic: 1024 distinct openings (8 types) from the library's host commitment, tiled; "
+                    "1 % tampered values (seed 0xF7A500A0 + rank)",
+            "config": {"workload": "SURVEY 8f rank 3: %d token openings per GPU per step via fts_token_open_batch, "
+                                   "%d calls in flight" % (n, len(batches)), "tokens_per_gpu": n,
+                       "parallelism": "shard%d" % world},
+            "roofline": _roofline_from(kt, reps), "cpu_baseline": cpu,
+            "kernel_ms": {k: round(v[0] / reps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),
             flush=True)
     if dist is not None:
         dist.destroy_process_group()

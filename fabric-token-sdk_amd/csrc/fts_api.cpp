@@ -52,6 +52,9 @@ void launch_sig_prep(const SigBatchDev& d, hipStream_t s);
 void launch_sig_finish(const SigBatchDev& d, const uint32_t* tables, int n, hipStream_t s);
 size_t table_build_scratch_bytes(int nb);
 size_t fb_words_per_base();
+// audit_kernels.hip
+void launch_open_check(int n, const uint8_t* raw, const uint32_t* sc, const uint32_t* tables, int nb,
+                       int32_t* status, hipStream_t s);
 }  // namespace fts
 
 using namespace fts;
@@ -104,8 +107,9 @@ struct Workspace {
   // action (transfer / issue) batches
   DBuf rp_raw, rp_sc, rp_status, rp_ipa;
   DBuf s_act, s_raw, s_owner, s_pts, s_sc, s_status, s_work, s_terms, s_aff, s_affoff, s_msgs, s_jac, s_scratch;
+  DBuf open_rec;  // token opening checks: [raw n*64][scalars n*96][status n*4]
   void release() {
-    for (DBuf* b : {&pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &terms, &scratch, &ypow, &svec, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
+    for (DBuf* b : {&open_rec, &pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &terms, &scratch, &ypow, &svec, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
                     &rp_status, &rp_ipa, &s_act, &s_raw, &s_owner, &s_pts, &s_sc, &s_status, &s_work, &s_terms, &s_aff,
                     &s_affoff, &s_msgs, &s_jac, &s_scratch, &r_key, &r_msc, &r_coef, &r_colsum, &r_fixed, &r_flag,
                     &m_keys, &m_counts, &m_offsets, &m_cursor, &m_sorted, &m_buckets, &m_segs, &m_wins, &m_out,
@@ -540,6 +544,7 @@ const char* fts_status_str(int32_t s) {
     case FTS_E_ST_INVALID: return "invalid same type proof";
     case FTS_E_NOT_RUN: return "not evaluated";
     case FTS_E_ACTION_INVALID: return "invalid action";
+    case FTS_E_OPEN_MISMATCH: return "does not match the provided opening";
     default: return "unknown status";
   }
 }
@@ -1737,6 +1742,97 @@ int fts_issue_prove(const fts_ctx* c, const uint8_t* type, size_t type_len, size
   *out_len = s.size();
   if (s.size() > out_cap) return FTS_API_ESIZE;
   memcpy(out_der, s.data(), s.size());
+  return FTS_API_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Token opening checks (crypto/audit/auditor.go:226-238, crypto/token/token.go:69-83)
+// ---------------------------------------------------------------------------
+namespace {
+// canonical LE u32 limbs of a BE 32-byte integer reduced mod r (G1.Mul(s) = (s mod r) P)
+void zr_canon_words(const uint8_t* be32, uint32_t out[8]) {
+  uint64_t c[4];
+  be32_to_u64(be32, c);
+  while (geq_mod<ModR>(c)) sub_mod_raw<ModR>(c);
+  for (int i = 0; i < 4; i++) out[2 * i] = (uint32_t)c[i], out[2 * i + 1] = (uint32_t)(c[i] >> 32);
+}
+void fr_canon_words(const Fr& a, uint32_t out[8]) {
+  uint64_t c[4];
+  from_mont(a, c);
+  for (int i = 0; i < 4; i++) out[2 * i] = (uint32_t)c[i], out[2 * i + 1] = (uint32_t)(c[i] >> 32);
+}
+constexpr size_t OPEN_REC = 64 + 96 + 4;       // staged bytes per token
+constexpr double OPEN_PRODUCTS = 48.0 * 11 + 4;  // Fp products: <= 48 mixed additions + the projective compare
+}  // namespace
+
+extern "C" {
+
+int fts_token_open_batch(fts_ctx* c, size_t n, const fts_token_opening* items, int32_t* status) {
+  if (!c || n > (size_t)(1u << 26) || (n && (!items || !status))) return FTS_API_EINVAL;
+  if (n == 0) return FTS_API_OK;
+  if (c->device < 0) return FTS_API_EDEVICE;
+  HIP_OK(hipSetDevice(c->device));
+  LaneGuard lg(c);
+  Lane& L = *lg.L;
+  const double t0 = now_ms();
+  uint8_t* st = L.stage_buf(n * OPEN_REC);
+  if (!st || L.ws.open_rec.ensure(n * OPEN_REC)) return FTS_API_ENOMEM;
+  uint8_t* h_raw = st;
+  uint32_t* h_sc = reinterpret_cast<uint32_t*>(st + n * 64);
+  int32_t* h_st = reinterpret_cast<int32_t*>(st + n * 160);
+  // host: HashToZr(type) (one SHA-256 per distinct type within a chunk), scalars mod r
+  const size_t CH = 512, nch = (n + CH - 1) / CH;
+  parallel_for(nch, 2, [&](size_t ch) {
+    // HashToZr of the last few distinct types (a batch carries few token types)
+    constexpr int NC = 8;
+    std::string key[NC];
+    uint32_t val[NC][8];
+    int nc = 0, rr = 0;
+    for (size_t i = ch * CH; i < std::min(n, (ch + 1) * CH); i++) {
+      const fts_token_opening& it = items[i];
+      uint32_t* S = h_sc + i * 24;
+      if (!it.com64 || !it.value32 || !it.bf32 || (it.type_len && !it.type)) {
+        h_st[i] = FTS_E_MALFORMED;
+        memset(h_raw + i * 64, 0, 64);
+        memset(S, 0, 96);
+        continue;
+      }
+      h_st[i] = FTS_OK;
+      memcpy(h_raw + i * 64, it.com64, 64);
+      int hit = -1;
+      for (int q = 0; q < nc && hit < 0; q++)
+        if (key[q].size() == it.type_len && !memcmp(key[q].data(), it.type, it.type_len)) hit = q;
+      if (hit < 0) {
+        hit = nc < NC ? nc++ : (rr++ % NC);
+        key[hit].assign((const char*)it.type, it.type_len);
+        fr_canon_words(hash_to_zr(key[hit]), val[hit]);
+      }
+      memcpy(S, val[hit], 32);
+      zr_canon_words(it.value32, S + 8);
+      zr_canon_words(it.bf32, S + 16);
+    }
+  });
+  const double t1 = now_ms();
+  uint8_t* d = L.ws.open_rec.as<uint8_t>();
+  L.tl.begin(L.s);
+  HIP_OK(hipMemcpyAsync(d, st, n * OPEN_REC, hipMemcpyHostToDevice, L.s));
+  L.tl.mark("h2d_open", L.s, 0);
+  launch_open_check((int)n, d, reinterpret_cast<const uint32_t*>(d + n * 64), c->d_tables, c->n,
+                    reinterpret_cast<int32_t*>(d + n * 160), L.s);
+  L.tl.mark("k_open_check", L.s, OPEN_PRODUCTS * (double)n);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(h_st, d + n * 160, n * 4, hipMemcpyDeviceToHost, L.s));
+  const double t2 = now_ms();
+  HIP_OK(L.sync());
+  memcpy(status, h_st, n * 4);
+  L.host_parse_ms = (float)(t1 - t0);
+  L.host_stage_ms = 0;
+  L.host_prep_ms = 0;
+  L.host_enqueue_ms = (float)(t2 - t1);
+  L.host_wait_ms = (float)(now_ms() - t2);
+  collect_timings(c, L, nullptr);
   return FTS_API_OK;
 }
 

@@ -32,7 +32,7 @@ import numpy as np
 from . import _lib as L
 from ._lib import (FTS_OK, FTS_E_MALFORMED, FTS_E_RP_NIL, FTS_E_RP_INVALID, FTS_E_IPA_NIL, FTS_E_IPA_LEN,  # noqa
                    FTS_E_IPA_INVALID, FTS_E_RC_COUNT, FTS_E_TAS_INVALID, FTS_E_ST_INVALID, FTS_DEVICE_NONE,
-                   FTS_E_ACTION_INVALID, FtsError)
+                   FTS_E_ACTION_INVALID, FTS_E_OPEN_MISMATCH, FtsError)
 from . import request  # noqa: F401  (TokenRequest writers)
 
 
@@ -212,6 +212,21 @@ class PublicParams:
         return out
 
     # ------------------------------------------------------------- prove
+    def prepare_openings(self, openings):
+        """Pack token openings ``(com64, type, value32, bf32)`` (None = nil field)
+        into the fts_token_opening array once; the result feeds check_openings."""
+        return OpeningBatch(openings)
+
+    def check_openings(self, openings):
+        """Batched token opening checks (fts_token_open_batch): one verdict per
+        token, FTS_OK iff HashToZr(type) ped0 + value ped1 + bf ped2 == com
+        (auditor.go:226-238, token.go:69-83)."""
+        ob = openings if isinstance(openings, OpeningBatch) else OpeningBatch(openings)
+        st = np.zeros(ob.n, dtype=np.int32)
+        L.check("fts_token_open_batch", L.lib.fts_token_open_batch(
+            self._ctx, ob.n, ob.items, st.ctypes.data_as(C.POINTER(C.c_int32))))
+        return st
+
     def token_commit(self, ttype, value, bf32):
         out = C.create_string_buffer(64)
         L.check("fts_token_commit", L.lib.fts_token_commit(self._ctx, ttype, len(ttype), value, bf32, out))
@@ -419,6 +434,72 @@ class StagedMsm:
             self.close()
         except Exception:
             pass
+
+
+class OpeningBatch:
+    """fts_token_opening[] over contiguous buffers (kept alive with the batch)."""
+
+    def __init__(self, openings):
+        n = self.n = len(openings)
+        fixed = [(64, 0), (32, 2), (32, 3)]
+        self._blobs = []
+        cols = np.zeros((n, 5), dtype=np.uint64)
+        for size, k in fixed:
+            vals = [o[k] for o in openings]
+            for v in vals:
+                assert v is None or len(v) == size
+            blob = np.frombuffer(b"".join(v if v is not None else bytes(size) for v in vals) or b"\0", dtype=np.uint8)
+            self._blobs.append(blob)
+            col = {0: 0, 2: 3, 3: 4}[k]
+            cols[:, col] = blob.ctypes.data + np.arange(n, dtype=np.uint64) * size
+            nil = np.array([v is None for v in vals], dtype=bool)
+            cols[nil, col] = 0
+        types = [o[1] or b"" for o in openings]
+        tblob = np.frombuffer(b"".join(types) or b"\0", dtype=np.uint8)
+        self._blobs.append(tblob)
+        lens = np.array([len(t) for t in types], dtype=np.uint64)
+        offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64) if n else lens
+        cols[:, 1] = tblob.ctypes.data + offs
+        cols[:, 2] = lens
+        self._cols = np.ascontiguousarray(cols)
+        self.items = self._cols.ctypes.data_as(C.POINTER(L.TokenOpening))
+
+
+class Auditor:
+    """The opening checks of audit.Auditor (crypto/audit/auditor.go): every
+    output of every action is re-committed on the device in one batch; the
+    error chain is the reference's (CheckIssueRequests / CheckTransferRequests
+    :168-210, InspectOutputs :213-222, InspectOutput :226-238).  Identity
+    inspection (InspectIdentity) is out of scope."""
+
+    def __init__(self, pp):
+        self.pp = pp
+
+    def InspectOutputs(self, tokens):
+        st = self.pp.check_openings(tokens)
+        for i, s in enumerate(st):
+            if s != FTS_OK:
+                raise VerifyError(_inspect_message(int(s), i), int(s), i)
+
+    def check_actions(self, actions, txid, kind="transfer"):
+        """actions: list (one per action) of lists of openings; raises the error of
+        the first failing output of the first failing action (auditor.go:178-210)."""
+        flat = [t for a in actions for t in a]
+        st = self.pp.check_openings(flat)
+        pos = 0
+        for k, a in enumerate(actions):
+            for i in range(len(a)):
+                s = int(st[pos + i])
+                if s != FTS_OK:
+                    what = "%d th transfer" % k if kind == "transfer" else "%d th issue" % k
+                    raise VerifyError("audit of %s in tx [%s] failed: %s" % (what, txid, _inspect_message(s, i)), s, i)
+            pos += len(a)
+
+
+def _inspect_message(status, i):
+    if status == FTS_E_OPEN_MISMATCH:
+        return "failed inspecting output [%d]: output at index [%d] does not match the provided opening" % (i, i)
+    return "failed inspecting output [%d]: invalid output at index [%d]" % (i, i)
 
 
 class RangeVerifier:

@@ -24,6 +24,7 @@ FTS_E_TAS_INVALID = 8
 FTS_E_ST_INVALID = 9
 FTS_E_NOT_RUN = 10
 FTS_E_ACTION_INVALID = 11
+FTS_E_OPEN_MISMATCH = 12
 
 FTS_API_OK = 0
 FTS_DEVICE_NONE = -2
@@ -35,7 +36,7 @@ EXPORTED = [
     "fts_status_str", "fts_rp_prove", "fts_rp_prove_batch", "fts_token_commit",
     "fts_transfer_prove", "fts_issue_prove", "fts_debug_rp_intermediates",
     "fts_debug_msm_stats", "fts_msm_g1", "fts_msm_stage", "fts_msm_run", "fts_msm_timings", "fts_msm_free",
-    "fts_request_verify_batch", "fts_request_inspect",
+    "fts_request_verify_batch", "fts_request_inspect", "fts_token_open_batch",
 ]
 
 
@@ -51,6 +52,11 @@ class TransferItem(C.Structure):
 
 class IssueItem(C.Structure):
     _fields_ = [("tokens", C.c_void_p), ("n_tok", C.c_size_t), ("proof", C.c_void_p), ("proof_len", C.c_size_t)]
+
+
+class TokenOpening(C.Structure):
+    _fields_ = [("com64", C.c_void_p), ("type", C.c_void_p), ("type_len", C.c_size_t), ("value32", C.c_void_p),
+                ("bf32", C.c_void_p)]
 
 
 def _load():
@@ -95,6 +101,7 @@ def _load():
         "fts_msm_free": ([P], None),
         "fts_request_verify_batch": ([P, S, C.POINTER(C.c_void_p), C.POINTER(S), I32P, I32P, I32P], C.c_int),
         "fts_request_inspect": ([U8P, S, I32P, I32P, I32P, I32P, I32P, I32P], C.c_int),
+        "fts_token_open_batch": ([P, S, C.POINTER(TokenOpening), I32P], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

@@ -53,8 +53,11 @@ enum fts_status {
   FTS_E_TAS_INVALID = 8,    /* "invalid sum and type proof"          typeandsum.go:232,274 */
   FTS_E_ST_INVALID = 9,     /* "invalid same type proof"             sametype.go:180 */
   FTS_E_NOT_RUN = 10,       /* item not evaluated (batch aborted by an API error) */
-  FTS_E_ACTION_INVALID = 11 /* action fails its structural Validate() before the ZK proof:
+  FTS_E_ACTION_INVALID = 11, /* action fails its structural Validate() before the ZK proof:
                                issue/action.go:161-185,273-282; transfer/action.go:244-283 */
+  FTS_E_OPEN_MISMATCH = 12  /* "output at index [%d] does not match the provided opening"
+                               audit/auditor.go:236-238; "... output does not match provided
+                               opening" token/token.go:78-80 */
 };
 
 /* ---- API return codes ---- */
@@ -200,6 +203,28 @@ int fts_msm_run(fts_ctx* ctx, fts_msm_batch* b, uint8_t* out64);
 /* per-kernel device time (ms) and algorithmic u32 MADs of b's last run */
 int fts_msm_timings(const fts_msm_batch* b, const char** names, float* ms, double* mads, int cap);
 void fts_msm_free(fts_msm_batch* b);
+
+/* ---- token opening checks (auditor / wallet) ----
+ * Replaces the per-token commit() + Equals of Auditor.InspectOutput
+ * (crypto/audit/auditor.go:226-238, reached from CheckIssueRequests / CheckTransferRequests
+ * :178-210) and of Token.ToClear (crypto/token/token.go:69-83):
+ *   status[i] <- FTS_OK iff HashToZr(type_i)*ped0 + value_i*ped1 + bf_i*ped2 == com_i
+ *                FTS_E_OPEN_MISMATCH otherwise
+ * com64:   token.Data as 64 B X||Y BE (G1.Bytes()), checked like NewG1FromBytes (flag bits,
+ *          canonical coordinates, on the curve; 64 zero bytes = identity) -> FTS_E_MALFORMED
+ * type:    metadata.Type bytes (HashToZr = SHA-256 mod r)
+ * value32, bf32: Zr.Bytes() 32 B BE, used mod r (G1.Mul semantics)
+ * A NULL com64 / value32 / bf32 -> FTS_E_MALFORMED (the reference returns "invalid output at
+ * index [%d]" / "cannot commit a nil element", or panics on a nil Zr in the auditor's commit).
+ * One device pass: three fixed-base products per token (audit_kernels.hip). */
+typedef struct {
+  const uint8_t* com64;
+  const uint8_t* type;
+  size_t type_len;
+  const uint8_t* value32;
+  const uint8_t* bf32;
+} fts_token_opening;
+int fts_token_open_batch(fts_ctx* ctx, size_t n, const fts_token_opening* items, int32_t* status);
 
 /* ---- error strings ---- */
 const char* fts_status_str(int32_t status);

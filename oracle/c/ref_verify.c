@@ -753,3 +753,76 @@ int oracle_msm(const uint8_t* pts, const uint8_t* scs, size_t n, int threads, ui
   g1_bytes(toaff(j.acc), out64);
   return j.bad ? -1 : 0;
 }
+
+/* ---------------------------------------------------------------- openings
+ * int oracle_open_check_many(const uint8_t* ped, int count, const uint8_t* coms,
+ *     const uint8_t* const* types, const size_t* type_lens, const uint8_t* values,
+ *     const uint8_t* bfs, int threads, int32_t* out)
+ * Auditor.InspectOutput's check in reference order (crypto/audit/auditor.go:226-238,
+ * commit() :412-418): com = NewG1(); com.Add(ped_i.Mul(v_i)) for (HashToZr(type),
+ * value, bf); Equals(token.Data).  ped: 3 x 64-byte BE generators; coms: count x 64;
+ * values / bfs: count x 32-byte BE (used mod r).  out[i]: 0 ok, 12 mismatch,
+ * 1 token.Data rejected by NewG1FromBytes (fts_status numbering). */
+typedef struct {
+  g1 ped[3];
+  const uint8_t *coms, *values, *bfs;
+  const uint8_t* const* types;
+  const size_t* tlens;
+  int32_t* out;
+  int count, next;
+  pthread_mutex_t mu;
+} open_job;
+static void* open_worker(void* arg) {
+  open_job* j = (open_job*)arg;
+  for (;;) {
+    pthread_mutex_lock(&j->mu);
+    int lo = j->next;
+    j->next += 16;
+    pthread_mutex_unlock(&j->mu);
+    if (lo >= j->count) break;
+    int hi = lo + 16 < j->count ? lo + 16 : j->count;
+    for (int i = lo; i < hi; i++) {
+      g1 data;
+      if (!g1_from_bytes(j->coms + 64 * (size_t)i, 64, &data)) {
+        j->out[i] = 1;
+        continue;
+      }
+      sha_t s;
+      uint8_t d[32];
+      sha_init(&s);
+      sha_upd(&s, j->types[i], j->tlens[i]);
+      sha_fin(&s, d);
+      g1 c;
+      memset(&c, 0, sizeof c);
+      c.inf = 1;
+      c = g1_add(c, g1_mul(j->ped[0], digest_zr(d)));
+      c = g1_add(c, g1_mul(j->ped[1], be_to_fe(j->values + 32 * (size_t)i)));
+      c = g1_add(c, g1_mul(j->ped[2], be_to_fe(j->bfs + 32 * (size_t)i)));
+      j->out[i] = g1_eq(c, data) ? 0 : 12;
+    }
+  }
+  return NULL;
+}
+int oracle_open_check_many(const uint8_t* ped, int count, const uint8_t* coms, const uint8_t* const* types,
+                           const size_t* type_lens, const uint8_t* values, const uint8_t* bfs, int threads,
+                           int32_t* out) {
+  init_consts();
+  open_job j;
+  for (int k = 0; k < 3; k++)
+    if (!g1_from_bytes(ped + 64 * k, 64, &j.ped[k])) return -1;
+  j.coms = coms;
+  j.values = values;
+  j.bfs = bfs;
+  j.types = types;
+  j.tlens = type_lens;
+  j.out = out;
+  j.count = count;
+  j.next = 0;
+  pthread_mutex_init(&j.mu, NULL);
+  if (threads < 1) threads = 1;
+  pthread_t* th = malloc(sizeof(pthread_t) * threads);
+  for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, open_worker, &j);
+  for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+  free(th);
+  return 0;
+}

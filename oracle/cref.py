@@ -59,3 +59,24 @@ def msm(points64, scalars32, threads=1):
     rc = lib().oracle_msm(points64, scalars32, n, threads, out)
     assert rc == 0
     return out.raw
+
+
+def open_check_many(pp, openings, threads=1):
+    """Auditor.InspectOutput in reference order for (com64, type, value32, bf32)
+    openings -> fts_status numbering (0 ok, 12 mismatch, 1 malformed data)"""
+    lb = lib()
+    if not hasattr(lb, "_open_sig"):
+        lb.oracle_open_check_many.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.POINTER(C.c_char_p),
+                                              C.POINTER(C.c_size_t), C.c_char_p, C.c_char_p, C.c_int,
+                                              C.POINTER(C.c_int32)]
+        lb.oracle_open_check_many.restype = C.c_int
+        lb._open_sig = True
+    n = len(openings)
+    ped = b"".join(bn.g1_bytes(p) for p in pp.ped)
+    types = (C.c_char_p * n)(*[o[1] for o in openings])
+    tl = (C.c_size_t * n)(*[len(o[1]) for o in openings])
+    out = (C.c_int32 * n)()
+    rc = lb.oracle_open_check_many(ped, n, b"".join(o[0] for o in openings), types, tl,
+                                   b"".join(o[2] for o in openings), b"".join(o[3] for o in openings), threads, out)
+    assert rc == 0
+    return list(out)

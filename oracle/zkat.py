@@ -641,3 +641,23 @@ def token_commit(ped, type_bytes, value, bf):
 
 def make_rng(seed):
     return random.Random(seed)
+
+
+# ------------------------------------------------------------------ auditor
+def inspect_output(ped, com_bytes, type_bytes, value_bytes, bf_bytes, index=0):
+    """Auditor.InspectOutput's opening check, crypto/audit/auditor.go:226-238
+    (commit() :412-418): tokenComm = HashToZr(type) ped0 + value ped1 + bf ped2,
+    compared with token.Data.  Returns the reference error string or None.
+    ``com_bytes`` goes through NewG1FromBytes (PointError -> "malformed");
+    value/bf through NewZrFromBytes (unreduced; G1.Mul uses them mod r).
+    A None field is the nil case the library reports as FTS_E_MALFORMED."""
+    if com_bytes is None or value_bytes is None or bf_bytes is None:
+        return "malformed"
+    try:
+        com = bn.g1_from_bytes(com_bytes)
+    except bn.PointError:
+        return "malformed"
+    c = token_commit(ped, type_bytes, bn.zr_from_bytes(value_bytes) % R, bn.zr_from_bytes(bf_bytes) % R)
+    if c != com:
+        return "output at index [%d] does not match the provided opening" % index
+    return None
