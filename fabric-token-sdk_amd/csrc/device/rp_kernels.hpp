@@ -34,6 +34,15 @@ inline __host__ __device__ int tb_count(int n) { return 2 * n + 6; }
 inline __host__ __device__ uint32_t x0_array_len(int n) { return 130u * (2u * n + 2u) - 2u; }
 inline __host__ __device__ uint32_t x0_msg_len(int n) { return x0_array_len(n) + 46u; }
 inline __host__ __device__ uint32_t x0_slot_bytes(int n) { return ((x0_msg_len(n) + 9u + 63u) / 64u) * 64u; }
+// SHA-256 blocks [x0_cb0, x0_cb1) of the x0 message lie entirely inside the
+// constant records hex(G_0) "||" ... hex(Q) "||" (bytes [8 + 130n, 8 + 130(2n+1)))
+// and are read by every proof from one shared template (x0_tmpl, L2-resident);
+// a proof's own slot holds only the other blocks (x0_var_bytes).
+inline __host__ __device__ uint32_t x0_const_off(int n) { return 8u + 130u * n; }
+inline __host__ __device__ uint32_t x0_const_end(int n) { return 8u + 130u * (2u * n + 1u); }
+inline __host__ __device__ uint32_t x0_cb0(int n) { return (x0_const_off(n) + 63u) / 64u; }
+inline __host__ __device__ uint32_t x0_cb1(int n) { return x0_const_end(n) / 64u; }
+inline __host__ __device__ uint32_t x0_var_bytes(int n) { return x0_slot_bytes(n) - 64u * (x0_cb1(n) - x0_cb0(n)); }
 
 // small transcripts slot (x: 258 B, y: 388 B, x_j: 258 B, z: 32 B) -> 512 B scratch each
 constexpr uint32_t SMALL_SLOT = 512;
@@ -143,7 +152,7 @@ struct RpBatchDev {
   uint32_t* hpj;       // [B][n+1][24] Jacobian H'_0..H'_{n-1}, com
   uint32_t* hpa;       // [B][n+1][16] affine Montgomery
   uint8_t* hp_be;      // [B][n+1][64] canonical big-endian encodings
-  uint8_t* x0_msgs;    // [B][x0_slot_bytes(n)]
+  uint8_t* x0_msgs;    // [B][x0_var_bytes(n)]: the message blocks outside the shared template
   uint32_t* terms;     // [B][6+2n+2k][24]
   uint32_t* scratch;   // var-base lane tables
   uint32_t* ypow;      // [n][B][8] y^-i (Montgomery Fr), i-major (coalesced over proofs)

@@ -37,7 +37,7 @@ size_t rp_scratch_words(int B, int n, int k);
 size_t rp_terms_words(int B, int n, int k);
 void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s);
 void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const uint32_t* wtables,
-                     const uint8_t* x0_const, hipStream_t s, hipStream_t s2, Timeline* tl);
+                     const uint8_t* x0_const, const uint8_t* x0_tmpl, hipStream_t s, hipStream_t s2, Timeline* tl);
 void launch_build_wide_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s);
 size_t wide_build_scratch_bytes(int nb);
 size_t fbw_words_per_base();
@@ -241,6 +241,7 @@ struct fts_ctx {
   uint32_t* d_tables = nullptr;
   uint32_t* d_wtables = nullptr;  // 20-bit tables of [H_0 .. H_{n-1}, K, P] (k_rp_fixed_exact)
   uint8_t* d_x0const = nullptr;
+  uint8_t* d_x0tmpl = nullptr;  // x0 message blocks [x0_cb0, x0_cb1): shared by every proof
   size_t table_bytes = 0;
   // lane pool
   std::vector<Lane*> lanes;
@@ -475,6 +476,11 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   }
   if (hipMalloc(&c->d_x0const, xc.size()) != hipSuccess) return fail(FTS_API_ENOMEM);
   hipMemcpyAsync(c->d_x0const, xc.data(), xc.size(), hipMemcpyHostToDevice, s0);
+  // block-aligned template of the fully constant SHA-256 blocks of the x0 message
+  std::string xt(64u * (x0_cb1(n) - x0_cb0(n)), '\0');
+  for (size_t j = 0; j < xt.size(); j++) xt[j] = xc[64u * x0_cb0(n) + j - x0_const_off(n)];
+  if (hipMalloc(&c->d_x0tmpl, xt.size()) != hipSuccess) return fail(FTS_API_ENOMEM);
+  hipMemcpyAsync(c->d_x0tmpl, xt.data(), xt.size(), hipMemcpyHostToDevice, s0);
   hipError_t e = hipStreamSynchronize(s0);
   hipFree(d_bases);
   hipFree(d_scr);
@@ -516,6 +522,7 @@ void fts_ctx_destroy(fts_ctx* c) {
   if (c->d_tables) hipFree(c->d_tables);
   if (c->d_wtables) hipFree(c->d_wtables);
   if (c->d_x0const) hipFree(c->d_x0const);
+  if (c->d_x0tmpl) hipFree(c->d_x0tmpl);
   delete c;
 }
 
@@ -674,7 +681,7 @@ static int rp_buffers(fts_ctx* c, Lane& L, int B) {
   if (w.pts.ensure((size_t)B * npts * 64) || w.ch.ensure((size_t)B * rp_nch(k) * 32) ||
       w.small.ensure((size_t)B * (2 + k) * SMALL_SLOT) || w.hpj.ensure((size_t)B * (n + 1) * 96) ||
       w.hpa.ensure((size_t)B * (n + 1) * 64) || w.hpbe.ensure((size_t)B * (n + 1) * 64) ||
-      w.x0.ensure((size_t)B * x0_slot_bytes(n)) || w.terms.ensure(rp_terms_words(B, n, k) * 4) ||
+      w.x0.ensure((size_t)B * x0_var_bytes(n)) || w.terms.ensure(rp_terms_words(B, n, k) * 4) ||
       w.scratch.ensure(std::max(rp_scratch_words(B, n, k), (size_t)B * 10 * 24) * 4) || w.r_key.ensure(32) ||
       w.r_msc.ensure((size_t)N * 32) || w.r_coef.ensure((size_t)B * 5 * 32) || w.r_colsum.ensure((3 + 2 * n) * 32) ||
       w.r_fixed.ensure((3 + 2 * n) * 96) || w.r_flag.ensure(4) || w.ypow.ensure((size_t)B * n * 32) ||
@@ -742,7 +749,7 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   HIP_OK(hipMemcpyAsync(r.key, L.pin->key, sizeof L.pin->key, hipMemcpyHostToDevice, L.s));
   const double t_prep = now_ms();
   L.tl.begin(L.s);
-  launch_rp_batch(d, r, c->d_tables, c->d_wtables, c->d_x0const, L.s, L.s2, &L.tl);
+  launch_rp_batch(d, r, c->d_tables, c->d_wtables, c->d_x0const, c->d_x0tmpl, L.s, L.s2, &L.tl);
   between();
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(&L.pin->flag, r.flag, 4, hipMemcpyDeviceToHost, L.s));

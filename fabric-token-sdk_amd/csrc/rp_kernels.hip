@@ -576,38 +576,102 @@ FTS_DEV uint32_t x0_unit(const X0Src& m, uint32_t u) {
   return 0u;
 }
 
-// thread per (16-byte chunk, proof): each writes one uint4 of the padded
-// message, so a wave's stores cover 1 KB of one proof's message contiguously
+// One block per proof: the proof's variable message blocks (everything but
+// the shared template blocks) are assembled in LDS -- hex records of H'_i and
+// com (one 16-byte quarter of a point per work item), the DER header, the
+// constant bytes that share a block with variable ones, Zb(ip) and the SHA-256
+// padding -- then written to the compact slot with coalesced uint4 stores.
+// LDS offset of message byte `pos` (outside the template blocks):
+FTS_DEV uint32_t x0_lds_off(uint32_t pos, uint32_t cb0, uint32_t cb1) {
+  return pos < 64u * cb0 ? pos : pos - 64u * (cb1 - cb0);
+}
 __global__ void __launch_bounds__(256) k_rp_x0_build(int B, int n, const int32_t* __restrict__ status,
                                                      const uint8_t* __restrict__ hp_be,
                                                      const uint8_t* __restrict__ x0_const, const uint32_t* __restrict__ sc,
                                                      uint8_t* __restrict__ msgs) {
-  const uint32_t nchk = x0_slot_bytes(n) / 16u;
-  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (size_t)B * nchk) return;
-  const int b = (int)(gid / nchk);
-  const uint32_t c = (uint32_t)(gid % nchk);
-  if (status[b] != 0) return;
-  X0Src m;
-  m.hp = hp_be + (size_t)b * (n + 1) * 64;
-  m.cst = reinterpret_cast<const uint16_t*>(x0_const);
-  m.ip = sc + ((size_t)b * RP_NSC + RP_SC_IP) * 8;
-  m.A = x0_array_len(n);
-  m.len = x0_msg_len(n);
-  m.end = x0_slot_bytes(n);
-  m.n = n;
-  uint32_t v[4];
+  extern __shared__ uint4 x0_lds[];
+  uint8_t* Lb = reinterpret_cast<uint8_t*>(x0_lds);
+  const int b = blockIdx.x;
+  if (b >= B || status[b] != 0) return;  // uniform per block
+  const uint32_t A = x0_array_len(n), len = x0_msg_len(n), end = x0_slot_bytes(n);
+  const uint32_t cb0 = x0_cb0(n), cb1 = x0_cb1(n), var = x0_var_bytes(n);
+  const uint32_t c_off = x0_const_off(n), c_end = x0_const_end(n);
+  const uint8_t* hp = hp_be + (size_t)b * (n + 1) * 64;
+  // hex records: H'_0..H'_{n-1} (records 0..n-1) and com (record 2n+1, no "||")
+  for (int it = threadIdx.x; it < (n + 1) * 4; it += blockDim.x) {
+    const int r = it >> 2, q = it & 3;
+    const uint4 v = *reinterpret_cast<const uint4*>(hp + r * 64 + q * 16);
+    const uint32_t rec = r < n ? (uint32_t)r : 2u * n + 1u;
+    uint16_t* d = reinterpret_cast<uint16_t*>(Lb + x0_lds_off(8u + 130u * rec + 32u * q, cb0, cb1));
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-  for (int q = 0; q < 4; q++) v[q] = x0_unit(m, 8u * c + 2u * q) | (x0_unit(m, 8u * c + 2u * q + 1u) << 16);
-  reinterpret_cast<uint4*>(msgs + (size_t)b * m.end)[c] = make_uint4(v[0], v[1], v[2], v[3]);
+    for (int j = 0; j < 16; j++) d[j] = hex2((w[j >> 2] >> (8 * (j & 3))) & 0xffu);
+    if (q == 3 && r < n) d[16] = 0x7c7cu;
+  }
+  // header, constant bytes in variable blocks, trailer (DER tail, Zb(ip), padding, length)
+  const uint32_t* ip = sc + ((size_t)b * RP_NSC + RP_SC_IP) * 8;
+  const uint32_t t0 = 8u + A;
+  auto put = [&](uint32_t pos) {
+    uint32_t v;
+    if (pos < 8u) {  // 30 82 L L 04 82 A A
+      const uint32_t L = A + 42u;
+      const uint8_t h[8] = {0x30, 0x82, (uint8_t)(L >> 8), (uint8_t)L, 0x04, 0x82, (uint8_t)(A >> 8), (uint8_t)A};
+      v = h[pos];
+    } else if (pos >= c_off && pos < c_end) {
+      v = x0_const[pos - c_off];
+    } else if (pos < t0 + 6u) {  // 04 02 "||" 04 20
+      const uint8_t h[6] = {0x04, 0x02, 0x7c, 0x7c, 0x04, 0x20};
+      v = h[pos - t0];
+    } else if (pos < len) {  // Zb(ip): big-endian bytes of the canonical LE limbs
+      const uint32_t k = pos - t0 - 6u;
+      v = (ip[7 - (k >> 2)] >> (24 - 8 * (k & 3u))) & 0xffu;
+    } else if (pos == len) {
+      v = 0x80u;
+    } else if (pos >= end - 8u) {
+      v = (uint32_t)(((uint64_t)len * 8u) >> (8 * (end - 1u - pos))) & 0xffu;
+    } else {
+      v = 0u;
+    }
+    Lb[x0_lds_off(pos, cb0, cb1)] = (uint8_t)v;
+  };
+  const uint32_t nh = 8u, nc0 = 64u * cb0 - c_off, nc1 = c_end - 64u * cb1, nt = end - t0;
+  for (uint32_t it = threadIdx.x; it < nh + nc0 + nc1 + nt; it += blockDim.x) {
+    uint32_t pos;
+    if (it < nh) pos = it;
+    else if (it < nh + nc0) pos = c_off + (it - nh);
+    else if (it < nh + nc0 + nc1) pos = 64u * cb1 + (it - nh - nc0);
+    else pos = t0 + (it - nh - nc0 - nc1);
+    put(pos);
+  }
+  __syncthreads();
+  uint4* dst = reinterpret_cast<uint4*>(msgs + (size_t)b * var);
+  for (uint32_t c = threadIdx.x; c < var / 16u; c += blockDim.x) dst[c] = x0_lds[c];
 }
+inline size_t x0_build_lds(int n) { return x0_var_bytes(n); }
 
 __global__ void __launch_bounds__(64) k_rp_x0_hash(int B, int n, int k, const int32_t* __restrict__ status,
-                                                   const uint8_t* __restrict__ msgs, uint32_t* __restrict__ ch) {
+                                                   const uint8_t* __restrict__ msgs, const uint8_t* __restrict__ tmpl,
+                                                   uint32_t* __restrict__ ch) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B || status[b] != 0) return;
+  const uint32_t cb0 = x0_cb0(n), cb1 = x0_cb1(n), nb = sha_blocks(x0_msg_len(n));
+  const uint4* own = reinterpret_cast<const uint4*>(msgs + (size_t)b * x0_var_bytes(n));
+  const uint4* shared = reinterpret_cast<const uint4*>(tmpl);
   uint32_t st[8];
-  sha256_blocks(msgs + (size_t)b * x0_slot_bytes(n), sha_blocks(x0_msg_len(n)), st);
+  sha256_init(st);
+  for (uint32_t blk = 0; blk < nb; blk++) {
+    const uint4* m = blk < cb0 ? own + 4u * blk : blk < cb1 ? shared + 4u * (blk - cb0) : own + 4u * (blk - (cb1 - cb0));
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      uint4 u = m[i];
+      w[4 * i + 0] = __builtin_bswap32(u.x);
+      w[4 * i + 1] = __builtin_bswap32(u.y);
+      w[4 * i + 2] = __builtin_bswap32(u.z);
+      w[4 * i + 3] = __builtin_bswap32(u.w);
+    }
+    sha256_compress(st, w);
+  }
   store_f(ch + ((size_t)b * rp_nch(k) + CH_X0) * 8, f_to_mont(digest_to_fr(st)));
 }
 
@@ -949,7 +1013,7 @@ void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalar
 // random-linear-combination check of all final equations (one MSM).
 // s = main stream, s2 = side stream.
 void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const uint32_t* wtables,
-                     const uint8_t* x0_const, hipStream_t s, hipStream_t s2, Timeline* tl) {
+                     const uint8_t* x0_const, const uint8_t* x0_tmpl, hipStream_t s, hipStream_t s2, Timeline* tl) {
   const int B = d.B, n = d.n, k = d.k;
   if (!B) return;
   FTS_LAUNCH(k_rp_decode, B * rp_npts(k), 256, s, B, rp_npts(k), d.raw, d.pts, d.status);
@@ -981,10 +1045,10 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   tl->mark("k_rp_normalize_com", s, (double)B * (2.0 * 8.0 / NORM_E + 9.0));
   // side: x0 transcript + hash, then the fixed-base columns (need x0)
   tl->fork(s, s2);
-  FTS_LAUNCH(k_rp_x0_build, (size_t)B * (x0_slot_bytes(n) / 16), 256, s2, B, n, d.status, d.hp_be, x0_const, d.sc,
-             d.x0_msgs);
+  hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s2, B, n, d.status, d.hp_be, x0_const, d.sc,
+                     d.x0_msgs);
   tl->mark("k_rp_x0_build", s2, 0);
-  FTS_LAUNCH(k_rp_x0_hash, B, 64, s2, B, n, k, d.status, d.x0_msgs, d.ch);
+  FTS_LAUNCH(k_rp_x0_hash, B, 64, s2, B, n, k, d.status, d.x0_msgs, x0_tmpl, d.ch);
   tl->mark("k_rp_x0_hash", s2, 0);
   // main: variable points of the batch equation -> MSM
   FTS_LAUNCH(k_rlc_prep, B, 64, s, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, r.key, d.hpa, d.pts, r.msc, r.coef);
