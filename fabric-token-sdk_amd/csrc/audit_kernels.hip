@@ -24,34 +24,6 @@
 
 namespace fts {
 
-// acc += k * B over a 16-bit window table (fb_mul of fixed_base.hpp, but into
-// an existing accumulator)
-FTS_DEV void fb_mul_acc(G1J& acc, const uint32_t* __restrict__ table, const Scalar& k) {
-  uint32_t s[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) s[i] = k.v[i];
-  int carry = 0, w = 0, d = 0;
-  for (; w < FB_NW; w++) {
-    d = fb_next_digit(s, carry);
-    if (d != 0) break;
-  }
-  if (w == FB_NW) return;
-  G1A cur = fb_entry(table, w, d);
-  for (;;) {
-    int wn = w + 1, dn = 0;
-    for (; wn < FB_NW; wn++) {
-      dn = fb_next_digit(s, carry);
-      if (dn != 0) break;
-    }
-    G1A nxt;
-    if (wn < FB_NW) nxt = fb_entry(table, wn, dn);  // in flight during the addition
-    madd_inl(acc, cur);
-    if (wn >= FB_NW) break;
-    cur = nxt;
-    w = wn;
-  }
-}
-
 __global__ void __launch_bounds__(64) k_open_check(int n, const uint8_t* __restrict__ raw,
                                                    const uint32_t* __restrict__ sc, const uint32_t* __restrict__ t_ped0,
                                                    const uint32_t* __restrict__ t_ped1,

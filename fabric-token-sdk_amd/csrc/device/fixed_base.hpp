@@ -166,6 +166,34 @@ FTS_DEV G1J fb_mul_w(const uint32_t* __restrict__ table, const Scalar& k) {
   return acc;
 }
 
+// acc += k * B over a 16-bit window table (fb_mul of fixed_base.hpp, but into
+// an existing accumulator)
+FTS_DEV void fb_mul_acc(G1J& acc, const uint32_t* __restrict__ table, const Scalar& k) {
+  uint32_t s[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = k.v[i];
+  int carry = 0, w = 0, d = 0;
+  for (; w < FB_NW; w++) {
+    d = fb_next_digit(s, carry);
+    if (d != 0) break;
+  }
+  if (w == FB_NW) return;
+  G1A cur = fb_entry(table, w, d);
+  for (;;) {
+    int wn = w + 1, dn = 0;
+    for (; wn < FB_NW; wn++) {
+      dn = fb_next_digit(s, carry);
+      if (dn != 0) break;
+    }
+    G1A nxt;
+    if (wn < FB_NW) nxt = fb_entry(table, wn, dn);  // in flight during the addition
+    madd_inl(acc, cur);
+    if (wn >= FB_NW) break;
+    cur = nxt;
+    w = wn;
+  }
+}
+
 // out-of-line copy for cold call sites (keeps their kernels small)
 __device__ __noinline__ G1J nl_fb_mul(const uint32_t* __restrict__ table, Scalar k) { return fb_mul(table, k); }
 

@@ -23,6 +23,7 @@
 #include "../../include/fts_gpu.h"
 #include "device/rp_kernels.hpp"
 #include "device/sigma.hpp"
+#include "device/prove.hpp"
 #include "host/bn254_host.hpp"
 #include "host/der.hpp"
 #include "host/pp_parse.hpp"
@@ -52,6 +53,9 @@ void launch_sig_prep(const SigBatchDev& d, hipStream_t s);
 void launch_sig_finish(const SigBatchDev& d, const uint32_t* tables, int n, hipStream_t s);
 size_t table_build_scratch_bytes(int nb);
 size_t fb_words_per_base();
+// prove_kernels.hip
+void launch_rp_prove(const PvDev& d, const PvStage* stages, const uint8_t* x0_const, const uint8_t* x0_tmpl,
+                     hipStream_t s, Timeline* tl);
 // audit_kernels.hip
 void launch_open_check(int n, const uint8_t* raw, const uint32_t* sc, const uint32_t* tables, int nb,
                        int32_t* status, hipStream_t s);
@@ -108,8 +112,9 @@ struct Workspace {
   DBuf rp_raw, rp_sc, rp_status, rp_ipa;
   DBuf s_act, s_raw, s_owner, s_pts, s_sc, s_status, s_work, s_terms, s_aff, s_affoff, s_msgs, s_jac, s_scratch;
   DBuf open_rec;  // token opening checks: [raw n*64][scalars n*96][status n*4]
+  DBuf pv;        // batched prover: one arena (prove_arena)
   void release() {
-    for (DBuf* b : {&open_rec, &pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &terms, &scratch, &ypow, &svec, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
+    for (DBuf* b : {&open_rec, &pv, &pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &terms, &scratch, &ypow, &svec, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
                     &rp_status, &rp_ipa, &s_act, &s_raw, &s_owner, &s_pts, &s_sc, &s_status, &s_work, &s_terms, &s_aff,
                     &s_affoff, &s_msgs, &s_jac, &s_scratch, &r_key, &r_msc, &r_coef, &r_colsum, &r_fixed, &r_flag,
                     &m_keys, &m_counts, &m_offsets, &m_cursor, &m_sorted, &m_buckets, &m_segs, &m_wins, &m_out,
@@ -1840,6 +1845,203 @@ int fts_token_open_batch(fts_ctx* c, size_t n, const fts_token_opening* items, i
   L.host_enqueue_ms = (float)(t2 - t1);
   L.host_wait_ms = (float)(now_ms() - t2);
   collect_timings(c, L, nullptr);
+  return FTS_API_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Batched range-proof prover on the device (prove_kernels.hip)
+// ---------------------------------------------------------------------------
+namespace {
+constexpr size_t PV_CHUNK = 16384;  // proofs per device pass (~54 KB of arena each at n = 64)
+
+struct PvArena {
+  size_t off = 0;
+  template <class T>
+  size_t take(size_t count) {
+    size_t o = off;
+    off += (count * sizeof(T) + 255) & ~(size_t)255;
+    return o;
+  }
+};
+
+// stage tables: per-term table slot, groups {t0, t1, seg} of <= PV_TPG terms, segments {g0, g1}
+struct PvStageHost {
+  std::vector<int32_t> base;
+  std::vector<int32_t> grp;  // 4 per group
+  std::vector<int32_t> seg;  // 2 per segment
+  void segment(int t0, int t1) {  // terms [t0, t1) form the next output point
+    const int s = (int)seg.size() / 2, g0 = (int)grp.size() / 4;
+    for (int t = t0; t < t1; t += PV_TPG) grp.insert(grp.end(), {t, std::min(t1, t + PV_TPG), s, 0});
+    seg.insert(seg.end(), {g0, (int)grp.size() / 4});
+  }
+};
+
+std::vector<PvStageHost> pv_stage_tables(int n, int k) {
+  std::vector<PvStageHost> st(3 + k);
+  PvStageHost& s1 = st[0];  // V | C (rho P) | D
+  s1.base = {tb_G(n), tb_H(n), tb_P(n)};
+  for (int i = 0; i < n; i++) s1.base.insert(s1.base.end(), {i, n + i});
+  s1.base.push_back(tb_P(n));
+  s1.segment(0, 2);
+  s1.segment(2, 3);
+  s1.segment(3, 2 * n + 4);
+  PvStageHost& s2 = st[1];  // T1 | T2
+  s2.base = {tb_G(n), tb_H(n), tb_G(n), tb_H(n)};
+  s2.segment(0, 2);
+  s2.segment(2, 4);
+  PvStageHost& s3 = st[2];  // H'_0 | ... | H'_{n-1} | com
+  for (int i = 0; i < n; i++) s3.base.push_back(n + i);
+  for (int i = 0; i < n; i++) s3.base.insert(s3.base.end(), {i, n + i});
+  for (int i = 0; i < n; i++) s3.segment(i, i + 1);
+  s3.segment(n, 3 * n);
+  for (int j = 0; j < k; j++) {  // L_j | R_j
+    PvStageHost& r = st[3 + j];
+    const int m = n >> (j + 1);
+    for (int t = 0; t < n; t++) r.base.push_back((t % (2 * m)) >= m ? t : n + t);
+    r.base.push_back(tb_Q(n));
+    for (int t = 0; t < n; t++) r.base.push_back((t % (2 * m)) < m ? t : n + t);
+    r.base.push_back(tb_Q(n));
+    r.segment(0, n + 1);
+    r.segment(n + 1, 2 * n + 2);
+  }
+  return st;
+}
+}  // namespace
+
+extern "C" {
+
+int fts_rp_prove_batch_gpu(fts_ctx* c, size_t N, const uint64_t* values, const uint8_t* bfs, uint64_t seed,
+                           uint8_t* out, size_t out_cap, size_t* offsets, size_t* lens, uint8_t* com64_out) {
+  if (!c || !values || !bfs || !out || !offsets || !lens || !com64_out || N > (size_t)(1u << 24))
+    return FTS_API_EINVAL;
+  if (N == 0) return FTS_API_OK;
+  if (c->device < 0) return FTS_API_EDEVICE;
+  const int n = c->n, k = c->k;
+  HIP_OK(hipSetDevice(c->device));
+  LaneGuard lg(c);
+  Lane& L = *lg.L;
+  // stage tables (proof-independent), uploaded once per call
+  const std::vector<PvStageHost> sth = pv_stage_tables(n, k);
+  std::vector<int32_t> tab;
+  std::vector<size_t> tb_off;
+  for (const PvStageHost& s : sth)
+    for (const std::vector<int32_t>* v : {&s.base, &s.grp, &s.seg}) {
+      while (tab.size() % 4) tab.push_back(0);  // int4 alignment of the group arrays
+      tb_off.push_back(tab.size());
+      tab.insert(tab.end(), v->begin(), v->end());
+    }
+  const size_t B0 = std::min(N, PV_CHUNK);
+  PvArena ar;
+  const size_t o_tab = ar.take<int32_t>(tab.size()), o_val = ar.take<uint64_t>(B0),
+               o_rnd = ar.take<uint32_t>(B0 * pv_nrnd(n) * 8), o_bf = ar.take<uint32_t>(B0 * 8),
+               o_st = ar.take<uint32_t>(B0 * pv_nst(n) * 8), o_terms = ar.take<uint32_t>(B0 * pv_tmax(n) * 8),
+               o_part = ar.take<uint32_t>(B0 * pv_gmax(n) * 24), o_jac = ar.take<uint32_t>(B0 * (n + 1) * 24),
+               o_aff = ar.take<uint32_t>(B0 * (n + 1) * 16), o_hp = ar.take<uint8_t>(B0 * (n + 1) * 64),
+               o_out = ar.take<uint8_t>(B0 * pv_npts(k) * 64), o_fr = ar.take<uint32_t>(B0 * PV_NFR * 8),
+               o_ch = ar.take<uint32_t>(B0 * rp_nch(k) * 8), o_sc = ar.take<uint32_t>(B0 * RP_NSC * 8),
+               o_status = ar.take<int32_t>(B0), o_x0 = ar.take<uint8_t>(B0 * x0_var_bytes(n)),
+               o_hs = ar.take<uint8_t>(B0 * PV_HSLOT);
+  if (L.ws.pv.ensure(ar.off)) return FTS_API_ENOMEM;
+  uint8_t* base = L.ws.pv.as<uint8_t>();
+  // pinned staging: inputs [values | rnd | bf], outputs [points | scalars]
+  const size_t in_bytes = B0 * (8 + pv_nrnd(n) * 32 + 32), out_pts_b = B0 * pv_npts(k) * 64,
+               out_fr_b = B0 * PV_NFR * 32;
+  uint8_t* stg = L.stage_buf(in_bytes + out_pts_b + out_fr_b);
+  if (!stg) return FTS_API_ENOMEM;
+  HIP_OK(hipMemcpyAsync(base + o_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, L.s));
+  HIP_OK(hipMemsetAsync(base + o_status, 0, B0 * 4, L.s));
+  PvStage stages[3 + 16];
+  for (size_t s = 0; s < sth.size(); s++) {
+    const int32_t* tb = reinterpret_cast<const int32_t*>(base + o_tab);
+    stages[s].T = (int)sth[s].base.size();
+    stages[s].G = (int)sth[s].grp.size() / 4;
+    stages[s].S = (int)sth[s].seg.size() / 2;
+    stages[s].base = tb + tb_off[3 * s];
+    stages[s].grp = reinterpret_cast<const int4*>(tb + tb_off[3 * s + 1]);
+    stages[s].seg = reinterpret_cast<const int2*>(tb + tb_off[3 * s + 2]);
+  }
+  std::vector<std::string> der(N);
+  for (size_t p0 = 0; p0 < N; p0 += B0) {
+    const size_t B = std::min(B0, N - p0);
+    uint64_t* h_val = reinterpret_cast<uint64_t*>(stg);
+    uint32_t* h_rnd = reinterpret_cast<uint32_t*>(stg + B0 * 8);
+    uint32_t* h_bf = reinterpret_cast<uint32_t*>(stg + B0 * 8 + B0 * pv_nrnd(n) * 32);
+    // randomness in the host prover's draw order (prove_range): rho, eta, (rl_i, rr_i), tau1, tau2
+    parallel_for(B, 256, [&](size_t i) {
+      const size_t g = p0 + i;
+      h_val[i] = values[g];
+      Rng rng(seed + g);
+      uint32_t* R = h_rnd + i * pv_nrnd(n) * 8;
+      for (int r = 0; r < pv_nrnd(n); r++) fr_canon_words(rng.fr(), R + r * 8);
+      fr_canon_words(fr_from_be(bfs + 32 * g), h_bf + i * 8);
+    });
+    HIP_OK(hipMemcpyAsync(base + o_val, h_val, B * 8, hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(base + o_rnd, h_rnd, B * pv_nrnd(n) * 32, hipMemcpyHostToDevice, L.s));
+    HIP_OK(hipMemcpyAsync(base + o_bf, h_bf, B * 32, hipMemcpyHostToDevice, L.s));
+    PvDev d;
+    d.B = (int)B, d.n = n, d.k = k;
+    d.tables = c->d_tables;
+    d.values = reinterpret_cast<const uint64_t*>(base + o_val);
+    d.rnd = reinterpret_cast<const uint32_t*>(base + o_rnd);
+    d.bf = reinterpret_cast<const uint32_t*>(base + o_bf);
+    d.st = reinterpret_cast<uint32_t*>(base + o_st);
+    d.terms = reinterpret_cast<uint32_t*>(base + o_terms);
+    d.partial = reinterpret_cast<uint32_t*>(base + o_part);
+    d.jac = reinterpret_cast<uint32_t*>(base + o_jac);
+    d.aff = reinterpret_cast<uint32_t*>(base + o_aff);
+    d.hp_be = base + o_hp;
+    d.out_pts = base + o_out;
+    d.out_fr = reinterpret_cast<uint32_t*>(base + o_fr);
+    d.ch = reinterpret_cast<uint32_t*>(base + o_ch);
+    d.sc_ip = reinterpret_cast<uint32_t*>(base + o_sc);
+    d.status = reinterpret_cast<int32_t*>(base + o_status);
+    d.x0_msgs = base + o_x0;
+    d.hslot = base + o_hs;
+    L.tl.begin(L.s);
+    launch_rp_prove(d, stages, c->d_x0const, c->d_x0tmpl, L.s, &L.tl);
+    HIP_OK(hipGetLastError());
+    uint8_t* h_pts = stg + in_bytes;
+    uint32_t* h_fr = reinterpret_cast<uint32_t*>(stg + in_bytes + out_pts_b);
+    HIP_OK(hipMemcpyAsync(h_pts, base + o_out, B * pv_npts(k) * 64, hipMemcpyDeviceToHost, L.s));
+    HIP_OK(hipMemcpyAsync(h_fr, base + o_fr, B * PV_NFR * 32, hipMemcpyDeviceToHost, L.s));
+    HIP_OK(L.sync());
+    bool bad = false;
+    parallel_for(B, 256, [&](size_t i) {
+      const uint8_t* P = h_pts + i * pv_npts(k) * 64;
+      const uint32_t* F = h_fr + i * PV_NFR * 8;
+      auto pt = [&](int slot) {
+        G1A a;
+        if (!g1_from_bytes(P + slot * 64, 64, a)) bad = true;
+        return a;
+      };
+      auto fr = [&](int slot) {
+        uint64_t w[4];
+        for (int q = 0; q < 4; q++) w[q] = (uint64_t)F[slot * 8 + 2 * q] | ((uint64_t)F[slot * 8 + 2 * q + 1] << 32);
+        return to_mont<ModR>(w);
+      };
+      RangeProofOut ro;
+      ro.T1 = pt(PV_T1), ro.T2 = pt(PV_T2), ro.C = pt(PV_C), ro.D = pt(PV_D);
+      ro.tau = fr(PV_F_TAU), ro.delta = fr(PV_F_DELTA), ro.ip = fr(PV_F_IP), ro.a = fr(PV_F_A), ro.b = fr(PV_F_B);
+      for (int j = 0; j < k; j++) {
+        ro.L.push_back(pt(PV_L(j)));
+        ro.R.push_back(pt(PV_R(j)));
+      }
+      der[p0 + i] = ro.serialize();
+      memcpy(com64_out + 64 * (p0 + i), P + PV_V * 64, 64);
+    });
+    if (bad) return FTS_API_EDEVICE;  // a device point failed its own encoding check
+    collect_timings(c, L, nullptr);
+  }
+  size_t off = 0;
+  for (size_t i = 0; i < N; i++) {
+    offsets[i] = off;
+    lens[i] = der[i].size();
+    if (off + der[i].size() > out_cap) return FTS_API_ESIZE;
+    memcpy(out + off, der[i].data(), der[i].size());
+    off += der[i].size();
+  }
   return FTS_API_OK;
 }
 

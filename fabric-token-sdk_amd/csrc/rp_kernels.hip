@@ -1079,3 +1079,15 @@ void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, hipStream_t
 }
 
 }  // namespace fts
+
+namespace fts {
+// x0 = Hz(DER(Arr(H'..., G..., Q, com), "||", Zb(ip))) for B proofs whose
+// H'/com BE points are in hp_be and ip in sc (RP_SC_IP): the prover's entry
+// to the same transcript kernels (prove_kernels.hip)
+void launch_x0(int B, int n, int k, const int32_t* status, const uint8_t* hp_be, const uint8_t* x0_const,
+               const uint8_t* x0_tmpl, const uint32_t* sc, uint8_t* msgs, uint32_t* ch, hipStream_t s) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s, B, n, status, hp_be, x0_const, sc, msgs);
+  FTS_LAUNCH(k_rp_x0_hash, B, 64, s, B, n, k, status, msgs, x0_tmpl, ch);
+}
+}  // namespace fts

@@ -252,6 +252,21 @@ class PublicParams:
         raw = out.raw
         return [raw[offs[i]:offs[i] + lens[i]] for i in range(n)], [coms.raw[64 * i:64 * i + 64] for i in range(n)]
 
+    def prove_range_batch_gpu(self, values, bfs, seed):
+        """rangeProver.Prove for a batch on the device (fts_rp_prove_batch_gpu): the
+        same proofs as prove_range_batch (proof i seeded with seed + i)."""
+        n = len(values)
+        vals = (C.c_uint64 * n)(*values)
+        cap = n * (1500 + 150 * self.rounds) + 4096
+        out = C.create_string_buffer(cap)
+        offs = (C.c_size_t * n)()
+        lens = (C.c_size_t * n)()
+        coms = C.create_string_buffer(64 * n)
+        L.check("fts_rp_prove_batch_gpu", L.lib.fts_rp_prove_batch_gpu(
+            self._ctx, n, vals, b"".join(bfs), seed, out, cap, offs, lens, coms))
+        raw = out.raw
+        return [raw[offs[i]:offs[i] + lens[i]] for i in range(n)], [coms.raw[64 * i:64 * i + 64] for i in range(n)]
+
     def prove_transfer(self, ttype, in_values, in_bfs, out_values, out_bfs, seed):
         buf = C.create_string_buffer(1 << 16)
         ln = C.c_size_t()

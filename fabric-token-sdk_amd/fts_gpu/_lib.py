@@ -36,7 +36,7 @@ EXPORTED = [
     "fts_status_str", "fts_rp_prove", "fts_rp_prove_batch", "fts_token_commit",
     "fts_transfer_prove", "fts_issue_prove", "fts_debug_rp_intermediates",
     "fts_debug_msm_stats", "fts_msm_g1", "fts_msm_stage", "fts_msm_run", "fts_msm_timings", "fts_msm_free",
-    "fts_request_verify_batch", "fts_request_inspect", "fts_token_open_batch",
+    "fts_request_verify_batch", "fts_request_inspect", "fts_token_open_batch", "fts_rp_prove_batch_gpu",
 ]
 
 
@@ -102,6 +102,8 @@ def _load():
         "fts_request_verify_batch": ([P, S, C.POINTER(C.c_void_p), C.POINTER(S), I32P, I32P, I32P], C.c_int),
         "fts_request_inspect": ([U8P, S, I32P, I32P, I32P, I32P, I32P, I32P], C.c_int),
         "fts_token_open_batch": ([P, S, C.POINTER(TokenOpening), I32P], C.c_int),
+        "fts_rp_prove_batch_gpu": ([P, S, C.POINTER(C.c_uint64), U8P, C.c_uint64, P, S, C.POINTER(S),
+                                    C.POINTER(S), P], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

@@ -240,6 +240,14 @@ int fts_rp_prove(const fts_ctx* ctx, uint64_t value, const uint8_t* bf32, uint64
 int fts_rp_prove_batch(const fts_ctx* ctx, size_t n, const uint64_t* values, const uint8_t* bfs, uint64_t seed,
                        int threads, uint8_t* out, size_t out_cap, size_t* offsets, size_t* lens,
                        uint8_t* com64_out);
+/* Batched range-proof prover on the device: rangeProver.Prove
+ * (rp/bulletproof.go:209-249, preprocess :336-466, IPA prover ipa.go:158-186,267-322) for n
+ * proofs in device passes of up to 16,384 (prove_kernels.hip).  Same arguments and output as
+ * fts_rp_prove_batch -- byte-identical proofs for the same seed (proof i uses seed + i; the
+ * host draws the randomness, the device computes every group element, transcript and
+ * Fiat-Shamir challenge).  Needs a device context. */
+int fts_rp_prove_batch_gpu(fts_ctx* ctx, size_t n, const uint64_t* values, const uint8_t* bfs, uint64_t seed,
+                           uint8_t* out, size_t out_cap, size_t* offsets, size_t* lens, uint8_t* com64_out);
 /* Token commitments (token.go:208-217): tok = H(type)*ped0 + value*ped1 + bf*ped2 */
 int fts_token_commit(const fts_ctx* ctx, const uint8_t* type, size_t type_len, uint64_t value,
                      const uint8_t* bf32, uint8_t* com64_out);
