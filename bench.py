@@ -81,7 +81,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall-time bound of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    ap.add_argument("--workload", choices=["rp", "msm", "transfer", "mixed", "request", "audit"], default="rp")
+    ap.add_argument("--workload", choices=["rp", "msm", "transfer", "mixed", "request", "audit", "prove"], default="rp")
     ap.add_argument("--tokens", type=int, default=65536, help="audit workload: token openings per GPU per step")
     ap.add_argument("--msm-log", type=int, default=20, help="msm workload: log2 of the point count")
     ap.add_argument("--transfers", type=int, default=8192, help="transfer/mixed workloads: transfers per GPU per step")
@@ -96,6 +96,8 @@ def main():
         return bench_mixed(args)
     if args.workload == "audit":
         return bench_audit(args)
+    if args.workload == "prove":
+        return bench_prove(args)
     if args.workload == "request":
         return bench_transfer(args, raw_requests=True)
 
@@ -473,6 +475,77 @@ def bench_msm(args):
             "roofline": _roofline_from(kt, args.steps), "cpu_baseline": cpu,
             "kernel_ms": {k: round(v[0] / args.steps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),
             flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_prove(args):
+    """batched range-proof proving (rangeProver.Prove,
+    bulletproof.go:209-249) on the device.  One step = one fts_rp_prove_batch_gpu
+    over --batch proofs (host randomness draw + DER serialisation included)."""
+    world, rank, local, dist = _dist_setup()
+    import random
+    import fts_gpu
+    with open(os.path.join(ROOT, "tests", "golden", "zkatdlog_pp.json"), "rb") as f:
+        pp_raw = f.read()
+    pp = fts_gpu.PublicParams(pp_raw, bit_length=args.bits, device=local)
+    n = args.batch
+    rng = random.Random(0xF7A500B0 + rank)
+    vals = [rng.randrange(1 << args.bits) for _ in range(n)]
+    bfs = [rng.randrange(R_ORDER).to_bytes(32, "big") for _ in range(n)]
+    proofs, coms = pp.prove_range_batch_gpu(vals, bfs, seed=1)
+    st = pp.verify_range_proofs(proofs, coms)
+    assert int((st != 0).sum()) == 0, "device proofs rejected"
+    for _ in range(max(0, args.warmup - 1)):
+        pp.prove_range_batch_gpu(vals, bfs, seed=1)
+    if dist is not None:
+        dist.barrier()
+
+    class Step:  # concurrent calls run on different device lanes: host work overlaps device work
+        def __init__(self, i):
+            self.i, self.s = i, 0
+
+        def verify(self):
+            self.s += 1
+            return pp.prove_range_batch_gpu(vals, bfs, seed=1 + (self.i * 1000 + self.s) * n)
+
+    elapsed, _ = _run_action_steps([Step(i) for i in range(max(1, args.action_inflight))], args.steps, None, None)
+    elapsed = _max_over_ranks(dist, elapsed)
+    value = world * n * args.steps / elapsed
+    kt = {}  # one call alone on the GPU (per-kernel view)
+    reps = 2
+    for s in range(reps):
+        pp.prove_range_batch_gpu(vals, bfs, seed=1)
+        for name, (ms, mads) in pp.last_timings_ex().items():
+            o = kt.get(name, (0.0, 0.0))
+            kt[name] = (o[0] + ms, mads)
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        done, cs = 0, 0.0
+        while cs < args.cpu_seconds and done < n:
+            c = min(1024, n - done)
+            t1 = time.perf_counter()
+            h, _ = pp.prove_range_batch(vals[done:done + c], bfs[done:done + c], seed=1 + done, threads=thr)
+            cs += time.perf_counter() - t1
+            assert h[0] == proofs[done], "host and device proofs differ"
+            done += c
+        cpu = {"value": round(done / cs, 1), "unit": "rp64 proofs/s", "cores": thr, "kind": "port",
+               "sample": "%d of the same proofs, the library's host prover (C++ restatement of rangeProver.Prove "
+                         "with 16-bit fixed-base tables, byte-identical output), %d threads, %.1f s wall"
+                         % (done, thr, cs)}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "range-proof proves/sec (BN254, %d-bit)" % args.bits, "value": round(value, 1),
+            "unit": "proofs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32 (BN254 Fp/Fr 8x32-bit Montgomery)",
+            "data": "synthetic: %d seeded values / blinding factors (seed 0xF7A500B0 + rank)" % n,
+            "config": {"workload": "SURVEY 8f rank 2: %d range proofs per GPU per step via fts_rp_prove_batch_gpu, "
+                                   "%d calls in flight" % (n, max(1, args.action_inflight)), "batch_per_gpu": n, "bit_length": args.bits,
+                       "parallelism": "shard%d" % world},
+            "roofline": _roofline_from(kt, reps), "cpu_baseline": cpu, "inflight": max(1, args.action_inflight),
+            "kernel_ms": {k: round(v[0] / reps, 4) for k, v in kt.items()}}), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

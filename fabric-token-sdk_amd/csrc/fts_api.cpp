@@ -1969,6 +1969,7 @@ int fts_rp_prove_batch_gpu(fts_ctx* c, size_t N, const uint64_t* values, const u
     uint32_t* h_rnd = reinterpret_cast<uint32_t*>(stg + B0 * 8);
     uint32_t* h_bf = reinterpret_cast<uint32_t*>(stg + B0 * 8 + B0 * pv_nrnd(n) * 32);
     // randomness in the host prover's draw order (prove_range): rho, eta, (rl_i, rr_i), tau1, tau2
+    const double h0 = now_ms();
     parallel_for(B, 256, [&](size_t i) {
       const size_t g = p0 + i;
       h_val[i] = values[g];
@@ -1999,6 +2000,7 @@ int fts_rp_prove_batch_gpu(fts_ctx* c, size_t N, const uint64_t* values, const u
     d.status = reinterpret_cast<int32_t*>(base + o_status);
     d.x0_msgs = base + o_x0;
     d.hslot = base + o_hs;
+    const double h1 = now_ms();
     L.tl.begin(L.s);
     launch_rp_prove(d, stages, c->d_x0const, c->d_x0tmpl, L.s, &L.tl);
     HIP_OK(hipGetLastError());
@@ -2006,7 +2008,9 @@ int fts_rp_prove_batch_gpu(fts_ctx* c, size_t N, const uint64_t* values, const u
     uint32_t* h_fr = reinterpret_cast<uint32_t*>(stg + in_bytes + out_pts_b);
     HIP_OK(hipMemcpyAsync(h_pts, base + o_out, B * pv_npts(k) * 64, hipMemcpyDeviceToHost, L.s));
     HIP_OK(hipMemcpyAsync(h_fr, base + o_fr, B * PV_NFR * 32, hipMemcpyDeviceToHost, L.s));
+    const double h2 = now_ms();
     HIP_OK(L.sync());
+    const double h3 = now_ms();
     bool bad = false;
     parallel_for(B, 256, [&](size_t i) {
       const uint8_t* P = h_pts + i * pv_npts(k) * 64;
@@ -2032,6 +2036,11 @@ int fts_rp_prove_batch_gpu(fts_ctx* c, size_t N, const uint64_t* values, const u
       memcpy(com64_out + 64 * (p0 + i), P + PV_V * 64, 64);
     });
     if (bad) return FTS_API_EDEVICE;  // a device point failed its own encoding check
+    L.host_prep_ms = (float)(h1 - h0);         // randomness draw
+    L.host_enqueue_ms = (float)(h2 - h1);
+    L.host_wait_ms = (float)(h3 - h2);         // device
+    L.host_parse_ms = (float)(now_ms() - h3);  // DER serialisation
+    L.host_stage_ms = 0;
     collect_timings(c, L, nullptr);
   }
   size_t off = 0;

@@ -70,11 +70,13 @@ FTS_DEV uint8_t* pv_out(const PvDev& d, int b, int slot) {
 FTS_DEV uint32_t* pv_term(const PvDev& d, int b, int t) { return d.terms + ((size_t)b * pv_tmax(d.n) + t) * 8; }
 
 // ------------------------------------------------------------- generic sums
-// thread per (proof, group): sum of the group's terms sc_t * B_{base[t]}
+// thread per (proof, group): sum of the group's terms sc_t * B_{base[t]}.
+// Proof index fastest: the lanes of a wave walk the same bases (one table
+// at a time, TLB- and L2-friendly gathers) and run the same number of terms.
 __global__ void __launch_bounds__(64) k_pv_fbsum(PvDev d, PvStage s) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= d.B * s.G) return;
-  const int b = gid / s.G, g = gid % s.G;
+  const int g = gid / d.B, b = gid % d.B;
   const int4 gr = s.grp[g];
   G1J acc = g1j_identity();
   for (int t = gr.x; t < gr.y; t++) {
@@ -87,10 +89,11 @@ __global__ void __launch_bounds__(64) k_pv_fbsum(PvDev d, PvStage s) {
   store_g1j(d.partial + ((size_t)b * pv_gmax(d.n) + g) * 24, acc);
 }
 // thread per (proof, segment): jac[b][seg] = sum of the segment's group partials
+// (proof index fastest: a wave's lanes sum equally many partials)
 __global__ void __launch_bounds__(64) k_pv_segsum(PvDev d, PvStage s) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= d.B * s.S) return;
-  const int b = gid / s.S, q = gid % s.S;
+  const int q = gid / d.B, b = gid % d.B;
   const int2 sg = s.seg[q];
   const uint32_t* P = d.partial + (size_t)b * pv_gmax(d.n) * 24;
   G1J acc = load_g1j(P + sg.x * 24);
@@ -358,20 +361,33 @@ void launch_rp_prove(const PvDev& d, const PvStage* stages, const uint8_t* x0_co
   pv_sum(d, stages[1], s);
   hipLaunchKernelGGL(k_pv_t12, gp, bs, 0, s, d);
   tl->mark("k_pv_stage2", s, B * (stages[1].T * COST_FB + 8.0 * d.n));
-  // stage 3: a, b, H', com ; x0
+  // stage 3: a, b, H', com ; x0 (per-kernel marks: the stage is latency-heavy)
   hipLaunchKernelGGL(k_pv_stage3, gp, bs, 0, s, d);
-  pv_sum(d, stages[2], s);
+  tl->mark("k_pv_stage3_fr", s, B * 14.0 * d.n);
+  hipLaunchKernelGGL(k_pv_fbsum, dim3((unsigned)((d.B * stages[2].G + 63) / 64)), dim3(64), 0, s, d, stages[2]);
+  tl->mark("k_pv_stage3_fbsum", s, B * stages[2].T * COST_FB);
+  hipLaunchKernelGGL(k_pv_segsum, dim3((unsigned)((d.B * stages[2].S + 63) / 64)), dim3(64), 0, s, d, stages[2]);
+  tl->mark("k_pv_stage3_segsum", s, B * (stages[2].G - stages[2].S) * 16.0);
   hipLaunchKernelGGL(k_pv_hp, gp, bs, 0, s, d);
+  tl->mark("k_pv_hp", s, B * (d.n + 1) * 9.0);
   launch_x0(d.B, d.n, d.k, d.status, d.hp_be, x0_const, x0_tmpl, d.sc_ip, d.x0_msgs, d.ch, s);
-  tl->mark("k_pv_stage3", s, B * (stages[2].T * COST_FB + 12.0 * d.n));
-  // IPA rounds
+  tl->mark("k_pv_x0", s, 0);
+  // IPA rounds (round 0 per kernel, the rest as one span)
+  const PvStage& r0 = stages[3];
   for (int j = 0; j < d.k; j++) {
     hipLaunchKernelGGL(k_pv_round, gp, bs, 0, s, d, j);
-    pv_sum(d, stages[3 + j], s);
+    if (j == 0) tl->mark("k_pv_round_fr", s, B * 8.0 * d.n);
+    hipLaunchKernelGGL(k_pv_fbsum, dim3((unsigned)((d.B * stages[3 + j].G + 63) / 64)), dim3(64), 0, s, d,
+                       stages[3 + j]);
+    if (j == 0) tl->mark("k_pv_round_fbsum", s, B * r0.T * COST_FB);
+    hipLaunchKernelGGL(k_pv_segsum, dim3((unsigned)((d.B * stages[3 + j].S + 63) / 64)), dim3(64), 0, s, d,
+                       stages[3 + j]);
+    if (j == 0) tl->mark("k_pv_round_segsum", s, B * (r0.G - r0.S) * 16.0);
     hipLaunchKernelGGL(k_pv_lr, gp, bs, 0, s, d, j);
+    if (j == 0) tl->mark("k_pv_round_lr", s, B * 20.0);
   }
   hipLaunchKernelGGL(k_pv_round, gp, bs, 0, s, d, d.k);
-  tl->mark("k_pv_ipa", s, B * d.k * (stages[3].T * COST_FB + 6.0 * d.n));
+  tl->mark("k_pv_rounds_rest", s, B * (d.k - 1) * (r0.T * COST_FB + 8.0 * d.n));
 }
 
 }  // namespace fts

@@ -249,8 +249,8 @@ class PublicParams:
         coms = C.create_string_buffer(64 * n)
         L.check("fts_rp_prove_batch", L.lib.fts_rp_prove_batch(
             self._ctx, n, vals, b"".join(bfs), seed, threads, out, cap, offs, lens, coms))
-        raw = out.raw
-        return [raw[offs[i]:offs[i] + lens[i]] for i in range(n)], [coms.raw[64 * i:64 * i + 64] for i in range(n)]
+        raw, cr = out.raw, coms.raw
+        return [raw[offs[i]:offs[i] + lens[i]] for i in range(n)], [cr[64 * i:64 * i + 64] for i in range(n)]
 
     def prove_range_batch_gpu(self, values, bfs, seed):
         """rangeProver.Prove for a batch on the device (fts_rp_prove_batch_gpu): the
@@ -258,14 +258,14 @@ class PublicParams:
         n = len(values)
         vals = (C.c_uint64 * n)(*values)
         cap = n * (1500 + 150 * self.rounds) + 4096
-        out = C.create_string_buffer(cap)
+        out = np.empty(cap, dtype=np.uint8)
         offs = (C.c_size_t * n)()
         lens = (C.c_size_t * n)()
-        coms = C.create_string_buffer(64 * n)
+        coms = np.empty(64 * n, dtype=np.uint8)
         L.check("fts_rp_prove_batch_gpu", L.lib.fts_rp_prove_batch_gpu(
-            self._ctx, n, vals, b"".join(bfs), seed, out, cap, offs, lens, coms))
-        raw = out.raw
-        return [raw[offs[i]:offs[i] + lens[i]] for i in range(n)], [coms.raw[64 * i:64 * i + 64] for i in range(n)]
+            self._ctx, n, vals, b"".join(bfs), seed, out.ctypes.data, cap, offs, lens, coms.ctypes.data))
+        raw, cr = out[:offs[n - 1] + lens[n - 1]].tobytes() if n else b"", coms.tobytes()
+        return [raw[offs[i]:offs[i] + lens[i]] for i in range(n)], [cr[64 * i:64 * i + 64] for i in range(n)]
 
     def prove_transfer(self, ttype, in_values, in_bfs, out_values, out_bfs, seed):
         buf = C.create_string_buffer(1 << 16)
