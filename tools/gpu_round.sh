@@ -44,6 +44,8 @@ if [ "${EXTRA:-1}" = 1 ]; then
   step bench_transfer 300 python3 -u bench.py --workload transfer --steps 96 --warmup 4
   step bench_request 300 python3 -u bench.py --workload request --steps 96 --warmup 4
   step bench_mixed 300 python3 -u bench.py --workload mixed --transfers 4096 --steps 48 --warmup 4
-  for w in transfer request mixed; do grep '^{' $OUT/bench_$w.log | tail -1 > $OUT/bench_$w.json; done
+  step bench_audit 200 python3 -u bench.py --workload audit --steps 64 --warmup 4
+  step bench_prove 300 python3 -u bench.py --workload prove --batch 16384 --steps 12 --warmup 2
+  for w in transfer request mixed audit prove; do grep '^{' $OUT/bench_$w.log | tail -1 > $OUT/bench_$w.json; done
 fi
 echo "== done"
