@@ -68,3 +68,39 @@ struct PvDev {
 };
 
 }  // namespace fts
+
+namespace fts {
+// ---- sigma-proof provers (TypeAndSum for transfers, SameType for issues) ----
+// one action to prove; scalar inputs (canonical limbs, 8 words each):
+//   TAS [type, tbf, r_t, r_tbf, r_sum, in_v (n_in), in_bf (n_in), r_iv (n_in), r_ibf (n_in),
+//        out_v (n_out), out_bf (n_out)]
+//   ST  [type, tbf, r_t, r_bf]
+// transcript points (sp_npts): TAS [cin_i (n_in), cct, csum, in'_i, out'_j, CT, sum]; ST [CT, cm]
+// outputs (canonical): TAS [pibf_i (n_in), piv_i (n_in), ptype, ptbf, peq, chal]; ST [ptype, pbf, chal]
+struct SpAction {
+  int32_t kind;  // 0 = TypeAndSum (transfer), 1 = SameType (issue)
+  int32_t n_in, n_out;
+  int32_t sc_off;   // first input scalar
+  int32_t pt_off;   // first point slot
+  int32_t msg_off;  // transcript slot (bytes)
+  int32_t out_off;  // first output scalar
+  int32_t ct_idx;   // CT's index among the action's points
+};
+inline __host__ __device__ int sp_nsc(int kind, int n_in, int n_out) { return kind == 0 ? 5 + 4 * n_in + 2 * n_out : 4; }
+inline __host__ __device__ int sp_npts(int kind, int n_in, int n_out) { return kind == 0 ? 2 * n_in + n_out + 4 : 2; }
+inline __host__ __device__ int sp_nout(int kind, int n_in) { return kind == 0 ? 2 * n_in + 4 : 3; }
+inline __host__ __device__ uint32_t sp_msg_slot(int m) { return ((130u * m - 2u + 9u + 63u) / 64u) * 64u; }
+
+struct SpDev {
+  int A;
+  const uint32_t* tables;  // context 16-bit tables
+  int n;                   // context bit length (table slots)
+  const SpAction* act;
+  const uint32_t* sc;      // input scalars
+  uint32_t* jac;           // [points][24]
+  uint32_t* aff;           // [points][16]
+  uint8_t* be;             // [points][64]
+  uint8_t* msgs;           // transcript slots
+  uint32_t* out;           // output scalars
+};
+}  // namespace fts

@@ -14,6 +14,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <deque>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -56,6 +57,7 @@ size_t fb_words_per_base();
 // prove_kernels.hip
 void launch_rp_prove(const PvDev& d, const PvStage* stages, const uint8_t* x0_const, const uint8_t* x0_tmpl,
                      hipStream_t s, Timeline* tl);
+void launch_sigma_prove(const SpDev& d, hipStream_t s);
 // audit_kernels.hip
 void launch_open_check(int n, const uint8_t* raw, const uint32_t* sc, const uint32_t* tables, int nb,
                        int32_t* status, hipStream_t s);
@@ -113,8 +115,9 @@ struct Workspace {
   DBuf s_act, s_raw, s_owner, s_pts, s_sc, s_status, s_work, s_terms, s_aff, s_affoff, s_msgs, s_jac, s_scratch;
   DBuf open_rec;  // token opening checks: [raw n*64][scalars n*96][status n*4]
   DBuf pv;        // batched prover: one arena (prove_arena)
+  DBuf sp;        // sigma provers: one arena
   void release() {
-    for (DBuf* b : {&open_rec, &pv, &pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &terms, &scratch, &ypow, &svec, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
+    for (DBuf* b : {&open_rec, &pv, &sp, &pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &terms, &scratch, &ypow, &svec, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
                     &rp_status, &rp_ipa, &s_act, &s_raw, &s_owner, &s_pts, &s_sc, &s_status, &s_work, &s_terms, &s_aff,
                     &s_affoff, &s_msgs, &s_jac, &s_scratch, &r_key, &r_msc, &r_coef, &r_colsum, &r_fixed, &r_flag,
                     &m_keys, &m_counts, &m_offsets, &m_cursor, &m_sorted, &m_buckets, &m_segs, &m_wins, &m_out,
@@ -1910,18 +1913,13 @@ std::vector<PvStageHost> pv_stage_tables(int n, int k) {
 }
 }  // namespace
 
-extern "C" {
-
-int fts_rp_prove_batch_gpu(fts_ctx* c, size_t N, const uint64_t* values, const uint8_t* bfs, uint64_t seed,
-                           uint8_t* out, size_t out_cap, size_t* offsets, size_t* lens, uint8_t* com64_out) {
-  if (!c || !values || !bfs || !out || !offsets || !lens || !com64_out || N > (size_t)(1u << 24))
-    return FTS_API_EINVAL;
-  if (N == 0) return FTS_API_OK;
-  if (c->device < 0) return FTS_API_EDEVICE;
+// N range proofs on the device: input(i, value, bf8, rnd) supplies proof i's value, its
+// blinding factor and its 2n + 4 random scalars (canonical limbs, pv_nrnd order);
+// der[i] <- the serialized proof, com64_out[i] (optional) <- V
+using PvInput = std::function<void(size_t, uint64_t&, uint32_t*, uint32_t*)>;
+static int rp_prove_device(fts_ctx* c, Lane& L, size_t N, const PvInput& input, std::vector<std::string>& der,
+                           uint8_t* com64_out) {
   const int n = c->n, k = c->k;
-  HIP_OK(hipSetDevice(c->device));
-  LaneGuard lg(c);
-  Lane& L = *lg.L;
   // stage tables (proof-independent), uploaded once per call
   const std::vector<PvStageHost> sth = pv_stage_tables(n, k);
   std::vector<int32_t> tab;
@@ -1962,7 +1960,7 @@ int fts_rp_prove_batch_gpu(fts_ctx* c, size_t N, const uint64_t* values, const u
     stages[s].grp = reinterpret_cast<const int4*>(tb + tb_off[3 * s + 1]);
     stages[s].seg = reinterpret_cast<const int2*>(tb + tb_off[3 * s + 2]);
   }
-  std::vector<std::string> der(N);
+  der.assign(N, std::string());
   for (size_t p0 = 0; p0 < N; p0 += B0) {
     const size_t B = std::min(B0, N - p0);
     uint64_t* h_val = reinterpret_cast<uint64_t*>(stg);
@@ -1970,14 +1968,7 @@ int fts_rp_prove_batch_gpu(fts_ctx* c, size_t N, const uint64_t* values, const u
     uint32_t* h_bf = reinterpret_cast<uint32_t*>(stg + B0 * 8 + B0 * pv_nrnd(n) * 32);
     // randomness in the host prover's draw order (prove_range): rho, eta, (rl_i, rr_i), tau1, tau2
     const double h0 = now_ms();
-    parallel_for(B, 256, [&](size_t i) {
-      const size_t g = p0 + i;
-      h_val[i] = values[g];
-      Rng rng(seed + g);
-      uint32_t* R = h_rnd + i * pv_nrnd(n) * 8;
-      for (int r = 0; r < pv_nrnd(n); r++) fr_canon_words(rng.fr(), R + r * 8);
-      fr_canon_words(fr_from_be(bfs + 32 * g), h_bf + i * 8);
-    });
+    parallel_for(B, 256, [&](size_t i) { input(p0 + i, h_val[i], h_bf + i * 8, h_rnd + i * pv_nrnd(n) * 8); });
     HIP_OK(hipMemcpyAsync(base + o_val, h_val, B * 8, hipMemcpyHostToDevice, L.s));
     HIP_OK(hipMemcpyAsync(base + o_rnd, h_rnd, B * pv_nrnd(n) * 32, hipMemcpyHostToDevice, L.s));
     HIP_OK(hipMemcpyAsync(base + o_bf, h_bf, B * 32, hipMemcpyHostToDevice, L.s));
@@ -2033,7 +2024,7 @@ int fts_rp_prove_batch_gpu(fts_ctx* c, size_t N, const uint64_t* values, const u
         ro.R.push_back(pt(PV_R(j)));
       }
       der[p0 + i] = ro.serialize();
-      memcpy(com64_out + 64 * (p0 + i), P + PV_V * 64, 64);
+      if (com64_out) memcpy(com64_out + 64 * (p0 + i), P + PV_V * 64, 64);
     });
     if (bad) return FTS_API_EDEVICE;  // a device point failed its own encoding check
     L.host_prep_ms = (float)(h1 - h0);         // randomness draw
@@ -2043,6 +2034,28 @@ int fts_rp_prove_batch_gpu(fts_ctx* c, size_t N, const uint64_t* values, const u
     L.host_stage_ms = 0;
     collect_timings(c, L, nullptr);
   }
+  return FTS_API_OK;
+}
+
+extern "C" {
+
+int fts_rp_prove_batch_gpu(fts_ctx* c, size_t N, const uint64_t* values, const uint8_t* bfs, uint64_t seed,
+                           uint8_t* out, size_t out_cap, size_t* offsets, size_t* lens, uint8_t* com64_out) {
+  if (!c || !values || !bfs || !out || !offsets || !lens || !com64_out || N > (size_t)(1u << 24))
+    return FTS_API_EINVAL;
+  if (N == 0) return FTS_API_OK;
+  if (c->device < 0) return FTS_API_EDEVICE;
+  HIP_OK(hipSetDevice(c->device));
+  LaneGuard lg(c);
+  const int nr = pv_nrnd(c->n);
+  std::vector<std::string> der;
+  int rc = rp_prove_device(c, *lg.L, N, [&](size_t g, uint64_t& v, uint32_t* bf8, uint32_t* R) {
+    v = values[g];
+    Rng rng(seed + g);  // the host prover's draw order (prove_range)
+    for (int r = 0; r < nr; r++) fr_canon_words(rng.fr(), R + r * 8);
+    fr_canon_words(fr_from_be(bfs + 32 * g), bf8);
+  }, der, com64_out);
+  if (rc) return rc;
   size_t off = 0;
   for (size_t i = 0; i < N; i++) {
     offsets[i] = off;
@@ -2054,4 +2067,171 @@ int fts_rp_prove_batch_gpu(fts_ctx* c, size_t N, const uint64_t* values, const u
   return FTS_API_OK;
 }
 
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Whole transfer / issue proofs on the device: sigma prover (k_sp_prove) + the
+// range proofs of every output (rp_prove_device), byte-identical to
+// fts_transfer_prove / fts_issue_prove for the same seeds
+// ---------------------------------------------------------------------------
+static int actions_prove_device(fts_ctx* c, size_t A, const fts_action_witness* w, int issue, uint64_t seed,
+                                uint8_t* out, size_t out_cap, size_t* offsets, size_t* lens) {
+  if (!c || !w || !out || !offsets || !lens || A > (size_t)(1u << 22)) return FTS_API_EINVAL;
+  if (A == 0) return FTS_API_OK;
+  if (c->device < 0) return FTS_API_EDEVICE;
+  const int n = c->n, nr = pv_nrnd(n), kind = issue ? 1 : 0;
+  for (size_t a = 0; a < A; a++) {
+    const fts_action_witness& x = w[a];
+    const size_t nin = issue ? 0 : x.n_in;
+    if ((!issue && (!nin || !x.in_values || !x.in_bfs)) || !x.n_out || !x.out_values || !x.out_bfs ||
+        (x.type_len && !x.type) || nin > 4096 || x.n_out > 4096)
+      return FTS_API_EINVAL;
+  }
+  HIP_OK(hipSetDevice(c->device));
+  LaneGuard lg(c);
+  Lane& L = *lg.L;
+  // layout: offsets of every action's scalars / points / transcript / outputs / range proofs
+  std::vector<SpAction> act(A);
+  std::vector<size_t> rp_first(A + 1, 0);
+  size_t nsc = 0, npt = 0, nmsg = 0, nout = 0;
+  for (size_t a = 0; a < A; a++) {
+    const int nin = issue ? 0 : (int)w[a].n_in, no = (int)w[a].n_out;
+    const int m = sp_npts(kind, nin, no);
+    act[a] = SpAction{kind, nin, no, (int32_t)nsc, (int32_t)npt, (int32_t)nmsg, (int32_t)nout,
+                      kind == 0 ? 2 * nin + no + 2 : 0};
+    nsc += sp_nsc(kind, nin, no);
+    npt += m;
+    nmsg += sp_msg_slot(m);
+    nout += sp_nout(kind, nin);
+    const bool has_rc = issue || nin != 1 || no != 1;  // transfer.go:85-87 (1-in/1-out: no range proof)
+    rp_first[a + 1] = rp_first[a] + (has_rc ? no : 0);
+  }
+  const size_t NR = rp_first[A];
+  std::vector<uint32_t> h_sc(nsc * 8);
+  std::vector<uint64_t> rp_val(NR);
+  std::vector<uint32_t> rp_bf(NR * 8), rp_rnd(NR * nr * 8);
+  // host: the draws of the host prover, in its order (prove_transfer / prove_issue)
+  parallel_for(A, 64, [&](size_t a) {
+    const fts_action_witness& x = w[a];
+    const SpAction& ac = act[a];
+    uint32_t* S = h_sc.data() + (size_t)ac.sc_off * 8;
+    Rng rng(seed + a);
+    const Fr type = type_to_zr(x.type, x.type_len);
+    const Fr tbf = rng.fr();
+    fr_canon_words(type, S);
+    fr_canon_words(tbf, S + 8);
+    auto rp_draw = [&](size_t q, uint64_t v, const uint8_t* bf32) {
+      const size_t r = rp_first[a] + q;
+      rp_val[r] = v;
+      fr_canon_words(sub(fr_from_be(bf32), tbf), rp_bf.data() + r * 8);  // V = Out - CT
+      for (int t = 0; t < nr; t++) fr_canon_words(rng.fr(), rp_rnd.data() + (r * nr + t) * 8);
+    };
+    const int N = ac.n_in, M = ac.n_out;
+    if (!issue) {
+      if (rp_first[a + 1] > rp_first[a])
+        for (int j = 0; j < M; j++) rp_draw(j, x.out_values[j], x.out_bfs + 32 * j);
+      fr_canon_words(rng.fr(), S + 2 * 8);  // r_t
+      fr_canon_words(rng.fr(), S + 3 * 8);  // r_tbf
+      for (int i = 0; i < N; i++) {
+        fr_canon_words(rng.fr(), S + (5 + 2 * N + i) * 8);  // r_iv_i
+        fr_canon_words(rng.fr(), S + (5 + 3 * N + i) * 8);  // r_ibf_i
+      }
+      fr_canon_words(rng.fr(), S + 4 * 8);  // r_sum
+      for (int i = 0; i < N; i++) {
+        fr_canon_words(fr_u64(x.in_values[i]), S + (5 + i) * 8);
+        fr_canon_words(fr_from_be(x.in_bfs + 32 * i), S + (5 + N + i) * 8);
+      }
+      for (int j = 0; j < M; j++) {
+        fr_canon_words(fr_u64(x.out_values[j]), S + (5 + 4 * N + j) * 8);
+        fr_canon_words(fr_from_be(x.out_bfs + 32 * j), S + (5 + 4 * N + M + j) * 8);
+      }
+    } else {
+      fr_canon_words(rng.fr(), S + 2 * 8);  // r_t
+      fr_canon_words(rng.fr(), S + 3 * 8);  // r_bf
+      for (int j = 0; j < M; j++) rp_draw(j, x.out_values[j], x.out_bfs + 32 * j);
+    }
+  });
+  // device: sigma proofs
+  PvArena ar;
+  const size_t o_act = ar.take<SpAction>(A), o_sc = ar.take<uint32_t>(nsc * 8), o_jac = ar.take<uint32_t>(npt * 24),
+               o_aff = ar.take<uint32_t>(npt * 16), o_be = ar.take<uint8_t>(npt * 64), o_msg = ar.take<uint8_t>(nmsg),
+               o_out = ar.take<uint32_t>(nout * 8);
+  if (L.ws.sp.ensure(ar.off)) return FTS_API_ENOMEM;
+  uint8_t* base = L.ws.sp.as<uint8_t>();
+  std::vector<uint8_t> h_be(npt * 64);
+  std::vector<uint32_t> h_out(nout * 8);
+  HIP_OK(hipMemcpyAsync(base + o_act, act.data(), A * sizeof(SpAction), hipMemcpyHostToDevice, L.s));
+  HIP_OK(hipMemcpyAsync(base + o_sc, h_sc.data(), nsc * 32, hipMemcpyHostToDevice, L.s));
+  SpDev d;
+  d.A = (int)A, d.tables = c->d_tables, d.n = n;
+  d.act = reinterpret_cast<const SpAction*>(base + o_act);
+  d.sc = reinterpret_cast<const uint32_t*>(base + o_sc);
+  d.jac = reinterpret_cast<uint32_t*>(base + o_jac);
+  d.aff = reinterpret_cast<uint32_t*>(base + o_aff);
+  d.be = base + o_be;
+  d.msgs = base + o_msg;
+  d.out = reinterpret_cast<uint32_t*>(base + o_out);
+  launch_sigma_prove(d, L.s);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(h_be.data(), base + o_be, npt * 64, hipMemcpyDeviceToHost, L.s));
+  HIP_OK(hipMemcpyAsync(h_out.data(), base + o_out, nout * 32, hipMemcpyDeviceToHost, L.s));
+  HIP_OK(L.sync());
+  // device: every range proof of the batch
+  std::vector<std::string> rps;
+  if (NR) {
+    int rc = rp_prove_device(c, L, NR, [&](size_t r, uint64_t& v, uint32_t* bf8, uint32_t* R) {
+      v = rp_val[r];
+      memcpy(bf8, rp_bf.data() + r * 8, 32);
+      memcpy(R, rp_rnd.data() + r * nr * 8, (size_t)nr * 32);
+    }, rps, nullptr);
+    if (rc) return rc;
+  }
+  // host: DER (transfer.go:140-149 / issue/prover.go:100-111)
+  std::vector<std::string> der(A);
+  bool bad = false;
+  parallel_for(A, 64, [&](size_t a) {
+    const SpAction& ac = act[a];
+    const uint32_t* O = h_out.data() + (size_t)ac.out_off * 8;
+    auto fr = [&](int i) {
+      uint64_t q[4];
+      for (int t = 0; t < 4; t++) q[t] = (uint64_t)O[i * 8 + 2 * t] | ((uint64_t)O[i * 8 + 2 * t + 1] << 32);
+      return to_mont<ModR>(q);
+    };
+    G1A ct;
+    if (!g1_from_bytes(h_be.data() + ((size_t)ac.pt_off + ac.ct_idx) * 64, 64, ct)) bad = true;
+    std::vector<std::string> proofs;
+    for (size_t r = rp_first[a]; r < rp_first[a + 1]; r++) proofs.push_back(rps[r]);
+    if (!issue) {
+      const int N = ac.n_in;
+      std::vector<Fr> pibf(N), piv(N);
+      for (int i = 0; i < N; i++) pibf[i] = fr(i), piv[i] = fr(N + i);
+      std::string tas = der::values({el_g1(ct), el_fr_array(pibf), el_fr_array(piv), el_fr(fr(2 * N)),
+                                     el_fr(fr(2 * N + 1)), el_fr(fr(2 * N + 2)), el_fr(fr(2 * N + 3))});
+      der[a] = der::values({tas, proofs.empty() ? std::string() : rc_serialize(proofs)});
+    } else {
+      std::string st = der::values({el_fr(fr(0)), el_fr(fr(1)), el_fr(fr(2)), el_g1(ct)});
+      der[a] = der::values({st, rc_serialize(proofs)});
+    }
+  });
+  if (bad) return FTS_API_EDEVICE;
+  size_t off = 0;
+  for (size_t a = 0; a < A; a++) {
+    offsets[a] = off;
+    lens[a] = der[a].size();
+    if (off + der[a].size() > out_cap) return FTS_API_ESIZE;
+    memcpy(out + off, der[a].data(), der[a].size());
+    off += der[a].size();
+  }
+  return FTS_API_OK;
+}
+
+extern "C" {
+int fts_transfer_prove_batch_gpu(fts_ctx* c, size_t n, const fts_action_witness* w, uint64_t seed, uint8_t* out,
+                                 size_t out_cap, size_t* offsets, size_t* lens) {
+  return actions_prove_device(c, n, w, 0, seed, out, out_cap, offsets, lens);
+}
+int fts_issue_prove_batch_gpu(fts_ctx* c, size_t n, const fts_action_witness* w, uint64_t seed, uint8_t* out,
+                              size_t out_cap, size_t* offsets, size_t* lens) {
+  return actions_prove_device(c, n, w, 1, seed, out, out_cap, offsets, lens);
+}
 }  // extern "C"

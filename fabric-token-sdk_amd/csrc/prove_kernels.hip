@@ -391,3 +391,115 @@ void launch_rp_prove(const PvDev& d, const PvStage* stages, const uint8_t* x0_co
 }
 
 }  // namespace fts
+
+namespace fts {
+// ------------------------------------------------------------ sigma provers
+// TypeAndSum prover (transfer/typeandsum.go:189-227,280-356 as transfer.go:69-150
+// calls it) and SameType prover (issue/sametype.go:103-149), thread per action.
+// Every transcript point is a sum of two fixed-base products over ped0/ped1/ped2:
+// in'_i = In_i - CT = v_i ped1 + (bf_i - tbf) ped2 (the type terms cancel), and
+// sum = (sum v_in - sum v_out) ped1 + sumbf ped2 -- group-equal to the reference's
+// subtractions, so the affine encodings (and the challenge) are identical.
+FTS_DEV Scalar sp_canon(const Fr& m) { return fr_canon(m); }
+FTS_DEV Scalar sp_raw(const uint32_t* p) {
+  Scalar s;
+#pragma unroll
+  for (int i = 0; i < 8; i++) s.v[i] = p[i];
+  return s;
+}
+__global__ void __launch_bounds__(64) k_sp_prove(SpDev d) {
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= d.A) return;
+  const SpAction ac = d.act[a];
+  const uint32_t* S = d.sc + (size_t)ac.sc_off * 8;
+  const uint32_t* t0 = d.tables + (size_t)tb_ped0(d.n) * FB_WORDS_PER_BASE;
+  const uint32_t* t1 = d.tables + (size_t)tb_G(d.n) * FB_WORDS_PER_BASE;
+  const uint32_t* t2 = d.tables + (size_t)tb_H(d.n) * FB_WORDS_PER_BASE;
+  uint32_t* J = d.jac + (size_t)ac.pt_off * 24;
+  auto pt2 = [&](int slot, const uint32_t* ta, const Scalar& ka, const uint32_t* tb, const Scalar& kb) {
+    G1J acc = g1j_identity();
+    if (ta) fb_mul_acc(acc, ta, ka);
+    fb_mul_acc(acc, tb, kb);
+    store_g1j(J + slot * 24, acc);
+  };
+  auto mont = [&](int i) { return fr_from_canon(S + i * 8); };
+  const Fr type = mont(0), tbf = mont(1), r_t = mont(2);
+  int m;
+  if (ac.kind == 0) {
+    const int N = ac.n_in, M = ac.n_out;
+    const int IV = 5, IBF = 5 + N, RIV = 5 + 2 * N, RIBF = 5 + 3 * N, OV = 5 + 4 * N, OBF = 5 + 4 * N + M;
+    for (int i = 0; i < N; i++) pt2(i, t1, sp_raw(S + (RIV + i) * 8), t2, sp_raw(S + (RIBF + i) * 8));  // cin_i
+    pt2(N, t0, sp_raw(S + 2 * 8), t2, sp_raw(S + 3 * 8));                                           // cct
+    pt2(N + 1, nullptr, Scalar{}, t2, sp_raw(S + 4 * 8));                                           // csum
+    Fr sumv = f_zero<FrP>(), sumbf = f_zero<FrP>();
+    for (int i = 0; i < N; i++) {
+      const Fr d_bf = f_sub(mont(IBF + i), tbf);
+      sumv = f_add(sumv, mont(IV + i));
+      sumbf = f_add(sumbf, d_bf);
+      pt2(N + 2 + i, t1, sp_raw(S + (IV + i) * 8), t2, sp_canon(d_bf));                             // in'_i
+    }
+    for (int j = 0; j < M; j++) {
+      const Fr d_bf = f_sub(mont(OBF + j), tbf);
+      sumv = f_sub(sumv, mont(OV + j));
+      sumbf = f_sub(sumbf, d_bf);
+      pt2(2 * N + 2 + j, t1, sp_raw(S + (OV + j) * 8), t2, sp_canon(d_bf));                         // out'_j
+    }
+    pt2(2 * N + M + 2, t0, sp_raw(S), t2, sp_raw(S + 8));                                           // CT
+    pt2(2 * N + M + 3, t1, sp_canon(sumv), t2, sp_canon(sumbf));                                    // sum
+    m = 2 * N + M + 4;
+    // challenge over Arr(cin..., cct, csum, in'..., out'..., CT, sum)   typeandsum.go:210-221
+    uint32_t* A = d.aff + (size_t)ac.pt_off * 16;
+    batch_to_affine(J, A, m);
+    uint8_t* msg = d.msgs + ac.msg_off;
+    for (int i = 0; i < m; i++) {
+      const G1A p = load_g1a(A + i * 16);
+      store_point_be(d.be + ((size_t)ac.pt_off + i) * 64, p);
+      uint32_t pw[16];
+      g1_mont_to_be_words(p.x, p.y, pw);
+      put_hex_record(msg, 130u * i, pw, i + 1 < m);
+    }
+    const uint32_t len = 130u * m - 2u;
+    write_sha_padding_u16(msg, len);
+    uint32_t st[8];
+    sha256_blocks(msg, sha_blocks(len), st);
+    const Fr chal = f_to_mont(digest_to_fr(st));
+    uint32_t* O = d.out + (size_t)ac.out_off * 8;
+    for (int i = 0; i < N; i++) {
+      pv_put_canon(O + i * 8, f_add(fr_mul(chal, f_sub(mont(IBF + i), tbf)), mont(RIBF + i)));  // pibf_i
+      pv_put_canon(O + (N + i) * 8, f_add(fr_mul(chal, mont(IV + i)), mont(RIV + i)));          // piv_i
+    }
+    pv_put_canon(O + (2 * N) * 8, f_add(fr_mul(chal, type), r_t));
+    pv_put_canon(O + (2 * N + 1) * 8, f_add(fr_mul(chal, tbf), mont(3)));
+    pv_put_canon(O + (2 * N + 2) * 8, f_add(fr_mul(chal, sumbf), mont(4)));
+    pv_put_canon(O + (2 * N + 3) * 8, chal);
+  } else {
+    pt2(0, t0, sp_raw(S), t2, sp_raw(S + 8));          // CT
+    pt2(1, t0, sp_raw(S + 2 * 8), t2, sp_raw(S + 3 * 8));  // r_t ped0 + r_bf ped2
+    m = 2;
+    uint32_t* A = d.aff + (size_t)ac.pt_off * 16;
+    batch_to_affine(J, A, m);
+    uint8_t* msg = d.msgs + ac.msg_off;
+    for (int i = 0; i < m; i++) {
+      const G1A p = load_g1a(A + i * 16);
+      store_point_be(d.be + ((size_t)ac.pt_off + i) * 64, p);
+      uint32_t pw[16];
+      g1_mont_to_be_words(p.x, p.y, pw);
+      put_hex_record(msg, 130u * i, pw, i + 1 < m);  // Arr(CT, com)   sametype.go:127
+    }
+    const uint32_t len = 130u * m - 2u;
+    write_sha_padding_u16(msg, len);
+    uint32_t st[8];
+    sha256_blocks(msg, sha_blocks(len), st);
+    const Fr chal = f_to_mont(digest_to_fr(st));
+    uint32_t* O = d.out + (size_t)ac.out_off * 8;
+    pv_put_canon(O, f_add(fr_mul(chal, type), r_t));
+    pv_put_canon(O + 8, f_add(fr_mul(chal, tbf), mont(3)));
+    pv_put_canon(O + 16, chal);
+  }
+}
+
+void launch_sigma_prove(const SpDev& d, hipStream_t s) {
+  if (d.A <= 0) return;
+  hipLaunchKernelGGL(k_sp_prove, dim3((unsigned)((d.A + 63) / 64)), dim3(64), 0, s, d);
+}
+}  // namespace fts

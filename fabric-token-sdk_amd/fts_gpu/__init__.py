@@ -267,6 +267,44 @@ class PublicParams:
         raw, cr = out[:offs[n - 1] + lens[n - 1]].tobytes() if n else b"", coms.tobytes()
         return [raw[offs[i]:offs[i] + lens[i]] for i in range(n)], [cr[64 * i:64 * i + 64] for i in range(n)]
 
+    def _prove_actions_gpu(self, fn, actions, seed):
+        keep = []
+
+        def buf(b):
+            keep.append(C.create_string_buffer(b, len(b)) if b else None)
+            return C.cast(keep[-1], C.c_void_p) if b else None
+
+        def u64(vs):
+            keep.append((C.c_uint64 * max(1, len(vs)))(*vs))
+            return C.cast(keep[-1], C.c_void_p)
+
+        n = len(actions)
+        ws = (L.ActionWitness * n)()
+        cap = 4096
+        for w, (ttype, iv, ib, ov, ob) in zip(ws, actions):
+            w.type, w.type_len = buf(ttype), len(ttype)
+            w.n_in, w.in_values, w.in_bfs = len(iv), u64(iv), buf(b"".join(ib))
+            w.n_out, w.out_values, w.out_bfs = len(ov), u64(ov), buf(b"".join(ob))
+            cap += 1024 + 200 * len(iv) + len(ov) * (1500 + 150 * self.rounds)
+        out = np.empty(cap, dtype=np.uint8)
+        offs, lens = (C.c_size_t * n)(), (C.c_size_t * n)()
+        L.check(fn, getattr(L.lib, fn)(self._ctx, n, ws, seed, out.ctypes.data, cap, offs, lens))
+        raw = out[:offs[n - 1] + lens[n - 1]].tobytes() if n else b""
+        return [raw[offs[i]:offs[i] + lens[i]] for i in range(n)]
+
+    def prove_transfers_gpu(self, transfers, seed):
+        """transfer.NewProver(...).Prove() for a batch on the device
+        (fts_transfer_prove_batch_gpu): transfers = [(type, in_values, in_bfs,
+        out_values, out_bfs)], transfer i seeded with seed + i -- the proofs of
+        prove_transfer."""
+        return self._prove_actions_gpu("fts_transfer_prove_batch_gpu", transfers, seed)
+
+    def prove_issues_gpu(self, issues, seed):
+        """issue.NewProver(...).Prove() for a batch on the device: issues = [(type,
+        values, bfs)], issue i seeded with seed + i -- the proofs of prove_issue."""
+        return self._prove_actions_gpu("fts_issue_prove_batch_gpu",
+                                       [(t, [], [], v, b) for t, v, b in issues], seed)
+
     def prove_transfer(self, ttype, in_values, in_bfs, out_values, out_bfs, seed):
         buf = C.create_string_buffer(1 << 16)
         ln = C.c_size_t()

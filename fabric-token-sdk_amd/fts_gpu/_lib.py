@@ -37,6 +37,7 @@ EXPORTED = [
     "fts_transfer_prove", "fts_issue_prove", "fts_debug_rp_intermediates",
     "fts_debug_msm_stats", "fts_msm_g1", "fts_msm_stage", "fts_msm_run", "fts_msm_timings", "fts_msm_free",
     "fts_request_verify_batch", "fts_request_inspect", "fts_token_open_batch", "fts_rp_prove_batch_gpu",
+    "fts_transfer_prove_batch_gpu", "fts_issue_prove_batch_gpu",
 ]
 
 
@@ -57,6 +58,11 @@ class IssueItem(C.Structure):
 class TokenOpening(C.Structure):
     _fields_ = [("com64", C.c_void_p), ("type", C.c_void_p), ("type_len", C.c_size_t), ("value32", C.c_void_p),
                 ("bf32", C.c_void_p)]
+
+
+class ActionWitness(C.Structure):
+    _fields_ = [("type", C.c_void_p), ("type_len", C.c_size_t), ("n_in", C.c_size_t), ("in_values", C.c_void_p),
+                ("in_bfs", C.c_void_p), ("n_out", C.c_size_t), ("out_values", C.c_void_p), ("out_bfs", C.c_void_p)]
 
 
 def _load():
@@ -102,6 +108,10 @@ def _load():
         "fts_request_verify_batch": ([P, S, C.POINTER(C.c_void_p), C.POINTER(S), I32P, I32P, I32P], C.c_int),
         "fts_request_inspect": ([U8P, S, I32P, I32P, I32P, I32P, I32P, I32P], C.c_int),
         "fts_token_open_batch": ([P, S, C.POINTER(TokenOpening), I32P], C.c_int),
+        "fts_transfer_prove_batch_gpu": ([P, S, C.POINTER(ActionWitness), C.c_uint64, P, S, C.POINTER(S),
+                                          C.POINTER(S)], C.c_int),
+        "fts_issue_prove_batch_gpu": ([P, S, C.POINTER(ActionWitness), C.c_uint64, P, S, C.POINTER(S),
+                                       C.POINTER(S)], C.c_int),
         "fts_rp_prove_batch_gpu": ([P, S, C.POINTER(C.c_uint64), U8P, C.c_uint64, P, S, C.POINTER(S),
                                     C.POINTER(S), P], C.c_int),
     }

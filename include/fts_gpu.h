@@ -248,6 +248,26 @@ int fts_rp_prove_batch(const fts_ctx* ctx, size_t n, const uint64_t* values, con
  * Fiat-Shamir challenge).  Needs a device context. */
 int fts_rp_prove_batch_gpu(fts_ctx* ctx, size_t n, const uint64_t* values, const uint8_t* bfs, uint64_t seed,
                            uint8_t* out, size_t out_cap, size_t* offsets, size_t* lens, uint8_t* com64_out);
+/* Whole transfer / issue proofs on the device: the TypeAndSum
+ * (transfer/typeandsum.go:189-227,280-356) or SameType (issue/sametype.go:103-149) sigma
+ * proof in one kernel (thread per action), then the range proofs of every output of every
+ * action in one fts_rp_prove_batch_gpu-style pass.  Action i is seeded with seed + i and the
+ * output is byte-identical to fts_transfer_prove / fts_issue_prove.  Issues ignore n_in /
+ * in_values / in_bfs (their tokens are the outputs). */
+typedef struct {
+  const uint8_t* type;
+  size_t type_len;
+  size_t n_in;
+  const uint64_t* in_values;
+  const uint8_t* in_bfs;  /* n_in x 32 B BE */
+  size_t n_out;
+  const uint64_t* out_values;
+  const uint8_t* out_bfs; /* n_out x 32 B BE */
+} fts_action_witness;
+int fts_transfer_prove_batch_gpu(fts_ctx* ctx, size_t n, const fts_action_witness* w, uint64_t seed, uint8_t* out,
+                                 size_t out_cap, size_t* offsets, size_t* lens);
+int fts_issue_prove_batch_gpu(fts_ctx* ctx, size_t n, const fts_action_witness* w, uint64_t seed, uint8_t* out,
+                              size_t out_cap, size_t* offsets, size_t* lens);
 /* Token commitments (token.go:208-217): tok = H(type)*ped0 + value*ped1 + bf*ped2 */
 int fts_token_commit(const fts_ctx* ctx, const uint8_t* type, size_t type_len, uint64_t value,
                      const uint8_t* bf32, uint8_t* com64_out);

@@ -72,3 +72,46 @@ def test_device_prover_large_batch_verifies(gpu_pp):
     for i in idx:
         h, hc = pp.prove_range_batch([vals[i]], [bfs[i]], seed=90000 + i)
         assert h[0] == proofs[i] and hc[0] == coms[i]
+
+
+def _bf(rng):
+    return rng.randrange(1 << 250).to_bytes(32, "big")
+
+
+def test_device_transfer_prover_matches_host(gpu_pp):
+    """TypeAndSum + range proofs on the device == host prove_transfer (1-in/1-out: no range
+    proofs, transfer.go:85-87); the device verifier accepts them"""
+    pp = gpu_pp(64)
+    rng = random.Random(11)
+    trs = []
+    for nin, nout in [(2, 2), (1, 1), (1, 2), (3, 1), (2, 3)]:
+        iv = [rng.randrange(1 << 40) for _ in range(nin)]
+        tot = sum(iv)
+        ov = [rng.randrange(tot + 1) for _ in range(nout - 1)] if nout > 1 else []
+        ov = [min(v, tot - sum(ov[:i])) for i, v in enumerate(ov)]
+        ov.append(tot - sum(ov))
+        trs.append((b"ABC" if nin % 2 else b"USD", iv, [_bf(rng) for _ in iv], ov, [_bf(rng) for _ in ov]))
+    dev = pp.prove_transfers_gpu(trs, seed=500)
+    for i, (t, iv, ib, ov, ob) in enumerate(trs):
+        assert dev[i] == pp.prove_transfer(t, iv, ib, ov, ob, seed=500 + i), i
+    items = [([pp.token_commit(t, v, b) for v, b in zip(iv, ib)], [pp.token_commit(t, v, b) for v, b in zip(ov, ob)],
+              dev[i]) for i, (t, iv, ib, ov, ob) in enumerate(trs)]
+    st, fi = pp.verify_transfers(items)
+    assert [int(x) for x in st] == [0] * len(trs)
+
+
+def test_device_issue_prover_matches_host(gpu_pp, oracle_pp):
+    import fts_gpu as F
+    from oracle import bn254 as bn, zkat
+    pp = gpu_pp(32)
+    rng = random.Random(12)
+    iss = [(b"ABC", [rng.randrange(1 << 32) for _ in range(m)], [_bf(rng) for _ in range(m)]) for m in (1, 4, 16)]
+    dev = pp.prove_issues_gpu(iss, seed=600)
+    for i, (t, v, b) in enumerate(iss):
+        assert dev[i] == pp.prove_issue(t, v, b, seed=600 + i), i
+    t, v, b = iss[1]
+    toks = [pp.token_commit(t, x, y) for x, y in zip(v, b)]
+    F.IssueVerifier(toks, pp).Verify(dev[1])
+    opp = oracle_pp.with_bit_length(32)
+    err, _ = zkat.issue_verify(opp, [bn.g1_from_bytes(x) for x in toks], dev[1])
+    assert err is None
