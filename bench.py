@@ -83,6 +83,8 @@ def main():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     ap.add_argument("--workload", choices=["rp", "msm", "transfer", "mixed", "request", "audit", "prove"], default="rp")
     ap.add_argument("--tokens", type=int, default=65536, help="audit workload: token openings per GPU per step")
+    ap.add_argument("--prove-kind", choices=["rp", "transfer"], default="rp",
+                    help="prove workload: standalone range proofs, or whole 2-in/2-out transfers")
     ap.add_argument("--msm-log", type=int, default=20, help="msm workload: log2 of the point count")
     ap.add_argument("--transfers", type=int, default=8192, help="transfer/mixed workloads: transfers per GPU per step")
     ap.add_argument("--action-inflight", type=int, default=3,
@@ -489,6 +491,8 @@ def bench_prove(args):
     with open(os.path.join(ROOT, "tests", "golden", "zkatdlog_pp.json"), "rb") as f:
         pp_raw = f.read()
     pp = fts_gpu.PublicParams(pp_raw, bit_length=args.bits, device=local)
+    if args.prove_kind == "transfer":
+        return _bench_prove_transfers(args, pp, world, rank, dist)
     n = args.batch
     rng = random.Random(0xF7A500B0 + rank)
     vals = [rng.randrange(1 << args.bits) for _ in range(n)]
@@ -546,6 +550,81 @@ def bench_prove(args):
                        "parallelism": "shard%d" % world},
             "roofline": _roofline_from(kt, reps), "cpu_baseline": cpu, "inflight": max(1, args.action_inflight),
             "kernel_ms": {k: round(v[0] / reps, 4) for k, v in kt.items()}}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def _bench_prove_transfers(args, pp, world, rank, dist):
+    """2-in/2-out transfers proven whole on the device (TypeAndSum + 2 range proofs each,
+    fts_transfer_prove_batch_gpu), --transfers per step"""
+    import random
+    import fts_gpu
+    rng = random.Random(0xF7A500B1 + rank)
+    n = args.transfers
+    trs = []
+    for _ in range(n):
+        a, b = rng.randrange(1 << 62), rng.randrange(1 << 62)
+        c = rng.randrange(a + b + 1)
+        trs.append((b"ABC", [a, b], [rng.randrange(R_ORDER).to_bytes(32, "big") for _ in range(2)], [c, a + b - c],
+                    [rng.randrange(R_ORDER).to_bytes(32, "big") for _ in range(2)]))
+    proofs = pp.prove_transfers_gpu(trs, seed=1)
+    chk = list(range(0, n, max(1, n // 64)))
+    items = [([pp.token_commit(t, v, b) for v, b in zip(iv, ib)], [pp.token_commit(t, v, b) for v, b in zip(ov, ob)],
+              proofs[i]) for i, (t, iv, ib, ov, ob) in ((i, trs[i]) for i in chk)]
+    st, _ = pp.verify_transfers(items)
+    assert int((st != 0).sum()) == 0, "device transfer proofs rejected"
+    if dist is not None:
+        dist.barrier()
+
+    class Step:
+        def __init__(self, i):
+            self.i, self.s = i, 0
+
+        def verify(self):
+            self.s += 1
+            return pp.prove_transfers_gpu(wb, seed=1 + (self.i * 1000 + self.s) * n)
+
+    wb = fts_gpu.WitnessBatch(trs, pp.rounds)  # packed once (host structs, reused by every call)
+    elapsed, _ = _run_action_steps([Step(i) for i in range(max(1, args.action_inflight))], args.steps, None, None)
+    elapsed = _max_over_ranks(dist, elapsed)
+    value = world * n * args.steps / elapsed
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        done, cs = 0, 0.0
+        while cs < args.cpu_seconds and done < n:
+            c = min(thr * 32, n - done)
+            t1 = time.perf_counter()
+            outs = [None] * c
+
+            def work(w):
+                for j in range(w, c, thr):
+                    t, iv, ib, ov, ob = trs[done + j]
+                    outs[j] = pp.prove_transfer(t, iv, ib, ov, ob, seed=1 + done + j)
+
+            ths = [threading.Thread(target=work, args=(w,)) for w in range(thr)]
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+            cs += time.perf_counter() - t1
+            assert outs == proofs[done:done + c], "host and device transfer proofs differ"
+            done += c
+        cpu = {"value": round(done / cs, 1), "unit": "transfer proofs/s", "cores": thr, "kind": "port",
+               "sample": "%d of the same transfers, the library's host prover (fts_transfer_prove, byte-identical "
+                         "output), %d threads, %.1f s wall" % (done, thr, cs)}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "2-in/2-out transfer proves/sec (TypeAndSum + 2 x rp64, BN254)", "value": round(value, 1),
+            "unit": "transfer proofs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32 (BN254 Fp/Fr 8x32-bit Montgomery)",
+            "data": "synthetic: %d seeded 2-in/2-out transfers of type ABC (seed 0xF7A500B1 + rank)" % n,
+            "config": {"workload": "SURVEY 8f rank 2: %d transfers per GPU per step via fts_transfer_prove_batch_gpu, "
+                                   "%d calls in flight" % (n, max(1, args.action_inflight)),
+                       "transfers_per_gpu": n, "parallelism": "shard%d" % world},
+            "cpu_baseline": cpu, "kernel_ms": {k: round(v[0], 4) for k, v in pp.last_timings_ex().items()}}),
+            flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -268,27 +268,11 @@ class PublicParams:
         return [raw[offs[i]:offs[i] + lens[i]] for i in range(n)], [cr[64 * i:64 * i + 64] for i in range(n)]
 
     def _prove_actions_gpu(self, fn, actions, seed):
-        keep = []
-
-        def buf(b):
-            keep.append(C.create_string_buffer(b, len(b)) if b else None)
-            return C.cast(keep[-1], C.c_void_p) if b else None
-
-        def u64(vs):
-            keep.append((C.c_uint64 * max(1, len(vs)))(*vs))
-            return C.cast(keep[-1], C.c_void_p)
-
-        n = len(actions)
-        ws = (L.ActionWitness * n)()
-        cap = 4096
-        for w, (ttype, iv, ib, ov, ob) in zip(ws, actions):
-            w.type, w.type_len = buf(ttype), len(ttype)
-            w.n_in, w.in_values, w.in_bfs = len(iv), u64(iv), buf(b"".join(ib))
-            w.n_out, w.out_values, w.out_bfs = len(ov), u64(ov), buf(b"".join(ob))
-            cap += 1024 + 200 * len(iv) + len(ov) * (1500 + 150 * self.rounds)
-        out = np.empty(cap, dtype=np.uint8)
+        wb = actions if isinstance(actions, WitnessBatch) else WitnessBatch(actions, self.rounds)
+        n = wb.n
+        out = np.empty(wb.cap, dtype=np.uint8)
         offs, lens = (C.c_size_t * n)(), (C.c_size_t * n)()
-        L.check(fn, getattr(L.lib, fn)(self._ctx, n, ws, seed, out.ctypes.data, cap, offs, lens))
+        L.check(fn, getattr(L.lib, fn)(self._ctx, n, wb.items, seed, out.ctypes.data, wb.cap, offs, lens))
         raw = out[:offs[n - 1] + lens[n - 1]].tobytes() if n else b""
         return [raw[offs[i]:offs[i] + lens[i]] for i in range(n)]
 
@@ -302,8 +286,9 @@ class PublicParams:
     def prove_issues_gpu(self, issues, seed):
         """issue.NewProver(...).Prove() for a batch on the device: issues = [(type,
         values, bfs)], issue i seeded with seed + i -- the proofs of prove_issue."""
-        return self._prove_actions_gpu("fts_issue_prove_batch_gpu",
-                                       [(t, [], [], v, b) for t, v, b in issues], seed)
+        if not isinstance(issues, WitnessBatch):
+            issues = WitnessBatch([(t, [], [], v, b) for t, v, b in issues], self.rounds)
+        return self._prove_actions_gpu("fts_issue_prove_batch_gpu", issues, seed)
 
     def prove_transfer(self, ttype, in_values, in_bfs, out_values, out_bfs, seed):
         buf = C.create_string_buffer(1 << 16)
@@ -516,6 +501,36 @@ class OpeningBatch:
         cols[:, 2] = lens
         self._cols = np.ascontiguousarray(cols)
         self.items = self._cols.ctypes.data_as(C.POINTER(L.TokenOpening))
+
+
+class WitnessBatch:
+    """fts_action_witness[] over contiguous buffers: actions = [(type, in_values,
+    in_bfs, out_values, out_bfs)] (issues: empty inputs); reusable across calls."""
+
+    def __init__(self, actions, rounds=6):
+        n = self.n = len(actions)
+        cols = np.zeros((n, 8), dtype=np.uint64)
+        self._keep = []
+
+        def blob(parts, col_ptr, col_len=None, unit=1):
+            data = b"".join(parts)
+            arr = np.frombuffer(data or b"\0", dtype=np.uint8)
+            self._keep.append(arr)
+            lens = np.array([len(p) for p in parts], dtype=np.uint64)
+            offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64) if n else lens
+            cols[:, col_ptr] = arr.ctypes.data + offs
+            if col_len is not None:
+                cols[:, col_len] = lens // unit
+
+        u64 = lambda vs: np.asarray(vs, dtype=np.uint64).tobytes()  # noqa: E731
+        blob([a[0] for a in actions], 0, 1)
+        blob([u64(a[1]) for a in actions], 3, 2, 8)
+        blob([b"".join(a[2]) for a in actions], 4)
+        blob([u64(a[3]) for a in actions], 6, 5, 8)
+        blob([b"".join(a[4]) for a in actions], 7)
+        self.cap = 4096 + sum(1024 + 200 * len(a[1]) + len(a[3]) * (1500 + 150 * rounds) for a in actions)
+        self._cols = np.ascontiguousarray(cols)
+        self.items = self._cols.ctypes.data_as(C.POINTER(L.ActionWitness))
 
 
 class Auditor:
