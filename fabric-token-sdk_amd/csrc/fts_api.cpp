@@ -2235,3 +2235,39 @@ int fts_issue_prove_batch_gpu(fts_ctx* c, size_t n, const fts_action_witness* w,
   return actions_prove_device(c, n, w, 1, seed, out, out_cap, offsets, lens);
 }
 }  // extern "C"
+
+extern "C" {
+// token.Metadata.Deserialize + the opening check (auditor GetAuditInfoFor* + InspectOutput)
+int fts_token_metadata_open_batch(fts_ctx* c, size_t n, const uint8_t* com64, const uint8_t* const* meta,
+                                  const size_t* meta_len, int32_t* status) {
+  if (!c || n > (size_t)(1u << 26) || (n && (!com64 || !meta || !meta_len || !status))) return FTS_API_EINVAL;
+  if (n == 0) return FTS_API_OK;
+  std::vector<req::TokenMeta> md(n);
+  std::vector<fts_token_opening> items(n);
+  parallel_for(n, 1024, [&](size_t i) {
+    fts_token_opening& it = items[i];
+    memset(&it, 0, sizeof it);
+    req::TokenMeta& m = md[i];
+    if (!meta[i] || !req::token_metadata(meta[i], meta_len[i], m)) return;  // NULL com64 -> FTS_E_MALFORMED
+    it.com64 = com64 + 64 * i;
+    it.type = m.type;
+    it.type_len = m.type_len;
+    it.value32 = m.has_value ? m.value : nullptr;
+    it.bf32 = m.has_bf ? m.bf : nullptr;
+  });
+  return fts_token_open_batch(c, n, items.data(), status);
+}
+
+int fts_token_metadata_decode(const uint8_t* meta, size_t meta_len, int32_t* status, size_t* type_off,
+                              size_t* type_len, uint8_t* value32, uint8_t* bf32, int32_t* has) {
+  if (!status || !type_off || !type_len || !value32 || !bf32 || !has) return FTS_API_EINVAL;
+  req::TokenMeta m;
+  *status = meta && req::token_metadata(meta, meta_len, m) ? FTS_OK : FTS_E_MALFORMED;
+  *type_off = m.type ? (size_t)(m.type - meta) : 0;
+  *type_len = m.type_len;
+  memcpy(value32, m.has_value ? m.value : req::kZero64, 32);
+  memcpy(bf32, m.has_bf ? m.bf : req::kZero64, 32);
+  *has = (m.has_value ? 1 : 0) | (m.has_bf ? 2 : 0);
+  return FTS_API_OK;
+}
+}  // extern "C"

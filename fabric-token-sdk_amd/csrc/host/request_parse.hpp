@@ -503,6 +503,83 @@ inline void parse_request(const uint8_t* b, size_t n, int kind_transfer, int kin
   (void)n_iss;
 }
 
+
+// ---------------------------------------------------------------------------
+// token.Metadata.Deserialize (crypto/token/token.go:136-158) on driver.Metadata bytes:
+//   comm.UnmarshalTypedToken (services/tokens/typed.go:28-35, core/comm/token.go:45-54):
+//     asn1.Unmarshal into TypedToken{Type int32, Token []byte} = DER SEQUENCE{INTEGER,
+//     OCTET STRING}; bytes after the outer TLV and extra elements inside the SEQUENCE are
+//     ignored (Go encoding/asn1); Type must be comm.Type = 2 ("invalid token type")
+//   proto TokenMetadata{type=1 string, value=2 Zr, blinding_factor=3 Zr, issuer=4 Identity}
+//   FromZrProto (protos-go/utils/proto.go:62-72): nil message -> nil Zr; otherwise mathlib
+//     Zr.UnmarshalJSON {"curve":id,"element":b64}: NewZrFromBytes = big-endian integer
+//     (not reduced; G1.Mul uses it mod r).  Only curve 1 (BN254) is accepted here.
+// Outputs the type bytes and value / bf reduced mod r as 32 BE bytes; has_* = false for
+// a nil Zr (the caller's commit() then fails: FTS_E_MALFORMED).
+struct TokenMeta {
+  const uint8_t* type = nullptr;
+  size_t type_len = 0;
+  bool has_value = false, has_bf = false;
+  uint8_t value[32], bf[32];
+};
+// big-endian integer of any length mod r -> 32 BE bytes
+inline void be_mod_r(const uint8_t* p, size_t n, uint8_t out[32]) {
+  Fr acc = Fr::zero();
+  const Fr k256 = from_u64<ModR>(256);
+  for (size_t i = 0; i < n; i++) acc = add(mul(acc, k256), from_u64<ModR>(p[i]));
+  fr_to_be(acc, out);
+}
+inline bool zr_json_value(const Sub& z, bool& has, uint8_t out[32]) {
+  has = false;
+  if (!z.present) return true;
+  Bytes raw;
+  if (!raw_field(z.p, z.n, raw)) return false;
+  std::string js((const char*)raw.p, raw.n), el, bin;
+  long long curve = -1;
+  if (!json_int_field(js, "curve", curve) || curve != 1) return false;
+  if (!json_string_field(js, "element", el) || !b64_decode(el, bin)) return false;
+  be_mod_r((const uint8_t*)bin.data(), bin.size(), out);
+  has = true;
+  return true;
+}
+inline bool token_metadata(const uint8_t* b, size_t n, TokenMeta& m) {
+  using der::Span;
+  size_t i = 0;
+  uint8_t t;
+  Span c;
+  if (!der::read_tlv(b, n, i, t, c) || t != 0x30) return false;
+  size_t j = 0;
+  Span iv, tok;
+  if (!der::read_tlv(c.p, c.n, j, t, iv) || t != 0x02 || iv.n == 0 || iv.n > 4) return false;  // int32
+  if (iv.n > 1 && ((iv.p[0] == 0 && iv.p[1] < 0x80) || (iv.p[0] == 0xff && iv.p[1] >= 0x80))) return false;
+  int64_t type = (iv.p[0] & 0x80) ? -1 : 0;
+  for (size_t k = 0; k < iv.n; k++) type = (int64_t)(((uint64_t)type << 8) | iv.p[k]);
+  if (!der::read_tlv(c.p, c.n, j, t, tok) || t != 0x04) return false;
+  if (type != 2) return false;  // comm.Type
+  Bytes ty;
+  Sub value, bf, issuer;
+  if (!each(tok.p, tok.n, [&](const Field& x) {
+        if (x.wt != 2) return true;
+        if (x.no == 1) {
+          if (!utf8_valid(x.p, x.n)) return false;
+          ty.set(x);
+        } else if (x.no == 2) {
+          value.add(x);
+        } else if (x.no == 3) {
+          bf.add(x);
+        } else if (x.no == 4) {
+          issuer.add(x);
+        }
+        return true;
+      }))
+    return false;
+  Bytes iraw;
+  if (issuer.present && !raw_field(issuer.p, issuer.n, iraw)) return false;
+  m.type = ty.p;
+  m.type_len = ty.n;
+  return zr_json_value(value, m.has_value, m.value) && zr_json_value(bf, m.has_bf, m.bf);
+}
+
 }  // namespace req
 }  // namespace host
 }  // namespace fts

@@ -84,6 +84,19 @@ def inspect_request(raw):
     return {k: o.value for k, o in zip(keys, out)}
 
 
+def decode_metadata(raw):
+    """host-only token.Metadata.Deserialize (fts_token_metadata_decode): None if it does
+    not decode, else (type, value32 or None, bf32 or None) with value / bf mod r"""
+    st, toff, tlen, has = C.c_int32(), C.c_size_t(), C.c_size_t(), C.c_int32()
+    v, b = C.create_string_buffer(32), C.create_string_buffer(32)
+    L.check("fts_token_metadata_decode", L.lib.fts_token_metadata_decode(
+        raw, len(raw), C.byref(st), C.byref(toff), C.byref(tlen), v, b, C.byref(has)))
+    if st.value != FTS_OK:
+        return None
+    return (raw[toff.value:toff.value + tlen.value], v.raw if has.value & 1 else None,
+            b.raw if has.value & 2 else None)
+
+
 def _ptr_array(blobs):
     bufs = [C.create_string_buffer(b, len(b)) if b else None for b in blobs]
     ptrs = (C.c_void_p * len(blobs))(*[C.cast(b, C.c_void_p) if b is not None else None for b in bufs])
@@ -225,6 +238,18 @@ class PublicParams:
         st = np.zeros(ob.n, dtype=np.int32)
         L.check("fts_token_open_batch", L.lib.fts_token_open_batch(
             self._ctx, ob.n, ob.items, st.ctypes.data_as(C.POINTER(C.c_int32))))
+        return st
+
+    def check_metadata_openings(self, coms, metas):
+        """fts_token_metadata_open_batch: token.Data (64 B each) + serialized
+        driver.Metadata per output -> one verdict per output (auditor GetAuditInfoFor*
+        + InspectOutput, auditor.go:285-400,226-238)."""
+        n = len(coms)
+        assert len(metas) == n
+        bufs, ptrs, lens = _ptr_array(metas)
+        st = np.zeros(n, dtype=np.int32)
+        L.check("fts_token_metadata_open_batch", L.lib.fts_token_metadata_open_batch(
+            self._ctx, n, b"".join(coms), ptrs, lens, st.ctypes.data_as(C.POINTER(C.c_int32))))
         return st
 
     def token_commit(self, ttype, value, bf32):

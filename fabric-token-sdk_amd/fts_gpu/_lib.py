@@ -37,7 +37,8 @@ EXPORTED = [
     "fts_transfer_prove", "fts_issue_prove", "fts_debug_rp_intermediates",
     "fts_debug_msm_stats", "fts_msm_g1", "fts_msm_stage", "fts_msm_run", "fts_msm_timings", "fts_msm_free",
     "fts_request_verify_batch", "fts_request_inspect", "fts_token_open_batch", "fts_rp_prove_batch_gpu",
-    "fts_transfer_prove_batch_gpu", "fts_issue_prove_batch_gpu",
+    "fts_transfer_prove_batch_gpu", "fts_issue_prove_batch_gpu", "fts_token_metadata_open_batch",
+    "fts_token_metadata_decode",
 ]
 
 
@@ -108,6 +109,8 @@ def _load():
         "fts_request_verify_batch": ([P, S, C.POINTER(C.c_void_p), C.POINTER(S), I32P, I32P, I32P], C.c_int),
         "fts_request_inspect": ([U8P, S, I32P, I32P, I32P, I32P, I32P, I32P], C.c_int),
         "fts_token_open_batch": ([P, S, C.POINTER(TokenOpening), I32P], C.c_int),
+        "fts_token_metadata_open_batch": ([P, S, U8P, C.POINTER(C.c_void_p), C.POINTER(S), I32P], C.c_int),
+        "fts_token_metadata_decode": ([U8P, S, I32P, C.POINTER(S), C.POINTER(S), P, P, I32P], C.c_int),
         "fts_transfer_prove_batch_gpu": ([P, S, C.POINTER(ActionWitness), C.c_uint64, P, S, C.POINTER(S),
                                           C.POINTER(S)], C.c_int),
         "fts_issue_prove_batch_gpu": ([P, S, C.POINTER(ActionWitness), C.c_uint64, P, S, C.POINTER(S),

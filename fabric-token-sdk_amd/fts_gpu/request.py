@@ -122,3 +122,41 @@ def token_request(actions, signatures=(), auditor_signatures=(), version=1):
     for s in auditor_signatures:
         out += field_bytes(4, opt_bytes(1, s))
     return out
+
+
+# ----------------------------------------------------------- token metadata
+def zr_json(b32):
+    """mathlib Zr.MarshalJSON: {"curve":1,"element":b64(Zr.Bytes())}"""
+    return b'{"curve":1,"element":"' + base64.b64encode(b32) + b'"}'
+
+
+def zr(b32):
+    return field_bytes(1, zr_json(b32))
+
+
+def der_tlv(tag, body):
+    n = len(body)
+    if n < 0x80:
+        ln = bytes([n])
+    else:
+        nb = (n.bit_length() + 7) // 8
+        ln = bytes([0x80 | nb]) + n.to_bytes(nb, "big")
+    return bytes([tag]) + ln + body
+
+
+def typed_token(typ, raw):
+    """asn1.Marshal(TypedToken{Type, Token}) (services/tokens/typed.go:24-26)"""
+    ib = typ.to_bytes(max(1, (typ.bit_length() + 8) // 8), "big", signed=True)
+    return der_tlv(0x30, der_tlv(0x02, ib) + der_tlv(0x04, raw))
+
+
+def token_metadata(ttype, value32, bf32, issuer=b"", typ=2):
+    """token.Metadata.Serialize (crypto/token/token.go:160-180): TypedToken-wrapped
+    TokenMetadata{type, value, blinding_factor, issuer}; value32 / bf32 None = nil Zr"""
+    body = field_bytes(1, ttype) if ttype else b""
+    if value32 is not None:
+        body += msg(2, zr(value32))
+    if bf32 is not None:
+        body += msg(3, zr(bf32))
+    body += msg(4, field_bytes(1, issuer) if issuer else b"")
+    return typed_token(typ, body)

@@ -225,6 +225,18 @@ typedef struct {
   const uint8_t* bf32;
 } fts_token_opening;
 int fts_token_open_batch(fts_ctx* ctx, size_t n, const fts_token_opening* items, int32_t* status);
+/* The same check from the serialized form the auditor receives: meta[i] = driver.Metadata
+ * bytes of output i (ASN.1 TypedToken{2, proto TokenMetadata}), decoded as
+ * token.Metadata.Deserialize does (crypto/token/token.go:136-158; audit/auditor.go:296-300,
+ * :370-374 call it), com64 = n x 64 B token.Data.  A metadata that does not decode, or
+ * carries a nil value / blinding factor -> FTS_E_MALFORMED. */
+int fts_token_metadata_open_batch(fts_ctx* ctx, size_t n, const uint8_t* com64, const uint8_t* const* meta,
+                                  const size_t* meta_len, int32_t* status);
+/* Host-only decode of one driver.Metadata (no device): status FTS_OK / FTS_E_MALFORMED, the
+ * type as (offset, length) into meta, value / bf mod r as 32 B BE, has bit 0 / bit 1 = value /
+ * bf present (non-nil). */
+int fts_token_metadata_decode(const uint8_t* meta, size_t meta_len, int32_t* status, size_t* type_off,
+                              size_t* type_len, uint8_t* value32, uint8_t* bf32, int32_t* has);
 
 /* ---- error strings ---- */
 const char* fts_status_str(int32_t status);

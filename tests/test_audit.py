@@ -139,3 +139,55 @@ def test_c_oracle_matches_golden(oracle_pp):
     got = cref.open_check_many(oracle_pp, [_opening(c) for c in cases], threads=2)
     want = [{"ok": 0, "mismatch": 12, "malformed": 1}[c["expect"]] for c in cases]
     assert got == want
+
+
+# ------------------------------------------- serialized metadata (token.go:136-158)
+def _meta_cases():
+    """(token.Data, driver.Metadata bytes, expected) built with fts_gpu.request's writer
+    (token.Metadata.Serialize layout) from the golden openings"""
+    from fts_gpu import request as rq
+    out = []
+    for c in CASES:
+        com, t, v, bf = _opening(c)
+        if com is None:
+            continue
+        try:
+            t.decode("utf-8")
+            expect = c["expect"]
+        except UnicodeDecodeError:  # proto3 string field: invalid UTF-8 fails proto.Unmarshal
+            expect = "malformed"
+        out.append((c["name"], com, rq.token_metadata(t, v, bf), expect))
+    com, t, v, bf = _opening(CASES[0])
+    out += [("bad_typed_token_type", com, rq.token_metadata(t, v, bf, typ=3), "malformed"),
+            ("nil_value", com, rq.token_metadata(t, None, bf), "malformed"),
+            ("truncated", com, rq.token_metadata(t, v, bf)[:-5], "malformed"),
+            ("short_element", com, rq.token_metadata(t, v.lstrip(b"\0"), bf), "ok"),
+            ("issuer_set", com, rq.token_metadata(t, v, bf, issuer=b"alice"), "ok"),
+            ("trailing_bytes", com, rq.token_metadata(t, v, bf) + b"\x00\x01", "ok")]
+    return out
+
+
+def test_metadata_decode_host():
+    """fts_token_metadata_decode round-trips the writer; malformed forms are rejected"""
+    import fts_gpu
+    for name, com, meta, expect in _meta_cases():
+        d = fts_gpu.decode_metadata(meta)
+        if name in ("bad_typed_token_type", "truncated", "long_type"):
+            assert d is None, name
+            continue
+        assert d is not None, name
+        if name == "nil_value":
+            assert d[1] is None
+    c = next(c for c in CASES if c["name"] == "unreduced_value")
+    com, t, v, bf = _opening(c)
+    from oracle import bn254 as bn
+    d = fts_gpu.decode_metadata(__import__("fts_gpu").request.token_metadata(t, v, bf))
+    assert d[0] == t and int.from_bytes(d[1], "big") == int.from_bytes(v, "big") % bn.R and d[2] == bf
+
+
+@pytest.mark.gpu
+def test_gpu_metadata_openings(gpu_pp):
+    import fts_gpu as F
+    cases = _meta_cases()
+    st = gpu_pp(64).check_metadata_openings([c[1] for c in cases], [c[2] for c in cases])
+    assert [int(s) for s in st] == [_want(F, c[3]) for c in cases]
