@@ -81,7 +81,10 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall-time bound of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    ap.add_argument("--workload", choices=["rp", "msm", "transfer", "mixed", "request", "audit", "prove"], default="rp")
+    ap.add_argument("--workload", choices=["rp", "msm", "transfer", "mixed", "request", "audit", "prove", "ecdsa"],
+                    default="rp")
+    ap.add_argument("--sigs", type=int, default=65536, help="ecdsa workload: owner signatures per GPU per step")
+    ap.add_argument("--msg-len", type=int, default=1024, help="ecdsa workload: signed message bytes")
     ap.add_argument("--tokens", type=int, default=65536, help="audit workload: token openings per GPU per step")
     ap.add_argument("--prove-kind", choices=["rp", "transfer"], default="rp",
                     help="prove workload: standalone range proofs, or whole 2-in/2-out transfers")
@@ -96,6 +99,8 @@ def main():
         return bench_transfer(args)
     if args.workload == "mixed":
         return bench_mixed(args)
+    if args.workload == "ecdsa":
+        return bench_ecdsa(args)
     if args.workload == "audit":
         return bench_audit(args)
     if args.workload == "prove":
@@ -714,6 +719,115 @@ def bench_audit(args):
                        "parallelism": "shard%d" % world},
             "roofline": _roofline_from(kt, reps), "cpu_baseline": cpu,
             "kernel_ms": {k: round(v[0] / reps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),
+            flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def _ecdsa_muls_per_verify():
+    """Montgomery products one k_ecdsa_verify lane executes per valid
+    signature (csrc/ecdsa_kernels.hip; madd 11, full add 16, a=-3 dbl 8):
+    pk check 5 + s^-1 by Fermat (256 sqr + popcount(n-2) mul) + u1, u2 2 +
+    u1*G 32 madd + Q table (13 madd + 1 dbl) + 252 dbl + 60 expected adds
+    (64 nibbles x 15/16) + final add 16 + projective x-compare 3."""
+    n = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
+    return 5 + 1 + 256 + bin(n - 2).count("1") + 2 + 32 * 11 + 13 * 11 + 8 + 252 * 8 + 60 * 16 + 16 + 3
+
+
+def bench_ecdsa(args):
+    """SURVEY §8f rank 4 (x509 half): owner-signature checks of
+    TransferSignatureValidate (validator/validator_transfer.go:29-62) ->
+    ecdsa.Verifier.Verify (validator/ecdsa/ecdsa.go:82-113).  One step = one
+    fts_ecdsa_verify_batch over --sigs (message, DER signature, P-256 key)
+    triples from host buffers (DER parse, packing, upload, SHA-256 and the
+    verification on the device, verdicts back)."""
+    world, rank, local, dist = _dist_setup()
+    import random
+    import numpy as np
+    from fts_gpu import ecdsa as E
+    from oracle import ecdsa_p256 as O
+    t0 = time.time()
+    rng = random.Random(0xF7A5EC00 + rank)
+    ndist, L = 512, args.msg_len
+    keys = []
+    for _ in range(16):
+        d = rng.randrange(1, O.N)
+        Q = O.mul(d, O.G)
+        keys.append((d, Q[0].to_bytes(32, "big") + Q[1].to_bytes(32, "big")))
+    dm, ds, dp = [], [], []
+    for i in range(ndist):
+        d, pk = keys[i % len(keys)]
+        m = rng.randbytes(L)
+        dm.append(m)
+        ds.append(O.sign(d, m, rng.randrange(1, O.N)))
+        dp.append(pk)
+    n = args.sigs
+    idx = np.arange(n) % ndist
+    msg_buf = bytearray(b"".join(dm[i] for i in idx))
+    bad = np.arange(13, n, 97)  # ~1 % tampered messages
+    for j in bad:
+        msg_buf[j * L] ^= 1
+    sig_lens = np.array([len(ds[i]) for i in idx], dtype=np.uint64)
+    sig_off = np.concatenate([[0], np.cumsum(sig_lens)[:-1]]).astype(np.uint64)
+    sig_buf = b"".join(ds[i] for i in idx)
+    pk_buf = b"".join(dp[i] for i in idx)
+    msg_off = np.arange(n, dtype=np.uint64) * L
+    msg_len = np.full(n, L, dtype=np.uint64)
+    msg_buf = bytes(msg_buf)
+    want = np.zeros(n, dtype=np.int32)
+    want[bad] = E.FTS_E_SIG_INVALID
+    setup_s = time.time() - t0
+
+    def step():
+        st = E.verify_packed(msg_buf, msg_off, msg_len, sig_buf, sig_off, sig_lens, pk_buf, device=local)
+        assert (st == want).all(), "ECDSA verdicts differ"
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    if dist is not None:
+        dist.barrier()
+    t1 = time.perf_counter()
+    kt = {"k_ecdsa_digest": 0.0, "k_ecdsa_verify": 0.0}
+    for _ in range(args.steps):
+        step()
+        for k, v in E.last_timings(local).items():
+            kt[k] += v
+    elapsed = _max_over_ranks(dist, time.perf_counter() - t1)
+    value = world * n * args.steps / elapsed
+    muls = _ecdsa_muls_per_verify()
+    mads = (n - len(bad)) * muls * MAD_PER_MUL + len(bad) * muls * MAD_PER_MUL  # tampered items run the full path
+    ms = kt["k_ecdsa_verify"] / args.steps
+    ach = mads / (ms * 1e-3) / 1e12
+    roof = {"bound": "int32_valu (v_mad_u64_u32)", "kernel": "k_ecdsa_verify", "achieved": round(ach, 3),
+            "peak": round(PEAK_TMAD, 3), "unit": "TMAD/s", "frac": round(ach / PEAK_TMAD, 4), "traffic": None,
+            "kernel_ms": round(ms, 4), "mads_per_launch": mads, "muls_per_verify": muls,
+            "measured": "HIP events around each launch on the library's stream, every timed step"}
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        done, t2 = 0, time.perf_counter()
+        while time.perf_counter() - t2 < min(args.cpu_seconds, 10.0) and done < n:
+            i = int(idx[done])
+            m = msg_buf[done * L:(done + 1) * L]
+            got = O.verify(m, ds[i], (int.from_bytes(dp[i][:32], "big"), int.from_bytes(dp[i][32:], "big")))
+            assert got == want[done], "CPU oracle verdict differs"
+            done += 1
+        cs = time.perf_counter() - t2
+        cpu = {"value": round(done / cs, 1), "unit": "signatures/s", "cores": 1, "kind": "port",
+               "sample": "first %d signatures of the batch, oracle/ecdsa_p256.py (pure-Python restatement of "
+                         "Verifier.Verify, affine double-and-add), 1 thread, %.1f s wall" % (done, cs)}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "ECDSA P-256 owner signature verifies/sec (Verifier.Verify)", "value": round(value, 1),
+            "unit": "signatures/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32 (P-256 Fp/Fn 8x32-bit Montgomery)",
+            "data": "synthetic: %d distinct signatures (16 keys, %d-byte messages) from the oracle signer, tiled; "
+                    "1 %% tampered messages (seed 0xF7A5EC00 + rank)" % (ndist, L),
+            "config": {"workload": "SURVEY 8f rank 4 (x509): %d owner signatures per GPU per step via "
+                                   "fts_ecdsa_verify_batch" % n, "sigs_per_gpu": n, "msg_len": L,
+                       "parallelism": "shard%d" % world},
+            "roofline": roof, "cpu_baseline": cpu,
+            "kernel_ms": {k: round(v / args.steps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),
             flush=True)
     if dist is not None:
         dist.destroy_process_group()

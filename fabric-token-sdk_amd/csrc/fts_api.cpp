@@ -560,6 +560,9 @@ const char* fts_status_str(int32_t s) {
     case FTS_E_NOT_RUN: return "not evaluated";
     case FTS_E_ACTION_INVALID: return "invalid action";
     case FTS_E_OPEN_MISMATCH: return "does not match the provided opening";
+    case FTS_E_SIG_MALFORMED: return "asn1: signature does not deserialize";
+    case FTS_E_SIG_NOT_LOW_S: return "signature is not in lowS";
+    case FTS_E_SIG_INVALID: return "signature not valid";
     default: return "unknown status";
   }
 }

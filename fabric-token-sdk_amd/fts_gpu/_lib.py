@@ -25,6 +25,9 @@ FTS_E_ST_INVALID = 9
 FTS_E_NOT_RUN = 10
 FTS_E_ACTION_INVALID = 11
 FTS_E_OPEN_MISMATCH = 12
+FTS_E_SIG_MALFORMED = 13
+FTS_E_SIG_NOT_LOW_S = 14
+FTS_E_SIG_INVALID = 15
 
 FTS_API_OK = 0
 FTS_DEVICE_NONE = -2
@@ -38,7 +41,8 @@ EXPORTED = [
     "fts_debug_msm_stats", "fts_msm_g1", "fts_msm_stage", "fts_msm_run", "fts_msm_timings", "fts_msm_free",
     "fts_request_verify_batch", "fts_request_inspect", "fts_token_open_batch", "fts_rp_prove_batch_gpu",
     "fts_transfer_prove_batch_gpu", "fts_issue_prove_batch_gpu", "fts_token_metadata_open_batch",
-    "fts_token_metadata_decode",
+    "fts_token_metadata_decode", "fts_ecdsa_verify_batch", "fts_ecdsa_sig_parse", "fts_p256_pubkey_from_pkix",
+    "fts_ecdsa_last_timings",
 ]
 
 
@@ -59,6 +63,11 @@ class IssueItem(C.Structure):
 class TokenOpening(C.Structure):
     _fields_ = [("com64", C.c_void_p), ("type", C.c_void_p), ("type_len", C.c_size_t), ("value32", C.c_void_p),
                 ("bf32", C.c_void_p)]
+
+
+class EcdsaItem(C.Structure):
+    _fields_ = [("msg", C.c_void_p), ("msg_len", C.c_size_t), ("sig", C.c_void_p), ("sig_len", C.c_size_t),
+                ("pk64", C.c_void_p)]
 
 
 class ActionWitness(C.Structure):
@@ -117,6 +126,10 @@ def _load():
                                        C.POINTER(S)], C.c_int),
         "fts_rp_prove_batch_gpu": ([P, S, C.POINTER(C.c_uint64), U8P, C.c_uint64, P, S, C.POINTER(S),
                                     C.POINTER(S), P], C.c_int),
+        "fts_ecdsa_verify_batch": ([C.c_int, S, C.POINTER(EcdsaItem), I32P], C.c_int),
+        "fts_ecdsa_sig_parse": ([U8P, S, P, P, I32P], C.c_int),
+        "fts_p256_pubkey_from_pkix": ([U8P, S, P], C.c_int),
+        "fts_ecdsa_last_timings": ([C.c_int, C.POINTER(C.c_float)], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

@@ -55,9 +55,12 @@ enum fts_status {
   FTS_E_NOT_RUN = 10,       /* item not evaluated (batch aborted by an API error) */
   FTS_E_ACTION_INVALID = 11, /* action fails its structural Validate() before the ZK proof:
                                issue/action.go:161-185,273-282; transfer/action.go:244-283 */
-  FTS_E_OPEN_MISMATCH = 12  /* "output at index [%d] does not match the provided opening"
+  FTS_E_OPEN_MISMATCH = 12, /* "output at index [%d] does not match the provided opening"
                                audit/auditor.go:236-238; "... output does not match provided
                                opening" token/token.go:78-80 */
+  FTS_E_SIG_MALFORMED = 13, /* asn1.Unmarshal of the ECDSA signature failed   validator/ecdsa/ecdsa.go:84-87 */
+  FTS_E_SIG_NOT_LOW_S = 14, /* "signature is not in lowS"                     validator/ecdsa/ecdsa.go:103-105 */
+  FTS_E_SIG_INVALID = 15    /* "signature not valid" (ecdsa.Verify false)     validator/ecdsa/ecdsa.go:107-110 */
 };
 
 /* ---- API return codes ---- */
@@ -290,6 +293,34 @@ int fts_transfer_prove(const fts_ctx* ctx, const uint8_t* type, size_t type_len,
 /* issue.NewProver(...).Prove() */
 int fts_issue_prove(const fts_ctx* ctx, const uint8_t* type, size_t type_len, size_t n_tok, const uint64_t* values,
                     const uint8_t* bfs, uint64_t seed, uint8_t* out_der, size_t out_cap, size_t* out_len);
+
+/* ---- ECDSA P-256 owner signatures (x509 identities) ----
+ * Replaces, per item, ecdsa.Verifier.Verify(message, sigma)
+ * (validator/ecdsa/ecdsa.go:82-113; identical logic in
+ * services/identity/x509/crypto/ecdsa.go:46-77), called by
+ * TransferSignatureValidate (validator/validator_transfer.go:29-62) once per
+ * input owner.  Independent of the zkatdlog public parameters: takes a device
+ * ordinal, not an fts_ctx. */
+typedef struct {
+  const uint8_t* msg;  /* signed message; SHA-256 is computed on the device */
+  size_t msg_len;
+  const uint8_t* sig;  /* DER ECDSA-Sig-Value SEQUENCE{INTEGER r, INTEGER s} */
+  size_t sig_len;
+  const uint8_t* pk64; /* public key X||Y, 32 B big-endian each (see fts_p256_pubkey_from_pkix) */
+} fts_ecdsa_item;
+/* status[i] <- FTS_OK | FTS_E_SIG_MALFORMED | FTS_E_SIG_NOT_LOW_S | FTS_E_SIG_INVALID
+ * (an off-curve / non-canonical public key is FTS_E_SIG_INVALID, as in Go's ecdsa.Verify). */
+int fts_ecdsa_verify_batch(int device, size_t n, const fts_ecdsa_item* items, int32_t* status);
+/* Host-only: the asn1.Unmarshal + IsLowS + range part of Verify; r32/s32 <- 32 B big-endian
+ * (valid when *status == FTS_OK). */
+int fts_ecdsa_sig_parse(const uint8_t* sig, size_t sig_len, uint8_t* r32, uint8_t* s32, int32_t* status);
+/* Host-only: DER SubjectPublicKeyInfo of a P-256 key (x509.MarshalPKIXPublicKey, the body of
+ * the PEM "PUBLIC KEY" block of ecdsa.Verifier.Serialize, ecdsa.go:115-150) -> X||Y.
+ * FTS_API_EINVAL for anything else. */
+int fts_p256_pubkey_from_pkix(const uint8_t* der, size_t len, uint8_t* pk64);
+/* HIP-event durations (ms) of the last fts_ecdsa_verify_batch on `device`:
+ * ms2[0] = k_ecdsa_digest, ms2[1] = k_ecdsa_verify. */
+int fts_ecdsa_last_timings(int device, float* ms2);
 
 #ifdef __cplusplus
 }
