@@ -23,7 +23,10 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
+#include <atomic>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/fts_gpu.h"
@@ -215,6 +218,8 @@ struct DevState {
   size_t msg_cap = 0;
   uint8_t* d_rec = nullptr;  // rec | e | moff | mlen | status
   size_t rec_cap = 0;
+  uint8_t* h_stage = nullptr;  // pinned host staging
+  size_t h_cap = 0;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   float ms[2] = {0.f, 0.f};  // k_ecdsa_digest, k_ecdsa_verify of the last call
 };
@@ -301,49 +306,78 @@ int fts_ecdsa_verify_batch(int device, size_t n, const fts_ecdsa_item* items, in
     ECHK(hipStreamSynchronize(D.stream));
     D.init = true;
   }
-  // host: parse + low-S + range checks, pack records and messages
+  // host: parse + low-S + range checks, pack records and messages into one
+  // pinned staging buffer (records | e | moff | mlen | status | messages),
+  // chunks in parallel, one H2D copy
   const size_t rec_b = n * REC_WORDS * 4, e_b = n * 32, off_b = n * 8, len_b = n * 4, st_b = n * 4;
   const size_t tot = rec_b + e_b + off_b + len_b + st_b;
-  std::vector<uint8_t> h(tot);
-  uint32_t* hrec = reinterpret_cast<uint32_t*>(h.data());
-  uint64_t* hoff = reinterpret_cast<uint64_t*>(h.data() + rec_b + e_b);
-  uint32_t* hlen = reinterpret_cast<uint32_t*>(h.data() + rec_b + e_b + off_b);
-  int32_t* hst = reinterpret_cast<int32_t*>(h.data() + rec_b + e_b + off_b + len_b);
   size_t mtot = 0;
   for (size_t i = 0; i < n; i++) {
-    const fts_ecdsa_item& it = items[i];
-    uint8_t r32[32], s32[32];
-    int32_t st = FTS_E_SIG_MALFORMED;
-    if (it.msg_len > 0xffffffffu || (it.msg_len && !it.msg)) return FTS_API_EINVAL;
-    fts_ecdsa_sig_parse(it.sig, it.sig_len, r32, s32, &st);
-    if (st == FTS_OK && !it.pk64) st = FTS_E_SIG_INVALID;
-    hst[i] = st;
-    uint32_t* R = hrec + i * REC_WORDS;
-    for (int k = 0; k < 8; k++) {
-      auto be = [&](const uint8_t* b) {
-        return ((uint32_t)b[28 - 4 * k] << 24) | ((uint32_t)b[29 - 4 * k] << 16) | ((uint32_t)b[30 - 4 * k] << 8) |
-               (uint32_t)b[31 - 4 * k];
-      };
-      R[k] = be(r32);
-      R[8 + k] = be(s32);
-      R[16 + k] = st == FTS_OK ? be(it.pk64) : 0;
-      R[24 + k] = st == FTS_OK ? be(it.pk64 + 32) : 0;
-    }
-    hoff[i] = mtot;
-    hlen[i] = st == FTS_OK ? (uint32_t)it.msg_len : 0;
-    mtot += hlen[i];
+    if (items[i].msg_len > 0xffffffffu || (items[i].msg_len && !items[i].msg)) return FTS_API_EINVAL;
+    mtot += items[i].msg_len;
   }
-  std::vector<uint8_t> hm(mtot ? mtot : 1);
-  for (size_t i = 0; i < n; i++)
-    if (hlen[i]) memcpy(hm.data() + hoff[i], items[i].msg, hlen[i]);
+  const size_t need = tot + mtot;
+  if (D.h_cap < need) {
+    if (D.h_stage) hipHostFree(D.h_stage);
+    D.h_cap = need + need / 2;
+    ECHK(hipHostMalloc(&D.h_stage, D.h_cap, hipHostMallocDefault));
+  }
+  uint8_t* h = D.h_stage;
+  uint32_t* hrec = reinterpret_cast<uint32_t*>(h);
+  uint64_t* hoff = reinterpret_cast<uint64_t*>(h + rec_b + e_b);
+  uint32_t* hlen = reinterpret_cast<uint32_t*>(h + rec_b + e_b + off_b);
+  int32_t* hst = reinterpret_cast<int32_t*>(h + rec_b + e_b + off_b + len_b);
+  uint8_t* hm = h + tot;
+  {
+    uint64_t o = 0;
+    for (size_t i = 0; i < n; i++) hoff[i] = o, o += items[i].msg_len;
+  }
+  auto pack = [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; i++) {
+      const fts_ecdsa_item& it = items[i];
+      uint8_t r32[32], s32[32];
+      int32_t st = FTS_E_SIG_MALFORMED;
+      fts_ecdsa_sig_parse(it.sig, it.sig_len, r32, s32, &st);
+      if (st == FTS_OK && !it.pk64) st = FTS_E_SIG_INVALID;
+      hst[i] = st;
+      uint32_t* R = hrec + i * REC_WORDS;
+      for (int k = 0; k < 8; k++) {
+        auto be = [&](const uint8_t* b) {
+          return ((uint32_t)b[28 - 4 * k] << 24) | ((uint32_t)b[29 - 4 * k] << 16) | ((uint32_t)b[30 - 4 * k] << 8) |
+                 (uint32_t)b[31 - 4 * k];
+        };
+        R[k] = be(r32);
+        R[8 + k] = be(s32);
+        R[16 + k] = st == FTS_OK ? be(it.pk64) : 0;
+        R[24 + k] = st == FTS_OK ? be(it.pk64 + 32) : 0;
+      }
+      hlen[i] = (uint32_t)it.msg_len;
+      if (it.msg_len) memcpy(hm + hoff[i], it.msg, it.msg_len);
+    }
+  };
+  const size_t CH = 2048, nch = (n + CH - 1) / CH;
+  const unsigned hw = std::thread::hardware_concurrency();
+  const size_t nth = std::min<size_t>(nch, std::min<unsigned>(16u, hw ? hw : 1u));
+  if (nth <= 1) {
+    pack(0, n);
+  } else {
+    std::atomic<size_t> next{0};
+    auto worker = [&]() {
+      for (size_t c; (c = next.fetch_add(1)) < nch;) pack(c * CH, std::min(n, (c + 1) * CH));
+    };
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nth; t++) th.emplace_back(worker);
+    worker();
+    for (auto& t : th) t.join();
+  }
   if (D.rec_cap < tot) {
     if (D.d_rec) hipFree(D.d_rec);
     D.rec_cap = tot + tot / 2;
     ECHK(hipMalloc(&D.d_rec, D.rec_cap));
   }
-  if (D.msg_cap < hm.size()) {
+  if (D.msg_cap < std::max<size_t>(mtot, 1)) {
     if (D.d_msg) hipFree(D.d_msg);
-    D.msg_cap = hm.size() + hm.size() / 2;
+    D.msg_cap = mtot + mtot / 2 + 1;
     ECHK(hipMalloc(&D.d_msg, D.msg_cap));
   }
   uint32_t* drec = reinterpret_cast<uint32_t*>(D.d_rec);
@@ -351,8 +385,8 @@ int fts_ecdsa_verify_batch(int device, size_t n, const fts_ecdsa_item* items, in
   uint64_t* doff = reinterpret_cast<uint64_t*>(D.d_rec + rec_b + e_b);
   uint32_t* dlen = reinterpret_cast<uint32_t*>(D.d_rec + rec_b + e_b + off_b);
   int32_t* dst = reinterpret_cast<int32_t*>(D.d_rec + rec_b + e_b + off_b + len_b);
-  ECHK(hipMemcpyAsync(D.d_rec, h.data(), tot, hipMemcpyHostToDevice, D.stream));
-  ECHK(hipMemcpyAsync(D.d_msg, hm.data(), hm.size(), hipMemcpyHostToDevice, D.stream));
+  ECHK(hipMemcpyAsync(D.d_rec, h, tot, hipMemcpyHostToDevice, D.stream));
+  if (mtot) ECHK(hipMemcpyAsync(D.d_msg, hm, mtot, hipMemcpyHostToDevice, D.stream));
   const int nb = (int)((n + 255) / 256);
   ECHK(hipEventRecord(D.ev[0], D.stream));
   k_ecdsa_digest<<<nb, 256, 0, D.stream>>>((int)n, D.d_msg, doff, dlen, dst, de);
@@ -361,8 +395,9 @@ int fts_ecdsa_verify_batch(int device, size_t n, const fts_ecdsa_item* items, in
   k_ecdsa_verify<<<nb, 256, 0, D.stream>>>((int)n, drec, de, D.d_table, dst);
   ECHK(hipGetLastError());
   ECHK(hipEventRecord(D.ev[2], D.stream));
-  ECHK(hipMemcpyAsync(status, dst, st_b, hipMemcpyDeviceToHost, D.stream));
+  ECHK(hipMemcpyAsync(hst, dst, st_b, hipMemcpyDeviceToHost, D.stream));
   ECHK(hipStreamSynchronize(D.stream));
+  memcpy(status, hst, st_b);
   ECHK(hipEventElapsedTime(&D.ms[0], D.ev[0], D.ev[1]));
   ECHK(hipEventElapsedTime(&D.ms[1], D.ev[1], D.ev[2]));
   return FTS_API_OK;
