@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -209,11 +210,12 @@ bool der_int(const uint8_t* p, size_t L, bool& neg, bool& zero, bool& big, uint8
 
 int cmp32(const uint8_t* a, const uint8_t* b) { return memcmp(a, b, 32); }
 
-struct DevState {
-  std::mutex mu;
-  bool init = false;
+// One staging slot per concurrent call: its own stream, device buffers and
+// pinned host staging, so one call's host parse/pack overlaps another's kernels.
+constexpr int NSLOT = 3;
+struct Slot {
   hipStream_t stream = nullptr;
-  uint32_t* d_table = nullptr;
+  uint32_t* d_table = nullptr;  // the device's shared table
   uint8_t* d_msg = nullptr;
   size_t msg_cap = 0;
   uint8_t* d_rec = nullptr;  // rec | e | moff | mlen | status
@@ -221,9 +223,30 @@ struct DevState {
   uint8_t* h_stage = nullptr;  // pinned host staging
   size_t h_cap = 0;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  float ms[2] = {0.f, 0.f};  // k_ecdsa_digest, k_ecdsa_verify of the last call
+  float ms[2] = {0.f, 0.f};
+};
+struct DevState {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool init = false;
+  uint32_t* d_table = nullptr;
+  Slot slot[NSLOT];
+  bool busy[NSLOT] = {false, false, false};
+  float ms[2] = {0.f, 0.f};  // k_ecdsa_digest, k_ecdsa_verify of the last finished call
 };
 DevState g_dev[16];
+
+struct SlotGuard {
+  DevState& G;
+  int k;
+  ~SlotGuard() {
+    std::lock_guard<std::mutex> l(G.mu);
+    G.ms[0] = G.slot[k].ms[0];
+    G.ms[1] = G.slot[k].ms[1];
+    G.busy[k] = false;
+    G.cv.notify_one();
+  }
+};
 
 #define ECHK(x)                                 \
   do {                                          \
@@ -294,18 +317,38 @@ int fts_ecdsa_verify_batch(int device, size_t n, const fts_ecdsa_item* items, in
   if (n == 0) return FTS_API_OK;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) return FTS_API_EDEVICE;
-  DevState& D = g_dev[device];
-  std::lock_guard<std::mutex> g(D.mu);
-  ECHK(hipSetDevice(device));
-  if (!D.init) {
-    ECHK(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking));
-    ECHK(hipMalloc(&D.d_table, (size_t)32 * 256 * 16 * 4));
-    for (auto& e : D.ev) ECHK(hipEventCreate(&e));
-    k_ecdsa_table<<<32, 256, 0, D.stream>>>(D.d_table);
-    ECHK(hipGetLastError());
-    ECHK(hipStreamSynchronize(D.stream));
-    D.init = true;
+  DevState& G = g_dev[device];
+  int k = -1;
+  {
+    std::unique_lock<std::mutex> l(G.mu);
+    ECHK(hipSetDevice(device));
+    if (!G.init) {
+      hipStream_t s0;
+      ECHK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
+      ECHK(hipMalloc(&G.d_table, (size_t)32 * 256 * 16 * 4));
+      k_ecdsa_table<<<32, 256, 0, s0>>>(G.d_table);
+      ECHK(hipGetLastError());
+      ECHK(hipStreamSynchronize(s0));
+      ECHK(hipStreamDestroy(s0));
+      for (auto& S : G.slot) {
+        ECHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
+        for (auto& e : S.ev) ECHK(hipEventCreate(&e));
+        S.d_table = G.d_table;
+      }
+      G.init = true;
+    }
+    G.cv.wait(l, [&] {
+      for (int j = 0; j < NSLOT; j++)
+        if (!G.busy[j]) return true;
+      return false;
+    });
+    for (int j = 0; j < NSLOT && k < 0; j++)
+      if (!G.busy[j]) k = j;
+    G.busy[k] = true;
   }
+  SlotGuard guard{G, k};
+  Slot& D = G.slot[k];
+  ECHK(hipSetDevice(device));
   // host: parse + low-S + range checks, pack records and messages into one
   // pinned staging buffer (records | e | moff | mlen | status | messages),
   // chunks in parallel, one H2D copy
@@ -405,7 +448,7 @@ int fts_ecdsa_verify_batch(int device, size_t n, const fts_ecdsa_item* items, in
 
 int fts_ecdsa_last_timings(int device, float* ms2) {
   if (device < 0 || device >= 16 || !ms2) return FTS_API_EINVAL;
-  std::lock_guard<std::mutex> g(g_dev[device].mu);
+  std::lock_guard<std::mutex> l(g_dev[device].mu);
   ms2[0] = g_dev[device].ms[0];
   ms2[1] = g_dev[device].ms[1];
   return FTS_API_OK;
