@@ -223,7 +223,7 @@ FTS_DEV PJ pj_inf() {
 }
 
 // dbl-2001-b
-__device__ __noinline__ PJ pj_dbl(PJ p) {
+__device__ __forceinline__ PJ pj_dbl(PJ p) {
   if (is_zero(p.z)) return p;
   const Fp delta = sqr(p.z), gamma = sqr(p.y), beta = mul(p.x, gamma);
   const Fp t = mul(sub(p.x, delta), add(p.x, delta));
@@ -241,7 +241,7 @@ __device__ __noinline__ PJ pj_dbl(PJ p) {
 }
 
 // add-2007-bl style full addition, complete over all Jacobian inputs
-__device__ __noinline__ PJ pj_add(PJ p, PJ q) {
+__device__ __forceinline__ PJ pj_add(PJ p, PJ q) {
   if (is_zero(p.z)) return q;
   if (is_zero(q.z)) return p;
   const Fp z1z1 = sqr(p.z), z2z2 = sqr(q.z);
@@ -258,7 +258,7 @@ __device__ __noinline__ PJ pj_add(PJ p, PJ q) {
 }
 
 // mixed addition with an affine (Montgomery) point q != O
-__device__ __noinline__ PJ pj_madd(PJ p, Fp qx, Fp qy) {
+__device__ __forceinline__ PJ pj_madd(PJ p, Fp qx, Fp qy) {
   if (is_zero(p.z)) {
     PJ r;
     r.x = qx, r.y = qy, r.z = load<PM>(PM::ONE);
