@@ -362,8 +362,10 @@ int fts_ecdsa_verify_batch(int device, size_t n, const fts_ecdsa_item* items, in
   const size_t need = tot + mtot;
   if (D.h_cap < need) {
     if (D.h_stage) hipHostFree(D.h_stage);
-    D.h_cap = need + need / 2;
-    ECHK(hipHostMalloc(&D.h_stage, D.h_cap, hipHostMallocDefault));
+    D.h_stage = nullptr, D.h_cap = 0;
+    const size_t cap = need + need / 2;
+    if (hipHostMalloc(&D.h_stage, cap, hipHostMallocDefault) != hipSuccess) return D.h_stage = nullptr, FTS_API_ENOMEM;
+    D.h_cap = cap;
   }
   uint8_t* h = D.h_stage;
   uint32_t* hrec = reinterpret_cast<uint32_t*>(h);
@@ -415,13 +417,17 @@ int fts_ecdsa_verify_batch(int device, size_t n, const fts_ecdsa_item* items, in
   }
   if (D.rec_cap < tot) {
     if (D.d_rec) hipFree(D.d_rec);
-    D.rec_cap = tot + tot / 2;
-    ECHK(hipMalloc(&D.d_rec, D.rec_cap));
+    D.d_rec = nullptr, D.rec_cap = 0;
+    const size_t cap = tot + tot / 2;
+    if (hipMalloc(&D.d_rec, cap) != hipSuccess) return D.d_rec = nullptr, FTS_API_ENOMEM;
+    D.rec_cap = cap;
   }
   if (D.msg_cap < std::max<size_t>(mtot, 1)) {
     if (D.d_msg) hipFree(D.d_msg);
-    D.msg_cap = mtot + mtot / 2 + 1;
-    ECHK(hipMalloc(&D.d_msg, D.msg_cap));
+    D.d_msg = nullptr, D.msg_cap = 0;
+    const size_t cap = mtot + mtot / 2 + 1;
+    if (hipMalloc(&D.d_msg, cap) != hipSuccess) return D.d_msg = nullptr, FTS_API_ENOMEM;
+    D.msg_cap = cap;
   }
   uint32_t* drec = reinterpret_cast<uint32_t*>(D.d_rec);
   uint32_t* de = reinterpret_cast<uint32_t*>(D.d_rec + rec_b);
