@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "field.hpp"  // fts::mac96 / mac96s (96-bit column accumulators)
+
 #ifndef FTS_DEV
 #define FTS_DEV __device__ __forceinline__
 #endif
@@ -146,39 +148,36 @@ FTS_DEV F<P> sub(const F<P>& a, const F<P>& b) {
   return r;
 }
 
-// Montgomery product a*b*2^-256 mod M for a, b < M (full-width CIOS).
+// Montgomery product a*b*2^-256 mod M for a, b < M: finely-integrated
+// product scanning (as fts::f_mul_fips) with each column in a 96-bit
+// accumulator (v_mad_u64_u32 + carry add per product).  Full-width moduli:
+// the result is < 2M < 2^257, so the bit above column 15 is kept and folded
+// into the final conditional subtraction.  Zero limbs of M (p has three) are
+// skipped at compile time.
 template <class P>
 FTS_DEV F<P> mul(const F<P>& a, const F<P>& b) {
-  uint32_t t[9];
-#pragma unroll
-  for (int i = 0; i < 9; i++) t[i] = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint32_t bi = b.v[i];
-    uint64_t s = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      s = (uint64_t)a.v[j] * bi + t[j] + (s >> 32);
-      t[j] = (uint32_t)s;
-    }
-    s = (uint64_t)t[8] + (s >> 32);
-    t[8] = (uint32_t)s;
-    const uint32_t t9 = (uint32_t)(s >> 32);
-    const uint32_t m = t[0] * P::INV;
-    uint64_t c = (uint64_t)m * P::M[0] + t[0];
-#pragma unroll
-    for (int j = 1; j < 8; j++) {
-      c = (uint64_t)m * P::M[j] + t[j] + (c >> 32);
-      t[j - 1] = (uint32_t)c;
-    }
-    c = (uint64_t)t[8] + (c >> 32);
-    t[7] = (uint32_t)c;
-    t[8] = t9 + (uint32_t)(c >> 32);
-  }
+  uint32_t m[8];
   F<P> r;
+  uint64_t acc = 0;
+  uint32_t ovf = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) r.v[i] = t[i];
-  cond_sub(r, t[8]);
+  for (int k = 0; k < 15; k++) {
+#pragma unroll
+    for (int i = (k > 7 ? k - 7 : 0); i <= (k < 7 ? k : 7); i++) fts::mac96(acc, ovf, a.v[i], b.v[k - i]);
+#pragma unroll
+    for (int i = (k > 7 ? k - 7 : 0); i < (k < 8 ? k : 8); i++)
+      if (P::M[k - i] != 0) fts::mac96s(acc, ovf, m[i], P::M[k - i]);
+    if (k < 8) {
+      m[k] = (uint32_t)acc * P::INV;
+      fts::mac96s(acc, ovf, m[k], P::M[0]);
+    } else {
+      r.v[k - 8] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)ovf << 32);
+    ovf = 0;
+  }
+  r.v[7] = (uint32_t)acc;
+  cond_sub(r, (uint32_t)(acc >> 32));
   return r;
 }
 template <class P>
