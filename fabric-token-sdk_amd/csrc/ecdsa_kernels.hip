@@ -12,10 +12,10 @@
 // (validator/validator_transfer.go:29-62) once per input token.
 //
 // Kernels (one signature per lane):
-//   k_ecdsa_table   once per device: 32 x 256 affine multiples d*2^(8w)*G
-//                   (8-bit fixed-base windows, 512 KiB, L2-resident)
+//   k_ecdsa_table   once per device: 16 x 65536 affine multiples d*2^(16w)*G
+//                   (16-bit fixed-base windows, 64 MiB in HBM)
 //   k_ecdsa_digest  SHA-256 of each message (full-rate INT32 work)
-//   k_ecdsa_verify  pk on-curve check, w = s^-1 mod n (Fermat), u1*G as 32
+//   k_ecdsa_verify  pk on-curve check, w = s^-1 mod n (Fermat), u1*G as 16
 //                   mixed additions from the table, u2*Q with a 4-bit window
 //                   (252 doublings + <= 64 additions), X.x == r checked
 //                   projectively (r*Z^2 == X, and (r+n)*Z^2 when r+n < p)
@@ -40,10 +40,14 @@ namespace {
 
 constexpr int REC_WORDS = 32;  // r[8] s[8] qx[8] qy[8], little-endian u32 limbs
 
+// FB_W-bit fixed-base windows for u1*G: entry (w, d) = d * 2^(FB_W w) * G,
+// affine Montgomery (16 words); d = 0 unused
+constexpr int FB_W = 16, FB_NW = 256 / FB_W, FB_ND = 1 << FB_W;
+
 __global__ __launch_bounds__(256) void k_ecdsa_table(uint32_t* __restrict__ table) {
   const int id = blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= 32 * 256) return;
-  const int w = id >> 8, d = id & 255;
+  if (id >= FB_NW * FB_ND) return;
+  const int w = id / FB_ND, d = id % FB_ND;
   uint32_t* out = table + (size_t)id * 16;
   if (d == 0) {
     for (int i = 0; i < 16; i++) out[i] = 0;
@@ -51,11 +55,11 @@ __global__ __launch_bounds__(256) void k_ecdsa_table(uint32_t* __restrict__ tabl
   }
   const Fp gx = load<PM>(CGX), gy = load<PM>(CGY);
   PJ p = pj_inf();
-  for (int b = 7; b >= 0; b--) {
+  for (int b = FB_W - 1; b >= 0; b--) {
     p = pj_dbl(p);
     if ((d >> b) & 1) p = pj_madd(p, gx, gy);
   }
-  for (int k = 0; k < 8 * w; k++) p = pj_dbl(p);
+  for (int k = 0; k < FB_W * w; k++) p = pj_dbl(p);
   const Fp zi = inv(p.z), zi2 = sqr(zi);
   const Fp x = mul(p.x, zi2), y = mul(p.y, mul(zi2, zi));
   for (int i = 0; i < 8; i++) out[i] = x.v[i], out[8 + i] = y.v[i];
@@ -116,12 +120,12 @@ __global__ __launch_bounds__(256) void k_ecdsa_verify(int n, const uint32_t* __r
   cond_sub(em, 0);
   const Fn wm = inv(to_mont(load<NM>(s)));
   const Fn u1 = mul(wm, em), u2 = mul(wm, load<NM>(r));
-  // u1*G: 32 mixed additions from the fixed-base table
+  // u1*G: FB_NW mixed additions from the fixed-base table
   PJ accg = pj_inf();
-  for (int w = 0; w < 32; w++) {
-    const uint32_t d = (u1.v[w >> 2] >> (8 * (w & 3))) & 255u;
+  for (int w = 0; w < FB_NW; w++) {
+    const uint32_t d = (u1.v[(w * FB_W) >> 5] >> ((w * FB_W) & 31)) & (uint32_t)(FB_ND - 1);
     if (d) {
-      const uint32_t* t = table + ((size_t)w * 256 + d) * 16;
+      const uint32_t* t = table + ((size_t)w * FB_ND + d) * 16;
       accg = pj_madd(accg, load<PM>(t), load<PM>(t + 8));
     }
   }
@@ -325,8 +329,8 @@ int fts_ecdsa_verify_batch(int device, size_t n, const fts_ecdsa_item* items, in
     if (!G.init) {
       hipStream_t s0;
       ECHK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
-      ECHK(hipMalloc(&G.d_table, (size_t)32 * 256 * 16 * 4));
-      k_ecdsa_table<<<32, 256, 0, s0>>>(G.d_table);
+      ECHK(hipMalloc(&G.d_table, (size_t)FB_NW * FB_ND * 16 * 4));
+      k_ecdsa_table<<<FB_NW * FB_ND / 256, 256, 0, s0>>>(G.d_table);
       ECHK(hipGetLastError());
       ECHK(hipStreamSynchronize(s0));
       ECHK(hipStreamDestroy(s0));
