@@ -129,16 +129,34 @@ __global__ __launch_bounds__(256) void k_ecdsa_verify(int n, const uint32_t* __r
       accg = pj_madd(accg, load<PM>(t), load<PM>(t + 8));
     }
   }
-  // u2*Q: 4-bit fixed window over 1..15 Q
-  PJ tab[16];
+  // u2*Q: signed 4-bit window, digits in [-7, 8] over a table of 1..8 Q.
+  // Carry into window w is bit w of cm (carry out of window 63 -> top digit).
+  uint64_t cm = 0;
+  {
+    uint32_t c = 0;
+    for (int w = 0; w < 64; w++) {
+      cm |= (uint64_t)c << w;
+      c = ((u2.v[w >> 3] >> (4 * (w & 7))) & 15u) + c > 8u;
+    }
+  }
+  // carry out of window 63 = the top digit (0 or 1)
+  const uint32_t c64 = (u2.v[7] >> 28) + ((uint32_t)(cm >> 63) & 1u) > 8u;
+  PJ tab[9];
   tab[0] = pj_inf();
   tab[1].x = Qx, tab[1].y = Qy, tab[1].z = load<PM>(PM::ONE);
-  for (int k = 2; k < 16; k++) tab[k] = pj_madd(tab[k - 1], Qx, Qy);
-  PJ acc = pj_inf();
+  for (int k = 2; k < 9; k++) tab[k] = pj_madd(tab[k - 1], Qx, Qy);
+  PJ acc = c64 ? tab[1] : pj_inf();
   for (int nib = 63; nib >= 0; nib--) {
     acc = pj_dbl(pj_dbl(pj_dbl(pj_dbl(acc))));
-    const uint32_t d = (u2.v[nib >> 3] >> (4 * (nib & 7))) & 15u;
-    if (d) acc = pj_add(acc, tab[d]);
+    const int raw = (int)((u2.v[nib >> 3] >> (4 * (nib & 7))) & 15u);
+    const int cin = (int)((cm >> nib) & 1u);
+    const int cout = nib < 63 ? (int)((cm >> (nib + 1)) & 1u) : (int)c64;
+    const int d = raw + cin - 16 * cout;
+    if (d) {
+      PJ q = tab[d < 0 ? -d : d];
+      if (d < 0) q.y = sub(Fp{}, q.y);
+      acc = pj_add(acc, q);
+    }
   }
   const PJ X = pj_add(accg, acc);
   if (is_zero(X.z)) {
