@@ -195,16 +195,20 @@ FTS_DEV F<P> from_mont(const F<P>& a) {
   for (int i = 0; i < 8; i++) one.v[i] = i == 0;
   return mul(a, one);
 }
-// a^(M-2) (Fermat inverse; 0 -> 0), Montgomery in and out
+// a^(M-2) (Fermat inverse; 0 -> 0), Montgomery in and out: fixed 4-bit
+// window over a^1..a^15 (14 products) -> 252 squarings + one product per
+// non-zero nibble, instead of one product per set bit.
 template <class P>
 FTS_DEV F<P> inv(const F<P>& a) {
-  F<P> r = load<P>(P::ONE);
-  for (int i = 7; i >= 0; i--) {
-    const uint32_t e = P::EXP_INV[i];
-    for (int b = 31; b >= 0; b--) {
-      r = sqr(r);
-      if ((e >> b) & 1) r = mul(r, a);
-    }
+  F<P> t[16];
+  t[0] = load<P>(P::ONE);
+  t[1] = a;
+  for (int k = 2; k < 16; k++) t[k] = mul(t[k - 1], a);
+  F<P> r = t[P::EXP_INV[7] >> 28];
+  for (int nb = 62; nb >= 0; nb--) {
+    r = sqr(sqr(sqr(sqr(r))));
+    const uint32_t d = (P::EXP_INV[nb >> 3] >> (4 * (nb & 7))) & 15u;
+    if (d) r = mul(r, t[d]);
   }
   return r;
 }
