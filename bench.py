@@ -50,6 +50,60 @@ MAD_PER_MUL = 136          # 8x32-bit no-carry CIOS / FIPS Montgomery product
 SURVEY_MAD_PER_RP64 = 8.13e6   # SURVEY §8(d) fixed cost model per rp64 verify
 
 
+def _cpu_env():
+    """host CPU model, logical CPUs and the cgroup CPU quota (the cores a baseline may use)"""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"cpu_model": model, "logical_cpus": os.cpu_count(), "cgroup_cpu_quota": quota}
+
+
+def _timed_sample(fn, total, chunk, seconds):
+    """run fn(lo, hi) over chunks of [0, total) until `seconds` of wall time; -> (items, s)"""
+    done, cs = 0, 0.0
+    while cs < seconds and done < total:
+        c = min(chunk, total - done)
+        t0 = time.perf_counter()
+        fn(done, done + c)
+        cs += time.perf_counter() - t0
+        done += c
+    return done, cs
+
+
+def _action_cpu_baseline(pp_raw, bits, actions, want, args, unit, what):
+    """reference-order C restatement of transfer / issue Verify (oracle/c/ref_verify.c
+    oracle_action_verify_many) on a bounded sample of the same actions: 1 core, then
+    --cpu-threads cores; verdicts checked against `want` [(status, fail index)]"""
+    from oracle import cref, pp as oppm
+    opp = oppm.load_pp(pp_raw).with_bit_length(bits)
+    thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+
+    def run(lo, hi, t):
+        got = cref.action_verify_many(opp, actions[lo:hi], threads=t)
+        assert got == want[lo:hi], "CPU oracle verdicts differ"
+    d1, s1 = _timed_sample(lambda lo, hi: run(lo, hi, 1), len(actions), 2, args.cpu_seconds / 3)
+    dn, sn = _timed_sample(lambda lo, hi: run(lo, hi, thr), len(actions), 4 * thr, args.cpu_seconds)
+    cpu = {"value": round(dn / sn, 3), "unit": unit, "cores": thr, "kind": "port", "value_1core": round(d1 / s1, 3),
+           "sample": "%d (%d threads) and %d (1 thread) of the same %s, reference-order C restatement of "
+                     "transfer/issue Verify (oracle/c/ref_verify.c oracle_action_verify_many: TypeAndSum / "
+                     "SameType + RangeCorrectness, affine G1.Mul per operation), %.1f + %.1f s wall"
+                     % (dn, thr, d1, what, sn, s1)}
+    cpu.update(_cpu_env())
+    return cpu
+
+
 def _cg_throttle():
     """(nr_throttled, throttled_usec) of this process's cgroup (v2), if readable"""
     try:
@@ -74,13 +128,14 @@ def main():
     ap.add_argument("--distinct", type=int, default=4,
                     help="batches with distinct proofs; the other in-flight batches re-stage them (setup time)")
     ap.add_argument("--pass-batches", type=int, default=0,
-                    help="batches in the isolated roofline pass (0: the timed region's average pass size)")
+                    help="batches in the isolated roofline pass (0: FTS_COALESCE_MAX / batch, the pass size the "
+                         "library runs under load; the PMC traffic file is keyed by this pass size)")
     ap.add_argument("--roofline-steps", type=int, default=6,
                     help="isolated steps (one batch alone on the GPU) for the per-kernel roofline")
     ap.add_argument("--cpu-sample", type=int, default=256, help="CPU baseline chunk size (0: skip the CPU baseline)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall-time bound of the CPU baseline sample")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     ap.add_argument("--workload", choices=["rp", "msm", "transfer", "mixed", "request", "audit", "prove", "ecdsa"],
                     default="rp")
     ap.add_argument("--sigs", type=int, default=65536, help="ecdsa workload: owner signatures per GPU per step")
@@ -148,7 +203,8 @@ def main():
             rng = random.Random(fdist.shard_seed(0xF7A50002, rank, ln))
             vals = [rng.getrandbits(n) for _ in range(B)]
             bfs = [rng.randrange(R_ORDER).to_bytes(32, "big") for _ in range(B)]
-            proofs, coms = pp.prove_range_batch(vals, bfs, seed=0xF7A50002 + 1000003 * rank + 7777 * ln)
+            # device prover: byte-identical to the host prover (tests/test_gpu_prove.py), seconds faster
+            proofs, coms = pp.prove_range_batch_gpu(vals, bfs, seed=0xF7A50002 + 1000003 * rank + 7777 * ln)
             sets.append((proofs, coms))
         batches.append(pp.stage_range_proofs(proofs, coms))
     proofs0, coms0 = sets[0]
@@ -222,7 +278,7 @@ def main():
         return acc, (time.perf_counter() - t) * 1e3 / reps
 
     kt1, iso_ms = isolated(batches[0], R)
-    m = args.pass_batches or max(1, min(int(round(merged_avg)), 32768 // B))
+    m = args.pass_batches or max(1, int(os.environ.get("FTS_COALESCE_MAX", "32768")) // B)
     pass_proofs = [sets[i % len(sets)] for i in range(m)]
     big = pp.stage_range_proofs([p for ps, _ in pass_proofs for p in ps], [c for _, cs in pass_proofs for c in cs])
     kt, pass_ms = isolated(big, R)
@@ -246,10 +302,11 @@ def main():
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-            # HBM bytes per launch = corrected FETCH_SIZE + WRITE_SIZE of the isolated pass (PMC runs)
-            e = tj.get(dom + "@isolated", tj.get(dom, {}))
-            if e.get("fetch_bytes_corrected") is not None:
-                traffic = int(e["fetch_bytes_corrected"] + e.get("write_bytes", 0))
+            # HBM bytes per launch of THIS pass size: FETCH_SIZE (scaled by the factor calibrated for the
+            # kernel's access pattern, tools/fetch_calib) + WRITE_SIZE, from separate PMC runs of the same command
+            e = tj.get("%s@pass%d" % (dom, m * B), {})
+            if e.get("fetch_bytes") is not None:
+                traffic = int(e["fetch_bytes"] * e.get("fetch_scale", 1.0) + e.get("write_bytes", 0))
     except (OSError, ValueError, AttributeError):
         pass
     rd = kernel_roof(dom)
@@ -265,21 +322,22 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        # bounded sample: chunks of the same proofs until ~cpu_seconds of wall time
+        # bounded samples of the same proofs: one core, then --cpu-threads cores
         from oracle import cref, pp as oppm
         opp = oppm.load_pp(pp_raw).with_bit_length(n)
         thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        done, cs, chunk = 0, 0.0, max(thr, args.cpu_sample)
-        while cs < args.cpu_seconds and done < B:
-            m = min(chunk, B - done)
-            t0 = time.perf_counter()
-            res = cref.rp_verify_many(opp, coms0[done:done + m], proofs0[done:done + m], threads=thr)
-            cs += time.perf_counter() - t0
+
+        def chk(lo, hi, t):
+            res = cref.rp_verify_many(opp, coms0[lo:hi], proofs0[lo:hi], threads=t)
             assert all(r == 0 for r in res), res
-            done += m
-        cpu = {"value": round(done / cs, 3), "unit": "rp%d verifies/s" % n, "cores": thr, "kind": "port",
-               "sample": "%d of the same rp%d proofs, reference-order C restatement (oracle/c/ref_verify.c, "
-                         "%d affine G1.Mul per proof), %d threads, %.1f s wall" % (done, n, 7 * n + 2 * k + 9, thr, cs)}
+        d1, s1 = _timed_sample(lambda lo, hi: chk(lo, hi, 1), B, 8, args.cpu_seconds / 3)
+        dn, sn = _timed_sample(lambda lo, hi: chk(lo, hi, thr), B, max(thr, args.cpu_sample), args.cpu_seconds)
+        cpu = {"value": round(dn / sn, 3), "unit": "rp%d verifies/s" % n, "cores": thr, "kind": "port",
+               "value_1core": round(d1 / s1, 3),
+               "sample": "%d (%d threads) and %d (1 thread) of the same rp%d proofs, reference-order C restatement "
+                         "(oracle/c/ref_verify.c, %d affine G1.Mul per proof, no GLV / assembly), %.1f + %.1f s wall"
+                         % (dn, thr, d1, n, 7 * n + 2 * k + 9, sn, s1)}
+        cpu.update(_cpu_env())
 
     if rank == 0:
         out = {
@@ -294,7 +352,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32 (BN254 Fp/Fr 8x32-bit Montgomery)",
-            "data": "synthetic: %d seeded %d-bit range proofs per GPU from the library's host prover" % (B, n),
+            "data": "synthetic: %d seeded %d-bit range proofs per GPU from the library's device prover "
+                    "(byte-identical to its host prover)" % (B, n),
             "config": {"workload": "C2: batch of %d standalone %d-bit Bulletproof range proofs per GPU "
                                    "(exact transcripts per proof + RLC batch check via one Pippenger MSM)" % (B, n),
                        "batch_per_gpu": B, "bit_length": n, "rounds": k, "parallelism": "shard%d" % world},
@@ -897,6 +956,11 @@ def bench_transfer(args, raw_requests=False):
     elapsed = _max_over_ranks(dist, elapsed)
     kt = {k: (v[0] * args.steps, v[1]) for k, v in pp.last_timings_ex().items()}
     value = world * args.transfers * args.steps / elapsed
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0 and not raw_requests:
+        acts = [("transfer", ins, outs, proof) for ins, outs, proof in items]
+        cpu = _action_cpu_baseline(pp_raw, args.bits, acts, [(0, -1)] * len(acts), args, "transfer verifies/s",
+                                   "2-in/2-out %d-bit transfers" % args.bits)
     if raw_requests:
         metric = "raw TokenRequest verifies/sec (1 transfer 2-in/2-out each, BN254, %d-bit range proofs)" % args.bits
         unit, entry = "requests/s", "fts_request_verify_batch (protobuf + G1 JSON decode in the timed region)"
@@ -914,7 +978,7 @@ def bench_transfer(args, raw_requests=False):
             "config": {"workload": "C4 per GPU: %d transfers (TypeAndSum + 2 rp%d each) per step via "
                                    "%s, %d calls in flight" % (args.transfers, args.bits, entry, nb),
                        "transfers_per_gpu": args.transfers, "parallelism": "shard%d" % world},
-            "roofline": _roofline_from(kt, args.steps),
+            "roofline": _roofline_from(kt, args.steps), "cpu_baseline": cpu,
             "kernel_ms": {k: round(v[0] / args.steps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),
             flush=True)
     if dist is not None:
@@ -971,7 +1035,7 @@ def bench_mixed(args):
     batches = [pp.prepare_actions(transfers, issues) for _ in range(nb)]
     setup_s = time.time() - t0
     for _ in range(max(1, args.warmup)):
-        st_t, _, st_i, _ = batches[0].verify()
+        st_t, fi_t, st_i, fi_i = batches[0].verify()
     assert set(np.nonzero(st_t)[0]) == bad_tr and set(np.nonzero(st_i)[0]) == bad_is, "verdict mismatch"
     _run_action_steps(batches, nb, None, None)
     if dist is not None:
@@ -985,6 +1049,24 @@ def bench_mixed(args):
             assert set(np.nonzero(r[0])[0]) == bad_tr and set(np.nonzero(r[2])[0]) == bad_is
     kt = {k: (v[0] * args.steps, v[1]) for k, v in pp.last_timings_ex().items()}
     value = world * (n_tr + n_is) * args.steps / elapsed
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        # the same interleaving as the batch (1 issue : 4 transfers), verdicts from the GPU run
+        order = []
+        for j in range(n_is):
+            order += [("t", 4 * j + q) for q in range(4) if 4 * j + q < n_tr] + [("i", j)]
+        acts, want = [], []
+        for kind, i in order:
+            if kind == "t":
+                ins, outs, proof = transfers[i]
+                acts.append(("transfer", ins, outs, proof))
+                want.append((int(st_t[i]), int(fi_t[i])))
+            else:
+                toks, proof = issues[i]
+                acts.append(("issue", [], toks, proof))
+                want.append((int(st_i[i]), int(fi_i[i])))
+        cpu = _action_cpu_baseline(pp_raw, bits, acts, want, args, "actions/s",
+                                   "mixed actions (1 issue-16 : 4 transfers, 32-bit)")
     if rank == 0:
         print(json.dumps({
             "metric": "mixed action verifies/sec (issue-16 + 2-in/2-out transfers, BN254, 32-bit)",
@@ -995,7 +1077,7 @@ def bench_mixed(args):
             "config": {"workload": "C5 per GPU: 1 issue-16 : 4 transfers at 32-bit, one fts_actions_verify_batch "
                                    "per step (%d range proofs), %d calls in flight" % (2 * n_tr + 16 * n_is, nb),
                        "transfers_per_gpu": n_tr, "issues_per_gpu": n_is, "parallelism": "shard%d" % world},
-            "roofline": _roofline_from(kt, args.steps),
+            "roofline": _roofline_from(kt, args.steps), "cpu_baseline": cpu,
             "kernel_ms": {k: round(v[0] / args.steps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),
             flush=True)
     if dist is not None:

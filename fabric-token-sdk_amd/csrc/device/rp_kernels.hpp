@@ -55,8 +55,14 @@ constexpr double MADS_PER_MUL = 136.0;
 constexpr double COST_MADD = 11.0;    // madd-2007-bl 7M + 4S
 constexpr double COST_ADD = 16.0;     // add-2007-bl 11M + 5S
 constexpr double COST_DBL = 7.0;      // dbl-2009-l 2M + 5S
-constexpr double COST_FB = 16.0 * COST_MADD;   // fixed-base, 16 signed 16-bit windows (fixed_base.hpp)
-constexpr double COST_FBW = 13.0 * COST_MADD;  // fixed-base, 13 signed 20-bit windows (FbWide)
+// fixed-base products (fixed_base.hpp): one mixed addition per signed window; a
+// product computed into a fresh accumulator starts from the identity, so its first
+// window is a copy (fb_mul / fb_mul_w: 15 resp. 12 real additions), a product added
+// into a running accumulator (fb_mul_acc, fbw_mul_acc) pays every window
+constexpr double COST_FB = 16.0 * COST_MADD;         // accumulate, 16 signed 16-bit windows
+constexpr double COST_FB_FRESH = 15.0 * COST_MADD;   // fresh, 16-bit windows
+constexpr double COST_FBW = 13.0 * COST_MADD;        // accumulate, 13 signed 20-bit windows (FbWide)
+constexpr double COST_FBW_FRESH = 12.0 * COST_MADD;  // fresh, 20-bit windows
 constexpr double COST_VB4 = 7.0 + 6.0 * COST_MADD + 256.0 * COST_DBL + 60.0 * COST_ADD;  // 4-bit var-base
 constexpr double COST_VB128 = 7.0 + 6.0 * COST_ADD + 124.0 * COST_DBL + 30.0 * COST_ADD;  // GLV half (glv.hpp)
 constexpr double COST_STRAUS2 = 2.0 * (7.0 + 6.0 * COST_ADD) + 124.0 * COST_DBL + 60.0 * COST_ADD;  // glv.hpp straus2_128

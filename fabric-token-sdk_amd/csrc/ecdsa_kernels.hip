@@ -251,6 +251,7 @@ struct DevState {
   std::mutex mu;
   std::condition_variable cv;
   bool init = false;
+  int init_err = 0;  // a failed initialisation is cached (no re-allocation on every retry)
   uint32_t* d_table = nullptr;
   Slot slot[NSLOT];
   bool busy[NSLOT] = {false, false, false};
@@ -262,6 +263,10 @@ struct SlotGuard {
   DevState& G;
   int k;
   ~SlotGuard() {
+    // an error path may leave a copy or kernel queued on the slot's stream that
+    // still reads its pinned staging / device buffers: drain it before the next
+    // caller may reuse (or re-allocate) them
+    if (G.slot[k].stream) (void)hipStreamSynchronize(G.slot[k].stream);
     std::lock_guard<std::mutex> l(G.mu);
     G.ms[0] = G.slot[k].ms[0];
     G.ms[1] = G.slot[k].ms[1];
@@ -344,18 +349,32 @@ int fts_ecdsa_verify_batch(int device, size_t n, const fts_ecdsa_item* items, in
   {
     std::unique_lock<std::mutex> l(G.mu);
     ECHK(hipSetDevice(device));
+    if (G.init_err) return G.init_err;
     if (!G.init) {
-      hipStream_t s0;
-      ECHK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
-      ECHK(hipMalloc(&G.d_table, (size_t)FB_NW * FB_ND * 16 * 4));
-      k_ecdsa_table<<<FB_NW * FB_ND / 256, 256, 0, s0>>>(G.d_table);
-      ECHK(hipGetLastError());
-      ECHK(hipStreamSynchronize(s0));
-      ECHK(hipStreamDestroy(s0));
+      // all or nothing: on any failure release what was created and cache the error
+      hipStream_t s0 = nullptr;
+      bool ok = hipStreamCreateWithFlags(&s0, hipStreamNonBlocking) == hipSuccess &&
+                hipMalloc(&G.d_table, (size_t)FB_NW * FB_ND * 16 * 4) == hipSuccess;
+      if (ok) {
+        k_ecdsa_table<<<FB_NW * FB_ND / 256, 256, 0, s0>>>(G.d_table);
+        ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(s0) == hipSuccess;
+      }
+      if (s0) (void)hipStreamDestroy(s0);
       for (auto& S : G.slot) {
-        ECHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
-        for (auto& e : S.ev) ECHK(hipEventCreate(&e));
+        ok = ok && hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) == hipSuccess;
+        for (auto& e : S.ev) ok = ok && hipEventCreate(&e) == hipSuccess;
         S.d_table = G.d_table;
+      }
+      if (!ok) {
+        for (auto& S : G.slot) {
+          for (auto& e : S.ev)
+            if (e) (void)hipEventDestroy(e), e = nullptr;
+          if (S.stream) (void)hipStreamDestroy(S.stream), S.stream = nullptr;
+          S.d_table = nullptr;
+        }
+        if (G.d_table) (void)hipFree(G.d_table), G.d_table = nullptr;
+        G.init_err = FTS_API_EDEVICE;
+        return G.init_err;
       }
       G.init = true;
     }

@@ -238,6 +238,7 @@ struct RpReq {
   int32_t* status;  // caller's host status array (may be null)
   int rc = 0;
   bool done = false;
+  std::chrono::steady_clock::time_point arrived = std::chrono::steady_clock::now();
   std::condition_variable cv;  // this caller's wake-up (targeted, no thundering herd)
   RpReq(fts_rp_batch* bb, int32_t* st) : b(bb), status(st) {}
 };
@@ -267,7 +268,14 @@ struct fts_ctx {
   // batch coalescing (fts_rp_batch_verify): staged batches submitted
   // concurrently are merged into one device pass of up to coalesce_max proofs
   std::deque<RpReq*> rp_pending;
+  size_t pending_proofs = 0;  // proofs queued in rp_pending
   size_t coalesce_max = 32768;
+  // gather window: while the device is busy and fewer than gather_target proofs
+  // are queued, the head request waits up to gather_us for more batches before
+  // it takes a lane (a burst of callers then shares a few large passes instead
+  // of one lone 4,096-proof pass per free lane); an idle device starts at once
+  size_t gather_target = 16384;
+  int gather_us = 300;
   // a lane was freed (call with mu held): the head pending range-proof request
   // becomes the next leader; LaneGuard waiters re-check too
   void wake_lane_waiters() {
@@ -389,6 +397,8 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   int nl = 5;
   if (const char* e = getenv("FTS_LANES")) nl = std::max(1, std::min(16, atoi(e)));
   if (const char* e = getenv("FTS_COALESCE_MAX")) c->coalesce_max = (size_t)std::max(0L, atol(e));
+  c->gather_target = c->coalesce_max / 2;
+  if (const char* e = getenv("FTS_GATHER_US")) c->gather_us = std::max(0, atoi(e));
   // FTS_SIDE_STREAM=0: run each lane's side work on its main stream
   bool side = true;
   if (const char* e = getenv("FTS_SIDE_STREAM")) side = atoi(e) != 0;
@@ -939,8 +949,24 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
   RpReq me(b, status);
   std::unique_lock<std::mutex> lk(c->mu);
   c->rp_pending.push_back(&me);
+  c->pending_proofs += (size_t)b->B;
+  // enough queued for a full pass: the head stops gathering
+  if (c->pending_proofs >= c->gather_target && c->rp_pending.front() != &me) c->rp_pending.front()->cv.notify_one();
   while (!me.done) {
     if (c->free_lanes.empty() || c->rp_pending.empty()) {
+      me.cv.wait(lk);
+      continue;
+    }
+    const bool device_busy = c->free_lanes.size() < c->lanes.size();
+    if (device_busy && c->rp_pending.front() == &me && c->pending_proofs < c->gather_target) {
+      const auto deadline = me.arrived + std::chrono::microseconds(c->gather_us);
+      if (std::chrono::steady_clock::now() < deadline) {
+        me.cv.wait_until(lk, deadline);
+        continue;
+      }
+    }
+    if (c->rp_pending.front() != &me && !me.done) {  // only the head leads a pass
+      c->rp_pending.front()->cv.notify_one();
       me.cv.wait(lk);
       continue;
     }
@@ -953,8 +979,11 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
       if (!grp.empty() && (tot + (size_t)q->b->B > c->coalesce_max || (int)grp.size() == RP_GATHER_MAX)) break;
       grp.push_back(q);
       tot += (size_t)q->b->B;
+      c->pending_proofs -= (size_t)q->b->B;
       c->rp_pending.pop_front();
     }
+    // the next head (if any) may lead a pass on another free lane
+    if (!c->rp_pending.empty() && !c->free_lanes.empty()) c->rp_pending.front()->cv.notify_one();
     lk.unlock();
     const int rc = run_rp_group(c, *L, grp);
     lk.lock();
@@ -1656,6 +1685,14 @@ int fts_request_inspect(const uint8_t* req, size_t req_len, int32_t* status, int
 }  // extern "C"
 
 // ------------------------------------------------------------------ prover
+namespace fts {
+namespace host {
+RngSource::RngSource(uint64_t sd) : secure(sd == FTS_SEED_OS_RANDOM), seed(sd) {
+  if (secure) ok = getrandom(key, sizeof key, 0) == (ssize_t)sizeof key;
+}
+}  // namespace host
+}  // namespace fts
+
 static const ProverTables& prover_tables(const fts_ctx* cc) {
   fts_ctx* c = const_cast<fts_ctx*>(cc);
   std::call_once(c->prover_once, [&]() { build_prover_tables(c->pp, c->n, c->ptab); });
@@ -1687,7 +1724,9 @@ int fts_rp_prove(const fts_ctx* c, uint64_t value, const uint8_t* bf32, uint64_t
   vm.add_fb(T.ped(1), fr_u64(value));
   vm.add_fb(T.ped(2), bf);
   G1A V = vm.aff();
-  Rng rng(seed);
+  RngSource src(seed);
+  if (!src.ok) return FTS_API_EDEVICE;
+  Rng rng = src.at(0);
   RangeProofOut rp = prove_range(T, c->pp, c->n, c->k, V, value, bf, rng);
   std::string s = rp.serialize();
   *out_len = s.size();
@@ -1702,6 +1741,8 @@ int fts_rp_prove_batch(const fts_ctx* c, size_t n, const uint64_t* values, const
                        uint8_t* com64_out) {
   if (!c || !values || !bfs || !out || !offsets || !lens || !com64_out) return FTS_API_EINVAL;
   const ProverTables& T = prover_tables(c);
+  RngSource src(seed);
+  if (!src.ok) return FTS_API_EDEVICE;
   std::vector<std::string> res(n);
   std::atomic<size_t> next{0};
   int nth = threads > 0 ? threads : (int)host_threads();
@@ -1714,7 +1755,7 @@ int fts_rp_prove_batch(const fts_ctx* c, size_t n, const uint64_t* values, const
         vm.add_fb(T.ped(1), fr_u64(values[i]));
         vm.add_fb(T.ped(2), bf);
         G1A V = vm.aff();
-        Rng rng(seed + i);
+        Rng rng = src.at(i);
         res[i] = prove_range(T, c->pp, c->n, c->k, V, values[i], bf, rng).serialize();
         g1_to_bytes(V, com64_out + 64 * i);
       }
@@ -1740,7 +1781,9 @@ int fts_transfer_prove(const fts_ctx* c, const uint8_t* type, size_t type_len, s
   std::vector<Fr> ib(n_in), ob(n_out);
   for (size_t i = 0; i < n_in; i++) ib[i] = fr_from_be(in_bfs + 32 * i);
   for (size_t i = 0; i < n_out; i++) ob[i] = fr_from_be(out_bfs + 32 * i);
-  Rng rng(seed);
+  RngSource src(seed);
+  if (!src.ok) return FTS_API_EDEVICE;
+  Rng rng = src.at(0);
   std::string s = prove_transfer(T, c->pp, c->n, c->k, type_to_zr(type, type_len), iv, ib, ov, ob, rng);
   *out_len = s.size();
   if (s.size() > out_cap) return FTS_API_ESIZE;
@@ -1755,7 +1798,9 @@ int fts_issue_prove(const fts_ctx* c, const uint8_t* type, size_t type_len, size
   std::vector<uint64_t> v(values, values + n_tok);
   std::vector<Fr> b(n_tok);
   for (size_t i = 0; i < n_tok; i++) b[i] = fr_from_be(bfs + 32 * i);
-  Rng rng(seed);
+  RngSource src(seed);
+  if (!src.ok) return FTS_API_EDEVICE;
+  Rng rng = src.at(0);
   std::string s = prove_issue(T, c->pp, c->n, c->k, type_to_zr(type, type_len), v, b, rng);
   *out_len = s.size();
   if (s.size() > out_cap) return FTS_API_ESIZE;
@@ -2049,12 +2094,14 @@ int fts_rp_prove_batch_gpu(fts_ctx* c, size_t N, const uint64_t* values, const u
   if (N == 0) return FTS_API_OK;
   if (c->device < 0) return FTS_API_EDEVICE;
   HIP_OK(hipSetDevice(c->device));
+  RngSource src(seed);
+  if (!src.ok) return FTS_API_EDEVICE;
   LaneGuard lg(c);
   const int nr = pv_nrnd(c->n);
   std::vector<std::string> der;
   int rc = rp_prove_device(c, *lg.L, N, [&](size_t g, uint64_t& v, uint32_t* bf8, uint32_t* R) {
     v = values[g];
-    Rng rng(seed + g);  // the host prover's draw order (prove_range)
+    Rng rng = src.at(g);  // the host prover's draw order (prove_range)
     for (int r = 0; r < nr; r++) fr_canon_words(rng.fr(), R + r * 8);
     fr_canon_words(fr_from_be(bfs + 32 * g), bf8);
   }, der, com64_out);
@@ -2090,6 +2137,8 @@ static int actions_prove_device(fts_ctx* c, size_t A, const fts_action_witness* 
         (x.type_len && !x.type) || nin > 4096 || x.n_out > 4096)
       return FTS_API_EINVAL;
   }
+  RngSource src(seed);
+  if (!src.ok) return FTS_API_EDEVICE;
   HIP_OK(hipSetDevice(c->device));
   LaneGuard lg(c);
   Lane& L = *lg.L;
@@ -2118,7 +2167,7 @@ static int actions_prove_device(fts_ctx* c, size_t A, const fts_action_witness* 
     const fts_action_witness& x = w[a];
     const SpAction& ac = act[a];
     uint32_t* S = h_sc.data() + (size_t)ac.sc_off * 8;
-    Rng rng(seed + a);
+    Rng rng = src.at(a);
     const Fr type = type_to_zr(x.type, x.type_len);
     const Fr tbf = rng.fr();
     fr_canon_words(type, S);

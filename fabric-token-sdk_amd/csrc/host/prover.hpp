@@ -23,9 +23,22 @@
 namespace fts {
 namespace host {
 
-// xoshiro256** -> uniform Fr by rejection (deterministic synthetic witnesses)
+// Prover randomness, uniform Fr by rejection, in one of two modes:
+//  - seeded (tests and benchmarks ONLY): xoshiro256** from a 64-bit seed.  Two
+//    proofs whose seeds collide reuse their nonces, which reveals the committed
+//    values and blinding factors -- never use it for real tokens.
+//  - secure: ChaCha20 (RFC 8439 block function) under a 256-bit key drawn from
+//    getrandom() once per call, one keystream per proof / action (nonce = its
+//    index), the role crypto/rand plays for the reference provers
+//    (rp/bulletproof.go:336-466 via Curve.NewRandomZr).
+// The C-ABI selects the mode by the seed argument: FTS_SEED_OS_RANDOM = secure.
 struct Rng {
+  bool secure = false;
   uint64_t s[4];
+  uint32_t key[8], blk[16];
+  uint64_t stream = 0;
+  uint32_t ctr = 0;
+  int pos = 16;
   explicit Rng(uint64_t seed) {
     uint64_t z = seed;
     for (int i = 0; i < 4; i++) {
@@ -36,8 +49,36 @@ struct Rng {
       s[i] = x ^ (x >> 31);
     }
   }
+  Rng(const uint32_t k[8], uint64_t stream_id) : secure(true), stream(stream_id) {
+    for (int i = 0; i < 8; i++) key[i] = k[i];
+  }
   static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+  static uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+  void refill() {  // ChaCha20 block (key, counter = ctr, nonce = stream)
+    uint32_t st[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key[0], key[1], key[2], key[3],
+                       key[4], key[5], key[6], key[7], ctr++, (uint32_t)stream, (uint32_t)(stream >> 32), 0u};
+    uint32_t x[16];
+    for (int i = 0; i < 16; i++) x[i] = st[i];
+    auto qr = [&](int a, int b, int c, int d) {
+      x[a] += x[b]; x[d] = rotl32(x[d] ^ x[a], 16);
+      x[c] += x[d]; x[b] = rotl32(x[b] ^ x[c], 12);
+      x[a] += x[b]; x[d] = rotl32(x[d] ^ x[a], 8);
+      x[c] += x[d]; x[b] = rotl32(x[b] ^ x[c], 7);
+    };
+    for (int r = 0; r < 10; r++) {
+      qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15);
+      qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14);
+    }
+    for (int i = 0; i < 16; i++) blk[i] = x[i] + st[i];
+    pos = 0;
+  }
   uint64_t next() {
+    if (secure) {
+      if (pos > 14) refill();
+      const uint64_t v = (uint64_t)blk[pos] | ((uint64_t)blk[pos + 1] << 32);
+      pos += 2;
+      return v;
+    }
     uint64_t r = rotl(s[1] * 5, 7) * 9, t = s[1] << 17;
     s[2] ^= s[0];
     s[3] ^= s[1];
@@ -53,6 +94,16 @@ struct Rng {
       if (!geq_mod<ModR>(c)) return to_mont<ModR>(c);
     }
   }
+};
+
+// the randomness of one prover call: item i draws from at(i) (seeded: seed + i)
+struct RngSource {
+  bool secure = false;
+  uint64_t seed = 0;
+  uint32_t key[8] = {0};
+  bool ok = true;
+  explicit RngSource(uint64_t sd);
+  Rng at(uint64_t i) const { return secure ? Rng(key, i) : Rng(seed + i); }
 };
 
 inline std::string hex_of(const uint8_t* p, size_t n) {

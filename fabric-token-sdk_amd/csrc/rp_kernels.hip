@@ -1025,7 +1025,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   FTS_LAUNCH(k_rp_powers, B * (n >> std::min(PW_LC, k)), 64, s, B, n, k, d.status, d.ch, d.ypow, d.svec);
   tl->mark("k_rp_powers", s, (double)B * (2.0 * n + 2.0 * k));
   FTS_LAUNCH(k_rp_fixed_exact, B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, wtables, d.hpj, d.terms);
-  tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FBW);
+  tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FBW_FRESH);
   // H'_i -> affine + BE bytes (x0 transcript) now; com is normalised after com_sum
   const int nhp = B * n;
   FTS_LAUNCH(k_rp_normalize, (nhp + NORM_E - 1) / NORM_E, NORM_BS, s, nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be);
@@ -1056,7 +1056,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   hipLaunchKernelGGL(k_rlc_columns, dim3(3 + 2 * n), dim3(256), 0, s2, B, n, k, d.ch, r.coef, d.ypow, d.svec, r.colsum);
   tl->mark("k_rlc_columns", s2, (double)B * 3 * n);
   FTS_LAUNCH(k_rlc_fixed, 3 + 2 * n, 64, s2, n, r.colsum, tables, r.fixed);
-  tl->mark("k_rlc_fixed", s2, (double)(3 + 2 * n) * COST_FB);
+  tl->mark("k_rlc_fixed", s2, (double)(3 + 2 * n) * COST_FB_FRESH);
   launch_msm(r.plan, d.pts, r.msc, r.fixed, 3 + 2 * n, r.msm_scratch, s, s2, tl);
   FTS_LAUNCH(k_rlc_finalize, B, 64, s, B, r.plan.out, d.status, d.ipa_flag, r.flag);
   tl->mark("k_rlc_finalize", s, 0);
@@ -1071,7 +1071,7 @@ void launch_rp_gather(const RpGather& g, int k, uint8_t* raw, uint32_t* sc, int3
 void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, hipStream_t s, Timeline* tl) {
   const int B = d.B, n = d.n, k = d.k;
   FTS_LAUNCH(k_rp_terms_fixed, B * (3 + 2 * n), 64, s, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, tables, d.terms);
-  tl->mark("k_rp_terms_fixed", s, (double)B * (3 + 2 * n) * COST_FB);
+  tl->mark("k_rp_terms_fixed", s, (double)B * (3 + 2 * n) * COST_FB_FRESH);
   FTS_LAUNCH(k_rp_terms_var, B * (3 + 2 * k), 64, s, B, n, k, d.status, d.ipa_flag, d.pts, d.ch, d.terms, d.scratch);
   tl->mark("k_rp_terms_var", s, (double)B * (3 + 2 * k) * COST_VB4);
   FTS_LAUNCH(k_rp_check, B, 64, s, B, n, k, d.status, d.ipa_flag, d.terms, d.hpa);

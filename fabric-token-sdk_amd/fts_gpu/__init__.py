@@ -32,7 +32,7 @@ import numpy as np
 from . import _lib as L
 from ._lib import (FTS_OK, FTS_E_MALFORMED, FTS_E_RP_NIL, FTS_E_RP_INVALID, FTS_E_IPA_NIL, FTS_E_IPA_LEN,  # noqa
                    FTS_E_IPA_INVALID, FTS_E_RC_COUNT, FTS_E_TAS_INVALID, FTS_E_ST_INVALID, FTS_DEVICE_NONE,
-                   FTS_E_ACTION_INVALID, FTS_E_OPEN_MISMATCH, FtsError)
+                   FTS_E_ACTION_INVALID, FTS_E_OPEN_MISMATCH, FTS_SEED_OS_RANDOM, FtsError)
 from . import request  # noqa: F401  (TokenRequest writers)
 
 

@@ -31,6 +31,8 @@ FTS_E_SIG_INVALID = 15
 
 FTS_API_OK = 0
 FTS_DEVICE_NONE = -2
+# prover seed: fresh getrandom() key per call (production); any other seed is test-only
+FTS_SEED_OS_RANDOM = (1 << 64) - 1
 
 EXPORTED = [
     "fts_ctx_create", "fts_ctx_create_bits", "fts_ctx_destroy", "fts_ctx_info",

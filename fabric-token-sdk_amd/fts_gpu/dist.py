@@ -14,13 +14,30 @@ def _dev(dist):
 
 
 def allgather_verdicts(dist, status):
-    """status: this rank's per-proof verdicts (np.int32, 0 = accepted) ->
-    np.uint8 bitmap of accepted proofs, all ranks concatenated in rank order"""
+    """status: this rank's per-proof verdicts (np.int32, 0 = accepted; any length,
+    ranks may differ) -> np.bool_ array of accepted flags of ALL ranks' proofs,
+    concatenated in rank order (one entry per proof, no padding).
+
+    Two collectives: the per-rank counts first, then the bit-packed verdicts padded
+    to the largest rank's packed size (all_gather_into_tensor needs equal sizes);
+    each rank's block is unpacked and trimmed to its true count."""
     import torch
-    bits = torch.from_numpy(np.packbits(np.asarray(status) == 0)).to(_dev(dist))
-    out = torch.empty(dist.get_world_size() * bits.numel(), dtype=torch.uint8, device=bits.device)
+    dev = _dev(dist)
+    acc = np.asarray(status) == 0
+    world = dist.get_world_size()
+    cnt = torch.tensor([acc.size], dtype=torch.int64, device=dev)
+    counts = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(counts, cnt)
+    counts = [int(c) for c in counts.cpu()]
+    width = max(1, (max(counts) + 7) // 8)
+    packed = np.zeros(width, dtype=np.uint8)
+    pb = np.packbits(acc)
+    packed[:pb.size] = pb
+    bits = torch.from_numpy(packed).to(dev)
+    out = torch.empty(world * width, dtype=torch.uint8, device=dev)
     dist.all_gather_into_tensor(out, bits)
-    return out.cpu().numpy()
+    blocks = out.cpu().numpy().reshape(world, width)
+    return np.concatenate([np.unpackbits(blocks[r])[:counts[r]].astype(bool) for r in range(world)])
 
 
 def reduce_scalar(dist, x, op="max"):

@@ -85,15 +85,29 @@ def verify_batch(msgs, sigs, pks, device=0):
 
 
 def verify_packed(msg_buf, msg_off, msg_len, sig_buf, sig_off, sig_len, pk_buf, device=0):
-    """Zero-copy batch form over contiguous buffers (bench / large batches)."""
+    """Zero-copy batch form over contiguous buffers (bench / large batches).
+    Every (offset, length) must lie inside its buffer and pk_buf must hold 64 bytes
+    per item: the C library is handed raw pointers, so this is checked here
+    (ValueError) before any pointer is formed."""
     n = len(msg_off)
+    mo, ml = np.asarray(msg_off, dtype=np.uint64), np.asarray(msg_len, dtype=np.uint64)
+    so, sl = np.asarray(sig_off, dtype=np.uint64), np.asarray(sig_len, dtype=np.uint64)
+    if not (mo.shape == ml.shape == so.shape == sl.shape == (n,)):
+        raise ValueError("offset and length arrays must be 1-D and of equal length")
+    if len(pk_buf) < 64 * n:
+        raise ValueError("pk_buf holds %d bytes, %d items need %d" % (len(pk_buf), n, 64 * n))
+    for name, off, ln, buf in (("msg", mo, ml, msg_buf), ("sig", so, sl, sig_buf)):
+        # end = off + len without uint64 wrap-around: off <= size and len <= size - off
+        size = np.uint64(len(buf))
+        if n and ((off > size).any() or (ln > size - np.minimum(off, size)).any()):
+            raise ValueError("%s offset + length outside its buffer (%d bytes)" % (name, len(buf)))
     st = np.zeros(n, dtype=np.int32)
     items = np.zeros(n, dtype=[("msg", "u8"), ("msg_len", "u8"), ("sig", "u8"), ("sig_len", "u8"), ("pk64", "u8")])
     mb, sb, pb = (np.frombuffer(b, dtype=np.uint8) for b in (msg_buf, sig_buf, pk_buf))
-    items["msg"] = mb.ctypes.data + np.asarray(msg_off, dtype=np.uint64)
-    items["msg_len"] = msg_len
-    items["sig"] = sb.ctypes.data + np.asarray(sig_off, dtype=np.uint64)
-    items["sig_len"] = sig_len
+    items["msg"] = mb.ctypes.data + mo
+    items["msg_len"] = ml
+    items["sig"] = sb.ctypes.data + so
+    items["sig_len"] = sl
     items["pk64"] = pb.ctypes.data + 64 * np.arange(n, dtype=np.uint64)
     L.check("fts_ecdsa_verify_batch",
             L.lib.fts_ecdsa_verify_batch(int(device), n, items.ctypes.data_as(C.POINTER(L.EcdsaItem)),

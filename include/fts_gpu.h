@@ -244,7 +244,16 @@ int fts_token_metadata_decode(const uint8_t* meta, size_t meta_len, int32_t* sta
 /* ---- error strings ---- */
 const char* fts_status_str(int32_t status);
 
-/* ---- host prover (synthetic inputs; reference prover semantics) ---- */
+/* ---- host prover (reference prover semantics) ----
+ * seed selects the prover randomness of every fts_*_prove* entry point:
+ *   FTS_SEED_OS_RANDOM  secure: ChaCha20 keystreams under a fresh 256-bit getrandom() key
+ *                       per call, one per proof / action (the role of crypto/rand in
+ *                       Curve.NewRandomZr, rp/bulletproof.go:336-466).  Use this for real tokens.
+ *   any other value     deterministic, FOR TESTS AND BENCHMARKS ONLY: item i draws from
+ *                       xoshiro256**(seed + i).  Two calls whose seed ranges overlap reuse
+ *                       nonces across different witnesses, which reveals the committed
+ *                       values and blinding factors. */
+#define FTS_SEED_OS_RANDOM UINT64_MAX
 /* value < 2^bit_length expected (larger values produce a proof that fails, as in the
  * reference).  bf32: blinding factor (BE, reduced mod r).  seed: deterministic RNG seed.
  * out_der: caller buffer of out_cap bytes; *out_len <- bytes written. com64_out: V. */

@@ -826,3 +826,180 @@ int oracle_open_check_many(const uint8_t* ped, int count, const uint8_t* coms, c
   free(th);
   return 0;
 }
+
+/* ---------------------------------------------------------------- actions
+ * int oracle_action_verify_many(const uint8_t* ped, const uint8_t* gens, int n, int count,
+ *     const int32_t* kind, const int32_t* n_in, const int32_t* n_out, const uint8_t* const* in64,
+ *     const uint8_t* const* out64, const uint8_t* const* ders, const size_t* lens, int threads,
+ *     int32_t* status, int32_t* index)
+ * kind 0: transfer.NewVerifier(in, out, pp).Verify (transfer/transfer.go:153-197):
+ *   TypeAndSumVerifier.Verify (typeandsum.go:230-277) then, unless 1-in/1-out,
+ *   RangeCorrectnessVerifier.Verify on V_j = Out_j - CT (rangecorrectness.go:137-162);
+ *   the TypeAndSum error wins.
+ * kind 1: issue.NewVerifier(tokens, pp).Verify (issue/verifier.go:32-57): SameType
+ *   (sametype.go:167-183), then RangeCorrectness on Tok_j - CT (tokens in out64).
+ * Both in the reference's operation order: every G1 operation affine, one G1.Mul per
+ * scalar multiplication, sequential range proofs (the reference's extra goroutine in
+ * transfer.go:171 overlaps TypeAndSum with the range proofs; the verdicts do not
+ * depend on it).  status: fts_status numbering (0 ok, 1 malformed, 3/6.. range-proof
+ * class at index[i], 7 #proofs != #outputs, 8 TypeAndSum, 9 SameType). */
+static int g1_el(span d, g1* out) {
+  span e;
+  return element(d, &e) && g1_from_bytes(e.p, e.n, out);
+}
+static int zr_el(span d, fe* out) {
+  span e;
+  if (!element(d, &e)) return 0;
+  *out = zr_from(e);
+  return 1;
+}
+static int zr_arr_el(span d, fe* out, int cap) {
+  span e, it[16];
+  if (!element(d, &e)) return -1;
+  int m = values(e, it, 16, 1);
+  if (m < 0 || m > cap) return -1;
+  for (int i = 0; i < m; i++) out[i] = zr_from(it[i]);
+  return m;
+}
+static int rc_verify(const params* pp, const g1* coms, int m, span rc, int32_t* idx) {
+  span outer[2], rps[32];
+  if (values(rc, outer, 2, 0) != 1) return 1;
+  int np = values(outer[0], rps, 32, 0);
+  if (np < 0) return 1;
+  if (np != m) return 7;
+  for (int j = 0; j < m; j++) {
+    int r = verify_one(pp, coms[j], rps[j]);
+    if (r) {
+      *idx = j;
+      return r;
+    }
+  }
+  return 0;
+}
+static int tas_verify(const g1* ped, const g1* in, int nin, const g1* out, int nout, span raw, g1* ct) {
+  span d[8];
+  if (values(raw, d, 8, 0) != 7) return 1;
+  fe ibf[16], iv[16], type, tbf, eqs, chal;
+  if (!g1_el(d[0], ct)) return 1;
+  if (zr_arr_el(d[1], ibf, 16) < nin || zr_arr_el(d[2], iv, 16) < nin) return 1;
+  if (!zr_el(d[3], &type) || !zr_el(d[4], &tbf) || !zr_el(d[5], &eqs) || !zr_el(d[6], &chal)) return 1;
+  g1 arr[40], ins[16], outs[16], incom[16];
+  g1 sum;
+  memset(&sum, 0, sizeof sum);
+  sum.inf = 1;
+  for (int i = 0; i < nin; i++) { /* typeandsum.go:240-252 */
+    ins[i] = g1_sub(in[i], *ct);
+    sum = g1_add(sum, ins[i]);
+    g1 c = g1_mul(ped[1], iv[i]);
+    c = g1_add(c, g1_mul(ped[2], ibf[i]));
+    incom[i] = g1_sub(c, g1_mul(ins[i], chal));
+  }
+  for (int j = 0; j < nout; j++) {
+    outs[j] = g1_sub(out[j], *ct);
+    sum = g1_sub(sum, outs[j]);
+  }
+  g1 sumcom = g1_sub(g1_mul(ped[2], eqs), g1_mul(sum, chal)); /* :254-256 */
+  g1 typecom = g1_add(g1_mul(ped[0], type), g1_mul(ped[2], tbf));
+  typecom = g1_sub(typecom, g1_mul(*ct, chal));
+  int m = 0;
+  for (int i = 0; i < nin; i++) arr[m++] = incom[i];
+  arr[m++] = typecom;
+  arr[m++] = sumcom;
+  for (int i = 0; i < nin; i++) arr[m++] = ins[i];
+  for (int j = 0; j < nout; j++) arr[m++] = outs[j];
+  arr[m++] = *ct;
+  arr[m++] = sum;
+  fe h = hash_points(arr, m); /* :267-274: raw Zr.Equals */
+  return feq(h, chal) ? 0 : 8;
+}
+static int st_verify(const g1* ped, span raw, g1* ct) {
+  span d[5];
+  fe type, bf, chal;
+  if (values(raw, d, 5, 0) != 4) return 1;
+  if (!zr_el(d[0], &type) || !zr_el(d[1], &bf) || !zr_el(d[2], &chal) || !g1_el(d[3], ct)) return 1;
+  g1 com = g1_add(g1_mul(ped[0], type), g1_mul(ped[2], bf));
+  com = g1_sub(com, g1_mul(*ct, chal));
+  g1 arr[2] = {*ct, com};
+  return feq(hash_points(arr, 2), chal) ? 0 : 9;
+}
+static int action_one(const params* pp, const g1* ped, int kind, int nin, int nout, const uint8_t* in64,
+                      const uint8_t* out64, span der, int32_t* idx) {
+  g1 in[16], out[32], ct, coms[32];
+  span v[3];
+  *idx = -1;
+  if (nin > 16 || nout > 32 || values(der, v, 3, 0) != 2 || v[0].n == 0) return 1;
+  for (int i = 0; i < nin; i++)
+    if (!g1_from_bytes(in64 + 64 * i, 64, &in[i])) return 1;
+  for (int j = 0; j < nout; j++)
+    if (!g1_from_bytes(out64 + 64 * j, 64, &out[j])) return 1;
+  int sig = kind == 0 ? tas_verify(ped, in, nin, out, nout, v[0], &ct) : st_verify(ped, v[0], &ct);
+  if (sig == 1) return 1;
+  if (kind == 1 && sig) return sig; /* issue/verifier.go:40-43: SameType first */
+  int rc = 0;
+  if (kind == 1 || nin != 1 || nout != 1) {
+    for (int j = 0; j < nout; j++) coms[j] = g1_sub(out[j], ct);
+    if (v[1].n == 0) rc = 7;
+    else rc = rc_verify(pp, coms, nout, v[1], idx);
+  }
+  if (sig) { /* transfer.go:192-196: the TypeAndSum error wins */
+    *idx = -1;
+    return sig;
+  }
+  if (rc == 1) *idx = -1;
+  return rc;
+}
+typedef struct {
+  const params* pp;
+  g1 ped[3];
+  const int32_t *kind, *nin, *nout;
+  const uint8_t* const* in64;
+  const uint8_t* const* out64;
+  const uint8_t* const* ders;
+  const size_t* lens;
+  int32_t *status, *index;
+  int count, next;
+  pthread_mutex_t mu;
+} act_job;
+static void* act_worker(void* arg) {
+  act_job* j = (act_job*)arg;
+  for (;;) {
+    pthread_mutex_lock(&j->mu);
+    int i = j->next++;
+    pthread_mutex_unlock(&j->mu);
+    if (i >= j->count) return NULL;
+    span s = {j->ders[i], j->lens[i]};
+    j->status[i] = action_one(j->pp, j->ped, j->kind[i], j->nin[i], j->nout[i], j->in64[i], j->out64[i], s,
+                              &j->index[i]);
+  }
+}
+int oracle_action_verify_many(const uint8_t* ped, const uint8_t* gens, int n, int count, const int32_t* kind,
+                              const int32_t* n_in, const int32_t* n_out, const uint8_t* const* in64,
+                              const uint8_t* const* out64, const uint8_t* const* ders, const size_t* lens,
+                              int threads, int32_t* status, int32_t* index) {
+  params pp;
+  if (!load_params(gens, n, &pp)) return -1;
+  act_job j;
+  for (int q = 0; q < 3; q++)
+    if (!g1_from_bytes(ped + 64 * q, 64, &j.ped[q])) return -1;
+  j.pp = &pp;
+  j.kind = kind;
+  j.nin = n_in;
+  j.nout = n_out;
+  j.in64 = in64;
+  j.out64 = out64;
+  j.ders = ders;
+  j.lens = lens;
+  j.status = status;
+  j.index = index;
+  j.count = count;
+  j.next = 0;
+  pthread_mutex_init(&j.mu, NULL);
+  if (threads < 1) threads = 1;
+  pthread_t* th = malloc(sizeof(pthread_t) * threads);
+  for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, act_worker, &j);
+  for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+  free(th);
+  free(pp.L);
+  free(pp.R);
+  return 0;
+}

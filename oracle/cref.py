@@ -80,3 +80,33 @@ def open_check_many(pp, openings, threads=1):
                                    b"".join(o[2] for o in openings), b"".join(o[3] for o in openings), threads, out)
     assert rc == 0
     return list(out)
+
+
+def action_verify_many(pp, actions, threads=1):
+    """transfer / issue Verify in reference order (oracle_action_verify_many):
+    actions = [(kind, inputs[list of 64 B], outputs[list of 64 B], proof)] with kind
+    "transfer" or "issue" (issue: tokens as outputs, no inputs) ->
+    [(fts_status, fail index)]"""
+    lb = lib()
+    if not hasattr(lb, "_act_sig"):
+        P = C.POINTER
+        lb.oracle_action_verify_many.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, P(C.c_int32),
+                                                 P(C.c_int32), P(C.c_int32), P(C.c_char_p), P(C.c_char_p),
+                                                 P(C.c_char_p), P(C.c_size_t), C.c_int, P(C.c_int32),
+                                                 P(C.c_int32)]
+        lb.oracle_action_verify_many.restype = C.c_int
+        lb._act_sig = True
+    n = len(actions)
+    kind = (C.c_int32 * n)(*[0 if a[0] == "transfer" else 1 for a in actions])
+    nin = (C.c_int32 * n)(*[len(a[1]) for a in actions])
+    nout = (C.c_int32 * n)(*[len(a[2]) for a in actions])
+    ins = (C.c_char_p * n)(*[b"".join(a[1]) or b"\0" for a in actions])
+    outs = (C.c_char_p * n)(*[b"".join(a[2]) or b"\0" for a in actions])
+    ders = (C.c_char_p * n)(*[a[3] for a in actions])
+    lens = (C.c_size_t * n)(*[len(a[3]) for a in actions])
+    st, ix = (C.c_int32 * n)(), (C.c_int32 * n)()
+    ped = b"".join(bn.g1_bytes(p) for p in pp.ped)
+    rc = lb.oracle_action_verify_many(ped, gens_blob(pp), pp.bit_length, n, kind, nin, nout, ins, outs, ders, lens,
+                                      threads, st, ix)
+    assert rc == 0
+    return list(zip(list(st), list(ix)))

@@ -17,6 +17,9 @@ from conftest import GOLDEN
 
 with open(os.path.join(GOLDEN, "ecdsa_golden.json")) as f:
     GOLD = json.load(f)["cases"]
+# the X.x = r + n branch (make_ecdsa_crafted.py; validity double-checked with OpenSSL)
+with open(os.path.join(GOLDEN, "ecdsa_crafted_golden.json")) as f:
+    CRAFTED = json.load(f)["cases"]
 
 
 def _case(c):
@@ -65,6 +68,16 @@ def test_oracle_matches_golden():
     for c in GOLD:
         m, s, pk = _case(c)
         assert O.verify(m, s, _pt(pk)) == c["expect"], c["tag"]
+
+
+def test_oracle_matches_crafted_r_plus_n():
+    from oracle import ecdsa_p256 as O
+    assert [c["expect"] for c in CRAFTED] == [0, 15] * 3
+    for c in CRAFTED:
+        m, s, pk = _case(c)
+        r, _ = O.parse_sig(s)
+        assert O.verify(m, s, _pt(pk)) == c["expect"], c["tag"]
+        assert (r < O.N) == (c["expect"] == 0)
 
 
 def test_oracle_sign_roundtrip():
@@ -117,6 +130,16 @@ def test_gpu_golden():
     st = E.verify_batch(ms, ss, ps, device=0)
     bad = [(c["tag"], int(s), c["expect"]) for c, s in zip(GOLD, st) if int(s) != c["expect"]]
     assert not bad, bad[:10]
+
+
+@pytest.mark.gpu
+def test_gpu_crafted_r_plus_n():
+    """accept iff X.x == r or X.x == r + n (< p): the r + n branch is reached only by
+    crafted signatures (ecdsa_kernels.hip final check)"""
+    from fts_gpu import ecdsa as E
+    ms, ss, ps = zip(*[_case(c) for c in CRAFTED])
+    st = E.verify_batch(ms, ss, ps, device=0)
+    assert [int(x) for x in st] == [c["expect"] for c in CRAFTED]
 
 
 @pytest.mark.gpu
@@ -180,3 +203,23 @@ def test_gpu_verifier_api_and_empty():
     with pytest.raises(E.SignatureError, match="signature is not in lowS"):
         E.Verifier(bytes.fromhex(hi["pk64"])).Verify(*_case(hi)[:2])
     assert len(E.verify_batch([], [], [])) == 0
+
+
+def test_verify_packed_rejects_out_of_bounds():
+    """bounds of the zero-copy form are checked before any pointer reaches the C library"""
+    import numpy as np
+    from fts_gpu import ecdsa as E
+    m, s, pk = b"abcd", b"\x30" * 8, bytes(64)
+    u = lambda *v: np.array(v, dtype=np.uint64)  # noqa: E731
+    bad = [
+        dict(msg_off=u(1), msg_len=u(4)),                       # message runs past its buffer
+        dict(sig_off=u(0), sig_len=u(9)),                       # signature runs past its buffer
+        dict(msg_off=u(2 ** 64 - 1), msg_len=u(2)),             # wrap-around offset
+        dict(pk_buf=bytes(63)),                                 # short key buffer
+        dict(msg_off=u(0, 0), msg_len=u(1, 1)),                 # unequal array lengths
+    ]
+    for kw in bad:
+        args = dict(msg_buf=m, msg_off=u(0), msg_len=u(4), sig_buf=s, sig_off=u(0), sig_len=u(8), pk_buf=pk)
+        args.update(kw)
+        with pytest.raises(ValueError):
+            E.verify_packed(**args)

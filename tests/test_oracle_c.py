@@ -1,0 +1,79 @@
+"""CPU: the C restatement (oracle/c/ref_verify.c, bench.py's cpu_baseline)
+pinned against the committed golden vectors of the Python oracle.
+
+rp_golden.json: every standalone range proof (8..64 bits, honest, out of
+range, tampered T1 / L0 / Left / ip) -> the same verdict class as the
+reference error string recorded in the fixture (bulletproof.go:252-333,
+ipa.go:190-262).
+headline_golden.json: the range proofs inside the 64-bit 2-in/2-out
+transfers, verified one by one against V_j = Out_j - CT as the range
+goroutine of transfer.go:171-187 does, give the recorded first failing
+index and class (rangecorrectness.go:141-160)."""
+import json
+import os
+
+import pytest
+
+from conftest import GOLDEN
+
+from oracle import bn254 as bn, cref, der, zkat
+
+# verify_one's return codes = fts_status numbering of the library
+RP_CODE = {None: 0, "invalid range proof": 3, "invalid IPA": 6, "invalid range proof: nil elements": 2,
+           "invalid IPA proof: nil elements": 4, "invalid IPA proof": 5}
+
+
+def _load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def built():
+    cref.build()
+
+
+def test_c_oracle_rp_golden(built, oracle_pp):
+    cases = _load("rp_golden.json")
+    for bits in sorted({c["bits"] for c in cases}):
+        pp = oracle_pp.with_bit_length(bits)
+        sel = [c for c in cases if c["bits"] == bits]
+        got = cref.rp_verify_many(pp, [bytes.fromhex(c["commitment"]) for c in sel],
+                                  [bytes.fromhex(c["proof"]) for c in sel], threads=4)
+        assert got == [RP_CODE[c["expect"]] for c in sel], bits
+
+
+def test_c_oracle_headline_transfer_range_proofs(built, oracle_pp):
+    """the C oracle on the 64-bit range proofs of the headline transfers"""
+    cases = _load("headline_golden.json")["transfers"]
+    for c in cases:
+        raw = bytes.fromhex(c["proof"])
+        tas_raw, rc_raw = der.unmarshal_values(raw)
+        tas = zkat.TypeAndSumProof.deserialize(tas_raw)
+        rps = der.unmarshal_values(der.unmarshal_values(rc_raw)[0])
+        outs = [bn.g1_from_bytes(bytes.fromhex(h)) for h in c["outputs"]]
+        coms = [bn.g1_bytes(bn.g1_sub(o, tas.CT)) for o in outs]
+        got = cref.rp_verify_many(oracle_pp, coms, rps, threads=2)
+        first = next(((j, s) for j, s in enumerate(got) if s != 0), None)
+        if c["expect"] is None:
+            assert first is None, c["name"]
+        elif c["expect"].startswith("invalid range proof at index"):
+            inner = c["expect"].split(": ", 1)[1]
+            assert first == (c["index"], RP_CODE[inner]), c["name"]
+        else:  # TypeAndSum failures: the range proofs themselves are honest
+            assert first is None, c["name"]
+
+
+def test_c_oracle_headline_actions(built, oracle_pp):
+    """the C oracle's whole transfer / issue verifier (bench cpu_baseline of C4/C5)
+    on the headline fixtures: same verdict class and fail index as the Python oracle"""
+    head = _load("headline_golden.json")
+    from fts_gpu_msgs import classify
+    tr = [("transfer", [bytes.fromhex(h) for h in c["inputs"]], [bytes.fromhex(h) for h in c["outputs"]],
+           bytes.fromhex(c["proof"])) for c in head["transfers"]]
+    got = cref.action_verify_many(oracle_pp, tr, threads=4)
+    assert got == [classify(c["expect"], c["index"]) for c in head["transfers"]]
+    p32 = oracle_pp.with_bit_length(32)
+    iss = [("issue", [], [bytes.fromhex(h) for h in c["tokens"]], bytes.fromhex(c["proof"])) for c in head["issues"]]
+    got = cref.action_verify_many(p32, iss, threads=4)
+    assert got == [classify(c["expect"], c["index"]) for c in head["issues"]]
