@@ -194,6 +194,35 @@ FTS_DEV void fb_mul_acc(G1J& acc, const uint32_t* __restrict__ table, const Scal
   }
 }
 
+// acc += k * B over a width-W table (FbCfg<W> layout; fb_mul_w into a running accumulator)
+template <int W>
+FTS_DEV void fb_mul_acc_w(G1J& acc, const uint32_t* __restrict__ table, const Scalar& k) {
+  constexpr int NW = FbCfg<W>::NW;
+  uint32_t s[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = k.v[i];
+  int carry = 0, w = 0, d = 0;
+  for (; w < NW; w++) {
+    d = fb_next_digit_w<W>(s, carry);
+    if (d != 0) break;
+  }
+  if (w == NW) return;
+  G1A cur = fb_entry_w<W>(table, w, d);
+  for (;;) {
+    int wn = w + 1, dn = 0;
+    for (; wn < NW; wn++) {
+      dn = fb_next_digit_w<W>(s, carry);
+      if (dn != 0) break;
+    }
+    G1A nxt;
+    if (wn < NW) nxt = fb_entry_w<W>(table, wn, dn);  // in flight during the addition
+    madd_inl(acc, cur);
+    if (wn >= NW) break;
+    cur = nxt;
+    w = wn;
+  }
+}
+
 // out-of-line copy for cold call sites (keeps their kernels small)
 __device__ __noinline__ G1J nl_fb_mul(const uint32_t* __restrict__ table, Scalar k) { return fb_mul(table, k); }
 

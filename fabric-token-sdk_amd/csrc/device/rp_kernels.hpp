@@ -163,6 +163,9 @@ struct RpBatchDev {
   uint32_t* scratch;   // var-base lane tables
   uint32_t* ypow;      // [n][B][8] y^-i (Montgomery Fr), i-major (coalesced over proofs)
   uint32_t* svec;      // [n][B][8] s_i = prod_j x_j^(+-1) (ipa.go:343-356 unrolled), i-major
+  uint32_t* zvec;      // [n][B][8] z^2 2^i y^-i (latency path only), i-major
+  int com_fixed;       // 1: com by fixed-base groups + x*D on the side stream (latency path,
+                       //    small passes); 0: Horner sum + joint GLV/Straus chains (work path)
 };
 
 }  // namespace fts

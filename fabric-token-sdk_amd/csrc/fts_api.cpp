@@ -106,7 +106,7 @@ struct DBuf {
 };
 
 struct Workspace {
-  DBuf pts, ch, small, hpj, hpa, hpbe, x0, terms, scratch, ypow, svec;
+  DBuf pts, ch, small, hpj, hpa, hpbe, x0, terms, scratch, ypow, svec, zvec;
   // random-linear-combination check + MSM
   DBuf r_key, r_msc, r_coef, r_colsum, r_fixed, r_flag, m_keys, m_counts, m_offsets, m_cursor, m_sorted, m_buckets,
       m_segs, m_wins, m_out, m_scratch, m_win, m_choff, m_chbkt, m_partials;
@@ -117,7 +117,7 @@ struct Workspace {
   DBuf pv;        // batched prover: one arena (prove_arena)
   DBuf sp;        // sigma provers: one arena
   void release() {
-    for (DBuf* b : {&open_rec, &pv, &sp, &pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &terms, &scratch, &ypow, &svec, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
+    for (DBuf* b : {&open_rec, &pv, &sp, &pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &terms, &scratch, &ypow, &svec, &zvec, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
                     &rp_status, &rp_ipa, &s_act, &s_raw, &s_owner, &s_pts, &s_sc, &s_status, &s_work, &s_terms, &s_aff,
                     &s_affoff, &s_msgs, &s_jac, &s_scratch, &r_key, &r_msc, &r_coef, &r_colsum, &r_fixed, &r_flag,
                     &m_keys, &m_counts, &m_offsets, &m_cursor, &m_sorted, &m_buckets, &m_segs, &m_wins, &m_out,
@@ -245,6 +245,9 @@ struct RpReq {
 
 struct fts_ctx {
   int device = 0;
+  // multi-device context (fts_ctx_create_devices): one child context per device;
+  // batch entry points shard their batch over the children (multi_* below)
+  std::vector<fts_ctx*> shards;
   PublicParams pp;
   int n = 0, k = 0;
   uint32_t* d_tables = nullptr;
@@ -276,6 +279,10 @@ struct fts_ctx {
   // of one lone 4,096-proof pass per free lane); an idle device starts at once
   size_t gather_target = 16384;
   int gather_us = 300;
+  // passes of up to com_fixed_max proofs compute com on the latency path (fixed-base
+  // groups, rp_kernels.hip k_rp_fixed_all), larger ones on the work path (Horner +
+  // joint GLV chains): the same group element either way
+  size_t com_fixed_max = 16384;
   // a lane was freed (call with mu held): the head pending range-proof request
   // becomes the next leader; LaneGuard waiters re-check too
   void wake_lane_waiters() {
@@ -310,6 +317,11 @@ struct LaneGuard {
 struct fts_rp_batch {
   int B = 0;
   int device = 0;
+  // staged on a multi-device context: one child batch per shard, shard j holds
+  // proofs [bounds[j], bounds[j+1]) of the caller's batch
+  std::vector<fts_rp_batch*> parts;
+  std::vector<fts_ctx*> part_ctx;
+  std::vector<size_t> bounds;
   int merged = 1;  // batches in the device pass that verified it last
   // timings of this batch's last verification
   int ntim = 0;
@@ -399,6 +411,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_COALESCE_MAX")) c->coalesce_max = (size_t)std::max(0L, atol(e));
   c->gather_target = c->coalesce_max / 2;
   if (const char* e = getenv("FTS_GATHER_US")) c->gather_us = std::max(0, atoi(e));
+  if (const char* e = getenv("FTS_COM_FIXED_MAX")) c->com_fixed_max = (size_t)std::max(0L, atol(e));
   // FTS_SIDE_STREAM=0: run each lane's side work on its main stream
   bool side = true;
   if (const char* e = getenv("FTS_SIDE_STREAM")) side = atoi(e) != 0;
@@ -510,6 +523,116 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   return FTS_API_OK;
 }
 
+// ------------------------------------------------------ multi-device layer
+// A context over several devices (fts_ctx_create_devices / _mask) owns one
+// child context per device -- its own fixed-base tables, lanes, streams and
+// workspace -- and parses the public parameters itself as a host-only context
+// (host provers, commitments).  Each batch entry point splits the caller's
+// batch into contiguous shards balanced by a cost weight (fts_shard_plan),
+// runs shard j on child j from its own host thread, and lets every child write
+// its verdicts straight into the caller's arrays at the shard's offset: the
+// verdicts come back in caller order.  The reference verifies every action
+// independently (core/common/validator.go:215-224), so no data crosses devices;
+// each device closes its own random-linear-combination check.
+extern "C" int fts_shard_plan(size_t n, const double* weights, int nshards, size_t* bounds) {
+  if (nshards < 1 || !bounds) return FTS_API_EINVAL;
+  double tot = 0;
+  for (size_t i = 0; i < n; i++) tot += weights ? std::max(0.0, weights[i]) : 1.0;
+  bounds[0] = 0;
+  size_t i = 0;
+  double acc = 0;
+  for (int j = 1; j < nshards; j++) {
+    const double target = tot * j / nshards;
+    // first index whose prefix weight reaches the target (never behind the previous cut)
+    while (i < n && acc + (weights ? std::max(0.0, weights[i]) : 1.0) * 0.5 <= target) {
+      acc += weights ? std::max(0.0, weights[i]) : 1.0;
+      i++;
+    }
+    bounds[j] = i;
+  }
+  bounds[nshards] = n;
+  return FTS_API_OK;
+}
+
+// run f(j, lo, hi) for every non-empty shard j concurrently; first error wins
+template <class F>
+static int run_shards(const std::vector<size_t>& bnd, F&& f) {
+  const int ns = (int)bnd.size() - 1;
+  std::vector<int> rc(ns, FTS_API_OK);
+  std::vector<std::thread> th;
+  for (int j = 0; j < ns; j++)
+    if (bnd[j + 1] > bnd[j]) th.emplace_back([&, j]() { rc[j] = f(j, bnd[j], bnd[j + 1]); });
+  for (auto& t : th) t.join();
+  for (int r : rc)
+    if (r != FTS_API_OK) return r;
+  return FTS_API_OK;
+}
+static std::vector<size_t> plan(size_t n, const std::vector<double>* w, int ns) {
+  std::vector<size_t> b(ns + 1);
+  fts_shard_plan(n, w ? w->data() : nullptr, ns, b.data());
+  return b;
+}
+
+extern "C" {
+
+int fts_ctx_create_devices(const uint8_t* pp, size_t pp_len, uint32_t bit_length, const int32_t* devices, int ndev,
+                           fts_ctx** out) {
+  if (!pp || !out || !devices || ndev < 1 || ndev > 64) return FTS_API_EINVAL;
+  *out = nullptr;
+  fts_ctx* c = nullptr;
+  // the parent: parsed parameters, host-only (host provers / commitments run here)
+  int rc = fts_ctx_create_bits(pp, pp_len, bit_length, FTS_DEVICE_NONE, &c);
+  if (rc != FTS_API_OK) return rc;
+  c->shards.assign(ndev, nullptr);
+  std::vector<int> crc(ndev, FTS_API_OK);
+  std::vector<std::thread> th;  // tables of every device built concurrently
+  for (int j = 0; j < ndev; j++)
+    th.emplace_back([&, j]() { crc[j] = fts_ctx_create_bits(pp, pp_len, bit_length, devices[j], &c->shards[j]); });
+  for (auto& t : th) t.join();
+  for (int j = 0; j < ndev; j++)
+    if (crc[j] != FTS_API_OK) rc = crc[j];
+  if (rc != FTS_API_OK) {
+    fts_ctx_destroy(c);
+    return rc;
+  }
+  c->device = c->shards[0]->device;
+  *out = c;
+  return FTS_API_OK;
+}
+
+int fts_ctx_create_mask(const uint8_t* pp, size_t pp_len, uint32_t bit_length, uint64_t device_mask, fts_ctx** out) {
+  std::vector<int32_t> devs;
+  for (int d = 0; d < 64; d++)
+    if ((device_mask >> d) & 1u) devs.push_back(d);
+  if (devs.empty()) return FTS_API_EINVAL;
+  return fts_ctx_create_devices(pp, pp_len, bit_length, devs.data(), (int)devs.size(), out);
+}
+
+int fts_ctx_devices(const fts_ctx* c, int32_t* devices, int cap) {
+  if (!c) return 0;
+  if (c->shards.empty()) {
+    if (devices && cap > 0) devices[0] = c->device;
+    return c->device == FTS_DEVICE_NONE ? 0 : 1;
+  }
+  for (int j = 0; j < (int)c->shards.size() && j < cap; j++)
+    if (devices) devices[j] = c->shards[j]->device;
+  return (int)c->shards.size();
+}
+
+}  // extern "C"
+
+static int multi_rp_verify(fts_ctx* c, size_t n, const uint8_t* const* der, const size_t* len, const uint8_t* com64,
+                           int32_t* status) {
+  return run_shards(plan(n, nullptr, (int)c->shards.size()), [&](int j, size_t lo, size_t hi) {
+    return fts_rp_verify_batch(c->shards[j], hi - lo, der + lo, len + lo, com64 + 64 * lo, status + lo);
+  });
+}
+
+// cost weight of an action: its range proofs (none for a 1-in/1-out transfer) + the sigma proof
+static double action_weight(size_t n_in, size_t n_out, bool transfer) {
+  return (transfer && n_in == 1 && n_out == 1 ? 0.0 : (double)n_out) + 0.25;
+}
+
 extern "C" {
 
 int fts_ctx_create(const uint8_t* pp, size_t pp_len, int device, fts_ctx** out) {
@@ -521,7 +644,9 @@ int fts_ctx_create_bits(const uint8_t* pp, size_t pp_len, uint32_t bit_length, i
 
 void fts_ctx_destroy(fts_ctx* c) {
   if (!c) return;
-  if (c->device == FTS_DEVICE_NONE) {
+  for (fts_ctx* ch : c->shards) fts_ctx_destroy(ch);
+  c->shards.clear();
+  if (c->device == FTS_DEVICE_NONE || c->lanes.empty()) {
     delete c;
     return;
   }
@@ -546,6 +671,11 @@ void fts_ctx_destroy(fts_ctx* c) {
 
 int fts_ctx_info(const fts_ctx* c, fts_pp_info* o) {
   if (!c || !o) return FTS_API_EINVAL;
+  if (!c->shards.empty()) {  // device of shard 0; tables summed over the devices
+    int rc = fts_ctx_info(c->shards[0], o);
+    for (size_t j = 1; j < c->shards.size(); j++) o->table_bytes += c->shards[j]->table_bytes;
+    return rc;
+  }
   o->bit_length = (uint32_t)c->pp.bit_length;
   o->rounds = (uint32_t)c->pp.rounds;
   o->curve_id = (uint32_t)c->pp.curve_id;
@@ -583,6 +713,7 @@ int fts_last_timings(const fts_ctx* c, const char** names, float* ms, int cap) {
 
 int fts_last_timings_ex(const fts_ctx* cc, const char** names, float* ms, double* mads, int cap) {
   if (!cc) return 0;
+  if (!cc->shards.empty()) return fts_last_timings_ex(cc->shards[0], names, ms, mads, cap);
   fts_ctx* c = const_cast<fts_ctx*>(cc);
   std::lock_guard<std::mutex> g(c->tim_mu);
   int m = std::min(cap, c->ntim);
@@ -706,7 +837,8 @@ static int rp_buffers(fts_ctx* c, Lane& L, int B) {
       w.scratch.ensure(std::max(rp_scratch_words(B, n, k), (size_t)B * 10 * 24) * 4) || w.r_key.ensure(32) ||
       w.r_msc.ensure((size_t)N * 32) || w.r_coef.ensure((size_t)B * 5 * 32) || w.r_colsum.ensure((3 + 2 * n) * 32) ||
       w.r_fixed.ensure((3 + 2 * n) * 96) || w.r_flag.ensure(4) || w.ypow.ensure((size_t)B * n * 32) ||
-      w.svec.ensure((size_t)B * n * 32) || !L.status_buf((size_t)B))
+      w.svec.ensure((size_t)B * n * 32) || ((size_t)B <= c->com_fixed_max && w.zvec.ensure((size_t)B * n * 32)) ||
+      !L.status_buf((size_t)B))
     return FTS_API_ENOMEM;
   return FTS_API_OK;
 }
@@ -762,7 +894,9 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
                w.terms.as<uint32_t>(),
                w.scratch.as<uint32_t>(),
                w.ypow.as<uint32_t>(),
-               w.svec.as<uint32_t>()};
+               w.svec.as<uint32_t>(),
+               w.zvec.as<uint32_t>(),
+               (size_t)B <= c->com_fixed_max ? 1 : 0};
   RlcDev r{w.r_key.as<uint32_t>(), w.r_msc.as<uint32_t>(),   w.r_coef.as<uint32_t>(), w.r_colsum.as<uint32_t>(),
            w.r_fixed.as<uint32_t>(), w.r_flag.as<int32_t>(), w.m_scratch.as<uint32_t>(), mp};
   // fresh RLC weights key (getrandom), unpredictable to the provers
@@ -858,6 +992,7 @@ extern "C" {
 //   ch_out: (8 + 2k) x 32 bytes canonical BE Fr  [x, x^2, y, y^-1, z, z^2, polEval, x0, x_j.., x_j^-1..]
 //   com_out: 64 bytes com (BE) ; hp_out: n x 64 bytes H'_i (BE)
 int fts_debug_rp_intermediates(fts_ctx* c, size_t i, uint8_t* ch_out, uint8_t* com_out, uint8_t* hp_out) {
+  if (c && !c->shards.empty()) return fts_debug_rp_intermediates(c->shards[0], i, ch_out, com_out, hp_out);
   if (!c || c->device < 0) return FTS_API_EINVAL;
   int want;
   {
@@ -885,6 +1020,7 @@ int fts_debug_rp_intermediates(fts_ctx* c, size_t i, uint8_t* ch_out, uint8_t* c
 // debug: bucket-occupancy statistics of the last RLC MSM
 // out[0] = max bucket count, out[1] = its bucket index, out[2] = NB, out[3] = #nonzero buckets
 int fts_debug_msm_stats(fts_ctx* c, int64_t* out) {
+  if (c && !c->shards.empty()) return fts_debug_msm_stats(c->shards[0], out);
   if (!c || c->device < 0 || !out) return FTS_API_EINVAL;
   int want;
   {
@@ -911,6 +1047,23 @@ int fts_debug_msm_stats(fts_ctx* c, int64_t* out) {
 int fts_rp_batch_stage(fts_ctx* c, size_t n, const uint8_t* const* rp_der, const size_t* rp_len, const uint8_t* com64,
                        fts_rp_batch** out) {
   if (!c || !out || (n && (!rp_der || !rp_len || !com64))) return FTS_API_EINVAL;
+  if (!c->shards.empty()) {  // one child batch per device, contiguous shards
+    fts_rp_batch* b = new fts_rp_batch();
+    b->B = (int)n;
+    b->device = c->device;
+    b->bounds = plan(n, nullptr, (int)c->shards.size());
+    b->parts.assign(c->shards.size(), nullptr);
+    b->part_ctx = c->shards;
+    int rc = run_shards(b->bounds, [&](int j, size_t lo, size_t hi) {
+      return fts_rp_batch_stage(c->shards[j], hi - lo, rp_der + lo, rp_len + lo, com64 + 64 * lo, &b->parts[j]);
+    });
+    if (rc != FTS_API_OK) {
+      fts_rp_batch_free(b);
+      return rc;
+    }
+    *out = b;
+    return FTS_API_OK;
+  }
   if (c->device < 0) return FTS_API_EDEVICE;
   HIP_OK(hipSetDevice(c->device));
   RpHost h;
@@ -938,6 +1091,17 @@ int fts_rp_batch_stage(fts_ctx* c, size_t n, const uint8_t* const* rp_der, const
 
 int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
   if (!c || !b) return FTS_API_EINVAL;
+  if (!b->parts.empty()) {
+    if (c->shards != b->part_ctx) return FTS_API_EINVAL;  // staged on another context
+    int m = 0;
+    int rc = run_shards(b->bounds, [&](int j, size_t lo, size_t hi) {
+      return fts_rp_batch_verify(c->shards[j], b->parts[j], status ? status + lo : nullptr);
+    });
+    for (fts_rp_batch* q : b->parts)
+      if (q) m = std::max(m, q->merged);
+    b->merged = m;
+    return rc;
+  }
   if (c->device < 0) return FTS_API_EDEVICE;
   if (b->B == 0) return FTS_API_OK;
   HIP_OK(hipSetDevice(c->device));
@@ -1000,6 +1164,7 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
 
 int fts_rp_batch_timings(const fts_rp_batch* b, const char** names, float* ms, double* mads, int cap) {
   if (!b) return 0;
+  if (!b->parts.empty()) return b->parts[0] ? fts_rp_batch_timings(b->parts[0], names, ms, mads, cap) : 0;
   int m = std::min(cap, b->ntim);
   for (int i = 0; i < m; i++) {
     if (names) names[i] = b->tim_name[i];
@@ -1013,6 +1178,11 @@ int fts_rp_batch_merged(const fts_rp_batch* b) { return b ? b->merged : 0; }
 
 int fts_ctx_reserve(fts_ctx* c, size_t max_pass_proofs) {
   if (!c) return FTS_API_EINVAL;
+  if (!c->shards.empty()) {
+    std::vector<size_t> all(c->shards.size() + 1);
+    for (size_t j = 0; j < all.size(); j++) all[j] = j;  // one "item" per device
+    return run_shards(all, [&](int j, size_t, size_t) { return fts_ctx_reserve(c->shards[j], max_pass_proofs); });
+  }
   if (c->device < 0) return FTS_API_EDEVICE;
   const size_t B = max_pass_proofs ? max_pass_proofs : c->coalesce_max;
   if (B == 0 || B > (1u << 20)) return FTS_API_ESIZE;
@@ -1049,6 +1219,7 @@ void fts_msm_free(fts_msm_batch* b) {
 }
 
 int fts_msm_stage(fts_ctx* c, size_t n, const uint8_t* points64, const uint8_t* scalars32, fts_msm_batch** out) {
+  if (c && !c->shards.empty()) return fts_msm_stage(c->shards[0], n, points64, scalars32, out);
   if (!c || !out || !n || !points64 || !scalars32 || n > (size_t)(1u << 26)) return FTS_API_EINVAL;
   if (c->device < 0) return FTS_API_EDEVICE;
   HIP_OK(hipSetDevice(c->device));
@@ -1089,6 +1260,7 @@ int fts_msm_stage(fts_ctx* c, size_t n, const uint8_t* points64, const uint8_t* 
 }
 
 int fts_msm_run(fts_ctx* c, fts_msm_batch* b, uint8_t* out64) {
+  if (c && !c->shards.empty()) return fts_msm_run(c->shards[0], b, out64);
   if (!c || !b || !out64) return FTS_API_EINVAL;
   if (c->device < 0) return FTS_API_EDEVICE;
   HIP_OK(hipSetDevice(c->device));
@@ -1130,6 +1302,23 @@ int fts_msm_g1(fts_ctx* c, size_t n, const uint8_t* points64, const uint8_t* sca
     memset(out64, 0, 64);
     return FTS_API_OK;
   }
+  if (c && !c->shards.empty()) {
+    // partial MSM per device, the partial points combined on the host
+    const std::vector<size_t> bnd = plan(n, nullptr, (int)c->shards.size());
+    std::vector<uint8_t> part(64 * c->shards.size(), 0);
+    int rc = run_shards(bnd, [&](int j, size_t lo, size_t hi) {
+      return fts_msm_g1(c->shards[j], hi - lo, points64 + 64 * lo, scalars32 + 32 * lo, &part[64 * j]);
+    });
+    if (rc != FTS_API_OK) return rc;
+    G1J acc = jac_identity();
+    for (size_t j = 0; j < c->shards.size(); j++) {
+      G1A a;
+      if (!g1_from_bytes(&part[64 * j], 64, a)) return FTS_API_EDEVICE;
+      acc = jadd_aff(acc, a);
+    }
+    g1_to_bytes(to_aff(acc), out64);
+    return FTS_API_OK;
+  }
   fts_msm_batch* b = nullptr;
   int rc = fts_msm_stage(c, n, points64, scalars32, &b);
   if (rc != FTS_API_OK) return rc;
@@ -1140,6 +1329,11 @@ int fts_msm_g1(fts_ctx* c, size_t n, const uint8_t* points64, const uint8_t* sca
 
 void fts_rp_batch_free(fts_rp_batch* b) {
   if (!b) return;
+  if (!b->parts.empty() || !b->part_ctx.empty()) {
+    for (fts_rp_batch* q : b->parts) fts_rp_batch_free(q);
+    delete b;
+    return;
+  }
   hipSetDevice(b->device);
   for (void* p : {(void*)b->raw, (void*)b->sc, (void*)b->status0, (void*)b->status, (void*)b->ipa_flag})
     if (p) hipFree(p);
@@ -1150,6 +1344,10 @@ int fts_rp_verify_batch(fts_ctx* c, size_t n, const uint8_t* const* rp_der, cons
                         int32_t* status) {
   if (!c || !status) return FTS_API_EINVAL;
   if (n == 0) return FTS_API_OK;
+  if (!c->shards.empty()) {
+    if (!rp_der || !rp_len || !com64) return FTS_API_EINVAL;
+    return multi_rp_verify(c, n, rp_der, rp_len, com64, status);
+  }
   fts_rp_batch* b = nullptr;
   int rc = fts_rp_batch_stage(c, n, rp_der, rp_len, com64, &b);
   if (rc != FTS_API_OK) {
@@ -1529,6 +1727,14 @@ extern "C" {
 int fts_transfer_verify_batch(fts_ctx* c, size_t n, const fts_transfer_item* items, int32_t* status,
                               int32_t* fail_index) {
   if (!c || !status || (n && !items)) return FTS_API_EINVAL;
+  if (!c->shards.empty()) {
+    std::vector<double> w(n);
+    for (size_t i = 0; i < n; i++) w[i] = action_weight(items[i].n_in, items[i].n_out, true);
+    return run_shards(plan(n, &w, (int)c->shards.size()), [&](int j, size_t lo, size_t hi) {
+      return fts_transfer_verify_batch(c->shards[j], hi - lo, items + lo, status + lo,
+                                       fail_index ? fail_index + lo : nullptr);
+    });
+  }
   if (c->device < 0) return FTS_API_EDEVICE;
   if (n == 0) return FTS_API_OK;
   std::vector<ActionIn> acts(n);
@@ -1545,6 +1751,13 @@ int fts_transfer_verify_batch(fts_ctx* c, size_t n, const fts_transfer_item* ite
 
 int fts_issue_verify_batch(fts_ctx* c, size_t n, const fts_issue_item* items, int32_t* status, int32_t* fail_index) {
   if (!c || !status || (n && !items)) return FTS_API_EINVAL;
+  if (!c->shards.empty()) {
+    std::vector<double> w(n);
+    for (size_t i = 0; i < n; i++) w[i] = action_weight(0, items[i].n_tok, false);
+    return run_shards(plan(n, &w, (int)c->shards.size()), [&](int j, size_t lo, size_t hi) {
+      return fts_issue_verify_batch(c->shards[j], hi - lo, items + lo, status + lo, fail_index ? fail_index + lo : nullptr);
+    });
+  }
   if (c->device < 0) return FTS_API_EDEVICE;
   if (n == 0) return FTS_API_OK;
   std::vector<ActionIn> acts(n);
@@ -1565,6 +1778,22 @@ int fts_actions_verify_batch(fts_ctx* c, size_t n_tr, const fts_transfer_item* t
                              const fts_issue_item* issues, int32_t* status_tr, int32_t* fail_tr, int32_t* status_is,
                              int32_t* fail_is) {
   if (!c || (n_tr && (!transfers || !status_tr)) || (n_is && (!issues || !status_is))) return FTS_API_EINVAL;
+  if (!c->shards.empty()) {  // transfers and issues each split into balanced shards, device j gets part j of both
+    const int ns = (int)c->shards.size();
+    std::vector<double> wt(n_tr), wi(n_is);
+    for (size_t i = 0; i < n_tr; i++) wt[i] = action_weight(transfers[i].n_in, transfers[i].n_out, true);
+    for (size_t i = 0; i < n_is; i++) wi[i] = action_weight(0, issues[i].n_tok, false);
+    const std::vector<size_t> bt = plan(n_tr, &wt, ns), bi = plan(n_is, &wi, ns);
+    std::vector<size_t> all(ns + 1);
+    for (int j = 0; j <= ns; j++) all[j] = j;
+    return run_shards(all, [&](int j, size_t, size_t) {
+      const size_t t0 = bt[j], t1 = bt[j + 1], i0 = bi[j], i1 = bi[j + 1];
+      if (t1 == t0 && i1 == i0) return FTS_API_OK;
+      return fts_actions_verify_batch(c->shards[j], t1 - t0, transfers + t0, i1 - i0, issues + i0,
+                                      status_tr ? status_tr + t0 : nullptr, fail_tr ? fail_tr + t0 : nullptr,
+                                      status_is ? status_is + i0 : nullptr, fail_is ? fail_is + i0 : nullptr);
+    });
+  }
   if (c->device < 0) return FTS_API_EDEVICE;
   const size_t n = n_tr + n_is;
   if (n == 0) return FTS_API_OK;
@@ -1600,6 +1829,14 @@ int fts_actions_verify_batch(fts_ctx* c, size_t n_tr, const fts_transfer_item* t
 int fts_request_verify_batch(fts_ctx* c, size_t n, const uint8_t* const* req, const size_t* req_len,
                              int32_t* status, int32_t* fail_action, int32_t* fail_index) {
   if (!c || !status || (n && (!req || !req_len))) return FTS_API_EINVAL;
+  if (!c->shards.empty()) {  // request bytes approximate the proofs they carry
+    std::vector<double> w(n);
+    for (size_t i = 0; i < n; i++) w[i] = (double)req_len[i] + 64.0;
+    return run_shards(plan(n, &w, (int)c->shards.size()), [&](int j, size_t lo, size_t hi) {
+      return fts_request_verify_batch(c->shards[j], hi - lo, req + lo, req_len + lo, status + lo,
+                                      fail_action ? fail_action + lo : nullptr, fail_index ? fail_index + lo : nullptr);
+    });
+  }
   if (c->device < 0) return FTS_API_EDEVICE;
   if (n == 0) return FTS_API_OK;
   namespace rq = fts::host::req;
@@ -1835,6 +2072,10 @@ extern "C" {
 int fts_token_open_batch(fts_ctx* c, size_t n, const fts_token_opening* items, int32_t* status) {
   if (!c || n > (size_t)(1u << 26) || (n && (!items || !status))) return FTS_API_EINVAL;
   if (n == 0) return FTS_API_OK;
+  if (!c->shards.empty())
+    return run_shards(plan(n, nullptr, (int)c->shards.size()), [&](int j, size_t lo, size_t hi) {
+      return fts_token_open_batch(c->shards[j], hi - lo, items + lo, status + lo);
+    });
   if (c->device < 0) return FTS_API_EDEVICE;
   HIP_OK(hipSetDevice(c->device));
   LaneGuard lg(c);
@@ -2092,6 +2333,8 @@ int fts_rp_prove_batch_gpu(fts_ctx* c, size_t N, const uint64_t* values, const u
   if (!c || !values || !bfs || !out || !offsets || !lens || !com64_out || N > (size_t)(1u << 24))
     return FTS_API_EINVAL;
   if (N == 0) return FTS_API_OK;
+  if (!c->shards.empty())  // provers run on the first device of a multi-device context
+    return fts_rp_prove_batch_gpu(c->shards[0], N, values, bfs, seed, out, out_cap, offsets, lens, com64_out);
   if (c->device < 0) return FTS_API_EDEVICE;
   HIP_OK(hipSetDevice(c->device));
   RngSource src(seed);
@@ -2280,10 +2523,12 @@ static int actions_prove_device(fts_ctx* c, size_t A, const fts_action_witness* 
 extern "C" {
 int fts_transfer_prove_batch_gpu(fts_ctx* c, size_t n, const fts_action_witness* w, uint64_t seed, uint8_t* out,
                                  size_t out_cap, size_t* offsets, size_t* lens) {
+  if (c && !c->shards.empty()) c = c->shards[0];
   return actions_prove_device(c, n, w, 0, seed, out, out_cap, offsets, lens);
 }
 int fts_issue_prove_batch_gpu(fts_ctx* c, size_t n, const fts_action_witness* w, uint64_t seed, uint8_t* out,
                               size_t out_cap, size_t* offsets, size_t* lens) {
+  if (c && !c->shards.empty()) c = c->shards[0];
   return actions_prove_device(c, n, w, 1, seed, out, out_cap, offsets, lens);
 }
 }  // extern "C"
@@ -2294,6 +2539,10 @@ int fts_token_metadata_open_batch(fts_ctx* c, size_t n, const uint8_t* com64, co
                                   const size_t* meta_len, int32_t* status) {
   if (!c || n > (size_t)(1u << 26) || (n && (!com64 || !meta || !meta_len || !status))) return FTS_API_EINVAL;
   if (n == 0) return FTS_API_OK;
+  if (!c->shards.empty())
+    return run_shards(plan(n, nullptr, (int)c->shards.size()), [&](int j, size_t lo, size_t hi) {
+      return fts_token_metadata_open_batch(c->shards[j], hi - lo, com64 + 64 * lo, meta + lo, meta_len + lo, status + lo);
+    });
   std::vector<req::TokenMeta> md(n);
   std::vector<fts_token_opening> items(n);
   parallel_for(n, 1024, [&](size_t i) {

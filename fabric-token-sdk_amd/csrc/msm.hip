@@ -191,14 +191,24 @@ __global__ void __launch_bounds__(64, 4) k_msm_chunks(int N, int nw, const uint3
   const uint32_t* S = sorted + offsets[b];
   const Fp beta = glv_beta();
   G1J acc = g1j_identity();
+  // the next entry's point is gathered while the current addition runs
+  uint32_t e = S[lo];
+  G1A q = load_g1a(points + (size_t)((e & 0x7fffffffu) >= (uint32_t)N ? (e & 0x7fffffffu) - N : (e & 0x7fffffffu)) * 16);
   for (uint32_t t = lo; t < hi; t++) {
-    const uint32_t e = S[t], v = e & 0x7fffffffu;
-    const bool ph = v >= (uint32_t)N;
-    G1A q = load_g1a(points + (size_t)(ph ? v - N : v) * 16);
-    if (g1a_is_identity(q)) continue;
-    if (ph) q.x = fp_mul(q.x, beta);
-    if (e >> 31) q.y = f_neg(q.y);
-    madd_inl(acc, q);
+    uint32_t en = 0;
+    G1A qn;
+    if (t + 1 < hi) {
+      en = S[t + 1];
+      const uint32_t vn = en & 0x7fffffffu;
+      qn = load_g1a(points + (size_t)(vn >= (uint32_t)N ? vn - N : vn) * 16);
+    }
+    if (!g1a_is_identity(q)) {
+      if ((e & 0x7fffffffu) >= (uint32_t)N) q.x = fp_mul(q.x, beta);
+      if (e >> 31) q.y = f_neg(q.y);
+      madd_inl(acc, q);
+    }
+    e = en;
+    q = qn;
   }
   store_g1j(partials + (size_t)g * 24, acc);
 }
@@ -280,27 +290,32 @@ __global__ void __launch_bounds__(256) k_msm_windows(int nw, int WB, const MsmWi
   if (t == 0) store_g1j(parts + ((size_t)w * WB + j) * 24, acc);
 }
 
-// lane w <= nw: W_w = sum of window w's parts; then lane 0:
-// result = sum_w 2^off_w W_w (Horner) + W_nw (the extra points)
+// lane w <= nw: W_w = sum of window w's parts, shifted to its bit offset
+// (2^off_w W_w: the windows' doubling chains run in parallel lanes, the longest
+// is the top window's ~off_top doublings instead of one 127-doubling Horner
+// chain), lane nw: the extra points; then an LDS tree over the lanes
 __global__ void __launch_bounds__(64) k_msm_final(int nw, int WB, const MsmWindow* __restrict__ win,
                                                   const uint32_t* __restrict__ parts, uint32_t* __restrict__ wins,
                                                   uint32_t* __restrict__ out) {
+  __shared__ uint32_t sh[64 * 24];
   const int t = threadIdx.x;
+  G1J acc = g1j_identity();
   for (int w = t; w <= nw; w += 64) {
-    G1J acc = load_g1j(parts + (size_t)w * WB * 24);
-    for (int j = 1; j < WB; j++) add_inl(acc, load_g1j(parts + ((size_t)w * WB + j) * 24));
-    store_g1j(wins + (size_t)w * 24, acc);
+    G1J W = load_g1j(parts + (size_t)w * WB * 24);
+    for (int j = 1; j < WB; j++) add_inl(W, load_g1j(parts + ((size_t)w * WB + j) * 24));
+    if (w < nw)
+      for (int q = 0; q < win[w].off; q++) W = g1j_dbl(W);
+    add_inl(acc, W);
   }
+  store_g1j(sh + t * 24, acc);
   __syncthreads();
-  if (t != 0) return;
-  G1J acc = load_g1j(wins + (size_t)(nw - 1) * 24);
-  for (int w = nw - 2; w >= 0; w--) {
-    const int shift = win[w + 1].off - win[w].off;
-    for (int q = 0; q < shift; q++) acc = g1j_dbl(acc);
-    add_inl(acc, load_g1j(wins + (size_t)w * 24));
+  for (int half = 32; half >= 1; half >>= 1) {
+    if (t < half) add_inl(acc, load_g1j(sh + (t + half) * 24));
+    __syncthreads();
+    if (t < half) store_g1j(sh + t * 24, acc);
+    __syncthreads();
   }
-  add_inl(acc, load_g1j(wins + (size_t)nw * 24));
-  store_g1j(out, acc);
+  if (t == 0) store_g1j(out, acc);
 }
 
 // ------------------------------------------------ standalone MSM (fts_msm_*)
@@ -375,7 +390,11 @@ void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalar
                      parts);
   tl->mark("k_msm_windows", s, (double)(p.NS + nextra) * COST_ADD);
   hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, s, p.nw, p.WB, p.d_win, parts, p.wins, p.out);
-  tl->mark("k_msm_final", s, (double)MSM_BITS * COST_DBL + p.nw * COST_ADD);
+  {
+    double dbl = 0;
+    for (int w = 0; w < p.nw; w++) dbl += p.win[w].off;
+    tl->mark("k_msm_final", s, dbl * COST_DBL + (p.nw + 1) * (p.WB + 1) * COST_ADD);
+  }
 }
 
 void launch_msm_load(int N, const uint8_t* raw_pts, const uint8_t* raw_sc, uint32_t* pts, uint32_t* sc, uint32_t* bad,

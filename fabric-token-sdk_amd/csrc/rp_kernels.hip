@@ -153,6 +153,7 @@ __global__ void __launch_bounds__(64) k_rp_hash_small(int B, int n, int k, const
   if (m == 0) {
     const uint8_t* px[2] = {P + RP_PT_T1 * 64, P + RP_PT_T2 * 64};
     h = hash_raw_points(slot, px, 2);
+    store_f(reinterpret_cast<uint32_t*>(slot), h);  // canonical x for k_rp_xd (runs beside k_rp_chal_fr)
     dst = CH_X;
   } else if (m == 1) {
     const uint8_t* py[3] = {P + RP_PT_C * 64, P + RP_PT_D * 64, P + RP_PT_V * 64};
@@ -244,9 +245,11 @@ __global__ void __launch_bounds__(64) k_rp_chal_fr(int B, int n, int k, const in
 // H'_fin = sum s_i^-1 H'_i = sum s_{n-1-i} H'_i).  The chunk's high index
 // bits give a common prefix product; the low bits expand as a binary tree.
 constexpr int PW_LC = 3, PW_CH = 1 << PW_LC;
+// (latency path, zvec != nullptr: also zvec[i][b] = z^2 2^i y^-i, the scalars of
+// the com terms Z_i of k_rp_fixed_all)
 __global__ void __launch_bounds__(64) k_rp_powers(int B, int n, int k, const int32_t* __restrict__ status,
                                                   const uint32_t* __restrict__ ch, uint32_t* __restrict__ ypow,
-                                                  uint32_t* __restrict__ svec) {
+                                                  uint32_t* __restrict__ svec, uint32_t* __restrict__ zvec) {
   const int lc = min(PW_LC, k), cs = 1 << lc, nch = n >> lc;
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * nch) return;
@@ -257,9 +260,18 @@ __global__ void __launch_bounds__(64) k_rp_powers(int B, int n, int k, const int
   Fr yinv;
   load_f(C + CH_YINV * 8, yinv);
   Fr yp = fr_pow_small(yinv, (uint32_t)i0);
+  Fr zv;  // z^2 2^i
+  if (zvec) {
+    load_f(C + CH_Z2 * 8, zv);
+    for (int i = 0; i < i0; i++) zv = f_add(zv, zv);
+  }
   for (int q = 0; q < cs; q++) {
     if (q) yp = fr_mul(yp, yinv);
     store_f(ypow + ((size_t)(i0 + q) * B + b) * 8, yp);
+    if (zvec) {
+      store_f(zvec + ((size_t)(i0 + q) * B + b) * 8, fr_mul(zv, yp));
+      zv = f_add(zv, zv);
+    }
   }
   // prefix over the high bits: j = 0 .. k-1-lc  (bit k-1-j of i0)
   Fr pre = f_one<FrP>();
@@ -431,6 +443,112 @@ __global__ void __launch_bounds__(64) k_rp_com_sum(int B, int n, int k, const in
   G1J acc = g1j_from_affine(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_C) * 16));
   for (int q = 0; q < COM_NTERMS; q++) add_inl(acc, load_g1j(T + q * 24));
   store_g1j(hpj + ((size_t)b * (n + 1) + n) * 24, acc);
+}
+
+// ----------------------------------------- com, latency path (small passes)
+// The same group element as the work path below/above, computed without a
+// per-proof doubling chain on the critical path (bulletproof.go:477-492):
+//   com = C + x*D + z*K - delta*P + sum_i (z^2 2^i y^-i) H_i
+// (z^2 2^i H'_i = z^2 2^i y^-i H_i): the n z^2-terms become fixed-base products
+// on the 20-bit tables of H_i, computed by the same lanes as the H'_i
+// (k_rp_fixed_all: two products per lane, same table), summed by an LDS tree
+// (k_rp_com_tree); x*D runs beside them on the side stream (k_rp_xd, one GLV
+// half per lane, started right after the x transcript).  ~3.8 k more products
+// per rp64 than the work path, but every product runs at the fixed-base
+// kernels' occupancy: used for passes of up to FTS_COM_FIXED_MAX proofs, where
+// the work path's per-proof chains leave most SIMDs idle.
+// terms layout [B][n + 4][24]: Z_0..Z_{n-1}, z K, -delta P, x*D halves
+inline __host__ __device__ int com_fx_slots(int n) { return n + 4; }
+
+// lane per (item, proof), proof index fastest (a wave's 64 lanes gather from
+// the same table), one fixed-base product per lane: items i < n: H'_i = y^-i H_i
+// -> hpj[b][i]; items n + i: Z_i = (z^2 2^i y^-i) H_i -> terms[b][i]; item 2n:
+// z K -> terms[b][n]; item 2n + 1: -delta P -> terms[b][n + 1]
+__global__ void __launch_bounds__(64, 4) k_rp_fixed_all(int B, int n, int k, const int32_t* __restrict__ status,
+                                                        const uint32_t* __restrict__ sc, const uint32_t* __restrict__ ch,
+                                                        const uint32_t* __restrict__ ypow,
+                                                        const uint32_t* __restrict__ zvec,
+                                                        const uint32_t* __restrict__ wtables, uint32_t* __restrict__ hpj,
+                                                        uint32_t* __restrict__ terms) {
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (size_t)(2 * n + 2) * B) return;
+  const int t = (int)(gid / B), b = (int)(gid % B);
+  if (status[b] != 0) return;
+  const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
+  const int base = t < n ? t : t - n;  // H_i (i < n), K (n), P (n + 1)
+  Scalar sk;
+  if (t < 2 * n) {
+    Fr v;
+    load_f((t < n ? ypow : zvec) + ((size_t)base * B + b) * 8, v);
+    sk = fr_canon(v);
+  } else if (t == 2 * n) {
+    Fr z;
+    load_f(C + CH_Z * 8, z);
+    sk = fr_canon(z);
+  } else {
+    Fr d;
+    load_f(sc + ((size_t)b * RP_NSC + RP_SC_DELTA) * 8, d);  // canonical
+    const Fr nd = f_neg(d);
+#pragma unroll
+    for (int q = 0; q < 8; q++) sk.v[q] = nd.v[q];
+  }
+  const G1J r = fb_mul_w<FBW_W>(wtables + (size_t)base * FbWide::WORDS_PER_BASE, sk);
+  uint32_t* out = t < n ? hpj + ((size_t)b * (n + 1) + t) * 24 : terms + ((size_t)b * com_fx_slots(n) + base) * 24;
+  store_g1j(out, r);
+}
+
+// x*D (bulletproof.go:478), one GLV half per lane: x = x1 + x2 lambda, lane h
+// computes x_h phi^h(D) -> terms[b][n + 2 + h]; lane tables 1..8 * P in vtab.
+// x is read from the digest k_rp_hash_small left at the head of its slot
+// (canonical), so this runs concurrently with k_rp_chal_fr.
+__global__ void __launch_bounds__(64) k_rp_xd(int B, int n, int k, const int32_t* __restrict__ status,
+                                              const uint32_t* __restrict__ pts, const uint8_t* __restrict__ small_msgs,
+                                              uint32_t* __restrict__ vtab, uint32_t* __restrict__ terms) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= 2 * B) return;
+  const int h = gid / B, b = gid % B;
+  if (status[b] != 0) return;
+  Fr x;
+  load_f(reinterpret_cast<const uint32_t*>(small_msgs + (size_t)b * (2 + k) * SMALL_SLOT), x);
+  uint32_t xk[2][4], xs[2];
+  glv_decompose(x.v, xk[0], xs[0], xk[1], xs[1]);
+  G1J D = g1j_from_affine(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_D) * 16));
+  if (h) D.x = fp_mul(D.x, glv_beta());
+  if (xs[h]) D.y = f_neg(D.y);
+  const G1J r = vb128j(D, xk[h], vtab, (size_t)2 * B, (size_t)gid);
+  store_g1j(terms + ((size_t)b * com_fx_slots(n) + n + 2 + h) * 24, r);
+}
+
+// com = C + sum of the n + 4 terms: CT_LANES lanes per proof (CT_PROOFS proofs
+// per block), lane l sums slots l, l + CT_LANES, ... (5 full additions at
+// n = 64), then a log2(CT_LANES)-level LDS tree -> hpj[b][n]
+constexpr int CT_LANES = 16, CT_PROOFS = 16;
+__global__ void __launch_bounds__(CT_LANES * CT_PROOFS) k_rp_com_tree(int B, int n, int k,
+                                                                      const int32_t* __restrict__ status,
+                                                                      const uint32_t* __restrict__ pts,
+                                                                      const uint32_t* __restrict__ terms,
+                                                                      uint32_t* __restrict__ hpj) {
+  __shared__ uint32_t sh[CT_LANES * CT_PROOFS * 24];
+  const int l = threadIdx.x % CT_LANES, pl = threadIdx.x / CT_LANES;
+  const int b = blockIdx.x * CT_PROOFS + pl;
+  const bool live = b < B && status[b] == 0;
+  const int ns = com_fx_slots(n);
+  G1J acc = g1j_identity();
+  if (live) {
+    const uint32_t* T = terms + (size_t)b * ns * 24;
+    if (l == 0) acc = g1j_from_affine(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_C) * 16));
+    for (int q = l; q < ns; q += CT_LANES) add_inl(acc, load_g1j(T + q * 24));
+  }
+  uint32_t* S = sh + (size_t)pl * CT_LANES * 24;
+  store_g1j(S + l * 24, acc);
+  __syncthreads();
+  for (int half = CT_LANES / 2; half >= 1; half >>= 1) {
+    if (live && l < half) add_inl(acc, load_g1j(S + (l + half) * 24));
+    __syncthreads();
+    if (live && l < half) store_g1j(S + l * 24, acc);
+    __syncthreads();
+  }
+  if (live && l == 0) store_g1j(hpj + ((size_t)b * (n + 1) + n) * 24, acc);
 }
 
 // Batch affine normalisation (Montgomery's trick), NORM_E points per lane and
@@ -1020,27 +1138,51 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   tl->mark("k_rp_decode", s, 0);
   FTS_LAUNCH(k_rp_hash_small, B * (2 + k), 64, s, B, n, k, d.raw, d.status, d.ch, d.small_msgs);
   tl->mark("k_rp_hash_small", s, 0);
+  const int nhp = B * n;
+  if (d.com_fixed) {
+    // latency path: x*D on the side stream beside chal_fr and the fixed-base products
+    tl->fork(s, s2);
+    FTS_LAUNCH(k_rp_xd, 2 * B, 64, s2, B, n, k, d.status, d.pts, d.small_msgs, d.scratch + (size_t)B * (k + 1) * 8,
+               d.terms);
+    tl->mark("k_rp_xd", s2, (double)B * 2 * COST_VB128);
+  }
   FTS_LAUNCH(k_rp_chal_fr, B, 64, s, B, n, k, d.status, d.ch, d.scratch);
   tl->mark("k_rp_chal_fr", s, (double)B * (3 * k + 4 * (k + 1) + 12));
-  FTS_LAUNCH(k_rp_powers, B * (n >> std::min(PW_LC, k)), 64, s, B, n, k, d.status, d.ch, d.ypow, d.svec);
-  tl->mark("k_rp_powers", s, (double)B * (2.0 * n + 2.0 * k));
-  FTS_LAUNCH(k_rp_fixed_exact, B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, wtables, d.hpj, d.terms);
-  tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FBW_FRESH);
-  // H'_i -> affine + BE bytes (x0 transcript) now; com is normalised after com_sum
-  const int nhp = B * n;
-  FTS_LAUNCH(k_rp_normalize, (nhp + NORM_E - 1) / NORM_E, NORM_BS, s, nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be);
-  tl->mark("k_rp_normalize", s, (double)nhp * (2.0 * 8.0 / NORM_E + 9.0));
-  const int nch = (n + HS_CHUNK - 1) / HS_CHUNK;
-  FTS_LAUNCH(k_rp_hsum_chunks, B * nch, 64, s, B, n, d.status, d.hpa, d.scratch);
-  tl->mark("k_rp_hsum_chunks", s, (double)B * (n - nch) * (COST_DBL + COST_MADD));
-  FTS_LAUNCH(k_rp_hsum_join, B, 64, s, B, n, d.status, d.scratch);
-  tl->mark("k_rp_hsum_join", s, (double)B * (nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD));
-  // scratch: [0, B*192) Horner chunks of S, then the 2B lanes' joint tables
-  FTS_LAUNCH(k_rp_com_var, 2 * B, 64, s, B, n, k, d.status, d.pts, d.ch, d.scratch, d.scratch + (size_t)B * HS_SCRATCH,
-             d.terms);
-  tl->mark("k_rp_com_var", s, (double)B * 2 * COST_STRAUS2);
-  FTS_LAUNCH(k_rp_com_sum, B, 64, s, B, n, k, d.status, d.pts, d.terms, d.hpj);
-  tl->mark("k_rp_com_sum", s, (double)B * COM_NTERMS * COST_ADD);
+  if (d.com_fixed) {
+    FTS_LAUNCH(k_rp_powers, B * (n >> std::min(PW_LC, k)), 64, s, B, n, k, d.status, d.ch, d.ypow, d.svec, d.zvec);
+    tl->mark("k_rp_powers", s, (double)B * (3.0 * n + 2.0 * k));
+    FTS_LAUNCH(k_rp_fixed_all, (size_t)B * (2 * n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, d.zvec, wtables,
+               d.hpj, d.terms);
+    tl->mark("k_rp_fixed_all", s, (double)B * (2.0 * n + 2.0) * COST_FBW_FRESH);
+    FTS_LAUNCH(k_rp_normalize, (nhp + NORM_E - 1) / NORM_E, NORM_BS, s, nhp, n, n + 1, 0, d.status, d.hpj, d.hpa,
+               d.hp_be);
+    tl->mark("k_rp_normalize", s, (double)nhp * (2.0 * 8.0 / NORM_E + 9.0));
+    tl->fork(s2, s);
+    hipLaunchKernelGGL(k_rp_com_tree, dim3((B + CT_PROOFS - 1) / CT_PROOFS), dim3(CT_LANES * CT_PROOFS), 0, s, B, n,
+                       k, d.status, d.pts, d.terms, d.hpj);
+    tl->mark("k_rp_com_sum", s, (double)B * (com_fx_slots(n) + 1) * COST_ADD);
+  } else {
+    FTS_LAUNCH(k_rp_powers, B * (n >> std::min(PW_LC, k)), 64, s, B, n, k, d.status, d.ch, d.ypow, d.svec,
+               (uint32_t*)nullptr);
+    tl->mark("k_rp_powers", s, (double)B * (2.0 * n + 2.0 * k));
+    FTS_LAUNCH(k_rp_fixed_exact, B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, wtables, d.hpj, d.terms);
+    tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FBW_FRESH);
+    // H'_i -> affine + BE bytes (x0 transcript) now; com is normalised after com_sum
+    FTS_LAUNCH(k_rp_normalize, (nhp + NORM_E - 1) / NORM_E, NORM_BS, s, nhp, n, n + 1, 0, d.status, d.hpj, d.hpa,
+               d.hp_be);
+    tl->mark("k_rp_normalize", s, (double)nhp * (2.0 * 8.0 / NORM_E + 9.0));
+    const int nch = (n + HS_CHUNK - 1) / HS_CHUNK;
+    FTS_LAUNCH(k_rp_hsum_chunks, B * nch, 64, s, B, n, d.status, d.hpa, d.scratch);
+    tl->mark("k_rp_hsum_chunks", s, (double)B * (n - nch) * (COST_DBL + COST_MADD));
+    FTS_LAUNCH(k_rp_hsum_join, B, 64, s, B, n, d.status, d.scratch);
+    tl->mark("k_rp_hsum_join", s, (double)B * (nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD));
+    // scratch: [0, B*192) Horner chunks of S, then the 2B lanes' joint tables
+    FTS_LAUNCH(k_rp_com_var, 2 * B, 64, s, B, n, k, d.status, d.pts, d.ch, d.scratch,
+               d.scratch + (size_t)B * HS_SCRATCH, d.terms);
+    tl->mark("k_rp_com_var", s, (double)B * 2 * COST_STRAUS2);
+    FTS_LAUNCH(k_rp_com_sum, B, 64, s, B, n, k, d.status, d.pts, d.terms, d.hpj);
+    tl->mark("k_rp_com_sum", s, (double)B * COM_NTERMS * COST_ADD);
+  }
   FTS_LAUNCH(k_rp_normalize, (B + NORM_E - 1) / NORM_E, NORM_BS, s, B, 1, n + 1, n, d.status, d.hpj, d.hpa, d.hp_be);
   tl->mark("k_rp_normalize_com", s, (double)B * (2.0 * 8.0 / NORM_E + 9.0));
   // side: x0 transcript + hash, then the fixed-base columns (need x0)

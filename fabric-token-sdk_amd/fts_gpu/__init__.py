@@ -108,9 +108,16 @@ class PublicParams:
     """A verification context: parsed public parameters plus their device
     tables (fixed-base windows of every generator) on one MI355X."""
 
-    def __init__(self, raw, bit_length=None, device=0):
+    def __init__(self, raw, bit_length=None, device=0, devices=None):
+        """device: one HIP ordinal (FTS_DEVICE_NONE: host-only); devices: a list of
+        ordinals -> a multi-device context (fts_ctx_create_devices) whose batch calls
+        shard over them and return verdicts in caller order"""
         self._ctx = C.c_void_p()
-        if bit_length:
+        if devices is not None:
+            arr = (C.c_int32 * len(devices))(*devices)
+            rc = L.lib.fts_ctx_create_devices(raw, len(raw), int(bit_length or 0), arr, len(devices),
+                                               C.byref(self._ctx))
+        elif bit_length:
             rc = L.lib.fts_ctx_create_bits(raw, len(raw), int(bit_length), int(device), C.byref(self._ctx))
         else:
             rc = L.lib.fts_ctx_create(raw, len(raw), int(device), C.byref(self._ctx))
@@ -119,6 +126,8 @@ class PublicParams:
         L.check("fts_ctx_info", L.lib.fts_ctx_info(self._ctx, C.byref(info)))
         self.bit_length, self.rounds, self.device = info.bit_length, info.rounds, info.device
         self.max_token, self.table_bytes = info.max_token, info.table_bytes
+        devs = (C.c_int32 * 64)()
+        self.devices = list(devs[:L.lib.fts_ctx_devices(self._ctx, devs, 64)])
 
     def close(self):
         if self._ctx:

@@ -44,7 +44,7 @@ EXPORTED = [
     "fts_request_verify_batch", "fts_request_inspect", "fts_token_open_batch", "fts_rp_prove_batch_gpu",
     "fts_transfer_prove_batch_gpu", "fts_issue_prove_batch_gpu", "fts_token_metadata_open_batch",
     "fts_token_metadata_decode", "fts_ecdsa_verify_batch", "fts_ecdsa_sig_parse", "fts_p256_pubkey_from_pkix",
-    "fts_ecdsa_last_timings",
+    "fts_ecdsa_last_timings", "fts_ctx_create_devices", "fts_ctx_create_mask", "fts_ctx_devices", "fts_shard_plan",
 ]
 
 
@@ -132,6 +132,10 @@ def _load():
         "fts_ecdsa_sig_parse": ([U8P, S, P, P, I32P], C.c_int),
         "fts_p256_pubkey_from_pkix": ([U8P, S, P], C.c_int),
         "fts_ecdsa_last_timings": ([C.c_int, C.POINTER(C.c_float)], C.c_int),
+        "fts_ctx_create_devices": ([U8P, S, C.c_uint32, I32P, C.c_int, C.POINTER(P)], C.c_int),
+        "fts_ctx_create_mask": ([U8P, S, C.c_uint32, C.c_uint64, C.POINTER(P)], C.c_int),
+        "fts_ctx_devices": ([P, I32P, C.c_int], C.c_int),
+        "fts_shard_plan": ([S, C.POINTER(C.c_double), C.c_int, C.POINTER(S)], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -152,6 +156,14 @@ class FtsError(RuntimeError):
 def check(fn, code):
     if code != FTS_API_OK:
         raise FtsError(fn, code)
+
+
+def shard_plan(n, nshards, weights=None):
+    """fts_shard_plan: contiguous shard bounds [b_0 = 0, ..., b_nshards = n]"""
+    b = (C.c_size_t * (nshards + 1))()
+    w = (C.c_double * n)(*weights) if weights is not None else None
+    check("fts_shard_plan", lib.fts_shard_plan(n, w, nshards, b))
+    return list(b)
 
 
 def status_str(s):

@@ -111,6 +111,24 @@ int fts_ctx_create(const uint8_t* pp, size_t pp_len, int device, fts_ctx** out);
 /* Same generators, range proofs truncated to bit_length (Setup(bit_length) semantics,
  * setup.go:388-406: labels do not depend on the bit length). */
 int fts_ctx_create_bits(const uint8_t* pp, size_t pp_len, uint32_t bit_length, int device, fts_ctx** out);
+/* Multi-device context (SURVEY §8b device_mask; the reference verifies every action
+ * independently, core/common/validator.go:215-224): one child context per device (its
+ * own tables, lanes, streams).  Every batch entry point below splits the caller's batch
+ * into contiguous shards balanced by cost (fts_shard_plan: range proofs per action),
+ * runs the shards on their devices concurrently and returns the verdicts in the
+ * caller's order; fts_msm_g1 sums the devices' partial MSM points on the host.
+ * Provers, staged MSMs, timings and debug hooks use the first device.  devices[] may
+ * repeat an ordinal (several shards on one device).  bit_length 0: the PP's own. */
+int fts_ctx_create_devices(const uint8_t* pp, size_t pp_len, uint32_t bit_length, const int32_t* devices, int ndev,
+                           fts_ctx** out);
+/* bit d of device_mask = HIP device d */
+int fts_ctx_create_mask(const uint8_t* pp, size_t pp_len, uint32_t bit_length, uint64_t device_mask, fts_ctx** out);
+/* devices of the context (up to cap written); returns their number (0: host-only) */
+int fts_ctx_devices(const fts_ctx* ctx, int32_t* devices, int cap);
+/* contiguous split of n items into nshards shards of (near) equal total weight
+ * (weights NULL: equal weights): shard j = [bounds[j], bounds[j+1]), bounds[0] = 0,
+ * bounds[nshards] = n.  Host-only; the split every multi-device entry point uses. */
+int fts_shard_plan(size_t n, const double* weights, int nshards, size_t* bounds);
 void fts_ctx_destroy(fts_ctx* ctx);
 int fts_ctx_info(const fts_ctx* ctx, fts_pp_info* out);
 

@@ -49,6 +49,51 @@ def test_golden_batch_verdicts_and_intermediates(gpu_pp, bits):
             assert vals[8:8 + pp.rounds] == c["xj"]
 
 
+_WORK_CTX = {}
+
+
+def _work_path_pp(pp_raw, bits):
+    """a context whose passes all take the work path for com (FTS_COM_FIXED_MAX=0:
+    Horner sum of H'_i + joint GLV/Straus chains); the default contexts run batches
+    of this size on the latency path (fixed-base groups + x*D on the side stream)"""
+    import fts_gpu
+    if bits not in _WORK_CTX:
+        old = {k: os.environ.get(k) for k in ("FTS_COM_FIXED_MAX", "FTS_LANES")}
+        os.environ.update(FTS_COM_FIXED_MAX="0", FTS_LANES="1")
+        try:
+            _WORK_CTX[bits] = fts_gpu.PublicParams(pp_raw, bit_length=bits, device=0)
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+    return _WORK_CTX[bits]
+
+
+@pytest.mark.parametrize("bits", [8, 32, 64])
+def test_golden_work_path_com(pp_raw, bits):
+    """the work path (large passes) computes the same com, H'_i and x0 bytes"""
+    pp = _work_path_pp(pp_raw, bits)
+    cases = [c for c in RP_GOLDEN if c["bits"] == bits]
+    st = pp.verify_range_proofs([bytes.fromhex(c["proof"]) for c in cases],
+                                [bytes.fromhex(c["commitment"]) for c in cases])
+    assert [int(s) for s in st] == [STATUS_OF[c["expect"]] for c in cases]
+    assert "k_rp_com_var" in pp.last_timings() and "k_rp_fixed_all" not in pp.last_timings()
+    for i, c in enumerate(cases):
+        vals, com, hp = _intermediates(pp, i)
+        if "com" in c:
+            assert com.hex() == c["com"] and [h.hex() for h in hp] == c["hprime"] and vals[7] == int(c["x0"])
+
+
+def test_latency_path_is_default_for_small_passes(gpu_pp):
+    pp = gpu_pp(8)
+    cases = [c for c in RP_GOLDEN if c["bits"] == 8]
+    pp.verify_range_proofs([bytes.fromhex(c["proof"]) for c in cases], [bytes.fromhex(c["commitment"]) for c in cases])
+    t = pp.last_timings()
+    assert "k_rp_fixed_all" in t and "k_rp_xd" in t and "k_rp_com_var" not in t
+
+
 def test_host_prover_batch_n64(gpu_pp, oracle_pp):
     """128 fresh proofs from the product prover, all accepted; intermediates
     of a sample match the oracle's reference-order trace."""
