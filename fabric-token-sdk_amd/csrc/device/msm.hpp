@@ -49,15 +49,27 @@ struct MsmWindow {
 
 constexpr int MSM_BITS = 127;  // magnitude < 2^126 + sign-recoding carry
 
+// Grouped MSMs (G > 1): G independent sums over consecutive ranges of ptsg points
+// each (point i belongs to group i / ptsg), sharing one digit / sort / bucket
+// pass: bucket (g, window, digit) = g * NBg + window base + |digit| - 1, and the
+// reduction kernels run per (group, window).  Used by the batch check's group
+// test (one MSM gives every group's partial random linear combination).
+// Optional indirection (sel != nullptr): point i is input point
+// sel[i / sel_pts] * sel_pts + i % sel_pts, or absent (zero) if that entry is -1.
 struct MsmPlan {
-  int N;           // real points
+  int N;           // points (including absent padding points of a grouped plan)
   int NV;          // virtual points (2N)
   int nw;
-  int NB;          // total buckets
-  int NS;          // total segments
+  int NB;          // total buckets (G * NBg)
+  int NS;          // total segments (G * NSg)
   int NC;          // total chunk slots
   int NBLK;        // scan blocks (ceil(NB / MSM_SCAN_ITEMS))
   int WB;          // k_msm_windows blocks per window
+  int G;           // groups (1: one MSM)
+  int ptsg;        // points per group
+  int NBg, NSg;    // buckets / segments per group
+  const int32_t* sel;  // device: proof indirection (grouped fallback), or nullptr
+  int sel_pts;         // points per proof of the indirection
   MsmWindow win[MSM_MAX_WINDOWS];  // host copy
   MsmWindow* d_win;                // device copy
   int32_t* keys;      // [nw][NV] bucket (global) index | sign<<31, or -1
@@ -71,11 +83,13 @@ struct MsmPlan {
   uint32_t* buckets;  // [NB][24] Jacobian
   uint32_t* segs;     // [NS][24]
   uint32_t* wins;     // [nw + 1][24] (slot nw: sum of the extra points)
-  uint32_t* out;      // [24] result (Jacobian)
+  uint32_t* out;      // [G][24] results (Jacobian)
   uint32_t* scratch;  // >= msm_scratch_words(p): scan block sums + window parts
 };
 
-inline size_t msm_scratch_words(const MsmPlan& p) { return (size_t)2 * p.NBLK + 2 + (size_t)(p.nw + 1) * p.WB * 24; }
+inline size_t msm_scratch_words(const MsmPlan& p) {
+  return (size_t)2 * p.NBLK + 2 + (size_t)p.G * (p.nw + 1) * p.WB * 24;
+}
 
 // Field-product count of the bucket phase for window width c (host cost model)
 inline double msm_cost(int N, int c) {
@@ -83,31 +97,37 @@ inline double msm_cost(int N, int c) {
   return (double)nw * ((double)N * 11.0 + (double)(1 << c) * 16.0);
 }
 
-inline void msm_layout(int N, MsmPlan& p) {
-  const int NV = 2 * N;
+// G groups of ptsg points (N = G * ptsg, or fewer in the last group); the window
+// width minimises the per-group bucket cost
+inline void msm_layout_groups(int N, int G, int ptsg, MsmPlan& p) {
+  const int NV = 2 * N, NVg = 2 * ptsg;
   int best = 4;
   for (int c = 5; c <= 16; c++)
-    if (msm_cost(NV, c) < msm_cost(NV, best)) best = c;
+    if (msm_cost(NVg, c) < msm_cost(NVg, best)) best = c;
   const int c = best;
   const int nw = (MSM_BITS + c - 1) / c;
   // balanced widths: (MSM_BITS mod nw) windows of ceil, the rest floor
   const int lo = MSM_BITS / nw, extra = MSM_BITS - lo * nw;
   p.nw = nw;
-  int off = 0, bb = 0, sb = 0, cb = 0;
+  int off = 0, bb = 0, sb = 0;
   for (int w = 0; w < nw; w++) {
     const int width = lo + (w < extra ? 1 : 0);
     const int nb = 1 << (width - 1);
     const int ns = (nb + MSM_SEG - 1) / MSM_SEG;
-    p.win[w] = MsmWindow{width, off, bb, sb, cb, {0, 0, 0}};
+    p.win[w] = MsmWindow{width, off, bb, sb, 0, {0, 0, 0}};
     off += width;
     bb += nb;
     sb += ns;
-    cb += NV / MSM_CH + nb;
   }
-  p.NB = bb;
-  p.NS = sb;
-  p.NC = cb;
-  p.NBLK = (bb + MSM_SCAN_ITEMS - 1) / MSM_SCAN_ITEMS;
+  p.G = G;
+  p.ptsg = ptsg;
+  p.NBg = bb;
+  p.NSg = sb;
+  p.NB = G * bb;
+  p.NS = G * sb;
+  // chunk slots: sum over buckets of ceil(count / MSM_CH) <= entries / MSM_CH + buckets
+  p.NC = nw * (NV / MSM_CH + 1) + p.NB;
+  p.NBLK = (p.NB + MSM_SCAN_ITEMS - 1) / MSM_SCAN_ITEMS;
   int maxs = 0;
   for (int w = 0; w < nw; w++) {
     const int ns = ((1 << (p.win[w].width - 1)) + MSM_SEG - 1) / MSM_SEG;
@@ -117,6 +137,9 @@ inline void msm_layout(int N, MsmPlan& p) {
   if (p.WB < 1) p.WB = 1;
   p.N = N;
   p.NV = NV;
+  p.sel = nullptr;
+  p.sel_pts = 1;
 }
+inline void msm_layout(int N, MsmPlan& p) { msm_layout_groups(N, 1, N > 0 ? N : 1, p); }
 
 }  // namespace fts

@@ -73,8 +73,12 @@ constexpr double COST_NORM = 7.0;
 // after each kernel; the time of mark i is elapsed(previous event on the same
 // stream, mark i).  fork()/join() record the cross-stream dependencies (their
 // events start the next kernel's interval on the waiting stream).
+// Marks made after fallback() (the batch check's group test and per-proof
+// checks) are reported under "fb:" names, apart from the main pass's kernels.
+const char* fallback_name(const char* nm);
 struct Timeline {
-  static constexpr int CAP = 48;
+  static constexpr int CAP = 96;
+  bool in_fallback = false;
   static constexpr int MAXS = 4;
   hipEvent_t ev[CAP + 1];
   const char* name[CAP];
@@ -102,16 +106,18 @@ struct Timeline {
     last[ns] = 0;
     return last[ns++];
   }
+  void fallback() { in_fallback = true; }
   void begin(hipStream_t s) {
     n = 0;
     ns = 0;
+    in_fallback = false;
     (void)hipEventRecord(ev[0], s);
     last_of(s) = 0;
   }
   void mark(const char* nm, hipStream_t s, double w) {
     if (n >= CAP) return;
     int& l = last_of(s);
-    name[n] = nm;
+    name[n] = nm && in_fallback ? fallback_name(nm) : nm;
     work[n] = w;
     start[n] = l;
     (void)hipEventRecord(ev[n + 1], s);
@@ -164,6 +170,8 @@ struct RpBatchDev {
   uint32_t* ypow;      // [n][B][8] y^-i (Montgomery Fr), i-major (coalesced over proofs)
   uint32_t* svec;      // [n][B][8] s_i = prod_j x_j^(+-1) (ipa.go:343-356 unrolled), i-major
   uint32_t* zvec;      // [n][B][8] z^2 2^i y^-i (latency path only), i-major
+  void (*pre_rlc)(void* arg, hipStream_t s);  // optional hook launched on s before the batch check
+  void* pre_rlc_arg;
   int com_fixed;       // 1: com by fixed-base groups + x*D on the side stream (latency path,
                        //    small passes); 0: Horner sum + joint GLV/Straus chains (work path)
 };

@@ -49,6 +49,7 @@ inline __host__ __device__ int sig_naff(int kind, int n_in, int n_out) {
 struct SigBatchDev {
   int A;              // #actions
   int npts;           // total points
+  int naff;           // total per-action affine / Jacobian slots (aff_off of the end)
   int nwork;          // total (action, term) work items
   const SigAction* act;
   uint8_t* raw;       // [npts][64] raw BE

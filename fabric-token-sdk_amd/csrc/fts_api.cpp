@@ -43,7 +43,11 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
 void launch_build_wide_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s);
 size_t wide_build_scratch_bytes(int nb);
 size_t fbw_words_per_base();
-void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, hipStream_t s, Timeline* tl);
+void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, const int32_t* sel, int nsel, hipStream_t s,
+                        Timeline* tl);
+void launch_rlc_group_test(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const MsmPlan& p,
+                           const int32_t* sel, int G, int gs, uint32_t* gcol, uint32_t* gfix, int32_t* next,
+                           uint32_t* next_count, hipStream_t s, Timeline* tl);
 void launch_rp_gather(const RpGather& g, int k, uint8_t* raw, uint32_t* sc, int32_t* status, int32_t* ipa, hipStream_t s);
 void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
                 uint32_t* scratch, hipStream_t s, hipStream_t s_extra, Timeline* tl);
@@ -52,6 +56,7 @@ void launch_msm_load(int N, const uint8_t* raw_pts, const uint8_t* raw_sc, uint3
 void launch_msm_to_bytes(const uint32_t* jac, uint8_t* out, hipStream_t s);
 void launch_sig_prep(const SigBatchDev& d, hipStream_t s);
 void launch_sig_finish(const SigBatchDev& d, const uint32_t* tables, int n, hipStream_t s);
+void launch_sig_exclude(const SigBatchDev& d, int32_t* rp_status, hipStream_t s);
 size_t table_build_scratch_bytes(int nb);
 size_t fb_words_per_base();
 // prove_kernels.hip
@@ -61,6 +66,20 @@ void launch_sigma_prove(const SpDev& d, hipStream_t s);
 // audit_kernels.hip
 void launch_open_check(int n, const uint8_t* raw, const uint32_t* sc, const uint32_t* tables, int nb,
                        int32_t* status, hipStream_t s);
+}  // namespace fts
+
+namespace fts {
+// "fb:" + nm, interned (Timeline marks after fallback())
+const char* fallback_name(const char* nm) {
+  static std::mutex mu;
+  static std::deque<std::string> names;  // stable storage (deque never moves elements)
+  std::lock_guard<std::mutex> g(mu);
+  const std::string want = std::string("fb:") + nm;
+  for (const std::string& x : names)
+    if (x == want) return x.c_str();
+  names.push_back(want);
+  return names.back().c_str();
+}
 }  // namespace fts
 
 using namespace fts;
@@ -108,7 +127,7 @@ struct DBuf {
 struct Workspace {
   DBuf pts, ch, small, hpj, hpa, hpbe, x0, terms, scratch, ypow, svec, zvec;
   // random-linear-combination check + MSM
-  DBuf r_key, r_msc, r_coef, r_colsum, r_fixed, r_flag, m_keys, m_counts, m_offsets, m_cursor, m_sorted, m_buckets,
+  DBuf r_key, r_msc, r_coef, r_colsum, r_fixed, r_flag, r_gcol, r_gfix, r_sel, r_next, r_cnt, m_keys, m_counts, m_offsets, m_cursor, m_sorted, m_buckets,
       m_segs, m_wins, m_out, m_scratch, m_win, m_choff, m_chbkt, m_partials;
   // action (transfer / issue) batches
   DBuf rp_raw, rp_sc, rp_status, rp_ipa;
@@ -119,7 +138,8 @@ struct Workspace {
   void release() {
     for (DBuf* b : {&open_rec, &pv, &sp, &pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &terms, &scratch, &ypow, &svec, &zvec, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
                     &rp_status, &rp_ipa, &s_act, &s_raw, &s_owner, &s_pts, &s_sc, &s_status, &s_work, &s_terms, &s_aff,
-                    &s_affoff, &s_msgs, &s_jac, &s_scratch, &r_key, &r_msc, &r_coef, &r_colsum, &r_fixed, &r_flag,
+                    &s_affoff, &s_msgs, &s_jac, &s_scratch, &r_key, &r_msc, &r_coef, &r_colsum, &r_fixed, &r_flag, &r_gcol, &r_gfix,
+                    &r_sel, &r_next, &r_cnt,
                     &m_keys, &m_counts, &m_offsets, &m_cursor, &m_sorted, &m_buckets, &m_segs, &m_wins, &m_out,
                     &m_scratch, &m_win})
       b->release();
@@ -147,6 +167,8 @@ struct Lane {
   }
   bool presized = false;  // workspace sized for the context's largest coalesced pass
   hipStream_t s = nullptr, s2 = nullptr;
+  hipStream_t s3 = nullptr;         // sigma proofs of action batches (beside the range-proof pass)
+  hipEvent_t ev_a = nullptr, ev_b = nullptr;  // cross-stream ordering (no timing)
   Workspace ws;
   Timeline tl;
   float host_prep_ms = 0, host_enqueue_ms = 0, host_wait_ms = 0;  // host wall time of the last run
@@ -393,6 +415,9 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   c->device = device;
   auto fail = [&](int code) {
     for (Lane* L : c->lanes) {
+      if (L->s3) hipStreamDestroy(L->s3);
+      if (L->ev_a) hipEventDestroy(L->ev_a);
+      if (L->ev_b) hipEventDestroy(L->ev_b);
       if (L->s2 && L->s2 != L->s) hipStreamDestroy(L->s2);
       if (L->s) hipStreamDestroy(L->s);
       L->tl.destroy();
@@ -426,6 +451,10 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
     if (hipHostMalloc((void**)&L->pin, sizeof(Lane::Pinned), 0) != hipSuccess) return fail(FTS_API_ENOMEM);
     if (!side) L->s2 = L->s;
     else if (hipStreamCreateWithFlags(&L->s2, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
+    if (hipStreamCreateWithFlags(&L->s3, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&L->ev_a, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&L->ev_b, hipEventDisableTiming) != hipSuccess)
+      return fail(FTS_API_EDEVICE);
     L->tl.create();
   }
   hipStream_t s0 = c->lanes[0]->s;
@@ -654,7 +683,11 @@ void fts_ctx_destroy(fts_ctx* c) {
   for (Lane* L : c->lanes) {
     if (L->s) hipStreamSynchronize(L->s);
     if (L->s2 && L->s2 != L->s) hipStreamSynchronize(L->s2);
+    if (L->s3) hipStreamSynchronize(L->s3);
     L->ws.release();
+    if (L->s3) hipStreamDestroy(L->s3);
+    if (L->ev_a) hipEventDestroy(L->ev_a);
+    if (L->ev_b) hipEventDestroy(L->ev_b);
     L->tl.destroy();
     if (L->done) hipEventDestroy(L->done);
     if (L->s2 && L->s2 != L->s) hipStreamDestroy(L->s2);
@@ -792,16 +825,21 @@ static void collect_timings(fts_ctx* c, Lane& L, fts_rp_batch* b) {
 
 // MSM plan for N real points on lane L's workspace (buffers grown as needed,
 // window table uploaded on L.s).  Returns 0 or FTS_API_ENOMEM.
+static int msm_prepare_plan(Lane& L, MsmPlan& mp);
 static int msm_prepare(Lane& L, int N, MsmPlan& mp) {
-  Workspace& w = L.ws;
   mp = MsmPlan{};
   msm_layout(N, mp);
+  return msm_prepare_plan(L, mp);
+}
+// buffers of an already laid-out plan (msm_layout / msm_layout_groups) on lane L
+static int msm_prepare_plan(Lane& L, MsmPlan& mp) {
+  Workspace& w = L.ws;
   if (w.m_choff.ensure((size_t)mp.NB * 4) || w.m_chbkt.ensure((size_t)mp.NC * 4) ||
       w.m_partials.ensure((size_t)mp.NC * 96) || w.m_keys.ensure((size_t)mp.nw * mp.NV * 4) ||
       w.m_counts.ensure((size_t)mp.NB * 4) || w.m_offsets.ensure((size_t)mp.NB * 4) ||
       w.m_cursor.ensure((size_t)mp.nw * mp.NV * 4) || w.m_sorted.ensure((size_t)mp.nw * mp.NV * 4) ||
       w.m_buckets.ensure((size_t)mp.NB * 96) || w.m_segs.ensure((size_t)mp.NS * 96) ||
-      w.m_wins.ensure((size_t)(mp.nw + 1) * 96) || w.m_out.ensure(96) ||
+      w.m_wins.ensure((size_t)(mp.nw + 1) * 96) || w.m_out.ensure((size_t)mp.G * 96) ||
       w.m_scratch.ensure(std::max((size_t)mp.NS * 96, msm_scratch_words(mp) * 4)) || w.m_win.ensure(sizeof(mp.win)))
     return FTS_API_ENOMEM;
   mp.d_win = w.m_win.as<MsmWindow>();
@@ -859,13 +897,82 @@ static int lane_reserve(fts_ctx* c, Lane& L, int B, bool inputs) {
   return FTS_API_OK;
 }
 
+// The batch check failed: find the failing proofs without re-checking the whole
+// pass proof by proof ("fall back to per-proof checks
+// (bisection)").  Round 1 tests groups of RP_GT1 consecutive proofs that never
+// straddle two caller batches (`groups`: the batches' first proofs, the pass's
+// end last); if more than RP_GT2_MIN proofs sit in failing groups, round 2 tests
+// groups of RP_GT2 among them.  Every group test is ONE grouped MSM over the
+// batch check's own weights.  The proofs of groups that do not close get the
+// per-proof final equations (bulletproof.go:314-324, ipa.go:254-259), whose
+// verdicts are the reference's.  A single bad proof costs one grouped MSM plus
+// RP_GT1 per-proof checks, all of them in its own caller batch.
+constexpr int RP_GT1 = 64, RP_GT2 = 8, RP_GT2_MIN = 2048;
+static int rp_group_fallback(fts_ctx* c, Lane& L, const RpBatchDev& d, const RlcDev& r,
+                             const std::vector<int>& groups) {
+  const int B = d.B, n = d.n, npts = rp_npts(d.k);
+  Workspace& w = L.ws;
+  L.tl.fallback();
+  // round-1 selection: each batch cut into groups of RP_GT1, -1 padded
+  std::vector<int32_t> sel;
+  for (size_t q = 0; q + 1 < groups.size(); q++)
+    for (int lo = groups[q]; lo < groups[q + 1]; lo += RP_GT1)
+      for (int j = 0; j < RP_GT1; j++) sel.push_back(lo + j < groups[q + 1] ? lo + j : -1);
+  const size_t slots = std::max<size_t>(sel.size(), (size_t)B + RP_GT2);
+  // groups of either round: round 1 has sel.size() / RP_GT1, round 2 at most slots / RP_GT2
+  const size_t gmax = std::max(sel.size() / RP_GT1, (slots + RP_GT2 - 1) / RP_GT2);
+  if (w.r_sel.ensure(slots * 4) || w.r_next.ensure(slots * 4) || w.r_cnt.ensure(8) ||
+      w.r_gcol.ensure(gmax * (3 + 2 * n) * 32) || w.r_gfix.ensure(gmax * (3 + 2 * n) * 96))
+    return FTS_API_ENOMEM;
+  uint8_t* hs = L.stage_buf(sel.size() * 4);
+  if (!hs) return FTS_API_ENOMEM;
+  memcpy(hs, sel.data(), sel.size() * 4);
+  HIP_OK(hipMemcpyAsync(w.r_sel.p, hs, sel.size() * 4, hipMemcpyHostToDevice, L.s));
+  int32_t* cur = w.r_sel.as<int32_t>();
+  int32_t* nxt = w.r_next.as<int32_t>();
+  uint32_t* cnt = w.r_cnt.as<uint32_t>();
+  int G = (int)(sel.size() / RP_GT1), gs = RP_GT1;
+  for (int round = 0; round < 2; round++) {
+    MsmPlan gp{};
+    msm_layout_groups(G * gs * npts, G, gs * npts, gp);
+    gp.sel = cur;
+    gp.sel_pts = npts;
+    if (int rc = msm_prepare_plan(L, gp)) return rc;
+    HIP_OK(hipMemsetAsync(nxt, 0xff, slots * 4, L.s));  // -1: empty slots of the next round
+    HIP_OK(hipMemsetAsync(cnt, 0, 4, L.s));
+    launch_rlc_group_test(d, r, c->d_tables, gp, cur, G, gs, w.r_gcol.as<uint32_t>(), w.r_gfix.as<uint32_t>(), nxt,
+                          cnt, L.s, &L.tl);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(&L.pin->flag, cnt, 4, hipMemcpyDeviceToHost, L.s));
+    HIP_OK(L.sync());
+    const int nfail = L.pin->flag;
+    if (nfail == 0) return FTS_API_OK;
+    std::swap(cur, nxt);
+    // per-proof checks of what is left; a second group test only pays when round 1
+    // left many proofs (the per-proof check's latency is one GLV chain whatever
+    // their number, its work grows with it)
+    if (round == 1 || nfail <= RP_GT2_MIN) {
+      launch_rp_fallback(d, c->d_tables, cur, nfail, L.s, &L.tl);
+      HIP_OK(hipGetLastError());
+      return FTS_API_OK;
+    }
+    gs = RP_GT2;
+    G = (nfail + RP_GT2 - 1) / RP_GT2;
+    if ((size_t)G > gmax) return FTS_API_EINVAL;  // cannot happen: nfail <= B
+  }
+  return FTS_API_OK;
+}
+
 // Range-proof pipeline on B proofs already on the device: exact phase, RLC
-// batch check, and the per-proof fallback when the combination fails.
+// batch check, and the group-test fallback when the combination fails.
 // `between` (optional) is launched after the RLC check and before the flag
 // sync (the sigma-proof kernels of transfer/issue batches).
+// `groups`: first proof of every caller batch in the pass, then B ({0, B}: one batch)
+// `pre_rlc` (optional): launched on the main stream right before the batch check
 template <class F>
 static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc, int32_t* d_status, int32_t* d_ipa,
-                       F&& between) {
+                       F&& between, const std::vector<int>& groups, void (*pre_rlc)(void*, hipStream_t) = nullptr,
+                       void* pre_rlc_arg = nullptr) {
   const int n = c->n, k = c->k, npts = rp_npts(k);
   Workspace& w = L.ws;
   const int N = B * npts;
@@ -896,7 +1003,11 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
                w.ypow.as<uint32_t>(),
                w.svec.as<uint32_t>(),
                w.zvec.as<uint32_t>(),
+               nullptr,
+               nullptr,
                (size_t)B <= c->com_fixed_max ? 1 : 0};
+  d.pre_rlc = pre_rlc;
+  d.pre_rlc_arg = pre_rlc_arg;
   RlcDev r{w.r_key.as<uint32_t>(), w.r_msc.as<uint32_t>(),   w.r_coef.as<uint32_t>(), w.r_colsum.as<uint32_t>(),
            w.r_fixed.as<uint32_t>(), w.r_flag.as<int32_t>(), w.m_scratch.as<uint32_t>(), mp};
   // fresh RLC weights key (getrandom), unpredictable to the provers
@@ -916,16 +1027,13 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   L.host_wait_ms = (float)(t_wait - t_enq);
   const int32_t flag = L.pin->flag;
   c->last_fallback = flag ? 0 : 1;
-  if (!flag) {
-    launch_rp_fallback(d, c->d_tables, L.s, &L.tl);
-    HIP_OK(hipGetLastError());
-  }
+  if (!flag) return rp_group_fallback(c, L, d, r, groups);
   return FTS_API_OK;
 }
 
 static int run_rp(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc, int32_t* d_status, int32_t* d_ipa,
                   int32_t* host_status, fts_rp_batch* batch) {
-  int rc = rp_pipeline(c, L, B, d_raw, d_sc, d_status, d_ipa, [] {});
+  int rc = rp_pipeline(c, L, B, d_raw, d_sc, d_status, d_ipa, [] {}, std::vector<int>{0, B});
   if (rc != FTS_API_OK) return rc;
   int32_t* pst = host_status ? L.status_buf((size_t)B) : nullptr;
   if (host_status && !pst) return FTS_API_ENOMEM;
@@ -969,8 +1077,9 @@ static int run_rp_group(fts_ctx* c, Lane& L, const std::vector<RpReq*>& grp) {
   g.off[g.G] = (int)off;
   launch_rp_gather(g, c->k, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
                    w.rp_ipa.as<int32_t>(), L.s);
+  std::vector<int> bounds(g.off, g.off + g.G + 1);
   int rc = rp_pipeline(c, L, (int)B, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
-                       w.rp_ipa.as<int32_t>(), [] {});
+                       w.rp_ipa.as<int32_t>(), [] {}, bounds);
   if (rc != FTS_API_OK) return rc;
   int32_t* pst = L.status_buf(B);
   if (!pst) return FTS_API_ENOMEM;
@@ -1669,19 +1778,36 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
     sd.scratch = w.s_scratch.as<uint32_t>();
     sd.rp_raw = rp_total ? w.rp_raw.as<uint8_t>() : nullptr;
     sd.rp_k = k;
+    sd.naff = aff_off;
     launch_sig_prep(sd, L.s);
     L.host_stage_ms = (float)(now_ms() - t_parse1);
   }
-  auto sig_finish = [&]() {
-    if (SA) launch_sig_finish(sd, c->d_tables, n, L.s);
-    if (SA && rp_total) L.tl.mark("k_sig_finish", L.s, 0);
-  };
   if (rp_total) {
+    // the sigma proofs run on the lane's third stream beside the range-proof pass;
+    // right before the batch check the main stream joins them and drops the range
+    // proofs of actions whose sigma proof failed from the check (k_sig_exclude)
+    struct Hook {
+      const SigBatchDev* sd;
+      Lane* L;
+      int32_t* rp_status;
+    } hook{&sd, &L, w.rp_status.as<int32_t>()};
+    void (*pre)(void*, hipStream_t) = nullptr;
+    if (SA) {
+      HIP_OK(hipEventRecord(L.ev_a, L.s));
+      HIP_OK(hipStreamWaitEvent(L.s3, L.ev_a, 0));
+      launch_sig_finish(sd, c->d_tables, n, L.s3);
+      HIP_OK(hipEventRecord(L.ev_b, L.s3));
+      pre = [](void* arg, hipStream_t s) {
+        Hook* h = static_cast<Hook*>(arg);
+        (void)hipStreamWaitEvent(s, h->L->ev_b, 0);
+        launch_sig_exclude(*h->sd, h->rp_status, s);
+      };
+    }
     int rc = rp_pipeline(c, L, rp_total, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
-                         w.rp_ipa.as<int32_t>(), sig_finish);
+                         w.rp_ipa.as<int32_t>(), [] {}, std::vector<int>{0, rp_total}, pre, &hook);
     if (rc != FTS_API_OK) return rc;
-  } else {
-    sig_finish();
+  } else if (SA) {
+    launch_sig_finish(sd, c->d_tables, n, L.s);
   }
   HIP_OK(hipGetLastError());
   std::vector<int32_t> sig_res(SA), rp_res(rp_total);

@@ -27,16 +27,33 @@ FTS_DEV uint32_t scalar_bits4(const uint32_t s[4], int off, int width) {
   return (uint32_t)(v & ((1ull << width) - 1));
 }
 
+// the point-indexing part of a plan, passed to the kernels by value
+struct MsmIdx {
+  int N, nw, ptsg, NBg, sel_pts;
+  const int32_t* sel;
+};
+inline MsmIdx msm_idx(const MsmPlan& p) { return MsmIdx{p.N, p.nw, p.ptsg, p.NBg, p.sel_pts, p.sel}; }
+// input index of plan point i (-1: absent padding point of a grouped plan)
+FTS_DEV long msm_src(const MsmIdx& p, int i) {
+  if (!p.sel) return i;
+  const int q = p.sel[i / p.sel_pts];
+  return q < 0 ? -1L : (long)q * p.sel_pts + i % p.sel_pts;
+}
+
 // lane per real point i: GLV split, then the signed digits of both halves
-// (virtual points i and N + i) for every window
-__global__ void __launch_bounds__(256) k_msm_digits(int N, int nw, const MsmWindow* __restrict__ win,
+// (virtual points i and N + i) for every window; group g = i / ptsg owns the
+// buckets [g NBg, (g + 1) NBg)
+__global__ void __launch_bounds__(256) k_msm_digits(MsmIdx p, const MsmWindow* __restrict__ win,
                                                     const uint32_t* __restrict__ scalars, int32_t* __restrict__ keys,
                                                     uint32_t* __restrict__ ranks, uint32_t* __restrict__ counts) {
+  const int N = p.N, nw = p.nw;
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
+  const long src = msm_src(p, i);
+  const int gb = (i / p.ptsg) * p.NBg;
   uint32_t s[8];
 #pragma unroll
-  for (int q = 0; q < 8; q++) s[q] = scalars[(size_t)i * 8 + q];
+  for (int q = 0; q < 8; q++) s[q] = src < 0 ? 0u : scalars[(size_t)src * 8 + q];
   uint32_t k[2][4], sg[2];
   glv_decompose(s, k[0], sg[0], k[1], sg[1]);
   const int NV = 2 * N;
@@ -51,7 +68,7 @@ __global__ void __launch_bounds__(256) k_msm_digits(int N, int nw, const MsmWind
       d = carry ? d - (1 << W.width) : d;
       int key = -1;
       if (d != 0) {
-        int b = W.bbase + (d < 0 ? -d : d) - 1;
+        int b = gb + W.bbase + (d < 0 ? -d : d) - 1;
         key = ((d < 0) != (sg[h] != 0)) ? (b | (int)0x80000000) : b;
         ranks[(size_t)w * NV + h * N + i] = atomicAdd(&counts[b], 1u);  // rank within the bucket
       }
@@ -175,7 +192,7 @@ __global__ void __launch_bounds__(256) k_msm_scatter(int NV, int nw, const int32
 
 // one lane per chunk slot: <= MSM_CH mixed additions of sorted virtual points
 // (index >= N: phi(P_{index-N}) = (beta x, y))
-__global__ void __launch_bounds__(64, 4) k_msm_chunks(int N, int nw, const uint32_t* __restrict__ nc_total,
+__global__ void __launch_bounds__(64, 4) k_msm_chunks(MsmIdx p, const uint32_t* __restrict__ nc_total,
                                                    const MsmWindow* __restrict__ win,
                                                    const uint32_t* __restrict__ points,
                                                    const uint32_t* __restrict__ offsets,
@@ -183,6 +200,7 @@ __global__ void __launch_bounds__(64, 4) k_msm_chunks(int N, int nw, const uint3
                                                    const uint32_t* __restrict__ chunk_off,
                                                    const int32_t* __restrict__ chunk_bkt,
                                                    const uint32_t* __restrict__ sorted, uint32_t* __restrict__ partials) {
+  const int N = p.N;
   int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= (int)*nc_total) return;
   const int b = chunk_bkt[g];
@@ -192,15 +210,17 @@ __global__ void __launch_bounds__(64, 4) k_msm_chunks(int N, int nw, const uint3
   const Fp beta = glv_beta();
   G1J acc = g1j_identity();
   // the next entry's point is gathered while the current addition runs
+  // (absent points never get a bucket entry, so msm_src is >= 0 here)
   uint32_t e = S[lo];
-  G1A q = load_g1a(points + (size_t)((e & 0x7fffffffu) >= (uint32_t)N ? (e & 0x7fffffffu) - N : (e & 0x7fffffffu)) * 16);
+  G1A q = load_g1a(points + (size_t)msm_src(p, (int)((e & 0x7fffffffu) >= (uint32_t)N ? (e & 0x7fffffffu) - N
+                                                                                      : (e & 0x7fffffffu))) * 16);
   for (uint32_t t = lo; t < hi; t++) {
     uint32_t en = 0;
     G1A qn;
     if (t + 1 < hi) {
       en = S[t + 1];
       const uint32_t vn = en & 0x7fffffffu;
-      qn = load_g1a(points + (size_t)(vn >= (uint32_t)N ? vn - N : vn) * 16);
+      qn = load_g1a(points + (size_t)msm_src(p, (int)(vn >= (uint32_t)N ? vn - N : vn)) * 16);
     }
     if (!g1a_is_identity(q)) {
       if ((e & 0x7fffffffu) >= (uint32_t)N) q.x = fp_mul(q.x, beta);
@@ -227,20 +247,21 @@ __global__ void __launch_bounds__(64) k_msm_bucket_sum(int NB, const uint32_t* _
   store_g1j(buckets + (size_t)b * 24, acc);
 }
 
-// running-sum reduction of MSM_SEG consecutive buckets of one window:
+// running-sum reduction of MSM_SEG consecutive buckets of one (group, window):
 // sum_j (j+1) B_j for the window-local bucket indices j of the segment
-__global__ void __launch_bounds__(64) k_msm_segments(int nw, int NS, const MsmWindow* __restrict__ win,
+__global__ void __launch_bounds__(64) k_msm_segments(int nw, int NS, int NSg, int NBg, const MsmWindow* __restrict__ win,
                                                      const uint32_t* __restrict__ buckets,
                                                      uint32_t* __restrict__ segs, uint32_t* __restrict__ scratch) {
   int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= NS) return;
+  const int grp = g / NSg, gl = g % NSg;
   int w = 0;
-  while (w + 1 < nw && win[w + 1].sbase <= g) w++;
+  while (w + 1 < nw && win[w + 1].sbase <= gl) w++;
   const MsmWindow W = win[w];
   const int nb = 1 << (W.width - 1);
-  const int s = g - W.sbase;
+  const int s = gl - W.sbase;
   const int lo = s * MSM_SEG, cnt = (nb - lo) < MSM_SEG ? (nb - lo) : MSM_SEG;
-  const uint32_t* Bk = buckets + ((size_t)W.bbase + lo) * 24;
+  const uint32_t* Bk = buckets + ((size_t)grp * NBg + W.bbase + lo) * 24;
   G1J sum = g1j_identity(), acc = g1j_identity();
   for (int j = cnt - 1; j >= 0; j--) {
     add_inl(sum, load_g1j(Bk + j * 24));
@@ -259,22 +280,22 @@ __global__ void __launch_bounds__(64) k_msm_segments(int nw, int NS, const MsmWi
 }
 
 // LDS tree (block of 256 lanes) over <= MSM_WIN_ITEMS consecutive segments:
-// block (w, j) with w < nw sums part j of window w's segments; w = nw sums
-// part j of the nextra extra Jacobian points (the fixed-base part)
-__global__ void __launch_bounds__(256) k_msm_windows(int nw, int WB, const MsmWindow* __restrict__ win,
+// block (w, j, group) with w < nw sums part j of the group's window-w segments;
+// w = nw sums part j of the group's nextra extra Jacobian points (the fixed-base part)
+__global__ void __launch_bounds__(256) k_msm_windows(int nw, int WB, int NSg, const MsmWindow* __restrict__ win,
                                                      const uint32_t* __restrict__ segs, const uint32_t* __restrict__ extra,
                                                      int nextra, uint32_t* __restrict__ parts) {
   __shared__ uint32_t sh[256 * 24];
-  const int t = threadIdx.x, w = blockIdx.x, j = blockIdx.y;
+  const int t = threadIdx.x, w = blockIdx.x, j = blockIdx.y, grp = blockIdx.z;
   const uint32_t* S;
   int cnt;
   if (w < nw) {
     const MsmWindow W = win[w];
     cnt = ((1 << (W.width - 1)) + MSM_SEG - 1) / MSM_SEG;
-    S = segs + (size_t)W.sbase * 24;
+    S = segs + ((size_t)grp * NSg + W.sbase) * 24;
   } else {
-    cnt = nextra;
-    S = extra;
+    cnt = extra ? nextra : 0;
+    S = extra + (size_t)grp * nextra * 24;
   }
   const int lo = j * MSM_WIN_ITEMS, hi = min(cnt, lo + MSM_WIN_ITEMS);
   G1J acc = g1j_identity();
@@ -287,7 +308,7 @@ __global__ void __launch_bounds__(256) k_msm_windows(int nw, int WB, const MsmWi
     if (t < half) store_g1j(sh + t * 24, acc);
     __syncthreads();
   }
-  if (t == 0) store_g1j(parts + ((size_t)w * WB + j) * 24, acc);
+  if (t == 0) store_g1j(parts + (((size_t)grp * (nw + 1) + w) * WB + j) * 24, acc);
 }
 
 // lane w <= nw: W_w = sum of window w's parts, shifted to its bit offset
@@ -295,10 +316,11 @@ __global__ void __launch_bounds__(256) k_msm_windows(int nw, int WB, const MsmWi
 // is the top window's ~off_top doublings instead of one 127-doubling Horner
 // chain), lane nw: the extra points; then an LDS tree over the lanes
 __global__ void __launch_bounds__(64) k_msm_final(int nw, int WB, const MsmWindow* __restrict__ win,
-                                                  const uint32_t* __restrict__ parts, uint32_t* __restrict__ wins,
-                                                  uint32_t* __restrict__ out) {
+                                                  const uint32_t* __restrict__ parts_all, uint32_t* __restrict__ out_all) {
   __shared__ uint32_t sh[64 * 24];
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, grp = blockIdx.x;  // one block per group
+  const uint32_t* parts = parts_all + (size_t)grp * (nw + 1) * WB * 24;
+  uint32_t* out = out_all + (size_t)grp * 24;
   G1J acc = g1j_identity();
   for (int w = t; w <= nw; w += 64) {
     G1J W = load_g1j(parts + (size_t)w * WB * 24);
@@ -367,7 +389,7 @@ __global__ void k_msm_to_bytes(const uint32_t* __restrict__ jac, uint8_t* __rest
 void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
                 uint32_t* scratch, hipStream_t s, hipStream_t s_extra, Timeline* tl) {
   (void)hipMemsetAsync(p.counts, 0, (size_t)p.NB * 4, s);
-  FTS_LAUNCH(k_msm_digits, p.N, 256, s, p.N, p.nw, p.d_win, scalars, p.keys, p.cursor, p.counts);
+  FTS_LAUNCH(k_msm_digits, p.N, 256, s, msm_idx(p), p.d_win, scalars, p.keys, p.cursor, p.counts);
   tl->mark("k_msm_digits", s, 0);
   FTS_LAUNCH(k_msm_scan1, (size_t)p.NBLK * 256, 256, s, p.NB, p.counts, p.offsets, p.chunk_off, p.scratch);
   hipLaunchKernelGGL(k_msm_scan2, dim3(1), dim3(256), 0, s, p.NBLK, p.scratch);
@@ -375,25 +397,25 @@ void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalar
   tl->mark("k_msm_scan", s, 0);
   FTS_LAUNCH(k_msm_scatter, p.NV, 256, s, p.NV, p.nw, p.keys, p.cursor, p.offsets, p.sorted);
   tl->mark("k_msm_scatter", s, 0);
-  FTS_LAUNCH(k_msm_chunks, p.NC, 64, s, p.N, p.nw, p.scratch + 2 * (size_t)p.NBLK + 1, p.d_win, points, p.offsets,
+  FTS_LAUNCH(k_msm_chunks, p.NC, 64, s, msm_idx(p), p.scratch + 2 * (size_t)p.NBLK + 1, p.d_win, points, p.offsets,
              p.counts, p.chunk_off,
              p.chunk_bkt, p.sorted, p.partials);
   // expected nonzero digits: N * nw * (1 - 2^-c) ~ N * nw mixed additions
   tl->mark("k_msm_chunks", s, (double)p.NV * p.nw * (COST_MADD + 0.5));
   FTS_LAUNCH(k_msm_bucket_sum, p.NB, 64, s, p.NB, p.counts, p.chunk_off, p.partials, p.buckets);
   tl->mark("k_msm_bucket_sum", s, 0);
-  FTS_LAUNCH(k_msm_segments, p.NS, 64, s, p.nw, p.NS, p.d_win, p.buckets, p.segs, scratch);
+  FTS_LAUNCH(k_msm_segments, p.NS, 64, s, p.nw, p.NS, p.NSg, p.NBg, p.d_win, p.buckets, p.segs, scratch);
   tl->mark("k_msm_segments", s, (double)p.NB * 2 * COST_ADD);
   if (s_extra != s) tl->fork(s_extra, s);
   uint32_t* parts = p.scratch + 2 * (size_t)p.NBLK + 2;
-  hipLaunchKernelGGL(k_msm_windows, dim3(p.nw + 1, p.WB), dim3(256), 0, s, p.nw, p.WB, p.d_win, p.segs, extra, nextra,
-                     parts);
-  tl->mark("k_msm_windows", s, (double)(p.NS + nextra) * COST_ADD);
-  hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, s, p.nw, p.WB, p.d_win, parts, p.wins, p.out);
+  hipLaunchKernelGGL(k_msm_windows, dim3(p.nw + 1, p.WB, p.G), dim3(256), 0, s, p.nw, p.WB, p.NSg, p.d_win, p.segs,
+                     extra, nextra, parts);
+  tl->mark("k_msm_windows", s, (double)(p.NS + (double)p.G * nextra) * COST_ADD);
+  hipLaunchKernelGGL(k_msm_final, dim3(p.G), dim3(64), 0, s, p.nw, p.WB, p.d_win, parts, p.out);
   {
     double dbl = 0;
     for (int w = 0; w < p.nw; w++) dbl += p.win[w].off;
-    tl->mark("k_msm_final", s, dbl * COST_DBL + (p.nw + 1) * (p.WB + 1) * COST_ADD);
+    tl->mark("k_msm_final", s, p.G * (dbl * COST_DBL + (p.nw + 1) * (p.WB + 1) * COST_ADD));
   }
 }
 

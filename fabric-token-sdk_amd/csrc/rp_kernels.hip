@@ -810,7 +810,10 @@ FTS_DEV Fr s_vec(const uint32_t* C, int k, int i) {
   return s;
 }
 
-__global__ void __launch_bounds__(64) k_rp_terms_fixed(int B, int n, int k, const int32_t* __restrict__ status,
+// sel != nullptr: lanes cover the B proofs sel[0 .. B) (the group test's failing
+// proofs) instead of proofs 0 .. B
+__global__ void __launch_bounds__(64) k_rp_terms_fixed(int B, int n, int k, const int32_t* __restrict__ sel,
+                                                       const int32_t* __restrict__ status,
                                                        const int32_t* __restrict__ ipa_flag,
                                                        const uint32_t* __restrict__ sc, const uint32_t* __restrict__ ch,
                                                        const uint32_t* __restrict__ tables, uint32_t* __restrict__ terms) {
@@ -818,6 +821,7 @@ __global__ void __launch_bounds__(64) k_rp_terms_fixed(int B, int n, int k, cons
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * nf) return;
   int b = gid / nf, t = gid % nf;
+  if (sel) b = sel[b];
   if (status[b] != 0) return;
   const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
   const uint32_t* S = sc + (size_t)b * RP_NSC * 8;
@@ -862,7 +866,8 @@ __global__ void __launch_bounds__(64) k_rp_terms_fixed(int B, int n, int k, cons
   store_g1j(terms + ((size_t)b * rp_nterms(n, k) + slot) * 24, r);
 }
 
-__global__ void __launch_bounds__(64) k_rp_terms_var(int B, int n, int k, const int32_t* __restrict__ status,
+__global__ void __launch_bounds__(64) k_rp_terms_var(int B, int n, int k, const int32_t* __restrict__ sel,
+                                                     const int32_t* __restrict__ status,
                                                      const int32_t* __restrict__ ipa_flag,
                                                      const uint32_t* __restrict__ pts, const uint32_t* __restrict__ ch,
                                                      uint32_t* __restrict__ terms, uint32_t* __restrict__ scratch) {
@@ -870,6 +875,7 @@ __global__ void __launch_bounds__(64) k_rp_terms_var(int B, int n, int k, const 
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * nv) return;
   int b = gid / nv, t = gid % nv;
+  if (sel) b = sel[b];
   if (status[b] != 0) return;
   const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
   const uint32_t* Pt = pts + (size_t)b * rp_npts(k) * 16;
@@ -898,17 +904,19 @@ __global__ void __launch_bounds__(64) k_rp_terms_var(int B, int n, int k, const 
       pt = RP_PT_L + k + j;
     }
   }
-  // all variable terms enter with a minus sign
-  G1J r = var_base_mul(load_g1a(Pt + pt * 16), fr_canon(f_neg(s)), scratch + (size_t)gid * 10 * 24);
+  // all variable terms enter with a minus sign; GLV + joint Straus (124 doublings)
+  G1J r = glv_mul(load_g1a(Pt + pt * 16), fr_canon(f_neg(s)), scratch, (size_t)B * nv, (size_t)gid);
   store_g1j(terms + ((size_t)b * rp_nterms(n, k) + slot) * 24, r);
 }
 
 // ------------------------------------------------------------------ check
-__global__ void __launch_bounds__(64) k_rp_check(int B, int n, int k, int32_t* __restrict__ status,
-                                                 const int32_t* __restrict__ ipa_flag,
+__global__ void __launch_bounds__(64) k_rp_check(int B, int n, int k, const int32_t* __restrict__ sel,
+                                                 int32_t* __restrict__ status, const int32_t* __restrict__ ipa_flag,
                                                  const uint32_t* __restrict__ terms, const uint32_t* __restrict__ hpa) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B || status[b] != 0) return;
+  if (b >= B) return;
+  if (sel) b = sel[b];
+  if (status[b] != 0) return;
   const uint32_t* T = terms + (size_t)b * rp_nterms(n, k) * 24;
   G1J e1 = load_g1j(T);
   for (int t = 1; t < 5; t++) e1 = nl_add_mem(e1, T + t * 24, 0);
@@ -995,15 +1003,20 @@ __global__ void __launch_bounds__(64) k_rlc_prep(int B, int n, int k, const int3
   store_f(K + 4 * 8, fr_mul(rho2, bb));
 }
 
-// one block per column: col 0 G (ped1), 1 H (ped2), 2 Q, 3+i G_i, 3+n+i H_i
-// (s_i and y^-i come precomputed, i-major, from k_rp_powers)
-__global__ void __launch_bounds__(256) k_rlc_columns(int B, int n, int k, const uint32_t* __restrict__ ch,
+// one block per (column, group): col 0 G (ped1), 1 H (ped2), 2 Q, 3+i G_i, 3+n+i H_i
+// (s_i and y^-i come precomputed, i-major, from k_rp_powers).  The batch check
+// has one group of all B proofs; the group test has G groups of gs proof slots
+// (sel[g gs + j], -1 = empty) -> colsum[g][col]
+__global__ void __launch_bounds__(256) k_rlc_columns(int B, int n, int k, int gs, const int32_t* __restrict__ sel,
+                                                     const uint32_t* __restrict__ ch,
                                                      const uint32_t* __restrict__ coef, const uint32_t* __restrict__ ypow,
                                                      const uint32_t* __restrict__ svec, uint32_t* __restrict__ colsum) {
   __shared__ uint32_t sh[256 * 8];
-  const int col = blockIdx.x, t = threadIdx.x;
+  const int col = blockIdx.x, grp = blockIdx.y, t = threadIdx.x, nt = blockDim.x;  // nt: 64 or 256
   Fr acc = f_zero<FrP>();
-  for (int b = t; b < B; b += 256) {
+  for (int j = t; j < gs; j += nt) {
+    const int b = sel ? sel[(size_t)grp * gs + j] : grp * gs + j;
+    if (b < 0 || b >= B) continue;
     const uint32_t* K = coef + (size_t)b * RLC_NCOEF * 8;
     Fr v;
     if (col < 3) {
@@ -1040,7 +1053,7 @@ __global__ void __launch_bounds__(256) k_rlc_columns(int B, int n, int k, const 
   }
   store_f(sh + t * 8, acc);
   __syncthreads();
-  for (int half = 128; half >= 1; half >>= 1) {
+  for (int half = nt / 2; half >= 1; half >>= 1) {
     if (t < half) {
       Fr o;
       load_f(sh + (t + half) * 8, o);
@@ -1049,13 +1062,17 @@ __global__ void __launch_bounds__(256) k_rlc_columns(int B, int n, int k, const 
     }
     __syncthreads();
   }
-  if (t == 0) store_f(colsum + col * 8, f_from_mont(acc));
+  if (t == 0) store_f(colsum + ((size_t)grp * (3 + 2 * n) + col) * 8, f_from_mont(acc));
 }
 
-__global__ void __launch_bounds__(64) k_rlc_fixed(int n, const uint32_t* __restrict__ colsum,
+// lane per (group, column): the fixed-base product of the column sum
+__global__ void __launch_bounds__(64) k_rlc_fixed(int n, int G, const uint32_t* __restrict__ colsum,
                                                   const uint32_t* __restrict__ tables, uint32_t* __restrict__ out) {
-  int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= 3 + 2 * n) return;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (3 + 2 * n) * G) return;
+  const int col = gid % (3 + 2 * n);
+  colsum += (size_t)(gid / (3 + 2 * n)) * (3 + 2 * n) * 8;
+  out += (size_t)(gid / (3 + 2 * n)) * (3 + 2 * n) * 24;
   int base = col == 0 ? tb_G(n) : col == 1 ? tb_H(n) : col == 2 ? tb_Q(n) : col - 3;
   Scalar s;
 #pragma unroll
@@ -1076,6 +1093,28 @@ __global__ void __launch_bounds__(64) k_rlc_finalize(int B, const uint32_t* __re
   if (b < B && pass && status[b] == 0 && ipa_flag[b] != 0) status[b] = ipa_flag[b];
 }
 
+// group test verdicts: lane per proof slot j of the selection (group j / gs);
+// a group whose partial combination is the identity accepts its proofs (their
+// deferred IPA structural verdicts become final, as in k_rlc_finalize), the
+// proofs of the other groups are appended to `next` (the next round's list)
+__global__ void __launch_bounds__(256) k_rlc_group_final(int slots, int gs, const int32_t* __restrict__ sel,
+                                                         const uint32_t* __restrict__ msm_out,
+                                                         int32_t* __restrict__ status,
+                                                         const int32_t* __restrict__ ipa_flag,
+                                                         int32_t* __restrict__ next, uint32_t* __restrict__ next_count) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= slots) return;
+  const int b = sel ? sel[j] : j;
+  if (b < 0 || status[b] != 0) return;
+  Fp z;
+  load_fp(msm_out + (size_t)(j / gs) * 24 + 16, z);
+  if (f_is_zero(z)) {
+    if (ipa_flag[b] != 0) status[b] = ipa_flag[b];
+  } else {
+    next[atomicAdd(next_count, 1u)] = b;
+  }
+}
+
 // ------------------------------------------------------------ host launch
 #define FTS_LAUNCH(kern, nthreads, bs, stream, ...)                                   \
   do {                                                                                \
@@ -1086,7 +1125,8 @@ __global__ void __launch_bounds__(64) k_rlc_finalize(int B, const uint32_t* __re
 
 
 size_t rp_scratch_words(int B, int n, int k) {
-  return std::max((size_t)B * (3 + 2 * k) * 10 * 24, (size_t)B * (HS_SCRATCH + 2 * 16 * 24));
+  // per-proof fallback: 16-entry GLV lane tables of the 3 + 2k variable terms
+  return std::max((size_t)B * (3 + 2 * k) * 16 * 24, (size_t)B * (HS_SCRATCH + 2 * 16 * 24));
 }
 size_t rp_terms_words(int B, int n, int k) { return (size_t)B * rp_nterms(n, k) * 24; }
 
@@ -1192,16 +1232,24 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   tl->mark("k_rp_x0_build", s2, 0);
   FTS_LAUNCH(k_rp_x0_hash, B, 64, s2, B, n, k, d.status, d.x0_msgs, x0_tmpl, d.ch);
   tl->mark("k_rp_x0_hash", s2, 0);
-  // main: variable points of the batch equation -> MSM
+  // main: variable points of the batch equation -> MSM (after the caller's hook, e.g. the
+  // exclusion of range proofs whose action failed its sigma proof)
+  if (d.pre_rlc) d.pre_rlc(d.pre_rlc_arg, s);
   FTS_LAUNCH(k_rlc_prep, B, 64, s, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, r.key, d.hpa, d.pts, r.msc, r.coef);
   tl->mark("k_rlc_prep", s, (double)B * (3 * k + 30));
-  hipLaunchKernelGGL(k_rlc_columns, dim3(3 + 2 * n), dim3(256), 0, s2, B, n, k, d.ch, r.coef, d.ypow, d.svec, r.colsum);
+  hipLaunchKernelGGL(k_rlc_columns, dim3(3 + 2 * n, 1), dim3(256), 0, s2, B, n, k, B, (const int32_t*)nullptr, d.ch,
+                     r.coef, d.ypow, d.svec, r.colsum);
   tl->mark("k_rlc_columns", s2, (double)B * 3 * n);
-  FTS_LAUNCH(k_rlc_fixed, 3 + 2 * n, 64, s2, n, r.colsum, tables, r.fixed);
+  FTS_LAUNCH(k_rlc_fixed, 3 + 2 * n, 64, s2, n, 1, r.colsum, tables, r.fixed);
   tl->mark("k_rlc_fixed", s2, (double)(3 + 2 * n) * COST_FB_FRESH);
   launch_msm(r.plan, d.pts, r.msc, r.fixed, 3 + 2 * n, r.msm_scratch, s, s2, tl);
   FTS_LAUNCH(k_rlc_finalize, B, 64, s, B, r.plan.out, d.status, d.ipa_flag, r.flag);
   tl->mark("k_rlc_finalize", s, 0);
+}
+
+void launch_normalize_all(int total, const uint32_t* jac, uint32_t* aff, hipStream_t s) {
+  FTS_LAUNCH(k_rp_normalize, (total + NORM_E - 1) / NORM_E, NORM_BS, s, total, 1, 1, 0, (const int32_t*)nullptr, jac,
+             aff, (uint8_t*)nullptr);
 }
 
 // per-proof final equations (fallback when the batch combination fails)
@@ -1210,14 +1258,38 @@ void launch_rp_gather(const RpGather& g, int k, uint8_t* raw, uint32_t* sc, int3
   FTS_LAUNCH(k_rp_gather, (size_t)g.off[g.G] * per, 256, s, g, rp_npts(k), raw, sc, status, ipa);
 }
 
-void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, hipStream_t s, Timeline* tl) {
-  const int B = d.B, n = d.n, k = d.k;
-  FTS_LAUNCH(k_rp_terms_fixed, B * (3 + 2 * n), 64, s, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, tables, d.terms);
+// per-proof final equations of the nsel proofs sel[0 .. nsel) (all B if sel == nullptr)
+void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, const int32_t* sel, int nsel, hipStream_t s,
+                        Timeline* tl) {
+  const int B = sel ? nsel : d.B, n = d.n, k = d.k;
+  FTS_LAUNCH(k_rp_terms_fixed, B * (3 + 2 * n), 64, s, B, n, k, sel, d.status, d.ipa_flag, d.sc, d.ch, tables, d.terms);
   tl->mark("k_rp_terms_fixed", s, (double)B * (3 + 2 * n) * COST_FB_FRESH);
-  FTS_LAUNCH(k_rp_terms_var, B * (3 + 2 * k), 64, s, B, n, k, d.status, d.ipa_flag, d.pts, d.ch, d.terms, d.scratch);
-  tl->mark("k_rp_terms_var", s, (double)B * (3 + 2 * k) * COST_VB4);
-  FTS_LAUNCH(k_rp_check, B, 64, s, B, n, k, d.status, d.ipa_flag, d.terms, d.hpa);
+  FTS_LAUNCH(k_rp_terms_var, B * (3 + 2 * k), 64, s, B, n, k, sel, d.status, d.ipa_flag, d.pts, d.ch, d.terms,
+             d.scratch);
+  tl->mark("k_rp_terms_var", s, (double)B * (3 + 2 * k) * (4.0 * 7.0 + 12.0 * COST_ADD + 124 * COST_DBL + 60 * COST_ADD));
+  FTS_LAUNCH(k_rp_check, B, 64, s, B, n, k, sel, d.status, d.ipa_flag, d.terms, d.hpa);
   tl->mark("k_rp_check", s, (double)B * rp_nterms(n, k) * COST_ADD);
+}
+
+// Group test of the batch check (after it failed): G groups of gs proof slots
+// sel[g gs + j] (-1 = empty); every group's partial random linear combination
+// (the batch check's weights) from per-group column sums + one grouped MSM
+// (plan p: G groups of gs * npts points, indirection sel).  Groups that close
+// accept their proofs; the proofs of the others are appended to next[] /
+// next_count for the next round (smaller groups, or per-proof checks).
+void launch_rlc_group_test(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const MsmPlan& p,
+                           const int32_t* sel, int G, int gs, uint32_t* gcol, uint32_t* gfix, int32_t* next,
+                           uint32_t* next_count, hipStream_t s, Timeline* tl) {
+  const int n = d.n, k = d.k;
+  hipLaunchKernelGGL(k_rlc_columns, dim3(3 + 2 * n, G), dim3(gs <= 64 ? 64 : 256), 0, s, d.B, n, k, gs, sel, d.ch,
+                     r.coef, d.ypow, d.svec, gcol);
+  tl->mark("k_rlc_group_columns", s, (double)G * gs * 3 * n);
+  FTS_LAUNCH(k_rlc_fixed, (size_t)(3 + 2 * n) * G, 64, s, n, G, gcol, tables, gfix);
+  tl->mark("k_rlc_group_fixed", s, (double)G * (3 + 2 * n) * COST_FB_FRESH);
+  launch_msm(p, d.pts, r.msc, gfix, 3 + 2 * n, r.msm_scratch, s, s, tl);
+  FTS_LAUNCH(k_rlc_group_final, (size_t)G * gs, 256, s, G * gs, gs, sel, p.out, d.status, d.ipa_flag, next,
+             next_count);
+  tl->mark("k_rlc_group_final", s, 0);
 }
 
 }  // namespace fts

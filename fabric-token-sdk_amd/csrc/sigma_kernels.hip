@@ -29,18 +29,20 @@ __global__ void __launch_bounds__(256) k_sig_decode(int npts, const uint8_t* __r
   store_g1a(pts + (size_t)gid * 16, a);
 }
 
-// aff layout per action (from aff_off): TAS [in' (n_in), out' (n_out), sum, inCom (n_in), typeCom, sumCom]
-//                                       ST  [V (n_out), com]
+// aff / jac layout per action (from aff_off): TAS [in' (n_in), out' (n_out), sum, inCom (n_in), typeCom, sumCom]
+//                                             ST  [V (n_out), com]
+// Every per-action point is computed Jacobian into jac, then ALL slots of the
+// batch are normalised at once (k_rp_normalize: one field inversion per 1,024
+// points instead of one per action).
+// lane per action: the primes In_i - CT, Out_j - CT and (TAS) their sum (typeandsum.go:240-252)
 __global__ void __launch_bounds__(64) k_sig_prep(int A, const SigAction* __restrict__ act,
                                                  const uint32_t* __restrict__ pts, const int32_t* __restrict__ status,
-                                                 uint32_t* __restrict__ aff, const int32_t* __restrict__ aff_off,
-                                                 uint32_t* __restrict__ jscr, uint8_t* __restrict__ rp_raw, int rp_k) {
+                                                 const int32_t* __restrict__ aff_off, uint32_t* __restrict__ jscr) {
   int a = blockIdx.x * blockDim.x + threadIdx.x;
   if (a >= A || status[a] != 0) return;
   const SigAction ac = act[a];
   const uint32_t* P = pts + (size_t)ac.pt_off * 16;
   uint32_t* J = jscr + (size_t)aff_off[a] * 24;
-  uint32_t* F = aff + (size_t)aff_off[a] * 16;
   const int nin = ac.kind == SIG_TAS ? ac.n_in : 0;
   const int m = nin + ac.n_out;
   G1J sum = g1j_identity();
@@ -50,18 +52,37 @@ __global__ void __launch_bounds__(64) k_sig_prep(int A, const SigAction* __restr
     store_g1j(J + i * 24, d);
     if (ac.kind == SIG_TAS) sum = nl_add_mem(sum, J + i * 24, i >= nin);
   }
-  int mm = m;
-  if (ac.kind == SIG_TAS) {
-    store_g1j(J + m * 24, sum);
-    mm = m + 1;
-  }
-  batch_to_affine(J, F, mm);
-  if (ac.rp_base >= 0 && rp_raw) {
-    const int npts_rp = rp_npts(rp_k);
-    const int nv = ac.n_out < ac.rp_count ? ac.n_out : ac.rp_count;
-    for (int j = 0; j < nv; j++)
-      store_point_be(rp_raw + ((size_t)(ac.rp_base + j) * npts_rp + RP_PT_V) * 64, load_g1a(F + (nin + j) * 16));
-  }
+  if (ac.kind == SIG_TAS) store_g1j(J + m * 24, sum);
+}
+
+// lane per action: the range proofs' V_j = Out_j - CT (affine) into the rp batch's raw V slots
+__global__ void __launch_bounds__(64) k_sig_vslots(int A, const SigAction* __restrict__ act,
+                                                   const int32_t* __restrict__ status, const uint32_t* __restrict__ aff,
+                                                   const int32_t* __restrict__ aff_off, uint8_t* __restrict__ rp_raw,
+                                                   int rp_k) {
+  int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= A || status[a] != 0) return;
+  const SigAction ac = act[a];
+  if (ac.rp_base < 0) return;
+  const uint32_t* F = aff + (size_t)aff_off[a] * 16;
+  const int nin = ac.kind == SIG_TAS ? ac.n_in : 0;
+  const int npts_rp = rp_npts(rp_k);
+  const int nv = ac.n_out < ac.rp_count ? ac.n_out : ac.rp_count;
+  for (int j = 0; j < nv; j++)
+    store_point_be(rp_raw + ((size_t)(ac.rp_base + j) * npts_rp + RP_PT_V) * 64, load_g1a(F + (nin + j) * 16));
+}
+
+// lane per action whose sigma proof failed: its range proofs leave the batch
+// check (their verdicts are never observable: the TypeAndSum / SameType error
+// wins, transfer.go:192-196, issue/verifier.go:40-43)
+__global__ void __launch_bounds__(256) k_sig_exclude(int A, const SigAction* __restrict__ act,
+                                                     const int32_t* __restrict__ status, int32_t* __restrict__ rp_status) {
+  int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= A || status[a] == 0) return;
+  const SigAction ac = act[a];
+  if (ac.rp_base < 0) return;
+  for (int j = 0; j < ac.rp_count; j++)
+    if (rp_status[ac.rp_base + j] == FTS_OK) rp_status[ac.rp_base + j] = FTS_E_NOT_RUN;
 }
 
 __global__ void __launch_bounds__(64) k_sig_terms(int nwork, const int2* __restrict__ work,
@@ -140,17 +161,35 @@ FTS_DEV void put_hex_aff(uint8_t* msg, int idx, const uint32_t* aff_pt, bool sep
   put_hex_record(msg, 130u * idx, pw, sep);
 }
 
-__global__ void __launch_bounds__(64) k_sig_finish(int A, const SigAction* __restrict__ act,
-                                                   const uint32_t* __restrict__ pts, const uint32_t* __restrict__ sc,
-                                                   int32_t* __restrict__ status, const uint32_t* __restrict__ terms,
-                                                   uint32_t* __restrict__ aff, const int32_t* __restrict__ aff_off,
-                                                   uint32_t* __restrict__ jscr, uint8_t* __restrict__ msgs) {
+// lane per action: the transcript commitments (Jacobian) from the terms
+__global__ void __launch_bounds__(64) k_sig_coms(int A, const SigAction* __restrict__ act,
+                                                 const int32_t* __restrict__ status, const uint32_t* __restrict__ terms,
+                                                 const int32_t* __restrict__ aff_off, uint32_t* __restrict__ jscr) {
   int a = blockIdx.x * blockDim.x + threadIdx.x;
   if (a >= A || status[a] != 0) return;
   const SigAction ac = act[a];
   const uint32_t* T = terms + (size_t)ac.term_off * 24;
-  uint32_t* F = aff + (size_t)aff_off[a] * 16;
   uint32_t* J = jscr + (size_t)aff_off[a] * 24;
+  if (ac.kind == SIG_TAS) {
+    const int N = ac.n_in, M = ac.n_out;
+    const int c0 = N + M + 1;  // first commitment slot
+    for (int i = 0; i < N; i++) store_g1j(J + (c0 + i) * 24, nl_add_mem(load_g1j(T + (2 * i) * 24), T + (2 * i + 1) * 24, 1));
+    store_g1j(J + (c0 + N) * 24, nl_add_mem(load_g1j(T + (2 * N + 2) * 24), T + (2 * N + 3) * 24, 1));  // typeCom
+    store_g1j(J + (c0 + N + 1) * 24, nl_add_mem(load_g1j(T + (2 * N) * 24), T + (2 * N + 1) * 24, 1));  // sumCom
+  } else {
+    store_g1j(J + ac.n_out * 24, nl_add_mem(load_g1j(T), T + 24, 1));
+  }
+}
+
+// lane per action: transcript (hex of the affine points) + SHA-256 + challenge compare
+__global__ void __launch_bounds__(64) k_sig_finish(int A, const SigAction* __restrict__ act,
+                                                   const uint32_t* __restrict__ pts, const uint32_t* __restrict__ sc,
+                                                   int32_t* __restrict__ status, const uint32_t* __restrict__ aff,
+                                                   const int32_t* __restrict__ aff_off, uint8_t* __restrict__ msgs) {
+  int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= A || status[a] != 0) return;
+  const SigAction ac = act[a];
+  const uint32_t* F = aff + (size_t)aff_off[a] * 16;
   const uint32_t* CT = pts + (size_t)ac.pt_off * 16;
   uint8_t* msg = msgs + ac.msg_off;
   const uint32_t* S = sc + (size_t)ac.sc_off * 8;
@@ -159,10 +198,6 @@ __global__ void __launch_bounds__(64) k_sig_finish(int A, const SigAction* __res
   if (ac.kind == SIG_TAS) {
     const int N = ac.n_in, M = ac.n_out;
     const int c0 = N + M + 1;  // first commitment slot
-    for (int i = 0; i < N; i++) store_g1j(J + (c0 + i) * 24, nl_add_mem(load_g1j(T + (2 * i) * 24), T + (2 * i + 1) * 24, 1));
-    store_g1j(J + (c0 + N) * 24, nl_add_mem(load_g1j(T + (2 * N + 2) * 24), T + (2 * N + 3) * 24, 1));  // typeCom
-    store_g1j(J + (c0 + N + 1) * 24, nl_add_mem(load_g1j(T + (2 * N) * 24), T + (2 * N + 1) * 24, 1));  // sumCom
-    batch_to_affine(J + c0 * 24, F + c0 * 16, N + 2);
     // Arr(inComs, typeCom, sumCom, in'..., out'..., CT, sum)     typeandsum.go:267
     int idx = 0;
     np = 2 * N + M + 4;
@@ -173,8 +208,6 @@ __global__ void __launch_bounds__(64) k_sig_finish(int A, const SigAction* __res
     chal = S + TAS_SC_CHAL * 8;
   } else {
     const int M = ac.n_out;
-    store_g1j(J + M * 24, nl_add_mem(load_g1j(T), T + 24, 1));
-    batch_to_affine(J + M * 24, F + M * 16, 1);
     put_hex_aff(msg, 0, CT, true);  // Arr(CT, com)   sametype.go:174
     put_hex_aff(msg, 1, F + M * 16, false);
     np = 2;
@@ -197,16 +230,27 @@ __global__ void __launch_bounds__(64) k_sig_finish(int A, const SigAction* __res
     if (nt_) hipLaunchKernelGGL(kern, dim3((unsigned)((nt_ + (bs)-1) / (bs))), dim3(bs), 0, stream, __VA_ARGS__); \
   } while (0)
 
+// batch affine normalisation (rp_kernels.hip): all naff slots of the sigma batch
+void launch_normalize_all(int total, const uint32_t* jac, uint32_t* aff, hipStream_t s);
+
 // phase 1 (before the range-proof batch): decode + primes (writes the rp V slots)
 void launch_sig_prep(const SigBatchDev& d, hipStream_t s) {
   FTS_LAUNCH(k_sig_decode, d.npts, 256, s, d.npts, d.raw, d.pt_owner, d.pts, d.status);
-  FTS_LAUNCH(k_sig_prep, d.A, 64, s, d.A, d.act, d.pts, d.status, d.aff, d.aff_off, d.jac, d.rp_raw, d.rp_k);
+  FTS_LAUNCH(k_sig_prep, d.A, 64, s, d.A, d.act, d.pts, d.status, d.aff_off, d.jac);
+  launch_normalize_all(d.naff, d.jac, d.aff, s);
+  if (d.rp_raw) FTS_LAUNCH(k_sig_vslots, d.A, 64, s, d.A, d.act, d.status, d.aff, d.aff_off, d.rp_raw, d.rp_k);
 }
 // phase 2: sigma equations (independent of the range proofs)
 void launch_sig_finish(const SigBatchDev& d, const uint32_t* tables, int n, hipStream_t s) {
   FTS_LAUNCH(k_sig_terms, d.nwork, 64, s, d.nwork, d.work, d.act, d.pts, d.sc, d.status, d.aff, d.aff_off, tables, n,
              d.terms, d.scratch);
-  FTS_LAUNCH(k_sig_finish, d.A, 64, s, d.A, d.act, d.pts, d.sc, d.status, d.terms, d.aff, d.aff_off, d.jac, d.msgs);
+  FTS_LAUNCH(k_sig_coms, d.A, 64, s, d.A, d.act, d.status, d.terms, d.aff_off, d.jac);
+  launch_normalize_all(d.naff, d.jac, d.aff, s);
+  FTS_LAUNCH(k_sig_finish, d.A, 64, s, d.A, d.act, d.pts, d.sc, d.status, d.aff, d.aff_off, d.msgs);
+}
+// the range proofs of actions whose sigma proof failed leave the batch check
+void launch_sig_exclude(const SigBatchDev& d, int32_t* rp_status, hipStream_t s) {
+  FTS_LAUNCH(k_sig_exclude, d.A, 256, s, d.A, d.act, d.status, rp_status);
 }
 
 }  // namespace fts

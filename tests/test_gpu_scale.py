@@ -141,3 +141,64 @@ def test_coalesced_batches_keep_their_verdicts(pp_raw):
     for b in batches:
         b.close()
     pp.close()
+
+
+def test_one_bad_proof_in_coalesced_pass_group_test(pp_raw):
+    """SURVEY Appendix B fallback: one tampered proof inside a coalesced pass of 8
+    caller batches.  The failed batch check is narrowed by group tests (groups never
+    straddle two caller batches) so only a handful of proofs -- all of the bad
+    proof's own batch -- get the per-proof final equations; every verdict equals
+    the reference's (rangecorrectness.go:141-160)."""
+    import os
+    import threading
+
+    import fts_gpu
+
+    old = os.environ.get("FTS_LANES")
+    os.environ["FTS_LANES"] = "1"
+    try:
+        pp = fts_gpu.PublicParams(pp_raw, bit_length=16, device=0)
+    finally:
+        if old is None:
+            del os.environ["FTS_LANES"]
+        else:
+            os.environ["FTS_LANES"] = old
+    rng = random.Random(0xB15EC7)
+    m, nb, bad_batch, bad_idx = 512, 8, 3, 333
+    batches, expect = [], []
+    for t in range(nb):
+        vals = [rng.getrandbits(16) for _ in range(m)]
+        bfs = [rng.randrange(bn.R).to_bytes(32, "big") for _ in range(m)]
+        proofs, coms = pp.prove_range_batch_gpu(vals, bfs, seed=7000 + 1000 * t)
+        exp = [0] * m
+        if t == bad_batch:
+            r = zkat.RangeProof.deserialize(proofs[bad_idx])
+            r.ipa.L[1] = bn.g1_add(r.ipa.L[1], bn.GEN)
+            proofs[bad_idx] = r.serialize()
+            exp[bad_idx] = 6
+        batches.append(pp.stage_range_proofs(proofs, coms))
+        expect.append(exp)
+    # occupy the single lane so the 8 submissions queue up and coalesce
+    blocker = batches[0]
+    out, merged, tim = [None] * nb, [0] * nb, [None] * nb
+
+    def work(t):
+        out[t] = [int(s) for s in batches[t].verify()]
+        merged[t] = batches[t].merged()
+        tim[t] = batches[t].timings()
+
+    th = [threading.Thread(target=blocker.verify)] + [threading.Thread(target=work, args=(t,)) for t in range(nb)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    for t in range(nb):
+        assert out[t] == expect[t], t
+    assert merged[bad_batch] > 1, merged
+    tb = tim[bad_batch]
+    assert "fb:k_rlc_group_final" in tb and "fb:k_rp_terms_fixed" in tb, sorted(tb)
+    per_proof = tb["fb:k_rp_terms_fixed"][1] / ((3 + 2 * 16) * 15 * 11 * 136)
+    assert 1 <= round(per_proof) <= 64, per_proof   # the bad proof's group of 64, not the pass (4,096)
+    for b in batches:
+        b.close()
+    pp.close()
