@@ -30,6 +30,31 @@ struct Sha256Const {
 };
 
 FTS_HD uint32_t sha_rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+// a ^ b ^ c: one v_bitop3_b32 (truth table 0x96) on gfx950 instead of two v_xor_b32
+// (the compiler fuses Ch / Maj into bitop3 itself, not the 3-way xors of the
+// Sigma / sigma functions); Ch / Maj get their truth tables explicitly
+// (0xCA = e ? f : g, 0xE8 = majority); the host side (prover, PP) keeps plain C++
+FTS_HD uint32_t sha_xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+FTS_HD uint32_t sha_ch(uint32_t e, uint32_t f, uint32_t g) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
+#else
+  return (e & f) ^ (~e & g);
+#endif
+}
+FTS_HD uint32_t sha_maj(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+#else
+  return (a & b) ^ (a & c) ^ (b & c);
+#endif
+}
 
 FTS_HD void sha256_init(uint32_t st[8]) {
   st[0] = 0x6a09e667u; st[1] = 0xbb67ae85u; st[2] = 0x3c6ef372u; st[3] = 0xa54ff53au;
@@ -46,16 +71,16 @@ FTS_HD void sha256_compress(uint32_t st[8], uint32_t w[16]) {
       wi = w[i];
     } else {
       uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      uint32_t s0 = sha_rotr(w15, 7) ^ sha_rotr(w15, 18) ^ (w15 >> 3);
-      uint32_t s1 = sha_rotr(w2, 17) ^ sha_rotr(w2, 19) ^ (w2 >> 10);
+      uint32_t s0 = sha_xor3(sha_rotr(w15, 7), sha_rotr(w15, 18), w15 >> 3);
+      uint32_t s1 = sha_xor3(sha_rotr(w2, 17), sha_rotr(w2, 19), w2 >> 10);
       wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
       w[i & 15] = wi;
     }
-    uint32_t S1 = sha_rotr(e, 6) ^ sha_rotr(e, 11) ^ sha_rotr(e, 25);
-    uint32_t ch = (e & f) ^ (~e & g);
+    uint32_t S1 = sha_xor3(sha_rotr(e, 6), sha_rotr(e, 11), sha_rotr(e, 25));
+    uint32_t ch = sha_ch(e, f, g);
     uint32_t t1 = h + S1 + ch + Sha256Const::K[i] + wi;
-    uint32_t S0 = sha_rotr(a, 2) ^ sha_rotr(a, 13) ^ sha_rotr(a, 22);
-    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint32_t S0 = sha_xor3(sha_rotr(a, 2), sha_rotr(a, 13), sha_rotr(a, 22));
+    uint32_t mj = sha_maj(a, b, c);
     uint32_t t2 = S0 + mj;
     h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
   }
