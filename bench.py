@@ -288,6 +288,7 @@ def main():
     # roofline kernel: the largest share of the algorithmic work (MADs/launch);
     # the longest (latency-bound) kernel is reported beside it
     dom = max(kt, key=lambda kname: kt[kname][1])
+    dom1 = max(kt1, key=lambda kname: kt1[kname][1])  # a lone batch may take the latency path's kernels
     longest = max((kn for kn in avg if not kn.startswith("host_")), key=avg.get)
 
     def kernel_roof(kname):
@@ -365,9 +366,10 @@ def main():
             "host": host,
             "isolated_batch": {"ms": round(iso_ms, 3), "verifies_per_s": round(B / iso_ms * 1e3, 1),
                                "note": "one %d-proof batch alone on the GPU (latency; no coalescing)" % B,
-                               "roofline_kernel_ms": round(avg1.get(dom, 0.0), 4),
-                               "roofline_frac": round(kt1[dom][1] / (avg1[dom] * 1e-3) / 1e12 / PEAK_TMAD, 4)
-                               if avg1.get(dom) else None},
+                               "roofline_kernel": dom1,
+                               "roofline_kernel_ms": round(avg1.get(dom1, 0.0), 4),
+                               "roofline_frac": round(kt1[dom1][1] / (avg1[dom1] * 1e-3) / 1e12 / PEAK_TMAD, 4)
+                               if avg1.get(dom1) else None},
             "isolated_pass": {"proofs": m * B, "ms": round(pass_ms, 3), "verifies_per_s": round(m * B / pass_ms * 1e3, 1)},
             "roofline": roofline,
             "longest_kernel": longest_kernel,

@@ -169,8 +169,8 @@ struct RpBatchDev {
   uint32_t* scratch;   // var-base lane tables
   uint32_t* ypow;      // [n][B][8] y^-i (Montgomery Fr), i-major (coalesced over proofs)
   uint32_t* svec;      // [n][B][8] s_i = prod_j x_j^(+-1) (ipa.go:343-356 unrolled), i-major
-  uint32_t* zvec;      // [n][B][8] z^2 2^i y^-i (latency path only), i-major
-  void (*pre_rlc)(void* arg, hipStream_t s);  // optional hook launched on s before the batch check
+  uint32_t* zvec;      // [n][B][8] z^2 2^i y^-i, i-major (fixed-base com terms; H_i columns of the batch check)
+  void (*pre_rlc)(void* arg, hipStream_t s);  // optional hook launched on the check's stream before k_rlc_prep
   void* pre_rlc_arg;
   int com_fixed;       // 1: com by fixed-base groups + x*D on the side stream (latency path,
                        //    small passes); 0: Horner sum + joint GLV/Straus chains (work path)
@@ -181,12 +181,19 @@ struct RpBatchDev {
 #include "msm.hpp"
 namespace fts {
 // device buffers of the random-linear-combination check
+// Per-proof coefficients (Montgomery Fr): 0 rho(ip - polEval), 1 rho tau,
+// 2 rho'(ab - ip) (times x0 in the Q column), 3 rho' a, 4 rho' b, 5 rho',
+// 6 -rho' z, 7 rho' delta.
+constexpr int RLC_NCOEF = 8;
+// fixed-base columns of the batch equation: 0 G, 1 H, 2+i G_i, 2+n+i H_i,
+// 2n+2 K, 2n+3 P, 2n+4 Q (last: the only column that needs x0)
+inline __host__ __device__ int rlc_ncols(int n) { return 2 * n + 5; }
 struct RlcDev {
   uint32_t* key;     // [8] ChaCha20 key (fresh per call)
   uint32_t* msc;     // [B][5+2k][8] MSM scalars (canonical)
-  uint32_t* coef;    // [B][5][8]
-  uint32_t* colsum;  // [3+2n][8]
-  uint32_t* fixed;   // [3+2n][24]
+  uint32_t* coef;    // [B][RLC_NCOEF][8]
+  uint32_t* colsum;  // [rlc_ncols(n)][8]
+  uint32_t* fixed;   // [rlc_ncols(n)][24]
   int32_t* flag;     // [1]
   uint32_t* msm_scratch;
   MsmPlan plan;

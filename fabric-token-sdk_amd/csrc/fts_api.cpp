@@ -39,7 +39,8 @@ size_t rp_scratch_words(int B, int n, int k);
 size_t rp_terms_words(int B, int n, int k);
 void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s);
 void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const uint32_t* wtables,
-                     const uint8_t* x0_const, const uint8_t* x0_tmpl, hipStream_t s, hipStream_t s2, Timeline* tl);
+                     const uint8_t* x0_const, const uint8_t* x0_tmpl, hipStream_t s, hipStream_t s2, hipStream_t s3,
+                     Timeline* tl);
 void launch_build_wide_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s);
 size_t wide_build_scratch_bytes(int nb);
 size_t fbw_words_per_base();
@@ -440,18 +441,43 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   // FTS_SIDE_STREAM=0: run each lane's side work on its main stream
   bool side = true;
   if (const char* e = getenv("FTS_SIDE_STREAM")) side = atoi(e) != 0;
+  // the batch check's stream (s3: RLC weights + MSM, the longest chain of a small
+  // pass) gets the device's highest stream priority, so its few waves are
+  // dispatched ahead of the exact phase's wide fixed-base launches
+  int prio_lo = 0, prio_hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
+  int s3_prio = prio_hi;
+  if (const char* e = getenv("FTS_S3_PRIO")) s3_prio = atoi(e) ? prio_hi : prio_lo;
+  // FTS_RESERVE_CUS=R: the lanes' main streams (the exact phase's wide launches,
+  // e.g. k_rp_fixed_all's two rounds of waves) leave R CUs, spread evenly over
+  // the XCDs, to the side and batch-check streams, whose latency-bound chains
+  // (x*D, RLC weights, MSM) would otherwise queue behind them
+  std::vector<uint32_t> cu_mask;
+  {
+    int reserve = 0;
+    if (const char* e = getenv("FTS_RESERVE_CUS")) reserve = std::max(0, atoi(e));
+    hipDeviceProp_t prop;
+    if (reserve > 0 && hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 2 * reserve) {
+      const int ncu = prop.multiProcessorCount, stride = ncu / reserve;
+      cu_mask.assign((ncu + 31) / 32, 0u);
+      for (int i = 0; i < ncu; i++)
+        if (i % stride != stride - 1 || i / stride >= reserve) cu_mask[i / 32] |= 1u << (i % 32);
+    }
+  }
   for (int i = 0; i < nl; i++) {
     Lane* L = new Lane();
     L->id = i;
     c->lanes.push_back(L);
     c->free_lanes.push_back(i);
-    if (hipStreamCreateWithFlags(&L->s, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
+    if ((cu_mask.empty() ? hipStreamCreateWithFlags(&L->s, hipStreamNonBlocking)
+                         : hipExtStreamCreateWithCUMask(&L->s, (uint32_t)cu_mask.size(), cu_mask.data())) != hipSuccess)
+      return fail(FTS_API_EDEVICE);
     if (hipEventCreateWithFlags(&L->done, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)
       return fail(FTS_API_EDEVICE);
     if (hipHostMalloc((void**)&L->pin, sizeof(Lane::Pinned), 0) != hipSuccess) return fail(FTS_API_ENOMEM);
     if (!side) L->s2 = L->s;
     else if (hipStreamCreateWithFlags(&L->s2, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
-    if (hipStreamCreateWithFlags(&L->s3, hipStreamNonBlocking) != hipSuccess ||
+    if (hipStreamCreateWithPriority(&L->s3, hipStreamNonBlocking, s3_prio) != hipSuccess ||
         hipEventCreateWithFlags(&L->ev_a, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&L->ev_b, hipEventDisableTiming) != hipSuccess)
       return fail(FTS_API_EDEVICE);
@@ -873,9 +899,9 @@ static int rp_buffers(fts_ctx* c, Lane& L, int B) {
       w.hpa.ensure((size_t)B * (n + 1) * 64) || w.hpbe.ensure((size_t)B * (n + 1) * 64) ||
       w.x0.ensure((size_t)B * x0_var_bytes(n)) || w.terms.ensure(rp_terms_words(B, n, k) * 4) ||
       w.scratch.ensure(std::max(rp_scratch_words(B, n, k), (size_t)B * 10 * 24) * 4) || w.r_key.ensure(32) ||
-      w.r_msc.ensure((size_t)N * 32) || w.r_coef.ensure((size_t)B * 5 * 32) || w.r_colsum.ensure((3 + 2 * n) * 32) ||
-      w.r_fixed.ensure((3 + 2 * n) * 96) || w.r_flag.ensure(4) || w.ypow.ensure((size_t)B * n * 32) ||
-      w.svec.ensure((size_t)B * n * 32) || ((size_t)B <= c->com_fixed_max && w.zvec.ensure((size_t)B * n * 32)) ||
+      w.r_msc.ensure((size_t)N * 32) || w.r_coef.ensure((size_t)B * RLC_NCOEF * 32) ||
+      w.r_colsum.ensure(rlc_ncols(n) * 32) || w.r_fixed.ensure(rlc_ncols(n) * 96) || w.r_flag.ensure(4) || w.ypow.ensure((size_t)B * n * 32) ||
+      w.svec.ensure((size_t)B * n * 32) || w.zvec.ensure((size_t)B * n * 32) ||
       !L.status_buf((size_t)B))
     return FTS_API_ENOMEM;
   return FTS_API_OK;
@@ -922,7 +948,7 @@ static int rp_group_fallback(fts_ctx* c, Lane& L, const RpBatchDev& d, const Rlc
   // groups of either round: round 1 has sel.size() / RP_GT1, round 2 at most slots / RP_GT2
   const size_t gmax = std::max(sel.size() / RP_GT1, (slots + RP_GT2 - 1) / RP_GT2);
   if (w.r_sel.ensure(slots * 4) || w.r_next.ensure(slots * 4) || w.r_cnt.ensure(8) ||
-      w.r_gcol.ensure(gmax * (3 + 2 * n) * 32) || w.r_gfix.ensure(gmax * (3 + 2 * n) * 96))
+      w.r_gcol.ensure(gmax * rlc_ncols(n) * 32) || w.r_gfix.ensure(gmax * rlc_ncols(n) * 96))
     return FTS_API_ENOMEM;
   uint8_t* hs = L.stage_buf(sel.size() * 4);
   if (!hs) return FTS_API_ENOMEM;
@@ -968,7 +994,7 @@ static int rp_group_fallback(fts_ctx* c, Lane& L, const RpBatchDev& d, const Rlc
 // `between` (optional) is launched after the RLC check and before the flag
 // sync (the sigma-proof kernels of transfer/issue batches).
 // `groups`: first proof of every caller batch in the pass, then B ({0, B}: one batch)
-// `pre_rlc` (optional): launched on the main stream right before the batch check
+// `pre_rlc` (optional): launched on the batch check's stream (lane s3) right before k_rlc_prep
 template <class F>
 static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc, int32_t* d_status, int32_t* d_ipa,
                        F&& between, const std::vector<int>& groups, void (*pre_rlc)(void*, hipStream_t) = nullptr,
@@ -1015,7 +1041,7 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   HIP_OK(hipMemcpyAsync(r.key, L.pin->key, sizeof L.pin->key, hipMemcpyHostToDevice, L.s));
   const double t_prep = now_ms();
   L.tl.begin(L.s);
-  launch_rp_batch(d, r, c->d_tables, c->d_wtables, c->d_x0const, c->d_x0tmpl, L.s, L.s2, &L.tl);
+  launch_rp_batch(d, r, c->d_tables, c->d_wtables, c->d_x0const, c->d_x0tmpl, L.s, L.s2, L.s3, &L.tl);
   between();
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(&L.pin->flag, r.flag, 4, hipMemcpyDeviceToHost, L.s));
@@ -1784,8 +1810,8 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
   }
   if (rp_total) {
     // the sigma proofs run on the lane's third stream beside the range-proof pass;
-    // right before the batch check the main stream joins them and drops the range
-    // proofs of actions whose sigma proof failed from the check (k_sig_exclude)
+    // the batch check's variable part follows them on that stream and first drops
+    // the range proofs of actions whose sigma proof failed (k_sig_exclude)
     struct Hook {
       const SigBatchDev* sd;
       Lane* L;

@@ -936,10 +936,13 @@ __global__ void __launch_bounds__(64) k_rp_check(int B, int n, int k, const int3
 // ------------------------------------------------------------ RLC batch check
 // Sum_p rho_p E1_p + rho'_p E2_p == O  (SURVEY Appendix B).  Fixed bases get
 // batch-summed scalars (column reduction), variable points go to one MSM.
-// coef per proof (Montgomery Fr): [rho(ip - polEval), rho tau, rho'(ab - ip), rho' a, rho' b]
-// (column Q is rho'(ab - ip) x0: x0 is applied by k_rlc_columns, so the MSM
-// side does not wait for the x0 transcript)
-constexpr int RLC_NCOEF = 5;
+// com never enters as a point: E2's -rho' com is expanded through its
+// definition (bulletproof.go:477-492)
+//   -rho' com = -rho' C - rho' x D - rho' z K + rho' delta P - rho' sum_i z^2 2^i y^-i H_i
+// so the variable points are T1, T2, V, C, D, L_j, R_j (all decoded from the
+// proof) and the K, P, H_i terms join the fixed-base columns.  The check then
+// depends only on the challenges (not on H'_i, com or x0, except column Q =
+// rho'(ab - ip) x0 Q): the MSM runs beside the exact per-proof phase.
 
 // full-width weight: 256 random bits reduced mod r (Montgomery form).  Full
 // width keeps every MSM window's digits uniform (a 128-bit weight would put
@@ -954,13 +957,10 @@ FTS_DEV Fr fr_from_u256(const uint32_t w[8]) {
 __global__ void __launch_bounds__(64) k_rlc_prep(int B, int n, int k, const int32_t* __restrict__ status,
                                                  const int32_t* __restrict__ ipa_flag, const uint32_t* __restrict__ sc,
                                                  const uint32_t* __restrict__ ch, const uint32_t* __restrict__ key,
-                                                 const uint32_t* __restrict__ hpa, uint32_t* __restrict__ pts,
                                                  uint32_t* __restrict__ msc, uint32_t* __restrict__ coef) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const int npts = rp_npts(k);
-  // C is consumed by com: the slot now holds -com for the MSM (scalar rho')
-  if (status[b] == 0) store_g1a(pts + ((size_t)b * npts + RP_PT_C) * 16, g1a_neg(load_g1a(hpa + ((size_t)b * (n + 1) + n) * 16)));
   uint32_t* M = msc + (size_t)b * npts * 8;
   uint32_t* K = coef + (size_t)b * RLC_NCOEF * 8;
   const bool e1 = status[b] == 0;
@@ -989,8 +989,10 @@ __global__ void __launch_bounds__(64) k_rlc_prep(int B, int n, int k, const int3
   store_f(K + 0 * 8, fr_mul(rho, f_sub(ip, pol)));
   store_f(K + 1 * 8, fr_mul(rho, fr_from_canon(S + RP_SC_TAU * 8)));
   if (!e2) return;
-  Fr a = fr_from_canon(S + RP_SC_A * 8), bb = fr_from_canon(S + RP_SC_B * 8);
-  store_f(M + RP_PT_C * 8, f_from_mont(rho2));  // slot C holds -com: scalar +rho' 
+  Fr a = fr_from_canon(S + RP_SC_A * 8), bb = fr_from_canon(S + RP_SC_B * 8), z;
+  load_f(C + CH_Z * 8, z);
+  put(RP_PT_C, rho2);
+  put(RP_PT_D, fr_mul(rho2, x));
   for (int j = 0; j < k; j++) {
     Fr xj, xji;
     load_f(C + (CH_XJ + j) * 8, xj);
@@ -1001,52 +1003,62 @@ __global__ void __launch_bounds__(64) k_rlc_prep(int B, int n, int k, const int3
   store_f(K + 2 * 8, fr_mul(rho2, f_sub(fr_mul(a, bb), ip)));
   store_f(K + 3 * 8, fr_mul(rho2, a));
   store_f(K + 4 * 8, fr_mul(rho2, bb));
+  store_f(K + 5 * 8, rho2);
+  store_f(K + 6 * 8, f_neg(fr_mul(rho2, z)));
+  store_f(K + 7 * 8, fr_mul(rho2, fr_from_canon(S + RP_SC_DELTA * 8)));
 }
 
-// one block per (column, group): col 0 G (ped1), 1 H (ped2), 2 Q, 3+i G_i, 3+n+i H_i
-// (s_i and y^-i come precomputed, i-major, from k_rp_powers).  The batch check
-// has one group of all B proofs; the group test has G groups of gs proof slots
-// (sel[g gs + j], -1 = empty) -> colsum[g][col]
-__global__ void __launch_bounds__(256) k_rlc_columns(int B, int n, int k, int gs, const int32_t* __restrict__ sel,
-                                                     const uint32_t* __restrict__ ch,
+// one block per (column, group), columns col0 + blockIdx.x (layout: rlc_ncols).
+// s_i, y^-i and z^2 2^i y^-i come precomputed, i-major, from k_rp_powers.  The
+// batch check has one group of all B proofs; the group test has G groups of
+// gs proof slots (sel[g gs + j], -1 = empty) -> colsum[g][col]
+__global__ void __launch_bounds__(256) k_rlc_columns(int B, int n, int k, int gs, int col0,
+                                                     const int32_t* __restrict__ sel, const uint32_t* __restrict__ ch,
                                                      const uint32_t* __restrict__ coef, const uint32_t* __restrict__ ypow,
-                                                     const uint32_t* __restrict__ svec, uint32_t* __restrict__ colsum) {
+                                                     const uint32_t* __restrict__ svec,
+                                                     const uint32_t* __restrict__ zvec, uint32_t* __restrict__ colsum) {
   __shared__ uint32_t sh[256 * 8];
-  const int col = blockIdx.x, grp = blockIdx.y, t = threadIdx.x, nt = blockDim.x;  // nt: 64 or 256
+  const int col = col0 + blockIdx.x, grp = blockIdx.y, t = threadIdx.x, nt = blockDim.x;  // nt: 64 or 256
   Fr acc = f_zero<FrP>();
   for (int j = t; j < gs; j += nt) {
     const int b = sel ? sel[(size_t)grp * gs + j] : grp * gs + j;
     if (b < 0 || b >= B) continue;
     const uint32_t* K = coef + (size_t)b * RLC_NCOEF * 8;
     Fr v;
-    if (col < 3) {
+    if (col < 2) {
       load_f(K + col * 8, v);
-      if (col == 2 && !f_is_zero(v)) {
-        Fr x0;
-        load_f(ch + ((size_t)b * rp_nch(k) + CH_X0) * 8, x0);
-        v = fr_mul(v, x0);
-      }
-    } else if (col < 3 + n) {
+    } else if (col < 2 + n) {  // rho' a s_i
       Fr ra;
       load_f(K + 3 * 8, ra);
       if (!f_is_zero(ra)) {
         Fr sv;
-        load_f(svec + ((size_t)(col - 3) * B + b) * 8, sv);
+        load_f(svec + ((size_t)(col - 2) * B + b) * 8, sv);
         v = fr_mul(ra, sv);
       } else {
         v = ra;
       }
-    } else {
-      const int i = col - 3 - n;
-      Fr rb;
-      load_f(K + 4 * 8, rb);
-      if (!f_is_zero(rb)) {
-        Fr sv, yp;
+    } else if (col < 2 + 2 * n) {  // rho' b s_i^-1 y^-i - rho' z^2 2^i y^-i
+      const int i = col - 2 - n;
+      Fr r2;
+      load_f(K + 5 * 8, r2);
+      if (!f_is_zero(r2)) {
+        Fr rb, sv, yp, zv;
+        load_f(K + 4 * 8, rb);
         load_f(svec + ((size_t)(n - 1 - i) * B + b) * 8, sv);
         load_f(ypow + ((size_t)i * B + b) * 8, yp);
-        v = fr_mul(fr_mul(rb, sv), yp);
+        load_f(zvec + ((size_t)i * B + b) * 8, zv);
+        v = f_sub(fr_mul(fr_mul(rb, sv), yp), fr_mul(r2, zv));
       } else {
-        v = rb;
+        v = r2;
+      }
+    } else if (col < 2 * n + 4) {  // -rho' z (K), rho' delta (P)
+      load_f(K + (col - 2 * n + 4) * 8, v);
+    } else {  // rho'(ab - ip) x0 (Q)
+      load_f(K + 2 * 8, v);
+      if (!f_is_zero(v)) {
+        Fr x0;
+        load_f(ch + ((size_t)b * rp_nch(k) + CH_X0) * 8, x0);
+        v = fr_mul(v, x0);
       }
     }
     acc = f_add(acc, v);
@@ -1062,33 +1074,60 @@ __global__ void __launch_bounds__(256) k_rlc_columns(int B, int n, int k, int gs
     }
     __syncthreads();
   }
-  if (t == 0) store_f(colsum + ((size_t)grp * (3 + 2 * n) + col) * 8, f_from_mont(acc));
+  if (t == 0) store_f(colsum + ((size_t)grp * rlc_ncols(n) + col) * 8, f_from_mont(acc));
 }
 
-// lane per (group, column): the fixed-base product of the column sum
-__global__ void __launch_bounds__(64) k_rlc_fixed(int n, int G, const uint32_t* __restrict__ colsum,
-                                                  const uint32_t* __restrict__ tables, uint32_t* __restrict__ out) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (3 + 2 * n) * G) return;
-  const int col = gid % (3 + 2 * n);
-  colsum += (size_t)(gid / (3 + 2 * n)) * (3 + 2 * n) * 8;
-  out += (size_t)(gid / (3 + 2 * n)) * (3 + 2 * n) * 24;
-  int base = col == 0 ? tb_G(n) : col == 1 ? tb_H(n) : col == 2 ? tb_Q(n) : col - 3;
-  Scalar s;
+FTS_DEV int rlc_col_base(int n, int col) {
+  return col == 0 ? tb_G(n) : col == 1 ? tb_H(n) : col < 2 * n + 2 ? col - 2 : col == 2 * n + 2 ? tb_K(n)
+         : col == 2 * n + 3 ? tb_P(n) : tb_Q(n);
+}
+
+// fixed-base product of each column sum, FB_NW lanes per (group, column):
+// lane w looks up its window's entry, then an LDS tree of log2(FB_NW) full
+// additions (latency: 4 additions instead of a chain of 16)
+constexpr int RF_ITEMS = 16;
+static_assert(FB_NW == 16, "one lane per 16-bit window");
+__global__ void __launch_bounds__(RF_ITEMS * FB_NW) k_rlc_fixed(int n, int G, int col0, int ncl,
+                                                               const uint32_t* __restrict__ colsum,
+                                                               const uint32_t* __restrict__ tables,
+                                                               uint32_t* __restrict__ out) {
+  __shared__ uint32_t sh[RF_ITEMS * FB_NW * 24];
+  const int w = threadIdx.x % FB_NW, it = blockIdx.x * RF_ITEMS + threadIdx.x / FB_NW;
+  const bool live = it < G * ncl;
+  const int NC = rlc_ncols(n), grp = live ? it / ncl : 0, col = col0 + (live ? it % ncl : 0);
+  G1J acc = g1j_identity();
+  if (live) {
+    uint32_t s[8];
 #pragma unroll
-  for (int q = 0; q < 8; q++) s.v[q] = colsum[col * 8 + q];
-  store_g1j(out + (size_t)col * 24, nl_fb_mul(tables + (size_t)base * FB_WORDS_PER_BASE, s));
+    for (int q = 0; q < 8; q++) s[q] = colsum[((size_t)grp * NC + col) * 8 + q];
+    int carry = 0, d = 0;
+    for (int q = 0; q <= w; q++) d = fb_next_digit(s, carry);
+    if (d != 0)
+      acc = g1j_from_affine(fb_entry(tables + (size_t)rlc_col_base(n, col) * FB_WORDS_PER_BASE, w, d));
+  }
+  uint32_t* S = sh + (size_t)(threadIdx.x - w) * 24;
+  store_g1j(S + w * 24, acc);
+  __syncthreads();
+  for (int half = FB_NW / 2; half >= 1; half >>= 1) {
+    if (live && w < half) add_inl(acc, load_g1j(S + (w + half) * 24));
+    __syncthreads();
+    if (live && w < half) store_g1j(S + w * 24, acc);
+    __syncthreads();
+  }
+  if (live && w == 0) store_g1j(out + ((size_t)grp * NC + col) * 24, acc);
 }
 
 // batch verdict: flag = 1 if the combination is the identity; on success the
 // deferred IPA structural verdicts become final (their E1 held)
+// (msm_out + addend: the Q column's product, computed after x0)
 __global__ void __launch_bounds__(64) k_rlc_finalize(int B, const uint32_t* __restrict__ msm_out,
+                                                     const uint32_t* __restrict__ addend,
                                                      int32_t* __restrict__ status, const int32_t* __restrict__ ipa_flag,
                                                      int32_t* __restrict__ flag) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
-  Fp z;
-  load_fp(msm_out + 16, z);
-  const bool pass = f_is_zero(z);
+  G1J e = load_g1j(msm_out);
+  add_inl(e, load_g1j(addend));
+  const bool pass = g1j_is_identity(e);
   if (b == 0) *flag = pass ? 1 : 0;
   if (b < B && pass && status[b] == 0 && ipa_flag[b] != 0) status[b] = ipa_flag[b];
 }
@@ -1169,10 +1208,13 @@ void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalar
 // Whole range-proof pipeline up to the batch verdict (flag): exact per-proof
 // phase (everything that is hashed: challenges, H'_i, com, x0) and the
 // random-linear-combination check of all final equations (one MSM).
-// s = main stream, s2 = side stream.
+// s = main stream (exact phase, then the x0-dependent tail), s2 = x*D beside
+// the fixed-base products (latency path), s3 = the batch check's variable part
+// (weights, x0-free columns, MSM), which needs only the challenges.
 void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const uint32_t* wtables,
-                     const uint8_t* x0_const, const uint8_t* x0_tmpl, hipStream_t s, hipStream_t s2, Timeline* tl) {
-  const int B = d.B, n = d.n, k = d.k;
+                     const uint8_t* x0_const, const uint8_t* x0_tmpl, hipStream_t s, hipStream_t s2, hipStream_t s3,
+                     Timeline* tl) {
+  const int B = d.B, n = d.n, k = d.k, NC = rlc_ncols(n);
   if (!B) return;
   FTS_LAUNCH(k_rp_decode, B * rp_npts(k), 256, s, B, rp_npts(k), d.raw, d.pts, d.status);
   tl->mark("k_rp_decode", s, 0);
@@ -1188,9 +1230,22 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   }
   FTS_LAUNCH(k_rp_chal_fr, B, 64, s, B, n, k, d.status, d.ch, d.scratch);
   tl->mark("k_rp_chal_fr", s, (double)B * (3 * k + 4 * (k + 1) + 12));
+  FTS_LAUNCH(k_rp_powers, B * (n >> std::min(PW_LC, k)), 64, s, B, n, k, d.status, d.ch, d.ypow, d.svec, d.zvec);
+  tl->mark("k_rp_powers", s, (double)B * (3.0 * n + 2.0 * k));
+  // batch check, x0-free part, on s3 (after the caller's hook, e.g. the exclusion
+  // of range proofs whose action failed its sigma proof)
+  tl->fork(s, s3);
+  if (d.pre_rlc) d.pre_rlc(d.pre_rlc_arg, s3);
+  FTS_LAUNCH(k_rlc_prep, B, 64, s3, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, r.key, r.msc, r.coef);
+  tl->mark("k_rlc_prep", s3, (double)B * (3 * k + 33));
+  hipLaunchKernelGGL(k_rlc_columns, dim3(NC - 1, 1), dim3(256), 0, s3, B, n, k, B, 0, (const int32_t*)nullptr, d.ch,
+                     r.coef, d.ypow, d.svec, d.zvec, r.colsum);
+  tl->mark("k_rlc_columns", s3, (double)B * 4 * n);
+  FTS_LAUNCH(k_rlc_fixed, (size_t)(NC - 1) * FB_NW, RF_ITEMS * FB_NW, s3, n, 1, 0, NC - 1, r.colsum, tables, r.fixed);
+  tl->mark("k_rlc_fixed", s3, (double)(NC - 1) * (FB_NW * 3 + (FB_NW - 1) * COST_ADD));
+  launch_msm(r.plan, d.pts, r.msc, r.fixed, NC - 1, r.msm_scratch, s3, s3, tl);
+  // exact per-proof phase on s
   if (d.com_fixed) {
-    FTS_LAUNCH(k_rp_powers, B * (n >> std::min(PW_LC, k)), 64, s, B, n, k, d.status, d.ch, d.ypow, d.svec, d.zvec);
-    tl->mark("k_rp_powers", s, (double)B * (3.0 * n + 2.0 * k));
     FTS_LAUNCH(k_rp_fixed_all, (size_t)B * (2 * n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, d.zvec, wtables,
                d.hpj, d.terms);
     tl->mark("k_rp_fixed_all", s, (double)B * (2.0 * n + 2.0) * COST_FBW_FRESH);
@@ -1202,9 +1257,6 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
                        k, d.status, d.pts, d.terms, d.hpj);
     tl->mark("k_rp_com_sum", s, (double)B * (com_fx_slots(n) + 1) * COST_ADD);
   } else {
-    FTS_LAUNCH(k_rp_powers, B * (n >> std::min(PW_LC, k)), 64, s, B, n, k, d.status, d.ch, d.ypow, d.svec,
-               (uint32_t*)nullptr);
-    tl->mark("k_rp_powers", s, (double)B * (2.0 * n + 2.0 * k));
     FTS_LAUNCH(k_rp_fixed_exact, B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, wtables, d.hpj, d.terms);
     tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FBW_FRESH);
     // H'_i -> affine + BE bytes (x0 transcript) now; com is normalised after com_sum
@@ -1225,25 +1277,18 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   }
   FTS_LAUNCH(k_rp_normalize, (B + NORM_E - 1) / NORM_E, NORM_BS, s, B, 1, n + 1, n, d.status, d.hpj, d.hpa, d.hp_be);
   tl->mark("k_rp_normalize_com", s, (double)B * (2.0 * 8.0 / NORM_E + 9.0));
-  // side: x0 transcript + hash, then the fixed-base columns (need x0)
-  tl->fork(s, s2);
-  hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s2, B, n, d.status, d.hp_be, x0_const, d.sc,
+  hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s, B, n, d.status, d.hp_be, x0_const, d.sc,
                      d.x0_msgs);
-  tl->mark("k_rp_x0_build", s2, 0);
-  FTS_LAUNCH(k_rp_x0_hash, B, 64, s2, B, n, k, d.status, d.x0_msgs, x0_tmpl, d.ch);
-  tl->mark("k_rp_x0_hash", s2, 0);
-  // main: variable points of the batch equation -> MSM (after the caller's hook, e.g. the
-  // exclusion of range proofs whose action failed its sigma proof)
-  if (d.pre_rlc) d.pre_rlc(d.pre_rlc_arg, s);
-  FTS_LAUNCH(k_rlc_prep, B, 64, s, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, r.key, d.hpa, d.pts, r.msc, r.coef);
-  tl->mark("k_rlc_prep", s, (double)B * (3 * k + 30));
-  hipLaunchKernelGGL(k_rlc_columns, dim3(3 + 2 * n, 1), dim3(256), 0, s2, B, n, k, B, (const int32_t*)nullptr, d.ch,
-                     r.coef, d.ypow, d.svec, r.colsum);
-  tl->mark("k_rlc_columns", s2, (double)B * 3 * n);
-  FTS_LAUNCH(k_rlc_fixed, 3 + 2 * n, 64, s2, n, 1, r.colsum, tables, r.fixed);
-  tl->mark("k_rlc_fixed", s2, (double)(3 + 2 * n) * COST_FB_FRESH);
-  launch_msm(r.plan, d.pts, r.msc, r.fixed, 3 + 2 * n, r.msm_scratch, s, s2, tl);
-  FTS_LAUNCH(k_rlc_finalize, B, 64, s, B, r.plan.out, d.status, d.ipa_flag, r.flag);
+  tl->mark("k_rp_x0_build", s, 0);
+  FTS_LAUNCH(k_rp_x0_hash, B, 64, s, B, n, k, d.status, d.x0_msgs, x0_tmpl, d.ch);
+  tl->mark("k_rp_x0_hash", s, 0);
+  // x0 tail: column Q and its product, then the verdict once the MSM is in
+  hipLaunchKernelGGL(k_rlc_columns, dim3(1, 1), dim3(256), 0, s, B, n, k, B, NC - 1, (const int32_t*)nullptr, d.ch,
+                     r.coef, d.ypow, d.svec, d.zvec, r.colsum);
+  FTS_LAUNCH(k_rlc_fixed, FB_NW, RF_ITEMS * FB_NW, s, n, 1, NC - 1, 1, r.colsum, tables, r.fixed);
+  tl->mark("k_rlc_q", s, (double)B + FB_NW * 3 + (FB_NW - 1) * COST_ADD);
+  tl->fork(s3, s);
+  FTS_LAUNCH(k_rlc_finalize, B, 64, s, B, r.plan.out, r.fixed + (size_t)(NC - 1) * 24, d.status, d.ipa_flag, r.flag);
   tl->mark("k_rlc_finalize", s, 0);
 }
 
@@ -1281,12 +1326,13 @@ void launch_rlc_group_test(const RpBatchDev& d, const RlcDev& r, const uint32_t*
                            const int32_t* sel, int G, int gs, uint32_t* gcol, uint32_t* gfix, int32_t* next,
                            uint32_t* next_count, hipStream_t s, Timeline* tl) {
   const int n = d.n, k = d.k;
-  hipLaunchKernelGGL(k_rlc_columns, dim3(3 + 2 * n, G), dim3(gs <= 64 ? 64 : 256), 0, s, d.B, n, k, gs, sel, d.ch,
-                     r.coef, d.ypow, d.svec, gcol);
-  tl->mark("k_rlc_group_columns", s, (double)G * gs * 3 * n);
-  FTS_LAUNCH(k_rlc_fixed, (size_t)(3 + 2 * n) * G, 64, s, n, G, gcol, tables, gfix);
-  tl->mark("k_rlc_group_fixed", s, (double)G * (3 + 2 * n) * COST_FB_FRESH);
-  launch_msm(p, d.pts, r.msc, gfix, 3 + 2 * n, r.msm_scratch, s, s, tl);
+  const int NC = rlc_ncols(n);
+  hipLaunchKernelGGL(k_rlc_columns, dim3(NC, G), dim3(gs <= 64 ? 64 : 256), 0, s, d.B, n, k, gs, 0, sel, d.ch,
+                     r.coef, d.ypow, d.svec, d.zvec, gcol);
+  tl->mark("k_rlc_group_columns", s, (double)G * gs * 4 * n);
+  FTS_LAUNCH(k_rlc_fixed, (size_t)NC * G * FB_NW, RF_ITEMS * FB_NW, s, n, G, 0, NC, gcol, tables, gfix);
+  tl->mark("k_rlc_group_fixed", s, (double)G * NC * (FB_NW * 3 + (FB_NW - 1) * COST_ADD));
+  launch_msm(p, d.pts, r.msc, gfix, NC, r.msm_scratch, s, s, tl);
   FTS_LAUNCH(k_rlc_group_final, (size_t)G * gs, 256, s, G * gs, gs, sel, p.out, d.status, d.ipa_flag, next,
              next_count);
   tl->mark("k_rlc_group_final", s, 0);

@@ -1,6 +1,6 @@
 set -o pipefail
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
-tail -3 gpurun_out/pytest_gpu.log
-TAG=default timeout -k 10 200 python3 tools/pass_times.py 4096 32768 || exit 1
+mkdir -p gpurun_out/tr
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tr -o tr -- python3 tools/pass_times.py 4096 > gpurun_out/tr.log 2>&1 || { tail -20 gpurun_out/tr.log; exit 1; }
+f=$(find gpurun_out/tr -name '*kernel_trace.csv' | head -1)
+python3 tools/trace_pass.py $f
