@@ -174,6 +174,7 @@ struct RpBatchDev {
   void* pre_rlc_arg;
   int com_fixed;       // 1: com by fixed-base groups + x*D on the side stream (latency path,
                        //    small passes); 0: Horner sum + joint GLV/Straus chains (work path)
+  int rlc_fork = 1;    // batch check's stream forks after the fixed-base products (1) or after the challenges (0)
 };
 
 }  // namespace fts

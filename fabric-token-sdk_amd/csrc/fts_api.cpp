@@ -306,6 +306,7 @@ struct fts_ctx {
   // groups, rp_kernels.hip k_rp_fixed_all), larger ones on the work path (Horner +
   // joint GLV chains): the same group element either way
   size_t com_fixed_max = 16384;
+  int rlc_fork = 1;                 // FTS_RLC_FORK: batch check forks after the fixed-base products (1) or the challenges (0)
   // a lane was freed (call with mu held): the head pending range-proof request
   // becomes the next leader; LaneGuard waiters re-check too
   void wake_lane_waiters() {
@@ -438,6 +439,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   c->gather_target = c->coalesce_max / 2;
   if (const char* e = getenv("FTS_GATHER_US")) c->gather_us = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_COM_FIXED_MAX")) c->com_fixed_max = (size_t)std::max(0L, atol(e));
+  if (const char* e = getenv("FTS_RLC_FORK")) c->rlc_fork = atoi(e) != 0;
   // FTS_SIDE_STREAM=0: run each lane's side work on its main stream
   bool side = true;
   if (const char* e = getenv("FTS_SIDE_STREAM")) side = atoi(e) != 0;
@@ -1034,6 +1036,7 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
                (size_t)B <= c->com_fixed_max ? 1 : 0};
   d.pre_rlc = pre_rlc;
   d.pre_rlc_arg = pre_rlc_arg;
+  d.rlc_fork = c->rlc_fork;
   RlcDev r{w.r_key.as<uint32_t>(), w.r_msc.as<uint32_t>(),   w.r_coef.as<uint32_t>(), w.r_colsum.as<uint32_t>(),
            w.r_fixed.as<uint32_t>(), w.r_flag.as<int32_t>(), w.m_scratch.as<uint32_t>(), mp};
   // fresh RLC weights key (getrandom), unpredictable to the provers

@@ -1233,22 +1233,29 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   FTS_LAUNCH(k_rp_powers, B * (n >> std::min(PW_LC, k)), 64, s, B, n, k, d.status, d.ch, d.ypow, d.svec, d.zvec);
   tl->mark("k_rp_powers", s, (double)B * (3.0 * n + 2.0 * k));
   // batch check, x0-free part, on s3 (after the caller's hook, e.g. the exclusion
-  // of range proofs whose action failed its sigma proof)
-  tl->fork(s, s3);
-  if (d.pre_rlc) d.pre_rlc(d.pre_rlc_arg, s3);
-  FTS_LAUNCH(k_rlc_prep, B, 64, s3, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, r.key, r.msc, r.coef);
-  tl->mark("k_rlc_prep", s3, (double)B * (3 * k + 33));
-  hipLaunchKernelGGL(k_rlc_columns, dim3(NC - 1, 1), dim3(256), 0, s3, B, n, k, B, 0, (const int32_t*)nullptr, d.ch,
-                     r.coef, d.ypow, d.svec, d.zvec, r.colsum);
-  tl->mark("k_rlc_columns", s3, (double)B * 4 * n);
-  FTS_LAUNCH(k_rlc_fixed, (size_t)(NC - 1) * FB_NW, RF_ITEMS * FB_NW, s3, n, 1, 0, NC - 1, r.colsum, tables, r.fixed);
-  tl->mark("k_rlc_fixed", s3, (double)(NC - 1) * (FB_NW * 3 + (FB_NW - 1) * COST_ADD));
-  launch_msm(r.plan, d.pts, r.msc, r.fixed, NC - 1, r.msm_scratch, s3, s3, tl);
+  // of range proofs whose action failed its sigma proof).  Forked after the
+  // exact phase's widest launch (d.rlc_fork = 1, default) so the check's
+  // latency-bound chain does not share SIMDs with it, or right after the
+  // challenges (0).
+  auto rlc_side = [&]() {
+    tl->fork(s, s3);
+    if (d.pre_rlc) d.pre_rlc(d.pre_rlc_arg, s3);
+    FTS_LAUNCH(k_rlc_prep, B, 64, s3, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, r.key, r.msc, r.coef);
+    tl->mark("k_rlc_prep", s3, (double)B * (3 * k + 33));
+    hipLaunchKernelGGL(k_rlc_columns, dim3(NC - 1, 1), dim3(256), 0, s3, B, n, k, B, 0, (const int32_t*)nullptr, d.ch,
+                       r.coef, d.ypow, d.svec, d.zvec, r.colsum);
+    tl->mark("k_rlc_columns", s3, (double)B * 4 * n);
+    FTS_LAUNCH(k_rlc_fixed, (size_t)(NC - 1) * FB_NW, RF_ITEMS * FB_NW, s3, n, 1, 0, NC - 1, r.colsum, tables, r.fixed);
+    tl->mark("k_rlc_fixed", s3, (double)(NC - 1) * (FB_NW * 3 + (FB_NW - 1) * COST_ADD));
+    launch_msm(r.plan, d.pts, r.msc, r.fixed, NC - 1, r.msm_scratch, s3, s3, tl);
+  };
+  if (!d.rlc_fork) rlc_side();
   // exact per-proof phase on s
   if (d.com_fixed) {
     FTS_LAUNCH(k_rp_fixed_all, (size_t)B * (2 * n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, d.zvec, wtables,
                d.hpj, d.terms);
     tl->mark("k_rp_fixed_all", s, (double)B * (2.0 * n + 2.0) * COST_FBW_FRESH);
+    if (d.rlc_fork) rlc_side();
     FTS_LAUNCH(k_rp_normalize, (nhp + NORM_E - 1) / NORM_E, NORM_BS, s, nhp, n, n + 1, 0, d.status, d.hpj, d.hpa,
                d.hp_be);
     tl->mark("k_rp_normalize", s, (double)nhp * (2.0 * 8.0 / NORM_E + 9.0));
@@ -1259,6 +1266,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   } else {
     FTS_LAUNCH(k_rp_fixed_exact, B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, wtables, d.hpj, d.terms);
     tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FBW_FRESH);
+    if (d.rlc_fork) rlc_side();
     // H'_i -> affine + BE bytes (x0 transcript) now; com is normalised after com_sum
     FTS_LAUNCH(k_rp_normalize, (nhp + NORM_E - 1) / NORM_E, NORM_BS, s, nhp, n, n + 1, 0, d.status, d.hpj, d.hpa,
                d.hp_be);

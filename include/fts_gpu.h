@@ -27,8 +27,9 @@
  * Return values: every function returns FTS_API_OK (0) or a negative
  * FTS_API_* code for API/driver errors (bad argument, HIP failure).
  * Per-item verdicts go to caller-owned int32 arrays as fts_status values.
- * Thread safety: a context runs up to FTS_LANES (default 8) calls concurrently,
- * each on its own pair of HIP streams and workspace; further callers wait.
+ * Thread safety: a context runs up to FTS_LANES (default 5) calls concurrently,
+ * each on its own HIP streams (main, side, batch check) and workspace; further
+ * callers wait (range-proof batches are coalesced into the next free lane's pass).
  */
 #ifndef FTS_GPU_H
 #define FTS_GPU_H
