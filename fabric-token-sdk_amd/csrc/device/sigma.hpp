@@ -32,6 +32,11 @@ constexpr int SIG_VTAB_WORDS = 16 * 24;
 inline __host__ __device__ size_t sig_scratch_words(size_t nwork) { return nwork * (SIG_VTAB_WORDS + 24); }
 
 inline __host__ __device__ int sig_nterms(int kind, int n_in) { return kind == SIG_TAS ? 2 * n_in + 4 : 2; }
+// term t is a variable-base (GLV) product (k_sig_terms); the others are fixed-base
+inline __host__ __device__ bool sig_term_var(int kind, int n_in, int t) {
+  return kind == SIG_TAS ? (t < 2 * n_in ? (t & 1) != 0 : (t == 2 * n_in + 1 || t == 2 * n_in + 3)) : t != 0;
+}
+inline __host__ __device__ int sig_nfixed(int kind, int n_in) { return kind == SIG_TAS ? n_in + 2 : 1; }
 inline __host__ __device__ int sig_nscalars(int kind, int n_in) { return kind == SIG_TAS ? 4 + 2 * n_in : 3; }
 // transcript points: TAS inComs(n_in), typeCom, sumCom, in'(n_in), out'(n_out), CT, sum ; ST CT, com
 inline __host__ __device__ int sig_ntranscript(int kind, int n_in, int n_out) {

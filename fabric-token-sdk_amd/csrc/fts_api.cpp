@@ -57,7 +57,8 @@ void launch_msm_load(int N, const uint8_t* raw_pts, const uint8_t* raw_sc, uint3
 void launch_msm_to_bytes(const uint32_t* jac, uint8_t* out, hipStream_t s);
 void launch_sig_prep(const SigBatchDev& d, hipStream_t s);
 void launch_sig_finish(const SigBatchDev& d, const uint32_t* tables, int n, hipStream_t s);
-void launch_sig_exclude(const SigBatchDev& d, int32_t* rp_status, hipStream_t s);
+extern int g_lat_bs;
+void launch_sig_exclude(const SigBatchDev& d, int32_t* rp_excl, hipStream_t s);
 size_t table_build_scratch_bytes(int nb);
 size_t fb_words_per_base();
 // prove_kernels.hip
@@ -126,7 +127,7 @@ struct DBuf {
 };
 
 struct Workspace {
-  DBuf pts, ch, small, hpj, hpa, hpbe, x0, terms, scratch, ypow, svec, zvec;
+  DBuf pts, ch, small, hpj, hpa, hpbe, x0, terms, scratch, ypow, svec, zvec, rp_excl;
   // random-linear-combination check + MSM
   DBuf r_key, r_msc, r_coef, r_colsum, r_fixed, r_flag, r_gcol, r_gfix, r_sel, r_next, r_cnt, m_keys, m_counts, m_offsets, m_cursor, m_sorted, m_buckets,
       m_segs, m_wins, m_out, m_scratch, m_win, m_choff, m_chbkt, m_partials;
@@ -137,7 +138,7 @@ struct Workspace {
   DBuf pv;        // batched prover: one arena (prove_arena)
   DBuf sp;        // sigma provers: one arena
   void release() {
-    for (DBuf* b : {&open_rec, &pv, &sp, &pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &terms, &scratch, &ypow, &svec, &zvec, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
+    for (DBuf* b : {&open_rec, &pv, &sp, &pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &terms, &scratch, &ypow, &svec, &zvec, &rp_excl, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
                     &rp_status, &rp_ipa, &s_act, &s_raw, &s_owner, &s_pts, &s_sc, &s_status, &s_work, &s_terms, &s_aff,
                     &s_affoff, &s_msgs, &s_jac, &s_scratch, &r_key, &r_msc, &r_coef, &r_colsum, &r_fixed, &r_flag, &r_gcol, &r_gfix,
                     &r_sel, &r_next, &r_cnt,
@@ -169,7 +170,7 @@ struct Lane {
   bool presized = false;  // workspace sized for the context's largest coalesced pass
   hipStream_t s = nullptr, s2 = nullptr;
   hipStream_t s3 = nullptr;         // sigma proofs of action batches (beside the range-proof pass)
-  hipEvent_t ev_a = nullptr, ev_b = nullptr;  // cross-stream ordering (no timing)
+  hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr;  // cross-stream ordering (no timing)
   Workspace ws;
   Timeline tl;
   float host_prep_ms = 0, host_enqueue_ms = 0, host_wait_ms = 0;  // host wall time of the last run
@@ -420,6 +421,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
       if (L->s3) hipStreamDestroy(L->s3);
       if (L->ev_a) hipEventDestroy(L->ev_a);
       if (L->ev_b) hipEventDestroy(L->ev_b);
+      if (L->ev_c) hipEventDestroy(L->ev_c);
       if (L->s2 && L->s2 != L->s) hipStreamDestroy(L->s2);
       if (L->s) hipStreamDestroy(L->s);
       L->tl.destroy();
@@ -440,6 +442,10 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_GATHER_US")) c->gather_us = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_COM_FIXED_MAX")) c->com_fixed_max = (size_t)std::max(0L, atol(e));
   if (const char* e = getenv("FTS_RLC_FORK")) c->rlc_fork = atoi(e) != 0;
+  if (const char* e = getenv("FTS_LAT_BS")) {  // block size of the latency-bound kernels (64, 128 or 256)
+    const int v = atoi(e);
+    g_lat_bs = v <= 64 ? 64 : v <= 128 ? 128 : 256;
+  }
   // FTS_SIDE_STREAM=0: run each lane's side work on its main stream
   bool side = true;
   if (const char* e = getenv("FTS_SIDE_STREAM")) side = atoi(e) != 0;
@@ -481,7 +487,8 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
     else if (hipStreamCreateWithFlags(&L->s2, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
     if (hipStreamCreateWithPriority(&L->s3, hipStreamNonBlocking, s3_prio) != hipSuccess ||
         hipEventCreateWithFlags(&L->ev_a, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&L->ev_b, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&L->ev_b, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&L->ev_c, hipEventDisableTiming) != hipSuccess)
       return fail(FTS_API_EDEVICE);
     L->tl.create();
   }
@@ -716,6 +723,7 @@ void fts_ctx_destroy(fts_ctx* c) {
     if (L->s3) hipStreamDestroy(L->s3);
     if (L->ev_a) hipEventDestroy(L->ev_a);
     if (L->ev_b) hipEventDestroy(L->ev_b);
+    if (L->ev_c) hipEventDestroy(L->ev_c);
     L->tl.destroy();
     if (L->done) hipEventDestroy(L->done);
     if (L->s2 && L->s2 != L->s) hipStreamDestroy(L->s2);
@@ -903,7 +911,7 @@ static int rp_buffers(fts_ctx* c, Lane& L, int B) {
       w.scratch.ensure(std::max(rp_scratch_words(B, n, k), (size_t)B * 10 * 24) * 4) || w.r_key.ensure(32) ||
       w.r_msc.ensure((size_t)N * 32) || w.r_coef.ensure((size_t)B * RLC_NCOEF * 32) ||
       w.r_colsum.ensure(rlc_ncols(n) * 32) || w.r_fixed.ensure(rlc_ncols(n) * 96) || w.r_flag.ensure(4) || w.ypow.ensure((size_t)B * n * 32) ||
-      w.svec.ensure((size_t)B * n * 32) || w.zvec.ensure((size_t)B * n * 32) ||
+      w.svec.ensure((size_t)B * n * 32) || w.zvec.ensure((size_t)B * n * 32) || w.rp_excl.ensure((size_t)B * 4) ||
       !L.status_buf((size_t)B))
     return FTS_API_ENOMEM;
   return FTS_API_OK;
@@ -1037,6 +1045,8 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   d.pre_rlc = pre_rlc;
   d.pre_rlc_arg = pre_rlc_arg;
   d.rlc_fork = c->rlc_fork;
+  d.ev_coef = L.ev_c;
+  d.excl = pre_rlc ? w.rp_excl.as<int32_t>() : nullptr;
   RlcDev r{w.r_key.as<uint32_t>(), w.r_msc.as<uint32_t>(),   w.r_coef.as<uint32_t>(), w.r_colsum.as<uint32_t>(),
            w.r_fixed.as<uint32_t>(), w.r_flag.as<int32_t>(), w.m_scratch.as<uint32_t>(), mp};
   // fresh RLC weights key (getrandom), unpredictable to the provers
@@ -1677,10 +1687,11 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
   struct Off {
     int sig = -1;               // index in the device sigma batch
     size_t scw = 0;             // word offset in s_sc
+    int fx = 0, vr = 0;         // first fixed-base / variable-base work item
   };
   std::vector<Off> off(A);
   std::vector<SigAction> sact;
-  int term_off = 0, aff_off = 0, pt_off = 0, sc_off = 0, rp_total = 0;
+  int term_off = 0, aff_off = 0, pt_off = 0, sc_off = 0, rp_total = 0, nfix_total = 0;
   size_t scw_total = 0;
   uint32_t msg_off = 0;
   std::vector<int> sig_of(A, -1);
@@ -1706,6 +1717,9 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
     sa.chal_canonical = p.chal_canonical;
     off[i].sig = (int)sact.size();
     off[i].scw = scw_total;
+    off[i].fx = nfix_total;
+    off[i].vr = term_off - nfix_total;
+    nfix_total += sig_nfixed(sa.kind, sa.n_in);
     scw_total += p.sig_sc.size();
     pt_off += 1 + sa.n_in + sa.n_out;
     sc_off += sig_nscalars(sa.kind, sa.n_in);
@@ -1742,8 +1756,11 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
     int32_t* own = (int32_t*)(hs + o_owner) + sa.pt_off;
     for (int q = 0; q < npt; q++) own[q] = g;
     if (!p.sig_sc.empty()) memcpy(hs + o_sc + off[i].scw * 4, p.sig_sc.data(), p.sig_sc.size() * 4);
-    int2* wk = (int2*)(hs + o_work) + sa.term_off;
-    for (int t = 0, nt = sig_nterms(sa.kind, sa.n_in); t < nt; t++) wk[t] = make_int2(g, t);
+    // work list: every fixed-base term first, then every variable-base (GLV) term,
+    // so no wave of k_sig_terms runs both kinds of product
+    int2* wk = (int2*)(hs + o_work);
+    for (int t = 0, nt = sig_nterms(sa.kind, sa.n_in), fi = off[i].fx, vi = nfix_total + off[i].vr; t < nt; t++)
+      wk[sig_term_var(sa.kind, sa.n_in, t) ? vi++ : fi++] = make_int2(g, t);
     ((int32_t*)(hs + o_affoff))[g] = 0;
     if (s.rp_base >= 0) {
       const size_t rb = (size_t)s.rp_base, rc = (size_t)s.rp_count;
@@ -1818,8 +1835,7 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
     struct Hook {
       const SigBatchDev* sd;
       Lane* L;
-      int32_t* rp_status;
-    } hook{&sd, &L, w.rp_status.as<int32_t>()};
+    } hook{&sd, &L};
     void (*pre)(void*, hipStream_t) = nullptr;
     if (SA) {
       HIP_OK(hipEventRecord(L.ev_a, L.s));
@@ -1829,7 +1845,8 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
       pre = [](void* arg, hipStream_t s) {
         Hook* h = static_cast<Hook*>(arg);
         (void)hipStreamWaitEvent(s, h->L->ev_b, 0);
-        launch_sig_exclude(*h->sd, h->rp_status, s);
+        // the mask is read at launch time: rp_pipeline sizes (and may re-allocate) it
+        launch_sig_exclude(*h->sd, h->L->ws.rp_excl.as<int32_t>(), s);
       };
     }
     int rc = rp_pipeline(c, L, rp_total, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),

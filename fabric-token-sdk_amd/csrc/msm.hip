@@ -11,8 +11,11 @@
 #include "device/helpers.hpp"
 #include "device/msm.hpp"
 #include "device/rp_kernels.hpp"
+#include "device/coop.hpp"
 
 namespace fts {
+extern int g_lat_bs;  // rp_kernels.hip
+
 
 // bits [off, off+width) of a 128-bit LE magnitude (width <= 20)
 FTS_DEV uint32_t scalar_bits4(const uint32_t s[4], int off, int width) {
@@ -234,7 +237,7 @@ __global__ void __launch_bounds__(64, 4) k_msm_chunks(MsmIdx p, const uint32_t* 
 }
 
 // one lane per bucket: sum of its chunk partials (usually 1..4)
-__global__ void __launch_bounds__(64) k_msm_bucket_sum(int NB, const uint32_t* __restrict__ counts,
+__global__ void __launch_bounds__(256) k_msm_bucket_sum(int NB, const uint32_t* __restrict__ counts,
                                                        const uint32_t* __restrict__ chunk_off,
                                                        const uint32_t* __restrict__ partials,
                                                        uint32_t* __restrict__ buckets) {
@@ -249,7 +252,7 @@ __global__ void __launch_bounds__(64) k_msm_bucket_sum(int NB, const uint32_t* _
 
 // running-sum reduction of MSM_SEG consecutive buckets of one (group, window):
 // sum_j (j+1) B_j for the window-local bucket indices j of the segment
-__global__ void __launch_bounds__(64) k_msm_segments(int nw, int NS, int NSg, int NBg, const MsmWindow* __restrict__ win,
+__global__ void __launch_bounds__(256) k_msm_segments(int nw, int NS, int NSg, int NBg, const MsmWindow* __restrict__ win,
                                                      const uint32_t* __restrict__ buckets,
                                                      uint32_t* __restrict__ segs, uint32_t* __restrict__ scratch) {
   int g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -317,24 +320,31 @@ __global__ void __launch_bounds__(256) k_msm_windows(int nw, int WB, int NSg, co
 // chain), lane nw: the extra points; then an LDS tree over the lanes
 __global__ void __launch_bounds__(64) k_msm_final(int nw, int WB, const MsmWindow* __restrict__ win,
                                                   const uint32_t* __restrict__ parts_all, uint32_t* __restrict__ out_all) {
-  __shared__ uint32_t sh[64 * 24];
-  const int t = threadIdx.x, grp = blockIdx.x;  // one block per group
+  // lane-cooperative (device/coop.hpp): 12 groups of COOP_G lanes, group g takes
+  // windows g, g + 12, ...; each doubling is 3 product levels instead of 7
+  constexpr int NGRP = 64 / COOP_G;
+  __shared__ uint32_t sh[NGRP * 24];
+  const int t = threadIdx.x, grp = blockIdx.x;  // one block per MSM group
+  const int g = t / COOP_G, role = t % COOP_G, base = g * COOP_G;
+  const bool live = g < NGRP;
   const uint32_t* parts = parts_all + (size_t)grp * (nw + 1) * WB * 24;
   uint32_t* out = out_all + (size_t)grp * 24;
   G1J acc = g1j_identity();
-  for (int w = t; w <= nw; w += 64) {
-    G1J W = load_g1j(parts + (size_t)w * WB * 24);
-    for (int j = 1; j < WB; j++) add_inl(W, load_g1j(parts + ((size_t)w * WB + j) * 24));
-    if (w < nw)
-      for (int q = 0; q < win[w].off; q++) W = g1j_dbl(W);
-    add_inl(acc, W);
+  if (live) {
+    for (int w = g; w <= nw; w += NGRP) {
+      G1J W = load_g1j(parts + (size_t)w * WB * 24);
+      for (int j = 1; j < WB; j++) coop_add(W, load_g1j(parts + ((size_t)w * WB + j) * 24), role, base);
+      if (w < nw)
+        for (int q = 0; q < win[w].off; q++) W = coop_dbl(W, role, base);
+      coop_add(acc, W, role, base);
+    }
+    if (role == 0) store_g1j(sh + g * 24, acc);
   }
-  store_g1j(sh + t * 24, acc);
   __syncthreads();
-  for (int half = 32; half >= 1; half >>= 1) {
-    if (t < half) add_inl(acc, load_g1j(sh + (t + half) * 24));
+  for (int half = 8; half >= 1; half >>= 1) {
+    if (live && g < half && g + half < NGRP) coop_add(acc, load_g1j(sh + (g + half) * 24), role, base);
     __syncthreads();
-    if (t < half) store_g1j(sh + t * 24, acc);
+    if (live && role == 0 && g < half && g + half < NGRP) store_g1j(sh + g * 24, acc);
     __syncthreads();
   }
   if (t == 0) store_g1j(out, acc);
@@ -402,9 +412,9 @@ void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalar
              p.chunk_bkt, p.sorted, p.partials);
   // expected nonzero digits: N * nw * (1 - 2^-c) ~ N * nw mixed additions
   tl->mark("k_msm_chunks", s, (double)p.NV * p.nw * (COST_MADD + 0.5));
-  FTS_LAUNCH(k_msm_bucket_sum, p.NB, 64, s, p.NB, p.counts, p.chunk_off, p.partials, p.buckets);
+  FTS_LAUNCH(k_msm_bucket_sum, p.NB, g_lat_bs, s, p.NB, p.counts, p.chunk_off, p.partials, p.buckets);
   tl->mark("k_msm_bucket_sum", s, 0);
-  FTS_LAUNCH(k_msm_segments, p.NS, 64, s, p.nw, p.NS, p.NSg, p.NBg, p.d_win, p.buckets, p.segs, scratch);
+  FTS_LAUNCH(k_msm_segments, p.NS, g_lat_bs, s, p.nw, p.NS, p.NSg, p.NBg, p.d_win, p.buckets, p.segs, scratch);
   tl->mark("k_msm_segments", s, (double)p.NB * 2 * COST_ADD);
   if (s_extra != s) tl->fork(s_extra, s);
   uint32_t* parts = p.scratch + 2 * (size_t)p.NBLK + 2;

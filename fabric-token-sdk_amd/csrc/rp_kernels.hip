@@ -31,6 +31,13 @@
 #include "../../include/fts_gpu.h"
 
 namespace fts {
+// block size of the latency-bound per-proof kernels (few waves, long chains):
+// 256-thread blocks put a block's 4 waves on the 4 SIMDs of one CU, and the
+// dispatcher spreads blocks over CUs, so concurrent small kernels of the
+// pass's streams rarely share a SIMD (64-thread blocks of two such kernels
+// slowed each other by ~26 %, tools/experiments/colocate.cpp).  FTS_LAT_BS.
+int g_lat_bs = 256;
+
 
 constexpr int NORM_BS = 256;
 constexpr int NORM_E = 4;  // points per lane of k_rp_normalize
@@ -170,7 +177,7 @@ __global__ void __launch_bounds__(64) k_rp_hash_small(int B, int n, int k, const
 
 // thread per proof: z = Hz(Zb(y)), Montgomery forms, polEval, and one batch
 // inversion (Montgomery trick) for y and the k round challenges
-__global__ void __launch_bounds__(64) k_rp_chal_fr(int B, int n, int k, const int32_t* __restrict__ status,
+__global__ void __launch_bounds__(256) k_rp_chal_fr(int B, int n, int k, const int32_t* __restrict__ status,
                                                    uint32_t* __restrict__ ch, uint32_t* __restrict__ tmp) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B || status[b] != 0) return;
@@ -501,7 +508,7 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_all(int B, int n, int k, con
 // computes x_h phi^h(D) -> terms[b][n + 2 + h]; lane tables 1..8 * P in vtab.
 // x is read from the digest k_rp_hash_small left at the head of its slot
 // (canonical), so this runs concurrently with k_rp_chal_fr.
-__global__ void __launch_bounds__(64) k_rp_xd(int B, int n, int k, const int32_t* __restrict__ status,
+__global__ void __launch_bounds__(256) k_rp_xd(int B, int n, int k, const int32_t* __restrict__ status,
                                               const uint32_t* __restrict__ pts, const uint8_t* __restrict__ small_msgs,
                                               uint32_t* __restrict__ vtab, uint32_t* __restrict__ terms) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -570,10 +577,19 @@ __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, in
   __shared__ uint32_t invs[8];
   const int t = threadIdx.x;
   const size_t g0 = (size_t)blockIdx.x * NORM_BS * NORM_E + t;
+  // liveness is read ONCE per point: status may change while this kernel runs
+  // (k_sig_exclude on the batch-check stream marks excluded proofs NOT_RUN), and
+  // the prefix products and the back-sweep must skip exactly the same points
+  uint32_t livem = 0;
+#pragma unroll
+  for (int j = 0; j < NORM_E; j++) {
+    const size_t g = g0 + (size_t)j * NORM_BS;
+    if (g < (size_t)total && !(status && status[g / per] != 0)) livem |= 1u << j;
+  }
   auto zload = [&](int j, Fp& z) -> bool {  // z of point j (1 if absent/skipped/identity); live?
     const size_t g = g0 + (size_t)j * NORM_BS;
     z = f_one<FpP>();
-    if (g >= (size_t)total || (status && status[g / per] != 0)) return false;
+    if (!((livem >> j) & 1u)) return false;
     Fp zz;
     load_fp(jac + ((g / per) * stride + g % per + first) * 24 + 16, zz);
     if (!f_is_zero(zz)) z = zz;
@@ -767,7 +783,7 @@ __global__ void __launch_bounds__(256) k_rp_x0_build(int B, int n, const int32_t
 }
 inline size_t x0_build_lds(int n) { return x0_var_bytes(n); }
 
-__global__ void __launch_bounds__(64) k_rp_x0_hash(int B, int n, int k, const int32_t* __restrict__ status,
+__global__ void __launch_bounds__(256) k_rp_x0_hash(int B, int n, int k, const int32_t* __restrict__ status,
                                                    const uint8_t* __restrict__ msgs, const uint8_t* __restrict__ tmpl,
                                                    uint32_t* __restrict__ ch) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -954,7 +970,8 @@ FTS_DEV Fr fr_from_u256(const uint32_t w[8]) {
   return f_to_mont(digest_to_fr(be));
 }
 
-__global__ void __launch_bounds__(64) k_rlc_prep(int B, int n, int k, const int32_t* __restrict__ status,
+__global__ void __launch_bounds__(256) k_rlc_prep(int B, int n, int k, const int32_t* __restrict__ status,
+                                                 const int32_t* __restrict__ excl,
                                                  const int32_t* __restrict__ ipa_flag, const uint32_t* __restrict__ sc,
                                                  const uint32_t* __restrict__ ch, const uint32_t* __restrict__ key,
                                                  uint32_t* __restrict__ msc, uint32_t* __restrict__ coef) {
@@ -963,7 +980,7 @@ __global__ void __launch_bounds__(64) k_rlc_prep(int B, int n, int k, const int3
   const int npts = rp_npts(k);
   uint32_t* M = msc + (size_t)b * npts * 8;
   uint32_t* K = coef + (size_t)b * RLC_NCOEF * 8;
-  const bool e1 = status[b] == 0;
+  const bool e1 = status[b] == 0 && !(excl && excl[b]);
   const bool e2 = e1 && ipa_flag[b] == 0;
   Fr zero = f_zero<FrP>();
   for (int q = 0; q < npts; q++) store_f(M + q * 8, zero);
@@ -1122,9 +1139,11 @@ __global__ void __launch_bounds__(RF_ITEMS * FB_NW) k_rlc_fixed(int n, int G, in
 // (msm_out + addend: the Q column's product, computed after x0)
 __global__ void __launch_bounds__(64) k_rlc_finalize(int B, const uint32_t* __restrict__ msm_out,
                                                      const uint32_t* __restrict__ addend,
+                                                     const int32_t* __restrict__ excl,
                                                      int32_t* __restrict__ status, const int32_t* __restrict__ ipa_flag,
                                                      int32_t* __restrict__ flag) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B && excl && excl[b] && status[b] == 0) status[b] = FTS_E_NOT_RUN;
   G1J e = load_g1j(msm_out);
   add_inl(e, load_g1j(addend));
   const bool pass = g1j_is_identity(e);
@@ -1216,6 +1235,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
                      Timeline* tl) {
   const int B = d.B, n = d.n, k = d.k, NC = rlc_ncols(n);
   if (!B) return;
+  if (d.excl) (void)hipMemsetAsync(d.excl, 0, (size_t)B * 4, s);
   FTS_LAUNCH(k_rp_decode, B * rp_npts(k), 256, s, B, rp_npts(k), d.raw, d.pts, d.status);
   tl->mark("k_rp_decode", s, 0);
   FTS_LAUNCH(k_rp_hash_small, B * (2 + k), 64, s, B, n, k, d.raw, d.status, d.ch, d.small_msgs);
@@ -1224,11 +1244,11 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   if (d.com_fixed) {
     // latency path: x*D on the side stream beside chal_fr and the fixed-base products
     tl->fork(s, s2);
-    FTS_LAUNCH(k_rp_xd, 2 * B, 64, s2, B, n, k, d.status, d.pts, d.small_msgs, d.scratch + (size_t)B * (k + 1) * 8,
+    FTS_LAUNCH(k_rp_xd, 2 * B, g_lat_bs, s2, B, n, k, d.status, d.pts, d.small_msgs, d.scratch + (size_t)B * (k + 1) * 8,
                d.terms);
     tl->mark("k_rp_xd", s2, (double)B * 2 * COST_VB128);
   }
-  FTS_LAUNCH(k_rp_chal_fr, B, 64, s, B, n, k, d.status, d.ch, d.scratch);
+  FTS_LAUNCH(k_rp_chal_fr, B, g_lat_bs, s, B, n, k, d.status, d.ch, d.scratch);
   tl->mark("k_rp_chal_fr", s, (double)B * (3 * k + 4 * (k + 1) + 12));
   FTS_LAUNCH(k_rp_powers, B * (n >> std::min(PW_LC, k)), 64, s, B, n, k, d.status, d.ch, d.ypow, d.svec, d.zvec);
   tl->mark("k_rp_powers", s, (double)B * (3.0 * n + 2.0 * k));
@@ -1240,8 +1260,9 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   auto rlc_side = [&]() {
     tl->fork(s, s3);
     if (d.pre_rlc) d.pre_rlc(d.pre_rlc_arg, s3);
-    FTS_LAUNCH(k_rlc_prep, B, 64, s3, B, n, k, d.status, d.ipa_flag, d.sc, d.ch, r.key, r.msc, r.coef);
+    FTS_LAUNCH(k_rlc_prep, B, g_lat_bs, s3, B, n, k, d.status, d.excl, d.ipa_flag, d.sc, d.ch, r.key, r.msc, r.coef);
     tl->mark("k_rlc_prep", s3, (double)B * (3 * k + 33));
+    (void)hipEventRecord(d.ev_coef, s3);
     hipLaunchKernelGGL(k_rlc_columns, dim3(NC - 1, 1), dim3(256), 0, s3, B, n, k, B, 0, (const int32_t*)nullptr, d.ch,
                        r.coef, d.ypow, d.svec, d.zvec, r.colsum);
     tl->mark("k_rlc_columns", s3, (double)B * 4 * n);
@@ -1288,15 +1309,18 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s, B, n, d.status, d.hp_be, x0_const, d.sc,
                      d.x0_msgs);
   tl->mark("k_rp_x0_build", s, 0);
-  FTS_LAUNCH(k_rp_x0_hash, B, 64, s, B, n, k, d.status, d.x0_msgs, x0_tmpl, d.ch);
+  FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s, B, n, k, d.status, d.x0_msgs, x0_tmpl, d.ch);
   tl->mark("k_rp_x0_hash", s, 0);
-  // x0 tail: column Q and its product, then the verdict once the MSM is in
+  // x0 tail: column Q (needs the weights of k_rlc_prep) and its product, then
+  // the verdict once the MSM is in
+  (void)hipStreamWaitEvent(s, d.ev_coef, 0);
   hipLaunchKernelGGL(k_rlc_columns, dim3(1, 1), dim3(256), 0, s, B, n, k, B, NC - 1, (const int32_t*)nullptr, d.ch,
                      r.coef, d.ypow, d.svec, d.zvec, r.colsum);
   FTS_LAUNCH(k_rlc_fixed, FB_NW, RF_ITEMS * FB_NW, s, n, 1, NC - 1, 1, r.colsum, tables, r.fixed);
   tl->mark("k_rlc_q", s, (double)B + FB_NW * 3 + (FB_NW - 1) * COST_ADD);
   tl->fork(s3, s);
-  FTS_LAUNCH(k_rlc_finalize, B, 64, s, B, r.plan.out, r.fixed + (size_t)(NC - 1) * 24, d.status, d.ipa_flag, r.flag);
+  FTS_LAUNCH(k_rlc_finalize, B, 64, s, B, r.plan.out, r.fixed + (size_t)(NC - 1) * 24, d.excl, d.status, d.ipa_flag,
+             r.flag);
   tl->mark("k_rlc_finalize", s, 0);
 }
 
@@ -1356,6 +1380,6 @@ void launch_x0(int B, int n, int k, const int32_t* status, const uint8_t* hp_be,
                const uint8_t* x0_tmpl, const uint32_t* sc, uint8_t* msgs, uint32_t* ch, hipStream_t s) {
   if (B <= 0) return;
   hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s, B, n, status, hp_be, x0_const, sc, msgs);
-  FTS_LAUNCH(k_rp_x0_hash, B, 64, s, B, n, k, status, msgs, x0_tmpl, ch);
+  FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s, B, n, k, status, msgs, x0_tmpl, ch);
 }
 }  // namespace fts

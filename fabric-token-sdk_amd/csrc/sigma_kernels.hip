@@ -74,15 +74,16 @@ __global__ void __launch_bounds__(64) k_sig_vslots(int A, const SigAction* __res
 
 // lane per action whose sigma proof failed: its range proofs leave the batch
 // check (their verdicts are never observable: the TypeAndSum / SameType error
-// wins, transfer.go:192-196, issue/verifier.go:40-43)
+// wins, transfer.go:192-196, issue/verifier.go:40-43).  Only the exclusion mask
+// is written here (the exact phase reads the range proofs' status concurrently);
+// k_rlc_prep drops the proofs from the check and k_rlc_finalize marks them NOT_RUN.
 __global__ void __launch_bounds__(256) k_sig_exclude(int A, const SigAction* __restrict__ act,
-                                                     const int32_t* __restrict__ status, int32_t* __restrict__ rp_status) {
+                                                     const int32_t* __restrict__ status, int32_t* __restrict__ rp_excl) {
   int a = blockIdx.x * blockDim.x + threadIdx.x;
   if (a >= A || status[a] == 0) return;
   const SigAction ac = act[a];
   if (ac.rp_base < 0) return;
-  for (int j = 0; j < ac.rp_count; j++)
-    if (rp_status[ac.rp_base + j] == FTS_OK) rp_status[ac.rp_base + j] = FTS_E_NOT_RUN;
+  for (int j = 0; j < ac.rp_count; j++) rp_excl[ac.rp_base + j] = 1;
 }
 
 __global__ void __launch_bounds__(64) k_sig_terms(int nwork, const int2* __restrict__ work,
@@ -249,8 +250,8 @@ void launch_sig_finish(const SigBatchDev& d, const uint32_t* tables, int n, hipS
   FTS_LAUNCH(k_sig_finish, d.A, 64, s, d.A, d.act, d.pts, d.sc, d.status, d.aff, d.aff_off, d.msgs);
 }
 // the range proofs of actions whose sigma proof failed leave the batch check
-void launch_sig_exclude(const SigBatchDev& d, int32_t* rp_status, hipStream_t s) {
-  FTS_LAUNCH(k_sig_exclude, d.A, 256, s, d.A, d.act, d.status, rp_status);
+void launch_sig_exclude(const SigBatchDev& d, int32_t* rp_excl, hipStream_t s) {
+  FTS_LAUNCH(k_sig_exclude, d.A, 256, s, d.A, d.act, d.status, rp_excl);
 }
 
 }  // namespace fts

@@ -1,0 +1,78 @@
+"""HBM traffic per launch for bench.py's `roofline.traffic`, from separate
+rocprofv3 PMC passes over the same bench command (tools/gpu_round_r02.sh).
+
+Inputs: the FETCH_SIZE and WRITE_SIZE counter CSVs of the bench command, the
+FETCH_SIZE CSV of lib/fetch_calib with the byte counts it printed, the bench
+JSON line of the PMC command (for the isolated pass size), and R = its
+--roofline-steps.  The LAST R dispatches of every kernel are bench.py's isolated
+roofline pass; their average is stored under "<kernel>@pass<proofs>".
+
+FETCH_SIZE counts memory-side read requests (KiB).  Its ratio to the bytes a
+kernel really reads depends on the access pattern, so it is calibrated with
+kernels that read a known number of bytes no cache can hold:
+  fetch_scale = known bytes / (FETCH_SIZE * 1024)
+from k_calib_gather64w (64-byte rows, the 64 lanes of a wave in one table
+window: the fixed-base gather pattern) for the table-gather kernels, and from
+k_calib_stream (16 B per lane, coalesced) for the others.  WRITE_SIZE is used
+as measured.
+
+    python tools/pmc_r02.py <fetch_dir> <write_dir> <calib_dir> <calib.json> <bench.json> <R> <out.json>
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+GATHER = {"k_rp_fixed_exact", "k_rp_fixed_all", "k_rp_terms_fixed", "k_pv_fbsum", "k_sig_terms", "k_token_open"}
+
+
+def per_kernel(d, counter):
+    acc = defaultdict(list)
+    for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(p) as f:
+            for r in sorted(csv.DictReader(f), key=lambda r: int(r["Start_Timestamp"])):
+                if r["Counter_Name"] == counter:
+                    acc[r["Kernel_Name"].split("(")[0].replace("fts::", "")].append(float(r["Counter_Value"]))
+    return acc
+
+
+def main():
+    fdir, wdir, cdir, cjson, bjson, R, dst = sys.argv[1:8]
+    R = int(R)
+    known = json.load(open(cjson))
+    cal = per_kernel(cdir, "FETCH_SIZE")
+    scale = {}
+    calib = {}
+    for k, b in known.items():
+        v = cal.get(k)
+        if v:
+            fs = sum(v) / len(v) * 1024
+            scale[k] = b / fs
+            calib[k] = {"known_bytes": b, "fetch_size_bytes": round(fs), "scale": round(b / fs, 4)}
+    bench = json.load(open(bjson))
+    proofs = bench["isolated_pass"]["proofs"]
+    fetch, write = per_kernel(fdir, "FETCH_SIZE"), per_kernel(wdir, "WRITE_SIZE")
+    out = {"_calibration": calib, "_source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate runs) of bench.py, "
+                                             "last %d dispatches per kernel = the isolated pass of %d proofs"
+                                             % (R, proofs)}
+    for k in sorted(set(fetch) | set(write)):
+        f, w = fetch.get(k, [])[-R:], write.get(k, [])[-R:]
+        e = {"dispatches": len(f)}
+        if f:
+            e["fetch_bytes"] = round(sum(f) / len(f) * 1024)
+            e["fetch_scale"] = round(scale.get("k_calib_gather64w" if k in GATHER else "k_calib_stream", 1.0), 4)
+        if w:
+            e["write_bytes"] = round(sum(w) / len(w) * 1024)
+        out["%s@pass%d" % (k, proofs)] = e
+    json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
+    print(json.dumps(calib))
+    for k in ("k_rp_fixed_exact", "k_rp_fixed_all", "k_msm_chunks"):
+        key = "%s@pass%d" % (k, proofs)
+        if key in out:
+            print(key, out[key])
+
+
+if __name__ == "__main__":
+    main()
