@@ -451,8 +451,9 @@ def _add(a, b, p):
 
 
 def _roofline_from(timings, steps):
-    """dominant kernel (largest algorithmic MAD count) of the per-kernel timings"""
-    dom = max(timings, key=lambda k: timings[k][1])
+    """dominant kernel (largest algorithmic MAD count) of the per-kernel timings
+    (the batch check's fallback kernels, "fb:" names, are reported apart)"""
+    dom = max((k for k in timings if not k.startswith("fb:")), key=lambda k: timings[k][1])
     ms, mads = timings[dom][0] / steps, timings[dom][1]
     ach = mads / (ms * 1e-3) / 1e12 if mads and ms > 0 else None
     return {"bound": "int32_valu (v_mad_u64_u32)", "kernel": dom, "achieved": round(ach, 3) if ach else None,
@@ -1080,10 +1081,21 @@ def bench_mixed(args):
                                    "per step (%d range proofs), %d calls in flight" % (2 * n_tr + 16 * n_is, nb),
                        "transfers_per_gpu": n_tr, "issues_per_gpu": n_is, "parallelism": "shard%d" % world},
             "roofline": _roofline_from(kt, args.steps), "cpu_baseline": cpu,
+            "fallback": _fallback_share(kt, args.steps, elapsed / args.steps * nb * 1e3),
             "kernel_ms": {k: round(v[0] / args.steps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),
             flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _fallback_share(kt, steps, call_ms):
+    """device time of the batch check's fallback (group test + per-proof checks,
+    "fb:" kernels) per call, against all kernel time and against the call's wall
+    time (ms_per_step x calls in flight)"""
+    fb = sum(v[0] for k, v in kt.items() if k.startswith("fb:")) / steps
+    dev = sum(v[0] for k, v in kt.items() if not k.startswith("host_")) / steps
+    return {"kernel_ms_per_call": round(fb, 3), "share_of_kernel_time": round(fb / dev, 4) if dev else None,
+            "call_wall_ms": round(call_ms, 3), "share_of_call_wall": round(fb / call_ms, 4) if call_ms else None}
 
 
 if __name__ == "__main__":

@@ -168,6 +168,10 @@ struct Lane {
     return e == hipSuccess ? hipEventSynchronize(done) : e;
   }
   bool presized = false;  // workspace sized for the context's largest coalesced pass
+  // no other pass was running when the current one started (set by the dispatchers):
+  // only then does a small pass take the latency path (k_rp_fixed_all), which does
+  // more total work than the work path and pays off only on an otherwise idle device
+  bool alone = true;
   hipStream_t s = nullptr, s2 = nullptr;
   hipStream_t s3 = nullptr;         // sigma proofs of action batches (beside the range-proof pass)
   hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr;  // cross-stream ordering (no timing)
@@ -331,6 +335,7 @@ struct LaneGuard {
     auto it = want < 0 ? c->free_lanes.end() - 1 : std::find(c->free_lanes.begin(), c->free_lanes.end(), want);
     L = c->lanes[*it];
     c->free_lanes.erase(it);
+    L->alone = c->free_lanes.size() + 1 == c->lanes.size();
   }
   ~LaneGuard() {
     std::lock_guard<std::mutex> lk(c->mu);
@@ -1041,7 +1046,7 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
                w.zvec.as<uint32_t>(),
                nullptr,
                nullptr,
-               (size_t)B <= c->com_fixed_max ? 1 : 0};
+               (size_t)B <= c->com_fixed_max && L.alone ? 1 : 0};
   d.pre_rlc = pre_rlc;
   d.pre_rlc_arg = pre_rlc_arg;
   d.rlc_fork = c->rlc_fork;
@@ -1284,6 +1289,7 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
     }
     Lane* L = c->lanes[c->free_lanes.back()];
     c->free_lanes.pop_back();
+    L->alone = c->free_lanes.size() + 1 == c->lanes.size();
     std::vector<RpReq*> grp;
     size_t tot = 0;
     while (!c->rp_pending.empty()) {

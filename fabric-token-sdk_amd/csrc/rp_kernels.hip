@@ -926,27 +926,50 @@ __global__ void __launch_bounds__(64) k_rp_terms_var(int B, int n, int k, const 
 }
 
 // ------------------------------------------------------------------ check
-__global__ void __launch_bounds__(64) k_rp_check(int B, int n, int k, const int32_t* __restrict__ sel,
-                                                 int32_t* __restrict__ status, const int32_t* __restrict__ ipa_flag,
-                                                 const uint32_t* __restrict__ terms, const uint32_t* __restrict__ hpa) {
-  int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  if (sel) b = sel[b];
-  if (status[b] != 0) return;
-  const uint32_t* T = terms + (size_t)b * rp_nterms(n, k) * 24;
-  G1J e1 = load_g1j(T);
-  for (int t = 1; t < 5; t++) e1 = nl_add_mem(e1, T + t * 24, 0);
-  if (!g1j_is_identity(e1)) {
+// CK_LANES lanes per proof: E1 (5 terms) on lane 0; E2 (-com + the 1 + 2n + 2k
+// other terms, 81 at n = 64) as CK_LANES partial sums + a 4-level LDS tree
+// instead of one chain of ~80 additions.  Group addition is associative, so the
+// verdict (identity or not) is the same.
+constexpr int CK_LANES = 16, CK_PROOFS = 16;
+__global__ void __launch_bounds__(CK_LANES * CK_PROOFS) k_rp_check(int B, int n, int k, const int32_t* __restrict__ sel,
+                                                                   int32_t* __restrict__ status,
+                                                                   const int32_t* __restrict__ ipa_flag,
+                                                                   const uint32_t* __restrict__ terms,
+                                                                   const uint32_t* __restrict__ hpa) {
+  __shared__ uint32_t sh[CK_LANES * CK_PROOFS * 24];
+  __shared__ int e1_ok[CK_PROOFS];
+  const int l = threadIdx.x % CK_LANES, pl = threadIdx.x / CK_LANES;
+  const int bi = blockIdx.x * CK_PROOFS + pl;
+  int b = bi < B ? (sel ? sel[bi] : bi) : -1;
+  const bool live = b >= 0 && status[b] == 0;
+  const uint32_t* T = live ? terms + (size_t)b * rp_nterms(n, k) * 24 : terms;
+  if (live && l == 0) {
+    G1J e1 = load_g1j(T);
+    for (int t = 1; t < 5; t++) e1 = nl_add_mem(e1, T + t * 24, 0);
+    e1_ok[pl] = g1j_is_identity(e1);
+  }
+  G1J acc = g1j_identity();
+  if (live) {
+    if (l == 0) acc = g1j_from_affine(g1a_neg(load_g1a(hpa + ((size_t)b * (n + 1) + n) * 16)));
+    for (int t = 5 + l; t < rp_nterms(n, k); t += CK_LANES) add_inl(acc, load_g1j(T + t * 24));
+  }
+  uint32_t* S = sh + (size_t)pl * CK_LANES * 24;
+  store_g1j(S + l * 24, acc);
+  __syncthreads();
+  for (int half = CK_LANES / 2; half >= 1; half >>= 1) {
+    if (live && l < half) add_inl(acc, load_g1j(S + (l + half) * 24));
+    __syncthreads();
+    if (live && l < half) store_g1j(S + l * 24, acc);
+    __syncthreads();
+  }
+  if (!live || l != 0) return;
+  if (!e1_ok[pl]) {
     status[b] = FTS_E_RP_INVALID;
-    return;
-  }
-  if (ipa_flag[b] != 0) {
+  } else if (ipa_flag[b] != 0) {
     status[b] = ipa_flag[b];
-    return;
+  } else {
+    status[b] = g1j_is_identity(acc) ? FTS_OK : FTS_E_IPA_INVALID;
   }
-  G1J e2 = g1j_from_affine(g1a_neg(load_g1a(hpa + ((size_t)b * (n + 1) + n) * 16)));
-  for (int t = 5; t < rp_nterms(n, k); t++) e2 = nl_add_mem(e2, T + t * 24, 0);
-  status[b] = g1j_is_identity(e2) ? FTS_OK : FTS_E_IPA_INVALID;
 }
 
 // ------------------------------------------------------------ RLC batch check
@@ -1344,7 +1367,9 @@ void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, const int32
   FTS_LAUNCH(k_rp_terms_var, B * (3 + 2 * k), 64, s, B, n, k, sel, d.status, d.ipa_flag, d.pts, d.ch, d.terms,
              d.scratch);
   tl->mark("k_rp_terms_var", s, (double)B * (3 + 2 * k) * (4.0 * 7.0 + 12.0 * COST_ADD + 124 * COST_DBL + 60 * COST_ADD));
-  FTS_LAUNCH(k_rp_check, B, 64, s, B, n, k, sel, d.status, d.ipa_flag, d.terms, d.hpa);
+  if (B > 0)
+    hipLaunchKernelGGL(k_rp_check, dim3((B + CK_PROOFS - 1) / CK_PROOFS), dim3(CK_LANES * CK_PROOFS), 0, s, B, n, k,
+                       sel, d.status, d.ipa_flag, d.terms, d.hpa);
   tl->mark("k_rp_check", s, (double)B * rp_nterms(n, k) * COST_ADD);
 }
 

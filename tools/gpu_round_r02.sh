@@ -46,7 +46,7 @@ if [ "${PMC:-1}" = 1 ]; then
   step pmc_valu 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE -T -f csv -d $OUT/pmc_valu -o run -- $PB
   step pmc_calib 120 rocprofv3 --pmc FETCH_SIZE -T -f csv -d $OUT/pmc_calib -o run -- fabric-token-sdk_amd/lib/fetch_calib
   json pmc_calib
-  python3 tools/pmc_r02.py $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_calib $OUT/pmc_calib.json $OUT/pmc_fetch.json 2 $OUT/traffic_$TAG.json
+  python3 tools/pmc_r02.py $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_calib $OUT/pmc_calib.json $OUT/pmc_fetch.json 2 $OUT/traffic_$TAG.json $OUT/pmc_valu
 fi
 if [ "${EXTRA:-1}" = 1 ]; then
   step bench_transfer 300 python3 -u bench.py --workload transfer --steps 96 --warmup 4

@@ -16,7 +16,10 @@ window: the fixed-base gather pattern) for the table-gather kernels, and from
 k_calib_stream (16 B per lane, coalesced) for the others.  WRITE_SIZE is used
 as measured.
 
-    python tools/pmc_r02.py <fetch_dir> <write_dir> <calib_dir> <calib.json> <bench.json> <R> <out.json>
+    python tools/pmc_r02.py <fetch_dir> <write_dir> <calib_dir> <calib.json> <bench.json> <R> <out.json> [valu_dir]
+
+With valu_dir (the SQ_* pass), each entry also carries the per-launch VALU
+instruction counts, including SQ_INSTS_VALU_MFMA_MOPS_F16 (0: no MFMA).
 """
 import csv
 import glob
@@ -53,7 +56,14 @@ def main():
             calib[k] = {"known_bytes": b, "fetch_size_bytes": round(fs), "scale": round(b / fs, 4)}
     bench = json.load(open(bjson))
     proofs = bench["isolated_pass"]["proofs"]
+    batch = bench["config"]["batch_per_gpu"]
+    # kernels that only the lone batch runs (passes <= FTS_COM_FIXED_MAX take the
+    # latency path): their last dispatches are the isolated single batch
+    LATENCY_ONLY = {"k_rp_fixed_all", "k_rp_xd", "k_rp_com_tree"}
     fetch, write = per_kernel(fdir, "FETCH_SIZE"), per_kernel(wdir, "WRITE_SIZE")
+    vdir = sys.argv[8] if len(sys.argv) > 8 else None
+    SQ = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_F16")
+    valu = {c: per_kernel(vdir, c) for c in SQ} if vdir else {}
     out = {"_calibration": calib, "_source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate runs) of bench.py, "
                                              "last %d dispatches per kernel = the isolated pass of %d proofs"
                                              % (R, proofs)}
@@ -65,7 +75,11 @@ def main():
             e["fetch_scale"] = round(scale.get("k_calib_gather64w" if k in GATHER else "k_calib_stream", 1.0), 4)
         if w:
             e["write_bytes"] = round(sum(w) / len(w) * 1024)
-        out["%s@pass%d" % (k, proofs)] = e
+        for c, per in valu.items():
+            v = per.get(k, [])[-R:]
+            if v:
+                e[c] = round(sum(v) / len(v))
+        out["%s@pass%d" % (k, batch if k in LATENCY_ONLY and proofs > batch else proofs)] = e
     json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
     print(json.dumps(calib))
     for k in ("k_rp_fixed_exact", "k_rp_fixed_all", "k_msm_chunks"):
