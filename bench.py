@@ -136,7 +136,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall-time bound of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
-    ap.add_argument("--workload", choices=["rp", "msm", "transfer", "mixed", "request", "audit", "prove", "ecdsa"],
+    ap.add_argument("--workload", choices=["rp", "msm", "transfer", "mixed", "request", "audit", "prove", "ecdsa",
+                                           "idemix"],
                     default="rp")
     ap.add_argument("--sigs", type=int, default=65536, help="ecdsa workload: owner signatures per GPU per step")
     ap.add_argument("--msg-len", type=int, default=1024, help="ecdsa workload: signed message bytes")
@@ -156,6 +157,8 @@ def main():
         return bench_mixed(args)
     if args.workload == "ecdsa":
         return bench_ecdsa(args)
+    if args.workload == "idemix":
+        return bench_idemix(args)
     if args.workload == "audit":
         return bench_audit(args)
     if args.workload == "prove":
@@ -904,6 +907,126 @@ def bench_ecdsa(args):
             "roofline": roof, "cpu_baseline": cpu,
             "kernel_ms": {k: round(v / reps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),
             flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+# products of one nym verification (k_nym_verify): HSk and HRand fixed-base products
+# (16-bit windows: 15 mixed additions of 11 products after the first copy), the GLV
+# product c*Nym (straus2_128: 2 x (1 dbl + 6 adds) table, 124 doublings of 7, ~60
+# additions of 16), the on-curve check (4); SHA-256 and the inversion are not counted
+NYM_MULS_PER_VERIFY = 2 * 15 * 11 + 2 * (7 + 6 * 16) + 124 * 7 + 60 * 16 + 4
+
+
+def bench_idemix(args):
+    """SURVEY §8f rank 4 (idemix half): owner-signature checks of
+    TransferSignatureValidate (validator/validator_transfer.go:29-62) for
+    idemix-owned inputs -> crypto.NymSignatureVerifier.Verify
+    (services/identity/idemix/crypto/id.go:145-161).  One step = one
+    fts_nym_verify_batch over --sigs (nym key, NymSignature, message) triples
+    from host buffers under the BN254 issuer key of zkatdlog_pp.json
+    (proto parse, packing, upload, the curve work and both hashes on the
+    device, verdicts back)."""
+    world, rank, local, dist = _dist_setup()
+    import random
+    import numpy as np
+    from fts_gpu import idemix as I
+    from oracle import bn254, idemix as O
+    t0 = time.time()
+    with open(os.path.join(ROOT, "tests", "golden", "idemix", "bn254_tokengen", "IssuerPublicKey"), "rb") as f:
+        ipk_raw = f.read()
+    ipk = O.parse_ipk(ipk_raw)
+    rng = random.Random(0xF7A51D00 + rank)
+    ndist, L = 256, args.msg_len
+    keys = []
+    for _ in range(16):
+        sk, rn = rng.randrange(bn254.R), rng.randrange(bn254.R)
+        keys.append((sk, rn, O.make_nym(ipk, sk, rn)))
+    dn, ds, dm = [], [], []
+    for i in range(ndist):
+        sk, rn, nym = keys[i % len(keys)]
+        m = rng.randbytes(L)
+        dm.append(m)
+        ds.append(O.nym_sign(ipk, sk, nym, rn, m, rng))
+        dn.append(bn254.g1_bytes(nym))
+    n = args.sigs
+    idx = np.arange(n) % ndist
+    msg_buf = bytearray(b"".join(dm[i] for i in idx))
+    bad = np.arange(13, n, 97)  # ~1 % tampered messages
+    for j in bad:
+        msg_buf[j * L] ^= 1
+    msg_buf = bytes(msg_buf)
+    sig_lens = np.array([len(ds[i]) for i in idx], dtype=np.uint64)
+    sig_off = np.concatenate([[0], np.cumsum(sig_lens)[:-1]]).astype(np.uint64)
+    sig_buf = b"".join(ds[i] for i in idx)
+    nym_buf = b"".join(dn[i] for i in idx)
+    msg_off = np.arange(n, dtype=np.uint64) * L
+    msg_len = np.full(n, L, dtype=np.uint64)
+    want = np.zeros(n, dtype=np.int32)
+    want[bad] = I.FTS_E_NYM_INVALID
+    K = I.IssuerKey(ipk_raw, device=local)
+    setup_s = time.time() - t0
+
+    def step():
+        st = K.verify_packed(nym_buf, sig_buf, sig_off, sig_lens, msg_buf, msg_off, msg_len)
+        assert (st == want).all(), "idemix verdicts differ"
+        return st
+
+    class Step:
+        verify = staticmethod(step)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    if dist is not None:
+        dist.barrier()
+    inflight = max(1, args.action_inflight)
+    elapsed, _ = _run_action_steps([Step() for _ in range(inflight)], args.steps, None, None)
+    elapsed = _max_over_ranks(dist, elapsed)
+    value = world * n * args.steps / elapsed
+    reps, kms = 4, 0.0
+    for _ in range(reps):
+        step()
+        kms += K.last_kernel_ms()
+    ms = kms / reps
+    mads = n * NYM_MULS_PER_VERIFY * MAD_PER_MUL  # tampered items run the full path
+    ach = mads / (ms * 1e-3) / 1e12
+    roof = {"bound": "int32_valu (v_mad_u64_u32)", "kernel": "k_nym_verify", "achieved": round(ach, 3),
+            "peak": round(PEAK_TMAD, 3), "unit": "TMAD/s", "frac": round(ach / PEAK_TMAD, 4), "traffic": None,
+            "kernel_ms": round(ms, 4), "mads_per_launch": mads, "muls_per_verify": NYM_MULS_PER_VERIFY,
+            "measured": "HIP events around each launch on the library's stream, %d isolated calls after the "
+                        "timed region (SHA-256 and the inversion not counted as work)" % reps}
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        done, t2 = 0, time.perf_counter()
+        while time.perf_counter() - t2 < min(args.cpu_seconds, 10.0) and done < n:
+            i = int(idx[done])
+            m = msg_buf[done * L:(done + 1) * L]
+            try:
+                O.nym_verify(ipk, dn[i], ds[i], m)
+                got = 0
+            except O.NymError:
+                got = I.FTS_E_NYM_INVALID
+            assert got == want[done], "CPU oracle verdict differs"
+            done += 1
+        cs = time.perf_counter() - t2
+        cpu = {"value": round(done / cs, 1), "unit": "signatures/s", "cores": 1, "kind": "port",
+               "sample": "first %d signatures of the batch, oracle/idemix.py (pure-Python restatement of "
+                         "NymSignature.Ver, affine double-and-add), 1 thread, %.1f s wall" % (done, cs)}
+    K.close()
+    if rank == 0:
+        print(json.dumps({
+            "metric": "idemix nym signature verifies/sec (NymSignatureVerifier.Verify, BN254)",
+            "value": round(value, 1), "unit": "signatures/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32 (BN254 Fp/Fr 8x32-bit Montgomery)",
+            "data": "synthetic: %d distinct nym signatures (16 nyms, %d-byte messages) from the oracle signer under "
+                    "the tokengen BN254 issuer key, tiled; 1 %% tampered messages (seed 0xF7A51D00 + rank)"
+                    % (ndist, L),
+            "config": {"workload": "SURVEY 8f rank 4 (idemix): %d owner signatures per GPU per step via "
+                                   "fts_nym_verify_batch, %d calls in flight" % (n, inflight), "sigs_per_gpu": n,
+                       "msg_len": L, "parallelism": "shard%d" % world},
+            "roofline": roof, "cpu_baseline": cpu, "kernel_ms": {"k_nym_verify": round(ms, 4)},
+            "setup_s": round(setup_s, 2)}), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

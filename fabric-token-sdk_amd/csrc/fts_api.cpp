@@ -777,6 +777,9 @@ const char* fts_status_str(int32_t s) {
     case FTS_E_SIG_MALFORMED: return "asn1: signature does not deserialize";
     case FTS_E_SIG_NOT_LOW_S: return "signature is not in lowS";
     case FTS_E_SIG_INVALID: return "signature not valid";
+    case FTS_E_NYM_MALFORMED: return "error unmarshalling signature";
+    case FTS_E_NYM_BADKEY: return "failed importing nym public key";
+    case FTS_E_NYM_INVALID: return "pseudonym signature invalid: zero-knowledge proof is invalid";
     default: return "unknown status";
   }
 }

@@ -28,6 +28,9 @@ FTS_E_OPEN_MISMATCH = 12
 FTS_E_SIG_MALFORMED = 13
 FTS_E_SIG_NOT_LOW_S = 14
 FTS_E_SIG_INVALID = 15
+FTS_E_NYM_MALFORMED = 16
+FTS_E_NYM_BADKEY = 17
+FTS_E_NYM_INVALID = 18
 
 FTS_API_OK = 0
 FTS_DEVICE_NONE = -2
@@ -45,6 +48,8 @@ EXPORTED = [
     "fts_transfer_prove_batch_gpu", "fts_issue_prove_batch_gpu", "fts_token_metadata_open_batch",
     "fts_token_metadata_decode", "fts_ecdsa_verify_batch", "fts_ecdsa_sig_parse", "fts_p256_pubkey_from_pkix",
     "fts_ecdsa_last_timings", "fts_ctx_create_devices", "fts_ctx_create_mask", "fts_ctx_devices", "fts_shard_plan",
+    "fts_idemix_ipk_create", "fts_idemix_ipk_destroy", "fts_nym_verify_batch", "fts_idemix_identity_nym",
+    "fts_nym_last_timings",
 ]
 
 
@@ -70,6 +75,11 @@ class TokenOpening(C.Structure):
 class EcdsaItem(C.Structure):
     _fields_ = [("msg", C.c_void_p), ("msg_len", C.c_size_t), ("sig", C.c_void_p), ("sig_len", C.c_size_t),
                 ("pk64", C.c_void_p)]
+
+
+class NymItem(C.Structure):
+    _fields_ = [("nym", C.c_void_p), ("nym_len", C.c_size_t), ("sig", C.c_void_p), ("sig_len", C.c_size_t),
+                ("msg", C.c_void_p), ("msg_len", C.c_size_t)]
 
 
 class ActionWitness(C.Structure):
@@ -136,6 +146,11 @@ def _load():
         "fts_ctx_create_mask": ([U8P, S, C.c_uint32, C.c_uint64, C.POINTER(P)], C.c_int),
         "fts_ctx_devices": ([P, I32P, C.c_int], C.c_int),
         "fts_shard_plan": ([S, C.POINTER(C.c_double), C.c_int, C.POINTER(S)], C.c_int),
+        "fts_idemix_ipk_create": ([C.c_int, U8P, S, C.POINTER(P)], C.c_int),
+        "fts_idemix_ipk_destroy": ([P], None),
+        "fts_nym_verify_batch": ([P, S, C.POINTER(NymItem), I32P], C.c_int),
+        "fts_idemix_identity_nym": ([U8P, S, C.POINTER(C.c_void_p), C.POINTER(S)], C.c_int),
+        "fts_nym_last_timings": ([P, C.POINTER(C.c_float)], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

@@ -61,7 +61,11 @@ enum fts_status {
                                opening" token/token.go:78-80 */
   FTS_E_SIG_MALFORMED = 13, /* asn1.Unmarshal of the ECDSA signature failed   validator/ecdsa/ecdsa.go:84-87 */
   FTS_E_SIG_NOT_LOW_S = 14, /* "signature is not in lowS"                     validator/ecdsa/ecdsa.go:103-105 */
-  FTS_E_SIG_INVALID = 15    /* "signature not valid" (ecdsa.Verify false)     validator/ecdsa/ecdsa.go:107-110 */
+  FTS_E_SIG_INVALID = 15,   /* "signature not valid" (ecdsa.Verify false)     validator/ecdsa/ecdsa.go:107-110 */
+  FTS_E_NYM_MALFORMED = 16, /* idemix nym signature empty / proto.Unmarshal failed (bccsp NymSigner.Verify) */
+  FTS_E_NYM_BADKEY = 17,    /* nym public key import failed (idemix/crypto/deserializer.go:49-56) */
+  FTS_E_NYM_INVALID = 18    /* "pseudonym signature invalid: zero-knowledge proof is invalid"
+                               (NymSignature.Ver, via idemix/crypto/id.go:151-161) */
 };
 
 /* ---- API return codes ---- */
@@ -349,6 +353,33 @@ int fts_p256_pubkey_from_pkix(const uint8_t* der, size_t len, uint8_t* pk64);
 /* HIP-event durations (ms) of the last fts_ecdsa_verify_batch on `device`:
  * ms2[0] = k_ecdsa_digest, ms2[1] = k_ecdsa_verify. */
 int fts_ecdsa_last_timings(int device, float* ms2);
+
+/* ---- idemix pseudonym signatures (idemix owner identities, BN254 issuer keys) ----
+ * Replaces, per item, crypto.NymSignatureVerifier.Verify(message, sigma)
+ * (services/identity/idemix/crypto/id.go:145-161 -> IBM/idemix NymSignature.Ver),
+ * the owner verifier that services/identity/idemix/deserializer.go:82-105 returns
+ * for an idemix identity; called by TransferSignatureValidate
+ * (validator/validator_transfer.go:29-62) once per input owner.
+ * One handle per issuer public key (the idemix IssuerPublicKey proto, as held in
+ * PublicParams.IdemixIssuerPublicKeys): HSk / HRand fixed-base tables in HBM. */
+typedef struct fts_idemix_ipk fts_idemix_ipk;
+int fts_idemix_ipk_create(int device, const uint8_t* ipk, size_t ipk_len, fts_idemix_ipk** out);
+void fts_idemix_ipk_destroy(fts_idemix_ipk* ipk);
+typedef struct {
+  const uint8_t* nym; /* NymPublicKey bytes: G1.Bytes() (64 B raw X||Y), see fts_idemix_identity_nym */
+  size_t nym_len;
+  const uint8_t* sig; /* NymSignature proto (proof_c, proof_s_sk, proof_s_r_nym, nonce) */
+  size_t sig_len;
+  const uint8_t* msg; /* signed message; hashed on the device */
+  size_t msg_len;
+} fts_nym_item;
+/* status[i] <- FTS_OK | FTS_E_NYM_MALFORMED | FTS_E_NYM_BADKEY | FTS_E_NYM_INVALID */
+int fts_nym_verify_batch(fts_idemix_ipk* ipk, size_t n, const fts_nym_item* items, int32_t* status);
+/* Host-only: SerializedIdemixIdentity.nym_public_key (idemix/crypto/protos/idemix_config.proto,
+ * crypto/deserializer.go:41-56); *nym points into `id`. FTS_API_EINVAL if absent or malformed. */
+int fts_idemix_identity_nym(const uint8_t* id, size_t len, const uint8_t** nym, size_t* nym_len);
+/* HIP-event duration (ms) of k_nym_verify in the last finished fts_nym_verify_batch on `ipk`. */
+int fts_nym_last_timings(fts_idemix_ipk* ipk, float* ms);
 
 #ifdef __cplusplus
 }

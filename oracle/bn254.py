@@ -7,8 +7,9 @@ verification path (SURVEY §8c "What must the CPU restatement follow"):
 * ``G1.Add/Sub``      -> affine group law, canonical affine result
 * ``G1.Bytes()``      -> 64 bytes X||Y big-endian; the identity is 64 zero bytes
 * ``NewG1FromBytes``  -> 64 bytes, coordinates < p, top two flag bits 0, on curve
-* ``Curve.HashToZr``  -> SHA-256(m) as a big-endian integer mod r   [UNPINNED]
-* ``Zr.Bytes()``      -> 32-byte big-endian of (z mod r)            [UNPINNED]
+* ``Curve.HashToZr``  -> SHA-256(m) as a big-endian integer mod r   [PINNED by the
+                         idemix IssuerPublicKey hash fields, tests/test_idemix_oracle.py]
+* ``Zr.Bytes()``      -> 32-byte big-endian of (z mod r)            [PINNED, same test]
 * ``Curve.HashToG1``  -> RFC 9380 hash_to_curve, expand_message_xmd(SHA-256),
                          empty DST, SVDW map with Z = 1              [PINNED by KAT-1]
 

@@ -1,0 +1,67 @@
+"""Generate tests/golden/idemix_golden.json: idemix nym signatures over the
+BN254 issuer key of cmd/tokengen/testdata/idemix (the key the benchmark's
+public parameters, zkatdlog_pp.json, carry), made and decided by the oracle
+(oracle/idemix.py, seeded).  Honest signatures plus the tamperings a verifier
+must reject, with the reference's error strings.
+
+    python tests/golden/make_idemix_golden.py
+"""
+import json
+import os
+import random
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from oracle import bn254, idemix  # noqa: E402
+
+
+def main():
+    raw = open(os.path.join(HERE, "idemix", "bn254_tokengen", "IssuerPublicKey"), "rb").read()
+    ipk = idemix.parse_ipk(raw)
+    rng = random.Random(0x1DE41)
+    cases = []
+
+    def add(name, nym, sig, msg):
+        try:
+            idemix.nym_verify(ipk, nym, sig, msg)
+            err = None
+        except idemix.NymError as e:
+            err = str(e)
+        cases.append({"name": name, "nym": nym.hex(), "sig": sig.hex(), "msg": msg.hex(), "error": err})
+
+    for i, ml in enumerate([0, 1, 27, 28, 55, 56, 63, 64, 91, 92, 119, 120, 200, 1000, 4099]):
+        sk, rn = rng.randrange(bn254.R), rng.randrange(bn254.R)
+        nym = idemix.make_nym(ipk, sk, rn)
+        msg = bytes(rng.randrange(256) for _ in range(ml))
+        sig = idemix.nym_sign(ipk, sk, nym, rn, msg, rng)
+        nb = bn254.g1_bytes(nym)
+        add("honest_len%d" % ml, nb, sig, msg)
+        if i % 3 == 0:
+            add("msg_flip_len%d" % ml, nb, sig, (msg[:-1] + bytes([msg[-1] ^ 1])) if msg else b"\0")
+        if i % 3 == 1:
+            c, s1, s2, nonce = idemix.decode_nym_sig(sig)
+            add("s_sk_plus1_len%d" % ml, nb, idemix.encode_nym_sig(c, (s1 + 1) % bn254.R, s2, nonce), msg)
+            add("nonce_plus1_len%d" % ml, nb, idemix.encode_nym_sig(c, s1, s2, nonce + 1), msg)
+            add("s_sk_unreduced_len%d" % ml, nb, idemix.encode_nym_sig(c, s1 + bn254.R, s2, nonce), msg)
+            add("c_unreduced_len%d" % ml, nb, idemix.encode_nym_sig(c + bn254.R, s1, s2, nonce), msg)
+        if i % 3 == 2:
+            other = bn254.g1_bytes(idemix.make_nym(ipk, sk + 1, rn))
+            add("wrong_nym_len%d" % ml, other, sig, msg)
+            add("truncated_sig_len%d" % ml, nb, sig[:-5], msg)
+            add("empty_sig_len%d" % ml, nb, b"", msg)
+            off = bytearray(nb)
+            off[63] ^= 1
+            add("nym_off_curve_len%d" % ml, bytes(off), sig, msg)
+            c, s1, s2, nonce = idemix.decode_nym_sig(sig)
+            add("nonce_too_wide_len%d" % ml, nb, idemix.encode_nym_sig(c, s1, s2, nonce + (1 << 256)), msg)
+    out = {"source": "oracle/idemix.py via tests/golden/make_idemix_golden.py (seed 0x1DE41)",
+           "ipk": raw.hex(), "cases": cases}
+    with open(os.path.join(HERE, "idemix_golden.json"), "w") as f:
+        json.dump(out, f, indent=0)
+    print(len(cases), "cases;", sum(c["error"] is None for c in cases), "accept")
+
+
+if __name__ == "__main__":
+    main()

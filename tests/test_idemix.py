@@ -1,0 +1,154 @@
+"""Idemix owner signatures (the idemix half):
+crypto.NymSignatureVerifier.Verify (services/identity/idemix/crypto/id.go:145-161).
+
+CPU tests cover the library's host parsing (SerializedIdemixIdentity) and that
+the issuer key in the benchmark's public parameters is the BN254 tokengen key
+the fixtures use.  GPU tests run fts_nym_verify_batch through the C-ABI and
+compare every verdict with tests/golden/idemix_golden.json and with the oracle
+(oracle/idemix.py) on seeded random batches."""
+import base64
+import json
+import os
+import random
+
+import pytest
+
+from conftest import GOLDEN, PP_PATH
+
+with open(os.path.join(GOLDEN, "idemix_golden.json")) as f:
+    GOLD = json.load(f)
+IPK = bytes.fromhex(GOLD["ipk"])
+
+
+def test_pp_carries_the_fixture_issuer_key():
+    # zkatdlog_pp.json (cmd/tokengen/testdata) holds this BN254 idemix issuer key (curve id 1)
+    with open(PP_PATH) as f:
+        raw = base64.b64decode(json.load(f)["raw"])
+    i = raw.find(IPK)
+    assert i > 0
+    assert raw[i + len(IPK):i + len(IPK) + 4] == bytes([0x12, 0x02, 0x08, 0x01])
+
+
+def test_identity_nym_parse():
+    from fts_gpu import idemix as I
+    from oracle import idemix as O
+    nym = bytes(range(64))
+    ser = O.serialize_identity(nym, ou=b"org1", role=b"\x08\x01", proof=b"p" * 300)
+    assert I.identity_nym(ser) == nym == O.identity_nym(ser)
+    with pytest.raises(Exception):
+        I.identity_nym(O.serialize_identity(b"", ou=b"org1"))
+    with pytest.raises(Exception):
+        I.identity_nym(ser[:-5])
+
+
+@pytest.fixture(scope="module")
+def ipk_dev():
+    from fts_gpu import idemix as I
+    k = I.IssuerKey(IPK, device=0)
+    yield k
+    k.close()
+
+
+@pytest.mark.gpu
+def test_golden_verdicts(ipk_dev):
+    from fts_gpu import idemix as I
+    cases = GOLD["cases"]
+    st = ipk_dev.verify_batch([bytes.fromhex(c["nym"]) for c in cases], [bytes.fromhex(c["sig"]) for c in cases],
+                              [bytes.fromhex(c["msg"]) for c in cases])
+    for c, s in zip(cases, st):
+        assert I.message(int(s)) == c["error"], c["name"]
+    assert sum(c["error"] is None for c in cases) == int((st == 0).sum())
+
+
+@pytest.mark.gpu
+def test_single_verifier_api(ipk_dev):
+    from fts_gpu import idemix as I
+    c = next(c for c in GOLD["cases"] if c["error"] is None)
+    v = I.NymSignatureVerifier(ipk_dev, bytes.fromhex(c["nym"]))
+    v.Verify(bytes.fromhex(c["msg"]), bytes.fromhex(c["sig"]))
+    with pytest.raises(I.SignatureError, match="zero-knowledge proof is invalid"):
+        v.Verify(bytes.fromhex(c["msg"]) + b"!", bytes.fromhex(c["sig"]))
+    with pytest.raises(I.SignatureError, match="error unmarshalling signature"):
+        v.Verify(b"m", b"")
+
+
+def _batch(n, seed, nkeys=6, tamper=0.1):
+    from oracle import bn254, idemix as O
+    ipk = O.parse_ipk(IPK)
+    rng = random.Random(seed)
+    keys = []
+    for _ in range(nkeys):
+        sk, rn = rng.randrange(bn254.R), rng.randrange(bn254.R)
+        keys.append((sk, rn, O.make_nym(ipk, sk, rn)))
+    nyms, sigs, msgs, want = [], [], [], []
+    shared = bytes(rng.randrange(256) for _ in range(700))  # one request message, many inputs
+    for i in range(n):
+        sk, rn, nym = keys[rng.randrange(nkeys)]
+        msg = shared if i % 2 else bytes(rng.randrange(256) for _ in range(rng.randrange(0, 300)))
+        sig = O.nym_sign(ipk, sk, nym, rn, msg, rng)
+        nb = bn254.g1_bytes(nym)
+        if rng.random() < tamper:
+            kind = rng.randrange(3)
+            if kind == 0:
+                msg = msg + b"x"
+            elif kind == 1:
+                c, s1, s2, nonce = O.decode_nym_sig(sig)
+                sig = O.encode_nym_sig(c, s1, (s2 + 1) % bn254.R, nonce)
+            else:
+                nb = bn254.g1_bytes(keys[(keys.index((sk, rn, nym)) + 1) % nkeys][2])
+        try:
+            O.nym_verify(ipk, nb, sig, msg)
+            w = None
+        except O.NymError as e:
+            w = str(e)
+        nyms.append(nb)
+        sigs.append(sig)
+        msgs.append(msg)
+        want.append(w)
+    return nyms, sigs, msgs, want
+
+
+@pytest.mark.gpu
+def test_random_batch_against_oracle(ipk_dev):
+    from fts_gpu import idemix as I
+    nyms, sigs, msgs, want = _batch(300, seed=11)
+    st = ipk_dev.verify_batch(nyms, sigs, msgs)
+    assert [I.message(int(s)) for s in st] == want
+    assert 0 < sum(w is not None for w in want) < 300
+
+
+@pytest.mark.gpu
+def test_large_batch_packed_tiled(ipk_dev):
+    """65,536 signatures (a tiled 256-signature oracle batch): verdicts exact at every position."""
+    import numpy as np
+    nyms, sigs, msgs, want = _batch(256, seed=12, tamper=0.05)
+    reps = 256
+    n = 256 * reps
+    nym_buf = b"".join(nyms) * reps
+    sig_buf, msg_buf = b"".join(sigs), b"".join(msgs)
+    so = np.cumsum([0] + [len(s) for s in sigs[:-1]]).astype(np.uint64)
+    mo = np.cumsum([0] + [len(m) for m in msgs[:-1]]).astype(np.uint64)
+    sl = np.array([len(s) for s in sigs], dtype=np.uint64)
+    ml = np.array([len(m) for m in msgs], dtype=np.uint64)
+    st = ipk_dev.verify_packed(nym_buf, sig_buf, np.tile(so, reps), np.tile(sl, reps), msg_buf, np.tile(mo, reps),
+                               np.tile(ml, reps))
+    exp = np.tile(np.array([w is None for w in want]), reps)
+    assert st.shape == (n,)
+    assert ((st == 0) == exp).all()
+
+
+@pytest.mark.gpu
+def test_packed_bounds_checked(ipk_dev):
+    import numpy as np
+    with pytest.raises(ValueError):
+        ipk_dev.verify_packed(b"\0" * 64, b"abc", np.array([0]), np.array([10]), b"", np.array([0]), np.array([0]))
+    with pytest.raises(ValueError):
+        ipk_dev.verify_packed(b"\0" * 10, b"abc", np.array([0]), np.array([3]), b"", np.array([0]), np.array([0]))
+
+
+@pytest.mark.gpu
+def test_bad_issuer_key_rejected():
+    from fts_gpu import idemix as I
+    from fts_gpu import _lib as L
+    with pytest.raises(L.FtsError):
+        I.IssuerKey(IPK[:100], device=0)
