@@ -140,7 +140,10 @@ def main():
                                            "idemix"],
                     default="rp")
     ap.add_argument("--sigs", type=int, default=65536, help="ecdsa workload: owner signatures per GPU per step")
-    ap.add_argument("--msg-len", type=int, default=1024, help="ecdsa workload: signed message bytes")
+    ap.add_argument("--msg-len", type=int, default=1024, help="ecdsa / idemix workloads: signed message bytes")
+    ap.add_argument("--idemix-curve", choices=["bn254", "fp256bn"], default="bn254",
+                    help="idemix workload: issuer key curve (bn254: the key of zkatdlog_pp.json; "
+                         "fp256bn: the validator tests' key)")
     ap.add_argument("--tokens", type=int, default=65536, help="audit workload: token openings per GPU per step")
     ap.add_argument("--prove-kind", choices=["rp", "transfer"], default="rp",
                     help="prove workload: standalone range proofs, or whole 2-in/2-out transfers")
@@ -933,14 +936,17 @@ def bench_idemix(args):
     from fts_gpu import idemix as I
     from oracle import bn254, idemix as O
     t0 = time.time()
-    with open(os.path.join(ROOT, "tests", "golden", "idemix", "bn254_tokengen", "IssuerPublicKey"), "rb") as f:
+    bn = args.idemix_curve == "bn254"
+    C = O.BN254C if bn else O.FP256BNC
+    kdir = "bn254_tokengen" if bn else "fp256bn_validator"
+    with open(os.path.join(ROOT, "tests", "golden", "idemix", kdir, "IssuerPublicKey"), "rb") as f:
         ipk_raw = f.read()
-    ipk = O.parse_ipk(ipk_raw)
+    ipk = O.parse_ipk(ipk_raw, C)
     rng = random.Random(0xF7A51D00 + rank)
     ndist, L = 256, args.msg_len
     keys = []
     for _ in range(16):
-        sk, rn = rng.randrange(bn254.R), rng.randrange(bn254.R)
+        sk, rn = rng.randrange(C.r), rng.randrange(C.r)
         keys.append((sk, rn, O.make_nym(ipk, sk, rn)))
     dn, ds, dm = [], [], []
     for i in range(ndist):
@@ -948,7 +954,7 @@ def bench_idemix(args):
         m = rng.randbytes(L)
         dm.append(m)
         ds.append(O.nym_sign(ipk, sk, nym, rn, m, rng))
-        dn.append(bn254.g1_bytes(nym))
+        dn.append(C.g1_bytes(nym))
     n = args.sigs
     idx = np.arange(n) % ndist
     msg_buf = bytearray(b"".join(dm[i] for i in idx))
@@ -964,7 +970,7 @@ def bench_idemix(args):
     msg_len = np.full(n, L, dtype=np.uint64)
     want = np.zeros(n, dtype=np.int32)
     want[bad] = I.FTS_E_NYM_INVALID
-    K = I.IssuerKey(ipk_raw, device=local)
+    K = I.IssuerKey(ipk_raw, device=local, curve=I.FTS_CURVE_BN254 if bn else I.FTS_CURVE_FP256BN_AMCL)
     setup_s = time.time() - t0
 
     def step():
@@ -988,11 +994,13 @@ def bench_idemix(args):
         step()
         kms += K.last_kernel_ms()
     ms = kms / reps
-    mads = n * NYM_MULS_PER_VERIFY * MAD_PER_MUL  # tampered items run the full path
+    # FP256BN: 2 x 16 mixed additions, table 7 additions, 252 doublings + 64 full additions, on-curve 4
+    muls = NYM_MULS_PER_VERIFY if bn else 2 * 16 * 11 + 7 * 11 + 252 * 7 + 64 * 16 + 4
+    mads = n * muls * MAD_PER_MUL  # tampered items run the full path
     ach = mads / (ms * 1e-3) / 1e12
-    roof = {"bound": "int32_valu (v_mad_u64_u32)", "kernel": "k_nym_verify", "achieved": round(ach, 3),
+    roof = {"bound": "int32_valu (v_mad_u64_u32)", "kernel": "k_nym_verify" + ("" if bn else "_fbn"), "achieved": round(ach, 3),
             "peak": round(PEAK_TMAD, 3), "unit": "TMAD/s", "frac": round(ach / PEAK_TMAD, 4), "traffic": None,
-            "kernel_ms": round(ms, 4), "mads_per_launch": mads, "muls_per_verify": NYM_MULS_PER_VERIFY,
+            "kernel_ms": round(ms, 4), "mads_per_launch": mads, "muls_per_verify": muls,
             "measured": "HIP events around each launch on the library's stream, %d isolated calls after the "
                         "timed region (SHA-256 and the inversion not counted as work)" % reps}
     cpu = None
@@ -1015,17 +1023,17 @@ def bench_idemix(args):
     K.close()
     if rank == 0:
         print(json.dumps({
-            "metric": "idemix nym signature verifies/sec (NymSignatureVerifier.Verify, BN254)",
+            "metric": "idemix nym signature verifies/sec (NymSignatureVerifier.Verify, %s)" % C.name,
             "value": round(value, 1), "unit": "signatures/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u32 (BN254 Fp/Fr 8x32-bit Montgomery)",
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32 (%s Fp/Fr 8x32-bit Montgomery)" % C.name,
             "data": "synthetic: %d distinct nym signatures (16 nyms, %d-byte messages) from the oracle signer under "
-                    "the tokengen BN254 issuer key, tiled; 1 %% tampered messages (seed 0xF7A51D00 + rank)"
-                    % (ndist, L),
+                    "the %s issuer key (%s), tiled; 1 %% tampered messages (seed 0xF7A51D00 + rank)"
+                    % (ndist, L, C.name, kdir),
             "config": {"workload": "SURVEY 8f rank 4 (idemix): %d owner signatures per GPU per step via "
                                    "fts_nym_verify_batch, %d calls in flight" % (n, inflight), "sigs_per_gpu": n,
                        "msg_len": L, "parallelism": "shard%d" % world},
-            "roofline": roof, "cpu_baseline": cpu, "kernel_ms": {"k_nym_verify": round(ms, 4)},
+            "roofline": roof, "cpu_baseline": cpu, "kernel_ms": {"k_nym_verify" + ("" if bn else "_fbn"): round(ms, 4)},
             "setup_s": round(setup_s, 2)}), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -1,4 +1,4 @@
-// Batched idemix pseudonym-signature verification over BN254 (SURVEY.md
+// Batched idemix pseudonym-signature verification over BN254 and FP256BN (SURVEY.md
 // §8(f) row 4, the idemix half): the owner signatures of transfers whose
 // input tokens are owned by idemix identities.
 //
@@ -40,6 +40,7 @@
 #include "device/glv.hpp"
 #include "device/helpers.hpp"
 #include "device/transcript.hpp"
+#include "device/fp256bn.hpp"
 #include "host/bn254_host.hpp"
 
 namespace fts {
@@ -168,6 +169,185 @@ __global__ __launch_bounds__(256) void k_nym_verify(int n, const uint32_t* __res
   uint32_t diff = 0;
 #pragma unroll
   for (int k = 0; k < 8; k++) diff |= c2.v[k] ^ R[k];
+  status[i] = diff ? FTS_E_NYM_INVALID : FTS_OK;
+}
+
+// ------------------------------------------------------------ FP256BN keys
+// 16-bit unsigned fixed-base windows: entry (w, d) = d * 2^(16 w) * B, affine
+// Montgomery (16 words), d = 0 unused; 64 MiB per base (as the ECDSA table)
+constexpr int FBN_W = 16, FBN_NW = 16, FBN_ND = 1 << FBN_W;
+
+// lane per (base, window, digit); bases: affine Montgomery (16 words each)
+__global__ __launch_bounds__(256) void k_fbn_table(int nb, const uint32_t* __restrict__ bases,
+                                                   uint32_t* __restrict__ table) {
+  const size_t id = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (size_t)nb * FBN_NW * FBN_ND) return;
+  const int b = (int)(id / (FBN_NW * FBN_ND)), w = (int)((id / FBN_ND) % FBN_NW), d = (int)(id % FBN_ND);
+  uint32_t* out = table + id * 16;
+  if (d == 0) {
+    for (int i = 0; i < 16; i++) out[i] = 0;
+    return;
+  }
+  const fbn::Fp bx = fbn::load<fbn::PM>(bases + b * 16), by = fbn::load<fbn::PM>(bases + b * 16 + 8);
+  fbn::PJ p = fbn::pj_inf();
+  for (int k = FBN_W - 1; k >= 0; k--) {
+    p = fbn::pj_dbl(p);
+    if ((d >> k) & 1) p = fbn::pj_madd(p, bx, by);
+  }
+  for (int k = 0; k < FBN_W * w; k++) p = fbn::pj_dbl(p);
+  const fbn::Fp zi = p256::inv(p.z), zi2 = fbn::sqr(zi);
+  const fbn::Fp x = fbn::mul(p.x, zi2), y = fbn::mul(p.y, fbn::mul(zi2, zi));
+  for (int i = 0; i < 8; i++) out[i] = x.v[i], out[8 + i] = y.v[i];
+}
+
+// big-endian word j of the materialised stream region (length ltot bytes), with
+// the SHA-256 terminator / zero fill and the bit length in the last two words
+FTS_DEV uint32_t region_word(const uint32_t* __restrict__ m, uint32_t ltot, uint32_t nb, uint32_t g) {
+  const uint64_t bits = (uint64_t)ltot * 8u;
+  if (g == 16 * nb - 2) return (uint32_t)(bits >> 32);
+  if (g == 16 * nb - 1) return (uint32_t)bits;
+  return msg_word(m, ltot, g);
+}
+
+// digest (state words) as a big-endian integer mod r_fbn, plain LE limbs
+// (2^256 < 2 r: at most one subtraction)
+FTS_DEV void digest_mod_rfbn(const uint32_t st[8], uint32_t out[8]) {
+  uint32_t t[8], bw = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) out[i] = st[7 - i];
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = subb(out[i], fbn::RM::M[i], bw, bw);
+#pragma unroll
+  for (int i = 0; i < 8; i++) out[i] = bw ? out[i] : t[i];
+}
+
+// One FP256BN nym signature per lane.  The host materialises each item's hashed
+// stream "sign" || 0x04 || t (64 zero bytes) || Nym (65) || ipk.Hash || msg in
+// the region (word aligned); the kernel supplies t's words in registers.
+// nymxy: X || Y (64 bytes, big-endian; the 0x04 prefix checked on the host).
+__global__ __launch_bounds__(256) void k_nym_verify_fbn(int n, const uint32_t* __restrict__ rec,
+                                                        const uint8_t* __restrict__ nymxy,
+                                                        const uint32_t* __restrict__ region,
+                                                        const uint64_t* __restrict__ roff,  // word offsets
+                                                        const uint32_t* __restrict__ rlen,  // stream bytes
+                                                        const uint32_t* __restrict__ tables,
+                                                        int32_t* __restrict__ status) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || status[i] != FTS_OK) return;
+  const uint32_t* R = rec + (size_t)i * NREC;
+  uint32_t pw[16];
+  load_be_words(nymxy + (size_t)i * 64, pw);
+  uint32_t nx[8], ny[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) nx[k] = pw[7 - k], ny[k] = pw[15 - k];
+  if (!p256::lt256(nx, fbn::PM::M) || !p256::lt256(ny, fbn::PM::M)) {
+    status[i] = FTS_E_NYM_BADKEY;
+    return;
+  }
+  const fbn::Fp Qx = p256::to_mont(fbn::load<fbn::PM>(nx)), Qy = p256::to_mont(fbn::load<fbn::PM>(ny));
+  if (!fbn::on_curve(Qx, Qy)) {
+    status[i] = FTS_E_NYM_BADKEY;
+    return;
+  }
+  // s_sk HSk + s_rnym HRand: 2 x 16 mixed additions from the tables
+  fbn::PJ acc = fbn::pj_inf();
+#pragma unroll 1
+  for (int q = 0; q < 2; q++) {
+    const uint32_t* sc = R + 8 + 8 * q;
+    const uint32_t* tb = tables + (size_t)q * FBN_NW * FBN_ND * 16;
+    for (int w = 0; w < FBN_NW; w++) {
+      const uint32_t d = (sc[w >> 1] >> (16 * (w & 1))) & 0xffffu;
+      if (d) {
+        const uint32_t* t = tb + ((size_t)w * FBN_ND + d) * 16;
+        acc = fbn::pj_madd(acc, fbn::load<fbn::PM>(t), fbn::load<fbn::PM>(t + 8));
+      }
+    }
+  }
+  // (r - c) Nym: signed 4-bit windows over a table of 1..8 Nym (as k_ecdsa_verify)
+  uint32_t e[8];
+  {
+    uint32_t bw = 0, nz = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) nz |= R[k];
+#pragma unroll
+    for (int k = 0; k < 8; k++) e[k] = nz ? subb(fbn::RM::M[k], R[k], bw, bw) : 0u;
+  }
+  uint64_t cm = 0;
+  {
+    uint32_t c = 0;
+    for (int w = 0; w < 64; w++) {
+      cm |= (uint64_t)c << w;
+      c = ((e[w >> 3] >> (4 * (w & 7))) & 15u) + c > 8u;
+    }
+  }
+  const uint32_t c64 = (e[7] >> 28) + ((uint32_t)(cm >> 63) & 1u) > 8u;
+  fbn::PJ tab[9];
+  tab[0] = fbn::pj_inf();
+  tab[1].x = Qx, tab[1].y = Qy, tab[1].z = fbn::load<fbn::PM>(fbn::PM::ONE);
+  for (int k = 2; k < 9; k++) tab[k] = fbn::pj_madd(tab[k - 1], Qx, Qy);
+  fbn::PJ vb = c64 ? tab[1] : fbn::pj_inf();
+  for (int nib = 63; nib >= 0; nib--) {
+    vb = fbn::pj_dbl(fbn::pj_dbl(fbn::pj_dbl(fbn::pj_dbl(vb))));
+    const int raw = (int)((e[nib >> 3] >> (4 * (nib & 7))) & 15u);
+    const int cin = (int)((cm >> nib) & 1u);
+    const int cout = nib < 63 ? (int)((cm >> (nib + 1)) & 1u) : (int)c64;
+    const int d = raw + cin - 16 * cout;
+    if (d) {
+      fbn::PJ q = tab[d < 0 ? -d : d];
+      if (d < 0) q.y = fbn::sub(fbn::Fp{}, q.y);
+      vb = fbn::pj_add(vb, q);
+    }
+  }
+  const fbn::PJ X = fbn::pj_add(acc, vb);
+  uint32_t tw[16];
+  if (fbn::is_zero(X.z)) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) tw[k] = 0u;  // unreachable for honest data
+  } else {
+    const fbn::Fp zi = p256::inv(X.z), zi2 = fbn::sqr(zi);
+    const fbn::Fp ax = p256::from_mont(fbn::mul(X.x, zi2)), ay = p256::from_mont(fbn::mul(X.y, fbn::mul(zi2, zi)));
+#pragma unroll
+    for (int k = 0; k < 8; k++) tw[k] = ax.v[7 - k], tw[8 + k] = ay.v[7 - k];
+  }
+  const uint32_t* m = region + roff[i];
+  const uint32_t ltot = rlen[i];
+  const uint32_t nb = sha_blocks(ltot);  // >= 3
+  uint32_t st[8], w[16];
+  sha256_init(st);
+  // block 0: "sign" 0x04 t[0..58]
+  w[0] = 0x7369676eu;
+  w[1] = 0x04000000u | (tw[0] >> 8);
+#pragma unroll
+  for (int k = 2; k < 16; k++) w[k] = (tw[k - 2] << 24) | (tw[k - 1] >> 8);
+  sha256_compress(st, w);
+  // block 1: t[59..63] then the host's bytes (Nym, ipk.Hash, message)
+  w[0] = (tw[14] << 24) | (tw[15] >> 8);
+  w[1] = (tw[15] << 24) | (region_word(m, ltot, nb, 17) & 0x00ffffffu);
+#pragma unroll
+  for (int k = 2; k < 16; k++) w[k] = region_word(m, ltot, nb, 16 + k);
+  sha256_compress(st, w);
+  for (uint32_t blk = 2; blk < nb; blk++) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) w[k] = region_word(m, ltot, nb, 16 * blk + k);
+    sha256_compress(st, w);
+  }
+  uint32_t c1[8], c2[8];
+  digest_mod_rfbn(st, c1);
+#pragma unroll
+  for (int k = 0; k < 8; k++) w[k] = c1[7 - k];
+#pragma unroll
+  for (int k = 0; k < 8; k++) w[8 + k] = R[24 + k];
+  sha256_init(st);
+  sha256_compress(st, w);
+  w[0] = 0x80000000u;
+#pragma unroll
+  for (int k = 1; k < 15; k++) w[k] = 0u;
+  w[15] = 512u;
+  sha256_compress(st, w);
+  digest_mod_rfbn(st, c2);
+  uint32_t diff = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) diff |= c2[k] ^ R[k];
   status[i] = diff ? FTS_E_NYM_INVALID : FTS_OK;
 }
 
@@ -303,6 +483,68 @@ int32_t parse_nym_sig(const uint8_t* sig, size_t len, uint32_t* rec) {
   return FTS_OK;
 }
 
+const uint32_t kRfbn[8] = {0xd10b500du, 0xf62d536cu, 0x1299921au, 0x0cdc65fbu,
+                           0xee71a49eu, 0x46e5f25eu, 0xfffcf0cdu, 0xffffffffu};
+bool ge_m(const uint32_t a[8], const uint32_t m[8]) {
+  for (int k = 7; k >= 0; k--)
+    if (a[k] != m[k]) return a[k] > m[k];
+  return true;
+}
+void sub_m(uint32_t a[8], const uint32_t m[8]) {
+  uint64_t bw = 0;
+  for (int k = 0; k < 8; k++) {
+    const uint64_t d = (uint64_t)a[k] - m[k] - bw;
+    a[k] = (uint32_t)d;
+    bw = (d >> 63) & 1;
+  }
+}
+// FP256BN_AMCL Zr from bytes: AMCL FromBytes reads exactly the first 32 bytes
+// (a shorter field makes the Go code index out of range -> FTS_E_NYM_MALFORMED)
+int32_t parse_nym_sig_fbn(const uint8_t* sig, size_t len, uint32_t* rec) {
+  memset(rec, 0, NREC * 4);
+  if (!sig || len == 0) return FTS_E_NYM_MALFORMED;
+  Pb pb{sig, len};
+  const uint8_t* fv[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  size_t fl[5] = {0, 0, 0, 0, 0};
+  while (pb.o < pb.n) {
+    uint32_t f, wt;
+    const uint8_t* v;
+    size_t vl;
+    uint64_t iv;
+    if (!pb.next(f, wt, v, vl, iv)) return FTS_E_NYM_MALFORMED;
+    if (f >= 1 && f <= 4) {
+      if (wt != 2) return FTS_E_NYM_MALFORMED;
+      fv[f] = v, fl[f] = vl;
+    }
+  }
+  for (int f = 1; f <= 4; f++)
+    if (fl[f] < 32) return FTS_E_NYM_MALFORMED;
+  uint32_t v[4][8];
+  for (int f = 1; f <= 4; f++) be_to_limbs(fv[f], 32, v[f - 1]);
+  for (int q = 1; q <= 2; q++)  // s mod r (2^256 < 2 r: one subtraction)
+    if (ge_m(v[q], kRfbn)) sub_m(v[q], kRfbn);
+  memcpy(rec + 8, v[1], 32);
+  memcpy(rec + 16, v[2], 32);
+  for (int k = 0; k < 8; k++) rec[24 + k] = v[3][7 - k];
+  if (ge_m(v[0], kRfbn)) return FTS_E_NYM_INVALID;  // Zr.Equals: an unreduced c never matches
+  memcpy(rec, v[0], 32);
+  return FTS_OK;
+}
+
+// FP256BN issuer bases: plain big-endian ECP coordinates -> Montgomery, on-curve flags
+__global__ void k_fbn_bases(int nb, const uint32_t* __restrict__ plain, uint32_t* __restrict__ mont,
+                            int32_t* __restrict__ ok) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  uint32_t x[8], y[8];
+  for (int k = 0; k < 8; k++) x[k] = plain[b * 16 + k], y[k] = plain[b * 16 + 8 + k];
+  bool good = p256::lt256(x, fbn::PM::M) && p256::lt256(y, fbn::PM::M);
+  const fbn::Fp mx = p256::to_mont(fbn::load<fbn::PM>(x)), my = p256::to_mont(fbn::load<fbn::PM>(y));
+  good = good && fbn::on_curve(mx, my);
+  for (int k = 0; k < 8; k++) mont[b * 16 + k] = mx.v[k], mont[b * 16 + 8 + k] = my.v[k];
+  ok[b] = good ? 1 : 0;
+}
+
 #define ICHK(x)                                    \
   do {                                             \
     if ((x) != hipSuccess) return FTS_API_EDEVICE; \
@@ -323,6 +565,7 @@ struct Slot {
 
 struct fts_idemix_ipk {
   int device = -1;
+  int curve = 1;                 // mathlib CurveID: 1 BN254, 0 FP256BN_AMCL
   uint32_t* d_tables = nullptr;  // HSk, HRand (FB_W-bit windows)
   uint32_t* d_hash = nullptr;    // ipk.Hash as 8 big-endian words
   uint8_t hash[32];
@@ -373,8 +616,9 @@ bool ecp_point(const uint8_t* v, size_t vl, host::G1A& out) {
 
 extern "C" {
 
-int fts_idemix_ipk_create(int device, const uint8_t* ipk, size_t ipk_len, fts_idemix_ipk** out) {
-  if (!out || !ipk || !ipk_len) return FTS_API_EINVAL;
+int fts_idemix_ipk_create(int device, const uint8_t* ipk, size_t ipk_len, int curve_id, fts_idemix_ipk** out) {
+  if (!out || !ipk || !ipk_len || (curve_id != FTS_CURVE_BN254 && curve_id != FTS_CURVE_FP256BN_AMCL))
+    return FTS_API_EINVAL;
   *out = nullptr;
   // IssuerPublicKey: 2 h_sk, 3 h_rand (ECP), 10 hash
   Pb pb{ipk, ipk_len};
@@ -391,12 +635,37 @@ int fts_idemix_ipk_create(int device, const uint8_t* ipk, size_t ipk_len, fts_id
     if (f == 3) hr = v, hrl = vl;
     if (f == 10) hash = v, hashl = vl;
   }
-  host::G1A base[2];
-  if (!hsk || !hr || !ecp_point(hsk, hskl, base[0]) || !ecp_point(hr, hrl, base[1])) return FTS_API_EPP;
+  if (!hsk || !hr) return FTS_API_EPP;
+  host::G1A base[2]{};
+  uint32_t plain[32];  // FP256BN: plain coordinates, little-endian limbs
+  if (curve_id == FTS_CURVE_BN254) {
+    if (!ecp_point(hsk, hskl, base[0]) || !ecp_point(hr, hrl, base[1])) return FTS_API_EPP;
+  } else {
+    const uint8_t* e[2] = {hsk, hr};
+    const size_t el[2] = {hskl, hrl};
+    for (int b = 0; b < 2; b++) {
+      Pb q{e[b], el[b]};
+      const uint8_t *x = nullptr, *y = nullptr;
+      size_t xl = 0, yl = 0;
+      while (q.o < q.n) {
+        uint32_t f, wt;
+        const uint8_t* fv;
+        size_t fl;
+        uint64_t iv;
+        if (!q.next(f, wt, fv, fl, iv)) return FTS_API_EPP;
+        if (f == 1 && wt == 2) x = fv, xl = fl;
+        if (f == 2 && wt == 2) y = fv, yl = fl;
+      }
+      if (xl != 32 || yl != 32) return FTS_API_EPP;
+      be_to_limbs(x, 32, plain + b * 16);
+      be_to_limbs(y, 32, plain + b * 16 + 8);
+    }
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return FTS_API_EDEVICE;
   fts_idemix_ipk* k = new fts_idemix_ipk();
   k->device = device;
+  k->curve = curve_id;
   // copy(proofData[index:], ipk.Hash) into a FieldBytes window
   memset(k->hash, 0, 32);
   if (hash) memcpy(k->hash, hash, std::min<size_t>(hashl, 32));
@@ -417,18 +686,40 @@ int fts_idemix_ipk_create(int device, const uint8_t* ipk, size_t ipk_len, fts_id
   uint32_t* d_bases = nullptr;
   uint32_t* d_scr = nullptr;
   hipStream_t s0 = nullptr;
+  const bool bn = curve_id == FTS_CURVE_BN254;
+  const size_t tab_b = bn ? 2 * fb_words_per_base() * 4 : (size_t)2 * FBN_NW * FBN_ND * 16 * 4;
+  const size_t scr_b = bn ? table_build_scratch_bytes(2) : 2 * 16 * 4 + 64;
   bool ok = hipStreamCreateWithFlags(&s0, hipStreamNonBlocking) == hipSuccess &&
-            hipMalloc(&k->d_tables, 2 * fb_words_per_base() * 4) == hipSuccess &&
-            hipMalloc(&k->d_hash, 32) == hipSuccess && hipMalloc(&d_bases, sizeof(hb)) == hipSuccess &&
-            hipMalloc(&d_scr, table_build_scratch_bytes(2)) == hipSuccess &&
-            hipMemcpyAsync(d_bases, hb, sizeof(hb), hipMemcpyHostToDevice, s0) == hipSuccess &&
+            hipMalloc(&k->d_tables, tab_b) == hipSuccess && hipMalloc(&k->d_hash, 32) == hipSuccess &&
+            hipMalloc(&d_bases, sizeof(hb)) == hipSuccess && hipMalloc(&d_scr, scr_b) == hipSuccess &&
+            hipMemcpyAsync(d_bases, bn ? hb : plain, sizeof(hb), hipMemcpyHostToDevice, s0) == hipSuccess &&
             hipMemcpyAsync(k->d_hash, hw, 32, hipMemcpyHostToDevice, s0) == hipSuccess;
-  if (ok) {
+  bool on_curve = true;
+  if (ok && bn) {
     launch_build_tables(d_bases, 2, k->d_tables, d_scr, s0);
     ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(s0) == hipSuccess;
+  } else if (ok) {
+    // plain -> Montgomery + on-curve flags (into the scratch), then the window tables
+    uint32_t* mont = d_scr;
+    int32_t* flags = reinterpret_cast<int32_t*>(d_scr + 32);
+    int32_t hf[2] = {0, 0};
+    k_fbn_bases<<<1, 64, 0, s0>>>(2, d_bases, mont, flags);
+    ok = hipGetLastError() == hipSuccess &&
+         hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, s0) == hipSuccess &&
+         hipStreamSynchronize(s0) == hipSuccess;
+    on_curve = hf[0] == 1 && hf[1] == 1;
+    if (ok && on_curve) {
+      const size_t ent = (size_t)2 * FBN_NW * FBN_ND;
+      k_fbn_table<<<(unsigned)((ent + 255) / 256), 256, 0, s0>>>(2, mont, k->d_tables);
+      ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(s0) == hipSuccess;
+    }
   }
   if (d_bases) (void)hipFree(d_bases);
   if (d_scr) (void)hipFree(d_scr);
+  if (ok && !on_curve) {
+    if (s0) (void)hipStreamDestroy(s0);
+    return fail(FTS_API_EPP);
+  }
   if (s0) (void)hipStreamDestroy(s0);
   for (auto& S : k->slot) {
     ok = ok && hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) == hipSuccess;
@@ -462,10 +753,14 @@ int fts_idemix_identity_nym(const uint8_t* id, size_t len, const uint8_t** nym, 
 int fts_nym_verify_batch(fts_idemix_ipk* K, size_t n, const fts_nym_item* items, int32_t* status) {
   if (!K || n > (size_t)(1u << 24) || (n && (!items || !status))) return FTS_API_EINVAL;
   if (n == 0) return FTS_API_OK;
-  size_t mtot_w = 0;  // message words (each message padded to whole words)
+  // message words per item: BN254 the message alone; FP256BN the whole hashed
+  // stream (166-byte prefix + message), each padded to whole words + 1
+  const bool bn = K->curve == FTS_CURVE_BN254;
+  const size_t pre = bn ? 0 : 166;
+  size_t mtot_w = 0;
   for (size_t i = 0; i < n; i++) {
     if (items[i].msg_len > 0xffffff00u || (items[i].msg_len && !items[i].msg)) return FTS_API_EINVAL;
-    mtot_w += (items[i].msg_len + 3) / 4 + 1;
+    mtot_w += (pre + items[i].msg_len + 3) / 4 + 1;
   }
   int k = -1;
   {
@@ -513,25 +808,34 @@ int fts_nym_verify_batch(fts_idemix_ipk* K, size_t n, const fts_nym_item* items,
   uint64_t* hoff = reinterpret_cast<uint64_t*>(h + o_off);
   {
     uint64_t o = 0;
-    for (size_t i = 0; i < n; i++) hoff[i] = o, o += (items[i].msg_len + 3) / 4 + 1;
+    for (size_t i = 0; i < n; i++) hoff[i] = o, o += (pre + items[i].msg_len + 3) / 4 + 1;
   }
   auto pack = [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; i++) {
       const fts_nym_item& it = items[i];
       uint32_t* rec = reinterpret_cast<uint32_t*>(h) + i * NREC;
-      int32_t st = parse_nym_sig(it.sig, it.sig_len, rec);
+      int32_t st = bn ? parse_nym_sig(it.sig, it.sig_len, rec) : parse_nym_sig_fbn(it.sig, it.sig_len, rec);
       uint8_t* nr = h + o_nym + i * 64;
-      if (it.nym && it.nym_len == 64) memcpy(nr, it.nym, 64);
-      else memset(nr, 0, 64);
       // NymPublicKey import (crypto/deserializer.go:49-56) precedes Verify: a key of
-      // the wrong length fails first; its point checks run on the device
-      if (!it.nym || it.nym_len != 64) st = FTS_E_NYM_BADKEY;
+      // the wrong length / form fails first; its point checks run on the device.
+      // BN254: G1.Bytes() raw X||Y (64 B); FP256BN: ECP.ToBytes 0x04||X||Y (65 B).
+      const bool key_ok = it.nym && (bn ? it.nym_len == 64 : it.nym_len == 65 && it.nym[0] == 0x04);
+      if (key_ok) memcpy(nr, it.nym + (bn ? 0 : 1), 64);
+      else memset(nr, 0, 64), st = FTS_E_NYM_BADKEY;
       reinterpret_cast<int32_t*>(h + o_st)[i] = st;
-      reinterpret_cast<uint32_t*>(h + o_len)[i] = (uint32_t)it.msg_len;
+      reinterpret_cast<uint32_t*>(h + o_len)[i] = (uint32_t)(pre + it.msg_len);
       uint8_t* mw = h + o_msg + hoff[i] * 4;
-      const size_t wl = ((it.msg_len + 3) / 4 + 1) * 4;
-      if (it.msg_len) memcpy(mw, it.msg, it.msg_len);
-      memset(mw + it.msg_len, 0, wl - it.msg_len);
+      const size_t wl = ((pre + it.msg_len + 3) / 4 + 1) * 4;
+      if (!bn) {  // "sign" || 0x04 || t (device) || Nym || ipk.Hash
+        memcpy(mw, "sign", 4);
+        mw[4] = 0x04;
+        memset(mw + 5, 0, 64);
+        if (key_ok) memcpy(mw + 69, it.nym, 65);
+        else memset(mw + 69, 0, 65);
+        memcpy(mw + 134, K->hash, 32);
+      }
+      if (it.msg_len) memcpy(mw + pre, it.msg, it.msg_len);
+      memset(mw + pre + it.msg_len, 0, wl - pre - it.msg_len);
     }
   };
   const size_t CH = 2048, nch = (n + CH - 1) / CH;
@@ -552,10 +856,16 @@ int fts_nym_verify_batch(fts_idemix_ipk* K, size_t n, const fts_nym_item* items,
   uint8_t* d = D.d_buf;
   ICHK(hipMemcpyAsync(d, h, h_need, hipMemcpyHostToDevice, D.stream));
   ICHK(hipEventRecord(D.ev[0], D.stream));
-  k_nym_verify<<<(unsigned)((n + 255) / 256), 256, 0, D.stream>>>(
-      (int)n, reinterpret_cast<const uint32_t*>(d), d + o_nym, reinterpret_cast<const uint32_t*>(d + o_msg),
-      reinterpret_cast<const uint64_t*>(d + o_off), reinterpret_cast<const uint32_t*>(d + o_len), K->d_tables,
-      K->d_hash, reinterpret_cast<uint32_t*>(d + o_vt), reinterpret_cast<int32_t*>(d + o_st));
+  if (bn)
+    k_nym_verify<<<(unsigned)((n + 255) / 256), 256, 0, D.stream>>>(
+        (int)n, reinterpret_cast<const uint32_t*>(d), d + o_nym, reinterpret_cast<const uint32_t*>(d + o_msg),
+        reinterpret_cast<const uint64_t*>(d + o_off), reinterpret_cast<const uint32_t*>(d + o_len), K->d_tables,
+        K->d_hash, reinterpret_cast<uint32_t*>(d + o_vt), reinterpret_cast<int32_t*>(d + o_st));
+  else
+    k_nym_verify_fbn<<<(unsigned)((n + 255) / 256), 256, 0, D.stream>>>(
+        (int)n, reinterpret_cast<const uint32_t*>(d), d + o_nym, reinterpret_cast<const uint32_t*>(d + o_msg),
+        reinterpret_cast<const uint64_t*>(d + o_off), reinterpret_cast<const uint32_t*>(d + o_len), K->d_tables,
+        reinterpret_cast<int32_t*>(d + o_st));
   ICHK(hipGetLastError());
   ICHK(hipEventRecord(D.ev[1], D.stream));
   ICHK(hipMemcpyAsync(h + o_st, d + o_st, st_b, hipMemcpyDeviceToHost, D.stream));

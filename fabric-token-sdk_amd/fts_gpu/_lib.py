@@ -31,6 +31,9 @@ FTS_E_SIG_INVALID = 15
 FTS_E_NYM_MALFORMED = 16
 FTS_E_NYM_BADKEY = 17
 FTS_E_NYM_INVALID = 18
+# mathlib CurveID of idemix issuer keys
+FTS_CURVE_FP256BN_AMCL = 0
+FTS_CURVE_BN254 = 1
 
 FTS_API_OK = 0
 FTS_DEVICE_NONE = -2
@@ -146,7 +149,7 @@ def _load():
         "fts_ctx_create_mask": ([U8P, S, C.c_uint32, C.c_uint64, C.POINTER(P)], C.c_int),
         "fts_ctx_devices": ([P, I32P, C.c_int], C.c_int),
         "fts_shard_plan": ([S, C.POINTER(C.c_double), C.c_int, C.POINTER(S)], C.c_int),
-        "fts_idemix_ipk_create": ([C.c_int, U8P, S, C.POINTER(P)], C.c_int),
+        "fts_idemix_ipk_create": ([C.c_int, U8P, S, C.c_int, C.POINTER(P)], C.c_int),
         "fts_idemix_ipk_destroy": ([P], None),
         "fts_nym_verify_batch": ([P, S, C.POINTER(NymItem), I32P], C.c_int),
         "fts_idemix_identity_nym": ([U8P, S, C.POINTER(C.c_void_p), C.POINTER(S)], C.c_int),

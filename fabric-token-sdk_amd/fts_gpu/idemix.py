@@ -10,7 +10,8 @@ Mirrors services/identity/idemix/crypto/id.go:145-161:
   (TransferSignatureValidate, validator/validator_transfer.go:29-62).
 
 The issuer key is the idemix IssuerPublicKey proto a zkatdlog PublicParams
-carries (BN254 curve).  There is no CPU fallback: every verdict comes from
+carries, on BN254 (the tokengen key of zkatdlog_pp.json) or FP256BN_AMCL (the
+validator's test keys).  There is no CPU fallback: every verdict comes from
 the HIP kernel k_nym_verify.
 """
 import ctypes as C
@@ -19,6 +20,7 @@ import numpy as np
 
 from . import _lib as L
 from ._lib import FTS_OK, FTS_E_NYM_MALFORMED, FTS_E_NYM_BADKEY, FTS_E_NYM_INVALID  # noqa: F401
+from ._lib import FTS_CURVE_BN254, FTS_CURVE_FP256BN_AMCL  # noqa: F401
 
 
 class SignatureError(Exception):
@@ -44,11 +46,15 @@ def identity_nym(serialized_identity):
 class IssuerKey:
     """Device-resident idemix issuer public key (HSk / HRand fixed-base tables)."""
 
-    def __init__(self, ipk, device=0):
+    def __init__(self, ipk, device=0, curve=FTS_CURVE_BN254):
+        """curve: mathlib CurveID (PublicParams.IdemixIssuerPublicKeys[i].Curve)."""
         self.ipk = bytes(ipk)
         self.device = device
+        self.curve = curve
+        self.nym_len = 64 if curve == FTS_CURVE_BN254 else 65
         h = C.c_void_p()
-        L.check("fts_idemix_ipk_create", L.lib.fts_idemix_ipk_create(int(device), self.ipk, len(self.ipk), C.byref(h)))
+        L.check("fts_idemix_ipk_create",
+                L.lib.fts_idemix_ipk_create(int(device), self.ipk, len(self.ipk), int(curve), C.byref(h)))
         self.h = h
 
     def close(self):
@@ -85,15 +91,16 @@ class IssuerKey:
         return st
 
     def verify_packed(self, nym_buf, sig_buf, sig_off, sig_len, msg_buf, msg_off, msg_len):
-        """Zero-copy batch over contiguous buffers (64-byte nyms back to back);
+        """Zero-copy batch over contiguous buffers (nym keys of self.nym_len bytes back to back);
         bounds are checked here before any raw pointer is formed."""
         n = len(sig_off)
         so, sl = np.asarray(sig_off, dtype=np.uint64), np.asarray(sig_len, dtype=np.uint64)
         mo, ml = np.asarray(msg_off, dtype=np.uint64), np.asarray(msg_len, dtype=np.uint64)
         if not (so.shape == sl.shape == mo.shape == ml.shape == (n,)):
             raise ValueError("offset and length arrays must be 1-D and of equal length")
-        if len(nym_buf) < 64 * n:
-            raise ValueError("nym_buf holds %d bytes, %d items need %d" % (len(nym_buf), n, 64 * n))
+        nl = self.nym_len
+        if len(nym_buf) < nl * n:
+            raise ValueError("nym_buf holds %d bytes, %d items need %d" % (len(nym_buf), n, nl * n))
         for name, off, ln, buf in (("sig", so, sl, sig_buf), ("msg", mo, ml, msg_buf)):
             size = np.uint64(len(buf))
             if n and ((off > size).any() or (ln > size - np.minimum(off, size)).any()):
@@ -102,8 +109,8 @@ class IssuerKey:
         items = np.zeros(n, dtype=[("nym", "u8"), ("nym_len", "u8"), ("sig", "u8"), ("sig_len", "u8"),
                                    ("msg", "u8"), ("msg_len", "u8")])
         nb, sb, mb = (np.frombuffer(b, dtype=np.uint8) for b in (nym_buf, sig_buf, msg_buf))
-        items["nym"] = nb.ctypes.data + 64 * np.arange(n, dtype=np.uint64)
-        items["nym_len"] = 64
+        items["nym"] = nb.ctypes.data + nl * np.arange(n, dtype=np.uint64)
+        items["nym_len"] = nl
         items["sig"] = sb.ctypes.data + so
         items["sig_len"] = sl
         items["msg"] = mb.ctypes.data + mo

@@ -361,12 +361,18 @@ int fts_ecdsa_last_timings(int device, float* ms2);
  * for an idemix identity; called by TransferSignatureValidate
  * (validator/validator_transfer.go:29-62) once per input owner.
  * One handle per issuer public key (the idemix IssuerPublicKey proto, as held in
- * PublicParams.IdemixIssuerPublicKeys): HSk / HRand fixed-base tables in HBM. */
+ * PublicParams.IdemixIssuerPublicKeys): HSk / HRand fixed-base tables in HBM
+ * (BN254: 2 x 32 MiB; FP256BN_AMCL: 2 x 64 MiB).  FTS_API_EPP for a key that does not
+ * parse or whose HSk / HRand are not on the curve. */
 typedef struct fts_idemix_ipk fts_idemix_ipk;
-int fts_idemix_ipk_create(int device, const uint8_t* ipk, size_t ipk_len, fts_idemix_ipk** out);
+/* curve_id: mathlib CurveID of the key (PublicParams.IdemixIssuerPublicKeys[i].Curve) */
+#define FTS_CURVE_FP256BN_AMCL 0
+#define FTS_CURVE_BN254 1
+int fts_idemix_ipk_create(int device, const uint8_t* ipk, size_t ipk_len, int curve_id, fts_idemix_ipk** out);
 void fts_idemix_ipk_destroy(fts_idemix_ipk* ipk);
 typedef struct {
-  const uint8_t* nym; /* NymPublicKey bytes: G1.Bytes() (64 B raw X||Y), see fts_idemix_identity_nym */
+  const uint8_t* nym; /* NymPublicKey bytes: G1.Bytes() (BN254: 64 B raw X||Y; FP256BN: 65 B 0x04||X||Y),
+                         see fts_idemix_identity_nym */
   size_t nym_len;
   const uint8_t* sig; /* NymSignature proto (proof_c, proof_s_sk, proof_s_r_nym, nonce) */
   size_t sig_len;

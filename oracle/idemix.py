@@ -1,4 +1,4 @@
-"""Idemix pseudonym (nym) signatures over BN254, restated in pure Python
+"""Idemix pseudonym (nym) signatures over BN254 and FP256BN, restated in pure Python
 (oracle; TEST INFRASTRUCTURE ONLY -- never imported by the product path).
 
 Reference call sites (fabric-token-sdk):
@@ -212,14 +212,108 @@ def zr_bytes(z):
     return z.to_bytes(n, "big")
 
 
+# --------------------------------------------------------------------- curves
+class _Bn254:
+    """mathlib BN254 (gurvy / gnark-crypto): G1.Bytes() = 64-byte raw X || Y,
+    NewZrFromBytes = big-endian integer of any length (not reduced)."""
+    name, p, r, g1_len = "BN254", P, R, 64
+
+    add, neg, mul = staticmethod(g1_add), staticmethod(g1_neg), staticmethod(g1_mul)
+    g1_bytes, g1_from_bytes = staticmethod(g1_bytes), staticmethod(g1_from_bytes)
+
+    def hash_to_zr(self, m):
+        return int.from_bytes(hashlib.sha256(m).digest(), "big") % R
+
+    @staticmethod
+    def zr_from_field(b):
+        return int.from_bytes(b, "big")
+
+    def ecp(self, x, y):
+        return g1_from_bytes(x + y)
+
+
+class _Fp256bn:
+    """mathlib FP256BN_AMCL (y^2 = x^3 + 3): G1.Bytes() = ECP.ToBytes(uncompressed),
+    0x04 || X || Y (65 bytes); Zr from bytes = AMCL FromBytes, which reads exactly
+    the first 32 bytes (a shorter field makes the Go code panic)."""
+    name = "FP256BN_AMCL"
+    p = 0xFFFFFFFFFFFCF0CD46E5F25EEE71A49F0CDC65FB12980A82D3292DDBAED33013
+    r = 0xFFFFFFFFFFFCF0CD46E5F25EEE71A49E0CDC65FB1299921AF62D536CD10B500D
+    g1_len = 65
+
+    def on_curve(self, pt):
+        x, y = pt
+        return (y * y - x * x * x - 3) % self.p == 0
+
+    def add(self, a, b):
+        p = self.p
+        if a is None:
+            return b
+        if b is None:
+            return a
+        if a[0] == b[0]:
+            if (a[1] + b[1]) % p == 0:
+                return None
+            lam = 3 * a[0] * a[0] * pow(2 * a[1], p - 2, p) % p
+        else:
+            lam = (b[1] - a[1]) * pow(b[0] - a[0], p - 2, p) % p
+        x = (lam * lam - a[0] - b[0]) % p
+        return (x, (lam * (a[0] - x) - a[1]) % p)
+
+    def neg(self, a):
+        return None if a is None else (a[0], (-a[1]) % self.p)
+
+    def mul(self, pt, k):
+        acc = None
+        for bit in bin(k % self.r)[2:]:
+            acc = self.add(acc, acc)
+            if bit == "1":
+                acc = self.add(acc, pt)
+        return acc
+
+    def g1_bytes(self, pt):
+        if pt is None:  # unreachable for honest data; unpinned
+            return b"\x04" + bytes(64)
+        return b"\x04" + pt[0].to_bytes(32, "big") + pt[1].to_bytes(32, "big")
+
+    def g1_from_bytes(self, b):
+        # 65-byte uncompressed only; an off-curve or non-canonical key is rejected
+        # (AMCL would yield the point at infinity: the verdict is a rejection either way)
+        if len(b) != 65 or b[0] != 4:
+            raise PointError("invalid point encoding")
+        x, y = int.from_bytes(b[1:33], "big"), int.from_bytes(b[33:], "big")
+        if x >= self.p or y >= self.p or not self.on_curve((x, y)):
+            raise PointError("point not on curve")
+        return (x, y)
+
+    def hash_to_zr(self, m):
+        return int.from_bytes(hashlib.sha256(m).digest(), "big") % self.r
+
+    @staticmethod
+    def zr_from_field(b):
+        if len(b) < 32:
+            raise ValueError("short Zr")  # AMCL FromBytes indexes 32 bytes: the reference panics
+        return int.from_bytes(b[:32], "big")
+
+    def ecp(self, x, y):
+        pt = (int.from_bytes(x, "big"), int.from_bytes(y, "big"))
+        if not self.on_curve(pt):
+            raise PointError("ECP not on curve")
+        return pt
+
+
+BN254C, FP256BNC = _Bn254(), _Fp256bn()
+CURVES = {1: BN254C, 0: FP256BNC}  # mathlib CurveID: FP256BN_AMCL = 0, BN254 = 1
+
+
 # ---------------------------------------------------------------- issuer key
-def _ecp(raw):
-    """idemix ECP{x, y} proto -> G1 point (gurvy translator: x || y raw bytes)."""
+def _ecp(raw, curve=BN254C):
+    """idemix ECP{x, y} proto -> G1 point (translator: 32-byte big-endian x, y)."""
     f = pb_fields(raw)
     x, y = _pb_bytes(f, 1), _pb_bytes(f, 2)
     if len(x) != 32 or len(y) != 32:
         raise PointError("ECP coordinate length")
-    return g1_from_bytes(x + y)
+    return curve.ecp(x, y)
 
 
 def _ecp2(raw):
@@ -230,18 +324,20 @@ def _ecp2(raw):
     return g2_from_bytes(b"".join(parts))
 
 
-def parse_ipk(raw):
+def parse_ipk(raw, curve=BN254C):
     """idemix IssuerPublicKey proto (fields: 1 attribute_names, 2 h_sk, 3 h_rand,
-    4 h_attrs, 5 w, 6 bar_g1, 7 bar_g2, 8 proof_c, 9 proof_s, 10 hash)."""
+    4 h_attrs, 5 w, 6 bar_g1, 7 bar_g2, 8 proof_c, 9 proof_s, 10 hash).  W (G2)
+    is decoded for BN254 only (the FP256BN G2 encoding is not needed for nyms)."""
     f = pb_fields(raw)
     return {
+        "curve": curve,
         "attribute_names": [v.decode() for ff, _, v in f if ff == 1],
-        "h_sk": _ecp(_pb_bytes(f, 2)),
-        "h_rand": _ecp(_pb_bytes(f, 3)),
-        "h_attrs": [_ecp(v) for ff, _, v in f if ff == 4],
-        "w": _ecp2(_pb_bytes(f, 5)),
-        "bar_g1": _ecp(_pb_bytes(f, 6)),
-        "bar_g2": _ecp(_pb_bytes(f, 7)),
+        "h_sk": _ecp(_pb_bytes(f, 2), curve),
+        "h_rand": _ecp(_pb_bytes(f, 3), curve),
+        "h_attrs": [_ecp(v, curve) for ff, _, v in f if ff == 4],
+        "w": _ecp2(_pb_bytes(f, 5)) if curve is BN254C else _pb_bytes(f, 5),
+        "bar_g1": _ecp(_pb_bytes(f, 6), curve),
+        "bar_g2": _ecp(_pb_bytes(f, 7), curve),
         "proof_c": _pb_bytes(f, 8),
         "proof_s": _pb_bytes(f, 9),
         "hash": _pb_bytes(f, 10),
@@ -287,28 +383,34 @@ def encode_nym_sig(c, s_sk, s_rnym, nonce):
     return b"".join(pb_bytes_field(f, zr_bytes(v)) for f, v in ((1, c), (2, s_sk), (3, s_rnym), (4, nonce)))
 
 
-def decode_nym_sig(raw):
+def decode_nym_sig(raw, curve=BN254C):
     f = pb_fields(raw)
-    return tuple(int.from_bytes(_pb_bytes(f, i), "big") for i in (1, 2, 3, 4))
+    return tuple(curve.zr_from_field(_pb_bytes(f, i)) for i in (1, 2, 3, 4))
 
 
 def make_nym(ipk, sk, r_nym):
     """MakeNym: Nym = HSk^sk * HRand^r_nym."""
-    return g1_add(g1_mul(ipk["h_sk"], sk), g1_mul(ipk["h_rand"], r_nym))
+    C = ipk["curve"]
+    return C.add(C.mul(ipk["h_sk"], sk), C.mul(ipk["h_rand"], r_nym))
 
 
-def _challenge(t, nym, ipk_hash, msg, nonce):
-    data = SIGN_LABEL + g1_bytes(t) + g1_bytes(nym) + ipk_hash[:32].ljust(32, b"\0") + msg
-    c1 = hash_to_zr(data)
-    return hash_to_zr(zr_bytes(c1) + zr_bytes(nonce))
+def nym_bytes(ipk, nym):
+    return ipk["curve"].g1_bytes(nym)
+
+
+def _challenge(C, t, nym, ipk_hash, msg, nonce):
+    data = SIGN_LABEL + C.g1_bytes(t) + C.g1_bytes(nym) + ipk_hash[:32].ljust(32, b"\0") + msg
+    c1 = C.hash_to_zr(data)
+    return C.hash_to_zr(zr_bytes(c1) + zr_bytes(nonce))
 
 
 def nym_sign(ipk, sk, nym, r_nym, msg, rng):
     """NewNymSignature with randomness from `rng` (random.Random; fixtures only)."""
-    nonce, r_sk, r_r = (rng.randrange(R) for _ in range(3))
-    t = g1_add(g1_mul(ipk["h_sk"], r_sk), g1_mul(ipk["h_rand"], r_r))
-    c = _challenge(t, nym, ipk["hash"], msg, nonce)
-    return encode_nym_sig(c, (r_sk + c * sk) % R, (r_r + c * r_nym) % R, nonce)
+    C = ipk["curve"]
+    nonce, r_sk, r_r = (rng.randrange(C.r) for _ in range(3))
+    t = C.add(C.mul(ipk["h_sk"], r_sk), C.mul(ipk["h_rand"], r_r))
+    c = _challenge(C, t, nym, ipk["hash"], msg, nonce)
+    return encode_nym_sig(c, (r_sk + c * sk) % C.r, (r_r + c * r_nym) % C.r, nonce)
 
 
 class NymError(ValueError):
@@ -321,18 +423,19 @@ def nym_verify(ipk, nym_bytes, sig, msg):
     # proto / point details that are not part of the verdict)
     if len(sig) == 0:  # bccsp: an empty signature is rejected before Unmarshal
         raise NymError(MSG_MALFORMED)
+    C = ipk["curve"]
     try:
-        c, s_sk, s_r, nonce = decode_nym_sig(sig)
+        c, s_sk, s_r, nonce = decode_nym_sig(sig, C)
     except ValueError:
         raise NymError(MSG_MALFORMED)
     if nonce >> 256:  # mathlib BigToBytes panics on a Zr wider than 32 bytes
         raise NymError(MSG_MALFORMED)
     try:
-        nym = g1_from_bytes(nym_bytes)
+        nym = C.g1_from_bytes(nym_bytes)
     except PointError:
         raise NymError(MSG_BADKEY)
-    t = g1_add(g1_add(g1_mul(ipk["h_sk"], s_sk), g1_mul(ipk["h_rand"], s_r)), g1_neg(g1_mul(nym, c)))
-    if c != _challenge(t, nym, ipk["hash"], msg, nonce):
+    t = C.add(C.add(C.mul(ipk["h_sk"], s_sk), C.mul(ipk["h_rand"], s_r)), C.neg(C.mul(nym, c)))
+    if c != _challenge(C, t, nym, ipk["hash"], msg, nonce):
         raise NymError(MSG_INVALID)
 
 

@@ -16,8 +16,11 @@ import pytest
 from conftest import GOLDEN, PP_PATH
 
 with open(os.path.join(GOLDEN, "idemix_golden.json")) as f:
-    GOLD = json.load(f)
+    GOLD_ALL = json.load(f)
+GOLD = GOLD_ALL["bn254"]
 IPK = bytes.fromhex(GOLD["ipk"])
+GOLD_FBN = GOLD_ALL["fp256bn"]
+IPK_FBN = bytes.fromhex(GOLD_FBN["ipk"])
 
 
 def test_pp_carries_the_fixture_issuer_key():
@@ -49,15 +52,40 @@ def ipk_dev():
     k.close()
 
 
-@pytest.mark.gpu
-def test_golden_verdicts(ipk_dev):
+@pytest.fixture(scope="module")
+def ipk_fbn():
     from fts_gpu import idemix as I
-    cases = GOLD["cases"]
-    st = ipk_dev.verify_batch([bytes.fromhex(c["nym"]) for c in cases], [bytes.fromhex(c["sig"]) for c in cases],
-                              [bytes.fromhex(c["msg"]) for c in cases])
+    k = I.IssuerKey(IPK_FBN, device=0, curve=I.FTS_CURVE_FP256BN_AMCL)
+    yield k
+    k.close()
+
+
+def _golden(dev, gold):
+    from fts_gpu import idemix as I
+    cases = gold["cases"]
+    st = dev.verify_batch([bytes.fromhex(c["nym"]) for c in cases], [bytes.fromhex(c["sig"]) for c in cases],
+                          [bytes.fromhex(c["msg"]) for c in cases])
     for c, s in zip(cases, st):
         assert I.message(int(s)) == c["error"], c["name"]
     assert sum(c["error"] is None for c in cases) == int((st == 0).sum())
+
+
+@pytest.mark.gpu
+def test_golden_verdicts(ipk_dev):
+    _golden(ipk_dev, GOLD)
+
+
+@pytest.mark.gpu
+def test_golden_verdicts_fp256bn(ipk_fbn):
+    _golden(ipk_fbn, GOLD_FBN)
+
+
+@pytest.mark.gpu
+def test_random_batch_fp256bn_against_oracle(ipk_fbn):
+    from fts_gpu import idemix as I
+    nyms, sigs, msgs, want = _batch(200, seed=21, curve="fp256bn")
+    st = ipk_fbn.verify_batch(nyms, sigs, msgs)
+    assert [I.message(int(s)) for s in st] == want
 
 
 @pytest.mark.gpu
@@ -72,13 +100,14 @@ def test_single_verifier_api(ipk_dev):
         v.Verify(b"m", b"")
 
 
-def _batch(n, seed, nkeys=6, tamper=0.1):
-    from oracle import bn254, idemix as O
-    ipk = O.parse_ipk(IPK)
+def _batch(n, seed, nkeys=6, tamper=0.1, curve="bn254"):
+    from oracle import idemix as O
+    C = O.BN254C if curve == "bn254" else O.FP256BNC
+    ipk = O.parse_ipk(IPK if curve == "bn254" else IPK_FBN, C)
     rng = random.Random(seed)
     keys = []
     for _ in range(nkeys):
-        sk, rn = rng.randrange(bn254.R), rng.randrange(bn254.R)
+        sk, rn = rng.randrange(C.r), rng.randrange(C.r)
         keys.append((sk, rn, O.make_nym(ipk, sk, rn)))
     nyms, sigs, msgs, want = [], [], [], []
     shared = bytes(rng.randrange(256) for _ in range(700))  # one request message, many inputs
@@ -86,16 +115,16 @@ def _batch(n, seed, nkeys=6, tamper=0.1):
         sk, rn, nym = keys[rng.randrange(nkeys)]
         msg = shared if i % 2 else bytes(rng.randrange(256) for _ in range(rng.randrange(0, 300)))
         sig = O.nym_sign(ipk, sk, nym, rn, msg, rng)
-        nb = bn254.g1_bytes(nym)
+        nb = C.g1_bytes(nym)
         if rng.random() < tamper:
             kind = rng.randrange(3)
             if kind == 0:
                 msg = msg + b"x"
             elif kind == 1:
-                c, s1, s2, nonce = O.decode_nym_sig(sig)
-                sig = O.encode_nym_sig(c, s1, (s2 + 1) % bn254.R, nonce)
+                c, s1, s2, nonce = O.decode_nym_sig(sig, C)
+                sig = O.encode_nym_sig(c, s1, (s2 + 1) % C.r, nonce)
             else:
-                nb = bn254.g1_bytes(keys[(keys.index((sk, rn, nym)) + 1) % nkeys][2])
+                nb = C.g1_bytes(keys[(keys.index((sk, rn, nym)) + 1) % nkeys][2])
         try:
             O.nym_verify(ipk, nb, sig, msg)
             w = None
@@ -152,3 +181,7 @@ def test_bad_issuer_key_rejected():
     from fts_gpu import _lib as L
     with pytest.raises(L.FtsError):
         I.IssuerKey(IPK[:100], device=0)
+    with pytest.raises(L.FtsError):  # a BN254 key read as FP256BN: HSk is not on that curve
+        I.IssuerKey(IPK, device=0, curve=I.FTS_CURVE_FP256BN_AMCL)
+    with pytest.raises(L.FtsError):
+        I.IssuerKey(IPK_FBN, device=0, curve=I.FTS_CURVE_BN254)

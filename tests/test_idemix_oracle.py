@@ -65,6 +65,27 @@ def test_bn254_issuer_key_proof_pins_encodings():
         assert not idemix.ipk_proof_valid(bad)
 
 
+def test_fp256bn_nym_roundtrip_and_amcl_field_rules():
+    ipk = idemix.parse_ipk(_raw("fp256bn_validator", "IssuerPublicKey"), idemix.FP256BNC)
+    C = idemix.FP256BNC
+    rng = random.Random(9)
+    sk, rn = rng.randrange(C.r), rng.randrange(C.r)
+    nym = idemix.make_nym(ipk, sk, rn)
+    nb = C.g1_bytes(nym)
+    assert len(nb) == 65 and nb[0] == 4
+    sig = idemix.nym_sign(ipk, sk, nym, rn, b"msg", rng)
+    idemix.nym_verify(ipk, nb, sig, b"msg")
+    # AMCL FromBytes: bytes after the first 32 of a field are ignored; fewer than 32 panic
+    f = idemix.pb_fields(sig)
+    longer = b"".join(idemix.pb_bytes_field(k, v + b"\1" if k == 4 else v) for k, _, v in f)
+    idemix.nym_verify(ipk, nb, longer, b"msg")
+    short = b"".join(idemix.pb_bytes_field(k, v[1:] if k == 1 else v) for k, _, v in f)
+    with pytest.raises(idemix.NymError, match="unmarshalling"):
+        idemix.nym_verify(ipk, nb, short, b"msg")
+    with pytest.raises(idemix.NymError, match="nym public key"):
+        idemix.nym_verify(ipk, nb[1:], sig, b"msg")
+
+
 def test_bn254_issuer_secret_key_relations():
     ipk = idemix.parse_ipk(_raw("bn254_tokengen", "IssuerPublicKey"))
     isk = int.from_bytes(_raw("bn254_tokengen", "IssuerSecretKey"), "big")
@@ -98,11 +119,14 @@ def test_nym_sign_verify_roundtrip_and_tampering():
     idemix.nym_verify(ipk, nb, idemix.encode_nym_sig(c, s1 + bn254.R, s2, nonce), msg)
 
 
-def test_golden_nym_vectors():
+@pytest.mark.parametrize("curve", ["bn254", "fp256bn"])
+def test_golden_nym_vectors(curve):
     """tests/golden/idemix_golden.json (tests/golden/make_idemix_golden.py) against the oracle."""
     with open(os.path.join(os.path.dirname(__file__), "golden", "idemix_golden.json")) as f:
-        g = json.load(f)
-    ipk = idemix.parse_ipk(bytes.fromhex(g["ipk"]))
+        g = json.load(f)[curve]
+    C = idemix.BN254C if curve == "bn254" else idemix.FP256BNC
+    assert g["curve"] == C.name
+    ipk = idemix.parse_ipk(bytes.fromhex(g["ipk"]), C)
     for case in g["cases"]:
         want = case["error"]
         try:
