@@ -122,7 +122,7 @@ def main():
     ap.add_argument("--bits", type=int, default=64)
     ap.add_argument("--inflight", type=int, default=64,
                     help="batches in flight: host threads, each submitting its own staged batch")
-    ap.add_argument("--lanes", type=int, default=int(os.environ.get("FTS_LANES", "5")),
+    ap.add_argument("--lanes", type=int, default=int(os.environ.get("FTS_LANES", "4")),
                     help="device lanes (stream pairs) of the library (FTS_LANES); batches submitted while "
                          "all lanes are busy are coalesced into one device pass (FTS_COALESCE_MAX proofs)")
     ap.add_argument("--distinct", type=int, default=4,
@@ -284,7 +284,7 @@ def main():
         return acc, (time.perf_counter() - t) * 1e3 / reps
 
     kt1, iso_ms = isolated(batches[0], R)
-    m = args.pass_batches or max(1, int(os.environ.get("FTS_COALESCE_MAX", "32768")) // B)
+    m = args.pass_batches or max(1, int(os.environ.get("FTS_COALESCE_MAX", "81920")) // B)
     pass_proofs = [sets[i % len(sets)] for i in range(m)]
     big = pp.stage_range_proofs([p for ps, _ in pass_proofs for p in ps], [c for _, cs in pass_proofs for c in cs])
     kt, pass_ms = isolated(big, R)

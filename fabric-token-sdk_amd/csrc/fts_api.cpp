@@ -300,13 +300,18 @@ struct fts_ctx {
   // concurrently are merged into one device pass of up to coalesce_max proofs
   std::deque<RpReq*> rp_pending;
   size_t pending_proofs = 0;  // proofs queued in rp_pending
-  size_t coalesce_max = 32768;
+  // 81,920 proofs (20 batches of 4,096): a burst of batches (the driver's 20-step
+  // bench) shares two or three large passes, whose chain kernels (com, the
+  // per-proof x0 hash, the MSM's final reduction) run at several waves per SIMD
+  // instead of under one (tools/s20_sweep4.sh: 3.0 -> 3.6 M rp64/s at 20 steps,
+  // 4.41 -> 4.47 M/s at 512 steps, single-batch latency unchanged)
+  size_t coalesce_max = 81920;
   // gather window: while the device is busy and fewer than gather_target proofs
   // are queued, the head request waits up to gather_us for more batches before
   // it takes a lane (a burst of callers then shares a few large passes instead
   // of one lone 4,096-proof pass per free lane); an idle device starts at once
   size_t gather_target = 16384;
-  int gather_us = 300;
+  int gather_us = 1000;
   // passes of up to com_fixed_max proofs compute com on the latency path (fixed-base
   // groups, rp_kernels.hip k_rp_fixed_all), larger ones on the work path (Horner +
   // joint GLV chains): the same group element either way
@@ -440,7 +445,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
     return code;
   };
   if (hipSetDevice(device) != hipSuccess) return fail(FTS_API_EDEVICE);
-  int nl = 5;
+  int nl = 4;  // lanes (FTS_LANES): 4 beat 5 and 3 on the burst and the steady state (s20_sweep4.sh)
   if (const char* e = getenv("FTS_LANES")) nl = std::max(1, std::min(16, atoi(e)));
   if (const char* e = getenv("FTS_COALESCE_MAX")) c->coalesce_max = (size_t)std::max(0L, atol(e));
   c->gather_target = c->coalesce_max / 2;

@@ -27,7 +27,7 @@
  * Return values: every function returns FTS_API_OK (0) or a negative
  * FTS_API_* code for API/driver errors (bad argument, HIP failure).
  * Per-item verdicts go to caller-owned int32 arrays as fts_status values.
- * Thread safety: a context runs up to FTS_LANES (default 5) calls concurrently,
+ * Thread safety: a context runs up to FTS_LANES (default 4) calls concurrently,
  * each on its own HIP streams (main, side, batch check) and workspace; further
  * callers wait (range-proof batches are coalesced into the next free lane's pass).
  */
@@ -184,9 +184,9 @@ int fts_rp_batch_stage(fts_ctx* ctx, size_t n, const uint8_t* const* rp_der, con
                        const uint8_t* com64, fts_rp_batch** out);
 /* runs the whole GPU verification of a staged batch; status may be NULL.
  * Thread-safe: concurrent calls on DIFFERENT batches run on different lanes
- * (stream pairs, FTS_LANES env, default 5) and overlap on the device; batches
+ * (stream pairs, FTS_LANES env, default 4) and overlap on the device; batches
  * submitted while every lane is busy are coalesced into one device pass of
- * up to FTS_COALESCE_MAX proofs (default 32768).  Verdicts are per proof and
+ * up to FTS_COALESCE_MAX proofs (default 81920).  Verdicts are per proof and
  * independent of the grouping. */
 int fts_rp_batch_verify(fts_ctx* ctx, fts_rp_batch* b, int32_t* status);
 /* pre-allocate every lane's workspace for device passes of up to max_pass_proofs

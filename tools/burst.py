@@ -7,6 +7,10 @@ environment, so an A/B is one process per setting.
 import argparse
 import json
 import os
+
+# as bench.py: 16 hardware queues (read once when HIP loads)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 import random
 import sys
 import threading
