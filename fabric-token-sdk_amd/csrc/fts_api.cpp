@@ -156,8 +156,22 @@ struct Workspace {
 // aggregation goroutines, or bench.py's pipeline) run on different lanes, so
 // one batch's latency-bound phases (transcript hashing, doubling chains)
 // overlap another batch's throughput-bound kernels.
+// host-side decoding of one action (verify_actions); kept per lane across calls so
+// the buffers' capacity is reused instead of allocated and freed per action per call
+// (freeing ~50k small vectors that 16 parse threads allocated cost ~5 ms per
+// 8,192-transfer call on the caller's critical path)
+struct ParsedAction {
+  std::vector<uint8_t> sig_raw;   // CT, in..., out...  (64 B each)
+  std::vector<uint32_t> sig_sc;   // scalars
+  int chal_canonical = 0;
+  std::vector<uint8_t> rp_raw;
+  std::vector<uint32_t> rp_sc;
+  std::vector<int32_t> rp_status, rp_ipa;
+};
+
 struct Lane {
   int id = 0;
+  std::vector<ParsedAction> parsed;  // verify_actions' per-action decode buffers (reused)
   // completion event created with hipEventBlockingSync: waiting on it sleeps
   // instead of spinning (a spinning waiter per lane burns the process's CPU
   // quota; on a CFS-throttled box that stalls every host thread for ~50 ms
@@ -179,6 +193,7 @@ struct Lane {
   Timeline tl;
   float host_prep_ms = 0, host_enqueue_ms = 0, host_wait_ms = 0;  // host wall time of the last run
   float host_parse_ms = 0, host_stage_ms = 0;  // action batches: DER parsing, assembly + upload
+  float host_misc_ms = 0, host_total_ms = 0, host_stage_copy_ms = 0;  // action batches: allocation before the parse + verdict assembly / release after the wait
   // pinned host staging (pageable async copies would block the enqueue)
   struct Pinned {
     uint32_t key[8];
@@ -239,21 +254,80 @@ static unsigned host_threads() {
   return n;
 }
 
-// run f(i) for i in [0, n) on up to host_threads() threads (inline when small)
+// Fork-join pool of host_threads() - 1 persistent workers for the host loops
+// (DER parsing, staging): spawning host_threads() std::threads per loop cost
+// ~0.5 ms per loop, twice per action call, with several calls in flight.
+// Every caller works on its own job too, so concurrent callers always progress.
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool* p = new HostPool();  // never destroyed: workers may outlive static destructors
+    return *p;
+  }
+  void run(size_t n, const std::function<void(size_t)>& f) {
+    auto j = std::make_shared<Job>();
+    j->n = n;
+    j->f = &f;
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      q_.push_back(j);
+    }
+    cv_.notify_all();
+    work(*j);
+    std::unique_lock<std::mutex> l(j->m);
+    j->cv.wait(l, [&] { return j->done.load() == j->n; });
+  }
+
+ private:
+  struct Job {
+    size_t n = 0;
+    const std::function<void(size_t)>* f = nullptr;
+    std::atomic<size_t> next{0}, done{0};
+    std::mutex m;
+    std::condition_variable cv;
+  };
+  HostPool() {
+    const unsigned nw = host_threads() > 1 ? host_threads() - 1 : 0;
+    for (unsigned t = 0; t < nw; t++) std::thread([this] { loop(); }).detach();
+  }
+  static void work(Job& j) {
+    for (size_t i; (i = j.next++) < j.n;) {
+      (*j.f)(i);
+      if (++j.done == j.n) {
+        std::lock_guard<std::mutex> l(j.m);
+        j.cv.notify_all();
+      }
+    }
+  }
+  void loop() {
+    for (;;) {
+      std::shared_ptr<Job> j;
+      {
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [&] { return !q_.empty(); });
+        j = q_.front();
+        if (j->next.load() >= j->n) {  // exhausted: drop it and look again
+          q_.pop_front();
+          continue;
+        }
+      }
+      work(*j);
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::shared_ptr<Job>> q_;
+};
+
+// run f(i) for i in [0, n) on the host pool (inline when small)
 template <class F>
 static void parallel_for(size_t n, size_t min_parallel, F&& f) {
-  const unsigned nth = n >= min_parallel ? host_threads() : 1u;
-  if (nth <= 1) {
+  if (n < min_parallel || host_threads() <= 1) {
     for (size_t i = 0; i < n; i++) f(i);
     return;
   }
-  std::atomic<size_t> next{0};
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < nth; t++)
-    th.emplace_back([&]() {
-      for (size_t i; (i = next++) < n;) f(i);
-    });
-  for (auto& t : th) t.join();
+  const std::function<void(size_t)> fn = std::ref(f);
+  HostPool::get().run(n, fn);
 }
 
 static inline double now_ms() {
@@ -854,9 +928,11 @@ static void collect_timings(fts_ctx* c, Lane& L, fts_rp_batch* b) {
     c->tim_work[j] = L.tl.work[i];
     hipEventElapsedTime(&c->tim_ms[j], L.tl.ev[L.tl.start[i]], L.tl.ev[i + 1]);
   }
-  const char* hn[5] = {"host_prep", "host_enqueue", "host_wait_flag", "host_parse", "host_stage"};
-  const float hv[5] = {L.host_prep_ms, L.host_enqueue_ms, L.host_wait_ms, L.host_parse_ms, L.host_stage_ms};
-  for (int q = 0; q < 5 && c->ntim < Timeline::CAP; q++) {
+  const char* hn[8] = {"host_prep", "host_enqueue", "host_wait_flag", "host_parse", "host_stage", "host_misc",
+                       "host_total", "host_stage_copy"};
+  const float hv[8] = {L.host_prep_ms, L.host_enqueue_ms, L.host_wait_ms, L.host_parse_ms, L.host_stage_ms,
+                       L.host_misc_ms, L.host_total_ms, L.host_stage_copy_ms};
+  for (int q = 0; q < 8 && c->ntim < Timeline::CAP; q++) {
     c->tim_name[c->ntim] = hn[q];
     c->tim_ms[c->ntim] = hv[q];
     c->tim_work[c->ntim] = 0;
@@ -1547,19 +1623,14 @@ struct ActionState {
 }  // namespace
 
 static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts, int32_t* status, int32_t* fail_index) {
+  const double t_fn0 = now_ms();
   const int k = c->k, n = c->n, npts_rp = rp_npts(k);
   const size_t A = acts.size();
   std::vector<ActionState> st(A);
   // host-side decoding (parallel over actions)
-  struct Parsed {
-    std::vector<uint8_t> sig_raw;   // CT, in..., out...  (64 B each)
-    std::vector<uint32_t> sig_sc;   // scalars
-    int chal_canonical = 0;
-    std::vector<uint8_t> rp_raw;
-    std::vector<uint32_t> rp_sc;
-    std::vector<int32_t> rp_status, rp_ipa;
-  };
-  std::vector<Parsed> P(A);
+  using Parsed = ParsedAction;
+  if (L.parsed.size() < A) L.parsed.resize(A);
+  std::vector<Parsed>& P = L.parsed;
   const double t_parse0 = now_ms();
   auto parse_one = [&](size_t i) {
     const ActionIn& ai = acts[i];
@@ -1684,16 +1755,7 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
     }
     s.sig_on_device = true;
   };
-  {
-    unsigned nth = A >= 64 ? host_threads() : 1u;
-    std::atomic<size_t> next{0};
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < nth; t++)
-      th.emplace_back([&]() {
-        for (size_t i; (i = next++) < A;) parse_one(i);
-      });
-    for (auto& t : th) t.join();
-  }
+  parallel_for(A, 64, parse_one);
   const double t_parse1 = now_ms();
   L.host_parse_ms = (float)(t_parse1 - t_parse0);
   // ---- assemble device batches: offsets on one thread (integer sums), then a
@@ -1784,6 +1846,8 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
       memcpy(hs + o_ripa + rb * 4, p.rp_ipa.data(), rc * 4);
     }
   });
+  const double t_copy1 = now_ms();
+  L.host_stage_copy_ms = (float)(t_copy1 - t_parse1);
   {  // affine-table offsets: prefix sum in sigma-batch order
     int32_t* ao = (int32_t*)(hs + o_affoff);
     int acc = 0;
@@ -1874,6 +1938,9 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
   if (SA) HIP_OK(hipMemcpyAsync(sig_res.data(), w.s_status.p, SA * 4, hipMemcpyDeviceToHost, L.s));
   if (rp_total) HIP_OK(hipMemcpyAsync(rp_res.data(), w.rp_status.p, rp_total * 4, hipMemcpyDeviceToHost, L.s));
   HIP_OK(L.sync());
+  const double t_post0 = now_ms();
+  L.host_misc_ms = (float)((t_parse0 - t_fn0) + (now_ms() - t_post0));
+  L.host_total_ms = (float)(now_ms() - t_fn0);  // verify_actions up to the verdict merge
   if (rp_total) collect_timings(c, L, nullptr);
   // ---- combine with the reference's precedence
   for (size_t i = 0; i < A; i++) {

@@ -11,5 +11,5 @@ run() {  # tag args...
 run if3 --action-inflight 3
 run if4 --action-inflight 4
 run if5 --action-inflight 5
-run if6l8 --action-inflight 6 --lanes 8
+
 run t16k_if3 --action-inflight 3 --transfers 16384

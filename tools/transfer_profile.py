@@ -52,3 +52,5 @@ dev = sum(v[0] for k, v in tm.items() if k == "host_wait_flag")
 print("python item build %.1f ms, C call %.1f ms, host_prep %.2f enqueue %.2f wait_flag %.2f, sig %.2f, ok=%d" % (
     (t1 - t0) * 1e3, (t3 - t2) * 1e3, tm.get("host_prep", (0,))[0], tm.get("host_enqueue", (0,))[0],
     tm.get("host_wait_flag", (0,))[0], tm.get("k_sig_finish", (0,))[0], int((st == 0).sum())))
+print("host:", {k: round(v[0], 3) for k, v in tm.items() if k.startswith("host_")})
+print("kernels:", {k: round(v[0], 3) for k, v in tm.items() if not k.startswith("host_")})
