@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -35,6 +36,10 @@
 #include "device/p256.hpp"
 
 using namespace p256;
+
+namespace fts {
+void host_parallel_for(size_t n, const std::function<void(size_t)>& f);  // fts_api.cpp (persistent host pool)
+}
 
 namespace {
 
@@ -442,20 +447,7 @@ int fts_ecdsa_verify_batch(int device, size_t n, const fts_ecdsa_item* items, in
     }
   };
   const size_t CH = 2048, nch = (n + CH - 1) / CH;
-  const unsigned hw = std::thread::hardware_concurrency();
-  const size_t nth = std::min<size_t>(nch, std::min<unsigned>(16u, hw ? hw : 1u));
-  if (nth <= 1) {
-    pack(0, n);
-  } else {
-    std::atomic<size_t> next{0};
-    auto worker = [&]() {
-      for (size_t c; (c = next.fetch_add(1)) < nch;) pack(c * CH, std::min(n, (c + 1) * CH));
-    };
-    std::vector<std::thread> th;
-    for (size_t t = 1; t < nth; t++) th.emplace_back(worker);
-    worker();
-    for (auto& t : th) t.join();
-  }
+  fts::host_parallel_for(nch, [&](size_t c) { pack(c * CH, std::min(n, (c + 1) * CH)); });
   if (D.rec_cap < tot) {
     if (D.d_rec) hipFree(D.d_rec);
     D.d_rec = nullptr, D.rec_cap = 0;

@@ -329,6 +329,10 @@ static void parallel_for(size_t n, size_t min_parallel, F&& f) {
   const std::function<void(size_t)> fn = std::ref(f);
   HostPool::get().run(n, fn);
 }
+namespace fts {
+// the same pool for the signature batches' packing loops (ecdsa_kernels.hip, idemix_kernels.hip)
+void host_parallel_for(size_t n, const std::function<void(size_t)>& f) { parallel_for(n, 2, f); }
+}  // namespace fts
 
 static inline double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();

@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -50,6 +51,10 @@ size_t fb_words_per_base();
 }  // namespace fts
 
 using namespace fts;
+
+namespace fts {
+void host_parallel_for(size_t n, const std::function<void(size_t)>& f);  // fts_api.cpp (persistent host pool)
+}
 
 namespace {
 
@@ -839,20 +844,7 @@ int fts_nym_verify_batch(fts_idemix_ipk* K, size_t n, const fts_nym_item* items,
     }
   };
   const size_t CH = 2048, nch = (n + CH - 1) / CH;
-  const unsigned hw = std::thread::hardware_concurrency();
-  const size_t nth = std::min<size_t>(nch, std::min<unsigned>(16u, hw ? hw : 1u));
-  if (nth <= 1) {
-    pack(0, n);
-  } else {
-    std::atomic<size_t> next{0};
-    auto worker = [&]() {
-      for (size_t c; (c = next.fetch_add(1)) < nch;) pack(c * CH, std::min(n, (c + 1) * CH));
-    };
-    std::vector<std::thread> th;
-    for (size_t t = 1; t < nth; t++) th.emplace_back(worker);
-    worker();
-    for (auto& t : th) t.join();
-  }
+  fts::host_parallel_for(nch, [&](size_t c) { pack(c * CH, std::min(n, (c + 1) * CH)); });
   uint8_t* d = D.d_buf;
   ICHK(hipMemcpyAsync(d, h, h_need, hipMemcpyHostToDevice, D.stream));
   ICHK(hipEventRecord(D.ev[0], D.stream));

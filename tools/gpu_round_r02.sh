@@ -57,6 +57,8 @@ if [ "${EXTRA:-1}" = 1 ]; then
   step bench_audit 200 python3 -u bench.py --workload audit --steps 64 --warmup 4
   step bench_prove 300 python3 -u bench.py --workload prove --batch 16384 --steps 12 --warmup 2
   step bench_ecdsa 300 python3 -u bench.py --workload ecdsa --steps 64 --warmup 4
-  for w in transfer mixed request msm msm22 audit prove ecdsa; do json bench_$w; done
+  step bench_idemix 300 python3 -u bench.py --workload idemix --steps 32 --warmup 4
+  step bench_idemix_fbn 300 python3 -u bench.py --workload idemix --idemix-curve fp256bn --steps 32 --warmup 4
+  for w in transfer mixed request msm msm22 audit prove ecdsa idemix idemix_fbn; do json bench_$w; done
 fi
 echo "== done $(date +%T)"
