@@ -127,7 +127,7 @@ struct DBuf {
 };
 
 struct Workspace {
-  DBuf pts, ch, small, hpj, hpa, hpbe, x0, terms, scratch, ypow, svec, zvec, rp_excl;
+  DBuf pts, ch, small, hpj, hpa, hpbe, x0, x0mid, terms, scratch, ypow, svec, zvec, rp_excl;
   // random-linear-combination check + MSM
   DBuf r_key, r_msc, r_coef, r_colsum, r_fixed, r_flag, r_gcol, r_gfix, r_sel, r_next, r_cnt, m_keys, m_counts, m_offsets, m_cursor, m_sorted, m_buckets,
       m_segs, m_wins, m_out, m_scratch, m_win, m_choff, m_chbkt, m_partials;
@@ -138,7 +138,7 @@ struct Workspace {
   DBuf pv;        // batched prover: one arena (prove_arena)
   DBuf sp;        // sigma provers: one arena
   void release() {
-    for (DBuf* b : {&open_rec, &pv, &sp, &pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &terms, &scratch, &ypow, &svec, &zvec, &rp_excl, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
+    for (DBuf* b : {&open_rec, &pv, &sp, &pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &x0mid, &terms, &scratch, &ypow, &svec, &zvec, &rp_excl, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
                     &rp_status, &rp_ipa, &s_act, &s_raw, &s_owner, &s_pts, &s_sc, &s_status, &s_work, &s_terms, &s_aff,
                     &s_affoff, &s_msgs, &s_jac, &s_scratch, &r_key, &r_msc, &r_coef, &r_colsum, &r_fixed, &r_flag, &r_gcol, &r_gfix,
                     &r_sel, &r_next, &r_cnt,
@@ -394,6 +394,7 @@ struct fts_ctx {
   // groups, rp_kernels.hip k_rp_fixed_all), larger ones on the work path (Horner +
   // joint GLV chains): the same group element either way
   size_t com_fixed_max = 16384;
+  int x0_split = 1;                 // FTS_X0_SPLIT: work path hashes the x0 prefix beside the com chain
   int rlc_fork = 1;                 // FTS_RLC_FORK: batch check forks after the fixed-base products (1) or the challenges (0)
   // a lane was freed (call with mu held): the head pending range-proof request
   // becomes the next leader; LaneGuard waiters re-check too
@@ -530,6 +531,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_GATHER_US")) c->gather_us = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_COM_FIXED_MAX")) c->com_fixed_max = (size_t)std::max(0L, atol(e));
   if (const char* e = getenv("FTS_RLC_FORK")) c->rlc_fork = atoi(e) != 0;
+  if (const char* e = getenv("FTS_X0_SPLIT")) c->x0_split = atoi(e) != 0;
   if (const char* e = getenv("FTS_LAT_BS")) {  // block size of the latency-bound kernels (64, 128 or 256)
     const int v = atoi(e);
     g_lat_bs = v <= 64 ? 64 : v <= 128 ? 128 : 256;
@@ -1000,7 +1002,7 @@ static int rp_buffers(fts_ctx* c, Lane& L, int B) {
   if (w.pts.ensure((size_t)B * npts * 64) || w.ch.ensure((size_t)B * rp_nch(k) * 32) ||
       w.small.ensure((size_t)B * (2 + k) * SMALL_SLOT) || w.hpj.ensure((size_t)B * (n + 1) * 96) ||
       w.hpa.ensure((size_t)B * (n + 1) * 64) || w.hpbe.ensure((size_t)B * (n + 1) * 64) ||
-      w.x0.ensure((size_t)B * x0_var_bytes(n)) || w.terms.ensure(rp_terms_words(B, n, k) * 4) ||
+      w.x0.ensure((size_t)B * x0_var_bytes(n)) || w.x0mid.ensure((size_t)B * 32) || w.terms.ensure(rp_terms_words(B, n, k) * 4) ||
       w.scratch.ensure(std::max(rp_scratch_words(B, n, k), (size_t)B * 10 * 24) * 4) || w.r_key.ensure(32) ||
       w.r_msc.ensure((size_t)N * 32) || w.r_coef.ensure((size_t)B * RLC_NCOEF * 32) ||
       w.r_colsum.ensure(rlc_ncols(n) * 32) || w.r_fixed.ensure(rlc_ncols(n) * 96) || w.r_flag.ensure(4) || w.ypow.ensure((size_t)B * n * 32) ||
@@ -1139,6 +1141,7 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   d.pre_rlc_arg = pre_rlc_arg;
   d.rlc_fork = c->rlc_fork;
   d.ev_coef = L.ev_c;
+  d.x0_mid = c->x0_split ? w.x0mid.as<uint32_t>() : nullptr;
   d.excl = pre_rlc ? w.rp_excl.as<int32_t>() : nullptr;
   RlcDev r{w.r_key.as<uint32_t>(), w.r_msc.as<uint32_t>(),   w.r_coef.as<uint32_t>(), w.r_colsum.as<uint32_t>(),
            w.r_fixed.as<uint32_t>(), w.r_flag.as<int32_t>(), w.m_scratch.as<uint32_t>(), mp};

@@ -719,10 +719,14 @@ FTS_DEV uint32_t x0_unit(const X0Src& m, uint32_t u) {
 FTS_DEV uint32_t x0_lds_off(uint32_t pos, uint32_t cb0, uint32_t cb1) {
   return pos < 64u * cb0 ? pos : pos - 64u * (cb1 - cb0);
 }
+// part: 2 = every variable block; 0 = the blocks before the shared template
+// (header, H'_0..H'_{n-1}: available right after their normalisation); 1 = the
+// blocks after it (com, DER tail, Zb(ip), padding).  Parts 0 and 1 write
+// disjoint byte ranges of the proof's slot.
 __global__ void __launch_bounds__(256) k_rp_x0_build(int B, int n, const int32_t* __restrict__ status,
                                                      const uint8_t* __restrict__ hp_be,
                                                      const uint8_t* __restrict__ x0_const, const uint32_t* __restrict__ sc,
-                                                     uint8_t* __restrict__ msgs) {
+                                                     uint8_t* __restrict__ msgs, int part) {
   extern __shared__ uint4 x0_lds[];
   uint8_t* Lb = reinterpret_cast<uint8_t*>(x0_lds);
   const int b = blockIdx.x;
@@ -732,7 +736,8 @@ __global__ void __launch_bounds__(256) k_rp_x0_build(int B, int n, const int32_t
   const uint32_t c_off = x0_const_off(n), c_end = x0_const_end(n);
   const uint8_t* hp = hp_be + (size_t)b * (n + 1) * 64;
   // hex records: H'_0..H'_{n-1} (records 0..n-1) and com (record 2n+1, no "||")
-  for (int it = threadIdx.x; it < (n + 1) * 4; it += blockDim.x) {
+  const int r_lo = part == 1 ? n : 0, r_hi = part == 0 ? n : n + 1;  // records of this part
+  for (int it = threadIdx.x + 4 * r_lo; it < r_hi * 4; it += blockDim.x) {
     const int r = it >> 2, q = it & 3;
     const uint4 v = *reinterpret_cast<const uint4*>(hp + r * 64 + q * 16);
     const uint32_t rec = r < n ? (uint32_t)r : 2u * n + 1u;
@@ -769,7 +774,9 @@ __global__ void __launch_bounds__(256) k_rp_x0_build(int B, int n, const int32_t
     Lb[x0_lds_off(pos, cb0, cb1)] = (uint8_t)v;
   };
   const uint32_t nh = 8u, nc0 = 64u * cb0 - c_off, nc1 = c_end - 64u * cb1, nt = end - t0;
-  for (uint32_t it = threadIdx.x; it < nh + nc0 + nc1 + nt; it += blockDim.x) {
+  // part 0: header + constants before the template; part 1: constants after it + trailer
+  const uint32_t i_lo = part == 1 ? nh + nc0 : 0u, i_hi = part == 0 ? nh + nc0 : nh + nc0 + nc1 + nt;
+  for (uint32_t it = threadIdx.x + i_lo; it < i_hi; it += blockDim.x) {
     uint32_t pos;
     if (it < nh) pos = it;
     else if (it < nh + nc0) pos = c_off + (it - nh);
@@ -779,21 +786,34 @@ __global__ void __launch_bounds__(256) k_rp_x0_build(int B, int n, const int32_t
   }
   __syncthreads();
   uint4* dst = reinterpret_cast<uint4*>(msgs + (size_t)b * var);
-  for (uint32_t c = threadIdx.x; c < var / 16u; c += blockDim.x) dst[c] = x0_lds[c];
+  const uint32_t c_lo = part == 1 ? 4u * cb0 : 0u, c_hi = part == 0 ? 4u * cb0 : var / 16u;
+  for (uint32_t c = threadIdx.x + c_lo; c < c_hi; c += blockDim.x) dst[c] = x0_lds[c];
 }
 inline size_t x0_build_lds(int n) { return x0_var_bytes(n); }
 
+// SHA-256 over message blocks [b0, b1) of each proof's x0 message: b0 == 0
+// starts from the initial state, else from mid[b]; b1 == every block finishes
+// (x0 = HashToZr -> ch), else the state is left in mid[b].  The whole hash
+// (0, all) or its prefix (0, cb1: H' records + the shared template, started
+// while com is still being computed) and suffix (cb1, all).
 __global__ void __launch_bounds__(256) k_rp_x0_hash(int B, int n, int k, const int32_t* __restrict__ status,
                                                    const uint8_t* __restrict__ msgs, const uint8_t* __restrict__ tmpl,
+                                                   uint32_t b0, uint32_t b1, uint32_t* __restrict__ mid,
                                                    uint32_t* __restrict__ ch) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B || status[b] != 0) return;
   const uint32_t cb0 = x0_cb0(n), cb1 = x0_cb1(n), nb = sha_blocks(x0_msg_len(n));
+  const uint32_t hi = b1 < nb ? b1 : nb;
   const uint4* own = reinterpret_cast<const uint4*>(msgs + (size_t)b * x0_var_bytes(n));
   const uint4* shared = reinterpret_cast<const uint4*>(tmpl);
   uint32_t st[8];
-  sha256_init(st);
-  for (uint32_t blk = 0; blk < nb; blk++) {
+  if (b0 == 0) {
+    sha256_init(st);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] = mid[(size_t)b * 8 + i];
+  }
+  for (uint32_t blk = b0; blk < hi; blk++) {
     const uint4* m = blk < cb0 ? own + 4u * blk : blk < cb1 ? shared + 4u * (blk - cb0) : own + 4u * (blk - (cb1 - cb0));
     uint32_t w[16];
 #pragma unroll
@@ -805,6 +825,11 @@ __global__ void __launch_bounds__(256) k_rp_x0_hash(int B, int n, int k, const i
       w[4 * i + 3] = __builtin_bswap32(u.w);
     }
     sha256_compress(st, w);
+  }
+  if (hi < nb) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) mid[(size_t)b * 8 + i] = st[i];
+    return;
   }
   store_f(ch + ((size_t)b * rp_nch(k) + CH_X0) * 8, f_to_mont(digest_to_fr(st)));
 }
@@ -1315,6 +1340,17 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     FTS_LAUNCH(k_rp_normalize, (nhp + NORM_E - 1) / NORM_E, NORM_BS, s, nhp, n, n + 1, 0, d.status, d.hpj, d.hpa,
                d.hp_be);
     tl->mark("k_rp_normalize", s, (double)nhp * (2.0 * 8.0 / NORM_E + 9.0));
+    if (d.x0_mid) {
+      // x0 prefix on the side stream: the H' records and the shared template
+      // (cb1 of the message's blocks) do not depend on com, so they are hashed
+      // beside the S / com chain; only the suffix waits for com
+      tl->fork(s, s2);
+      hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s2, B, n, d.status, d.hp_be, x0_const,
+                         d.sc, d.x0_msgs, 0);
+      tl->mark("k_rp_x0_build", s2, 0);
+      FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s2, B, n, k, d.status, d.x0_msgs, x0_tmpl, 0u, x0_cb1(n), d.x0_mid, d.ch);
+      tl->mark("k_rp_x0_prefix", s2, 0);
+    }
     const int nch = (n + HS_CHUNK - 1) / HS_CHUNK;
     FTS_LAUNCH(k_rp_hsum_chunks, B * nch, 64, s, B, n, d.status, d.hpa, d.scratch);
     tl->mark("k_rp_hsum_chunks", s, (double)B * (n - nch) * (COST_DBL + COST_MADD));
@@ -1329,10 +1365,13 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   }
   FTS_LAUNCH(k_rp_normalize, (B + NORM_E - 1) / NORM_E, NORM_BS, s, B, 1, n + 1, n, d.status, d.hpj, d.hpa, d.hp_be);
   tl->mark("k_rp_normalize_com", s, (double)B * (2.0 * 8.0 / NORM_E + 9.0));
+  const bool split = !d.com_fixed && d.x0_mid;
   hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s, B, n, d.status, d.hp_be, x0_const, d.sc,
-                     d.x0_msgs);
-  tl->mark("k_rp_x0_build", s, 0);
-  FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s, B, n, k, d.status, d.x0_msgs, x0_tmpl, d.ch);
+                     d.x0_msgs, split ? 1 : 2);
+  tl->mark(split ? "k_rp_x0_build_tail" : "k_rp_x0_build", s, 0);
+  if (split) tl->fork(s2, s);  // the prefix's midstate
+  FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s, B, n, k, d.status, d.x0_msgs, x0_tmpl, split ? x0_cb1(n) : 0u, 0xffffffffu,
+             d.x0_mid, d.ch);
   tl->mark("k_rp_x0_hash", s, 0);
   // x0 tail: column Q (needs the weights of k_rlc_prep) and its product, then
   // the verdict once the MSM is in
@@ -1404,7 +1443,7 @@ namespace fts {
 void launch_x0(int B, int n, int k, const int32_t* status, const uint8_t* hp_be, const uint8_t* x0_const,
                const uint8_t* x0_tmpl, const uint32_t* sc, uint8_t* msgs, uint32_t* ch, hipStream_t s) {
   if (B <= 0) return;
-  hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s, B, n, status, hp_be, x0_const, sc, msgs);
-  FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s, B, n, k, status, msgs, x0_tmpl, ch);
+  hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s, B, n, status, hp_be, x0_const, sc, msgs, 2);
+  FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s, B, n, k, status, msgs, x0_tmpl, 0u, 0xffffffffu, (uint32_t*)nullptr, ch);
 }
 }  // namespace fts
