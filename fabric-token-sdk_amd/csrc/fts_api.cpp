@@ -394,6 +394,12 @@ struct fts_ctx {
   // groups, rp_kernels.hip k_rp_fixed_all), larger ones on the work path (Horner +
   // joint GLV chains): the same group element either way
   size_t com_fixed_max = 16384;
+  // group test: round-1 group size and round-2 threshold (FTS_GT1 / FTS_GT2_MIN).  Larger
+  // round-1 groups make the grouped MSM's bucket reduction cheaper (it scales with the
+  // group count); the per-proof checks of the failing groups cost one GLV chain of
+  // latency whatever their number up to ~8k proofs (tools/gt_sweep.sh, C5 1 % tampered:
+  // 64/2048 -> 256/8192 = 485k -> 533k actions/s)
+  int gt1 = 256, gt2_min = 8192;
   int x0_split = 1;                 // FTS_X0_SPLIT: work path hashes the x0 prefix beside the com chain
   int rlc_fork = 1;                 // FTS_RLC_FORK: batch check forks after the fixed-base products (1) or the challenges (0)
   // a lane was freed (call with mu held): the head pending range-proof request
@@ -532,6 +538,8 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_COM_FIXED_MAX")) c->com_fixed_max = (size_t)std::max(0L, atol(e));
   if (const char* e = getenv("FTS_RLC_FORK")) c->rlc_fork = atoi(e) != 0;
   if (const char* e = getenv("FTS_X0_SPLIT")) c->x0_split = atoi(e) != 0;
+  if (const char* e = getenv("FTS_GT1")) c->gt1 = std::max(8, std::min(1024, atoi(e)));
+  if (const char* e = getenv("FTS_GT2_MIN")) c->gt2_min = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_LAT_BS")) {  // block size of the latency-bound kernels (64, 128 or 256)
     const int v = atoi(e);
     g_lat_bs = v <= 64 ? 64 : v <= 128 ? 128 : 256;
@@ -1037,10 +1045,12 @@ static int lane_reserve(fts_ctx* c, Lane& L, int B, bool inputs) {
 // batch check's own weights.  The proofs of groups that do not close get the
 // per-proof final equations (bulletproof.go:314-324, ipa.go:254-259), whose
 // verdicts are the reference's.  A single bad proof costs one grouped MSM plus
-// RP_GT1 per-proof checks, all of them in its own caller batch.
-constexpr int RP_GT1 = 64, RP_GT2 = 8, RP_GT2_MIN = 2048;
+// RP_GT1 per-proof checks, all of them in its own caller batch (RP_GT1, RP_GT2_MIN:
+// fts_ctx::gt1, gt2_min).
+constexpr int RP_GT2 = 8;
 static int rp_group_fallback(fts_ctx* c, Lane& L, const RpBatchDev& d, const RlcDev& r,
                              const std::vector<int>& groups) {
+  const int RP_GT1 = c->gt1, RP_GT2_MIN = c->gt2_min;
   const int B = d.B, n = d.n, npts = rp_npts(d.k);
   Workspace& w = L.ws;
   L.tl.fallback();

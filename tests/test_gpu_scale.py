@@ -198,7 +198,8 @@ def test_one_bad_proof_in_coalesced_pass_group_test(pp_raw):
     tb = tim[bad_batch]
     assert "fb:k_rlc_group_final" in tb and "fb:k_rp_terms_fixed" in tb, sorted(tb)
     per_proof = tb["fb:k_rp_terms_fixed"][1] / ((3 + 2 * 16) * 15 * 11 * 136)
-    assert 1 <= round(per_proof) <= 64, per_proof   # the bad proof's group of 64, not the pass (4,096)
+    # the bad proof's round-1 group (256 proofs of its own batch), not the pass (4,096)
+    assert 1 <= round(per_proof) <= 256, per_proof
     for b in batches:
         b.close()
     pp.close()
