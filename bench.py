@@ -221,31 +221,47 @@ def main():
             st = batches[ln].verify(want_status=True)
             sink.append((st, batches[ln].merged()))
 
-    def pipelined(nsteps):
+    def pipelined(nsteps, on_ready=None):
         """nsteps batch verifications spread over the in-flight slots (one host
-        thread each); for N > 1 every step's verdict bitmap is all-gathered."""
+        thread each); for N > 1 every step's verdict bitmap is all-gathered.
+        The submitter threads are created first and released together through
+        a barrier, so the timed region starts when the K steps are submitted
+        (not while Python spawns threads one by one).  on_ready runs once every
+        submitter waits at the gate, before the clock starts.  -> (res, t0)"""
         per = [nsteps // inflight + (1 if i < nsteps % inflight else 0) for i in range(inflight)]
+        active = [i for i in range(inflight) if per[i] > 0]
         sinks = [[] for _ in range(inflight)]
-        th = [threading.Thread(target=run, args=(i, per[i], sinks[i])) for i in range(inflight)]
+        gate = threading.Barrier(len(active) + 1)
+
+        def body(i):
+            gate.wait()
+            run(i, per[i], sinks[i])
+        th = [threading.Thread(target=body, args=(i,)) for i in active]
         for t in th:
             t.start()
+        if on_ready is not None:
+            on_ready()
+        t0 = time.perf_counter()
+        gate.wait()
         for t in th:
             t.join()
         res = [x for s in sinks for x in s]
         if dist is not None:
             for st, _ in res:
                 fdist.allgather_verdicts(dist, st)
-        return res
+        return res, t0
 
     pipelined(max(args.warmup, inflight))
+
+    def before_timed():
+        if dist is not None:
+            import torch
+            dist.barrier()
+            torch.cuda.synchronize()
+    cg0, cpu0 = _cg_throttle(), time.process_time()
+    res, t0 = pipelined(args.steps, on_ready=before_timed)
     if dist is not None:
         import torch
-        dist.barrier()
-        torch.cuda.synchronize()
-    cg0, cpu0 = _cg_throttle(), time.process_time()
-    t0 = time.perf_counter()
-    res = pipelined(args.steps)
-    if dist is not None:
         torch.cuda.synchronize()
         dist.barrier()
     elapsed = time.perf_counter() - t0

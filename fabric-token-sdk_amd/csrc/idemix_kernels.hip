@@ -719,6 +719,7 @@ int fts_idemix_ipk_create(int device, const uint8_t* ipk, size_t ipk_len, int cu
       ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(s0) == hipSuccess;
     }
   }
+  if (s0) (void)hipStreamSynchronize(s0);  // an error path may leave copies queued on s0
   if (d_bases) (void)hipFree(d_bases);
   if (d_scr) (void)hipFree(d_scr);
   if (ok && !on_curve) {

@@ -43,10 +43,16 @@ def burst():
 
     def run(i):
         out[i] = (batches[i].verify(want_status=True), batches[i].merged())
-    th = [threading.Thread(target=run, args=(i,)) for i in range(a.steps)]
-    t0 = time.perf_counter()
+    gate = threading.Barrier(a.steps + 1)  # as bench.py: submitters released together
+
+    def body(i):
+        gate.wait()
+        run(i)
+    th = [threading.Thread(target=body, args=(i,)) for i in range(a.steps)]
     for t in th:
         t.start()
+    t0 = time.perf_counter()
+    gate.wait()
     for t in th:
         t.join()
     dt = time.perf_counter() - t0
