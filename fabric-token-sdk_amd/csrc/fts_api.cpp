@@ -58,6 +58,7 @@ void launch_msm_to_bytes(const uint32_t* jac, uint8_t* out, hipStream_t s);
 void launch_sig_prep(const SigBatchDev& d, hipStream_t s);
 void launch_sig_finish(const SigBatchDev& d, const uint32_t* tables, int n, hipStream_t s);
 extern int g_lat_bs;
+extern int g_fx_proof_fastest;  // rp_kernels.hip (FTS_FX_ORDER)
 void launch_sig_exclude(const SigBatchDev& d, int32_t* rp_excl, hipStream_t s);
 size_t table_build_scratch_bytes(int nb);
 size_t fb_words_per_base();
@@ -540,6 +541,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_X0_SPLIT")) c->x0_split = atoi(e) != 0;
   if (const char* e = getenv("FTS_GT1")) c->gt1 = std::max(8, std::min(1024, atoi(e)));
   if (const char* e = getenv("FTS_GT2_MIN")) c->gt2_min = std::max(0, atoi(e));
+  if (const char* e = getenv("FTS_FX_ORDER")) g_fx_proof_fastest = atoi(e) != 0;
   if (const char* e = getenv("FTS_LAT_BS")) {  // block size of the latency-bound kernels (64, 128 or 256)
     const int v = atoi(e);
     g_lat_bs = v <= 64 ? 64 : v <= 128 ? 128 : 256;

@@ -37,6 +37,10 @@ namespace fts {
 // pass's streams rarely share a SIMD (64-thread blocks of two such kernels
 // slowed each other by ~26 %, tools/experiments/colocate.cpp).  FTS_LAT_BS.
 int g_lat_bs = 256;
+// k_rp_fixed_exact lane order (FTS_FX_ORDER): 1 = proof index fastest (a wave's
+// gathers stay inside one base's table: 6.9 -> 6.2 ms per 81,920-proof launch,
+// tools/run_fxorder.sh), 0 = one proof's 66 items side by side (round 1)
+int g_fx_proof_fastest = 1;
 
 
 constexpr int NORM_BS = 256;
@@ -338,11 +342,13 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, c
                                                           const uint32_t* __restrict__ sc, const uint32_t* __restrict__ ch,
                                                           const uint32_t* __restrict__ ypow,
                                                           const uint32_t* __restrict__ wtables, uint32_t* __restrict__ hpj,
-                                                          uint32_t* __restrict__ terms) {
+                                                          uint32_t* __restrict__ terms, int proof_fastest) {
   const int ni = n + 2;
-  int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= B * ni) return;
-  const int b = gid / ni, t = gid % ni;
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (size_t)B * ni) return;
+  // proof_fastest: a wave's 64 lanes gather from the same base's table (and read
+  // ypow[t][b] coalesced); else one proof's items side by side
+  const int b = proof_fastest ? (int)(gid % B) : (int)(gid / ni), t = proof_fastest ? (int)(gid / B) : (int)(gid % ni);
   if (status[b] != 0) return;
   const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
   uint32_t* out;
@@ -1333,7 +1339,8 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
                        k, d.status, d.pts, d.terms, d.hpj);
     tl->mark("k_rp_com_sum", s, (double)B * (com_fx_slots(n) + 1) * COST_ADD);
   } else {
-    FTS_LAUNCH(k_rp_fixed_exact, B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, wtables, d.hpj, d.terms);
+    FTS_LAUNCH(k_rp_fixed_exact, (size_t)B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, wtables, d.hpj,
+               d.terms, g_fx_proof_fastest);
     tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FBW_FRESH);
     if (d.rlc_fork) rlc_side();
     // H'_i -> affine + BE bytes (x0 transcript) now; com is normalised after com_sum
