@@ -44,7 +44,10 @@ int g_fx_proof_fastest = 1;
 
 
 constexpr int NORM_BS = 256;
-constexpr int NORM_E = 4;  // points per lane of k_rp_normalize
+#ifndef FTS_NORM_E
+#define FTS_NORM_E 4
+#endif
+constexpr int NORM_E = FTS_NORM_E;  // points per lane of k_rp_normalize
 __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, int stride, int first,
                                                           const int32_t* __restrict__ status,
                                                           const uint32_t* __restrict__ jac, uint32_t* __restrict__ aff,
