@@ -950,7 +950,7 @@ def bench_idemix(args):
     import random
     import numpy as np
     from fts_gpu import idemix as I
-    from oracle import bn254, idemix as O
+    from oracle import idemix as O
     t0 = time.time()
     bn = args.idemix_curve == "bn254"
     C = O.BN254C if bn else O.FP256BNC

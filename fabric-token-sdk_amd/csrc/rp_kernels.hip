@@ -44,14 +44,18 @@ int g_fx_proof_fastest = 1;
 
 
 constexpr int NORM_BS = 256;
-#ifndef FTS_NORM_E
-#define FTS_NORM_E 4
-#endif
-constexpr int NORM_E = FTS_NORM_E;  // points per lane of k_rp_normalize
+// points per lane of k_rp_normalize: 8 for normalisations of >= NORM_BIG points
+// (half the blocks, scans and inversions: 1.23 -> 0.89 ms at 5.3 M points),
+// 4 below (more blocks to fill the chip: at 262 k points 8 was 0.07 ms slower)
+constexpr int NORM_E = 4;  // nominal, for the cost model
+constexpr size_t NORM_BIG = (size_t)1 << 20;
+template <int E>
 __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, int stride, int first,
                                                           const int32_t* __restrict__ status,
                                                           const uint32_t* __restrict__ jac, uint32_t* __restrict__ aff,
                                                           uint8_t* __restrict__ be);
+static void launch_normalize(size_t total, int per, int stride, int first, const int32_t* status, const uint32_t* jac,
+                             uint32_t* aff, uint8_t* be, hipStream_t s);
 
 // ---------------------------------------------------------- context tables
 // Built once per context (device/fixed_base.hpp layout), for nb bases:
@@ -578,6 +582,7 @@ __global__ void __launch_bounds__(CT_LANES * CT_PROOFS) k_rp_com_tree(int B, int
 //   4. lane-local back-sweep: z_j^-1, then x z^-2, y z^-3.
 // ~9 products per point (the scans cost 16 / NORM_E per point).  Writes affine
 // Montgomery (aff, 16 words) and the canonical 64-byte BE encoding (be).
+template <int E>
 __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, int stride, int first,
                                                           const int32_t* __restrict__ status,
                                                           const uint32_t* __restrict__ jac, uint32_t* __restrict__ aff,
@@ -585,13 +590,13 @@ __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, in
   __shared__ uint32_t pre[NORM_BS * 8], suf[NORM_BS * 8];
   __shared__ uint32_t invs[8];
   const int t = threadIdx.x;
-  const size_t g0 = (size_t)blockIdx.x * NORM_BS * NORM_E + t;
+  const size_t g0 = (size_t)blockIdx.x * NORM_BS * E + t;
   // liveness is read ONCE per point: status may change while this kernel runs
   // (k_sig_exclude on the batch-check stream marks excluded proofs NOT_RUN), and
   // the prefix products and the back-sweep must skip exactly the same points
   uint32_t livem = 0;
 #pragma unroll
-  for (int j = 0; j < NORM_E; j++) {
+  for (int j = 0; j < E; j++) {
     const size_t g = g0 + (size_t)j * NORM_BS;
     if (g < (size_t)total && !(status && status[g / per] != 0)) livem |= 1u << j;
   }
@@ -604,18 +609,18 @@ __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, in
     if (!f_is_zero(zz)) z = zz;
     return true;
   };
-  Fp acc[NORM_E];
+  Fp acc[E];
   {
     Fp run = f_one<FpP>();
 #pragma unroll
-    for (int j = 0; j < NORM_E; j++) {
+    for (int j = 0; j < E; j++) {
       Fp z;
       zload(j, z);
       run = j ? fp_mul(run, z) : z;
       acc[j] = run;
     }
   }
-  const Fp tot = acc[NORM_E - 1];
+  const Fp tot = acc[E - 1];
   store_fp(pre + t * 8, tot);
   store_fp(suf + t * 8, tot);
   __syncthreads();
@@ -654,7 +659,7 @@ __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, in
     }
   }
 #pragma unroll
-  for (int j = NORM_E - 1; j >= 0; j--) {
+  for (int j = E - 1; j >= 0; j--) {
     Fp z;
     const bool live = zload(j, z);
     Fp zi = j ? fp_mul(inv, acc[j - 1]) : inv;  // z_j^-1
@@ -1236,6 +1241,14 @@ __global__ void __launch_bounds__(256) k_rlc_group_final(int slots, int gs, cons
     size_t nt_ = (size_t)(nthreads);                                                  \
     if (nt_) hipLaunchKernelGGL(kern, dim3((unsigned)((nt_ + (bs)-1) / (bs))), dim3(bs), 0, stream, __VA_ARGS__); \
   } while (0)
+static void launch_normalize(size_t total, int per, int stride, int first, const int32_t* status, const uint32_t* jac,
+                             uint32_t* aff, uint8_t* be, hipStream_t s) {
+  if (total >= NORM_BIG)
+    FTS_LAUNCH(k_rp_normalize<8>, (total + 7) / 8, NORM_BS, s, (int)total, per, stride, first, status, jac, aff, be);
+  else
+    FTS_LAUNCH(k_rp_normalize<4>, (total + 3) / 4, NORM_BS, s, (int)total, per, stride, first, status, jac, aff, be);
+}
+
 
 
 
@@ -1268,8 +1281,7 @@ static void build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32
   FTS_LAUNCH(kt_small_large<W>, nbw, 64, s, nb, bw, small, large);
   FTS_LAUNCH(kt_entries<W>, nbw * C::E, 64, s, nb, small, large, jac);
   const size_t tot = nbw * C::E;
-  FTS_LAUNCH(k_rp_normalize, (tot + NORM_E - 1) / NORM_E, NORM_BS, s, (int)tot, 1, 1, 0, (const int32_t*)nullptr, jac,
-             tables, (uint8_t*)nullptr);
+  launch_normalize(tot, 1, 1, 0, (const int32_t*)nullptr, jac, tables, (uint8_t*)nullptr, s);
 }
 void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s) {
   build_tables<FB_W>(bases, nb, tables, scratch, s);
@@ -1334,8 +1346,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
                d.hpj, d.terms);
     tl->mark("k_rp_fixed_all", s, (double)B * (2.0 * n + 2.0) * COST_FBW_FRESH);
     if (d.rlc_fork) rlc_side();
-    FTS_LAUNCH(k_rp_normalize, (nhp + NORM_E - 1) / NORM_E, NORM_BS, s, nhp, n, n + 1, 0, d.status, d.hpj, d.hpa,
-               d.hp_be);
+    launch_normalize(nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be, s);
     tl->mark("k_rp_normalize", s, (double)nhp * (2.0 * 8.0 / NORM_E + 9.0));
     tl->fork(s2, s);
     hipLaunchKernelGGL(k_rp_com_tree, dim3((B + CT_PROOFS - 1) / CT_PROOFS), dim3(CT_LANES * CT_PROOFS), 0, s, B, n,
@@ -1347,8 +1358,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FBW_FRESH);
     if (d.rlc_fork) rlc_side();
     // H'_i -> affine + BE bytes (x0 transcript) now; com is normalised after com_sum
-    FTS_LAUNCH(k_rp_normalize, (nhp + NORM_E - 1) / NORM_E, NORM_BS, s, nhp, n, n + 1, 0, d.status, d.hpj, d.hpa,
-               d.hp_be);
+    launch_normalize(nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be, s);
     tl->mark("k_rp_normalize", s, (double)nhp * (2.0 * 8.0 / NORM_E + 9.0));
     if (d.x0_mid) {
       // x0 prefix on the side stream: the H' records and the shared template
@@ -1373,7 +1383,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     FTS_LAUNCH(k_rp_com_sum, B, 64, s, B, n, k, d.status, d.pts, d.terms, d.hpj);
     tl->mark("k_rp_com_sum", s, (double)B * COM_NTERMS * COST_ADD);
   }
-  FTS_LAUNCH(k_rp_normalize, (B + NORM_E - 1) / NORM_E, NORM_BS, s, B, 1, n + 1, n, d.status, d.hpj, d.hpa, d.hp_be);
+  launch_normalize(B, 1, n + 1, n, d.status, d.hpj, d.hpa, d.hp_be, s);
   tl->mark("k_rp_normalize_com", s, (double)B * (2.0 * 8.0 / NORM_E + 9.0));
   const bool split = !d.com_fixed && d.x0_mid;
   hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s, B, n, d.status, d.hp_be, x0_const, d.sc,
@@ -1397,8 +1407,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
 }
 
 void launch_normalize_all(int total, const uint32_t* jac, uint32_t* aff, hipStream_t s) {
-  FTS_LAUNCH(k_rp_normalize, (total + NORM_E - 1) / NORM_E, NORM_BS, s, total, 1, 1, 0, (const int32_t*)nullptr, jac,
-             aff, (uint8_t*)nullptr);
+  launch_normalize(total, 1, 1, 0, (const int32_t*)nullptr, jac, aff, (uint8_t*)nullptr, s);
 }
 
 // per-proof final equations (fallback when the batch combination fails)
