@@ -59,6 +59,7 @@ void launch_sig_prep(const SigBatchDev& d, hipStream_t s);
 void launch_sig_finish(const SigBatchDev& d, const uint32_t* tables, int n, hipStream_t s);
 extern int g_lat_bs;
 extern int g_fx_proof_fastest;  // rp_kernels.hip (FTS_FX_ORDER)
+extern int g_chain_bs;          // rp_kernels.hip (FTS_CHAIN_BS)
 void launch_sig_exclude(const SigBatchDev& d, int32_t* rp_excl, hipStream_t s);
 size_t table_build_scratch_bytes(int nb);
 size_t fb_words_per_base();
@@ -542,6 +543,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_GT1")) c->gt1 = std::max(8, std::min(1024, atoi(e)));
   if (const char* e = getenv("FTS_GT2_MIN")) c->gt2_min = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_FX_ORDER")) g_fx_proof_fastest = atoi(e) != 0;
+  if (const char* e = getenv("FTS_CHAIN_BS")) g_chain_bs = atoi(e) >= 256 ? 256 : atoi(e) >= 128 ? 128 : 64;
   if (const char* e = getenv("FTS_LAT_BS")) {  // block size of the latency-bound kernels (64, 128 or 256)
     const int v = atoi(e);
     g_lat_bs = v <= 64 ? 64 : v <= 128 ? 128 : 256;

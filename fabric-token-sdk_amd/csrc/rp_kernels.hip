@@ -41,6 +41,8 @@ int g_lat_bs = 256;
 // gathers stay inside one base's table: 6.9 -> 6.2 ms per 81,920-proof launch,
 // tools/run_fxorder.sh), 0 = one proof's 66 items side by side (round 1)
 int g_fx_proof_fastest = 1;
+// block size of the work path's S / com chain kernels (FTS_CHAIN_BS: 64 or 256)
+int g_chain_bs = 64;
 
 
 constexpr int NORM_BS = 256;
@@ -387,7 +389,7 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, c
 }
 
 // lane per (proof, chunk c): S_c = sum_{j < 8} 2^j H'_{8c+j} (Horner over the affine H')
-__global__ void __launch_bounds__(64) k_rp_hsum_chunks(int B, int n, const int32_t* __restrict__ status,
+__global__ void __launch_bounds__(256) k_rp_hsum_chunks(int B, int n, const int32_t* __restrict__ status,
                                                        const uint32_t* __restrict__ hpa, uint32_t* __restrict__ chunks) {
   const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -407,7 +409,7 @@ __global__ void __launch_bounds__(64) k_rp_hsum_chunks(int B, int n, const int32
 
 // lane per proof: S = sum_c 2^(8c) S_c (Horner over the chunk sums), written
 // over chunk 0 -- once per proof instead of in both GLV lanes of k_rp_com_var
-__global__ void __launch_bounds__(64) k_rp_hsum_join(int B, int n, const int32_t* __restrict__ status,
+__global__ void __launch_bounds__(256) k_rp_hsum_join(int B, int n, const int32_t* __restrict__ status,
                                                      uint32_t* __restrict__ chunks) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B || status[b] != 0) return;
@@ -425,7 +427,7 @@ __global__ void __launch_bounds__(64) k_rp_hsum_join(int B, int n, const int32_t
 // with x = x1 + x2 lambda and z^2 = w1 + w2 lambda (GLV), lane h computes
 // x_h phi^h(D) + w_h phi^h(S) in one joint Straus chain (glv.hpp), where
 // S = sum_c 2^(8c) S_c is assembled by Horner first -> terms[b][2 + h]
-__global__ void __launch_bounds__(64) k_rp_com_var(int B, int n, int k, const int32_t* __restrict__ status,
+__global__ void __launch_bounds__(256) k_rp_com_var(int B, int n, int k, const int32_t* __restrict__ status,
                                                    const uint32_t* __restrict__ pts, const uint32_t* __restrict__ ch,
                                                    const uint32_t* __restrict__ chunks, uint32_t* __restrict__ vtab,
                                                    uint32_t* __restrict__ terms) {
@@ -1372,12 +1374,12 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
       tl->mark("k_rp_x0_prefix", s2, 0);
     }
     const int nch = (n + HS_CHUNK - 1) / HS_CHUNK;
-    FTS_LAUNCH(k_rp_hsum_chunks, B * nch, 64, s, B, n, d.status, d.hpa, d.scratch);
+    FTS_LAUNCH(k_rp_hsum_chunks, B * nch, g_chain_bs, s, B, n, d.status, d.hpa, d.scratch);
     tl->mark("k_rp_hsum_chunks", s, (double)B * (n - nch) * (COST_DBL + COST_MADD));
-    FTS_LAUNCH(k_rp_hsum_join, B, 64, s, B, n, d.status, d.scratch);
+    FTS_LAUNCH(k_rp_hsum_join, B, g_chain_bs, s, B, n, d.status, d.scratch);
     tl->mark("k_rp_hsum_join", s, (double)B * (nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD));
     // scratch: [0, B*192) Horner chunks of S, then the 2B lanes' joint tables
-    FTS_LAUNCH(k_rp_com_var, 2 * B, 64, s, B, n, k, d.status, d.pts, d.ch, d.scratch,
+    FTS_LAUNCH(k_rp_com_var, 2 * B, g_chain_bs, s, B, n, k, d.status, d.pts, d.ch, d.scratch,
                d.scratch + (size_t)B * HS_SCRATCH, d.terms);
     tl->mark("k_rp_com_var", s, (double)B * 2 * COST_STRAUS2);
     FTS_LAUNCH(k_rp_com_sum, B, 64, s, B, n, k, d.status, d.pts, d.terms, d.hpj);
