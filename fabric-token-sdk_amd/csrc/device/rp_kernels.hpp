@@ -174,7 +174,8 @@ struct RpBatchDev {
   void* pre_rlc_arg;
   int com_fixed;       // 1: com by fixed-base groups + x*D on the side stream (latency path,
                        //    small passes); 0: Horner sum + joint GLV/Straus chains (work path)
-  int rlc_fork = 1;    // batch check's stream forks after the fixed-base products (1) or after the challenges (0)
+  int rlc_fork = 1;    // batch check's stream forks after the fixed-base products (1) or after the challenges (0);
+                       //    fts_api.cpp picks 0 on the latency path, 1 on the work path (FTS_RLC_FORK=2)
   hipEvent_t ev_coef = nullptr;  // recorded on the check's stream after k_rlc_prep (column Q on s waits for it)
   uint32_t* x0_mid = nullptr;    // [B][8] SHA-256 midstate of the x0 prefix (work path; nullptr: one-piece hash)
   int32_t* excl = nullptr;       // [B] optional: 1 = left out of the batch check (set by the pre_rlc hook), NOT_RUN
