@@ -1010,8 +1010,9 @@ def bench_idemix(args):
         step()
         kms += K.last_kernel_ms()
     ms = kms / reps
-    # FP256BN: 2 x 16 mixed additions, table 7 additions, 252 doublings + 64 full additions, on-curve 4
-    muls = NYM_MULS_PER_VERIFY if bn else 2 * 16 * 11 + 7 * 11 + 252 * 7 + 64 * 16 + 4
+    # FP256BN: 2 x 16 mixed additions, GLV tables 2 x 7 mixed additions, 128 doublings,
+    # <= 2 x 33 full additions (~64), beta and the on-curve check (5)
+    muls = NYM_MULS_PER_VERIFY if bn else 2 * 16 * 11 + 14 * 11 + 128 * 7 + 64 * 16 + 5
     mads = n * muls * MAD_PER_MUL  # tampered items run the full path
     ach = mads / (ms * 1e-3) / 1e12
     roof = {"bound": "int32_valu (v_mad_u64_u32)", "kernel": "k_nym_verify" + ("" if bn else "_fbn"), "achieved": round(ach, 3),

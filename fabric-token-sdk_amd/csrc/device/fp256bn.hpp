@@ -31,6 +31,23 @@ struct RM {  // group order r = 0xFFFFFFFFFFFCF0CD46E5F25EEE71A49E0CDC65FB129992
 __device__ constexpr uint32_t CB3[8] = {0xf3866fc7u, 0x8684766cu, 0xc837e077u, 0xd96ace0eu,
                                         0x34ab1222u, 0x2b4e28e3u, 0x00092d98u, 0x00000000u};
 
+// GLV (j = 0): phi(x, y) = (beta x, y) = lambda (x, y) with
+// lambda = 0x27311c281242030ce379baf3be321c37067081e9398533016 (mod r) and
+// beta = 0x13988e140921018659bcdd79df1932d1edb1c0a24a3a1b807 (mod p); lattice
+// basis from the extended Euclid of (r, lambda), g_i = floor(2^384 b_i / r),
+// derived with Python the same way as glv.hpp's BN254 constants.  |k1|, |k2| < 2^128.
+struct GlvK {
+  static constexpr uint32_t BETA[8] = {0x84008c2cu, 0xac441038u, 0xf524db81u, 0x26e76706u,
+                                       0xb51eaff8u, 0x49cc4e27u, 0x3c3f9cffu, 0x26664872u};  // Montgomery
+  static constexpr uint32_t G1[7] = {0xf899d382u, 0x88097763u, 0xce889a08u, 0x859835ddu,
+                                     0x6163cf7bu, 0xd105eb80u, 0x00000000u};
+  static constexpr uint32_t G2[9] = {0xa170acebu, 0x8cb9048bu, 0xee129700u, 0xca13df5cu, 0xda9e04d4u,
+                                     0xf40a1113u, 0x00018798u, 0x00000000u, 0x00000001u};
+  static constexpr uint32_t A1[2] = {0x61615001u, 0xd105eb80u};                          // a1 (= b2)
+  static constexpr uint32_t A2[4] = {0x7c669004u, 0x0bf5eeeeu, 0xfffe7867u, 0xffffffffu};  // a2
+  static constexpr uint32_t NB1[4] = {0x1b054003u, 0x3af0036eu, 0xfffe7866u, 0xffffffffu}; // -b1
+};
+
 using Fp = p256::F<PM>;
 using p256::add;
 using p256::sub;

@@ -87,11 +87,14 @@ FTS_DEV uint32_t glv_abs(const uint32_t v[8], uint32_t out[4]) {
   return neg;
 }
 
-// k (canonical, 8 limbs) -> k1, k2 (|.| in 4 limbs) with signs: k = k1 + k2 lambda mod r
+// k (canonical, 8 limbs) -> k1, k2 (|.| in 4 limbs) with signs: k = k1 + k2 lambda mod r.
+// K: the curve's constants (Glv for BN254; fbn::GlvK for FP256BN, same basis shape:
+// a1 = b2 > 0 of 64 bits, a2 > 0 and -b1 > 0 of 128 bits)
+template <class K = Glv>
 FTS_DEV void glv_decompose(const uint32_t k[8], uint32_t k1[4], uint32_t& s1, uint32_t k2[4], uint32_t& s2) {
   uint32_t c1[5], c2[5];
-  glv_round<7>(k, Glv::G1, c1);
-  glv_round<9>(k, Glv::G2, c2);
+  glv_round<7>(k, K::G1, c1);
+  glv_round<9>(k, K::G2, c2);
   uint32_t r1[8], r2[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -99,15 +102,15 @@ FTS_DEV void glv_decompose(const uint32_t k[8], uint32_t k1[4], uint32_t& s1, ui
     r2[i] = 0;
   }
   // k1 = k - c1 a1 - c2 a2
-  sub_mul_256<3, 2>(r1, c1, Glv::A1);
-  sub_mul_256<5, 4>(r1, c2, Glv::A2);
+  sub_mul_256<3, 2>(r1, c1, K::A1);
+  sub_mul_256<5, 4>(r1, c2, K::A2);
   // k2 = c1 (-b1) - c2 b2 = -( c2 b2 - c1 (-b1) )   (b2 = a1)
-  sub_mul_256<5, 2>(r2, c2, Glv::A1);  // r2 = -c2 b2
+  sub_mul_256<5, 2>(r2, c2, K::A1);  // r2 = -c2 b2
   {
     uint32_t p[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) p[i] = 0;
-    sub_mul_256<3, 4>(p, c1, Glv::NB1);  // p = -c1 (-b1)
+    sub_mul_256<3, 4>(p, c1, K::NB1);  // p = -c1 (-b1)
     uint32_t bw = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) r2[i] = subb(r2[i], p[i], bw, bw);  // r2 = -c2 b2 + c1 (-b1)

@@ -226,6 +226,45 @@ FTS_DEV void digest_mod_rfbn(const uint32_t st[8], uint32_t out[8]) {
   for (int i = 0; i < 8; i++) out[i] = bw ? out[i] : t[i];
 }
 
+// FP256BN GLV chain helpers: the lane's 16-entry Jacobian table in global
+// memory, [entry][word][stride] (as glv.hpp's vtab for BN254), and the signed
+// 4-bit recoding of a 128-bit magnitude over 33 windows (window 32 = the carry)
+__device__ inline void fbn_vtab_store(uint32_t* __restrict__ tab, size_t stride, size_t idx, int e, const fbn::PJ& p) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    tab[((size_t)(e * 24) + k) * stride + idx] = p.x.v[k];
+    tab[((size_t)(e * 24) + 8 + k) * stride + idx] = p.y.v[k];
+    tab[((size_t)(e * 24) + 16 + k) * stride + idx] = p.z.v[k];
+  }
+}
+__device__ inline fbn::PJ fbn_vtab_load(const uint32_t* __restrict__ tab, size_t stride, size_t idx, int e) {
+  fbn::PJ p;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    p.x.v[k] = tab[((size_t)(e * 24) + k) * stride + idx];
+    p.y.v[k] = tab[((size_t)(e * 24) + 8 + k) * stride + idx];
+    p.z.v[k] = tab[((size_t)(e * 24) + 16 + k) * stride + idx];
+  }
+  return p;
+}
+__device__ inline uint64_t fbn_recode(const uint32_t s[4]) {  // bit w = carry into window w
+  uint64_t cm = 0;
+  uint32_t c = 0;
+#pragma unroll
+  for (int w = 0; w < 33; w++) {
+    cm |= (uint64_t)c << w;
+    const uint32_t raw = w < 32 ? (s[w >> 3] >> (4 * (w & 7))) & 15u : 0u;
+    c = raw + c > 8u;
+  }
+  return cm;
+}
+__device__ inline int fbn_digit(const uint32_t s[4], uint64_t cm, int w) {  // in [-8, 8]
+  const int raw = w < 32 ? (int)((s[w >> 3] >> (4 * (w & 7))) & 15u) : 0;
+  const int cin = (int)((cm >> w) & 1u);
+  const int cout = w < 32 ? (int)((cm >> (w + 1)) & 1u) : 0;
+  return raw + cin - 16 * cout;
+}
+
 // One FP256BN nym signature per lane.  The host materialises each item's hashed
 // stream "sign" || 0x04 || t (64 zero bytes) || Nym (65) || ipk.Hash || msg in
 // the region (word aligned); the kernel supplies t's words in registers.
@@ -236,6 +275,7 @@ __global__ __launch_bounds__(256) void k_nym_verify_fbn(int n, const uint32_t* _
                                                         const uint64_t* __restrict__ roff,  // word offsets
                                                         const uint32_t* __restrict__ rlen,  // stream bytes
                                                         const uint32_t* __restrict__ tables,
+                                                        uint32_t* __restrict__ vtab,
                                                         int32_t* __restrict__ status) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || status[i] != FTS_OK) return;
@@ -268,7 +308,9 @@ __global__ __launch_bounds__(256) void k_nym_verify_fbn(int n, const uint32_t* _
       }
     }
   }
-  // (r - c) Nym: signed 4-bit windows over a table of 1..8 Nym (as k_ecdsa_verify)
+  // (r - c) Nym by GLV: e = k1 + k2 lambda, one joint chain of k1 (+-Nym) +
+  // k2 (+-phi(Nym)) over 33 signed 4-bit windows (|k_i| < 2^128), 128 doublings
+  // instead of 252; tables 1..8 of both points in the lane's global slot
   uint32_t e[8];
   {
     uint32_t bw = 0, nz = 0;
@@ -277,30 +319,40 @@ __global__ __launch_bounds__(256) void k_nym_verify_fbn(int n, const uint32_t* _
 #pragma unroll
     for (int k = 0; k < 8; k++) e[k] = nz ? subb(fbn::RM::M[k], R[k], bw, bw) : 0u;
   }
-  uint64_t cm = 0;
+  uint32_t k1[4], k2[4], s1, s2;
+  fts::glv_decompose<fbn::GlvK>(e, k1, s1, k2, s2);
+  const fbn::Fp nQy = fbn::sub(fbn::Fp{}, Qy);
+  const fbn::Fp Px = Qx, Py = s1 ? nQy : Qy;
+  const fbn::Fp Ex = fbn::mul(Qx, fbn::load<fbn::PM>(fbn::GlvK::BETA)), Ey = s2 ? nQy : Qy;
+  const size_t stride = (size_t)n;
   {
-    uint32_t c = 0;
-    for (int w = 0; w < 64; w++) {
-      cm |= (uint64_t)c << w;
-      c = ((e[w >> 3] >> (4 * (w & 7))) & 15u) + c > 8u;
+    fbn::PJ cp, ce;
+    cp.x = Px, cp.y = Py, cp.z = fbn::load<fbn::PM>(fbn::PM::ONE);
+    ce.x = Ex, ce.y = Ey, ce.z = cp.z;
+    fbn_vtab_store(vtab, stride, (size_t)i, 0, cp);
+    fbn_vtab_store(vtab, stride, (size_t)i, 8, ce);
+    for (int k = 1; k < 8; k++) {
+      cp = fbn::pj_madd(cp, Px, Py);
+      ce = fbn::pj_madd(ce, Ex, Ey);
+      fbn_vtab_store(vtab, stride, (size_t)i, k, cp);
+      fbn_vtab_store(vtab, stride, (size_t)i, 8 + k, ce);
     }
   }
-  const uint32_t c64 = (e[7] >> 28) + ((uint32_t)(cm >> 63) & 1u) > 8u;
-  fbn::PJ tab[9];
-  tab[0] = fbn::pj_inf();
-  tab[1].x = Qx, tab[1].y = Qy, tab[1].z = fbn::load<fbn::PM>(fbn::PM::ONE);
-  for (int k = 2; k < 9; k++) tab[k] = fbn::pj_madd(tab[k - 1], Qx, Qy);
-  fbn::PJ vb = c64 ? tab[1] : fbn::pj_inf();
-  for (int nib = 63; nib >= 0; nib--) {
-    vb = fbn::pj_dbl(fbn::pj_dbl(fbn::pj_dbl(fbn::pj_dbl(vb))));
-    const int raw = (int)((e[nib >> 3] >> (4 * (nib & 7))) & 15u);
-    const int cin = (int)((cm >> nib) & 1u);
-    const int cout = nib < 63 ? (int)((cm >> (nib + 1)) & 1u) : (int)c64;
-    const int d = raw + cin - 16 * cout;
-    if (d) {
-      fbn::PJ q = tab[d < 0 ? -d : d];
-      if (d < 0) q.y = fbn::sub(fbn::Fp{}, q.y);
-      vb = fbn::pj_add(vb, q);
+  const uint64_t ca = fbn_recode(k1), cb = fbn_recode(k2);
+  fbn::PJ vb = fbn::pj_inf();
+  for (int w = 32; w >= 0; w--) {
+    const int da = fbn_digit(k1, ca, w), db = fbn_digit(k2, cb, w);
+    fbn::PJ qa, qb;
+    if (da) qa = fbn_vtab_load(vtab, stride, (size_t)i, (da < 0 ? -da : da) - 1);
+    if (db) qb = fbn_vtab_load(vtab, stride, (size_t)i, 8 + (db < 0 ? -db : db) - 1);
+    if (w != 32) vb = fbn::pj_dbl(fbn::pj_dbl(fbn::pj_dbl(fbn::pj_dbl(vb))));
+    if (da) {
+      if (da < 0) qa.y = fbn::sub(fbn::Fp{}, qa.y);
+      vb = fbn::pj_add(vb, qa);
+    }
+    if (db) {
+      if (db < 0) qb.y = fbn::sub(fbn::Fp{}, qb.y);
+      vb = fbn::pj_add(vb, qb);
     }
   }
   const fbn::PJ X = fbn::pj_add(acc, vb);
@@ -858,7 +910,7 @@ int fts_nym_verify_batch(fts_idemix_ipk* K, size_t n, const fts_nym_item* items,
     k_nym_verify_fbn<<<(unsigned)((n + 255) / 256), 256, 0, D.stream>>>(
         (int)n, reinterpret_cast<const uint32_t*>(d), d + o_nym, reinterpret_cast<const uint32_t*>(d + o_msg),
         reinterpret_cast<const uint64_t*>(d + o_off), reinterpret_cast<const uint32_t*>(d + o_len), K->d_tables,
-        reinterpret_cast<int32_t*>(d + o_st));
+        reinterpret_cast<uint32_t*>(d + o_vt), reinterpret_cast<int32_t*>(d + o_st));
   ICHK(hipGetLastError());
   ICHK(hipEventRecord(D.ev[1], D.stream));
   ICHK(hipMemcpyAsync(h + o_st, d + o_st, st_b, hipMemcpyDeviceToHost, D.stream));
