@@ -149,8 +149,18 @@ def test_random_batch_against_oracle(ipk_dev):
 @pytest.mark.gpu
 def test_large_batch_packed_tiled(ipk_dev):
     """65,536 signatures (a tiled 256-signature oracle batch): verdicts exact at every position."""
+    _tiled(ipk_dev, "bn254")
+
+
+@pytest.mark.gpu
+def test_large_batch_packed_tiled_fp256bn(ipk_fbn):
+    """The FP256BN kernel (GLV chain, per-lane tables strided over 65,536 lanes) at full size."""
+    _tiled(ipk_fbn, "fp256bn")
+
+
+def _tiled(dev, curve):
     import numpy as np
-    nyms, sigs, msgs, want = _batch(256, seed=12, tamper=0.05)
+    nyms, sigs, msgs, want = _batch(256, seed=12, tamper=0.05, curve=curve)
     reps = 256
     n = 256 * reps
     nym_buf = b"".join(nyms) * reps
@@ -159,8 +169,8 @@ def test_large_batch_packed_tiled(ipk_dev):
     mo = np.cumsum([0] + [len(m) for m in msgs[:-1]]).astype(np.uint64)
     sl = np.array([len(s) for s in sigs], dtype=np.uint64)
     ml = np.array([len(m) for m in msgs], dtype=np.uint64)
-    st = ipk_dev.verify_packed(nym_buf, sig_buf, np.tile(so, reps), np.tile(sl, reps), msg_buf, np.tile(mo, reps),
-                               np.tile(ml, reps))
+    st = dev.verify_packed(nym_buf, sig_buf, np.tile(so, reps), np.tile(sl, reps), msg_buf, np.tile(mo, reps),
+                           np.tile(ml, reps))
     exp = np.tile(np.array([w is None for w in want]), reps)
     assert st.shape == (n,)
     assert ((st == 0) == exp).all()
