@@ -297,7 +297,10 @@ FTS_DEV G1J straus2_128(const G1J& P, const uint32_t a[4], const G1J& Q, const u
 // then the joint chain k1 P + k2 phi(P) (124 doublings instead of 252);
 // tab/stride/idx: the lane's 16-entry table (straus2_128).  Keep it inlined
 // at ONE call site per kernel: an out-of-line (__noinline__) build of this
-// function never terminated on gfx950 (tools/glv_check reproduces it).
+// function never terminates on gfx950 -- branch relaxation in a callable
+// function clobbers its return address s[30:31] (reproducer
+// tools/experiments/glv_noinline_repro.hip, guard tools/long_branch_check.py,
+// run by build() and tests/test_isa_cpu.py).
 FTS_DEV G1J glv_mul(const G1A& p, const Scalar& k, uint32_t* __restrict__ tab, size_t stride, size_t idx) {
   if (g1a_is_identity(p)) return g1j_identity();
   uint32_t k1[4], k2[4], s1, s2;
