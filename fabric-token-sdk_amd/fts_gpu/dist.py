@@ -40,6 +40,29 @@ def allgather_verdicts(dist, status):
     return np.concatenate([np.unpackbits(blocks[r])[:counts[r]].astype(bool) for r in range(world)])
 
 
+def allgather_status(dist, values):
+    """values: this rank's int32 array (e.g. fts_status per action, or interleaved
+    (status, fail_index) pairs; ranks may hold different lengths) -> the int32
+    concatenation of ALL ranks' arrays in rank order.  Same two-collective shape
+    as allgather_verdicts (counts, then equal-size padded blocks), for endorsers
+    that need the error class and failing index of every item, not only the bit."""
+    import torch
+    dev = _dev(dist)
+    v = np.ascontiguousarray(np.asarray(values, dtype=np.int32).ravel())
+    world = dist.get_world_size()
+    cnt = torch.tensor([v.size], dtype=torch.int64, device=dev)
+    counts = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(counts, cnt)
+    counts = [int(c) for c in counts.cpu()]
+    width = max(1, max(counts))
+    pad = np.zeros(width, dtype=np.int32)
+    pad[:v.size] = v
+    out = torch.empty(world * width, dtype=torch.int32, device=dev)
+    dist.all_gather_into_tensor(out, torch.from_numpy(pad).to(dev))
+    blocks = out.cpu().numpy().reshape(world, width)
+    return np.concatenate([blocks[r][:counts[r]] for r in range(world)])
+
+
 def reduce_scalar(dist, x, op="max"):
     """max/sum of a Python number over ranks"""
     import torch
