@@ -547,12 +547,18 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_X0_SPLIT")) c->x0_split = atoi(e) != 0;
   if (const char* e = getenv("FTS_GT1")) c->gt1 = std::max(8, std::min(1024, atoi(e)));
   if (const char* e = getenv("FTS_GT2_MIN")) c->gt2_min = std::max(0, atoi(e));
-  if (const char* e = getenv("FTS_FX_ORDER")) g_fx_proof_fastest = atoi(e) != 0;
-  if (const char* e = getenv("FTS_CHAIN_BS")) g_chain_bs = atoi(e) >= 256 ? 256 : atoi(e) >= 128 ? 128 : 64;
-  if (const char* e = getenv("FTS_LAT_BS")) {  // block size of the latency-bound kernels (64, 128 or 256)
-    const int v = atoi(e);
-    g_lat_bs = v <= 64 ? 64 : v <= 128 ? 128 : 256;
-  }
+  // process-wide launch knobs of rp_kernels.hip: read once, before any context can
+  // launch (contexts are created concurrently by fts_ctx_create_devices, and the
+  // launch code of live contexts reads these values)
+  static std::once_flag knobs_once;
+  std::call_once(knobs_once, [] {
+    if (const char* e = getenv("FTS_FX_ORDER")) g_fx_proof_fastest = atoi(e) != 0;
+    if (const char* e = getenv("FTS_CHAIN_BS")) g_chain_bs = atoi(e) >= 256 ? 256 : atoi(e) >= 128 ? 128 : 64;
+    if (const char* e = getenv("FTS_LAT_BS")) {  // block size of the latency-bound kernels (64, 128 or 256)
+      const int v = atoi(e);
+      g_lat_bs = v <= 64 ? 64 : v <= 128 ? 128 : 256;
+    }
+  });
   // FTS_SIDE_STREAM=0: run each lane's side work on its main stream
   bool side = true;
   if (const char* e = getenv("FTS_SIDE_STREAM")) side = atoi(e) != 0;

@@ -100,9 +100,13 @@ __global__ __launch_bounds__(256) void k_nym_verify(int n, const uint32_t* __res
                                                     const uint32_t* __restrict__ mlen,
                                                     const uint32_t* __restrict__ tables,
                                                     const uint32_t* __restrict__ ipk_hash,  // 8 BE words
-                                                    uint32_t* __restrict__ vtab, int32_t* __restrict__ status) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || status[i] != FTS_OK) return;
+                                                    uint32_t* __restrict__ vtab, int32_t* __restrict__ status,
+                                                    int base, int tile) {
+  // one launch per tile of `tile` items starting at `base`; the GLV lane table is
+  // [entry][word][tile] (bounded device memory whatever n is)
+  const int li = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = base + li;
+  if (li >= tile || i >= n || status[i] != FTS_OK) return;
   const uint32_t* R = rec + (size_t)i * NREC;
   // Nym: NewG1FromBytes (64-byte raw, canonical coordinates, on the curve)
   G1A nym;
@@ -122,7 +126,7 @@ __global__ __launch_bounds__(256) void k_nym_verify(int n, const uint32_t* __res
 #pragma unroll
     for (int k = 0; k < 8; k++) nc.v[k] = nz ? subb(FrP::M[k], R[k], bw, bw) : 0u;
   }
-  const G1J cn = glv_mul(nym, nc, vtab, (size_t)n, (size_t)i);
+  const G1J cn = glv_mul(nym, nc, vtab, (size_t)tile, (size_t)li);
   add_inl(acc, cn);
   const G1A t = g1j_to_affine(acc);  // identity -> (0, 0) -> 64 zero bytes (gnark RawBytes)
   uint32_t tw[16], nw[16], hw[8];
@@ -276,9 +280,10 @@ __global__ __launch_bounds__(256) void k_nym_verify_fbn(int n, const uint32_t* _
                                                         const uint32_t* __restrict__ rlen,  // stream bytes
                                                         const uint32_t* __restrict__ tables,
                                                         uint32_t* __restrict__ vtab,
-                                                        int32_t* __restrict__ status) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || status[i] != FTS_OK) return;
+                                                        int32_t* __restrict__ status, int base, int tile) {
+  const int li = blockIdx.x * blockDim.x + threadIdx.x;  // tiled as k_nym_verify
+  const int i = base + li;
+  if (li >= tile || i >= n || status[i] != FTS_OK) return;
   const uint32_t* R = rec + (size_t)i * NREC;
   uint32_t pw[16];
   load_be_words(nymxy + (size_t)i * 64, pw);
@@ -324,18 +329,18 @@ __global__ __launch_bounds__(256) void k_nym_verify_fbn(int n, const uint32_t* _
   const fbn::Fp nQy = fbn::sub(fbn::Fp{}, Qy);
   const fbn::Fp Px = Qx, Py = s1 ? nQy : Qy;
   const fbn::Fp Ex = fbn::mul(Qx, fbn::load<fbn::PM>(fbn::GlvK::BETA)), Ey = s2 ? nQy : Qy;
-  const size_t stride = (size_t)n;
+  const size_t stride = (size_t)tile;
   {
     fbn::PJ cp, ce;
     cp.x = Px, cp.y = Py, cp.z = fbn::load<fbn::PM>(fbn::PM::ONE);
     ce.x = Ex, ce.y = Ey, ce.z = cp.z;
-    fbn_vtab_store(vtab, stride, (size_t)i, 0, cp);
-    fbn_vtab_store(vtab, stride, (size_t)i, 8, ce);
+    fbn_vtab_store(vtab, stride, (size_t)li, 0, cp);
+    fbn_vtab_store(vtab, stride, (size_t)li, 8, ce);
     for (int k = 1; k < 8; k++) {
       cp = fbn::pj_madd(cp, Px, Py);
       ce = fbn::pj_madd(ce, Ex, Ey);
-      fbn_vtab_store(vtab, stride, (size_t)i, k, cp);
-      fbn_vtab_store(vtab, stride, (size_t)i, 8 + k, ce);
+      fbn_vtab_store(vtab, stride, (size_t)li, k, cp);
+      fbn_vtab_store(vtab, stride, (size_t)li, 8 + k, ce);
     }
   }
   const uint64_t ca = fbn_recode(k1), cb = fbn_recode(k2);
@@ -343,8 +348,8 @@ __global__ __launch_bounds__(256) void k_nym_verify_fbn(int n, const uint32_t* _
   for (int w = 32; w >= 0; w--) {
     const int da = fbn_digit(k1, ca, w), db = fbn_digit(k2, cb, w);
     fbn::PJ qa, qb;
-    if (da) qa = fbn_vtab_load(vtab, stride, (size_t)i, (da < 0 ? -da : da) - 1);
-    if (db) qb = fbn_vtab_load(vtab, stride, (size_t)i, 8 + (db < 0 ? -db : db) - 1);
+    if (da) qa = fbn_vtab_load(vtab, stride, (size_t)li, (da < 0 ? -da : da) - 1);
+    if (db) qb = fbn_vtab_load(vtab, stride, (size_t)li, 8 + (db < 0 ? -db : db) - 1);
     if (w != 32) vb = fbn::pj_dbl(fbn::pj_dbl(fbn::pj_dbl(fbn::pj_dbl(vb))));
     if (da) {
       if (da < 0) qa.y = fbn::sub(fbn::Fp{}, qa.y);
@@ -608,6 +613,8 @@ __global__ void k_fbn_bases(int nb, const uint32_t* __restrict__ plain, uint32_t
   } while (0)
 
 constexpr int NSLOT = 3;
+// items per nym-kernel launch (the GLV lane tables are sized for one tile)
+constexpr size_t NYM_TILE = 262144;
 struct Slot {
   hipStream_t stream = nullptr;
   uint8_t* d_buf = nullptr;  // rec | nym | moff | mlen | status | vtab | messages
@@ -631,6 +638,7 @@ struct fts_idemix_ipk {
   Slot slot[NSLOT];
   bool busy[NSLOT] = {false, false, false};
   float last_ms = 0.f;
+  size_t tile = NYM_TILE;  // items per launch (FTS_NYM_TILE overrides, for tests)
 };
 
 namespace {
@@ -723,6 +731,7 @@ int fts_idemix_ipk_create(int device, const uint8_t* ipk, size_t ipk_len, int cu
   fts_idemix_ipk* k = new fts_idemix_ipk();
   k->device = device;
   k->curve = curve_id;
+  if (const char* e = getenv("FTS_NYM_TILE")) k->tile = (size_t)std::max(64L, std::min((long)NYM_TILE, atol(e)));
   // copy(proofData[index:], ipk.Hash) into a FieldBytes window
   memset(k->hash, 0, 32);
   if (hash) memcpy(k->hash, hash, std::min<size_t>(hashl, 32));
@@ -849,7 +858,12 @@ int fts_nym_verify_batch(fts_idemix_ipk* K, size_t n, const fts_nym_item* items,
   const size_t rec_b = n * NREC * 4, nym_b = n * 64, off_b = n * 8, len_b = n * 4, st_b = n * 4;
   const size_t o_nym = rec_b, o_off = o_nym + nym_b, o_len = o_off + off_b, o_st = o_len + len_b,
                o_msg = (o_st + st_b + 255) & ~size_t(255), h_need = o_msg + mtot_w * 4;
-  const size_t vt_b = (size_t)n * 16 * 24 * 4, o_vt = (h_need + 255) & ~size_t(255), d_need = o_vt + vt_b;
+  // GLV lane tables (16 Jacobian entries, 1,536 B per lane) for one tile of NYM_TILE
+  // items: bounded at 384 MiB per slot whatever n is; a call above NYM_TILE items
+  // runs one launch per tile on the slot's stream (a 2^24-item call
+  // asked for ~38 GB here)
+  const size_t tile = std::min<size_t>(n, K->tile);
+  const size_t vt_b = tile * 16 * 24 * 4, o_vt = (h_need + 255) & ~size_t(255), d_need = o_vt + vt_b;
   if (D.h_cap < h_need) {
     if (D.h_buf) (void)hipHostFree(D.h_buf);
     D.h_buf = nullptr, D.h_cap = 0;
@@ -901,16 +915,20 @@ int fts_nym_verify_batch(fts_idemix_ipk* K, size_t n, const fts_nym_item* items,
   uint8_t* d = D.d_buf;
   ICHK(hipMemcpyAsync(d, h, h_need, hipMemcpyHostToDevice, D.stream));
   ICHK(hipEventRecord(D.ev[0], D.stream));
-  if (bn)
-    k_nym_verify<<<(unsigned)((n + 255) / 256), 256, 0, D.stream>>>(
-        (int)n, reinterpret_cast<const uint32_t*>(d), d + o_nym, reinterpret_cast<const uint32_t*>(d + o_msg),
-        reinterpret_cast<const uint64_t*>(d + o_off), reinterpret_cast<const uint32_t*>(d + o_len), K->d_tables,
-        K->d_hash, reinterpret_cast<uint32_t*>(d + o_vt), reinterpret_cast<int32_t*>(d + o_st));
-  else
-    k_nym_verify_fbn<<<(unsigned)((n + 255) / 256), 256, 0, D.stream>>>(
-        (int)n, reinterpret_cast<const uint32_t*>(d), d + o_nym, reinterpret_cast<const uint32_t*>(d + o_msg),
-        reinterpret_cast<const uint64_t*>(d + o_off), reinterpret_cast<const uint32_t*>(d + o_len), K->d_tables,
-        reinterpret_cast<uint32_t*>(d + o_vt), reinterpret_cast<int32_t*>(d + o_st));
+  for (size_t base = 0; base < n; base += tile) {
+    const unsigned grid = (unsigned)((tile + 255) / 256);
+    if (bn)
+      k_nym_verify<<<grid, 256, 0, D.stream>>>(
+          (int)n, reinterpret_cast<const uint32_t*>(d), d + o_nym, reinterpret_cast<const uint32_t*>(d + o_msg),
+          reinterpret_cast<const uint64_t*>(d + o_off), reinterpret_cast<const uint32_t*>(d + o_len), K->d_tables,
+          K->d_hash, reinterpret_cast<uint32_t*>(d + o_vt), reinterpret_cast<int32_t*>(d + o_st), (int)base,
+          (int)tile);
+    else
+      k_nym_verify_fbn<<<grid, 256, 0, D.stream>>>(
+          (int)n, reinterpret_cast<const uint32_t*>(d), d + o_nym, reinterpret_cast<const uint32_t*>(d + o_msg),
+          reinterpret_cast<const uint64_t*>(d + o_off), reinterpret_cast<const uint32_t*>(d + o_len), K->d_tables,
+          reinterpret_cast<uint32_t*>(d + o_vt), reinterpret_cast<int32_t*>(d + o_st), (int)base, (int)tile);
+  }
   ICHK(hipGetLastError());
   ICHK(hipEventRecord(D.ev[1], D.stream));
   ICHK(hipMemcpyAsync(h + o_st, d + o_st, st_b, hipMemcpyDeviceToHost, D.stream));

@@ -203,3 +203,94 @@ def test_one_bad_proof_in_coalesced_pass_group_test(pp_raw):
     for b in batches:
         b.close()
     pp.close()
+
+
+def _raw_timing_names(batch):
+    """every timeline entry name of a staged batch's last verify (duplicates kept)"""
+    import ctypes as C
+
+    from fts_gpu import _lib as L
+    names = (C.c_char_p * 128)()
+    ms = (C.c_float * 128)()
+    mads = (C.c_double * 128)()
+    m = L.lib.fts_rp_batch_timings(batch._b, names, ms, mads, 128)
+    return [names[i].decode() for i in range(m)], {names[i].decode(): mads[i] for i in range(m)}
+
+
+def test_group_test_round2_exact_verdicts(pp_raw):
+    """the group test's second round (fts_api.cpp
+    rp_group_fallback: failing round-1 groups re-grouped by 8 over the compacted
+    survivors) decides which proofs are accepted without their per-proof
+    equations.  Forced here (FTS_GT1=64, FTS_GT2_MIN=0) on a coalesced pass of 3
+    caller batches with tampered proofs in every batch: two in one round-2 group,
+    two straddling a round-1 group boundary, the pass's last proof; two tamper
+    kinds (T1 -> E1 fails, L_j -> E2 fails).  Every verdict must equal the
+    oracle's, the group test must run twice, and only round-2 groups may reach
+    the per-proof stage."""
+    import os
+    import threading
+
+    import fts_gpu
+
+    saved = {k: os.environ.get(k) for k in ("FTS_LANES", "FTS_GT1", "FTS_GT2_MIN")}
+    os.environ.update(FTS_LANES="1", FTS_GT1="64", FTS_GT2_MIN="0")
+    try:
+        pp = fts_gpu.PublicParams(pp_raw, bit_length=16, device=0)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    from oracle import pp as oppm
+    opp = oppm.load_pp(pp_raw).with_bit_length(16)
+    rng = random.Random(0x6E0C2)
+    m, nb = 384, 3
+    bad = {0: {5: "T1", 6: "L"}, 1: {63: "L", 64: "T1", 200: "L"}, 2: {383: "T1"}}
+    batches, expect = [], []
+    for t in range(nb):
+        vals = [rng.getrandbits(16) for _ in range(m)]
+        bfs = [rng.randrange(bn.R).to_bytes(32, "big") for _ in range(m)]
+        proofs, coms = pp.prove_range_batch_gpu(vals, bfs, seed=8100 + 1000 * t)
+        exp = [0] * m
+        for i, kind in bad.get(t, {}).items():
+            r = zkat.RangeProof.deserialize(proofs[i])
+            if kind == "T1":
+                r.data.T1 = bn.g1_add(r.data.T1, bn.GEN)
+            else:
+                j = rng.randrange(4)
+                r.ipa.L[j] = bn.g1_add(r.ipa.L[j], bn.GEN)
+            proofs[i] = r.serialize()
+            err = zkat.rp_verify(bn.g1_from_bytes(coms[i]), opp.ped[1:], opp.left, opp.right, opp.P, opp.Q,
+                                 opp.rounds, 16, zkat.RangeProof.deserialize(proofs[i]))
+            assert err is not None
+            exp[i] = fts_gpu.FTS_E_RP_INVALID if "IPA" not in err else fts_gpu.FTS_E_IPA_INVALID
+        batches.append(pp.stage_range_proofs(proofs, coms))
+        expect.append(exp)
+    blocker = pp.stage_range_proofs(*pp.prove_range_batch_gpu([1] * 64, [(9).to_bytes(32, "big")] * 64, seed=1))
+    out, merged, names, work = [None] * nb, [0] * nb, [None] * nb, [None] * nb
+
+    def run(t):
+        out[t] = [int(s) for s in batches[t].verify()]
+        merged[t] = batches[t].merged()
+        names[t], work[t] = _raw_timing_names(batches[t])
+
+    th = [threading.Thread(target=blocker.verify)] + [threading.Thread(target=run, args=(t,)) for t in range(nb)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    for t in range(nb):
+        assert out[t] == expect[t], (t, {i: (out[t][i], expect[t][i]) for i in range(m) if out[t][i] != expect[t][i]})
+    # find a batch whose pass held every caller batch (the usual case); the last
+    # one to finish carries that pass's timeline
+    full = [t for t in range(nb) if merged[t] == nb]
+    assert full, merged
+    nm = names[full[0]]
+    assert nm.count("fb:k_rlc_group_final") == 2, nm       # round 1 and round 2 ran
+    per_proof = work[full[0]]["fb:k_rp_terms_fixed"] / ((3 + 2 * 16) * 15 * 11 * 136)
+    nbad = sum(len(v) for v in bad.values())
+    assert 1 <= round(per_proof) <= 8 * nbad, per_proof     # round-2 groups, not round-1 groups of 64
+    for b in batches + [blocker]:
+        b.close()
+    pp.close()

@@ -195,3 +195,30 @@ def test_bad_issuer_key_rejected():
         I.IssuerKey(IPK, device=0, curve=I.FTS_CURVE_FP256BN_AMCL)
     with pytest.raises(L.FtsError):
         I.IssuerKey(IPK_FBN, device=0, curve=I.FTS_CURVE_BN254)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("curve", ["bn254", "fp256bn"])
+def test_launch_tiling_gives_same_verdicts(curve):
+    """the GLV lane tables are sized for one launch tile, not for n; a
+    call above the tile runs several launches on the slot's stream.  A key built
+    with FTS_NYM_TILE=64 (ragged last tile: 300 = 4 x 64 + 44) must return the
+    oracle's verdicts at every position."""
+    import os
+
+    from fts_gpu import idemix as I
+    old = os.environ.get("FTS_NYM_TILE")
+    os.environ["FTS_NYM_TILE"] = "64"
+    try:
+        k = I.IssuerKey(IPK if curve == "bn254" else IPK_FBN, device=0,
+                        curve=I.FTS_CURVE_BN254 if curve == "bn254" else I.FTS_CURVE_FP256BN_AMCL)
+    finally:
+        if old is None:
+            del os.environ["FTS_NYM_TILE"]
+        else:
+            os.environ["FTS_NYM_TILE"] = old
+    nyms, sigs, msgs, want = _batch(300, seed=31, curve=curve)
+    st = k.verify_batch(nyms, sigs, msgs)
+    k.close()
+    assert [I.message(int(s)) for s in st] == want
+    assert 0 < sum(w is not None for w in want) < 300
