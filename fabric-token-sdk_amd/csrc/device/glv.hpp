@@ -10,7 +10,7 @@
 // (ecc/bn254 G1 ScalarMultiplication); the values here are derived from the
 // curve (tools/glv_constants.py), not copied.
 #pragma once
-#include "g1.hpp"
+#include "fixed_base.hpp"  // madd_inl (includes g1.hpp)
 
 namespace fts {
 
@@ -288,6 +288,102 @@ FTS_DEV G1J straus2_128(const G1J& P, const uint32_t a[4], const G1J& Q, const u
     if (db != 0) {
       if (db < 0) qb.y = f_neg(qb.y);
       add_inl(acc, qb);
+    }
+  }
+  return acc;
+}
+
+// --------------------------------------------------------- affine lane tables
+// Joint Straus a*P + b*Q over AFFINE tables (the work path's com chain,
+// DESIGN.md §3.1): entries 0..7 = 1..8 * P, 8..15 = 1..8 * Q, affine
+// Montgomery, one 64-byte row (x || y, four 16-byte loads) per lane and entry,
+// entry-major: row (e, lane) at ((e * L) + lane) * 16 words, L = lanes of the
+// launch.  The build phase writes and re-reads the same entry in every lane at
+// once (fully coalesced 4 KB per wave); a window lookup reads one row per lane.
+// The multiples are built Jacobian (X, Y into the row, Z and the running
+// product of the z's beside), then normalised with ONE inversion per lane
+// (Montgomery's trick over the 16 z's), so every window addition is mixed
+// (madd-2007-bl, 7M + 4S) instead of full (11M + 5S).
+// Region layout: XY [16][L][16] | Z [16][L][8] | PRE [16][L][8]  (2 KB per lane)
+constexpr int ATAB_WORDS = 512;  // words per lane of the region
+struct ATab {
+  uint32_t* base;
+  size_t L, lane;
+  FTS_DEV uint32_t* xy(int e) const { return base + ((size_t)e * L + lane) * 16; }
+  FTS_DEV uint32_t* z(int e) const { return base + (size_t)16 * L * 16 + ((size_t)e * L + lane) * 8; }
+  FTS_DEV uint32_t* pre(int e) const { return base + (size_t)16 * L * 24 + ((size_t)e * L + lane) * 8; }
+};
+
+// entries e0 .. e0+7 <- Jacobian 1..8 * P; `pre` carries the running product of
+// the z's over all entries built so far (written to PRE).  AFF: P.z == 1 (the
+// multiples are mixed additions of P).  An identity P is stored as (0, 0, 1),
+// which normalises to the affine identity encoding (0, 0); the chain skips it.
+template <bool AFF>
+FTS_DEV void atab_build8(const ATab& T, int e0, const G1J& P, Fp& pre, bool ident) {
+  G1J cur = P;
+  G1A pa;
+  if (AFF) pa.x = P.x, pa.y = P.y;
+  if (ident) {
+    cur.x = f_zero<FpP>();
+    cur.y = f_zero<FpP>();
+    cur.z = f_one<FpP>();
+  }
+  for (int e = 0; e < 8; e++) {
+    if (!ident && e == 1) cur = g1j_dbl(P);
+    if (!ident && e > 1) {
+      if (AFF) madd_inl(cur, pa);
+      else add_inl(cur, P);
+    }
+    store_fp(T.xy(e0 + e), cur.x);
+    store_fp(T.xy(e0 + e) + 8, cur.y);
+    store_fp(T.z(e0 + e), cur.z);
+    pre = (e0 == 0 && e == 0) ? cur.z : fp_mul(pre, cur.z);
+    store_fp(T.pre(e0 + e), pre);
+  }
+}
+
+// all 16 entries -> affine: z_e^-1 = (z_0 .. z_e)^-1 * (z_0 .. z_{e-1}), one inversion
+FTS_DEV void atab_normalize(const ATab& T) {
+  Fp inv;
+  load_fp(T.pre(15), inv);
+  inv = nl_fp_inv(inv);
+  for (int e = 15; e >= 0; e--) {
+    Fp zi = inv;
+    if (e > 0) {
+      Fp pp, z;
+      load_fp(T.pre(e - 1), pp);
+      load_fp(T.z(e), z);
+      zi = fp_mul(inv, pp);
+      inv = fp_mul(inv, z);
+    }
+    Fp x, y;
+    load_fp(T.xy(e), x);
+    load_fp(T.xy(e) + 8, y);
+    const Fp zi2 = fp_sqr(zi);
+    store_fp(T.xy(e), fp_mul(x, zi2));
+    store_fp(T.xy(e) + 8, fp_mul(fp_mul(y, zi2), zi));
+  }
+}
+
+// a * P + b * Q (127-bit magnitudes, signs folded into P, Q) over a normalised
+// table: 124 doublings, <= 64 mixed additions; ida / idb: P / Q is the identity
+FTS_DEV G1J straus2_atab(const ATab& T, const uint32_t a[4], const uint32_t b[4], bool ida, bool idb) {
+  const uint32_t ca = recode_carries(a), cb = recode_carries(b);
+  G1J acc = g1j_identity();
+  for (int w = 31; w >= 0; w--) {
+    const int da = ida ? 0 : window_digit(a, ca, w), db = idb ? 0 : window_digit(b, cb, w);
+    G1A qa, qb;
+    if (da != 0) qa = load_g1a(T.xy((da < 0 ? -da : da) - 1));
+    if (db != 0) qb = load_g1a(T.xy(8 + (db < 0 ? -db : db) - 1));
+    if (w != 31)
+      for (int r = 0; r < 4; r++) acc = g1j_dbl(acc);
+    if (da != 0) {
+      if (da < 0) qa.y = f_neg(qa.y);
+      madd_inl(acc, qa);
+    }
+    if (db != 0) {
+      if (db < 0) qb.y = f_neg(qb.y);
+      madd_inl(acc, qb);
     }
   }
   return acc;

@@ -66,6 +66,12 @@ constexpr double COST_FBW_FRESH = 12.0 * COST_MADD;  // fresh, 20-bit windows
 constexpr double COST_VB4 = 7.0 + 6.0 * COST_MADD + 256.0 * COST_DBL + 60.0 * COST_ADD;  // 4-bit var-base
 constexpr double COST_VB128 = 7.0 + 6.0 * COST_ADD + 124.0 * COST_DBL + 30.0 * COST_ADD;  // GLV half (glv.hpp)
 constexpr double COST_STRAUS2 = 2.0 * (7.0 + 6.0 * COST_ADD) + 124.0 * COST_DBL + 60.0 * COST_ADD;  // glv.hpp straus2_128
+// glv.hpp straus2_atab over an affine lane table: build 1..8 P (P affine: 1 dbl + 6
+// madd) and 1..8 S (Jacobian: 1 dbl + 6 add), Montgomery-trick normalisation of the
+// 16 entries (15 + 30 + 64 products; the one inversion is not priced), 124
+// doublings and ~60 mixed additions
+constexpr double COST_STRAUS2_ATAB = (COST_DBL + 6.0 * COST_MADD) + (COST_DBL + 6.0 * COST_ADD) + 109.0 +
+                                     124.0 * COST_DBL + 60.0 * COST_MADD;
 constexpr double COST_NORM = 7.0;
      // batched affine normalisation, per point
 

@@ -9,9 +9,9 @@
 //   S   k_rp_hash_small    (proof, msg)     x, y, x_j transcripts (SHA-256 over hex)  bulletproof.go:266-281, ipa.go:230
 //   S   k_rp_chal_fr       proof            z, polEval, batch inversion of y, x_j       bulletproof.go:282-311, ipa.go:236-244
 //   S   k_rp_fixed_exact   (proof, item)    H'_i = y^-i H_i, z K, -delta P (fixed base) bulletproof.go:483-489
-//   S   k_rp_hsum_chunks   (proof, chunk)   S_c = sum_j 2^j H'_{8c+j} (Horner)
-//   S   k_rp_hsum_join     proof            S = sum_c 2^(8c) S_c (Horner)
-//   S   k_rp_com_var       2 lanes/proof    x*D + z^2*S (joint GLV/Straus)
+//   S   k_rp_hsum_chunks   (proof, chunk)   S_c = sum_j 2^j H'_{16c+j} (Horner)
+//   S   k_rp_com_var       2 lanes/proof    S = sum_c 2^(16c) S_c, then x*D + z^2*S
+//                                           (joint GLV/Straus over affine lane tables)
 //   S   k_rp_com_sum       proof            com = C + z K - delta P + x D + z^2 S       bulletproof.go:477-492
 //   S   k_rp_normalize     point (block)    batch affine normalisation of H'_i and com (one inversion per 256 points)
 //   S2  k_rp_x0_build      (proof, record)  DER(hex(H'..., G..., Q, com) "||" Zb(ip))   ipa.go:200-212
@@ -340,8 +340,10 @@ __global__ void __launch_bounds__(64) k_rp_powers(int B, int n, int k, const int
 // Terms per proof (com_terms): 0 z*K, 1 -delta*P, 2,3 the GLV halves of x*D,
 // 4,5 the GLV halves of z^2*S.
 constexpr int COM_NTERMS = 4;  // z K, -delta P, the two joint GLV halves
-constexpr int HS_CHUNK = 8;  // H' per Horner chunk of S
-constexpr int HS_SCRATCH = 8 * 24;  // scratch words per proof for the chunks (n <= 64)
+// Horner chunks of S = sum_i 2^i H'_i: 16 H' per chunk (4 chunks at n = 64);
+// k_rp_com_var joins them in both of a proof's lanes
+constexpr int HS_CHUNK = 16;
+constexpr int HS_SCRATCH = 4 * 24;  // scratch words per proof for the chunks (n <= 64)
 inline __host__ __device__ int com_nterms(int n) { return COM_NTERMS; }
 
 // lane per (proof, item): items 0..n-1: H'_i = y^-i H_i (-> hpj[b][i]);
@@ -388,7 +390,7 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, c
   store_g1j(out, r);
 }
 
-// lane per (proof, chunk c): S_c = sum_{j < 8} 2^j H'_{8c+j} (Horner over the affine H')
+// lane per (proof, chunk c): S_c = sum_{j < 16} 2^j H'_{16c+j} (Horner over the affine H')
 __global__ void __launch_bounds__(256) k_rp_hsum_chunks(int B, int n, const int32_t* __restrict__ status,
                                                        const uint32_t* __restrict__ hpa, uint32_t* __restrict__ chunks) {
   const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
@@ -407,29 +409,15 @@ __global__ void __launch_bounds__(256) k_rp_hsum_chunks(int B, int n, const int3
   store_g1j(chunks + (size_t)gid * 24, acc);
 }
 
-// lane per proof: S = sum_c 2^(8c) S_c (Horner over the chunk sums), written
-// over chunk 0 -- once per proof instead of in both GLV lanes of k_rp_com_var
-__global__ void __launch_bounds__(256) k_rp_hsum_join(int B, int n, const int32_t* __restrict__ status,
-                                                     uint32_t* __restrict__ chunks) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B || status[b] != 0) return;
-  const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
-  uint32_t* Sc = chunks + (size_t)b * nc * 24;
-  G1J S = load_g1j(Sc + (nc - 1) * 24);
-  for (int c = nc - 2; c >= 0; c--) {
-    for (int q = 0; q < HS_CHUNK; q++) S = g1j_dbl(S);
-    add_inl(S, load_g1j(Sc + c * 24));
-  }
-  store_g1j(Sc, S);
-}
-
-// x*D + z^2*S (bulletproof.go:478, 486-489 via S), two lanes per proof:
-// with x = x1 + x2 lambda and z^2 = w1 + w2 lambda (GLV), lane h computes
-// x_h phi^h(D) + w_h phi^h(S) in one joint Straus chain (glv.hpp), where
-// S = sum_c 2^(8c) S_c is assembled by Horner first -> terms[b][2 + h]
-__global__ void __launch_bounds__(256) k_rp_com_var(int B, int n, int k, const int32_t* __restrict__ status,
+// x*D + z^2*S (bulletproof.go:478, 486-489 via S), two lanes per proof: with
+// x = x1 + x2 lambda and z^2 = w1 + w2 lambda (GLV), lane h computes
+// x_h phi^h(D) + w_h phi^h(S) in one joint Straus chain over an affine lane
+// table (glv.hpp straus2_atab).  Both lanes first join S = sum_c 2^(16c) S_c
+// from k_rp_hsum_chunks' Horner chunks (3 x (16 doublings + 1 addition) at
+// n = 64; no separate one-lane-per-proof join launch) -> terms[b][2 + h]
+__global__ void __launch_bounds__(256, 3) k_rp_com_var(int B, int n, int k, const int32_t* __restrict__ status,
                                                    const uint32_t* __restrict__ pts, const uint32_t* __restrict__ ch,
-                                                   const uint32_t* __restrict__ chunks, uint32_t* __restrict__ vtab,
+                                                   const uint32_t* __restrict__ chunks, uint32_t* __restrict__ atab,
                                                    uint32_t* __restrict__ terms) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = gid >> 1, h = gid & 1;
@@ -438,12 +426,20 @@ __global__ void __launch_bounds__(256) k_rp_com_var(int B, int n, int k, const i
   Fr x, z2;
   load_f(C + CH_X * 8, x);
   load_f(C + CH_Z2 * 8, z2);
-  const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
-  G1J S = load_g1j(chunks + (size_t)b * nc * 24);  // assembled by k_rp_hsum_join
-  G1J D = g1j_from_affine(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_D) * 16));
   uint32_t xk[2][4], xs[2], wk[2][4], ws[2];
   glv_decompose(fr_canon(x).v, xk[0], xs[0], xk[1], xs[1]);
   glv_decompose(fr_canon(z2).v, wk[0], ws[0], wk[1], ws[1]);
+  // S = sum_c 2^(16c) S_c (Horner over the chunk sums)
+  const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
+  const uint32_t* Sc = chunks + (size_t)b * nc * 24;
+  G1J S = load_g1j(Sc + (nc - 1) * 24);
+  for (int c = nc - 2; c >= 0; c--) {
+    for (int q = 0; q < HS_CHUNK; q++) S = g1j_dbl(S);
+    add_inl(S, load_g1j(Sc + c * 24));
+  }
+  const G1A Da = load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_D) * 16);
+  const bool idD = g1a_is_identity(Da), idS = f_is_zero(S.z);
+  G1J D = g1j_from_affine(Da);
   if (h) {  // phi
     const Fp beta = glv_beta();
     D.x = fp_mul(D.x, beta);
@@ -451,7 +447,12 @@ __global__ void __launch_bounds__(256) k_rp_com_var(int B, int n, int k, const i
   }
   if (xs[h]) D.y = f_neg(D.y);
   if (ws[h]) S.y = f_neg(S.y);
-  G1J r = straus2_128(D, xk[h], S, wk[h], vtab, (size_t)2 * B, (size_t)gid);
+  const ATab T{atab, (size_t)2 * B, (size_t)gid};
+  Fp pre;
+  atab_build8<true>(T, 0, D, pre, idD);
+  atab_build8<false>(T, 8, S, pre, idS);
+  atab_normalize(T);
+  const G1J r = straus2_atab(T, xk[h], wk[h], idD, idS);
   store_g1j(terms + ((size_t)b * COM_NTERMS + 2 + h) * 24, r);
 }
 
@@ -1256,7 +1257,7 @@ static void launch_normalize(size_t total, int per, int stride, int first, const
 
 size_t rp_scratch_words(int B, int n, int k) {
   // per-proof fallback: 16-entry GLV lane tables of the 3 + 2k variable terms
-  return std::max((size_t)B * (3 + 2 * k) * 16 * 24, (size_t)B * (HS_SCRATCH + 2 * 16 * 24));
+  return std::max((size_t)B * (3 + 2 * k) * 16 * 24, (size_t)B * (HS_SCRATCH + 2 * ATAB_WORDS));
 }
 size_t rp_terms_words(int B, int n, int k) { return (size_t)B * rp_nterms(n, k) * 24; }
 
@@ -1376,12 +1377,10 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     const int nch = (n + HS_CHUNK - 1) / HS_CHUNK;
     FTS_LAUNCH(k_rp_hsum_chunks, B * nch, g_chain_bs, s, B, n, d.status, d.hpa, d.scratch);
     tl->mark("k_rp_hsum_chunks", s, (double)B * (n - nch) * (COST_DBL + COST_MADD));
-    FTS_LAUNCH(k_rp_hsum_join, B, g_chain_bs, s, B, n, d.status, d.scratch);
-    tl->mark("k_rp_hsum_join", s, (double)B * (nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD));
-    // scratch: [0, B*192) Horner chunks of S, then the 2B lanes' joint tables
+    // scratch: [0, B*HS_SCRATCH) Horner chunks of S, then the 2B lanes' affine tables
     FTS_LAUNCH(k_rp_com_var, 2 * B, g_chain_bs, s, B, n, k, d.status, d.pts, d.ch, d.scratch,
                d.scratch + (size_t)B * HS_SCRATCH, d.terms);
-    tl->mark("k_rp_com_var", s, (double)B * 2 * COST_STRAUS2);
+    tl->mark("k_rp_com_var", s, (double)B * 2 * ((nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD) + COST_STRAUS2_ATAB));
     FTS_LAUNCH(k_rp_com_sum, B, 64, s, B, n, k, d.status, d.pts, d.terms, d.hpj);
     tl->mark("k_rp_com_sum", s, (double)B * COM_NTERMS * COST_ADD);
   }
