@@ -203,7 +203,7 @@ struct RlcDev {
   uint32_t* key;     // [8] ChaCha20 key (fresh per call)
   uint32_t* msc;     // [B][5+2k][8] MSM scalars (canonical)
   uint32_t* coef;    // [B][RLC_NCOEF][8]
-  uint32_t* colsum;  // [rlc_ncols(n)][8]
+  uint32_t* colsum;  // [1 + 64][rlc_ncols(n)][8]: the sums, then column Q's partial sums (k_rlc_qsum)
   uint32_t* fixed;   // [rlc_ncols(n)][24]
   int32_t* flag;     // [1]
   uint32_t* msm_scratch;

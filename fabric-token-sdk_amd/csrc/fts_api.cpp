@@ -888,6 +888,14 @@ const char* fts_status_str(int32_t s) {
     case FTS_E_NYM_MALFORMED: return "error unmarshalling signature";
     case FTS_E_NYM_BADKEY: return "failed importing nym public key";
     case FTS_E_NYM_INVALID: return "pseudonym signature invalid: zero-knowledge proof is invalid";
+    case FTS_E_ID_MALFORMED: return "identity malformed";
+    case FTS_E_ID_BADNYM: return "failed to import nym public key";
+    case FTS_E_ID_NO_EIDNYM: return "no EidNym provided but ExpectEidNym required";
+    case FTS_E_ID_NO_RHNYM: return "no RhNym provided but ExpectEidNymRhNym required";
+    case FTS_E_ID_REVOCATION: return "unsupported revocation algorithm";
+    case FTS_E_ID_APRIME: return "signature invalid: APrime = 1";
+    case FTS_E_ID_PAIRING: return "signature invalid: APrime and ABar don't have the expected structure";
+    case FTS_E_ID_ZK: return "signature invalid: zero-knowledge proof is invalid";
     default: return "unknown status";
   }
 }
@@ -1028,7 +1036,7 @@ static int rp_buffers(fts_ctx* c, Lane& L, int B) {
       w.x0.ensure((size_t)B * x0_var_bytes(n)) || w.x0mid.ensure((size_t)B * 32) || w.terms.ensure(rp_terms_words(B, n, k) * 4) ||
       w.scratch.ensure(std::max(rp_scratch_words(B, n, k), (size_t)B * 10 * 24) * 4) || w.r_key.ensure(32) ||
       w.r_msc.ensure((size_t)N * 32) || w.r_coef.ensure((size_t)B * RLC_NCOEF * 32) ||
-      w.r_colsum.ensure(rlc_ncols(n) * 32) || w.r_fixed.ensure(rlc_ncols(n) * 96) || w.r_flag.ensure(4) || w.ypow.ensure((size_t)B * n * 32) ||
+      w.r_colsum.ensure(rlc_ncols(n) * 32 * (1 + 64))  /* + RQ_PARTS partial rows of column Q */ || w.r_fixed.ensure(rlc_ncols(n) * 96) || w.r_flag.ensure(4) || w.ypow.ensure((size_t)B * n * 32) ||
       w.svec.ensure((size_t)B * n * 32) || w.zvec.ensure((size_t)B * n * 32) || w.rp_excl.ensure((size_t)B * 4) ||
       !L.status_buf((size_t)B))
     return FTS_API_ENOMEM;

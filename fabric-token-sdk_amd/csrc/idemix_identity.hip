@@ -1,0 +1,1189 @@
+// Idemix identity validity on the device (idemix half):
+// the association proof every idemix owner identity carries, checked for EVERY
+// transfer input by the reference with no cache:
+//   validator/validator_transfer.go:46 GetOwnerVerifier(tok.Owner)
+//   -> core/common/deserializer.go:63-64 DeserializeVerifier
+//   -> services/identity/idemix/deserializer.go:83 Deserialize(raw, true)
+//   -> services/identity/idemix/crypto/deserializer.go:36-86 (proto, nym import)
+//   -> crypto/id.go:74-108 verifyProof -> IBM/idemix Signature.Ver
+//      (ExpectEidNymRhNym, four hidden attributes, rhIndex 3, eidIndex 2, no message).
+// Restated in oracle/idemix_identity.py (pairing pinned by the reference's
+// credential fixtures; the proof's transcript layout is unpinned).
+//
+// One identity per lane, two kernels per curve:
+//   k_idv_tvals    decode the 7 points (nym key, A', ABar, B', Nym, EidNym, RhNym)
+//                  and the epoch key, the error precedence, then the five
+//                  t-values (6 variable-base GLV products over affine lane
+//                  tables + 14 fixed-base products from the issuer's tables),
+//                  one batch normalisation, the Fiat-Shamir transcript in lane
+//                  scratch ([byte][lane]: coalesced byte stores), SHA-256 and
+//                  c == HashToZr(c' || Nonce)
+//   k_idv_pairing  e(W, A') * e(g2, -ABar) == 1 (device/pairing.hpp: precomputed
+//                  lines of W and g2, multi-Miller loop, final exponentiation)
+// Curves: BN254 (gnark; G1 64-byte raw encodings, 16-bit signed fixed-base
+// tables) and FP256BN (AMCL; 0x04 || X || Y, 16-bit unsigned tables), behind a
+// traits struct each.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <vector>
+
+#include "../../include/fts_gpu.h"
+#include "common/sha256.hpp"
+#include "device/fixed_base.hpp"
+#include "device/glv.hpp"
+#include "device/helpers.hpp"
+#include "device/transcript.hpp"
+#include "device/fp256bn.hpp"
+#include "device/pairing.hpp"
+#include "host/bn254_host.hpp"
+#include "host/pb.hpp"
+
+namespace fts {
+void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s);
+size_t table_build_scratch_bytes(int nb);
+size_t fb_words_per_base();
+void fbn_build_tables(const uint32_t* plain, int nb, uint32_t* mont, int32_t* ok, uint32_t* tables, hipStream_t s);
+size_t fbn_words_per_base();
+void host_parallel_for(size_t n, const std::function<void(size_t)>& f);
+}  // namespace fts
+
+namespace idv {
+
+using namespace fts;
+
+// ------------------------------------------------------------- constants
+// bases of the issuer tables: HSk, HRand, HAttrs[0..3], g1
+constexpr int NB = 7, B_HSK = 0, B_HRAND = 1, B_HA = 2, B_G1 = 6;
+constexpr int NPT = 7;   // raw points per item: nymPK, A', ABar, B', Nym, EidNym, RhNym
+constexpr int P_NYMPK = 0, P_AP = 1, P_ABAR = 2, P_BP = 3, P_NYM = 4, P_EID = 5, P_RH = 6;
+constexpr int NVAR = 6;  // variable-base products: A' sE, D (-c), B' sR3, Nym (-c), EidNym (-c), RhNym (-c)
+constexpr int NFIX = 14;
+constexpr int NSC = NVAR + NFIX;
+// record words: flags, c (raw LE limbs, compared), nonce (BE words, hashed), scalars
+constexpr int R_FLAGS = 0, R_C = 1, R_NONCE = 9, R_SC = 17;
+constexpr int REC_WORDS = R_SC + NSC * 8;  // 177
+constexpr int REC_STRIDE = 180;            // 16-byte aligned records
+// flags (host parse), in the reference's order of checks
+constexpr uint32_t F_EARLY_MALFORMED = 1u, F_NO_EID = 2u, F_NO_RH = 4u, F_LATE_MALFORMED = 8u, F_REVOCATION = 16u,
+                   F_C_BIG = 32u;
+// targets: t1..t5 = 0..4
+__device__ constexpr int VAR_PT[NVAR] = {P_AP, -1, P_BP, P_NYM, P_EID, P_RH};  // -1: D = ABar - B'
+__device__ constexpr int VAR_T[NVAR] = {0, 0, 1, 2, 3, 4};
+__device__ constexpr int FIX_B[NFIX] = {B_HRAND, B_HRAND, B_HSK, B_HA + 0, B_HA + 1, B_HA + 2, B_HA + 3,
+                                         B_G1,    B_HSK,   B_HRAND, B_HA + 2, B_HRAND, B_HA + 3, B_HRAND};
+__device__ constexpr int FIX_T[NFIX] = {0, 1, 1, 1, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4};
+// transcript: label || t1 t2 t3 A' ABar B' Nym EidNym t4 RhNym t5 || ipk.Hash || Disclosure (4 zero bytes)
+constexpr char LABEL[] = "signWithEidNymRhNym";
+constexpr int LABEL_LEN = 19;
+constexpr int MSG_MAX = 832;  // 13 SHA-256 blocks (FP256BN: 19 + 11 * 65 + 36 = 770 bytes)
+
+// ----------------------------------------------------------- curve traits
+// BN254 (gnark-crypto through mathlib): G1.Bytes() = 64-byte raw X || Y, 64 zero
+// bytes = identity; fixed-base tables of fixed_base.hpp (signed 16-bit windows)
+struct BnCurve {
+  using B = pair::BnField;
+  using F = Fp;
+  using PJ = G1J;
+  static constexpr int G1_BYTES = 64;
+  static FTS_DEV PJ inf() { return g1j_identity(); }
+  static FTS_DEV bool is_inf(const PJ& p) { return f_is_zero(p.z); }
+  static FTS_DEV PJ dbl(const PJ& p) { return g1j_dbl(p); }
+  static FTS_DEV void add_to(PJ& acc, const PJ& q) { add_inl(acc, q); }
+  static FTS_DEV void madd_to(PJ& acc, const F& x, const F& y) {
+    G1A q;
+    q.x = x, q.y = y;
+    madd_inl(acc, q);
+  }
+  static FTS_DEV PJ from_affine(const F& x, const F& y) {
+    PJ r;
+    r.x = x, r.y = y, r.z = f_one<FpP>();
+    return r;
+  }
+  // raw BE X || Y -> affine Montgomery; NewG1FromBytes rules (canonical, on the curve; zeros = identity)
+  static FTS_DEV bool decode(const uint8_t* raw, F& x, F& y, bool& ident) {
+    G1A a;
+    const bool ok = decode_point(raw, a);
+    ident = ok && g1a_is_identity(a);
+    x = a.x, y = a.y;
+    return ok;
+  }
+  // affine Montgomery (identity: zeros) -> G1.Bytes()
+  template <class Sink>
+  static FTS_DEV void encode(Sink& s, const F& x, const F& y) {
+    uint32_t pw[16];
+    g1_mont_to_be_words(x, y, pw);
+    for (int k = 0; k < 16; k++) s.put_word(pw[k]);
+  }
+  static FTS_DEV void fixed_mul_acc(PJ& acc, const uint32_t* tables, int base, const uint32_t* k) {
+    Scalar s;
+#pragma unroll
+    for (int q = 0; q < 8; q++) s.v[q] = k[q];
+    fb_mul_acc(acc, tables + (size_t)base * FB_WORDS_PER_BASE, s);
+  }
+  static FTS_DEV void decompose(const uint32_t k[8], uint32_t k1[4], uint32_t& s1, uint32_t k2[4], uint32_t& s2) {
+    glv_decompose<Glv>(k, k1, s1, k2, s2);
+  }
+  static FTS_DEV F beta() { return glv_beta(); }
+  // HashToZr of a digest -> canonical LE limbs
+  static FTS_DEV void digest_mod_r(const uint32_t st[8], uint32_t out[8]) {
+    const Fr r = digest_to_fr(st);
+#pragma unroll
+    for (int q = 0; q < 8; q++) out[q] = r.v[q];
+  }
+};
+
+// FP256BN (AMCL through mathlib): G1.Bytes() = 0x04 || X || Y; decoded points
+// must be canonical and on the curve (no identity encoding); fixed-base tables
+// of idemix_kernels.hip (unsigned 16-bit windows, 2^16 entries)
+constexpr int FBN_NW = 16, FBN_ND = 1 << 16;
+struct FbnCurve {
+  using B = pair::FbnField;
+  using F = fbn::Fp;
+  using PJ = fbn::PJ;
+  static constexpr int G1_BYTES = 65;
+  static FTS_DEV PJ inf() { return fbn::pj_inf(); }
+  static FTS_DEV bool is_inf(const PJ& p) { return fbn::is_zero(p.z); }
+  static FTS_DEV PJ dbl(const PJ& p) { return fbn::pj_dbl(p); }
+  static FTS_DEV void add_to(PJ& acc, const PJ& q) { acc = fbn::pj_add(acc, q); }
+  static FTS_DEV void madd_to(PJ& acc, const F& x, const F& y) { acc = fbn::pj_madd(acc, x, y); }
+  static FTS_DEV PJ from_affine(const F& x, const F& y) {
+    PJ r;
+    r.x = x, r.y = y, r.z = fbn::load<fbn::PM>(fbn::PM::ONE);
+    return r;
+  }
+  static FTS_DEV bool decode(const uint8_t* raw, F& x, F& y, bool& ident) {
+    uint32_t pw[16];
+    load_be_words(raw, pw);
+    uint32_t nx[8], ny[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) nx[k] = pw[7 - k], ny[k] = pw[15 - k];
+    ident = false;
+    if (!p256::lt256(nx, fbn::PM::M) || !p256::lt256(ny, fbn::PM::M)) return false;
+    x = p256::to_mont(fbn::load<fbn::PM>(nx));
+    y = p256::to_mont(fbn::load<fbn::PM>(ny));
+    return fbn::on_curve(x, y);
+  }
+  template <class Sink>
+  static FTS_DEV void encode(Sink& s, const F& x, const F& y) {
+    s.put_byte(0x04);
+    const F ax = p256::from_mont(x), ay = p256::from_mont(y);
+    for (int k = 7; k >= 0; k--) s.put_word(ax.v[k]);
+    for (int k = 7; k >= 0; k--) s.put_word(ay.v[k]);
+  }
+  static FTS_DEV void fixed_mul_acc(PJ& acc, const uint32_t* tables, int base, const uint32_t* k) {
+    const uint32_t* tb = tables + (size_t)base * FBN_NW * FBN_ND * 16;
+    for (int w = 0; w < FBN_NW; w++) {
+      const uint32_t d = (k[w >> 1] >> (16 * (w & 1))) & 0xffffu;
+      if (d) {
+        const uint32_t* t = tb + ((size_t)w * FBN_ND + d) * 16;
+        acc = fbn::pj_madd(acc, fbn::load<fbn::PM>(t), fbn::load<fbn::PM>(t + 8));
+      }
+    }
+  }
+  static FTS_DEV void decompose(const uint32_t k[8], uint32_t k1[4], uint32_t& s1, uint32_t k2[4], uint32_t& s2) {
+    glv_decompose<fbn::GlvK>(k, k1, s1, k2, s2);
+  }
+  static FTS_DEV F beta() { return fbn::load<fbn::PM>(fbn::GlvK::BETA); }
+  static FTS_DEV void digest_mod_r(const uint32_t st[8], uint32_t out[8]) {
+    uint32_t t[8], bw = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) out[i] = st[7 - i];
+#pragma unroll
+    for (int i = 0; i < 8; i++) t[i] = subb(out[i], fbn::RM::M[i], bw, bw);
+#pragma unroll
+    for (int i = 0; i < 8; i++) out[i] = bw ? out[i] : t[i];
+  }
+};
+
+// ------------------------------------------------------------ lane scratch
+// [unit][lane] layouts: neighbouring lanes touch neighbouring addresses
+struct LaneWords {
+  uint32_t* base;
+  size_t L, lane;
+  FTS_DEV uint32_t& at(size_t w) const { return base[w * L + lane]; }
+};
+// transcript bytes, [byte][lane]
+struct ByteSink {
+  uint8_t* base;
+  size_t L, lane;
+  uint32_t off = 0;
+  FTS_DEV void put_byte(uint32_t b) { base[(size_t)(off++) * L + lane] = (uint8_t)b; }
+  FTS_DEV void put_word(uint32_t w) {  // big-endian
+    put_byte(w >> 24), put_byte(w >> 16), put_byte(w >> 8), put_byte(w);
+  }
+  FTS_DEV uint32_t word(uint32_t j) const {
+    const uint8_t* p = base + (size_t)(4 * j) * L + lane;
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[L] << 16) | ((uint32_t)p[2 * L] << 8) | p[3 * L];
+  }
+};
+
+// affine lane table of 1..8 * P: XY [8][16] | Z [8][8] | PRE [8][8] words, [word][lane]
+constexpr int AT_WORDS = 8 * 16 + 8 * 8 + 8 * 8;
+template <class CV>
+FTS_DEV void put_f(const LaneWords& T, size_t w0, const typename CV::F& a) {
+#pragma unroll
+  for (int q = 0; q < 8; q++) T.at(w0 + q) = a.v[q];
+}
+template <class CV>
+FTS_DEV typename CV::F get_f(const LaneWords& T, size_t w0) {
+  typename CV::F a;
+#pragma unroll
+  for (int q = 0; q < 8; q++) a.v[q] = T.at(w0 + q);
+  return a;
+}
+
+// k * P (k canonical mod r, P Jacobian) by GLV: k = k1 + k2 lambda; one table of
+// 1..8 * P, normalised with one inversion; phi(mP) = (beta x, y) read from the
+// same entries; 32 signed 4-bit windows, 124 doublings, <= 64 mixed additions
+template <class CV>
+FTS_DEV typename CV::PJ glv_mul(const typename CV::PJ& P, const uint32_t k[8], const LaneWords& T) {
+  using B = typename CV::B;
+  using F = typename CV::F;
+  using PJ = typename CV::PJ;
+  uint32_t nz = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) nz |= k[q];
+  if (CV::is_inf(P) || !nz) return CV::inf();
+  // 1..8 P (Jacobian), running product of the z's
+  PJ cur = P;
+  F pre = P.z;
+  for (int e = 0; e < 8; e++) {
+    if (e == 1) cur = CV::dbl(P);
+    if (e > 1) CV::add_to(cur, P);
+    put_f<CV>(T, e * 16, cur.x);
+    put_f<CV>(T, e * 16 + 8, cur.y);
+    put_f<CV>(T, 128 + e * 8, cur.z);
+    if (e) pre = B::mul(pre, cur.z);
+    put_f<CV>(T, 192 + e * 8, pre);
+  }
+  F inv = B::inv(pre);
+  for (int e = 7; e >= 0; e--) {
+    F zi = inv;
+    if (e > 0) {
+      zi = B::mul(inv, get_f<CV>(T, 192 + (e - 1) * 8));
+      inv = B::mul(inv, get_f<CV>(T, 128 + e * 8));
+    }
+    const F zi2 = B::mul(zi, zi);
+    put_f<CV>(T, e * 16, B::mul(get_f<CV>(T, e * 16), zi2));
+    put_f<CV>(T, e * 16 + 8, B::mul(B::mul(get_f<CV>(T, e * 16 + 8), zi2), zi));
+  }
+  uint32_t k1[4], k2[4], s1, s2;
+  CV::decompose(k, k1, s1, k2, s2);
+  const uint32_t c1 = recode_carries(k1), c2 = recode_carries(k2);
+  const F beta = CV::beta();
+  PJ acc = CV::inf();
+  for (int w = 31; w >= 0; w--) {
+    const int d1 = window_digit(k1, c1, w), d2 = window_digit(k2, c2, w);
+    F x1, y1, x2, y2;
+    if (d1) {
+      const int e = (d1 < 0 ? -d1 : d1) - 1;
+      x1 = get_f<CV>(T, e * 16), y1 = get_f<CV>(T, e * 16 + 8);
+    }
+    if (d2) {
+      const int e = (d2 < 0 ? -d2 : d2) - 1;
+      x2 = get_f<CV>(T, e * 16), y2 = get_f<CV>(T, e * 16 + 8);
+    }
+    if (w != 31)
+      for (int r = 0; r < 4; r++) acc = CV::dbl(acc);
+    if (d1) {
+      if ((d1 < 0) != (s1 != 0)) y1 = B::neg(y1);
+      CV::madd_to(acc, x1, y1);
+    }
+    if (d2) {
+      if ((d2 < 0) != (s2 != 0)) y2 = B::neg(y2);
+      CV::madd_to(acc, B::mul(x2, beta), y2);
+    }
+  }
+  return acc;
+}
+
+// G2 point (affine Montgomery Fp2) on the twist y^2 = x^3 + b'
+template <class B>
+FTS_DEV bool g2_on_twist(const pair::F2<B>& x, const pair::F2<B>& y) {
+  const pair::F2<B> rhs = pair::add(pair::mul(pair::sqr(x), x), pair::f2_ld<B>(B::K::TWB[0]));
+  return pair::eq(pair::sqr(y), rhs);
+}
+// 128 raw bytes (four 32-byte big-endian coordinates in the curve's ECP2 order) ->
+// affine Montgomery; false if a coordinate is >= p or the point is off the twist.
+// BN254 (gnark raw): X.A1 X.A0 Y.A1 Y.A0; FP256BN (AMCL): xa xb ya yb
+template <class CV>
+FTS_DEV bool decode_g2(const uint8_t* raw, pair::F2<typename CV::B>& x, pair::F2<typename CV::B>& y);
+template <>
+FTS_DEV bool decode_g2<BnCurve>(const uint8_t* raw, pair::F2<pair::BnField>& x, pair::F2<pair::BnField>& y) {
+  uint32_t pw[16], qw[16];
+  load_be_words(raw, pw);
+  load_be_words(raw + 64, qw);
+  Fp c[4];
+#pragma unroll
+  for (int k = 0; k < 8; k++) c[0].v[k] = pw[7 - k], c[1].v[k] = pw[15 - k], c[2].v[k] = qw[7 - k], c[3].v[k] = qw[15 - k];
+  bool ok = true, zero = true;
+  for (int q = 0; q < 4; q++) ok = ok && limbs_lt_mod<FpP>(c[q].v), zero = zero && f_is_zero(c[q]);
+  if (!ok) return false;
+  if (zero) return true;  // the identity's raw encoding
+  x.b = f_to_mont(c[0]), x.a = f_to_mont(c[1]), y.b = f_to_mont(c[2]), y.a = f_to_mont(c[3]);
+  return g2_on_twist<pair::BnField>(x, y);
+}
+template <>
+FTS_DEV bool decode_g2<FbnCurve>(const uint8_t* raw, pair::F2<pair::FbnField>& x, pair::F2<pair::FbnField>& y) {
+  uint32_t pw[16], qw[16];
+  load_be_words(raw, pw);
+  load_be_words(raw + 64, qw);
+  uint32_t c[4][8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) c[0][k] = pw[7 - k], c[1][k] = pw[15 - k], c[2][k] = qw[7 - k], c[3][k] = qw[15 - k];
+  uint32_t any = 0;
+  for (int q = 0; q < 4; q++) {
+    if (!p256::lt256(c[q], fbn::PM::M)) return false;
+    for (int k = 0; k < 8; k++) any |= c[q][k];
+  }
+  if (!any) return true;  // all zero: the identity (as the oracle's decoding)
+  x.a = p256::to_mont(fbn::load<fbn::PM>(c[0])), x.b = p256::to_mont(fbn::load<fbn::PM>(c[1]));
+  y.a = p256::to_mont(fbn::load<fbn::PM>(c[2])), y.b = p256::to_mont(fbn::load<fbn::PM>(c[3]));
+  return g2_on_twist<pair::FbnField>(x, y);
+}
+
+// ----------------------------------------------------------------- kernels
+// lines of W (lane 0) and g2 (lane 1); wraw: W as 128 raw bytes; ok[0] <- W valid
+template <class CV>
+__global__ void __launch_bounds__(64) k_idv_lines(const uint8_t* __restrict__ wraw, uint32_t* __restrict__ lines,
+                                                  int32_t* __restrict__ ok) {
+  using B = typename CV::B;
+  using K = typename B::K;
+  const int t = threadIdx.x;
+  if (t > 1) return;
+  pair::F2<B> qx, qy;
+  if (t == 0) {
+    if (!decode_g2<CV>(wraw, qx, qy) || (pair::is_zero(qx) && pair::is_zero(qy))) {
+      ok[0] = 0;
+      return;
+    }
+    ok[0] = 1;
+  } else {
+    qx = pair::f2_ld<B>(K::GEN2[0]);
+    qy = pair::f2_ld<B>(K::GEN2[1]);
+  }
+  pair::precompute_lines<B>(qx, qy, lines + (size_t)t * pair::n_lines<K>() * pair::LINE_WORDS);
+}
+
+// one identity per lane: status (pre-set by the host for identity-level errors),
+// then decode + t-values + transcript; pin[i] <- (A', -ABar) affine Montgomery and
+// zk[i] <- 1 if c == c'' for the pairing kernel
+template <class CV>
+__global__ void __launch_bounds__(256) k_idv_tvals(int n, const uint32_t* __restrict__ rec,
+                                                   const uint8_t* __restrict__ pts, const uint8_t* __restrict__ epk,
+                                                   const uint32_t* __restrict__ tables,
+                                                   const uint32_t* __restrict__ ipk_hash,  // 8 BE words
+                                                   uint32_t* __restrict__ scratch, uint8_t* __restrict__ msg,
+                                                   uint32_t* __restrict__ pin, int32_t* __restrict__ zk,
+                                                   int32_t* __restrict__ status) {
+  using B = typename CV::B;
+  using F = typename CV::F;
+  using PJ = typename CV::PJ;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || status[i] != FTS_OK) return;
+  const uint32_t* R = rec + (size_t)i * REC_STRIDE;
+  const uint8_t* P = pts + (size_t)i * NPT * 64;
+  const uint32_t flags = R[R_FLAGS];
+  zk[i] = 0;
+  // decoded points (affine Montgomery) in lane scratch: DP [7][16] words, identity mask
+  const LaneWords DP{scratch + (size_t)(5 * 24 + AT_WORDS) * n, (size_t)n, (size_t)i};
+  uint32_t okm = 0, idm = 0;
+#pragma unroll 1
+  for (int q = 0; q < NPT; q++) {
+    F px, py;
+    bool id;
+    if (CV::decode(P + q * 64, px, py, id)) okm |= 1u << q;
+    if (id) idm |= 1u << q;
+    put_f<CV>(DP, q * 16, px);
+    put_f<CV>(DP, q * 16 + 8, py);
+  }
+  // NymPublicKey import (crypto/deserializer.go:49-56) precedes the proof
+  if (!(okm & (1u << P_NYMPK))) {
+    status[i] = FTS_E_ID_BADNYM;
+    return;
+  }
+  if (flags & F_EARLY_MALFORMED) {
+    status[i] = FTS_E_ID_MALFORMED;
+    return;
+  }
+  if (flags & F_NO_EID) {
+    status[i] = FTS_E_ID_NO_EIDNYM;
+    return;
+  }
+  if (flags & F_NO_RH) {
+    status[i] = FTS_E_ID_NO_RHNYM;
+    return;
+  }
+  bool all = okm == (1u << NPT) - 1;
+  {
+    pair::F2<B> ex, ey;
+    all = all && decode_g2<CV>(epk + (size_t)i * 128, ex, ey);
+  }
+  if (!all || (flags & F_LATE_MALFORMED)) {
+    status[i] = FTS_E_ID_MALFORMED;
+    return;
+  }
+  if (flags & F_REVOCATION) {
+    status[i] = FTS_E_ID_REVOCATION;
+    return;
+  }
+  if (idm & (1u << P_AP)) {
+    status[i] = FTS_E_ID_APRIME;
+    return;
+  }
+  // pairing inputs: A' and -ABar
+  {
+    uint32_t* pq = pin + (size_t)i * 32;
+    const F ax = get_f<CV>(DP, P_AP * 16), ay = get_f<CV>(DP, P_AP * 16 + 8);
+    const F bx = get_f<CV>(DP, P_ABAR * 16), by = get_f<CV>(DP, P_ABAR * 16 + 8);
+    const F nby = (idm & (1u << P_ABAR)) ? by : B::neg(by);
+#pragma unroll
+    for (int q = 0; q < 8; q++) pq[q] = ax.v[q], pq[8 + q] = ay.v[q], pq[16 + q] = bx.v[q], pq[24 + q] = nby.v[q];
+  }
+  // t-values: accumulators t1..t5 in lane scratch ([word][lane]), Jacobian
+  const LaneWords S{scratch, (size_t)n, (size_t)i};  // 5 x 24 accumulator words, then the GLV table
+  const LaneWords T{scratch + (size_t)5 * 24 * n, (size_t)n, (size_t)i};
+  for (int t = 0; t < 5; t++) {
+    const PJ z = CV::inf();
+    put_f<CV>(S, t * 24, z.x);
+    put_f<CV>(S, t * 24 + 8, z.y);
+    put_f<CV>(S, t * 24 + 16, z.z);
+  }
+#pragma unroll 1
+  for (int v = 0; v < NVAR; v++) {
+    PJ base;
+    const int pq_ = VAR_PT[v] < 0 ? P_ABAR : VAR_PT[v];
+    base = (idm >> pq_) & 1u ? CV::inf() : CV::from_affine(get_f<CV>(DP, pq_ * 16), get_f<CV>(DP, pq_ * 16 + 8));
+    if (VAR_PT[v] < 0 && !((idm >> P_BP) & 1u))  // D = ABar - B'
+      CV::madd_to(base, get_f<CV>(DP, P_BP * 16), B::neg(get_f<CV>(DP, P_BP * 16 + 8)));
+    const PJ r = glv_mul<CV>(base, R + R_SC + v * 8, T);
+    const int t = VAR_T[v];
+    PJ acc;
+    acc.x = get_f<CV>(S, t * 24), acc.y = get_f<CV>(S, t * 24 + 8), acc.z = get_f<CV>(S, t * 24 + 16);
+    CV::add_to(acc, r);
+    put_f<CV>(S, t * 24, acc.x);
+    put_f<CV>(S, t * 24 + 8, acc.y);
+    put_f<CV>(S, t * 24 + 16, acc.z);
+  }
+#pragma unroll 1
+  for (int f = 0; f < NFIX; f++) {
+    const int t = FIX_T[f];
+    PJ acc;
+    acc.x = get_f<CV>(S, t * 24), acc.y = get_f<CV>(S, t * 24 + 8), acc.z = get_f<CV>(S, t * 24 + 16);
+    CV::fixed_mul_acc(acc, tables, FIX_B[f], R + R_SC + (NVAR + f) * 8);
+    put_f<CV>(S, t * 24, acc.x);
+    put_f<CV>(S, t * 24 + 8, acc.y);
+    put_f<CV>(S, t * 24 + 16, acc.z);
+  }
+  // the five t-values -> affine with one inversion (Montgomery's trick; identity -> (0, 0))
+  {
+    F pre = B::one();
+    for (int t = 0; t < 5; t++) {
+      put_f<CV>(T, t * 8, pre);
+      const F z = get_f<CV>(S, t * 24 + 16);
+      if (!B::is_zero(z)) pre = B::mul(pre, z);
+    }
+    F inv = B::inv(pre);
+    for (int t = 4; t >= 0; t--) {
+      const F z = get_f<CV>(S, t * 24 + 16);
+      F ax = B::zero(), ay = B::zero();
+      if (!B::is_zero(z)) {
+        const F zi = B::mul(inv, get_f<CV>(T, t * 8));
+        inv = B::mul(inv, z);
+        const F zi2 = B::mul(zi, zi);
+        ax = B::mul(get_f<CV>(S, t * 24), zi2);
+        ay = B::mul(B::mul(get_f<CV>(S, t * 24 + 8), zi2), zi);
+      }
+      put_f<CV>(S, t * 24, ax);
+      put_f<CV>(S, t * 24 + 8, ay);
+    }
+  }
+  // transcript
+  ByteSink M{msg, (size_t)n, (size_t)i};
+  for (int k = 0; k < LABEL_LEN; k++) M.put_byte((uint8_t)LABEL[k]);
+  // t1 t2 t3 A' ABar B' Nym EidNym t4 RhNym t5: tags >= 0 are t-values, < 0 points (-1 - index)
+  constexpr int ORDER[11] = {0, 1, 2, -1 - P_AP, -1 - P_ABAR, -1 - P_BP, -1 - P_NYM, -1 - P_EID, 3, -1 - P_RH, 4};
+  for (int q = 0; q < 11; q++) {
+    const int tag = ORDER[q];
+    if (tag >= 0) {
+      CV::encode(M, get_f<CV>(S, tag * 24), get_f<CV>(S, tag * 24 + 8));
+    } else {
+      const int pi = -1 - tag;
+      F zx = get_f<CV>(DP, pi * 16), zy = get_f<CV>(DP, pi * 16 + 8);
+      if ((idm >> pi) & 1u) zx = B::zero(), zy = B::zero();
+      CV::encode(M, zx, zy);
+    }
+  }
+  for (int k = 0; k < 8; k++) M.put_word(ipk_hash[k]);
+  M.put_word(0u);  // Disclosure: four hidden attributes
+  const uint32_t len = M.off;
+  // SHA-256 padding
+  const uint32_t nb = sha_blocks(len);
+  M.put_byte(0x80);
+  while (M.off < nb * 64 - 8) M.put_byte(0);
+  M.put_word(0u);
+  M.put_word(len * 8u);
+  uint32_t st[8], w[16];
+  sha256_init(st);
+  for (uint32_t b = 0; b < nb; b++) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) w[k] = M.word(16 * b + k);
+    sha256_compress(st, w);
+  }
+  uint32_t c1[8], c2[8];
+  CV::digest_mod_r(st, c1);
+  // c'' = HashToZr(Zr.Bytes(c') || Zr.Bytes(Nonce))
+#pragma unroll
+  for (int k = 0; k < 8; k++) w[k] = c1[7 - k];
+#pragma unroll
+  for (int k = 0; k < 8; k++) w[8 + k] = R[R_NONCE + k];
+  sha256_init(st);
+  sha256_compress(st, w);
+  w[0] = 0x80000000u;
+#pragma unroll
+  for (int k = 1; k < 15; k++) w[k] = 0u;
+  w[15] = 512u;
+  sha256_compress(st, w);
+  CV::digest_mod_r(st, c2);
+  uint32_t diff = (flags & F_C_BIG) ? 1u : 0u;
+#pragma unroll
+  for (int k = 0; k < 8; k++) diff |= c2[k] ^ R[R_C + k];
+  zk[i] = diff ? 0 : 1;
+}
+
+// e(W, A') * e(g2, -ABar) == 1, then the verdict (pairing before the ZK proof, as Ver checks)
+template <class CV>
+__global__ void __launch_bounds__(64) k_idv_pairing(int n, const uint32_t* __restrict__ pin,
+                                                    const uint32_t* __restrict__ lines, const int32_t* __restrict__ zk,
+                                                    int32_t* __restrict__ status) {
+  using B = typename CV::B;
+  using K = typename B::K;
+  using F = typename B::F;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || status[i] != FTS_OK) return;
+  const uint32_t* pq = pin + (size_t)i * 32;
+  const uint32_t* const L[2] = {lines, lines + (size_t)pair::n_lines<K>() * pair::LINE_WORDS};
+  const F xP[2] = {B::ld(pq), B::ld(pq + 16)};
+  const F yP[2] = {B::ld(pq + 8), B::ld(pq + 24)};
+  pair::F12<B> f;
+  if (B::is_zero(xP[1]) && B::is_zero(yP[1])) {  // ABar = O: e(g2, O) = 1
+    const uint32_t* const L1[1] = {L[0]};
+    const F x1[1] = {xP[0]}, y1[1] = {yP[0]};
+    f = pair::miller<B, 1>(L1, x1, y1);
+  } else {
+    f = pair::miller<B, 2>(L, xP, yP);
+  }
+  const bool one = pair::is_one(pair::final_exp(f));
+  status[i] = !one ? FTS_E_ID_PAIRING : (zk[i] ? FTS_OK : FTS_E_ID_ZK);
+}
+
+// debug: e(Q, P) for Q = W (which 0) or g2 (1), P affine Montgomery -> GT (12 Fp2
+// coefficients w^0..w^5 as (c0.c0, c1.c0, c0.c1, c1.c1, c0.c2, c1.c2), plain LE limbs)
+template <class CV>
+__global__ void k_idv_pairing_debug(const uint32_t* __restrict__ lines, int which, const uint32_t* __restrict__ p16,
+                                    uint32_t* __restrict__ out, int final_exp) {
+  using B = typename CV::B;
+  using K = typename B::K;
+  using F = typename B::F;
+  if (threadIdx.x) return;
+  const uint32_t* const L[1] = {lines + (size_t)which * pair::n_lines<K>() * pair::LINE_WORDS};
+  const F xP[1] = {B::ld(p16)}, yP[1] = {B::ld(p16 + 8)};
+  pair::F12<B> f = pair::miller<B, 1>(L, xP, yP);
+  if (final_exp) f = pair::final_exp(f);
+  const pair::F2<B> z[6] = {f.c0.c0, f.c1.c0, f.c0.c1, f.c1.c1, f.c0.c2, f.c1.c2};
+  for (int k = 0; k < 6; k++) {
+    pair::store_f2(out + k * 16, z[k]);
+  }
+}
+
+// ------------------------------------------------------------------- host
+const uint32_t kRbn[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
+                          0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+const uint32_t kRfbn[8] = {0xd10b500du, 0xf62d536cu, 0x1299921au, 0x0cdc65fbu,
+                           0xee71a49eu, 0x46e5f25eu, 0xfffcf0cdu, 0xffffffffu};
+
+bool ge(const uint32_t a[8], const uint32_t m[8]) {
+  for (int k = 7; k >= 0; k--)
+    if (a[k] != m[k]) return a[k] > m[k];
+  return true;
+}
+void subm(uint32_t a[8], const uint32_t m[8]) {
+  uint64_t bw = 0;
+  for (int k = 0; k < 8; k++) {
+    const uint64_t d = (uint64_t)a[k] - m[k] - bw;
+    a[k] = (uint32_t)d;
+    bw = (d >> 63) & 1;
+  }
+}
+// big-endian bytes -> LE limbs if the value fits 256 bits
+bool be_limbs(const uint8_t* b, size_t len, uint32_t out[8]) {
+  size_t st = 0;
+  while (st < len && b[st] == 0) st++;
+  memset(out, 0, 32);
+  if (len - st > 32) return false;
+  for (size_t k = st; k < len; k++) {
+    const size_t bit = (len - 1 - k) * 8;
+    out[bit / 32] |= (uint32_t)b[k] << (bit % 32);
+  }
+  return true;
+}
+// (x * 256 + byte) mod m for x < m < 2^256
+void mulacc_byte(uint32_t x[8], uint8_t byte, const uint32_t m[8]) {
+  uint32_t t[9];
+  uint64_t c = byte;
+  for (int k = 0; k < 8; k++) {
+    const uint64_t v = ((uint64_t)x[k] << 8) + c;
+    t[k] = (uint32_t)v;
+    c = v >> 32;
+  }
+  t[8] = (uint32_t)c;
+  for (int guard = 0; guard < 600; guard++) {
+    if (t[8] == 0 && !ge(t, m)) break;
+    uint64_t bw = 0;
+    for (int k = 0; k < 9; k++) {
+      const uint64_t d = (uint64_t)t[k] - (k < 8 ? m[k] : 0u) - bw;
+      t[k] = (uint32_t)d;
+      bw = (d >> 63) & 1;
+    }
+  }
+  memcpy(x, t, 32);
+}
+void mod_m(const uint8_t* b, size_t len, const uint32_t m[8], uint32_t out[8]) {
+  if (be_limbs(b, len, out)) {
+    while (ge(out, m)) subm(out, m);
+    return;
+  }
+  memset(out, 0, 32);
+  for (size_t k = 0; k < len; k++) mulacc_byte(out, b[k], m);
+}
+
+struct Span {
+  const uint8_t* p = nullptr;
+  size_t n = 0;
+  bool set = false;
+};
+// ECP{1 x, 2 y} -> 64 raw bytes; false if a coordinate is not 32 bytes or the message is malformed
+bool ecp_raw(const Span& s, uint8_t out[64]) {
+  if (!s.set) return false;
+  Pb pb{s.p, s.n};
+  Span f[3];
+  while (pb.o < pb.n) {
+    uint32_t fn, wt;
+    const uint8_t* v;
+    size_t vl;
+    uint64_t iv;
+    if (!pb.next(fn, wt, v, vl, iv)) return false;
+    if (fn == 1 || fn == 2) {
+      if (wt != 2) return false;
+      f[fn].p = v, f[fn].n = vl, f[fn].set = true;
+    }
+  }
+  if (f[1].n != 32 || f[2].n != 32) return false;
+  memcpy(out, f[1].p, 32);
+  memcpy(out + 32, f[2].p, 32);
+  return true;
+}
+bool ecp2_raw(const Span& s, uint8_t out[128]) {
+  if (!s.set) return false;
+  Pb pb{s.p, s.n};
+  Span f[5];
+  while (pb.o < pb.n) {
+    uint32_t fn, wt;
+    const uint8_t* v;
+    size_t vl;
+    uint64_t iv;
+    if (!pb.next(fn, wt, v, vl, iv)) return false;
+    if (fn >= 1 && fn <= 4) {
+      if (wt != 2) return false;
+      f[fn].p = v, f[fn].n = vl, f[fn].set = true;
+    }
+  }
+  for (int q = 1; q <= 4; q++) {
+    if (f[q].n != 32) return false;
+    memcpy(out + 32 * (q - 1), f[q].p, 32);
+  }
+  return true;
+}
+
+// SerializedIdemixIdentity + its Signature proto -> record, raw points, epoch key;
+// returns the identity-level status (FTS_OK: to the device)
+int32_t parse_identity(const uint8_t* id, size_t len, bool bn, const uint32_t* rmod, uint32_t* rec, uint8_t* pts,
+                       uint8_t* epk) {
+  memset(rec, 0, REC_STRIDE * 4);
+  memset(pts, 0, NPT * 64);
+  memset(epk, 0, 128);
+  if (!id || !len) return FTS_E_ID_MALFORMED;  // "empty identity"
+  Span nym, proof;
+  {
+    Pb pb{id, len};
+    while (pb.o < pb.n) {
+      uint32_t f, wt;
+      const uint8_t* v;
+      size_t vl;
+      uint64_t iv;
+      if (!pb.next(f, wt, v, vl, iv)) return FTS_E_ID_MALFORMED;
+      if (f >= 1 && f <= 4 && wt != 2) return FTS_E_ID_MALFORMED;
+      if (f == 1) nym.p = v, nym.n = vl, nym.set = true;
+      if (f == 4) proof.p = v, proof.n = vl, proof.set = true;
+    }
+  }
+  if (nym.n == 0) return FTS_E_ID_MALFORMED;  // "pseudonym's public key is empty"
+  // KeyImport: G1.Bytes() form; its point checks run on the device
+  if (bn ? nym.n != 64 : (nym.n != 65 || nym.p[0] != 0x04)) return FTS_E_ID_BADNYM;
+  memcpy(pts + P_NYMPK * 64, nym.p + (bn ? 0 : 1), 64);
+  uint32_t& flags = rec[R_FLAGS];
+  // Signature proto (IBM/idemix idemix.proto, restated): 1 a_prime 2 a_bar 3 b_prime (ECP),
+  // 4 c 5 s_sk 6 s_e 7 s_r2 8 s_r3 9 s_s_prime, 10 s_attrs (repeated), 11 nonce, 12 nym (ECP),
+  // 13 s_r_nym, 14 revocation_epoch_pk (ECP2), 15 revocation_pk_sig, 16 epoch, 17 non_revocation_proof,
+  // 18 eid_nym {1 nym, 2 s_eid}, 19 rh_nym {1 nym, 2 s_rh}
+  Span f[20];
+  std::vector<Span> attrs;
+  attrs.reserve(4);
+  if (proof.n == 0) {
+    flags |= F_EARLY_MALFORMED;  // an empty signature is rejected before Unmarshal
+  } else {
+    Pb pb{proof.p, proof.n};
+    while (pb.o < pb.n) {
+      uint32_t fn, wt;
+      const uint8_t* v;
+      size_t vl;
+      uint64_t iv;
+      if (!pb.next(fn, wt, v, vl, iv)) {
+        flags |= F_EARLY_MALFORMED;
+        break;
+      }
+      if (fn >= 1 && fn <= 19 && fn != 16 && wt != 2) {
+        flags |= F_EARLY_MALFORMED;
+        break;
+      }
+      if (fn == 16 && wt != 0) {
+        flags |= F_EARLY_MALFORMED;
+        break;
+      }
+      if (fn == 10) attrs.push_back(Span{v, vl, true});
+      else if (fn >= 1 && fn <= 19) f[fn] = Span{v, vl, true};
+    }
+  }
+  // Zr fields: BN254 big-endian integers of any length; FP256BN AMCL FromBytes reads
+  // exactly 32 bytes (a shorter field panics in the reference)
+  auto zr = [&](const Span& s, uint32_t out[8], bool& wide) -> bool {
+    wide = false;
+    if (bn) {
+      uint32_t raw[8];
+      if (!be_limbs(s.p, s.n, raw)) wide = true;
+      mod_m(s.p, s.n, rmod, out);
+      return true;
+    }
+    if (s.n < 32) return false;
+    be_limbs(s.p, 32, out);
+    if (ge(out, rmod)) subm(out, rmod);
+    return true;
+  };
+  uint32_t sc[24][8];
+  memset(sc, 0, sizeof sc);
+  Span eid_nym, rh_nym, s_eid, s_rh;
+  uint32_t rev_alg = 0;
+  if (!(flags & F_EARLY_MALFORMED)) {
+    // sub-messages: 17 NonRevocationProof{1 revocation_alg}, 18 / 19 {1 nym, 2 s}
+    auto sub = [&](const Span& s, Span& a, Span& b) -> bool {
+      if (!s.set) return true;
+      Pb pb{s.p, s.n};
+      while (pb.o < pb.n) {
+        uint32_t fn, wt;
+        const uint8_t* v;
+        size_t vl;
+        uint64_t iv;
+        if (!pb.next(fn, wt, v, vl, iv)) return false;
+        if ((fn == 1 || fn == 2) && wt != 2) return false;
+        if (fn == 1) a = Span{v, vl, true};
+        if (fn == 2) b = Span{v, vl, true};
+      }
+      return true;
+    };
+    bool good = sub(f[18], eid_nym, s_eid) && sub(f[19], rh_nym, s_rh);
+    if (f[17].set) {
+      Pb pb{f[17].p, f[17].n};
+      while (good && pb.o < pb.n) {
+        uint32_t fn, wt;
+        const uint8_t* v;
+        size_t vl;
+        uint64_t iv;
+        if (!pb.next(fn, wt, v, vl, iv)) good = false;
+        else if (fn == 1 && wt != 0) good = false;
+        else if (fn == 1) rev_alg = (uint32_t)iv;
+        else if (fn == 2 && wt != 2) good = false;
+      }
+    }
+    // the scalars: c(4) sSk(5) sE(6) sR2(7) sR3(8) sS'(9) nonce(11) sRNym(13) sAttrs sEid sRh
+    const int fld[8] = {4, 5, 6, 7, 8, 9, 11, 13};
+    bool wide[8] = {false};
+    for (int q = 0; q < 8 && good; q++) good = zr(f[fld[q]], sc[q], wide[q]);
+    for (size_t a = 0; a < attrs.size() && a < 4 && good; a++) {
+      bool w;
+      good = zr(attrs[a], sc[8 + a], w);
+    }
+    for (size_t a = 4; a < attrs.size() && good; a++) {
+      uint32_t tmp[8];
+      bool w;
+      good = zr(attrs[a], tmp, w);
+    }
+    if (good && f[18].set) {
+      bool w;
+      good = zr(s_eid, sc[12], w);
+    }
+    if (good && f[19].set) {
+      bool w;
+      good = zr(s_rh, sc[13], w);
+    }
+    if (!good) {
+      flags |= F_EARLY_MALFORMED;
+    } else {
+      // nonce: Zr.Bytes() of a value wider than 32 bytes panics (mathlib BigToBytes)
+      uint32_t nonce[8];
+      if (bn) {
+        if (!be_limbs(f[11].p, f[11].n, nonce)) flags |= F_EARLY_MALFORMED;
+      } else {
+        be_limbs(f[11].p, 32, nonce);
+      }
+      for (int k = 0; k < 8; k++) rec[R_NONCE + k] = nonce[7 - k];
+      // c: compared as an integer with the recomputed (reduced) challenge
+      uint32_t craw[8];
+      if (bn) {
+        if (!be_limbs(f[4].p, f[4].n, craw) || ge(craw, rmod)) flags |= F_C_BIG;
+      } else {
+        be_limbs(f[4].p, 32, craw);
+        if (ge(craw, rmod)) flags |= F_C_BIG;
+      }
+      memcpy(rec + R_C, craw, 32);
+    }
+  }
+  if (!(flags & F_EARLY_MALFORMED)) {
+    if (!f[18].set) flags |= F_NO_EID;
+    else if (!f[19].set) flags |= F_NO_RH;
+  }
+  if (!(flags & (F_EARLY_MALFORMED | F_NO_EID | F_NO_RH))) {
+    bool good = ecp_raw(f[1], pts + P_AP * 64) && ecp_raw(f[2], pts + P_ABAR * 64) &&
+                ecp_raw(f[3], pts + P_BP * 64) && ecp_raw(f[12], pts + P_NYM * 64) &&
+                ecp_raw(eid_nym, pts + P_EID * 64) && ecp_raw(rh_nym, pts + P_RH * 64) && attrs.size() == 4 &&
+                ecp2_raw(f[14], epk);
+    if (!good) flags |= F_LATE_MALFORMED;
+    if (rev_alg != 0) flags |= F_REVOCATION;
+    // scalars: var [sE, -c, sR3, -c, -c, -c]; fixed as FIX_B / FIX_T
+    uint32_t cm[8], nc[8];
+    memcpy(cm, sc[0], 32);
+    memset(nc, 0, 32);
+    {
+      uint32_t z = 0;
+      for (int k = 0; k < 8; k++) z |= cm[k];
+      if (z) {
+        uint64_t bw = 0;
+        for (int k = 0; k < 8; k++) {
+          const uint64_t d = (uint64_t)rmod[k] - cm[k] - bw;
+          nc[k] = (uint32_t)d;
+          bw = (d >> 63) & 1;
+        }
+      }
+    }
+    const uint32_t* var[NVAR] = {sc[2], nc, sc[4], nc, nc, nc};
+    // fixed: sR2, sS', sSk, sA0..3, c, sSk, sRNym, sA2, sEid, sA3, sRh
+    const uint32_t* fix[NFIX] = {sc[3], sc[5], sc[1], sc[8], sc[9], sc[10], sc[11], cm, sc[1], sc[7],
+                                 sc[10], sc[12], sc[11], sc[13]};
+    for (int v = 0; v < NVAR; v++) memcpy(rec + R_SC + v * 8, var[v], 32);
+    for (int q = 0; q < NFIX; q++) memcpy(rec + R_SC + (NVAR + q) * 8, fix[q], 32);
+  }
+  return FTS_OK;
+}
+
+#define ICHK(x)                                    \
+  do {                                             \
+    if ((x) != hipSuccess) return FTS_API_EDEVICE; \
+  } while (0)
+
+constexpr int NSLOT = 2;
+struct Slot {
+  hipStream_t stream = nullptr;
+  uint8_t* d_buf = nullptr;
+  size_t d_cap = 0;
+  uint8_t* h_buf = nullptr;
+  size_t h_cap = 0;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  float ms[2] = {0.f, 0.f};
+};
+
+}  // namespace idv
+
+struct fts_idemix_idv {
+  int device = -1;
+  int curve = 1;
+  uint32_t* d_tables = nullptr;  // HSk, HRand, HAttrs[0..3], g1
+  uint32_t* d_lines = nullptr;   // lines of W, then of g2
+  uint32_t* d_hash = nullptr;    // ipk.Hash as 8 big-endian words
+  std::mutex mu;
+  std::condition_variable cv;
+  idv::Slot slot[idv::NSLOT];
+  bool busy[idv::NSLOT] = {false, false};
+  float last_ms[2] = {0.f, 0.f};
+};
+
+namespace idv {
+void idv_free(fts_idemix_idv* k) {
+  if (!k) return;
+  if (k->device >= 0) (void)hipSetDevice(k->device);
+  for (auto& S : k->slot) {
+    if (S.stream) (void)hipStreamSynchronize(S.stream), (void)hipStreamDestroy(S.stream);
+    for (auto& e : S.ev)
+      if (e) (void)hipEventDestroy(e);
+    if (S.d_buf) (void)hipFree(S.d_buf);
+    if (S.h_buf) (void)hipHostFree(S.h_buf);
+  }
+  for (uint32_t* p : {k->d_tables, k->d_lines, k->d_hash})
+    if (p) (void)hipFree(p);
+  delete k;
+}
+int nlines(bool bn) { return bn ? pair::n_lines<pairc::Bn254>() : pair::n_lines<pairc::Fp256bn>(); }
+}  // namespace idv
+
+extern "C" {
+
+int fts_idemix_idv_create(int device, const uint8_t* ipk, size_t ipk_len, int curve_id, fts_idemix_idv** out) {
+  using namespace idv;
+  if (!out || !ipk || !ipk_len || (curve_id != FTS_CURVE_BN254 && curve_id != FTS_CURVE_FP256BN_AMCL))
+    return FTS_API_EINVAL;
+  *out = nullptr;
+  const bool bn = curve_id == FTS_CURVE_BN254;
+  // IssuerPublicKey: 2 h_sk, 3 h_rand, 4 h_attrs (repeated ECP), 5 w (ECP2), 10 hash
+  Pb pb{ipk, ipk_len};
+  Span hsk, hr, w, hash;
+  std::vector<Span> ha;
+  while (pb.o < pb.n) {
+    uint32_t f, wt;
+    const uint8_t* v;
+    size_t vl;
+    uint64_t iv;
+    if (!pb.next(f, wt, v, vl, iv)) return FTS_API_EPP;
+    if (wt != 2) continue;
+    if (f == 2) hsk = Span{v, vl, true};
+    if (f == 3) hr = Span{v, vl, true};
+    if (f == 4) ha.push_back(Span{v, vl, true});
+    if (f == 5) w = Span{v, vl, true};
+    if (f == 10) hash = Span{v, vl, true};
+  }
+  if (ha.size() != 4) return FTS_API_EPP;  // OU, Role, EnrollmentID, RevocationHandle
+  uint8_t raw[NB][64], wraw[128];
+  if (!ecp_raw(hsk, raw[B_HSK]) || !ecp_raw(hr, raw[B_HRAND]) || !ecp2_raw(w, wraw)) return FTS_API_EPP;
+  for (int a = 0; a < 4; a++)
+    if (!ecp_raw(ha[a], raw[B_HA + a])) return FTS_API_EPP;
+  memset(raw[B_G1], 0, 64);  // g1 = (1, 2) on both curves
+  raw[B_G1][31] = 1, raw[B_G1][63] = 2;
+  uint32_t bases[NB * 16];  // BN254: Montgomery (host decode); FP256BN: plain LE limbs
+  for (int b = 0; b < NB; b++) {
+    if (bn) {
+      host::G1A a;
+      if (!host::g1_from_bytes(raw[b], 64, a) || a.inf) return FTS_API_EPP;
+      memcpy(&bases[b * 16], a.x.v, 32);
+      memcpy(&bases[b * 16 + 8], a.y.v, 32);
+    } else {
+      be_limbs(raw[b], 32, &bases[b * 16]);
+      be_limbs(raw[b] + 32, 32, &bases[b * 16 + 8]);
+    }
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return FTS_API_EDEVICE;
+  fts_idemix_idv* k = new fts_idemix_idv();
+  k->device = device;
+  k->curve = curve_id;
+  auto fail = [&](int rc) {
+    idv_free(k);
+    return rc;
+  };
+  if (hipSetDevice(device) != hipSuccess) return fail(FTS_API_EDEVICE);
+  uint32_t hw[8] = {0};
+  {
+    uint8_t h[32] = {0};
+    if (hash.set) memcpy(h, hash.p, std::min<size_t>(hash.n, 32));
+    for (int q = 0; q < 8; q++)
+      hw[q] = ((uint32_t)h[4 * q] << 24) | ((uint32_t)h[4 * q + 1] << 16) | ((uint32_t)h[4 * q + 2] << 8) | h[4 * q + 3];
+  }
+  const size_t wpb = bn ? fb_words_per_base() : fbn_words_per_base();
+  const size_t nl = (size_t)nlines(bn) * pair::LINE_WORDS;
+  hipStream_t s0 = nullptr;
+  uint32_t *d_bases = nullptr, *d_scr = nullptr;
+  uint8_t* d_w = nullptr;
+  int32_t* d_ok = nullptr;
+  const size_t scr_b = bn ? table_build_scratch_bytes(NB) : (size_t)NB * 16 * 4;
+  bool ok = hipStreamCreateWithFlags(&s0, hipStreamNonBlocking) == hipSuccess &&
+            hipMalloc(&k->d_tables, (size_t)NB * wpb * 4) == hipSuccess &&
+            hipMalloc(&k->d_lines, 2 * nl * 4) == hipSuccess && hipMalloc(&k->d_hash, 32) == hipSuccess &&
+            hipMalloc(&d_bases, sizeof bases) == hipSuccess && hipMalloc(&d_scr, scr_b) == hipSuccess &&
+            hipMalloc(&d_w, 128) == hipSuccess && hipMalloc(&d_ok, 64) == hipSuccess &&
+            hipMemcpyAsync(d_bases, bases, sizeof bases, hipMemcpyHostToDevice, s0) == hipSuccess &&
+            hipMemcpyAsync(d_w, wraw, 128, hipMemcpyHostToDevice, s0) == hipSuccess &&
+            hipMemcpyAsync(k->d_hash, hw, 32, hipMemcpyHostToDevice, s0) == hipSuccess &&
+            hipMemsetAsync(d_ok, 0, 64, s0) == hipSuccess;
+  int32_t hok[NB + 1] = {0};
+  if (ok) {
+    if (bn) {
+      launch_build_tables(d_bases, NB, k->d_tables, d_scr, s0);
+      k_idv_lines<BnCurve><<<1, 64, 0, s0>>>(d_w, k->d_lines, d_ok + NB);
+    } else {
+      fbn_build_tables(d_bases, NB, d_scr, d_ok, k->d_tables, s0);
+      k_idv_lines<FbnCurve><<<1, 64, 0, s0>>>(d_w, k->d_lines, d_ok + NB);
+    }
+    ok = hipGetLastError() == hipSuccess &&
+         hipMemcpyAsync(hok, d_ok, sizeof hok, hipMemcpyDeviceToHost, s0) == hipSuccess &&
+         hipStreamSynchronize(s0) == hipSuccess;
+  }
+  if (s0) (void)hipStreamSynchronize(s0);
+  for (void* p : {(void*)d_bases, (void*)d_scr, (void*)d_w, (void*)d_ok})
+    if (p) (void)hipFree(p);
+  if (s0) (void)hipStreamDestroy(s0);
+  if (!ok) return fail(FTS_API_EDEVICE);
+  bool valid = hok[NB] == 1;  // W on the twist
+  if (!bn)
+    for (int b = 0; b < NB; b++) valid = valid && hok[b] == 1;
+  if (!valid) return fail(FTS_API_EPP);
+  for (auto& S : k->slot) {
+    ok = ok && hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) == hipSuccess;
+    for (auto& e : S.ev) ok = ok && hipEventCreate(&e) == hipSuccess;
+  }
+  if (!ok) return fail(FTS_API_EDEVICE);
+  *out = k;
+  return FTS_API_OK;
+}
+
+void fts_idemix_idv_destroy(fts_idemix_idv* k) { idv::idv_free(k); }
+
+int fts_idemix_identity_verify_batch(fts_idemix_idv* K, size_t n, const uint8_t* const* ids, const size_t* id_len,
+                                     int32_t* status) {
+  using namespace idv;
+  if (!K || n > (size_t)(1u << 22) || (n && (!ids || !id_len || !status))) return FTS_API_EINVAL;
+  if (n == 0) return FTS_API_OK;
+  const bool bn = K->curve == FTS_CURVE_BN254;
+  int k = -1;
+  {
+    std::unique_lock<std::mutex> l(K->mu);
+    K->cv.wait(l, [&] {
+      for (int j = 0; j < NSLOT; j++)
+        if (!K->busy[j]) return true;
+      return false;
+    });
+    for (int j = 0; j < NSLOT && k < 0; j++)
+      if (!K->busy[j]) k = j;
+    K->busy[k] = true;
+  }
+  struct Guard {
+    fts_idemix_idv* K;
+    int k;
+    ~Guard() {
+      if (K->slot[k].stream) (void)hipStreamSynchronize(K->slot[k].stream);
+      std::lock_guard<std::mutex> l(K->mu);
+      K->last_ms[0] = K->slot[k].ms[0], K->last_ms[1] = K->slot[k].ms[1];
+      K->busy[k] = false;
+      K->cv.notify_one();
+    }
+  } guard{K, k};
+  Slot& D = K->slot[k];
+  ICHK(hipSetDevice(K->device));
+  // staged (host + device): rec | pts | epk | status; device only: zk | pin | scratch | msg
+  const size_t rec_b = n * REC_STRIDE * 4, pts_b = n * NPT * 64, epk_b = n * 128, st_b = n * 4;
+  const size_t o_pts = rec_b, o_epk = o_pts + pts_b, o_st = o_epk + epk_b;
+  const size_t h_need = (o_st + st_b + 255) & ~size_t(255);
+  const size_t o_zk = h_need, o_pin = (o_zk + n * 4 + 255) & ~size_t(255), o_scr = o_pin + n * 32 * 4;
+  const size_t scr_w = (size_t)(5 * 24 + AT_WORDS + NPT * 16) * n;
+  const size_t o_msg = (o_scr + scr_w * 4 + 255) & ~size_t(255);
+  const size_t d_need = o_msg + (size_t)MSG_MAX * n;
+  if (D.h_cap < h_need) {
+    if (D.h_buf) (void)hipHostFree(D.h_buf);
+    D.h_buf = nullptr, D.h_cap = 0;
+    if (hipHostMalloc(&D.h_buf, h_need + h_need / 2, hipHostMallocDefault) != hipSuccess) return FTS_API_ENOMEM;
+    D.h_cap = h_need + h_need / 2;
+  }
+  if (D.d_cap < d_need) {
+    if (D.d_buf) (void)hipFree(D.d_buf);
+    D.d_buf = nullptr, D.d_cap = 0;
+    if (hipMalloc(&D.d_buf, d_need + d_need / 2) != hipSuccess) return FTS_API_ENOMEM;
+    D.d_cap = d_need + d_need / 2;
+  }
+  uint8_t* h = D.h_buf;
+  const uint32_t* rmod = bn ? kRbn : kRfbn;
+  const size_t CH = 1024, nch = (n + CH - 1) / CH;
+  host_parallel_for(nch, [&](size_t c) {
+    for (size_t i = c * CH; i < std::min(n, (c + 1) * CH); i++)
+      reinterpret_cast<int32_t*>(h + o_st)[i] =
+          parse_identity(ids[i], id_len[i], bn, rmod, reinterpret_cast<uint32_t*>(h) + i * REC_STRIDE,
+                         h + o_pts + i * NPT * 64, h + o_epk + i * 128);
+  });
+  uint8_t* d = D.d_buf;
+  ICHK(hipMemcpyAsync(d, h, h_need, hipMemcpyHostToDevice, D.stream));
+  ICHK(hipEventRecord(D.ev[0], D.stream));
+  const unsigned g256 = (unsigned)((n + 255) / 256), g64 = (unsigned)((n + 63) / 64);
+  const uint32_t* rec = reinterpret_cast<const uint32_t*>(d);
+  uint32_t* scr = reinterpret_cast<uint32_t*>(d + o_scr);
+  uint32_t* pin = reinterpret_cast<uint32_t*>(d + o_pin);
+  int32_t* zk = reinterpret_cast<int32_t*>(d + o_zk);
+  int32_t* st = reinterpret_cast<int32_t*>(d + o_st);
+  const size_t nl = (size_t)nlines(bn) * pair::LINE_WORDS;
+  if (bn) {
+    k_idv_tvals<BnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, d + o_pts, d + o_epk, K->d_tables, K->d_hash, scr,
+                                                      d + o_msg, pin, zk, st);
+    ICHK(hipEventRecord(D.ev[1], D.stream));
+    k_idv_pairing<BnCurve><<<g64, 64, 0, D.stream>>>((int)n, pin, K->d_lines, zk, st);
+  } else {
+    k_idv_tvals<FbnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, d + o_pts, d + o_epk, K->d_tables, K->d_hash, scr,
+                                                       d + o_msg, pin, zk, st);
+    ICHK(hipEventRecord(D.ev[1], D.stream));
+    k_idv_pairing<FbnCurve><<<g64, 64, 0, D.stream>>>((int)n, pin, K->d_lines, zk, st);
+  }
+  (void)nl;
+  ICHK(hipGetLastError());
+  ICHK(hipEventRecord(D.ev[2], D.stream));
+  ICHK(hipMemcpyAsync(h + o_st, d + o_st, st_b, hipMemcpyDeviceToHost, D.stream));
+  ICHK(hipStreamSynchronize(D.stream));
+  memcpy(status, h + o_st, st_b);
+  ICHK(hipEventElapsedTime(&D.ms[0], D.ev[0], D.ev[1]));
+  ICHK(hipEventElapsedTime(&D.ms[1], D.ev[1], D.ev[2]));
+  return FTS_API_OK;
+}
+
+int fts_idemix_identity_last_timings(fts_idemix_idv* K, float* ms) {
+  if (!K || !ms) return FTS_API_EINVAL;
+  std::lock_guard<std::mutex> l(K->mu);
+  ms[0] = K->last_ms[0], ms[1] = K->last_ms[1];
+  return FTS_API_OK;
+}
+
+int fts_idemix_pairing_debug(fts_idemix_idv* K, int which, const uint8_t* p64, int final_exp, uint32_t* out192) {
+  using namespace idv;
+  if (!K || !p64 || !out192 || (which != 0 && which != 1)) return FTS_API_EINVAL;
+  const bool bn = K->curve == FTS_CURVE_BN254;
+  // P: 64 raw BE bytes -> affine Montgomery (host for BN254; device converts FP256BN)
+  uint32_t pm[16];
+  if (bn) {
+    host::G1A a;
+    if (!host::g1_from_bytes(p64, 64, a) || a.inf) return FTS_API_EINVAL;
+    memcpy(pm, a.x.v, 32);
+    memcpy(pm + 8, a.y.v, 32);
+  } else {
+    return FTS_API_EINVAL;  // FP256BN points go through fts_idemix_pairing_debug_mont
+  }
+  std::lock_guard<std::mutex> l(K->mu);
+  ICHK(hipSetDevice(K->device));
+  uint32_t *d_p = nullptr, *d_o = nullptr;
+  ICHK(hipMalloc(&d_p, 64));
+  ICHK(hipMalloc(&d_o, 192 * 4));
+  ICHK(hipMemcpy(d_p, pm, 64, hipMemcpyHostToDevice));
+  k_idv_pairing_debug<BnCurve><<<1, 64>>>(K->d_lines, which, d_p, d_o, final_exp);
+  ICHK(hipGetLastError());
+  ICHK(hipMemcpy(out192, d_o, 192 * 4, hipMemcpyDeviceToHost));
+  (void)hipFree(d_p);
+  (void)hipFree(d_o);
+  return FTS_API_OK;
+}
+
+}  // extern "C"

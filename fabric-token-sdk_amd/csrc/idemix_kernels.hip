@@ -43,6 +43,7 @@
 #include "device/transcript.hpp"
 #include "device/fp256bn.hpp"
 #include "host/bn254_host.hpp"
+#include "host/pb.hpp"
 
 namespace fts {
 void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s);
@@ -417,43 +418,6 @@ __global__ __launch_bounds__(256) void k_nym_verify_fbn(int n, const uint32_t* _
 const uint32_t kR[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
                         0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
 
-// minimal protobuf wire reader (Go proto.Unmarshal failure modes: truncation,
-// varint overflow, field 0, bad / group wire types, wrong type for a known field)
-struct Pb {
-  const uint8_t* p;
-  size_t n, o = 0;
-  bool varint(uint64_t& v) {
-    v = 0;
-    for (int sh = 0; sh < 64; sh += 7) {
-      if (o >= n) return false;
-      const uint8_t c = p[o++];
-      v |= (uint64_t)(c & 0x7f) << sh;
-      if (!(c & 0x80)) return true;
-    }
-    return false;
-  }
-  // next field: f, wire type, value span (bytes) / varint
-  bool next(uint32_t& f, uint32_t& wt, const uint8_t*& v, size_t& vl, uint64_t& iv) {
-    uint64_t key;
-    if (!varint(key)) return false;
-    f = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
-    if (f == 0 || (key >> 3) > 0x1fffffff) return false;
-    v = nullptr, vl = 0, iv = 0;
-    switch (wt) {
-      case 0: return varint(iv);
-      case 1: if (n - o < 8) return false; v = p + o, vl = 8, o += 8; return true;
-      case 5: if (n - o < 4) return false; v = p + o, vl = 4, o += 4; return true;
-      case 2: {
-        uint64_t l;
-        if (!varint(l) || l > n - o) return false;
-        v = p + o, vl = (size_t)l, o += (size_t)l;
-        return true;
-      }
-      default: return false;
-    }
-  }
-};
-
 // big-endian bytes -> integer (LE limbs) if it fits 256 bits
 bool be_to_limbs(const uint8_t* b, size_t len, uint32_t out[8]) {
   size_t st = 0;
@@ -606,6 +570,23 @@ __global__ void k_fbn_bases(int nb, const uint32_t* __restrict__ plain, uint32_t
   for (int k = 0; k < 8; k++) mont[b * 16 + k] = mx.v[k], mont[b * 16 + 8 + k] = my.v[k];
   ok[b] = good ? 1 : 0;
 }
+
+}  // namespace
+
+namespace fts {
+// FP256BN fixed-base tables (FBN layout: FBN_NW windows x 2^16 unsigned digits,
+// affine Montgomery) of nb bases given as plain LE-limb affine coordinates
+// (16 words each, on the device); ok[b] <- base b canonical and on the curve.
+// mont: nb * 16 words of scratch.  Used by the nym and identity-proof handles.
+void fbn_build_tables(const uint32_t* plain, int nb, uint32_t* mont, int32_t* ok, uint32_t* tables, hipStream_t s) {
+  k_fbn_bases<<<1, 64, 0, s>>>(nb, plain, mont, ok);
+  const size_t ent = (size_t)nb * FBN_NW * FBN_ND;
+  k_fbn_table<<<(unsigned)((ent + 255) / 256), 256, 0, s>>>(nb, mont, tables);
+}
+size_t fbn_words_per_base() { return (size_t)FBN_NW * FBN_ND * 16; }
+}  // namespace fts
+
+namespace {
 
 #define ICHK(x)                                    \
   do {                                             \

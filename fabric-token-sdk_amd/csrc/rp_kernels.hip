@@ -12,7 +12,7 @@
 //   S   k_rp_hsum_chunks   (proof, chunk)   S_c = sum_j 2^j H'_{16c+j} (Horner)
 //   S   k_rp_com_var       2 lanes/proof    S = sum_c 2^(16c) S_c, then x*D + z^2*S
 //                                           (joint GLV/Straus over affine lane tables)
-//   S   k_rp_com_sum       proof            com = C + z K - delta P + x D + z^2 S       bulletproof.go:477-492
+//   S   (k_rp_com_var)     lane pair        com = C + z K - delta P + x D + z^2 S       bulletproof.go:477-492
 //   S   k_rp_normalize     point (block)    batch affine normalisation of H'_i and com (one inversion per 256 points)
 //   S2  k_rp_x0_build      (proof, record)  DER(hex(H'..., G..., Q, com) "||" Zb(ip))   ipa.go:200-212
 //   S2  k_rp_x0_hash       proof            x0 = HashToZr(...)                          ipa.go:213
@@ -418,7 +418,7 @@ __global__ void __launch_bounds__(256) k_rp_hsum_chunks(int B, int n, const int3
 __global__ void __launch_bounds__(256, 3) k_rp_com_var(int B, int n, int k, const int32_t* __restrict__ status,
                                                    const uint32_t* __restrict__ pts, const uint32_t* __restrict__ ch,
                                                    const uint32_t* __restrict__ chunks, uint32_t* __restrict__ atab,
-                                                   uint32_t* __restrict__ terms) {
+                                                   const uint32_t* __restrict__ terms, uint32_t* __restrict__ hpj) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = gid >> 1, h = gid & 1;
   if (b >= B || status[b] != 0) return;
@@ -452,20 +452,26 @@ __global__ void __launch_bounds__(256, 3) k_rp_com_var(int B, int n, int k, cons
   atab_build8<true>(T, 0, D, pre, idD);
   atab_build8<false>(T, 8, S, pre, idS);
   atab_normalize(T);
-  const G1J r = straus2_atab(T, xk[h], wk[h], idD, idS);
-  store_g1j(terms + ((size_t)b * COM_NTERMS + 2 + h) * 24, r);
-}
-
-// lane per proof: com = C + the 4 terms -> hpj[b][n] (Jacobian)
-__global__ void __launch_bounds__(64) k_rp_com_sum(int B, int n, int k, const int32_t* __restrict__ status,
-                                                   const uint32_t* __restrict__ pts, const uint32_t* __restrict__ terms,
-                                                   uint32_t* __restrict__ hpj) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B || status[b] != 0) return;
-  const uint32_t* T = terms + (size_t)b * COM_NTERMS * 24;
-  G1J acc = g1j_from_affine(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_C) * 16));
-  for (int q = 0; q < COM_NTERMS; q++) add_inl(acc, load_g1j(T + q * 24));
-  store_g1j(hpj + ((size_t)b * (n + 1) + n) * 24, acc);
+  G1J r = straus2_atab(T, xk[h], wk[h], idD, idS);
+  // com = C + z K - delta P + x D + z^2 S (bulletproof.go:477-492), summed by the
+  // proof's two lanes (adjacent lanes of one wave; both exit or both run): lane h
+  // adds its fixed-base term (z K or -delta P, k_rp_fixed_exact), lane 0 also C,
+  // then lane 0 adds lane 1's partial (cross-lane shuffle) and writes com
+  add_inl(r, load_g1j(terms + ((size_t)b * COM_NTERMS + h) * 24));
+  G1J c = g1j_identity();
+  if (h == 0) c = g1j_from_affine(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_C) * 16));
+  add_inl(r, c);
+  G1J o;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    o.x.v[q] = __shfl_xor(r.x.v[q], 1);
+    o.y.v[q] = __shfl_xor(r.y.v[q], 1);
+    o.z.v[q] = __shfl_xor(r.z.v[q], 1);
+  }
+  if (h == 0) {
+    add_inl(r, o);
+    store_g1j(hpj + ((size_t)b * (n + 1) + n) * 24, r);
+  }
 }
 
 // ----------------------------------------- com, latency path (small passes)
@@ -1159,6 +1165,29 @@ __global__ void __launch_bounds__(256) k_rlc_columns(int B, int n, int k, int gs
   if (t == 0) store_f(colsum + ((size_t)grp * rlc_ncols(n) + col) * 8, f_from_mont(acc));
 }
 
+// column Q over the whole pass, second stage: sum the RQ_PARTS partial sums that
+// k_rlc_columns wrote per slice of proofs (rows 1..RQ_PARTS of colsum) into row 0.
+// (One block over all B proofs took 0.76 ms at 81,920 on the x0-dependent tail.)
+constexpr int RQ_PARTS = 64;
+__global__ void __launch_bounds__(64) k_rlc_qsum(int ncols, int col, uint32_t* __restrict__ colsum) {
+  __shared__ uint32_t sh[RQ_PARTS * 8];
+  const int t = threadIdx.x;
+  Fr v;  // plain residues: the sum is the same in either representation
+  load_f(colsum + ((size_t)(1 + t) * ncols + col) * 8, v);
+  store_f(sh + t * 8, v);
+  __syncthreads();
+  for (int half = RQ_PARTS / 2; half >= 1; half >>= 1) {
+    if (t < half) {
+      Fr o;
+      load_f(sh + (t + half) * 8, o);
+      v = f_add(v, o);
+      store_f(sh + t * 8, v);
+    }
+    __syncthreads();
+  }
+  if (t == 0) store_f(colsum + (size_t)col * 8, v);
+}
+
 FTS_DEV int rlc_col_base(int n, int col) {
   return col == 0 ? tb_G(n) : col == 1 ? tb_H(n) : col < 2 * n + 2 ? col - 2 : col == 2 * n + 2 ? tb_K(n)
          : col == 2 * n + 3 ? tb_P(n) : tb_Q(n);
@@ -1379,10 +1408,9 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     tl->mark("k_rp_hsum_chunks", s, (double)B * (n - nch) * (COST_DBL + COST_MADD));
     // scratch: [0, B*HS_SCRATCH) Horner chunks of S, then the 2B lanes' affine tables
     FTS_LAUNCH(k_rp_com_var, 2 * B, g_chain_bs, s, B, n, k, d.status, d.pts, d.ch, d.scratch,
-               d.scratch + (size_t)B * HS_SCRATCH, d.terms);
-    tl->mark("k_rp_com_var", s, (double)B * 2 * ((nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD) + COST_STRAUS2_ATAB));
-    FTS_LAUNCH(k_rp_com_sum, B, 64, s, B, n, k, d.status, d.pts, d.terms, d.hpj);
-    tl->mark("k_rp_com_sum", s, (double)B * COM_NTERMS * COST_ADD);
+               d.scratch + (size_t)B * HS_SCRATCH, d.terms, d.hpj);
+    tl->mark("k_rp_com_var", s,
+             (double)B * 2 * ((nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD) + COST_STRAUS2_ATAB + 2.5 * COST_ADD));
   }
   launch_normalize(B, 1, n + 1, n, d.status, d.hpj, d.hpa, d.hp_be, s);
   tl->mark("k_rp_normalize_com", s, (double)B * (2.0 * 8.0 / NORM_E + 9.0));
@@ -1397,8 +1425,12 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   // x0 tail: column Q (needs the weights of k_rlc_prep) and its product, then
   // the verdict once the MSM is in
   (void)hipStreamWaitEvent(s, d.ev_coef, 0);
-  hipLaunchKernelGGL(k_rlc_columns, dim3(1, 1), dim3(256), 0, s, B, n, k, B, NC - 1, (const int32_t*)nullptr, d.ch,
-                     r.coef, d.ypow, d.svec, d.zvec, r.colsum);
+  {
+    const int gsq = (B + RQ_PARTS - 1) / RQ_PARTS;  // proofs per partial sum
+    hipLaunchKernelGGL(k_rlc_columns, dim3(1, RQ_PARTS), dim3(256), 0, s, B, n, k, gsq, NC - 1,
+                       (const int32_t*)nullptr, d.ch, r.coef, d.ypow, d.svec, d.zvec, r.colsum + (size_t)NC * 8);
+    hipLaunchKernelGGL(k_rlc_qsum, dim3(1), dim3(RQ_PARTS), 0, s, NC, NC - 1, r.colsum);
+  }
   FTS_LAUNCH(k_rlc_fixed, FB_NW, RF_ITEMS * FB_NW, s, n, 1, NC - 1, 1, r.colsum, tables, r.fixed);
   tl->mark("k_rlc_q", s, (double)B + FB_NW * 3 + (FB_NW - 1) * COST_ADD);
   tl->fork(s3, s);

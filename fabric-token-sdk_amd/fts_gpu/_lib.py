@@ -31,6 +31,14 @@ FTS_E_SIG_INVALID = 15
 FTS_E_NYM_MALFORMED = 16
 FTS_E_NYM_BADKEY = 17
 FTS_E_NYM_INVALID = 18
+FTS_E_ID_MALFORMED = 19
+FTS_E_ID_BADNYM = 20
+FTS_E_ID_NO_EIDNYM = 21
+FTS_E_ID_NO_RHNYM = 22
+FTS_E_ID_REVOCATION = 23
+FTS_E_ID_APRIME = 24
+FTS_E_ID_PAIRING = 25
+FTS_E_ID_ZK = 26
 # mathlib CurveID of idemix issuer keys
 FTS_CURVE_FP256BN_AMCL = 0
 FTS_CURVE_BN254 = 1
@@ -52,7 +60,8 @@ EXPORTED = [
     "fts_token_metadata_decode", "fts_ecdsa_verify_batch", "fts_ecdsa_sig_parse", "fts_p256_pubkey_from_pkix",
     "fts_ecdsa_last_timings", "fts_ctx_create_devices", "fts_ctx_create_mask", "fts_ctx_devices", "fts_shard_plan",
     "fts_idemix_ipk_create", "fts_idemix_ipk_destroy", "fts_nym_verify_batch", "fts_idemix_identity_nym",
-    "fts_nym_last_timings",
+    "fts_nym_last_timings", "fts_idemix_idv_create", "fts_idemix_idv_destroy", "fts_idemix_identity_verify_batch",
+    "fts_idemix_identity_last_timings", "fts_idemix_pairing_debug",
 ]
 
 
@@ -154,6 +163,11 @@ def _load():
         "fts_nym_verify_batch": ([P, S, C.POINTER(NymItem), I32P], C.c_int),
         "fts_idemix_identity_nym": ([U8P, S, C.POINTER(C.c_void_p), C.POINTER(S)], C.c_int),
         "fts_nym_last_timings": ([P, C.POINTER(C.c_float)], C.c_int),
+        "fts_idemix_idv_create": ([C.c_int, U8P, S, C.c_int, C.POINTER(P)], C.c_int),
+        "fts_idemix_idv_destroy": ([P], None),
+        "fts_idemix_identity_verify_batch": ([P, S, C.POINTER(C.c_void_p), C.POINTER(S), I32P], C.c_int),
+        "fts_idemix_identity_last_timings": ([P, C.POINTER(C.c_float)], C.c_int),
+        "fts_idemix_pairing_debug": ([P, C.c_int, U8P, C.c_int, C.POINTER(C.c_uint32)], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

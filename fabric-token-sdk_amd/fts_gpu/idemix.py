@@ -20,6 +20,8 @@ import numpy as np
 
 from . import _lib as L
 from ._lib import FTS_OK, FTS_E_NYM_MALFORMED, FTS_E_NYM_BADKEY, FTS_E_NYM_INVALID  # noqa: F401
+from ._lib import (FTS_E_ID_MALFORMED, FTS_E_ID_BADNYM, FTS_E_ID_NO_EIDNYM, FTS_E_ID_NO_RHNYM,  # noqa: F401
+                   FTS_E_ID_REVOCATION, FTS_E_ID_APRIME, FTS_E_ID_PAIRING, FTS_E_ID_ZK)
 from ._lib import FTS_CURVE_BN254, FTS_CURVE_FP256BN_AMCL  # noqa: F401
 
 
@@ -137,3 +139,70 @@ class NymSignatureVerifier:
         st = int(self.ipk.verify_batch([self.nym], [sigma], [message_])[0])
         if st != FTS_OK:
             raise SignatureError(message(st), st)
+
+
+class IdentityVerifier:
+    """Idemix identity validity on the device (fts_idemix_identity_verify_batch):
+    the check ``Deserializer.Deserialize(raw, true)`` makes for every idemix owner
+    (services/identity/idemix/deserializer.go:82-93 -> crypto/id.go:74-108, IBM/idemix
+    Signature.Ver with ExpectEidNymRhNym).  One handle per issuer public key."""
+
+    def __init__(self, ipk, device=0, curve=FTS_CURVE_BN254):
+        self.ipk = bytes(ipk)
+        self.device = device
+        self.curve = curve
+        h = C.c_void_p()
+        L.check("fts_idemix_idv_create",
+                L.lib.fts_idemix_idv_create(int(device), self.ipk, len(self.ipk), int(curve), C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            L.lib.fts_idemix_idv_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def verify_batch(self, identities):
+        """serialized identities -> int32 status array (FTS_OK or FTS_E_ID_*)"""
+        n = len(identities)
+        st = np.zeros(n, dtype=np.int32)
+        if n == 0:
+            return st
+        keep = [bytes(x) for x in identities]
+        ptrs = (C.c_void_p * n)(*[C.cast(C.c_char_p(b), C.c_void_p).value for b in keep])
+        lens = (C.c_size_t * n)(*[len(b) for b in keep])
+        L.check("fts_idemix_identity_verify_batch",
+                L.lib.fts_idemix_identity_verify_batch(self.h, n, ptrs, lens, st.ctypes.data_as(C.POINTER(C.c_int32))))
+        return st
+
+    def Deserialize(self, identity):
+        """raises IdentityError with the reference's message, as Deserialize(raw, true) errors"""
+        st = int(self.verify_batch([identity])[0])
+        if st != FTS_OK:
+            raise IdentityError(message(st), st)
+
+    def last_kernel_ms(self):
+        """(decode + t-values + transcript, pairings) HIP-event ms of the last batch"""
+        ms = (C.c_float * 2)()
+        L.check("fts_idemix_identity_last_timings", L.lib.fts_idemix_identity_last_timings(self.h, ms))
+        return float(ms[0]), float(ms[1])
+
+    def pairing_debug(self, which, p64, final_exp=True):
+        """e(W or g2, P) (BN254 only): 6 Fp2 coefficients (w^0..w^5) as Montgomery ints"""
+        out = (C.c_uint32 * 192)()
+        L.check("fts_idemix_pairing_debug",
+                L.lib.fts_idemix_pairing_debug(self.h, int(which), bytes(p64), int(bool(final_exp)), out))
+        w = list(out)
+        val = lambda o: sum(w[o + i] << (32 * i) for i in range(8))  # noqa: E731
+        return [(val(16 * k), val(16 * k + 8)) for k in range(6)]
+
+
+class IdentityError(Exception):
+    def __init__(self, msg, status):
+        super().__init__(msg)
+        self.status = status

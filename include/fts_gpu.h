@@ -64,8 +64,18 @@ enum fts_status {
   FTS_E_SIG_INVALID = 15,   /* "signature not valid" (ecdsa.Verify false)     validator/ecdsa/ecdsa.go:107-110 */
   FTS_E_NYM_MALFORMED = 16, /* idemix nym signature empty / proto.Unmarshal failed (bccsp NymSigner.Verify) */
   FTS_E_NYM_BADKEY = 17,    /* nym public key import failed (idemix/crypto/deserializer.go:49-56) */
-  FTS_E_NYM_INVALID = 18    /* "pseudonym signature invalid: zero-knowledge proof is invalid"
+  FTS_E_NYM_INVALID = 18,   /* "pseudonym signature invalid: zero-knowledge proof is invalid"
                                (NymSignature.Ver, via idemix/crypto/id.go:151-161) */
+  /* idemix identity validity (crypto/id.go:74-108 -> IBM/idemix Signature.Ver), in the order checked: */
+  FTS_E_ID_MALFORMED = 19,  /* empty identity, SerializedIdemixIdentity / Signature proto or a point
+                               encoding does not parse (crypto/deserializer.go:37-47) */
+  FTS_E_ID_BADNYM = 20,     /* nym public key import failed (crypto/deserializer.go:49-56) */
+  FTS_E_ID_NO_EIDNYM = 21,  /* "no EidNym provided but ExpectEidNym required" */
+  FTS_E_ID_NO_RHNYM = 22,   /* "no RhNym provided but ExpectEidNymRhNym required" */
+  FTS_E_ID_REVOCATION = 23, /* revocation algorithm other than ALG_NO_REVOCATION */
+  FTS_E_ID_APRIME = 24,     /* "signature invalid: APrime = 1" */
+  FTS_E_ID_PAIRING = 25,    /* "signature invalid: APrime and ABar don't have the expected structure" */
+  FTS_E_ID_ZK = 26          /* "signature invalid: zero-knowledge proof is invalid" */
 };
 
 /* ---- API return codes ---- */
@@ -386,6 +396,30 @@ int fts_nym_verify_batch(fts_idemix_ipk* ipk, size_t n, const fts_nym_item* item
 int fts_idemix_identity_nym(const uint8_t* id, size_t len, const uint8_t** nym, size_t* nym_len);
 /* HIP-event duration (ms) of k_nym_verify in the last finished fts_nym_verify_batch on `ipk`. */
 int fts_nym_last_timings(fts_idemix_ipk* ipk, float* ms);
+
+/* ---- idemix identity validity (idemix half) ----
+ * Replaces the validity check of idemix Deserializer.Deserialize(raw, true)
+ * (services/identity/idemix/deserializer.go:82-93 -> crypto/deserializer.go:36-86 ->
+ * crypto/id.go:74-108 verifyProof -> IBM/idemix Signature.Ver with ExpectEidNymRhNym),
+ * which TransferSignatureValidate reaches for every input through
+ * GetOwnerVerifier (validator/validator_transfer.go:46, core/common/deserializer.go:63-64).
+ * One handle per issuer public key: fixed-base tables of HSk, HRand, HAttrs[0..3] and
+ * g1 (BN254: 7 x 32 MiB; FP256BN_AMCL: 7 x 64 MiB) and the Miller-loop lines of W and g2.
+ * FTS_API_EPP for a key that does not parse, lacks four attributes, or has a point off
+ * its curve. */
+typedef struct fts_idemix_idv fts_idemix_idv;
+int fts_idemix_idv_create(int device, const uint8_t* ipk, size_t ipk_len, int curve_id, fts_idemix_idv** out);
+void fts_idemix_idv_destroy(fts_idemix_idv* idv);
+/* ids[i] = a serialized idemix owner identity (SerializedIdemixIdentity proto, the token's
+ * Owner); status[i] <- FTS_OK or FTS_E_ID_* (the first failing check). */
+int fts_idemix_identity_verify_batch(fts_idemix_idv* idv, size_t n, const uint8_t* const* ids, const size_t* id_len,
+                                     int32_t* status);
+/* HIP-event durations (ms) of the last batch: [0] decode + t-values + transcript, [1] pairings. */
+int fts_idemix_identity_last_timings(fts_idemix_idv* idv, float* ms);
+/* Debug (tests): e(Q, P) for Q = W (which 0) or g2 (1) and P = 64 raw BE bytes (BN254),
+ * after the final exponentiation (final_exp != 0) or the Miller value; out192 = 6 Fp2
+ * coefficients of w^0..w^5, Montgomery, little-endian limbs. */
+int fts_idemix_pairing_debug(fts_idemix_idv* idv, int which, const uint8_t* p64, int final_exp, uint32_t* out192);
 
 #ifdef __cplusplus
 }

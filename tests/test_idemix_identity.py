@@ -1,0 +1,120 @@
+"""GPU: idemix identity validity (fts_idemix_identity_verify_batch) against the
+oracle's verdicts on identities built from the reference's own credentials
+(tests/golden/idemix_identity_golden.json, tests/golden/make_idemix_identity_golden.py),
+on both curves: golden cases (honest, tampered responses / points, missing
+EidNym / RhNym, revocation, malformed protos and keys), the device pairing
+against the oracle's GT value, wrong-issuer identities, and a 65,536-identity
+batch at exact positions."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+pytestmark = pytest.mark.gpu
+
+
+def _doc():
+    with open(os.path.join(GOLD, "idemix_identity_golden.json")) as f:
+        return json.load(f)
+
+
+def _ipk(d):
+    with open(os.path.join(GOLD, "idemix", d, "IssuerPublicKey"), "rb") as f:
+        return f.read()
+
+
+@pytest.fixture(scope="module")
+def verifiers():
+    from fts_gpu import idemix as I
+    doc = _doc()
+    vs = {tag: I.IdentityVerifier(_ipk(doc[tag]["issuer"]), device=0, curve=doc[tag]["curve_id"])
+          for tag in ("bn254", "fp256bn")}
+    yield vs
+    for v in vs.values():
+        v.close()
+
+
+@pytest.mark.parametrize("tag", ["bn254", "fp256bn"])
+def test_golden_identity_verdicts(verifiers, tag):
+    from fts_gpu import idemix as I
+    cases = _doc()[tag]["cases"]
+    st = verifiers[tag].verify_batch([bytes.fromhex(c["identity"]) for c in cases])
+    got = {c["name"]: I.message(int(s)) for c, s in zip(cases, st)}
+    want = {c["name"]: c["error"] for c in cases}
+    assert got == want
+
+
+@pytest.mark.parametrize("tag", ["bn254", "fp256bn"])
+def test_single_identity_api(verifiers, tag):
+    from fts_gpu import idemix as I
+    by = {c["name"]: c for c in _doc()[tag]["cases"]}
+    verifiers[tag].Deserialize(bytes.fromhex(by["honest_1"]["identity"]))
+    with pytest.raises(I.IdentityError, match="zero-knowledge proof is invalid"):
+        verifiers[tag].Deserialize(bytes.fromhex(by["tampered_sE"]["identity"]))
+    assert len(verifiers[tag].verify_batch([])) == 0
+
+
+def test_device_pairing_equals_oracle_gt(verifiers):
+    """e(W, P) and e(g2, P) from the device (after the final exponentiation) equal
+    the oracle's optimal ate values coefficient for coefficient (BN254)"""
+    from oracle import idemix as OI, idemix_identity as ID, pairing as PR, pairing_tower as PT
+    PC, C = PR.BN254, OI.BN254C
+    T = PT.Tower(PC)
+    W = ID.ipk_w(PC, _ipk("bn254_charlie"))
+    P = C.mul((1, 2), 123456789)
+    R = 1 << 256
+    for which, Q in ((0, W), (1, PC.g2_gen)):
+        dev = verifiers["bn254"].pairing_debug(which, C.g1_bytes(P))
+        want = T._zs(T.final_exp(T.miller([(T.lines(Q), P)])))
+        got = [((a * pow(R, -1, PC.p)) % PC.p, (b * pow(R, -1, PC.p)) % PC.p) for a, b in dev]
+        assert got == [tuple(z) for z in want], which
+        # Miller value too (before the final exponentiation): same algorithm step for step
+        devm = verifiers["bn254"].pairing_debug(which, C.g1_bytes(P), final_exp=False)
+        wantm = T._zs(T.miller([(T.lines(Q), P)]))
+        gotm = [((a * pow(R, -1, PC.p)) % PC.p, (b * pow(R, -1, PC.p)) % PC.p) for a, b in devm]
+        assert gotm == [tuple(z) for z in wantm], which
+
+
+def test_wrong_issuer_rejected():
+    """charlie's BN254 identities under the tokengen BN254 issuer key: the pairing
+    (or the transcript, which hashes ipk.Hash) fails"""
+    from fts_gpu import idemix as I
+    doc = _doc()
+    with open(os.path.join(GOLD, "idemix", "bn254_tokengen", "IssuerPublicKey"), "rb") as f:
+        other = I.IdentityVerifier(f.read(), device=0, curve=I.FTS_CURVE_BN254)
+    ids = [bytes.fromhex(c["identity"]) for c in doc["bn254"]["cases"] if c["name"].startswith("honest")]
+    st = other.verify_batch(ids)
+    other.close()
+    assert all(int(s) == I.FTS_E_ID_PAIRING for s in st)
+
+
+def test_bad_issuer_keys_rejected():
+    from fts_gpu import idemix as I
+    from fts_gpu import _lib as L
+    with pytest.raises(L.FtsError):
+        I.IdentityVerifier(_ipk("bn254_charlie")[:200], device=0, curve=I.FTS_CURVE_BN254)
+    with pytest.raises(L.FtsError):  # a BN254 key read as FP256BN: points off that curve
+        I.IdentityVerifier(_ipk("bn254_charlie"), device=0, curve=I.FTS_CURVE_FP256BN_AMCL)
+
+
+@pytest.mark.parametrize("tag", ["bn254", "fp256bn"])
+def test_large_batch_exact_positions(verifiers, tag):
+    """65,536 identities (the fixture tile of 64, 1 in 8 tampered, repeated and
+    shuffled with golden cases mixed in): every verdict at its position"""
+    from fts_gpu import idemix as I
+    doc = _doc()[tag]
+    pool = [(bytes.fromhex(t["identity"]), t["error"]) for t in doc["tile"]]
+    pool += [(bytes.fromhex(c["identity"]), c["error"]) for c in doc["cases"]]
+    rng = random.Random(7)
+    n = 65536
+    pick = [rng.randrange(len(pool)) for _ in range(n)]
+    st = verifiers[tag].verify_batch([pool[k][0] for k in pick])
+    want = np.array([pool[k][1] is None for k in pick])
+    assert ((st == 0) == want).all()
+    msgs = {k: I.message(int(s)) for k, s in zip(pick[:4096], st[:4096])}
+    assert all(msgs[k] == pool[k][1] for k in msgs)
+    t = verifiers[tag].last_kernel_ms()
+    assert t[0] > 0 and t[1] > 0
