@@ -132,12 +132,15 @@ def main():
                          "library runs under load; the PMC traffic file is keyed by this pass size)")
     ap.add_argument("--roofline-steps", type=int, default=6,
                     help="isolated steps (one batch alone on the GPU) for the per-kernel roofline")
+    ap.add_argument("--tamper", type=float, default=0.0,
+                    help="rp workload: fraction of tampered proofs per batch (SURVEY 8d: the C2 variant with 1 %% "
+                         "tampered proofs exercises the group-test fallback); verdicts are checked every step")
     ap.add_argument("--cpu-sample", type=int, default=256, help="CPU baseline chunk size (0: skip the CPU baseline)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall-time bound of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     ap.add_argument("--workload", choices=["rp", "msm", "transfer", "mixed", "request", "audit", "prove", "ecdsa",
-                                           "idemix"],
+                                           "idemix", "identity"],
                     default="rp")
     ap.add_argument("--sigs", type=int, default=65536, help="ecdsa workload: owner signatures per GPU per step")
     ap.add_argument("--msg-len", type=int, default=1024, help="ecdsa / idemix workloads: signed message bytes")
@@ -162,6 +165,8 @@ def main():
         return bench_ecdsa(args)
     if args.workload == "idemix":
         return bench_idemix(args)
+    if args.workload == "identity":
+        return bench_identity(args)
     if args.workload == "audit":
         return bench_audit(args)
     if args.workload == "prove":
@@ -201,7 +206,7 @@ def main():
     # proofs, the rest re-stage them (verification work does not depend on it)
     inflight = max(1, args.inflight)
     t0 = time.time()
-    batches, sets = [], []
+    batches, sets, wants = [], [], []
     for ln in range(inflight):
         if ln >= max(1, args.distinct):
             proofs, coms = sets[ln % len(sets)]
@@ -211,7 +216,22 @@ def main():
             bfs = [rng.randrange(R_ORDER).to_bytes(32, "big") for _ in range(B)]
             # device prover: byte-identical to the host prover (tests/test_gpu_prove.py), seconds faster
             proofs, coms = pp.prove_range_batch_gpu(vals, bfs, seed=0xF7A50002 + 1000003 * rank + 7777 * ln)
+            want = np.zeros(B, dtype=np.int32)
+            if args.tamper > 0:  # T1 (-> invalid range proof) or one L_j (-> invalid IPA), before the clock
+                from oracle import bn254 as obn, zkat
+                trng = random.Random(0x7A3 + 31 * ln + 7919 * rank)
+                for i in trng.sample(range(B), max(1, round(args.tamper * B))):
+                    r = zkat.RangeProof.deserialize(proofs[i])
+                    if trng.random() < 0.5:
+                        r.data.T1 = obn.g1_add(r.data.T1, obn.GEN)
+                        want[i] = fts_gpu.FTS_E_RP_INVALID
+                    else:
+                        j = trng.randrange(k)
+                        r.ipa.L[j] = obn.g1_add(r.ipa.L[j], obn.GEN)
+                        want[i] = fts_gpu.FTS_E_IPA_INVALID
+                    proofs[i] = r.serialize()
             sets.append((proofs, coms))
+            wants.append(want)
         batches.append(pp.stage_range_proofs(proofs, coms))
     proofs0, coms0 = sets[0]
     prove_s = time.time() - t0
@@ -220,6 +240,8 @@ def main():
         for _ in range(nsteps):
             st = batches[ln].verify(want_status=True)
             sink.append((st, batches[ln].merged()))
+            if args.tamper > 0:
+                assert (st == wants[ln % len(wants)]).all(), "verdicts differ from the tampered positions"
 
     def pipelined(nsteps, on_ready=None):
         """nsteps batch verifications spread over the in-flight slots (one host
@@ -288,22 +310,22 @@ def main():
     #     last R dispatches of a rocprofv3 trace / PMC pass are exactly these.
     R = max(1, args.roofline_steps)
 
-    def isolated(batch, reps):
+    def isolated(batch, reps, want):
         acc = {}
         t = time.perf_counter()
         for _ in range(reps):
             st = batch.verify(want_status=True)
-            assert int((st != 0).sum()) == 0
+            assert (st == want).all()
             for name, (ms, mads) in batch.timings().items():
                 o = acc.get(name, (0.0, 0.0))
                 acc[name] = (o[0] + ms, mads)
         return acc, (time.perf_counter() - t) * 1e3 / reps
 
-    kt1, iso_ms = isolated(batches[0], R)
+    kt1, iso_ms = isolated(batches[0], R, wants[0])
     m = args.pass_batches or max(1, int(os.environ.get("FTS_COALESCE_MAX", "81920")) // B)
     pass_proofs = [sets[i % len(sets)] for i in range(m)]
     big = pp.stage_range_proofs([p for ps, _ in pass_proofs for p in ps], [c for _, cs in pass_proofs for c in cs])
-    kt, pass_ms = isolated(big, R)
+    kt, pass_ms = isolated(big, R, np.concatenate([wants[i % len(wants)] for i in range(m)]))
     big.close()
     avg = {kname: v[0] / R for kname, v in kt.items()}
     avg1 = {kname: v[0] / R for kname, v in kt1.items()}
@@ -352,7 +374,7 @@ def main():
 
         def chk(lo, hi, t):
             res = cref.rp_verify_many(opp, coms0[lo:hi], proofs0[lo:hi], threads=t)
-            assert all(r == 0 for r in res), res
+            assert res == [int(w) for w in wants[0][lo:hi]], res
         d1, s1 = _timed_sample(lambda lo, hi: chk(lo, hi, 1), B, 8, args.cpu_seconds / 3)
         dn, sn = _timed_sample(lambda lo, hi: chk(lo, hi, thr), B, max(thr, args.cpu_sample), args.cpu_seconds)
         cpu = {"value": round(dn / sn, 3), "unit": "rp%d verifies/s" % n, "cores": thr, "kind": "port",
@@ -378,7 +400,8 @@ def main():
             "data": "synthetic: %d seeded %d-bit range proofs per GPU from the library's device prover "
                     "(byte-identical to its host prover)" % (B, n),
             "config": {"workload": "C2: batch of %d standalone %d-bit Bulletproof range proofs per GPU "
-                                   "(exact transcripts per proof + RLC batch check via one Pippenger MSM)" % (B, n),
+                                   "(exact transcripts per proof + RLC batch check via one Pippenger MSM)%s"
+                                   % (B, n, ", %g %% tampered" % (100 * args.tamper) if args.tamper > 0 else ""),
                        "batch_per_gpu": B, "bit_length": n, "rounds": k, "parallelism": "shard%d" % world},
             "accepted": ok,
             "verified": world * B * args.steps,
@@ -397,6 +420,8 @@ def main():
             "longest_kernel": longest_kernel,
             "cpu_baseline": cpu,
             "kernel_ms_isolated": {kname: round(v, 4) for kname, v in avg.items()},
+            "tampered": args.tamper,
+            "fallback": _fallback_share(kt, R, pass_ms),
             "prove_s": round(prove_s, 2),
         }
         print(json.dumps(out), flush=True)
@@ -1052,6 +1077,109 @@ def bench_idemix(args):
                        "msg_len": L, "parallelism": "shard%d" % world},
             "roofline": roof, "cpu_baseline": cpu, "kernel_ms": {"k_nym_verify" + ("" if bn else "_fbn"): round(ms, 4)},
             "setup_s": round(setup_s, 2)}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+# Fp products of one identity check (cost model of csrc/idemix_identity.hip, BN254 loop
+# lengths): Fp2 mul 3, Fp6 mul 18, Fp12 mul 54 / sqr 36, sparse line product 44.
+#   pairing: multi-Miller loop of 2 pairings over |6u+2| (65 bits, 37 set): 63 squarings,
+#   (64 + 36 + 2) x 2 line products; final exponentiation: easy part ~250, hard part 3
+#   exponentiations by u (62 cyclotomic squarings of 18 + 27 products each) + ~10 products,
+#   4 cyclotomic squarings, 8 Frobenius
+#   t-values: 6 GLV products (table 103 + normalisation 53 + 124 doublings of 7 + ~60 mixed
+#   additions of 11 + ~30 beta products) + 14 fixed-base products (16 mixed additions) + ~20 additions
+ID_PAIRING_MULS = 63 * 36 + (64 + 36 + 2) * 2 * 44 + 250 + 3 * (62 * 18 + 27 * 54) + 10 * 54 + 4 * 18 + 8 * 15
+ID_TVAL_MULS = 6 * (103 + 53 + 124 * 7 + 60 * 11 + 30) + 14 * 16 * 11 + 20 * 16 + 65
+
+
+def bench_identity(args):
+    """SURVEY §8f rank 4 (idemix half): identity validity of idemix owners, checked
+    for every transfer input by GetOwnerVerifier -> Deserializer.Deserialize(raw, true)
+    (validator/validator_transfer.go:46, services/identity/idemix/deserializer.go:83,
+    crypto/id.go:74-108: IBM/idemix Signature.Ver).  One step = one
+    fts_idemix_identity_verify_batch over --sigs serialized identities (host proto
+    parse, upload, decode + t-values + transcript kernel, pairing kernel, verdicts back)."""
+    world, rank, local, dist = _dist_setup()
+    import numpy as np
+    from fts_gpu import idemix as I
+    t0 = time.time()
+    tag = args.idemix_curve
+    with open(os.path.join(ROOT, "tests", "golden", "idemix_identity_golden.json")) as f:
+        doc = json.load(f)[tag]
+    with open(os.path.join(ROOT, "tests", "golden", "idemix", doc["issuer"], "IssuerPublicKey"), "rb") as f:
+        ipk_raw = f.read()
+    pool = [(bytes.fromhex(t["identity"]), t["error"]) for t in doc["tile"]]  # 64 identities, 1 in 8 tampered
+    n = args.sigs
+    order = (np.arange(n) * 7 + 13 * rank) % len(pool)
+    ids = [pool[k][0] for k in order]
+    want_ok = np.array([pool[k][1] is None for k in order])
+    V = I.IdentityVerifier(ipk_raw, device=local, curve=doc["curve_id"])
+    setup_s = time.time() - t0
+
+    def step():
+        st = V.verify_batch(ids)
+        assert ((st == 0) == want_ok).all(), "identity verdicts differ"
+        return st
+
+    class Step:
+        verify = staticmethod(step)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    if dist is not None:
+        dist.barrier()
+    inflight = max(1, args.action_inflight)
+    elapsed, _ = _run_action_steps([Step() for _ in range(inflight)], args.steps, None, None)
+    elapsed = _max_over_ranks(dist, elapsed)
+    value = world * n * args.steps / elapsed
+    reps, kt, kp = 4, 0.0, 0.0
+    for _ in range(reps):
+        step()
+        a, b = V.last_kernel_ms()
+        kt, kp = kt + a, kp + b
+    kt, kp = kt / reps, kp / reps
+    mads = n * ID_PAIRING_MULS * MAD_PER_MUL
+    ach = mads / (kp * 1e-3) / 1e12
+    roof = {"bound": "int32_valu (v_mad_u64_u32)", "kernel": "k_idv_pairing", "achieved": round(ach, 3),
+            "peak": round(PEAK_TMAD, 3), "unit": "TMAD/s", "frac": round(ach / PEAK_TMAD, 4), "traffic": None,
+            "kernel_ms": round(kp, 4), "mads_per_launch": mads, "muls_per_identity": ID_PAIRING_MULS,
+            "measured": "HIP events around each launch on the library's stream, %d isolated calls after the "
+                        "timed region (the Fp inversions are not counted as work)" % reps}
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        from oracle import idemix as O, idemix_identity as ID, pairing as PR
+        C, PC = (O.BN254C, PR.BN254) if tag == "bn254" else (O.FP256BNC, PR.FP256BN)
+        ipk = O.parse_ipk(ipk_raw, C)
+        W = ID.ipk_w(PC, ipk_raw)
+        done, t2 = 0, time.perf_counter()
+        while time.perf_counter() - t2 < min(args.cpu_seconds, 10.0) and done < n:
+            try:
+                ID.verify_identity(ipk, PC, W, ids[done])
+                ok = True
+            except ID.IdentityError:
+                ok = False
+            assert ok == want_ok[done], "CPU oracle verdict differs"
+            done += 1
+        cs = time.perf_counter() - t2
+        cpu = {"value": round(done / cs, 3), "unit": "identities/s", "cores": 1, "kind": "port",
+               "sample": "first %d identities of the batch, oracle/idemix_identity.py (pure-Python restatement of "
+                         "Signature.Ver with a direct E(Fp12) pairing), 1 thread, %.1f s wall" % (done, cs)}
+    V.close()
+    if rank == 0:
+        print(json.dumps({
+            "metric": "idemix identity validity checks/sec (Deserialize(raw, true) -> Signature.Ver, %s)" % tag,
+            "value": round(value, 1), "unit": "identities/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32 (%s Fp 8x32-bit Montgomery, Fp12 tower)" % tag,
+            "data": "the 64 oracle-made identities of tests/golden/idemix_identity_golden.json (from the reference's "
+                    "%s SignerConfig credential; 1 in 8 with a tampered response), tiled" % doc["issuer"],
+            "config": {"workload": "SURVEY 8f rank 4 (idemix identity): %d identities per GPU per step via "
+                                   "fts_idemix_identity_verify_batch, %d calls in flight" % (n, inflight),
+                       "identities_per_gpu": n, "parallelism": "shard%d" % world},
+            "roofline": roof, "cpu_baseline": cpu,
+            "kernel_ms": {"k_idv_tvals": round(kt, 4), "k_idv_pairing": round(kp, 4)},
+            "tval_mads_per_identity": ID_TVAL_MULS * MAD_PER_MUL, "setup_s": round(setup_s, 2)}), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

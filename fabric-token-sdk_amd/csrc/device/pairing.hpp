@@ -247,6 +247,38 @@ PAIR_FN F12<B> sqr(const F12<B>& x) {
   r.c1 = add(t, t);
   return r;
 }
+// Granger-Scott squaring in the cyclotomic subgroup (after the easy part of the
+// final exponentiation): Fp12 = Fp4[w]/(w^3 - s), s = w^3, s^2 = xi;
+// A = z0 + z3 s, B = z1 + z4 s, C = z2 + z5 s (z_k: coefficient of w^k);
+// f^2 = (3A^2 - 2 conj A) + (3 s C^2 + 2 conj B) w + (3B^2 - 2 conj C) w^2:
+// 9 Fp2 squarings (18 products) instead of 36 products
+template <class B>
+FTS_DEV void sq4(const F2<B>& x0, const F2<B>& x1, F2<B>& r0, F2<B>& r1) {
+  const F2<B> t0 = sqr(x0), t1 = sqr(x1);
+  r1 = sub(sub(sqr(add(x0, x1)), t0), t1);
+  r0 = add(t0, mul_xi(t1));
+}
+template <class B>
+FTS_DEV F2<B> three(const F2<B>& x) {
+  return add(add(x, x), x);
+}
+template <class B>
+PAIR_FN F12<B> cyc_sqr(const F12<B>& x) {
+  // z0 = c0.c0, z1 = c1.c0, z2 = c0.c1, z3 = c1.c1, z4 = c0.c2, z5 = c1.c2
+  F2<B> a0, a1, b0, b1, c0, c1;
+  sq4(x.c0.c0, x.c1.c1, a0, a1);
+  sq4(x.c1.c0, x.c0.c2, b0, b1);
+  sq4(x.c0.c1, x.c1.c2, c0, c1);
+  F12<B> r;
+  r.c0.c0 = sub(three(a0), dbl(x.c0.c0));          // z0'
+  r.c1.c1 = add(three(a1), dbl(x.c1.c1));          // z3'
+  r.c1.c0 = add(three(mul_xi(c1)), dbl(x.c1.c0));  // z1'
+  r.c0.c2 = sub(three(c0), dbl(x.c0.c2));          // z4'
+  r.c0.c1 = sub(three(b0), dbl(x.c0.c1));          // z2'
+  r.c1.c2 = add(three(b1), dbl(x.c1.c2));          // z5'
+  return r;
+}
+
 template <class B>
 FTS_DEV F12<B> conj(const F12<B>& x) {
   return {x.c0, neg(x.c1)};
@@ -399,7 +431,7 @@ PAIR_FN F12<B> expt(const F12<B>& f) {
   constexpr int TOP = 63 - __builtin_clzll(K::U);
   F12<B> r = f;
   for (int i = TOP - 1; i >= 0; i--) {
-    r = sqr(r);
+    r = cyc_sqr(r);
     if ((K::U >> i) & 1ull) r = mul(r, f);
   }
   return K::U_NEG ? conj(r) : r;
@@ -417,13 +449,13 @@ PAIR_FN F12<B> final_exp(const F12<B>& f0) {
   const F12<B> y4 = conj(mul(fu, frob<B, 1>(fu2)));
   const F12<B> y5 = conj(fu2);
   const F12<B> y6 = conj(mul(fu3, frob<B, 1>(fu3)));
-  F12<B> t0 = mul(mul(sqr(y6), y4), y5);
+  F12<B> t0 = mul(mul(cyc_sqr(y6), y4), y5);
   F12<B> t1 = mul(mul(y3, y5), t0);
   t0 = mul(t0, y2);
-  t1 = sqr(mul(sqr(t1), t0));
+  t1 = cyc_sqr(mul(cyc_sqr(t1), t0));
   t0 = mul(t1, y1);
   t1 = mul(t1, y0);
-  t0 = sqr(t0);
+  t0 = cyc_sqr(t0);
   return mul(t0, t1);
 }
 

@@ -40,6 +40,7 @@ size_t rp_terms_words(int B, int n, int k);
 void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s);
 void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const uint32_t* wtables,
                      const uint8_t* x0_const, const uint8_t* x0_tmpl, hipStream_t s, hipStream_t s2, hipStream_t s3,
+                     hipStream_t s4,
                      Timeline* tl);
 void launch_build_wide_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s);
 size_t wide_build_scratch_bytes(int nb);
@@ -190,6 +191,7 @@ struct Lane {
   bool alone = true;
   hipStream_t s = nullptr, s2 = nullptr;
   hipStream_t s3 = nullptr;         // sigma proofs of action batches (beside the range-proof pass)
+  hipStream_t s4 = nullptr;         // latency path: the x0 transcript prefix beside the x*D chain
   hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr;  // cross-stream ordering (no timing)
   Workspace ws;
   Timeline tl;
@@ -525,6 +527,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
       if (L->ev_b) hipEventDestroy(L->ev_b);
       if (L->ev_c) hipEventDestroy(L->ev_c);
       if (L->s2 && L->s2 != L->s) hipStreamDestroy(L->s2);
+      if (L->s4 && L->s4 != L->s) hipStreamDestroy(L->s4);
       if (L->s) hipStreamDestroy(L->s);
       L->tl.destroy();
       if (L->done) hipEventDestroy(L->done);
@@ -596,8 +599,10 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
     if (hipEventCreateWithFlags(&L->done, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)
       return fail(FTS_API_EDEVICE);
     if (hipHostMalloc((void**)&L->pin, sizeof(Lane::Pinned), 0) != hipSuccess) return fail(FTS_API_ENOMEM);
-    if (!side) L->s2 = L->s;
-    else if (hipStreamCreateWithFlags(&L->s2, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
+    if (!side) L->s2 = L->s4 = L->s;
+    else if (hipStreamCreateWithFlags(&L->s2, hipStreamNonBlocking) != hipSuccess ||
+             hipStreamCreateWithFlags(&L->s4, hipStreamNonBlocking) != hipSuccess)
+      return fail(FTS_API_EDEVICE);
     if (hipStreamCreateWithPriority(&L->s3, hipStreamNonBlocking, s3_prio) != hipSuccess ||
         hipEventCreateWithFlags(&L->ev_a, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&L->ev_b, hipEventDisableTiming) != hipSuccess ||
@@ -831,6 +836,7 @@ void fts_ctx_destroy(fts_ctx* c) {
   for (Lane* L : c->lanes) {
     if (L->s) hipStreamSynchronize(L->s);
     if (L->s2 && L->s2 != L->s) hipStreamSynchronize(L->s2);
+    if (L->s4 && L->s4 != L->s) hipStreamSynchronize(L->s4);
     if (L->s3) hipStreamSynchronize(L->s3);
     L->ws.release();
     if (L->s3) hipStreamDestroy(L->s3);
@@ -840,6 +846,7 @@ void fts_ctx_destroy(fts_ctx* c) {
     L->tl.destroy();
     if (L->done) hipEventDestroy(L->done);
     if (L->s2 && L->s2 != L->s) hipStreamDestroy(L->s2);
+    if (L->s4 && L->s4 != L->s) hipStreamDestroy(L->s4);
     if (L->s) hipStreamDestroy(L->s);
     L->free_pinned();
     delete L;
@@ -1183,7 +1190,7 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   HIP_OK(hipMemcpyAsync(r.key, L.pin->key, sizeof L.pin->key, hipMemcpyHostToDevice, L.s));
   const double t_prep = now_ms();
   L.tl.begin(L.s);
-  launch_rp_batch(d, r, c->d_tables, c->d_wtables, c->d_x0const, c->d_x0tmpl, L.s, L.s2, L.s3, &L.tl);
+  launch_rp_batch(d, r, c->d_tables, c->d_wtables, c->d_x0const, c->d_x0tmpl, L.s, L.s2, L.s3, L.s4, &L.tl);
   between();
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(&L.pin->flag, r.flag, 4, hipMemcpyDeviceToHost, L.s));

@@ -905,7 +905,7 @@ int32_t parse_identity(const uint8_t* id, size_t len, bool bn, const uint32_t* r
     if ((x) != hipSuccess) return FTS_API_EDEVICE; \
   } while (0)
 
-constexpr int NSLOT = 2;
+constexpr int NSLOT = 3;
 struct Slot {
   hipStream_t stream = nullptr;
   uint8_t* d_buf = nullptr;
@@ -927,7 +927,7 @@ struct fts_idemix_idv {
   std::mutex mu;
   std::condition_variable cv;
   idv::Slot slot[idv::NSLOT];
-  bool busy[idv::NSLOT] = {false, false};
+  bool busy[idv::NSLOT] = {false, false, false};
   float last_ms[2] = {0.f, 0.f};
 };
 

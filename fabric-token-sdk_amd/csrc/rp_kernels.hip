@@ -1333,7 +1333,7 @@ void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalar
 // (weights, x0-free columns, MSM), which needs only the challenges.
 void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const uint32_t* wtables,
                      const uint8_t* x0_const, const uint8_t* x0_tmpl, hipStream_t s, hipStream_t s2, hipStream_t s3,
-                     Timeline* tl) {
+                     hipStream_t s4, Timeline* tl) {
   const int B = d.B, n = d.n, k = d.k, NC = rlc_ncols(n);
   if (!B) return;
   if (d.excl) (void)hipMemsetAsync(d.excl, 0, (size_t)B * 4, s);
@@ -1380,6 +1380,16 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     if (d.rlc_fork) rlc_side();
     launch_normalize(nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be, s);
     tl->mark("k_rp_normalize", s, (double)nhp * (2.0 * 8.0 / NORM_E + 9.0));
+    if (d.x0_mid) {
+      // x0 prefix (H' records + shared template: all but the last 3 blocks) on s4,
+      // beside the x*D chain still running on s2: only the suffix waits for com
+      tl->fork(s, s4);
+      hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s4, B, n, d.status, d.hp_be, x0_const,
+                         d.sc, d.x0_msgs, 0);
+      tl->mark("k_rp_x0_build", s4, 0);
+      FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s4, B, n, k, d.status, d.x0_msgs, x0_tmpl, 0u, x0_cb1(n), d.x0_mid, d.ch);
+      tl->mark("k_rp_x0_prefix", s4, 0);
+    }
     tl->fork(s2, s);
     hipLaunchKernelGGL(k_rp_com_tree, dim3((B + CT_PROOFS - 1) / CT_PROOFS), dim3(CT_LANES * CT_PROOFS), 0, s, B, n,
                        k, d.status, d.pts, d.terms, d.hpj);
@@ -1414,11 +1424,11 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   }
   launch_normalize(B, 1, n + 1, n, d.status, d.hpj, d.hpa, d.hp_be, s);
   tl->mark("k_rp_normalize_com", s, (double)B * (2.0 * 8.0 / NORM_E + 9.0));
-  const bool split = !d.com_fixed && d.x0_mid;
+  const bool split = d.x0_mid != nullptr;
   hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s, B, n, d.status, d.hp_be, x0_const, d.sc,
                      d.x0_msgs, split ? 1 : 2);
   tl->mark(split ? "k_rp_x0_build_tail" : "k_rp_x0_build", s, 0);
-  if (split) tl->fork(s2, s);  // the prefix's midstate
+  if (split) tl->fork(d.com_fixed ? s4 : s2, s);  // the prefix's midstate
   FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s, B, n, k, d.status, d.x0_msgs, x0_tmpl, split ? x0_cb1(n) : 0u, 0xffffffffu,
              d.x0_mid, d.ch);
   tl->mark("k_rp_x0_hash", s, 0);

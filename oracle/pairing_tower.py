@@ -117,6 +117,29 @@ class Tower:
         c0 = self.s6(self.s6(self.m6(self.a6(a[0], a[1]), self.a6(a[0], self.mv6(a[1]))), t), self.mv6(t))
         return (c0, self.a6(t, t))
 
+    def cyc_sq12(self, a):
+        """Granger-Scott squaring in the cyclotomic subgroup: Fp12 = Fp4[w]/(w^3 - s),
+        s = w^3, s^2 = xi; A = z0 + z3 s, B = z1 + z4 s, C = z2 + z5 s;
+        f^2 = (3A^2 - 2 conj A) + (3 s C^2 + 2 conj B) w + (3B^2 - 2 conj C) w^2"""
+        z = self._zs(a)
+
+        def sq4(x0, x1):  # (x0 + x1 s)^2 = (x0^2 + xi x1^2) + 2 x0 x1 s
+            t0, t1 = self.m2(x0, x0), self.m2(x1, x1)
+            t2 = self.s2(self.s2(self.m2(self.a2(x0, x1), self.a2(x0, x1)), t0), t1)
+            return self.a2(t0, self.xi(t1)), t2
+        a0, a1 = sq4(z[0], z[3])
+        b0, b1 = sq4(z[1], z[4])
+        c0, c1 = sq4(z[2], z[5])
+        three = lambda x: self.a2(self.a2(x, x), x)  # noqa: E731
+        two = lambda x: self.a2(x, x)  # noqa: E731
+        # A' = 3A^2 - 2 conj(A): (3a0 - 2z0, 3a1 + 2z3)
+        n0, n3 = self.s2(three(a0), two(z[0])), self.a2(three(a1), two(z[3]))
+        # B' = 3 s C^2 + 2 conj(B): s (c0 + c1 s) = xi c1 + c0 s
+        n1, n4 = self.a2(three(self.xi(c1)), two(z[1])), self.s2(three(c0), two(z[4]))
+        # C' = 3B^2 - 2 conj(C)
+        n2, n5 = self.s2(three(b0), two(z[2])), self.a2(three(b1), two(z[5]))
+        return self._from_zs([n0, n1, n2, n3, n4, n5])
+
     def cj12(self, a):
         return (a[0], self.n6(a[1]))
 
@@ -219,7 +242,7 @@ class Tower:
         """f^u (cyclotomic subgroup: inverse = conjugate)"""
         r = f
         for b in bin(abs(self.k["u"]))[3:]:
-            r = self.sq12(r)
+            r = self.cyc_sq12(r)
             if b == "1":
                 r = self.m12(r, f)
         return self.cj12(r) if self.k["u"] < 0 else r
@@ -237,14 +260,14 @@ class Tower:
         y4 = self.cj12(self.m12(fu, self.frob(fu2, 1)))
         y5 = self.cj12(fu2)
         y6 = self.cj12(self.m12(fu3, self.frob(fu3, 1)))
-        t0 = self.m12(self.m12(self.sq12(y6), y4), y5)
+        t0 = self.m12(self.m12(self.cyc_sq12(y6), y4), y5)
         t1 = self.m12(self.m12(y3, y5), t0)
         t0 = self.m12(t0, y2)
-        t1 = self.m12(self.sq12(t1), t0)
-        t1 = self.sq12(t1)
+        t1 = self.m12(self.cyc_sq12(t1), t0)
+        t1 = self.cyc_sq12(t1)
         t0 = self.m12(t1, y1)
         t1 = self.m12(t1, y0)
-        t0 = self.sq12(t0)
+        t0 = self.cyc_sq12(t0)
         return self.m12(t0, t1)
 
     # ------------------------------------------------------- helpers

@@ -78,3 +78,29 @@ def test_msm_2p16_linear_identity(gpu_pp):
     assert got == bn.g1_bytes(expect)
     assert st.run() == got  # idempotent re-run on the staged inputs
     st.close()
+
+
+def test_msm_2p20_linearity_and_identity(gpu_pp):
+    """BASELINE config C3 at the top of its range used by the tests (2^20 points):
+    MSM(P, a) + MSM(P, b) == MSM(P, a + b mod r) (linearity, three device MSMs),
+    the closed form sum k_i (i mod 2^16 + 1) G for P_i = (i mod 2^16 + 1) G, and a
+    300-term slice of the same points against the oracle term by term."""
+    pp = gpu_pp(64)
+    n, m = 1 << 20, 1 << 16
+    rng = random.Random(0xC3020)
+    base, acc = [], None
+    for _ in range(m):
+        acc = bn.g1_add(acc, bn.GEN)
+        base.append(acc)
+    pts = _pts(base) * (n // m)
+    a = [rng.randrange(bn.R) for _ in range(n)]
+    b = [rng.randrange(bn.R) for _ in range(n)]
+    ab = [(x + y) % bn.R for x, y in zip(a, b)]
+    ra, rb, rab = (bytes(pp.msm(pts, _scs(s))) for s in (a, b, ab))
+    assert bn.g1_bytes(bn.g1_add(bn.g1_from_bytes(ra), bn.g1_from_bytes(rb))) == rab
+    expect = bn.g1_mul(bn.GEN, sum(k * (i % m + 1) for i, k in enumerate(a)) % bn.R)
+    assert ra == bn.g1_bytes(expect)
+    lo = rng.randrange(n - 300)
+    sl = slice(lo, lo + 300)
+    got = pp.msm(pts[64 * lo:64 * (lo + 300)], _scs(a[sl]))
+    assert got == bn.g1_bytes(bn.g1_msm([base[i % m] for i in range(lo, lo + 300)], a[sl]))
