@@ -54,7 +54,7 @@ static void subm(uint64_t* a, const uint64_t* m) {
     b = (d >> 64) & 1;
   }
 }
-static fe fadd(fe a, fe b, const uint64_t* m) {
+static inline __attribute__((always_inline)) fe fadd(fe a, fe b, const uint64_t* m) {
   fe r;
   u128 c = 0;
   for (int i = 0; i < 4; i++) {
@@ -65,7 +65,7 @@ static fe fadd(fe a, fe b, const uint64_t* m) {
   if (geq(r.v, m)) subm(r.v, m);
   return r;
 }
-static fe fsub(fe a, fe b, const uint64_t* m) {
+static inline __attribute__((always_inline)) fe fsub(fe a, fe b, const uint64_t* m) {
   fe r;
   u128 bw = 0;
   for (int i = 0; i < 4; i++) {
@@ -83,7 +83,7 @@ static fe fsub(fe a, fe b, const uint64_t* m) {
   }
   return r;
 }
-static fe fmul(fe a, fe b, const uint64_t* m, uint64_t inv) {
+static inline __attribute__((always_inline)) fe fmul(fe a, fe b, const uint64_t* m, uint64_t inv) {
   uint64_t t[6] = {0, 0, 0, 0, 0, 0};
   for (int i = 0; i < 4; i++) {
     u128 c = 0;
@@ -463,57 +463,77 @@ static void reduce_gens(g1* lg, g1* rg, int m, fe x, fe xinv) { /* ipa.go:343-35
   }
 }
 
-static int verify_one(const params* pp, g1 V, span rp) {
+/* a parsed range proof (rp/bulletproof.go RangeProof, ipa.go IPA) */
+typedef struct {
+  g1 T1, T2, C, D;
+  fe tau, delta, ipv, a, b;
+  int ipa_err, nl, nr;
+  g1 Ls[70], Rs[70];
+} rp_parsed;
+
+/* DER -> rp_parsed.  Returns 1 malformed, 2 nil elements, else 0; IPA nil
+ * errors are kept in ipa_err (ipv.Verify reports them after the E1 check). */
+static int parse_rp(span rp, rp_parsed* o) {
   span dv[2], d[8], ip[4];
-  int n = pp->n, k = pp->k;
   if (values(rp, dv, 2, 0) != 2) return 1;
   if (dv[0].n == 0) return 2;
   int nd = values(dv[0], d, 8, 0);
   if (nd < 0) return 1;
   if (nd < 7) return 2;
-  g1 T1, T2, C, D;
-  fe tau, delta, ipv;
   span e;
-  if (!element(d[0], &e) || !g1_from_bytes(e.p, e.n, &T1)) return 1;
-  if (!element(d[1], &e) || !g1_from_bytes(e.p, e.n, &T2)) return 1;
+  if (!element(d[0], &e) || !g1_from_bytes(e.p, e.n, &o->T1)) return 1;
+  if (!element(d[1], &e) || !g1_from_bytes(e.p, e.n, &o->T2)) return 1;
   if (!element(d[2], &e)) return 1;
-  tau = zr_from(e);
-  if (!element(d[3], &e) || !g1_from_bytes(e.p, e.n, &C)) return 1;
-  if (!element(d[4], &e) || !g1_from_bytes(e.p, e.n, &D)) return 1;
+  o->tau = zr_from(e);
+  if (!element(d[3], &e) || !g1_from_bytes(e.p, e.n, &o->C)) return 1;
+  if (!element(d[4], &e) || !g1_from_bytes(e.p, e.n, &o->D)) return 1;
   if (!element(d[5], &e)) return 1;
-  delta = zr_from(e);
+  o->delta = zr_from(e);
   if (!element(d[6], &e)) return 1;
-  ipv = zr_from(e);
+  o->ipv = zr_from(e);
   /* IPA: structural errors are reported by ipv.Verify, i.e. only after the E1 check */
-  int ipa_err = 0, ni = 0, nl = 0, nr = 0;
-  fe a = zr_u64(0), b = zr_u64(0);
-  g1 Ls[70], Rs[70];
+  int ni = 0;
+  o->ipa_err = 0;
+  o->nl = o->nr = 0;
+  o->a = zr_u64(0);
+  o->b = zr_u64(0);
   if (dv[1].n == 0) {
-    ipa_err = 4;
+    o->ipa_err = 4;
   } else {
     ni = values(dv[1], ip, 4, 0);
     if (ni < 0) return 1;
     if (ni >= 1) {
       if (!element(ip[0], &e)) return 1;
-      a = zr_from(e);
+      o->a = zr_from(e);
     }
     if (ni >= 2) {
       if (!element(ip[1], &e)) return 1;
-      b = zr_from(e);
+      o->b = zr_from(e);
     }
     span la[70], ra[70], el, er;
     if (ni >= 3) {
-      if (!element(ip[2], &el) || (nl = values(el, la, 70, 1)) < 0) return 1;
-      for (int j = 0; j < nl && j < 70; j++)
-        if (!g1_from_bytes(la[j].p, la[j].n, &Ls[j])) return 1;
+      if (!element(ip[2], &el) || (o->nl = values(el, la, 70, 1)) < 0) return 1;
+      for (int j = 0; j < o->nl && j < 70; j++)
+        if (!g1_from_bytes(la[j].p, la[j].n, &o->Ls[j])) return 1;
     }
     if (ni >= 4) {
-      if (!element(ip[3], &er) || (nr = values(er, ra, 70, 1)) < 0) return 1;
-      for (int j = 0; j < nr && j < 70; j++)
-        if (!g1_from_bytes(ra[j].p, ra[j].n, &Rs[j])) return 1;
+      if (!element(ip[3], &er) || (o->nr = values(er, ra, 70, 1)) < 0) return 1;
+      for (int j = 0; j < o->nr && j < 70; j++)
+        if (!g1_from_bytes(ra[j].p, ra[j].n, &o->Rs[j])) return 1;
     }
-    if (ni < 2) ipa_err = 4;
+    if (ni < 2) o->ipa_err = 4;
   }
+  return 0;
+}
+
+static int verify_one(const params* pp, g1 V, span rp) {
+  int n = pp->n, k = pp->k;
+  rp_parsed P;
+  int pe = parse_rp(rp, &P);
+  if (pe) return pe;
+  g1 T1 = P.T1, T2 = P.T2, C = P.C, D = P.D, *Ls = P.Ls, *Rs = P.Rs;
+  fe tau = P.tau, delta = P.delta, ipv = P.ipv, a = P.a, b = P.b;
+  int ipa_err = P.ipa_err, nl = P.nl, nr = P.nr;
 
   /* bulletproof.go:266-311 */
   g1 arr[3] = {T1, T2};

@@ -77,3 +77,27 @@ def test_c_oracle_headline_actions(built, oracle_pp):
     iss = [("issue", [], [bytes.fromhex(h) for h in c["tokens"]], bytes.fromhex(c["proof"])) for c in head["issues"]]
     got = cref.action_verify_many(p32, iss, threads=4)
     assert got == [classify(c["expect"], c["index"]) for c in head["issues"]]
+
+
+def test_cpu_batch_rp_golden(built, oracle_pp):
+    """the optimized CPU batch baseline (oracle/c/cpu_batch.c, bench.py's
+    "optimized_batch" column): honest batches close the random linear
+    combination without any per-proof fallback (so its exact com / x0 / GLV
+    chain match the reference's transcript), and batches with tampered proofs
+    bisect to the reference-order verdicts"""
+    cases = _load("rp_golden.json")
+    for bits in sorted({c["bits"] for c in cases}):
+        pp = oracle_pp.with_bit_length(bits)
+        cb = cref.CpuBatch(pp, window_bits=8, threads=4)
+        sel = [c for c in cases if c["bits"] == bits]
+        honest = [c for c in sel if c["expect"] is None]
+        got, nfb = cb.verify([bytes.fromhex(c["commitment"]) for c in honest],
+                             [bytes.fromhex(c["proof"]) for c in honest], threads=4)
+        assert got == [0] * len(honest) and nfb == 0, bits
+        # honest proofs around the tampered ones, several times over (bisection)
+        mix = honest * 3 + sel + honest * 2
+        got, nfb = cb.verify([bytes.fromhex(c["commitment"]) for c in mix], [bytes.fromhex(c["proof"]) for c in mix],
+                             threads=3)
+        assert got == [RP_CODE[c["expect"]] for c in mix], bits
+        assert nfb < len(mix) or all(c["expect"] for c in sel), bits
+        cb.close()
