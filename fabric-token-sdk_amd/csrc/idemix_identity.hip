@@ -170,9 +170,13 @@ struct FbnCurve {
     return fbn::on_curve(x, y);
   }
   template <class Sink>
+  // AMCL ECP.ToBytes(b, false): the point at infinity (held here as (0, 0)) is
+  // AMCL's projective (0, 1, 0), which Affine() leaves as is -> 0x04 || 0 || 1
   static FTS_DEV void encode(Sink& s, const F& x, const F& y) {
     s.put_byte(0x04);
-    const F ax = p256::from_mont(x), ay = p256::from_mont(y);
+    const F ax = p256::from_mont(x);
+    F ay = p256::from_mont(y);
+    if (fbn::is_zero(ax) && fbn::is_zero(ay)) ay.v[0] = 1u;
     for (int k = 7; k >= 0; k--) s.put_word(ax.v[k]);
     for (int k = 7; k >= 0; k--) s.put_word(ay.v[k]);
   }

@@ -365,7 +365,8 @@ __global__ __launch_bounds__(256) void k_nym_verify_fbn(int n, const uint32_t* _
   uint32_t tw[16];
   if (fbn::is_zero(X.z)) {
 #pragma unroll
-    for (int k = 0; k < 16; k++) tw[k] = 0u;  // unreachable for honest data
+    for (int k = 0; k < 16; k++) tw[k] = 0u;  // t = O (zero nonces): AMCL ToBytes of infinity = 0x04 || 0 || 1
+    tw[15] = 1u;
   } else {
     const fbn::Fp zi = p256::inv(X.z), zi2 = fbn::sqr(zi);
     const fbn::Fp ax = p256::from_mont(fbn::mul(X.x, zi2)), ay = p256::from_mont(fbn::mul(X.y, fbn::mul(zi2, zi)));

@@ -272,8 +272,8 @@ class _Fp256bn:
         return acc
 
     def g1_bytes(self, pt):
-        if pt is None:  # unreachable for honest data; unpinned
-            return b"\x04" + bytes(64)
+        if pt is None:  # AMCL ECP.ToBytes of infinity: projective (0, 1, 0), Affine() keeps it
+            return b"\x04" + bytes(32) + (1).to_bytes(32, "big")
         return b"\x04" + pt[0].to_bytes(32, "big") + pt[1].to_bytes(32, "big")
 
     def g1_from_bytes(self, b):

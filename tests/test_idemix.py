@@ -222,3 +222,45 @@ def test_launch_tiling_gives_same_verdicts(curve):
     k.close()
     assert [I.message(int(s)) for s in st] == want
     assert 0 < sum(w is not None for w in want) < 300
+
+
+class _ZeroNonces:
+    """rng for nym_sign whose commitment nonces are 0 (t = O), nonce field random"""
+    def __init__(self, seed):
+        self.r, self.calls = random.Random(seed), 0
+
+    def randrange(self, n):
+        self.calls += 1
+        return self.r.randrange(n) if self.calls == 1 else 0
+
+
+def test_zero_nonce_signature_oracle():
+    """a signer with zero commitment nonces gets t = O; the transcript then
+    carries the curve's encoding of infinity (FP256BN: AMCL ToBytes of its
+    projective (0, 1, 0) = 0x04 || 0 || 1) and the signature is valid"""
+    from oracle import idemix as O
+    for C, ipk_raw in ((O.FP256BNC, IPK_FBN), (O.BN254C, IPK)):
+        ipk = O.parse_ipk(ipk_raw, C)
+        sk, rn = 12345, 67890
+        nym = O.make_nym(ipk, sk, rn)
+        sig = O.nym_sign(ipk, sk, nym, rn, b"zero nonces", _ZeroNonces(3))
+        O.nym_verify(ipk, C.g1_bytes(nym), sig, b"zero nonces")
+    assert O.FP256BNC.g1_bytes(None) == b"\x04" + bytes(32) + (1).to_bytes(32, "big")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("curve", ["bn254", "fp256bn"])
+def test_zero_nonce_signature_gpu(curve, ipk_dev, ipk_fbn):
+    """t = O on the device: the same verdicts as the oracle (valid, and invalid
+    for a different message)"""
+    from fts_gpu import idemix as I
+    from oracle import idemix as O
+    C, raw, dev = (O.BN254C, IPK, ipk_dev) if curve == "bn254" else (O.FP256BNC, IPK_FBN, ipk_fbn)
+    ipk = O.parse_ipk(raw, C)
+    sk, rn = 424242, 171717
+    nym = O.make_nym(ipk, sk, rn)
+    sig = O.nym_sign(ipk, sk, nym, rn, b"zero nonces", _ZeroNonces(5))
+    nb = C.g1_bytes(nym)
+    st = dev.verify_batch([nb, nb], [sig, sig], [b"zero nonces", b"other"])
+    assert I.message(int(st[0])) is None
+    assert I.message(int(st[1])) is not None
