@@ -199,6 +199,12 @@ constexpr int RLC_NCOEF = 8;
 // fixed-base columns of the batch equation: 0 G, 1 H, 2+i G_i, 2+n+i H_i,
 // 2n+2 K, 2n+3 P, 2n+4 Q (last: the only column that needs x0)
 inline __host__ __device__ int rlc_ncols(int n) { return 2 * n + 5; }
+// group test over many small groups (k_rlc_group_cols_small + launch_msm_small):
+// groups of at most GT_SMALL_MAX proof slots; GT_CC columns per lane, whose
+// fixed-base products are summed in the lane (gfix: [G][gt_nchunks][24])
+constexpr int GT_SMALL_MAX = 64;
+constexpr int GT_CC = 8;
+inline __host__ __device__ int gt_nchunks(int n) { return (rlc_ncols(n) + GT_CC - 1) / GT_CC; }
 struct RlcDev {
   uint32_t* key;     // [8] ChaCha20 key (fresh per call)
   uint32_t* msc;     // [B][5+2k][8] MSM scalars (canonical)

@@ -1181,7 +1181,10 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   d.pre_rlc_arg = pre_rlc_arg;
   d.rlc_fork = c->rlc_fork == 2 ? (d.com_fixed ? 0 : 1) : c->rlc_fork;
   d.ev_coef = L.ev_c;
-  d.x0_mid = c->x0_split ? w.x0mid.as<uint32_t>() : nullptr;
+  // x0 prefix beside the com chain: work path only.  On the latency path the
+  // prefix hash shares CUs with com_tree and the MSM's chunks and delays both
+  // (lone 4,096-proof batch: 3.51 ms with it, 3.06 ms without, one box)
+  d.x0_mid = c->x0_split && !d.com_fixed ? w.x0mid.as<uint32_t>() : nullptr;
   d.excl = pre_rlc ? w.rp_excl.as<int32_t>() : nullptr;
   RlcDev r{w.r_key.as<uint32_t>(), w.r_msc.as<uint32_t>(),   w.r_coef.as<uint32_t>(), w.r_colsum.as<uint32_t>(),
            w.r_fixed.as<uint32_t>(), w.r_flag.as<int32_t>(), w.m_scratch.as<uint32_t>(), mp};

@@ -5,6 +5,8 @@
 // (T1, T2, V, com, L_j, R_j) replaces the per-proof final equations of
 // bulletproof.go:314-324 and ipa.go:254-259.  Also exposed as fts_msm_g1
 // (BASELINE config C3 microbenchmark).
+#include <algorithm>
+
 #include "device/g1.hpp"
 #include "device/glv.hpp"
 #include "device/fixed_base.hpp"
@@ -314,24 +316,30 @@ __global__ void __launch_bounds__(256) k_msm_windows(int nw, int WB, int NSg, co
   if (t == 0) store_g1j(parts + (((size_t)grp * (nw + 1) + w) * WB + j) * 24, acc);
 }
 
-// lane w <= nw: W_w = sum of window w's parts, shifted to its bit offset
-// (2^off_w W_w: the windows' doubling chains run in parallel lanes, the longest
-// is the top window's ~off_top doublings instead of one 127-doubling Horner
-// chain), lane nw: the extra points; then an LDS tree over the lanes
-__global__ void __launch_bounds__(64) k_msm_final(int nw, int WB, const MsmWindow* __restrict__ win,
-                                                  const uint32_t* __restrict__ parts_all, uint32_t* __restrict__ out_all) {
-  // lane-cooperative (device/coop.hpp): 12 groups of COOP_G lanes, group g takes
-  // windows g, g + 12, ...; each doubling is 3 product levels instead of 7
-  constexpr int NGRP = 64 / COOP_G;
-  __shared__ uint32_t sh[NGRP * 24];
+// coop group per window w <= nw: W_w = sum of window w's parts, shifted to its
+// bit offset (2^off_w W_w: the windows' doubling chains run in parallel, the
+// longest is the top window's ~off_top doublings instead of one 127-doubling
+// Horner chain), group nw: the extra points; then an LDS tree over the groups.
+// Lane-cooperative (device/coop.hpp): 12 groups of COOP_G lanes per wave, and
+// as many waves as the windows need (a grouped plan's narrower windows: 14-16
+// of them; with one wave, two windows shared a group and its chain doubled).
+constexpr int FINAL_GPW = 64 / COOP_G;  // coop groups per wave
+constexpr int FINAL_MAXW = 4;           // waves per block (48 groups >= MSM windows + 1)
+__global__ void __launch_bounds__(64 * FINAL_MAXW) k_msm_final(int nw, int WB, const MsmWindow* __restrict__ win,
+                                                               const uint32_t* __restrict__ parts_all,
+                                                               uint32_t* __restrict__ out_all) {
+  __shared__ uint32_t sh[FINAL_MAXW * FINAL_GPW * 24];
   const int t = threadIdx.x, grp = blockIdx.x;  // one block per MSM group
-  const int g = t / COOP_G, role = t % COOP_G, base = g * COOP_G;
-  const bool live = g < NGRP;
+  const int wave = t / 64, lt = t % 64;
+  const int NG = (blockDim.x / 64) * FINAL_GPW;  // coop groups in the block
+  const int gi = lt / COOP_G, role = lt % COOP_G, base = gi * COOP_G;  // base: lane within the wave
+  const int g = wave * FINAL_GPW + gi;
+  const bool live = gi < FINAL_GPW;
   const uint32_t* parts = parts_all + (size_t)grp * (nw + 1) * WB * 24;
   uint32_t* out = out_all + (size_t)grp * 24;
   G1J acc = g1j_identity();
   if (live) {
-    for (int w = g; w <= nw; w += NGRP) {
+    for (int w = g; w <= nw; w += NG) {
       G1J W = load_g1j(parts + (size_t)w * WB * 24);
       for (int j = 1; j < WB; j++) coop_add(W, load_g1j(parts + ((size_t)w * WB + j) * 24), role, base);
       if (w < nw)
@@ -341,13 +349,62 @@ __global__ void __launch_bounds__(64) k_msm_final(int nw, int WB, const MsmWindo
     if (role == 0) store_g1j(sh + g * 24, acc);
   }
   __syncthreads();
-  for (int half = 8; half >= 1; half >>= 1) {
-    if (live && g < half && g + half < NGRP) coop_add(acc, load_g1j(sh + (g + half) * 24), role, base);
+  // tree over the NG groups' sums (NG = 12 * waves; pad to a power of two)
+  int P2 = 1;
+  while (P2 < NG) P2 <<= 1;
+  for (int half = P2 / 2; half >= 1; half >>= 1) {
+    const bool act = live && g < half && g + half < NG;
+    if (act) coop_add(acc, load_g1j(sh + (g + half) * 24), role, base);
     __syncthreads();
-    if (live && role == 0 && g < half && g + half < NGRP) store_g1j(sh + g * 24, acc);
+    if (act && role == 0) store_g1j(sh + g * 24, acc);
     __syncthreads();
   }
   if (t == 0) store_g1j(out, acc);
+}
+
+// ------------------------------------------------ many small groups
+// Finish of a grouped plan whose groups are small (the group test's later
+// rounds: 10^4 groups of a few proofs, windows of <= 2^5 buckets): the
+// segment / LDS-tree / one-block-per-group kernels above leave most lanes idle
+// there.  Lane per (window, group), window-major so a wave's lanes run the
+// same doubling count: W = sum_d d B_d by running sums over the window's
+// buckets, then 2^off W -> wparts[group][window].
+__global__ void __launch_bounds__(256) k_msm_small_windows(int nw, int G, int NBg, const MsmWindow* __restrict__ win,
+                                                          const uint32_t* __restrict__ buckets,
+                                                          uint32_t* __restrict__ wparts) {
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (size_t)nw * G) return;
+  const int w = (int)(gid / G), grp = (int)(gid % G);
+  const MsmWindow W = win[w];
+  const int nb = 1 << (W.width - 1);
+  const uint32_t* Bk = buckets + ((size_t)grp * NBg + W.bbase) * 24;
+  G1J sum = g1j_identity(), acc = g1j_identity();
+  for (int j = nb - 1; j >= 0; j--) {
+    add_inl(sum, load_g1j(Bk + (size_t)j * 24));
+    add_inl(acc, sum);
+  }
+  for (int q = 0; q < W.off; q++) acc = g1j_dbl(acc);
+  store_g1j(wparts + ((size_t)grp * nw + w) * 24, acc);
+}
+
+// one wave per group: its nw window parts + nextra extra points, LDS tree -> out[group]
+__global__ void __launch_bounds__(64) k_msm_small_final(int nw, const uint32_t* __restrict__ wparts,
+                                                        const uint32_t* __restrict__ extra, int nextra,
+                                                        uint32_t* __restrict__ out) {
+  __shared__ uint32_t sh[64 * 24];
+  const int t = threadIdx.x, grp = blockIdx.x;
+  G1J acc = g1j_identity();
+  for (int q = t; q < nw + nextra; q += 64)
+    add_inl(acc, load_g1j(q < nw ? wparts + ((size_t)grp * nw + q) * 24 : extra + ((size_t)grp * nextra + q - nw) * 24));
+  store_g1j(sh + t * 24, acc);
+  __syncthreads();
+  for (int half = 32; half >= 1; half >>= 1) {
+    if (t < half) add_inl(acc, load_g1j(sh + (t + half) * 24));
+    __syncthreads();
+    if (t < half) store_g1j(sh + t * 24, acc);
+    __syncthreads();
+  }
+  if (t == 0) store_g1j(out + (size_t)grp * 24, acc);
 }
 
 // ------------------------------------------------ standalone MSM (fts_msm_*)
@@ -396,8 +453,9 @@ __global__ void k_msm_to_bytes(const uint32_t* __restrict__ jac, uint8_t* __rest
 // scratch: NS * 24 words.  p.d_win must already hold p.win (uploaded by the caller).
 // `extra` (nextra Jacobian points) is produced on stream s_extra: joined
 // before the window reduction that sums it.
-void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
-                uint32_t* scratch, hipStream_t s, hipStream_t s_extra, Timeline* tl) {
+// digits, counting sort, chunked bucket accumulation and bucket sums (every plan)
+static void launch_msm_buckets(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, hipStream_t s,
+                               Timeline* tl) {
   (void)hipMemsetAsync(p.counts, 0, (size_t)p.NB * 4, s);
   FTS_LAUNCH(k_msm_digits, p.N, 256, s, msm_idx(p), p.d_win, scalars, p.keys, p.cursor, p.counts);
   tl->mark("k_msm_digits", s, 0);
@@ -414,6 +472,11 @@ void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalar
   tl->mark("k_msm_chunks", s, (double)p.NV * p.nw * (COST_MADD + 0.5));
   FTS_LAUNCH(k_msm_bucket_sum, p.NB, g_lat_bs, s, p.NB, p.counts, p.chunk_off, p.partials, p.buckets);
   tl->mark("k_msm_bucket_sum", s, 0);
+}
+
+void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
+                uint32_t* scratch, hipStream_t s, hipStream_t s_extra, Timeline* tl) {
+  launch_msm_buckets(p, points, scalars, s, tl);
   FTS_LAUNCH(k_msm_segments, p.NS, g_lat_bs, s, p.nw, p.NS, p.NSg, p.NBg, p.d_win, p.buckets, p.segs, scratch);
   tl->mark("k_msm_segments", s, (double)p.NB * 2 * COST_ADD);
   if (s_extra != s) tl->fork(s_extra, s);
@@ -421,12 +484,31 @@ void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalar
   hipLaunchKernelGGL(k_msm_windows, dim3(p.nw + 1, p.WB, p.G), dim3(256), 0, s, p.nw, p.WB, p.NSg, p.d_win, p.segs,
                      extra, nextra, parts);
   tl->mark("k_msm_windows", s, (double)(p.NS + (double)p.G * nextra) * COST_ADD);
-  hipLaunchKernelGGL(k_msm_final, dim3(p.G), dim3(64), 0, s, p.nw, p.WB, p.d_win, parts, p.out);
+  {
+    const int waves = std::min(FINAL_MAXW, (p.nw + 1 + FINAL_GPW - 1) / FINAL_GPW);
+    hipLaunchKernelGGL(k_msm_final, dim3(p.G), dim3(64 * waves), 0, s, p.nw, p.WB, p.d_win, parts, p.out);
+  }
   {
     double dbl = 0;
     for (int w = 0; w < p.nw; w++) dbl += p.win[w].off;
     tl->mark("k_msm_final", s, p.G * (dbl * COST_DBL + (p.nw + 1) * (p.WB + 1) * COST_ADD));
   }
+}
+
+// grouped plan with small groups: buckets as usual, then k_msm_small_windows /
+// k_msm_small_final (needs G * nw * 24 words of p.scratch past the scan sums)
+void launch_msm_small(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra,
+                      int nextra, hipStream_t s, Timeline* tl) {
+  launch_msm_buckets(p, points, scalars, s, tl);
+  uint32_t* wparts = p.scratch + 2 * (size_t)p.NBLK + 2;
+  FTS_LAUNCH(k_msm_small_windows, (size_t)p.nw * p.G, 256, s, p.nw, p.G, p.NBg, p.d_win, p.buckets, wparts);
+  {
+    double dbl = 0;
+    for (int w = 0; w < p.nw; w++) dbl += p.win[w].off;
+    tl->mark("k_msm_small_windows", s, (double)p.G * (dbl * COST_DBL + 2.0 * p.NBg * COST_ADD));
+  }
+  hipLaunchKernelGGL(k_msm_small_final, dim3(p.G), dim3(64), 0, s, p.nw, wparts, extra, nextra, p.out);
+  tl->mark("k_msm_small_final", s, (double)p.G * (p.nw + nextra) * COST_ADD);
 }
 
 void launch_msm_load(int N, const uint8_t* raw_pts, const uint8_t* raw_sc, uint32_t* pts, uint32_t* sc, uint32_t* bad,

@@ -1096,10 +1096,55 @@ __global__ void __launch_bounds__(256) k_rlc_prep(int B, int n, int k, const int
   store_f(K + 7 * 8, fr_mul(rho2, fr_from_canon(S + RP_SC_DELTA * 8)));
 }
 
-// one block per (column, group), columns col0 + blockIdx.x (layout: rlc_ncols).
-// s_i, y^-i and z^2 2^i y^-i come precomputed, i-major, from k_rp_powers.  The
-// batch check has one group of all B proofs; the group test has G groups of
-// gs proof slots (sel[g gs + j], -1 = empty) -> colsum[g][col]
+// proof b's scalar in RLC column col (layout: rlc_ncols), Montgomery form.
+// s_i, y^-i and z^2 2^i y^-i come precomputed, i-major, from k_rp_powers.
+FTS_DEV Fr rlc_col_value(int col, int b, int B, int n, int k, const uint32_t* __restrict__ ch,
+                         const uint32_t* __restrict__ coef, const uint32_t* __restrict__ ypow,
+                         const uint32_t* __restrict__ svec, const uint32_t* __restrict__ zvec) {
+  const uint32_t* K = coef + (size_t)b * RLC_NCOEF * 8;
+  Fr v;
+  if (col < 2) {
+    load_f(K + col * 8, v);
+  } else if (col < 2 + n) {  // rho' a s_i
+    Fr ra;
+    load_f(K + 3 * 8, ra);
+    if (!f_is_zero(ra)) {
+      Fr sv;
+      load_f(svec + ((size_t)(col - 2) * B + b) * 8, sv);
+      v = fr_mul(ra, sv);
+    } else {
+      v = ra;
+    }
+  } else if (col < 2 + 2 * n) {  // rho' b s_i^-1 y^-i - rho' z^2 2^i y^-i
+    const int i = col - 2 - n;
+    Fr r2;
+    load_f(K + 5 * 8, r2);
+    if (!f_is_zero(r2)) {
+      Fr rb, sv, yp, zv;
+      load_f(K + 4 * 8, rb);
+      load_f(svec + ((size_t)(n - 1 - i) * B + b) * 8, sv);
+      load_f(ypow + ((size_t)i * B + b) * 8, yp);
+      load_f(zvec + ((size_t)i * B + b) * 8, zv);
+      v = f_sub(fr_mul(fr_mul(rb, sv), yp), fr_mul(r2, zv));
+    } else {
+      v = r2;
+    }
+  } else if (col < 2 * n + 4) {  // -rho' z (K), rho' delta (P)
+    load_f(K + (col - 2 * n + 4) * 8, v);
+  } else {  // rho'(ab - ip) x0 (Q)
+    load_f(K + 2 * 8, v);
+    if (!f_is_zero(v)) {
+      Fr x0;
+      load_f(ch + ((size_t)b * rp_nch(k) + CH_X0) * 8, x0);
+      v = fr_mul(v, x0);
+    }
+  }
+  return v;
+}
+
+// one block per (column, group), columns col0 + blockIdx.x.  The batch check
+// has one group of all B proofs; the group test has G groups of gs proof slots
+// (sel[g gs + j], -1 = empty) -> colsum[g][col]
 __global__ void __launch_bounds__(256) k_rlc_columns(int B, int n, int k, int gs, int col0,
                                                      const int32_t* __restrict__ sel, const uint32_t* __restrict__ ch,
                                                      const uint32_t* __restrict__ coef, const uint32_t* __restrict__ ypow,
@@ -1111,45 +1156,7 @@ __global__ void __launch_bounds__(256) k_rlc_columns(int B, int n, int k, int gs
   for (int j = t; j < gs; j += nt) {
     const int b = sel ? sel[(size_t)grp * gs + j] : grp * gs + j;
     if (b < 0 || b >= B) continue;
-    const uint32_t* K = coef + (size_t)b * RLC_NCOEF * 8;
-    Fr v;
-    if (col < 2) {
-      load_f(K + col * 8, v);
-    } else if (col < 2 + n) {  // rho' a s_i
-      Fr ra;
-      load_f(K + 3 * 8, ra);
-      if (!f_is_zero(ra)) {
-        Fr sv;
-        load_f(svec + ((size_t)(col - 2) * B + b) * 8, sv);
-        v = fr_mul(ra, sv);
-      } else {
-        v = ra;
-      }
-    } else if (col < 2 + 2 * n) {  // rho' b s_i^-1 y^-i - rho' z^2 2^i y^-i
-      const int i = col - 2 - n;
-      Fr r2;
-      load_f(K + 5 * 8, r2);
-      if (!f_is_zero(r2)) {
-        Fr rb, sv, yp, zv;
-        load_f(K + 4 * 8, rb);
-        load_f(svec + ((size_t)(n - 1 - i) * B + b) * 8, sv);
-        load_f(ypow + ((size_t)i * B + b) * 8, yp);
-        load_f(zvec + ((size_t)i * B + b) * 8, zv);
-        v = f_sub(fr_mul(fr_mul(rb, sv), yp), fr_mul(r2, zv));
-      } else {
-        v = r2;
-      }
-    } else if (col < 2 * n + 4) {  // -rho' z (K), rho' delta (P)
-      load_f(K + (col - 2 * n + 4) * 8, v);
-    } else {  // rho'(ab - ip) x0 (Q)
-      load_f(K + 2 * 8, v);
-      if (!f_is_zero(v)) {
-        Fr x0;
-        load_f(ch + ((size_t)b * rp_nch(k) + CH_X0) * 8, x0);
-        v = fr_mul(v, x0);
-      }
-    }
-    acc = f_add(acc, v);
+    acc = f_add(acc, rlc_col_value(col, b, B, n, k, ch, coef, ypow, svec, zvec));
   }
   store_f(sh + t * 8, acc);
   __syncthreads();
@@ -1226,6 +1233,45 @@ __global__ void __launch_bounds__(RF_ITEMS * FB_NW) k_rlc_fixed(int n, int G, in
     __syncthreads();
   }
   if (live && w == 0) store_g1j(out + ((size_t)grp * NC + col) * 24, acc);
+}
+
+// Group test over many small groups (gs <= GT_SMALL_MAX proof slots): lane per
+// (chunk of GT_CC columns, group), chunk-major so a wave's lanes read the same
+// columns' tables: the group's column scalars (sum over its proof slots, as
+// k_rlc_columns) and their fixed-base products, 16 mixed additions each from
+// the 16-bit tables, accumulated in the lane -> gfix[grp][chunk] (Jacobian).
+// (The per-column LDS-tree form above is for a few large groups: with 10^4
+// groups of 8 it ran at ~20 % of the MAD peak.)
+__global__ void __launch_bounds__(256) k_rlc_group_cols_small(int B, int n, int k, int G, int gs,
+                                                              const int32_t* __restrict__ sel,
+                                                              const uint32_t* __restrict__ ch,
+                                                              const uint32_t* __restrict__ coef,
+                                                              const uint32_t* __restrict__ ypow,
+                                                              const uint32_t* __restrict__ svec,
+                                                              const uint32_t* __restrict__ zvec,
+                                                              const uint32_t* __restrict__ tables,
+                                                              uint32_t* __restrict__ gfix) {
+  const int NC = rlc_ncols(n), nch = gt_nchunks(n);
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (size_t)G * nch) return;
+  const int chk = (int)(gid / G), grp = (int)(gid % G);
+  G1J acc = g1j_identity();
+  const int c1 = min(NC, (chk + 1) * GT_CC);
+  for (int col = chk * GT_CC; col < c1; col++) {
+    Fr v = f_zero<FrP>();
+    for (int j = 0; j < gs; j++) {
+      const int b = sel[(size_t)grp * gs + j];
+      if (b < 0 || b >= B) continue;
+      v = f_add(v, rlc_col_value(col, b, B, n, k, ch, coef, ypow, svec, zvec));
+    }
+    if (f_is_zero(v)) continue;
+    const Fr cv = f_from_mont(v);
+    Scalar sk;
+#pragma unroll
+    for (int q = 0; q < 8; q++) sk.v[q] = cv.v[q];
+    fb_mul_acc(acc, tables + (size_t)rlc_col_base(n, col) * FB_WORDS_PER_BASE, sk);
+  }
+  store_g1j(gfix + ((size_t)grp * nch + chk) * 24, acc);
 }
 
 // batch verdict: flag = 1 if the combination is the identity; on success the
@@ -1324,6 +1370,8 @@ void launch_build_wide_tables(const uint32_t* bases, int nb, uint32_t* tables, u
 
 void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
                 uint32_t* scratch, hipStream_t s, hipStream_t s_extra, Timeline* tl);
+void launch_msm_small(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra,
+                      int nextra, hipStream_t s, Timeline* tl);
 
 // Whole range-proof pipeline up to the batch verdict (flag): exact per-proof
 // phase (everything that is hashed: challenges, H'_i, com, x0) and the
@@ -1351,25 +1399,37 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   }
   FTS_LAUNCH(k_rp_chal_fr, B, g_lat_bs, s, B, n, k, d.status, d.ch, d.scratch);
   tl->mark("k_rp_chal_fr", s, (double)B * (3 * k + 4 * (k + 1) + 12));
-  FTS_LAUNCH(k_rp_powers, B * (n >> std::min(PW_LC, k)), 64, s, B, n, k, d.status, d.ch, d.ypow, d.svec, d.zvec);
-  tl->mark("k_rp_powers", s, (double)B * (3.0 * n + 2.0 * k));
-  // batch check, x0-free part, on s3 (after the caller's hook, e.g. the exclusion
-  // of range proofs whose action failed its sigma proof).  Forked after the
-  // exact phase's widest launch (d.rlc_fork = 1, default) so the check's
-  // latency-bound chain does not share SIMDs with it, or right after the
-  // challenges (0).
-  auto rlc_side = [&]() {
+  // batch check on s3 (after the caller's hook, e.g. the exclusion of range
+  // proofs whose action failed its sigma proof): the weights need only the
+  // challenges, so on the latency path (d.rlc_fork = 0) they start right after
+  // k_rp_chal_fr, before the exact phase's wide launches take the CUs; the
+  // work path forks after its widest launch (d.rlc_fork = 1) so the check's
+  // latency-bound chain does not share SIMDs with it.  The x0-free columns and
+  // their fixed-base products run on s4 (they need k_rp_powers' vectors): the
+  // MSM's bucket phase does not wait for them, only its window reduction.
+  auto rlc_prep = [&]() {
     tl->fork(s, s3);
     if (d.pre_rlc) d.pre_rlc(d.pre_rlc_arg, s3);
     FTS_LAUNCH(k_rlc_prep, B, g_lat_bs, s3, B, n, k, d.status, d.excl, d.ipa_flag, d.sc, d.ch, r.key, r.msc, r.coef);
     tl->mark("k_rlc_prep", s3, (double)B * (3 * k + 33));
     (void)hipEventRecord(d.ev_coef, s3);
-    hipLaunchKernelGGL(k_rlc_columns, dim3(NC - 1, 1), dim3(256), 0, s3, B, n, k, B, 0, (const int32_t*)nullptr, d.ch,
+  };
+  auto rlc_rest = [&]() {
+    tl->fork(s, s4);   // k_rp_powers' vectors
+    tl->fork(s3, s4);  // the weights
+    hipLaunchKernelGGL(k_rlc_columns, dim3(NC - 1, 1), dim3(256), 0, s4, B, n, k, B, 0, (const int32_t*)nullptr, d.ch,
                        r.coef, d.ypow, d.svec, d.zvec, r.colsum);
-    tl->mark("k_rlc_columns", s3, (double)B * 4 * n);
-    FTS_LAUNCH(k_rlc_fixed, (size_t)(NC - 1) * FB_NW, RF_ITEMS * FB_NW, s3, n, 1, 0, NC - 1, r.colsum, tables, r.fixed);
-    tl->mark("k_rlc_fixed", s3, (double)(NC - 1) * (FB_NW * 3 + (FB_NW - 1) * COST_ADD));
-    launch_msm(r.plan, d.pts, r.msc, r.fixed, NC - 1, r.msm_scratch, s3, s3, tl);
+    tl->mark("k_rlc_columns", s4, (double)B * 4 * n);
+    FTS_LAUNCH(k_rlc_fixed, (size_t)(NC - 1) * FB_NW, RF_ITEMS * FB_NW, s4, n, 1, 0, NC - 1, r.colsum, tables, r.fixed);
+    tl->mark("k_rlc_fixed", s4, (double)(NC - 1) * (FB_NW * 3 + (FB_NW - 1) * COST_ADD));
+    launch_msm(r.plan, d.pts, r.msc, r.fixed, NC - 1, r.msm_scratch, s3, s4, tl);
+  };
+  if (!d.rlc_fork) rlc_prep();
+  FTS_LAUNCH(k_rp_powers, B * (n >> std::min(PW_LC, k)), 64, s, B, n, k, d.status, d.ch, d.ypow, d.svec, d.zvec);
+  tl->mark("k_rp_powers", s, (double)B * (3.0 * n + 2.0 * k));
+  auto rlc_side = [&]() {
+    if (d.rlc_fork) rlc_prep();
+    rlc_rest();
   };
   if (!d.rlc_fork) rlc_side();
   // exact per-proof phase on s
@@ -1485,6 +1545,17 @@ void launch_rlc_group_test(const RpBatchDev& d, const RlcDev& r, const uint32_t*
                            uint32_t* next_count, hipStream_t s, Timeline* tl) {
   const int n = d.n, k = d.k;
   const int NC = rlc_ncols(n);
+  if (gs <= GT_SMALL_MAX) {
+    const int nch = gt_nchunks(n);
+    FTS_LAUNCH(k_rlc_group_cols_small, (size_t)G * nch, 256, s, d.B, n, k, G, gs, sel, d.ch, r.coef, d.ypow, d.svec,
+               d.zvec, tables, gfix);
+    tl->mark("k_rlc_group_cols", s, (double)G * (gs * 3.0 * n + NC * FB_NW * COST_MADD));
+    launch_msm_small(p, d.pts, r.msc, gfix, nch, s, tl);
+    FTS_LAUNCH(k_rlc_group_final, (size_t)G * gs, 256, s, G * gs, gs, sel, p.out, d.status, d.ipa_flag, next,
+               next_count);
+    tl->mark("k_rlc_group_final", s, 0);
+    return;
+  }
   hipLaunchKernelGGL(k_rlc_columns, dim3(NC, G), dim3(gs <= 64 ? 64 : 256), 0, s, d.B, n, k, gs, 0, sel, d.ch,
                      r.coef, d.ypow, d.svec, d.zvec, gcol);
   tl->mark("k_rlc_group_columns", s, (double)G * gs * 4 * n);
