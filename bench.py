@@ -1357,6 +1357,17 @@ def bench_mixed(args):
             assert set(np.nonzero(r[0])[0]) == bad_tr and set(np.nonzero(r[2])[0]) == bad_is
     kt = {k: (v[0] * args.steps, v[1]) for k, v in pp.last_timings_ex().items()}
     value = world * (n_tr + n_is) * args.steps / elapsed
+    # one call alone after the timed region: the fallback's own cost (in the
+    # pipelined region the latency-bound fallback kernels share the CUs with the
+    # other calls' passes, which stretches their spans)
+    iso_reps = 3
+    kti, t_iso = {}, time.perf_counter()
+    for _ in range(iso_reps):
+        batches[0].verify()
+        for kname, (ms, mads) in pp.last_timings_ex().items():
+            o = kti.get(kname, (0.0, 0.0))
+            kti[kname] = (o[0] + ms, mads)
+    iso_ms = (time.perf_counter() - t_iso) * 1e3 / iso_reps
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         # the same interleaving as the batch (1 issue : 4 transfers), verdicts from the GPU run
@@ -1386,7 +1397,10 @@ def bench_mixed(args):
                                    "per step (%d range proofs), %d calls in flight" % (2 * n_tr + 16 * n_is, nb),
                        "transfers_per_gpu": n_tr, "issues_per_gpu": n_is, "parallelism": "shard%d" % world},
             "roofline": _roofline_from(kt, args.steps), "cpu_baseline": cpu,
-            "fallback": _fallback_share(kt, args.steps, elapsed / args.steps * nb * 1e3),
+            "fallback": _fallback_share(kti, iso_reps, iso_ms),
+            "fallback_pipelined": _fallback_share(kt, args.steps, elapsed / args.steps * nb * 1e3),
+            "isolated_call_ms": round(iso_ms, 3),
+            "kernel_ms_isolated": {k: round(v[0] / iso_reps, 4) for k, v in kti.items()},
             "kernel_ms": {k: round(v[0] / args.steps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),
             flush=True)
     if dist is not None:

@@ -27,6 +27,7 @@
 #include "device/transcript.hpp"
 #include "device/helpers.hpp"
 #include "device/msm.hpp"
+#include "device/coop.hpp"
 #include "common/chacha20.hpp"
 #include "../../include/fts_gpu.h"
 
@@ -930,6 +931,99 @@ __global__ void __launch_bounds__(64) k_rp_terms_fixed(int B, int n, int k, cons
   store_g1j(terms + ((size_t)b * rp_nterms(n, k) + slot) * 24, r);
 }
 
+// the same terms with COOP_G lanes per product (device/coop.hpp): 12 products
+// per wave, each doubling 3 product levels instead of 7 and each addition 5
+// instead of 16, tables of 1..8 P and 1..8 phi(P) in LDS.  For a few
+// thousand products on an otherwise idle GPU (the group test's last stage
+// after a small failing group set) the chain latency, not the work, bounds the
+// stage; the results are the same Jacobian triples as glv_mul's.
+constexpr int TV_GPW = 64 / COOP_G;  // products per wave
+constexpr size_t TV_COOP_MAX = 16384; // products up to which the cooperative form runs (~1,400 waves)
+__global__ void __launch_bounds__(64) k_rp_terms_var_coop(int B, int n, int k, const int32_t* __restrict__ sel,
+                                                          const int32_t* __restrict__ status,
+                                                          const int32_t* __restrict__ ipa_flag,
+                                                          const uint32_t* __restrict__ pts,
+                                                          const uint32_t* __restrict__ ch,
+                                                          uint32_t* __restrict__ terms) {
+  __shared__ uint32_t T[TV_GPW][16][24];
+  const int nv = 3 + 2 * k;
+  const int lt = threadIdx.x, gi = lt / COOP_G, role = lt % COOP_G, base = gi * COOP_G;
+  if (gi >= TV_GPW) return;  // lanes 60..63: no group
+  const int item = blockIdx.x * TV_GPW + gi;
+  if (item >= B * nv) return;  // whole groups leave together
+  int b = item / nv;
+  const int t = item % nv;
+  if (sel) b = sel[b];
+  if (status[b] != 0) return;
+  const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
+  const uint32_t* Pt = pts + (size_t)b * rp_npts(k) * 16;
+  int slot, pt;
+  Fr s;
+  if (t < 3) {
+    slot = 2 + t;
+    const int chi = t == 0 ? CH_X : (t == 1 ? CH_X2 : CH_Z2);
+    load_f(C + chi * 8, s);
+    pt = t == 0 ? RP_PT_T1 : (t == 1 ? RP_PT_T2 : RP_PT_V);
+  } else {
+    slot = 6 + 2 * n + (t - 3);
+    if (ipa_flag[b] != 0) {
+      if (role == 0) store_g1j(terms + ((size_t)b * rp_nterms(n, k) + slot) * 24, g1j_identity());
+      return;
+    }
+    int j = t - 3;
+    if (j < k) {
+      load_f(C + (CH_XJ + j) * 8, s);
+      pt = RP_PT_L + j;
+    } else {
+      j -= k;
+      load_f(C + (CH_XJ + k + j) * 8, s);
+      pt = RP_PT_L + k + j;
+    }
+    s = fr_sqr(s);
+  }
+  const G1A pa = load_g1a(Pt + pt * 16);
+  G1J acc = g1j_identity();
+  if (!g1a_is_identity(pa)) {
+    const Scalar sk = fr_canon(f_neg(s));
+    uint32_t k1[4], k2[4], s1, s2;
+    glv_decompose(sk.v, k1, s1, k2, s2);
+    G1J P = g1j_from_affine(pa), Q = P;
+    Q.x = fp_mul(Q.x, glv_beta());
+    if (s1) P.y = f_neg(P.y);
+    if (s2) Q.y = f_neg(Q.y);
+    uint32_t(*tb)[24] = T[gi];
+    // 1..8 P, 1..8 Q (every lane of the group writes the same words)
+    for (int h = 0; h < 2; h++) {
+      const G1J t0 = h ? Q : P;
+      G1J cur = t0;
+      store_g1j(tb[8 * h], cur);
+      cur = coop_dbl(t0, role, base);
+      store_g1j(tb[8 * h + 1], cur);
+      for (int e = 2; e < 8; e++) {
+        coop_add(cur, t0, role, base);
+        store_g1j(tb[8 * h + e], cur);
+      }
+    }
+    const uint32_t ca = recode_carries(k1), cb = recode_carries(k2);
+    for (int w = 31; w >= 0; w--) {
+      const int da = window_digit(k1, ca, w), db = window_digit(k2, cb, w);
+      if (w != 31)
+        for (int r = 0; r < 4; r++) acc = coop_dbl(acc, role, base);
+      if (da != 0) {
+        G1J q = load_g1j(tb[(da < 0 ? -da : da) - 1]);
+        if (da < 0) q.y = f_neg(q.y);
+        coop_add(acc, q, role, base);
+      }
+      if (db != 0) {
+        G1J q = load_g1j(tb[8 + (db < 0 ? -db : db) - 1]);
+        if (db < 0) q.y = f_neg(q.y);
+        coop_add(acc, q, role, base);
+      }
+    }
+  }
+  if (role == 0) store_g1j(terms + ((size_t)b * rp_nterms(n, k) + slot) * 24, acc);
+}
+
 __global__ void __launch_bounds__(64) k_rp_terms_var(int B, int n, int k, const int32_t* __restrict__ sel,
                                                      const int32_t* __restrict__ status,
                                                      const int32_t* __restrict__ ipa_flag,
@@ -1525,8 +1619,12 @@ void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, const int32
   const int B = sel ? nsel : d.B, n = d.n, k = d.k;
   FTS_LAUNCH(k_rp_terms_fixed, B * (3 + 2 * n), 64, s, B, n, k, sel, d.status, d.ipa_flag, d.sc, d.ch, tables, d.terms);
   tl->mark("k_rp_terms_fixed", s, (double)B * (3 + 2 * n) * COST_FB_FRESH);
-  FTS_LAUNCH(k_rp_terms_var, B * (3 + 2 * k), 64, s, B, n, k, sel, d.status, d.ipa_flag, d.pts, d.ch, d.terms,
-             d.scratch);
+  const size_t nvar = (size_t)B * (3 + 2 * k);
+  if (nvar <= TV_COOP_MAX)  // latency-bound: lane-cooperative chains
+    FTS_LAUNCH(k_rp_terms_var_coop, (nvar + TV_GPW - 1) / TV_GPW * 64, 64, s, B, n, k, sel, d.status, d.ipa_flag, d.pts,
+               d.ch, d.terms);
+  else
+    FTS_LAUNCH(k_rp_terms_var, nvar, 64, s, B, n, k, sel, d.status, d.ipa_flag, d.pts, d.ch, d.terms, d.scratch);
   tl->mark("k_rp_terms_var", s, (double)B * (3 + 2 * k) * (4.0 * 7.0 + 12.0 * COST_ADD + 124 * COST_DBL + 60 * COST_ADD));
   if (B > 0)
     hipLaunchKernelGGL(k_rp_check, dim3((B + CK_PROOFS - 1) / CK_PROOFS), dim3(CK_LANES * CK_PROOFS), 0, s, B, n, k,

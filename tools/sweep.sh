@@ -23,6 +23,6 @@ while IFS='|' read -r tag envs cmd; do
   grep '^{' $OUT/$tag.log | tail -1 | python3 -c "
 import json,sys
 d=json.loads(sys.stdin.read() or '{}')
-print('$tag', d.get('value'), d.get('ms_per_step'), *[d.get(f) for f in '${FIELDS:-}'.split()])" 2>/dev/null ||
+print('$tag', d.get('value', d.get('median')), d.get('ms_per_step', d.get('merged')), *[d.get(f) for f in '${FIELDS:-}'.split()])" 2>/dev/null ||
   tail -1 $OUT/$tag.log | sed "s/^/$tag /"
 done < "$recipe"
