@@ -342,12 +342,13 @@ FTS_DEV void atab_build8(const ATab& T, int e0, const G1J& P, Fp& pre, bool iden
   }
 }
 
-// all 16 entries -> affine: z_e^-1 = (z_0 .. z_e)^-1 * (z_0 .. z_{e-1}), one inversion
+// the first NE entries -> affine: z_e^-1 = (z_0 .. z_e)^-1 * (z_0 .. z_{e-1}), one inversion
+template <int NE = 16>
 FTS_DEV void atab_normalize(const ATab& T) {
   Fp inv;
-  load_fp(T.pre(15), inv);
+  load_fp(T.pre(NE - 1), inv);
   inv = nl_fp_inv(inv);
-  for (int e = 15; e >= 0; e--) {
+  for (int e = NE - 1; e >= 0; e--) {
     Fp zi = inv;
     if (e > 0) {
       Fp pp, z;
@@ -363,6 +364,25 @@ FTS_DEV void atab_normalize(const ATab& T) {
     store_fp(T.xy(e), fp_mul(x, zi2));
     store_fp(T.xy(e) + 8, fp_mul(fp_mul(y, zi2), zi));
   }
+}
+
+// a * P (127-bit magnitude, sign folded into P) over a normalised 8-entry
+// table (entries 0..7 = 1..8 P): 124 doublings, <= 32 mixed additions
+FTS_DEV G1J straus1_atab(const ATab& T, const uint32_t a[4], bool ida) {
+  const uint32_t ca = recode_carries(a);
+  G1J acc = g1j_identity();
+  for (int w = 31; w >= 0; w--) {
+    const int da = ida ? 0 : window_digit(a, ca, w);
+    G1A qa;
+    if (da != 0) qa = load_g1a(T.xy((da < 0 ? -da : da) - 1));
+    if (w != 31)
+      for (int r = 0; r < 4; r++) acc = g1j_dbl(acc);
+    if (da != 0) {
+      if (da < 0) qa.y = f_neg(qa.y);
+      madd_inl(acc, qa);
+    }
+  }
+  return acc;
 }
 
 // a * P + b * Q (127-bit magnitudes, signs folded into P, Q) over a normalised

@@ -192,7 +192,7 @@ struct Lane {
   hipStream_t s = nullptr, s2 = nullptr;
   hipStream_t s3 = nullptr;         // sigma proofs of action batches (beside the range-proof pass)
   hipStream_t s4 = nullptr;         // latency path: the x0 transcript prefix beside the x*D chain
-  hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr;  // cross-stream ordering (no timing)
+  hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr, ev_d = nullptr;  // cross-stream ordering (no timing)
   Workspace ws;
   Timeline tl;
   float host_prep_ms = 0, host_enqueue_ms = 0, host_wait_ms = 0;  // host wall time of the last run
@@ -405,6 +405,7 @@ struct fts_ctx {
   // 64/2048 -> 256/8192 = 485k -> 533k actions/s)
   int gt1 = 256, gt2_min = 8192;
   int x0_split = 1;                 // FTS_X0_SPLIT: work path hashes the x0 prefix beside the com chain
+  int com_split = 0;                // FTS_COM_SPLIT: work path computes x*D beside the exact phase (k_rp_xd)
   // FTS_RLC_FORK: the batch check forks after the fixed-base products (1) or after the
   // challenges (0); 2 (default): after the challenges on the latency path (a lone small
   // pass: its MSM chain is the critical path, 3.16 -> 2.98 ms per 4,096-proof batch),
@@ -526,6 +527,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
       if (L->ev_a) hipEventDestroy(L->ev_a);
       if (L->ev_b) hipEventDestroy(L->ev_b);
       if (L->ev_c) hipEventDestroy(L->ev_c);
+      if (L->ev_d) hipEventDestroy(L->ev_d);
       if (L->s2 && L->s2 != L->s) hipStreamDestroy(L->s2);
       if (L->s4 && L->s4 != L->s) hipStreamDestroy(L->s4);
       if (L->s) hipStreamDestroy(L->s);
@@ -548,6 +550,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_COM_FIXED_MAX")) c->com_fixed_max = (size_t)std::max(0L, atol(e));
   if (const char* e = getenv("FTS_RLC_FORK")) c->rlc_fork = std::max(0, std::min(2, atoi(e)));
   if (const char* e = getenv("FTS_X0_SPLIT")) c->x0_split = atoi(e) != 0;
+  if (const char* e = getenv("FTS_COM_SPLIT")) c->com_split = atoi(e) != 0;
   if (const char* e = getenv("FTS_GT1")) c->gt1 = std::max(8, std::min(1024, atoi(e)));
   if (const char* e = getenv("FTS_GT2_MIN")) c->gt2_min = std::max(0, atoi(e));
   // process-wide launch knobs of rp_kernels.hip: read once, before any context can
@@ -606,7 +609,8 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
     if (hipStreamCreateWithPriority(&L->s3, hipStreamNonBlocking, s3_prio) != hipSuccess ||
         hipEventCreateWithFlags(&L->ev_a, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&L->ev_b, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&L->ev_c, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&L->ev_c, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&L->ev_d, hipEventDisableTiming) != hipSuccess)
       return fail(FTS_API_EDEVICE);
     L->tl.create();
   }
@@ -843,6 +847,7 @@ void fts_ctx_destroy(fts_ctx* c) {
     if (L->ev_a) hipEventDestroy(L->ev_a);
     if (L->ev_b) hipEventDestroy(L->ev_b);
     if (L->ev_c) hipEventDestroy(L->ev_c);
+    if (L->ev_d) hipEventDestroy(L->ev_d);
     L->tl.destroy();
     if (L->done) hipEventDestroy(L->done);
     if (L->s2 && L->s2 != L->s) hipStreamDestroy(L->s2);
@@ -1185,6 +1190,8 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   // prefix hash shares CUs with com_tree and the MSM's chunks and delays both
   // (lone 4,096-proof batch: 3.51 ms with it, 3.06 ms without, one box)
   d.x0_mid = c->x0_split && !d.com_fixed ? w.x0mid.as<uint32_t>() : nullptr;
+  d.com_split = c->com_split && !d.com_fixed;
+  d.ev_xd = L.ev_d;
   d.excl = pre_rlc ? w.rp_excl.as<int32_t>() : nullptr;
   RlcDev r{w.r_key.as<uint32_t>(), w.r_msc.as<uint32_t>(),   w.r_coef.as<uint32_t>(), w.r_colsum.as<uint32_t>(),
            w.r_fixed.as<uint32_t>(), w.r_flag.as<int32_t>(), w.m_scratch.as<uint32_t>(), mp};

@@ -416,7 +416,10 @@ __global__ void __launch_bounds__(256) k_rp_hsum_chunks(int B, int n, const int3
 // table (glv.hpp straus2_atab).  Both lanes first join S = sum_c 2^(16c) S_c
 // from k_rp_hsum_chunks' Horner chunks (3 x (16 doublings + 1 addition) at
 // n = 64; no separate one-lane-per-proof join launch) -> terms[b][2 + h]
-__global__ void __launch_bounds__(256, 3) k_rp_com_var(int B, int n, int k, const int32_t* __restrict__ status,
+#ifndef FTS_COMVAR_OCC
+#define FTS_COMVAR_OCC 3  // waves per SIMD the register budget allows (A/B builds: -DFTS_COMVAR_OCC=4)
+#endif
+__global__ void __launch_bounds__(256, FTS_COMVAR_OCC) k_rp_com_var(int B, int n, int k, const int32_t* __restrict__ status,
                                                    const uint32_t* __restrict__ pts, const uint32_t* __restrict__ ch,
                                                    const uint32_t* __restrict__ chunks, uint32_t* __restrict__ atab,
                                                    const uint32_t* __restrict__ terms, uint32_t* __restrict__ hpj) {
@@ -459,6 +462,58 @@ __global__ void __launch_bounds__(256, 3) k_rp_com_var(int B, int n, int k, cons
   // adds its fixed-base term (z K or -delta P, k_rp_fixed_exact), lane 0 also C,
   // then lane 0 adds lane 1's partial (cross-lane shuffle) and writes com
   add_inl(r, load_g1j(terms + ((size_t)b * COM_NTERMS + h) * 24));
+  G1J c = g1j_identity();
+  if (h == 0) c = g1j_from_affine(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_C) * 16));
+  add_inl(r, c);
+  G1J o;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    o.x.v[q] = __shfl_xor(r.x.v[q], 1);
+    o.y.v[q] = __shfl_xor(r.y.v[q], 1);
+    o.z.v[q] = __shfl_xor(r.z.v[q], 1);
+  }
+  if (h == 0) {
+    add_inl(r, o);
+    store_g1j(hpj + ((size_t)b * (n + 1) + n) * 24, r);
+  }
+}
+
+// Split form of k_rp_com_var (d.com_split): x*D comes from k_rp_xd (terms[b][2 + h],
+// computed beside the exact phase), so a lane's chain is w_h phi^h(S) alone over an
+// 8-entry affine table (124 doublings, 32 mixed additions); the two lanes of a
+// proof then add their fixed-base term, their x*D half and (lane 0) C -> com
+__global__ void __launch_bounds__(256, FTS_COMVAR_OCC) k_rp_com_s(int B, int n, int k, const int32_t* __restrict__ status,
+                                                               const uint32_t* __restrict__ pts,
+                                                               const uint32_t* __restrict__ ch,
+                                                               const uint32_t* __restrict__ chunks,
+                                                               uint32_t* __restrict__ atab,
+                                                               const uint32_t* __restrict__ terms,
+                                                               uint32_t* __restrict__ hpj) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = gid >> 1, h = gid & 1;
+  if (b >= B || status[b] != 0) return;
+  const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
+  Fr z2;
+  load_f(C + CH_Z2 * 8, z2);
+  uint32_t wk[2][4], ws[2];
+  glv_decompose(fr_canon(z2).v, wk[0], ws[0], wk[1], ws[1]);
+  const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
+  const uint32_t* Sc = chunks + (size_t)b * nc * 24;
+  G1J S = load_g1j(Sc + (nc - 1) * 24);
+  for (int c = nc - 2; c >= 0; c--) {
+    for (int q = 0; q < HS_CHUNK; q++) S = g1j_dbl(S);
+    add_inl(S, load_g1j(Sc + c * 24));
+  }
+  const bool idS = f_is_zero(S.z);
+  if (h) S.x = fp_mul(S.x, glv_beta());
+  if (ws[h]) S.y = f_neg(S.y);
+  const ATab T{atab, (size_t)2 * B, (size_t)gid};
+  Fp pre;
+  atab_build8<false>(T, 0, S, pre, idS);
+  atab_normalize<8>(T);
+  G1J r = straus1_atab(T, wk[h], idS);
+  add_inl(r, load_g1j(terms + ((size_t)b * COM_NTERMS + 2 + h) * 24));  // x_h phi^h(D)
+  add_inl(r, load_g1j(terms + ((size_t)b * COM_NTERMS + h) * 24));      // z K or -delta P
   G1J c = g1j_identity();
   if (h == 0) c = g1j_from_affine(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_C) * 16));
   add_inl(r, c);
@@ -533,7 +588,8 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_all(int B, int n, int k, con
 // (canonical), so this runs concurrently with k_rp_chal_fr.
 __global__ void __launch_bounds__(256) k_rp_xd(int B, int n, int k, const int32_t* __restrict__ status,
                                               const uint32_t* __restrict__ pts, const uint8_t* __restrict__ small_msgs,
-                                              uint32_t* __restrict__ vtab, uint32_t* __restrict__ terms) {
+                                              uint32_t* __restrict__ vtab, uint32_t* __restrict__ terms, int tstride,
+                                              int toff) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= 2 * B) return;
   const int h = gid / B, b = gid % B;
@@ -546,7 +602,7 @@ __global__ void __launch_bounds__(256) k_rp_xd(int B, int n, int k, const int32_
   if (h) D.x = fp_mul(D.x, glv_beta());
   if (xs[h]) D.y = f_neg(D.y);
   const G1J r = vb128j(D, xk[h], vtab, (size_t)2 * B, (size_t)gid);
-  store_g1j(terms + ((size_t)b * com_fx_slots(n) + n + 2 + h) * 24, r);
+  store_g1j(terms + ((size_t)b * tstride + toff + h) * 24, r);
 }
 
 // com = C + sum of the n + 4 terms: CT_LANES lanes per proof (CT_PROOFS proofs
@@ -1488,8 +1544,16 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     // latency path: x*D on the side stream beside chal_fr and the fixed-base products
     tl->fork(s, s2);
     FTS_LAUNCH(k_rp_xd, 2 * B, g_lat_bs, s2, B, n, k, d.status, d.pts, d.small_msgs, d.scratch + (size_t)B * (k + 1) * 8,
-               d.terms);
+               d.terms, com_fx_slots(n), n + 2);
     tl->mark("k_rp_xd", s2, (double)B * 2 * COST_VB128);
+  } else if (d.com_split) {
+    // work path, split com: x*D (terms[b][2 + h]) beside the exact phase from the
+    // x digest on; lane tables past the S chunks and the com lanes' tables
+    tl->fork(s, s2);
+    FTS_LAUNCH(k_rp_xd, 2 * B, g_lat_bs, s2, B, n, k, d.status, d.pts, d.small_msgs,
+               d.scratch + (size_t)B * HS_SCRATCH + (size_t)2 * B * ATAB_WORDS, d.terms, COM_NTERMS, 2);
+    tl->mark("k_rp_xd", s2, (double)B * 2 * COST_VB128);
+    (void)hipEventRecord(d.ev_xd, s2);
   }
   FTS_LAUNCH(k_rp_chal_fr, B, g_lat_bs, s, B, n, k, d.status, d.ch, d.scratch);
   tl->mark("k_rp_chal_fr", s, (double)B * (3 * k + 4 * (k + 1) + 12));
@@ -1571,10 +1635,18 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     FTS_LAUNCH(k_rp_hsum_chunks, B * nch, g_chain_bs, s, B, n, d.status, d.hpa, d.scratch);
     tl->mark("k_rp_hsum_chunks", s, (double)B * (n - nch) * (COST_DBL + COST_MADD));
     // scratch: [0, B*HS_SCRATCH) Horner chunks of S, then the 2B lanes' affine tables
-    FTS_LAUNCH(k_rp_com_var, 2 * B, g_chain_bs, s, B, n, k, d.status, d.pts, d.ch, d.scratch,
-               d.scratch + (size_t)B * HS_SCRATCH, d.terms, d.hpj);
-    tl->mark("k_rp_com_var", s,
-             (double)B * 2 * ((nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD) + COST_STRAUS2_ATAB + 2.5 * COST_ADD));
+    if (d.com_split) {
+      (void)hipStreamWaitEvent(s, d.ev_xd, 0);
+      FTS_LAUNCH(k_rp_com_s, 2 * B, g_chain_bs, s, B, n, k, d.status, d.pts, d.ch, d.scratch,
+                 d.scratch + (size_t)B * HS_SCRATCH, d.terms, d.hpj);
+      tl->mark("k_rp_com_s", s,
+               (double)B * 2 * ((nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD) + COST_STRAUS1_ATAB + 3.5 * COST_ADD));
+    } else {
+      FTS_LAUNCH(k_rp_com_var, 2 * B, g_chain_bs, s, B, n, k, d.status, d.pts, d.ch, d.scratch,
+                 d.scratch + (size_t)B * HS_SCRATCH, d.terms, d.hpj);
+      tl->mark("k_rp_com_var", s,
+               (double)B * 2 * ((nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD) + COST_STRAUS2_ATAB + 2.5 * COST_ADD));
+    }
   }
   launch_normalize(B, 1, n + 1, n, d.status, d.hpj, d.hpa, d.hp_be, s);
   tl->mark("k_rp_normalize_com", s, (double)B * (2.0 * 8.0 / NORM_E + 9.0));
