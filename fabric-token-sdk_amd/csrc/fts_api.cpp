@@ -406,6 +406,7 @@ struct fts_ctx {
   int gt1 = 256, gt2_min = 8192;
   int x0_split = 1;                 // FTS_X0_SPLIT: work path hashes the x0 prefix beside the com chain
   int com_split = 0;                // FTS_COM_SPLIT: work path computes x*D beside the exact phase (k_rp_xd)
+  int idle_gather_us = 0;           // FTS_IDLE_GATHER_US: gather window on an idle device (0: start at once)
   // FTS_RLC_FORK: the batch check forks after the fixed-base products (1) or after the
   // challenges (0); 2 (default): after the challenges on the latency path (a lone small
   // pass: its MSM chain is the critical path, 3.16 -> 2.98 ms per 4,096-proof batch),
@@ -551,6 +552,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_RLC_FORK")) c->rlc_fork = std::max(0, std::min(2, atoi(e)));
   if (const char* e = getenv("FTS_X0_SPLIT")) c->x0_split = atoi(e) != 0;
   if (const char* e = getenv("FTS_COM_SPLIT")) c->com_split = atoi(e) != 0;
+  if (const char* e = getenv("FTS_IDLE_GATHER_US")) c->idle_gather_us = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_GT1")) c->gt1 = std::max(8, std::min(1024, atoi(e)));
   if (const char* e = getenv("FTS_GT2_MIN")) c->gt2_min = std::max(0, atoi(e));
   // process-wide launch knobs of rp_kernels.hip: read once, before any context can
@@ -1416,8 +1418,9 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
       continue;
     }
     const bool device_busy = c->free_lanes.size() < c->lanes.size();
-    if (device_busy && c->rp_pending.front() == &me && c->pending_proofs < c->gather_target) {
-      const auto deadline = me.arrived + std::chrono::microseconds(c->gather_us);
+    const int wait_us = device_busy ? c->gather_us : c->idle_gather_us;
+    if (wait_us > 0 && c->rp_pending.front() == &me && c->pending_proofs < c->gather_target) {
+      const auto deadline = me.arrived + std::chrono::microseconds(wait_us);
       if (std::chrono::steady_clock::now() < deadline) {
         me.cv.wait_until(lk, deadline);
         continue;
