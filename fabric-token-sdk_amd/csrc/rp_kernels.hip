@@ -994,7 +994,7 @@ __global__ void __launch_bounds__(64) k_rp_terms_fixed(int B, int n, int k, cons
 // after a small failing group set) the chain latency, not the work, bounds the
 // stage; the results are the same Jacobian triples as glv_mul's.
 constexpr int TV_GPW = 64 / COOP_G;  // products per wave
-constexpr size_t TV_COOP_MAX = 49152; // products up to which the cooperative form runs (~4,100 waves)
+constexpr size_t TV_COOP_MAX = 16384; // products up to which the cooperative form runs (~1,400 waves)
 __global__ void __launch_bounds__(64) k_rp_terms_var_coop(int B, int n, int k, const int32_t* __restrict__ sel,
                                                           const int32_t* __restrict__ status,
                                                           const int32_t* __restrict__ ipa_flag,

@@ -28,6 +28,9 @@
  *   int   cpu_batch_verify(void* ctx, int count, const uint8_t* coms, const uint8_t* const* ders,
  *                          const size_t* lens, int threads, int32_t* out)
  *         -> number of proofs that took the per-proof fallback, or -1
+ *   int   cpu_batch_verify_ex(..., uint8_t* com_out, uint8_t* x0_out)
+ *         the same, plus every proof's exact com (64 B) and x0 (32 B, BE) for
+ *         parity checks at full batch size (zeros where the proof stopped earlier)
  *   void  cpu_batch_free(void* ctx)
  * gens as in ref_verify.c: [G=ped1, H=ped2, P, Q, G_0..G_{n-1}, H_0..H_{n-1}].
  */
@@ -430,6 +433,8 @@ typedef struct {
   uint8_t* live;    /* [count]: in the combination */
   fe* col;          /* [count][5 + 2n]: the proof's column scalars (table base order) */
   uint64_t rng_key[4];
+  uint8_t* com_out; /* optional [count][64]: com (BE x || y) of every proof that reached it */
+  uint8_t* x0_out;  /* optional [count][32]: x0 (BE) */
   atomic_int next, tid;
 } batch_job;
 
@@ -575,6 +580,8 @@ static int proof_phase(batch_job* j, int i, fe* cs, uint8_t* x0buf, g1j* jtmp, a
   fe_to_be(ipv, x0buf + c->x0_len - 32);
   sha256_buf(x0buf, c->x0_len, dg);
   fe x0 = digest_zr(dg);
+  if (j->com_out) g1_bytes(com, j->com_out + 64 * (size_t)i);
+  if (j->x0_out) fe_to_be(x0, j->x0_out + 32 * (size_t)i);
   /* the proof's share of sum_p rho_p E1_p + rho'_p E2_p = O */
   fe rho = weight(j, i, 0), rho2 = weight(j, i, 1), rhom = zmont(rho), rho2m = zmont(rho2);
   aff* vp = j->vpts + (size_t)i * j->npv;
@@ -784,8 +791,8 @@ static int bisect(batch_job* j, int lo, int hi, int threads) {
   return m;
 }
 
-int cpu_batch_verify(void* ctx, int count, const uint8_t* coms, const uint8_t* const* ders, const size_t* lens,
-                     int threads, int32_t* out) {
+int cpu_batch_verify_ex(void* ctx, int count, const uint8_t* coms, const uint8_t* const* ders, const size_t* lens,
+                        int threads, int32_t* out, uint8_t* com_out, uint8_t* x0_out) {
   cpu_ctx* c = ctx;
   if (!c || count < 0) return -1;
   if (count == 0) return 0;
@@ -798,6 +805,10 @@ int cpu_batch_verify(void* ctx, int count, const uint8_t* coms, const uint8_t* c
   j.ders = ders;
   j.lens = lens;
   j.out = out;
+  j.com_out = com_out;
+  j.x0_out = x0_out;
+  if (com_out) memset(com_out, 0, 64 * (size_t)count);
+  if (x0_out) memset(x0_out, 0, 32 * (size_t)count);
   j.npv = 4 + 2 * c->k;
   j.vpts = malloc(sizeof(aff) * (size_t)count * j.npv);
   j.vinf = calloc((size_t)count * j.npv, 1);
@@ -819,4 +830,9 @@ int cpu_batch_verify(void* ctx, int count, const uint8_t* coms, const uint8_t* c
   free(j.live);
   free(j.col);
   return nfb;
+}
+
+int cpu_batch_verify(void* ctx, int count, const uint8_t* coms, const uint8_t* const* ders, const size_t* lens,
+                     int threads, int32_t* out) {
+  return cpu_batch_verify_ex(ctx, count, coms, ders, lens, threads, out, NULL, NULL);
 }

@@ -125,6 +125,10 @@ def _batch_lib():
         _blib.cpu_batch_verify.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.POINTER(C.c_char_p),
                                            C.POINTER(C.c_size_t), C.c_int, C.POINTER(C.c_int32)]
         _blib.cpu_batch_verify.restype = C.c_int
+        _blib.cpu_batch_verify_ex.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.POINTER(C.c_char_p),
+                                              C.POINTER(C.c_size_t), C.c_int, C.POINTER(C.c_int32), C.c_char_p,
+                                              C.c_char_p]
+        _blib.cpu_batch_verify_ex.restype = C.c_int
         _blib.cpu_batch_free.argtypes = [C.c_void_p]
     return _blib
 
@@ -148,6 +152,19 @@ class CpuBatch:
         nfb = _batch_lib().cpu_batch_verify(self.h, n, b"".join(coms), arr, lens, threads, out)
         assert nfb >= 0
         return list(out)[:n], nfb
+
+    def verify_ex(self, coms, ders, threads=1):
+        """verify() plus every proof's exact com (64 B) and x0 (32 B BE); zeros
+        where the proof stopped before them (parse errors, IPA structure)"""
+        n = len(ders)
+        arr = (C.c_char_p * max(n, 1))(*ders)
+        lens = (C.c_size_t * max(n, 1))(*[len(d) for d in ders])
+        out = (C.c_int32 * max(n, 1))()
+        com_out, x0_out = C.create_string_buffer(64 * max(n, 1)), C.create_string_buffer(32 * max(n, 1))
+        nfb = _batch_lib().cpu_batch_verify_ex(self.h, n, b"".join(coms), arr, lens, threads, out, com_out, x0_out)
+        assert nfb >= 0
+        return (list(out)[:n], nfb, [com_out.raw[64 * i:64 * i + 64] for i in range(n)],
+                [x0_out.raw[32 * i:32 * i + 32] for i in range(n)])
 
     def close(self):
         if self.h:

@@ -4,6 +4,7 @@ intermediates (x, y, z, polEval, x0, x_j, com, H'_i), bit-exact."""
 import ctypes as C
 import json
 import os
+import random
 
 import pytest
 
@@ -201,3 +202,42 @@ def test_reference_shaped_api(gpu_pp):
     with pytest.raises(fts_gpu.VerifyError) as e:
         fts_gpu.RangeVerifier(pp, com).Verify(raw2)
     assert str(e.value) == "invalid range proof"
+
+
+@pytest.mark.parametrize("path", ["latency", "work"])
+def test_full_batch_exact_intermediates_vs_cpu_batch(gpu_pp, pp_raw, oracle_pp, path):
+    """BASELINE C2 at full size with EXACT intermediates: 4,096 rp64 proofs
+    (1 % tampered in T1, an L_j or the IPA's a), every verdict, every com and
+    every x0 on the device equal those of the independent CPU batch verifier
+    (oracle/c/cpu_batch.c: its com / x0 pinned by the golden vectors, its
+    failing proofs' verdicts from the reference-order restatement); on both
+    com paths (latency: fixed-base groups + x*D; work: Horner + joint chain)"""
+    from oracle import cref
+    pp = gpu_pp(64) if path == "latency" else _work_path_pp(pp_raw, 64)
+    n = 4096
+    rng = random.Random(0xC2C2 + (path == "work"))
+    vals = [rng.getrandbits(64) for _ in range(n)]
+    bfs = [rng.randrange(bn.R).to_bytes(32, "big") for _ in range(n)]
+    proofs, coms = pp.prove_range_batch_gpu(vals, bfs, seed=0xC2C2)
+    for i in sorted(rng.sample(range(n), 41)):
+        r = zkat.RangeProof.deserialize(proofs[i])
+        kind = rng.randrange(3)
+        if kind == 0:
+            r.data.T1 = bn.g1_add(r.data.T1, bn.GEN)
+        elif kind == 1:
+            j = rng.randrange(6)
+            r.ipa.L[j] = bn.g1_add(r.ipa.L[j], bn.GEN)
+        else:
+            r.ipa.Left = (r.ipa.Left + 1) % bn.R
+        proofs[i] = r.serialize()
+    st = pp.verify_range_proofs(proofs, coms)
+    assert ("k_rp_fixed_all" in pp.last_timings()) == (path == "latency")
+    cb = cref.CpuBatch(oracle_pp.with_bit_length(64), window_bits=10, threads=8)
+    want, nfb, com_c, x0_c = cb.verify_ex(coms, proofs, threads=8)
+    cb.close()
+    assert [int(s) for s in st] == want
+    assert 0 < sum(w != 0 for w in want) <= 41 and nfb > 0
+    for i in range(n):
+        v, com, _ = _intermediates(pp, i)
+        assert com == com_c[i], i
+        assert v[7] == int.from_bytes(x0_c[i], "big"), i

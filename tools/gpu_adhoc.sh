@@ -1,11 +1,9 @@
-# ad-hoc GPU step: split-com A/B (FTS_COM_SPLIT) on the isolated 81,920-proof pass, bursts and steady state
+# ad-hoc GPU step: full-size exact-intermediate parity vs the CPU batch verifier + C5 with the coop per-proof stage
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r03f; mkdir -p $O
-FTS_COM_SPLIT=1 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_rp.py tests/test_gpu_scale.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/pt.log 2>&1 || { tail -30 $O/pt.log; exit 1; }
-tail -1 $O/pt.log
-for sp in 0 1 0 1; do
-  FTS_COM_SPLIT=$sp timeout -k 10 120 python3 tools/pass_times.py 81920 > $O/pass.log 2>&1 || { tail $O/pass.log; exit 1; }
-  echo "split=$sp: $(cat $O/pass.log | tr ' ' '\n' | grep -E 'wall|com_|hsum|fixed_exact|k_rp_xd|x0_prefix' | tr '\n' ' ')"
-done
-bash tools/sweep.sh tools/sweeps/com_split.txt || exit 1
+O=gpurun_out/r03g; mkdir -p $O
+timeout -k 10 500 python3 -u -m pytest tests/test_gpu_rp.py tests/test_gpu_scale.py tests/test_gpu_actions.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/pt.log 2>&1 || { tail -40 $O/pt.log; exit 1; }
+grep -E "PASS|FAIL" $O/pt.log | tail -8; tail -1 $O/pt.log
+timeout -k 10 300 python3 -u bench.py --workload mixed --transfers 4096 --steps 48 --warmup 4 --cpu-sample 0 > $O/bench_mixed.log 2>&1 || { tail $O/bench_mixed.log; exit 1; }
+grep '^{' $O/bench_mixed.log | tail -1 > $O/bench_mixed.json
+python3 -c "import json; d=json.load(open('$O/bench_mixed.json')); print('mixed', d['value'], d['isolated_call_ms'], d['fallback'], d['fallback_pipelined']); print({k:v for k,v in d['kernel_ms_isolated'].items() if k.startswith('fb:')})"
