@@ -34,7 +34,7 @@ namespace fts {
 
 constexpr int MSM_MAX_WINDOWS = 64;
 constexpr int MSM_SEG = 8;   // buckets per running-sum segment
-constexpr int MSM_CH = 8;    // points per bucket-accumulation chunk
+constexpr int MSM_CH = 8;    // smallest bucket-accumulation chunk (points per lane); plans pick 8..64 (MsmPlan::ch)
 constexpr int MSM_SCAN_ITEMS = 1024;  // buckets per block of the scan passes
 constexpr int MSM_WIN_ITEMS = 1024;   // segments per block of k_msm_windows
 
@@ -68,6 +68,7 @@ struct MsmPlan {
   int G;           // groups (1: one MSM)
   int ptsg;        // points per group
   int NBg, NSg;    // buckets / segments per group
+  int ch;          // points per bucket-accumulation chunk (MSM_CH)
   const int32_t* sel;  // device: proof indirection (grouped fallback), or nullptr
   int sel_pts;         // points per proof of the indirection
   MsmWindow win[MSM_MAX_WINDOWS];  // host copy
@@ -125,8 +126,13 @@ inline void msm_layout_groups(int N, int G, int ptsg, MsmPlan& p) {
   p.NSg = sb;
   p.NB = G * bb;
   p.NS = G * sb;
-  // chunk slots: sum over buckets of ceil(count / MSM_CH) <= entries / MSM_CH + buckets
-  p.NC = nw * (NV / MSM_CH + 1) + p.NB;
+  // chunk size: MSM_CH.  Larger chunks from the average bucket load (~3 partials
+  // per bucket) cut k_msm_bucket_sum 8x at 2^22 points but made k_msm_chunks
+  // slower (fewer lanes in flight to hide the point gathers: 81,920-proof pass
+  // 3.0 -> 6.1 ms, 512-step headline 4.77 -> 4.30 M/s); kept per plan for A/B
+  p.ch = MSM_CH;
+  // chunk slots: sum over buckets of ceil(count / ch) <= entries / ch + buckets
+  p.NC = nw * (NV / p.ch + 1) + p.NB;
   p.NBLK = (p.NB + MSM_SCAN_ITEMS - 1) / MSM_SCAN_ITEMS;
   int maxs = 0;
   for (int w = 0; w < nw; w++) {

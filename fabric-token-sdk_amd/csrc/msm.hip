@@ -34,10 +34,10 @@ FTS_DEV uint32_t scalar_bits4(const uint32_t s[4], int off, int width) {
 
 // the point-indexing part of a plan, passed to the kernels by value
 struct MsmIdx {
-  int N, nw, ptsg, NBg, sel_pts;
+  int N, nw, ptsg, NBg, sel_pts, ch;
   const int32_t* sel;
 };
-inline MsmIdx msm_idx(const MsmPlan& p) { return MsmIdx{p.N, p.nw, p.ptsg, p.NBg, p.sel_pts, p.sel}; }
+inline MsmIdx msm_idx(const MsmPlan& p) { return MsmIdx{p.N, p.nw, p.ptsg, p.NBg, p.sel_pts, p.ch, p.sel}; }
 // input index of plan point i (-1: absent padding point of a grouped plan)
 FTS_DEV long msm_src(const MsmIdx& p, int i) {
   if (!p.sel) return i;
@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(256) k_msm_digits(MsmIdx p, const MsmWindow* _
 // MSM_SCAN_ITEMS buckets (4 per lane) + block totals; pass 2: one block scans
 // the totals; pass 3: adds the block offsets, copies the cursor and fills the
 // chunk map; k_msm_chunks ignores slots past the chunk total (blk[2 NBLK + 1]).
-__global__ void __launch_bounds__(256) k_msm_scan1(int NB, const uint32_t* __restrict__ counts,
+__global__ void __launch_bounds__(256) k_msm_scan1(int NB, int ch, const uint32_t* __restrict__ counts,
                                                    uint32_t* __restrict__ offsets, uint32_t* __restrict__ chunk_off,
                                                    uint32_t* __restrict__ blk) {
   __shared__ uint32_t pe[256], pc[256];
@@ -99,7 +99,7 @@ __global__ void __launch_bounds__(256) k_msm_scan1(int NB, const uint32_t* __res
   for (int j = 0; j < 4; j++) {
     cnt[j] = base + j < NB ? counts[base + j] : 0u;
     le += cnt[j];
-    lc += (cnt[j] + MSM_CH - 1) / MSM_CH;
+    lc += (cnt[j] + ch - 1) / ch;
   }
   pe[t] = le;
   pc[t] = lc;
@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(256) k_msm_scan1(int NB, const uint32_t* __res
       chunk_off[base + j] = rc;
     }
     re += cnt[j];
-    rc += (cnt[j] + MSM_CH - 1) / MSM_CH;
+    rc += (cnt[j] + ch - 1) / ch;
   }
   if (t == 255) {
     blk[2 * blockIdx.x] = pe[255];
@@ -166,7 +166,7 @@ __global__ void __launch_bounds__(256) k_msm_scan2(int nblk, uint32_t* __restric
   }
 }
 
-__global__ void __launch_bounds__(256) k_msm_scan3(int NB, const uint32_t* __restrict__ counts,
+__global__ void __launch_bounds__(256) k_msm_scan3(int NB, int ch, const uint32_t* __restrict__ counts,
                                                    uint32_t* __restrict__ offsets, uint32_t* __restrict__ cursor,
                                                    uint32_t* __restrict__ chunk_off, int32_t* __restrict__ chunk_bkt,
                                                    const uint32_t* __restrict__ blk) {
@@ -176,7 +176,7 @@ __global__ void __launch_bounds__(256) k_msm_scan3(int NB, const uint32_t* __res
   const uint32_t o = offsets[b] + blk[2 * q], oc = chunk_off[b] + blk[2 * q + 1];
   offsets[b] = o;
   chunk_off[b] = oc;
-  const uint32_t nch = (counts[b] + MSM_CH - 1) / MSM_CH;
+  const uint32_t nch = (counts[b] + ch - 1) / ch;
   for (uint32_t c = 0; c < nch; c++) chunk_bkt[oc + c] = b;
 }
 
@@ -195,7 +195,7 @@ __global__ void __launch_bounds__(256) k_msm_scatter(int NV, int nw, const int32
   }
 }
 
-// one lane per chunk slot: <= MSM_CH mixed additions of sorted virtual points
+// one lane per chunk slot: <= p.ch mixed additions of sorted virtual points
 // (index >= N: phi(P_{index-N}) = (beta x, y))
 __global__ void __launch_bounds__(64, 4) k_msm_chunks(MsmIdx p, const uint32_t* __restrict__ nc_total,
                                                    const MsmWindow* __restrict__ win,
@@ -210,7 +210,7 @@ __global__ void __launch_bounds__(64, 4) k_msm_chunks(MsmIdx p, const uint32_t* 
   if (g >= (int)*nc_total) return;
   const int b = chunk_bkt[g];
   const uint32_t j = (uint32_t)g - chunk_off[b], cnt = counts[b];
-  const uint32_t lo = j * MSM_CH, hi = min(cnt, lo + MSM_CH);
+  const uint32_t lo = j * (uint32_t)p.ch, hi = min(cnt, lo + (uint32_t)p.ch);
   const uint32_t* S = sorted + offsets[b];
   const Fp beta = glv_beta();
   G1J acc = g1j_identity();
@@ -239,13 +239,13 @@ __global__ void __launch_bounds__(64, 4) k_msm_chunks(MsmIdx p, const uint32_t* 
 }
 
 // one lane per bucket: sum of its chunk partials (usually 1..4)
-__global__ void __launch_bounds__(256) k_msm_bucket_sum(int NB, const uint32_t* __restrict__ counts,
+__global__ void __launch_bounds__(256) k_msm_bucket_sum(int NB, int ch, const uint32_t* __restrict__ counts,
                                                        const uint32_t* __restrict__ chunk_off,
                                                        const uint32_t* __restrict__ partials,
                                                        uint32_t* __restrict__ buckets) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= NB) return;
-  const uint32_t nch = (counts[b] + MSM_CH - 1) / MSM_CH, c0 = chunk_off[b];
+  const uint32_t nch = (counts[b] + ch - 1) / ch, c0 = chunk_off[b];
   G1J acc = g1j_identity();
   if (nch) acc = load_g1j(partials + (size_t)c0 * 24);
   for (uint32_t q = 1; q < nch; q++) add_inl(acc, load_g1j(partials + (size_t)(c0 + q) * 24));
@@ -459,9 +459,9 @@ static void launch_msm_buckets(const MsmPlan& p, const uint32_t* points, const u
   (void)hipMemsetAsync(p.counts, 0, (size_t)p.NB * 4, s);
   FTS_LAUNCH(k_msm_digits, p.N, 256, s, msm_idx(p), p.d_win, scalars, p.keys, p.cursor, p.counts);
   tl->mark("k_msm_digits", s, 0);
-  FTS_LAUNCH(k_msm_scan1, (size_t)p.NBLK * 256, 256, s, p.NB, p.counts, p.offsets, p.chunk_off, p.scratch);
+  FTS_LAUNCH(k_msm_scan1, (size_t)p.NBLK * 256, 256, s, p.NB, p.ch, p.counts, p.offsets, p.chunk_off, p.scratch);
   hipLaunchKernelGGL(k_msm_scan2, dim3(1), dim3(256), 0, s, p.NBLK, p.scratch);
-  FTS_LAUNCH(k_msm_scan3, p.NB, 256, s, p.NB, p.counts, p.offsets, p.cursor, p.chunk_off, p.chunk_bkt, p.scratch);
+  FTS_LAUNCH(k_msm_scan3, p.NB, 256, s, p.NB, p.ch, p.counts, p.offsets, p.cursor, p.chunk_off, p.chunk_bkt, p.scratch);
   tl->mark("k_msm_scan", s, 0);
   FTS_LAUNCH(k_msm_scatter, p.NV, 256, s, p.NV, p.nw, p.keys, p.cursor, p.offsets, p.sorted);
   tl->mark("k_msm_scatter", s, 0);
@@ -470,7 +470,7 @@ static void launch_msm_buckets(const MsmPlan& p, const uint32_t* points, const u
              p.chunk_bkt, p.sorted, p.partials);
   // expected nonzero digits: N * nw * (1 - 2^-c) ~ N * nw mixed additions
   tl->mark("k_msm_chunks", s, (double)p.NV * p.nw * (COST_MADD + 0.5));
-  FTS_LAUNCH(k_msm_bucket_sum, p.NB, g_lat_bs, s, p.NB, p.counts, p.chunk_off, p.partials, p.buckets);
+  FTS_LAUNCH(k_msm_bucket_sum, p.NB, g_lat_bs, s, p.NB, p.ch, p.counts, p.chunk_off, p.partials, p.buckets);
   tl->mark("k_msm_bucket_sum", s, 0);
 }
 
