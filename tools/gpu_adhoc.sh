@@ -1,13 +1,21 @@
-# ad-hoc GPU step: per-plan MSM chunk size (tests, MSM 2^22, lone batch, headline)
+# ad-hoc GPU step: identity pairing memory traffic (PMC) and in-flight scaling
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r03h; mkdir -p $O
-timeout -k 10 500 python3 -u -m pytest tests/test_gpu_msm.py tests/test_gpu_rp.py tests/test_gpu_scale.py tests/test_gpu_headline.py tests/test_gpu_actions.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pt.log 2>&1 || { tail -40 $O/pt.log; exit 1; }
-tail -1 $O/pt.log
-timeout -k 10 300 python3 -u bench.py --workload msm --msm-log 22 --steps 16 --warmup 2 --cpu-sample 0 > $O/msm22.log 2>&1 || { tail $O/msm22.log; exit 1; }
-grep '^{' $O/msm22.log | tail -1 | python3 -c "import json,sys; d=json.load(sys.stdin); print('msm22', d['value'], d['ms_per_step'], d['kernel_ms'])"
-timeout -k 10 100 python3 tools/pass_times.py 4096 81920 > $O/pass.log 2>&1 && cat $O/pass.log | cut -c1-600 || exit 1
-timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --cpu-sample 0 > $O/s20.log 2>&1 || { tail $O/s20.log; exit 1; }
-grep '^{' $O/s20.log | tail -1 | python3 -c "import json,sys; d=json.load(sys.stdin); print('s20', d['value'], d['isolated_batch']['ms'], d['isolated_pass']['ms'])"
-timeout -k 10 300 python3 -u bench.py --steps 512 --warmup 64 --cpu-sample 0 > $O/s512.log 2>&1 || { tail $O/s512.log; exit 1; }
-grep '^{' $O/s512.log | tail -1 | python3 -c "import json,sys; d=json.load(sys.stdin); print('s512', d['value'])"
+O=gpurun_out/r03i; mkdir -p $O; rm -rf $O/pf $O/pw
+B="python3 bench.py --workload identity --steps 2 --warmup 1 --cpu-sample 0"
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -T -f csv -d $O/pf -o run -- $B > $O/pf.log 2>&1 || { tail $O/pf.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -T -f csv -d $O/pw -o run -- $B > $O/pw.log 2>&1 || { tail $O/pw.log; exit 1; }
+python3 - <<'PY'
+import csv, glob, collections
+for tag in ("pf", "pw"):
+    f = glob.glob("gpurun_out/r03i/%s/**/*counter_collection.csv" % tag, recursive=True)[0]
+    acc = collections.defaultdict(list)
+    for r in csv.DictReader(open(f)):
+        acc[(r["Kernel_Name"].split("(")[0][-30:], r["Counter_Name"])].append(float(r["Counter_Value"]))
+    for (k, c), v in sorted(acc.items()):
+        if "idv" in k: print(tag, k, c, "per dispatch avg %.3e" % (sum(v) / len(v)), "n", len(v))
+PY
+for f in 1 3 6; do
+  timeout -k 10 200 python3 bench.py --workload identity --steps 12 --warmup 2 --cpu-sample 0 --action-inflight $f > $O/if$f.log 2>&1 || { tail $O/if$f.log; exit 1; }
+  grep '^{' $O/if$f.log | tail -1 | python3 -c "import json,sys; d=json.load(sys.stdin); print('inflight $f', d['value'], d['ms_per_step'], d['kernel_ms'])"
+done
