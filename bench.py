@@ -24,6 +24,7 @@ Prints one JSON line (rank 0).  Usage:
   torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
+import ctypes
 import json
 import os
 
@@ -165,6 +166,9 @@ def main():
                          "tampered proofs exercises the group-test fallback); verdicts are checked every step")
     ap.add_argument("--cpu-sample", type=int, default=256, help="CPU baseline chunk size (0: skip the CPU baseline)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--host-steps", type=int, default=32,
+                    help="rp workload: calls of fts_rp_verify_batch from host DER bytes after the timed region "
+                         "(the PCIe-inclusive rate, reported apart; 0: skip)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall-time bound of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     ap.add_argument("--workload", choices=["rp", "msm", "transfer", "mixed", "request", "audit", "prove", "ecdsa",
@@ -393,6 +397,32 @@ def main():
                 "pipeline_frac_own_model": round(value / world * own_mads / (PEAK_TMAD * 1e12), 4)}
     longest_kernel = kernel_roof(longest)
 
+    # the drop-in boundary from host buffers, after the timed region: DER bytes in
+    # (fts_rp_verify_batch: host parse + upload + verify + verdicts back), the
+    # PCIe-inclusive rate a Go caller without staged batches sees; not `value`
+    host_inclusive = None
+    if rank == 0 and args.host_steps > 0:
+        from fts_gpu import _lib as FL, _ptr_array
+        _bufs, ptrs, lens = _ptr_array(proofs0)
+        comsb = b"".join(coms0)
+
+        class HostStep:
+            @staticmethod
+            def verify():
+                st = np.zeros(B, dtype=np.int32)
+                FL.check("fts_rp_verify_batch", FL.lib.fts_rp_verify_batch(
+                    pp._ctx, B, ptrs, lens, comsb, st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+                assert (st == wants[0]).all()
+                return st
+        hs = [HostStep() for _ in range(min(8, args.host_steps))]
+        _run_action_steps(hs, len(hs), None, None)  # warm the host pool
+        h_el, _ = _run_action_steps(hs, args.host_steps, None, None)
+        host_inclusive = {"value": round(B * args.host_steps / h_el, 1), "unit": "verifies/s",
+                          "ms_per_step": round(h_el / args.host_steps * 1e3, 4), "steps": args.host_steps,
+                          "inflight": len(hs),
+                          "note": "fts_rp_verify_batch from host DER bytes (parse + H2D + verify + D2H), %d calls "
+                                  "from %d host threads, after the timed region" % (args.host_steps, len(hs))}
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         # bounded samples of the same proofs: one core, then --cpu-threads cores
@@ -445,6 +475,7 @@ def main():
                                "roofline_frac": round(kt1[dom1][1] / (avg1[dom1] * 1e-3) / 1e12 / PEAK_TMAD, 4)
                                if avg1.get(dom1) else None},
             "isolated_pass": {"proofs": m * B, "ms": round(pass_ms, 3), "verifies_per_s": round(m * B / pass_ms * 1e3, 1)},
+            "host_inclusive": host_inclusive,
             "roofline": roofline,
             "longest_kernel": longest_kernel,
             "cpu_baseline": cpu,
