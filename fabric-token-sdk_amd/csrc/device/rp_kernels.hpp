@@ -190,7 +190,11 @@ struct RpBatchDev {
   int32_t* excl = nullptr;       // [B] optional: 1 = left out of the batch check (set by the pre_rlc hook), NOT_RUN
   int com_split = 0;             // work path: x*D on the side stream from the challenges (k_rp_xd), the
                                  //    com chain then runs z^2*S alone (k_rp_com_s); 0: joint chain (k_rp_com_var)
-  hipEvent_t ev_xd = nullptr;    // recorded on s2 after k_rp_xd (com_split)
+  hipEvent_t ev_xd = nullptr;    // recorded on s2 after k_rp_xd (com_split, lat_order bit 2)
+  int lat_order = 0;             // latency path (com_fixed) launch order: bits 0-1 = MSM stage (1: counting
+                                 //    sort, 2: bucket accumulation) k_rp_fixed_all waits for; bit 2 = x0
+                                 //    prefix on s2 after k_rp_xd (needs x0_mid)
+  hipEvent_t ev_msm = nullptr;   // recorded on the check's stream at that MSM stage
 };
 
 }  // namespace fts

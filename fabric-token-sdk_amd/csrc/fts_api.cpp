@@ -51,8 +51,11 @@ void launch_rlc_group_test(const RpBatchDev& d, const RlcDev& r, const uint32_t*
                            const int32_t* sel, int G, int gs, uint32_t* gcol, uint32_t* gfix, int32_t* next,
                            uint32_t* next_count, hipStream_t s, Timeline* tl);
 void launch_rp_gather(const RpGather& g, int k, uint8_t* raw, uint32_t* sc, int32_t* status, int32_t* ipa, hipStream_t s);
+// ev_stage (optional): recorded on s after the counting sort (stage 1) or the bucket
+// accumulation (stage 2)
 void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
-                uint32_t* scratch, hipStream_t s, hipStream_t s_extra, Timeline* tl);
+                uint32_t* scratch, hipStream_t s, hipStream_t s_extra, Timeline* tl, hipEvent_t ev_stage = nullptr,
+                int stage = 0);
 void launch_msm_load(int N, const uint8_t* raw_pts, const uint8_t* raw_sc, uint32_t* pts, uint32_t* sc, uint32_t* bad,
                      hipStream_t s);
 void launch_msm_to_bytes(const uint32_t* jac, uint8_t* out, hipStream_t s);
@@ -192,7 +195,7 @@ struct Lane {
   hipStream_t s = nullptr, s2 = nullptr;
   hipStream_t s3 = nullptr;         // sigma proofs of action batches (beside the range-proof pass)
   hipStream_t s4 = nullptr;         // latency path: the x0 transcript prefix beside the x*D chain
-  hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr, ev_d = nullptr;  // cross-stream ordering (no timing)
+  hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr, ev_d = nullptr, ev_e = nullptr;  // cross-stream ordering (no timing)
   Workspace ws;
   Timeline tl;
   float host_prep_ms = 0, host_enqueue_ms = 0, host_wait_ms = 0;  // host wall time of the last run
@@ -404,6 +407,10 @@ struct fts_ctx {
   // latency whatever their number up to ~8k proofs (tools/gt_sweep.sh, C5 1 % tampered:
   // 64/2048 -> 256/8192 = 485k -> 533k actions/s)
   int gt1 = 256, gt2_min = 8192;
+  // FTS_LAT_ORDER: latency-path launch order (RpBatchDev::lat_order).  5 = the MSM's
+  // digits / sort before k_rp_fixed_all + the x0 prefix behind k_rp_xd: lone
+  // 4,096-proof batch 2.82 vs 2.88 ms (3 A/B pairs, tools/sweeps/lat_ab.txt)
+  int lat_order = 5;
   int x0_split = 1;                 // FTS_X0_SPLIT: work path hashes the x0 prefix beside the com chain
   int com_split = 0;                // FTS_COM_SPLIT: work path computes x*D beside the exact phase (k_rp_xd)
   int idle_gather_us = 0;           // FTS_IDLE_GATHER_US: gather window on an idle device (0: start at once)
@@ -532,6 +539,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
       if (L->ev_b) hipEventDestroy(L->ev_b);
       if (L->ev_c) hipEventDestroy(L->ev_c);
       if (L->ev_d) hipEventDestroy(L->ev_d);
+      if (L->ev_e) hipEventDestroy(L->ev_e);
       if (L->s2 && L->s2 != L->s) hipStreamDestroy(L->s2);
       if (L->s4 && L->s4 != L->s) hipStreamDestroy(L->s4);
       if (L->s) hipStreamDestroy(L->s);
@@ -554,6 +562,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_COM_FIXED_MAX")) c->com_fixed_max = (size_t)std::max(0L, atol(e));
   if (const char* e = getenv("FTS_RLC_FORK")) c->rlc_fork = std::max(0, std::min(2, atoi(e)));
   if (const char* e = getenv("FTS_X0_SPLIT")) c->x0_split = atoi(e) != 0;
+  if (const char* e = getenv("FTS_LAT_ORDER")) c->lat_order = atoi(e) & 7;
   if (const char* e = getenv("FTS_COM_SPLIT")) c->com_split = atoi(e) != 0;
   if (const char* e = getenv("FTS_IDLE_GATHER_US")) c->idle_gather_us = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_SPLIT")) c->split = atoi(e) != 0;
@@ -617,7 +626,8 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
         hipEventCreateWithFlags(&L->ev_a, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&L->ev_b, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&L->ev_c, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&L->ev_d, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&L->ev_d, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&L->ev_e, hipEventDisableTiming) != hipSuccess)
       return fail(FTS_API_EDEVICE);
     L->tl.create();
   }
@@ -701,8 +711,20 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (hipMalloc(&c->d_x0const, xc.size()) != hipSuccess) return fail(FTS_API_ENOMEM);
   hipMemcpyAsync(c->d_x0const, xc.data(), xc.size(), hipMemcpyHostToDevice, s0);
   // block-aligned template of the fully constant SHA-256 blocks of the x0 message
-  std::string xt(64u * (x0_cb1(n) - x0_cb0(n)), '\0');
-  for (size_t j = 0; j < xt.size(); j++) xt[j] = xc[64u * x0_cb0(n) + j - x0_const_off(n)];
+  // followed by each block's expanded schedule K[i] + W[i] (64 words per block,
+  // sha256_compress_kw)
+  const size_t ncb = x0_cb1(n) - x0_cb0(n);
+  std::string xt(64u * ncb + 256u * ncb, '\0');
+  for (size_t j = 0; j < 64u * ncb; j++) xt[j] = xc[64u * x0_cb0(n) + j - x0_const_off(n)];
+  for (size_t blk = 0; blk < ncb; blk++) {
+    uint32_t w[16], kw[64];
+    for (int i = 0; i < 16; i++) {
+      const uint8_t* q = reinterpret_cast<const uint8_t*>(xt.data()) + 64u * blk + 4 * i;
+      w[i] = (uint32_t)q[0] << 24 | (uint32_t)q[1] << 16 | (uint32_t)q[2] << 8 | q[3];
+    }
+    sha256_expand_kw(w, kw);
+    memcpy(&xt[64u * ncb + 256u * blk], kw, sizeof kw);
+  }
   if (hipMalloc(&c->d_x0tmpl, xt.size()) != hipSuccess) return fail(FTS_API_ENOMEM);
   hipMemcpyAsync(c->d_x0tmpl, xt.data(), xt.size(), hipMemcpyHostToDevice, s0);
   hipError_t e = hipStreamSynchronize(s0);
@@ -855,6 +877,7 @@ void fts_ctx_destroy(fts_ctx* c) {
     if (L->ev_b) hipEventDestroy(L->ev_b);
     if (L->ev_c) hipEventDestroy(L->ev_c);
     if (L->ev_d) hipEventDestroy(L->ev_d);
+    if (L->ev_e) hipEventDestroy(L->ev_e);
     L->tl.destroy();
     if (L->done) hipEventDestroy(L->done);
     if (L->s2 && L->s2 != L->s) hipStreamDestroy(L->s2);
@@ -1193,10 +1216,12 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   d.pre_rlc_arg = pre_rlc_arg;
   d.rlc_fork = c->rlc_fork == 2 ? (d.com_fixed ? 0 : 1) : c->rlc_fork;
   d.ev_coef = L.ev_c;
-  // x0 prefix beside the com chain: work path only.  On the latency path the
-  // prefix hash shares CUs with com_tree and the MSM's chunks and delays both
-  // (lone 4,096-proof batch: 3.51 ms with it, 3.06 ms without, one box)
-  d.x0_mid = c->x0_split && !d.com_fixed ? w.x0mid.as<uint32_t>() : nullptr;
+  // x0 prefix beside the com chain on the work path; on the latency path only
+  // queued behind k_rp_xd (lat_order bit 2): started beside com_tree it shared
+  // CUs with it and the MSM's chunks and delayed both (3.51 vs 3.06 ms, round 2)
+  d.lat_order = d.com_fixed ? c->lat_order : 0;
+  d.x0_mid = c->x0_split && (!d.com_fixed || (d.lat_order & 4)) ? w.x0mid.as<uint32_t>() : nullptr;
+  d.ev_msm = L.ev_e;
   d.com_split = c->com_split && !d.com_fixed;
   d.ev_xd = L.ev_d;
   d.excl = pre_rlc ? w.rp_excl.as<int32_t>() : nullptr;

@@ -455,7 +455,7 @@ __global__ void k_msm_to_bytes(const uint32_t* __restrict__ jac, uint8_t* __rest
 // before the window reduction that sums it.
 // digits, counting sort, chunked bucket accumulation and bucket sums (every plan)
 static void launch_msm_buckets(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, hipStream_t s,
-                               Timeline* tl) {
+                               Timeline* tl, hipEvent_t ev_stage = nullptr, int stage = 0) {
   (void)hipMemsetAsync(p.counts, 0, (size_t)p.NB * 4, s);
   FTS_LAUNCH(k_msm_digits, p.N, 256, s, msm_idx(p), p.d_win, scalars, p.keys, p.cursor, p.counts);
   tl->mark("k_msm_digits", s, 0);
@@ -465,18 +465,20 @@ static void launch_msm_buckets(const MsmPlan& p, const uint32_t* points, const u
   tl->mark("k_msm_scan", s, 0);
   FTS_LAUNCH(k_msm_scatter, p.NV, 256, s, p.NV, p.nw, p.keys, p.cursor, p.offsets, p.sorted);
   tl->mark("k_msm_scatter", s, 0);
+  if (ev_stage && stage == 1) (void)hipEventRecord(ev_stage, s);
   FTS_LAUNCH(k_msm_chunks, p.NC, 64, s, msm_idx(p), p.scratch + 2 * (size_t)p.NBLK + 1, p.d_win, points, p.offsets,
              p.counts, p.chunk_off,
              p.chunk_bkt, p.sorted, p.partials);
   // expected nonzero digits: N * nw * (1 - 2^-c) ~ N * nw mixed additions
   tl->mark("k_msm_chunks", s, (double)p.NV * p.nw * (COST_MADD + 0.5));
+  if (ev_stage && stage == 2) (void)hipEventRecord(ev_stage, s);
   FTS_LAUNCH(k_msm_bucket_sum, p.NB, g_lat_bs, s, p.NB, p.ch, p.counts, p.chunk_off, p.partials, p.buckets);
   tl->mark("k_msm_bucket_sum", s, 0);
 }
 
 void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
-                uint32_t* scratch, hipStream_t s, hipStream_t s_extra, Timeline* tl) {
-  launch_msm_buckets(p, points, scalars, s, tl);
+                uint32_t* scratch, hipStream_t s, hipStream_t s_extra, Timeline* tl, hipEvent_t ev_stage, int stage) {
+  launch_msm_buckets(p, points, scalars, s, tl, ev_stage, stage);
   FTS_LAUNCH(k_msm_segments, p.NS, g_lat_bs, s, p.nw, p.NS, p.NSg, p.NBg, p.d_win, p.buckets, p.segs, scratch);
   tl->mark("k_msm_segments", s, (double)p.NB * 2 * COST_ADD);
   if (s_extra != s) tl->fork(s_extra, s);

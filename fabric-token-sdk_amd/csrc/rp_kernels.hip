@@ -885,7 +885,6 @@ __global__ void __launch_bounds__(256) k_rp_x0_hash(int B, int n, int k, const i
   const uint32_t cb0 = x0_cb0(n), cb1 = x0_cb1(n), nb = sha_blocks(x0_msg_len(n));
   const uint32_t hi = b1 < nb ? b1 : nb;
   const uint4* own = reinterpret_cast<const uint4*>(msgs + (size_t)b * x0_var_bytes(n));
-  const uint4* shared = reinterpret_cast<const uint4*>(tmpl);
   uint32_t st[8];
   if (b0 == 0) {
     sha256_init(st);
@@ -893,8 +892,14 @@ __global__ void __launch_bounds__(256) k_rp_x0_hash(int B, int n, int k, const i
 #pragma unroll
     for (int i = 0; i < 8; i++) st[i] = mid[(size_t)b * 8 + i];
   }
+  // template blocks [cb0, cb1): pre-expanded schedules after the template bytes
+  const uint32_t* kw = reinterpret_cast<const uint32_t*>(tmpl + 64u * (cb1 - cb0));
   for (uint32_t blk = b0; blk < hi; blk++) {
-    const uint4* m = blk < cb0 ? own + 4u * blk : blk < cb1 ? shared + 4u * (blk - cb0) : own + 4u * (blk - (cb1 - cb0));
+    if (blk >= cb0 && blk < cb1) {
+      sha256_compress_kw(st, kw + 64u * (blk - cb0));
+      continue;
+    }
+    const uint4* m = blk < cb0 ? own + 4u * blk : own + 4u * (blk - (cb1 - cb0));
     uint32_t w[16];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -1518,8 +1523,11 @@ void launch_build_wide_tables(const uint32_t* bases, int nb, uint32_t* tables, u
   build_tables<FBW_W>(bases, nb, tables, scratch, s);
 }
 
+// ev_stage (optional): recorded on s after the counting sort (stage 1) or the bucket
+// accumulation (stage 2)
 void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
-                uint32_t* scratch, hipStream_t s, hipStream_t s_extra, Timeline* tl);
+                uint32_t* scratch, hipStream_t s, hipStream_t s_extra, Timeline* tl, hipEvent_t ev_stage = nullptr,
+                int stage = 0);
 void launch_msm_small(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra,
                       int nextra, hipStream_t s, Timeline* tl);
 
@@ -1546,6 +1554,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     FTS_LAUNCH(k_rp_xd, 2 * B, g_lat_bs, s2, B, n, k, d.status, d.pts, d.small_msgs, d.scratch + (size_t)B * (k + 1) * 8,
                d.terms, com_fx_slots(n), n + 2);
     tl->mark("k_rp_xd", s2, (double)B * 2 * COST_VB128);
+    if (d.lat_order & 4) (void)hipEventRecord(d.ev_xd, s2);
   } else if (d.com_split) {
     // work path, split com: x*D (terms[b][2 + h]) beside the exact phase from the
     // x digest on; lane tables past the S chunks and the com lanes' tables
@@ -1580,7 +1589,8 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     tl->mark("k_rlc_columns", s4, (double)B * 4 * n);
     FTS_LAUNCH(k_rlc_fixed, (size_t)(NC - 1) * FB_NW, RF_ITEMS * FB_NW, s4, n, 1, 0, NC - 1, r.colsum, tables, r.fixed);
     tl->mark("k_rlc_fixed", s4, (double)(NC - 1) * (FB_NW * 3 + (FB_NW - 1) * COST_ADD));
-    launch_msm(r.plan, d.pts, r.msc, r.fixed, NC - 1, r.msm_scratch, s3, s4, tl);
+    launch_msm(r.plan, d.pts, r.msc, r.fixed, NC - 1, r.msm_scratch, s3, s4, tl, d.com_fixed ? d.ev_msm : nullptr,
+               d.com_fixed ? (d.lat_order & 3) : 0);
   };
   if (!d.rlc_fork) rlc_prep();
   FTS_LAUNCH(k_rp_powers, B * (n >> std::min(PW_LC, k)), 64, s, B, n, k, d.status, d.ch, d.ypow, d.svec, d.zvec);
@@ -1592,23 +1602,31 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   if (!d.rlc_fork) rlc_side();
   // exact per-proof phase on s
   if (d.com_fixed) {
+    // lat_order & 3: the MSM's digit / sort launches are short but latency-bound;
+    // sharing the CUs with k_rp_fixed_all stretches them ~6x, so they may go first
+    if ((d.lat_order & 3) && d.ev_msm) (void)hipStreamWaitEvent(s, d.ev_msm, 0);
     FTS_LAUNCH(k_rp_fixed_all, (size_t)B * (2 * n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, d.zvec, wtables,
                d.hpj, d.terms);
     tl->mark("k_rp_fixed_all", s, (double)B * (2.0 * n + 2.0) * COST_FBW_FRESH);
     if (d.rlc_fork) rlc_side();
     launch_normalize(nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be, s);
     tl->mark("k_rp_normalize", s, (double)nhp * (2.0 * 8.0 / NORM_E + 9.0));
+    // x0 prefix (H' records + shared template: all but the last 3 blocks): on s2
+    // queued behind k_rp_xd (lat_order bit 2; com_tree waits for x*D alone), else
+    // on s4 beside the x*D chain; only the suffix waits for com
+    hipStream_t xs = (d.lat_order & 4) ? s2 : s4;
     if (d.x0_mid) {
-      // x0 prefix (H' records + shared template: all but the last 3 blocks) on s4,
-      // beside the x*D chain still running on s2: only the suffix waits for com
-      tl->fork(s, s4);
-      hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s4, B, n, d.status, d.hp_be, x0_const,
+      tl->fork(s, xs);
+      hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), xs, B, n, d.status, d.hp_be, x0_const,
                          d.sc, d.x0_msgs, 0);
-      tl->mark("k_rp_x0_build", s4, 0);
-      FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s4, B, n, k, d.status, d.x0_msgs, x0_tmpl, 0u, x0_cb1(n), d.x0_mid, d.ch);
-      tl->mark("k_rp_x0_prefix", s4, 0);
+      tl->mark("k_rp_x0_build", xs, 0);
+      FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, xs, B, n, k, d.status, d.x0_msgs, x0_tmpl, 0u, x0_cb1(n), d.x0_mid, d.ch);
+      tl->mark("k_rp_x0_prefix", xs, 0);
     }
-    tl->fork(s2, s);
+    if (d.lat_order & 4)
+      (void)hipStreamWaitEvent(s, d.ev_xd, 0);
+    else
+      tl->fork(s2, s);
     hipLaunchKernelGGL(k_rp_com_tree, dim3((B + CT_PROOFS - 1) / CT_PROOFS), dim3(CT_LANES * CT_PROOFS), 0, s, B, n,
                        k, d.status, d.pts, d.terms, d.hpj);
     tl->mark("k_rp_com_sum", s, (double)B * (com_fx_slots(n) + 1) * COST_ADD);
@@ -1654,7 +1672,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s, B, n, d.status, d.hp_be, x0_const, d.sc,
                      d.x0_msgs, split ? 1 : 2);
   tl->mark(split ? "k_rp_x0_build_tail" : "k_rp_x0_build", s, 0);
-  if (split) tl->fork(d.com_fixed ? s4 : s2, s);  // the prefix's midstate
+  if (split) tl->fork(d.com_fixed && !(d.lat_order & 4) ? s4 : s2, s);  // the prefix's midstate
   FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s, B, n, k, d.status, d.x0_msgs, x0_tmpl, split ? x0_cb1(n) : 0u, 0xffffffffu,
              d.x0_mid, d.ch);
   tl->mark("k_rp_x0_hash", s, 0);
