@@ -87,33 +87,6 @@ FTS_HD void sha256_compress(uint32_t st[8], uint32_t w[16]) {
   st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
-// A block whose 16 words are known ahead (the x0 transcript's constant
-// template blocks) can have its schedule expanded once: kw[i] = K[i] + W[i].
-FTS_HD void sha256_expand_kw(const uint32_t w16[16], uint32_t kw[64]) {
-  uint32_t w[64];
-  for (int i = 0; i < 16; i++) w[i] = w16[i];
-  for (int i = 16; i < 64; i++) {
-    uint32_t s0 = sha_rotr(w[i - 15], 7) ^ sha_rotr(w[i - 15], 18) ^ (w[i - 15] >> 3);
-    uint32_t s1 = sha_rotr(w[i - 2], 17) ^ sha_rotr(w[i - 2], 19) ^ (w[i - 2] >> 10);
-    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
-  }
-  for (int i = 0; i < 64; i++) kw[i] = Sha256Const::K[i] + w[i];
-}
-// compression with a pre-expanded schedule (no message expansion: ~27 % fewer
-// instructions per block); kw is uniform across the wave (scalar loads)
-FTS_HD void sha256_compress_kw(uint32_t st[8], const uint32_t* __restrict__ kw) {
-  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-#pragma unroll
-  for (int i = 0; i < 64; i++) {
-    uint32_t S1 = sha_xor3(sha_rotr(e, 6), sha_rotr(e, 11), sha_rotr(e, 25));
-    uint32_t t1 = h + S1 + sha_ch(e, f, g) + kw[i];
-    uint32_t S0 = sha_xor3(sha_rotr(a, 2), sha_rotr(a, 13), sha_rotr(a, 22));
-    uint32_t t2 = S0 + sha_maj(a, b, c);
-    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
-  }
-  st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
-}
-
 // Byte-streaming context (host side and small device transcripts).
 struct Sha256 {
   uint32_t st[8];

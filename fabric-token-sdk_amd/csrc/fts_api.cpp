@@ -711,20 +711,8 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (hipMalloc(&c->d_x0const, xc.size()) != hipSuccess) return fail(FTS_API_ENOMEM);
   hipMemcpyAsync(c->d_x0const, xc.data(), xc.size(), hipMemcpyHostToDevice, s0);
   // block-aligned template of the fully constant SHA-256 blocks of the x0 message
-  // followed by each block's expanded schedule K[i] + W[i] (64 words per block,
-  // sha256_compress_kw)
-  const size_t ncb = x0_cb1(n) - x0_cb0(n);
-  std::string xt(64u * ncb + 256u * ncb, '\0');
-  for (size_t j = 0; j < 64u * ncb; j++) xt[j] = xc[64u * x0_cb0(n) + j - x0_const_off(n)];
-  for (size_t blk = 0; blk < ncb; blk++) {
-    uint32_t w[16], kw[64];
-    for (int i = 0; i < 16; i++) {
-      const uint8_t* q = reinterpret_cast<const uint8_t*>(xt.data()) + 64u * blk + 4 * i;
-      w[i] = (uint32_t)q[0] << 24 | (uint32_t)q[1] << 16 | (uint32_t)q[2] << 8 | q[3];
-    }
-    sha256_expand_kw(w, kw);
-    memcpy(&xt[64u * ncb + 256u * blk], kw, sizeof kw);
-  }
+  std::string xt(64u * (x0_cb1(n) - x0_cb0(n)), '\0');
+  for (size_t j = 0; j < xt.size(); j++) xt[j] = xc[64u * x0_cb0(n) + j - x0_const_off(n)];
   if (hipMalloc(&c->d_x0tmpl, xt.size()) != hipSuccess) return fail(FTS_API_ENOMEM);
   hipMemcpyAsync(c->d_x0tmpl, xt.data(), xt.size(), hipMemcpyHostToDevice, s0);
   hipError_t e = hipStreamSynchronize(s0);

@@ -892,22 +892,32 @@ __global__ void __launch_bounds__(256) k_rp_x0_hash(int B, int n, int k, const i
 #pragma unroll
     for (int i = 0; i < 8; i++) st[i] = mid[(size_t)b * 8 + i];
   }
-  // template blocks [cb0, cb1): pre-expanded schedules after the template bytes
-  const uint32_t* kw = reinterpret_cast<const uint32_t*>(tmpl + 64u * (cb1 - cb0));
+  // one block ahead: the next block's 64 bytes are loaded before this block's
+  // 64 rounds, so the load's latency (L2 / HBM, ~1 us under load) is hidden
+  // behind them instead of exposed once per block
+  const uint4* shared = reinterpret_cast<const uint4*>(tmpl);
+  auto block_ptr = [&](uint32_t blk) {
+    return blk < cb0 ? own + 4u * blk : blk < cb1 ? shared + 4u * (blk - cb0) : own + 4u * (blk - (cb1 - cb0));
+  };
+  uint4 nx[4];
+  if (b0 < hi) {
+    const uint4* m = block_ptr(b0);
+#pragma unroll
+    for (int i = 0; i < 4; i++) nx[i] = m[i];
+  }
   for (uint32_t blk = b0; blk < hi; blk++) {
-    if (blk >= cb0 && blk < cb1) {
-      sha256_compress_kw(st, kw + 64u * (blk - cb0));
-      continue;
-    }
-    const uint4* m = blk < cb0 ? own + 4u * blk : own + 4u * (blk - (cb1 - cb0));
     uint32_t w[16];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      uint4 u = m[i];
-      w[4 * i + 0] = __builtin_bswap32(u.x);
-      w[4 * i + 1] = __builtin_bswap32(u.y);
-      w[4 * i + 2] = __builtin_bswap32(u.z);
-      w[4 * i + 3] = __builtin_bswap32(u.w);
+      w[4 * i + 0] = __builtin_bswap32(nx[i].x);
+      w[4 * i + 1] = __builtin_bswap32(nx[i].y);
+      w[4 * i + 2] = __builtin_bswap32(nx[i].z);
+      w[4 * i + 3] = __builtin_bswap32(nx[i].w);
+    }
+    if (blk + 1 < hi) {
+      const uint4* m = block_ptr(blk + 1);
+#pragma unroll
+      for (int i = 0; i < 4; i++) nx[i] = m[i];
     }
     sha256_compress(st, w);
   }
