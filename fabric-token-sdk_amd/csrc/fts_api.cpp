@@ -409,8 +409,10 @@ struct fts_ctx {
   int gt1 = 256, gt2_min = 8192;
   // FTS_LAT_ORDER: latency-path launch order (RpBatchDev::lat_order).  5 = the MSM's
   // digits / sort before k_rp_fixed_all + the x0 prefix behind k_rp_xd: lone
-  // 4,096-proof batch 2.82 vs 2.88 ms (3 A/B pairs, tools/sweeps/lat_ab.txt)
-  int lat_order = 5;
+  // 4,096-proof batch 2.82 vs 2.88 ms in tools/pass_times.py, but 2.83 vs 2.84 ms
+  // in bench.py's isolated batch and a lower 20-step line (3.56 vs 3.74 M/s mean
+  // of 3 alternating runs, tools/sweeps/lat_bench_ab.txt): off by default
+  int lat_order = 0;
   int x0_split = 1;                 // FTS_X0_SPLIT: work path hashes the x0 prefix beside the com chain
   int com_split = 0;                // FTS_COM_SPLIT: work path computes x*D beside the exact phase (k_rp_xd)
   int idle_gather_us = 0;           // FTS_IDLE_GATHER_US: gather window on an idle device (0: start at once)
