@@ -32,10 +32,10 @@ for s in "$@"; do case $s in
   rp) step bench_s20 300 python3 -u bench.py --steps 20 --warmup 5; json bench_s20
       step bench 600 python3 -u bench.py --steps 512 --warmup 64; json bench ;;
   prof) rm -rf $OUT/prof
-        step rocprof 400 rocprofv3 --kernel-trace --stats -T -f csv -d $OUT/prof -o run -- python3 bench.py --steps 256 --warmup 64 --roofline-steps 6 --cpu-sample 0
+        step rocprof 400 rocprofv3 --kernel-trace --stats -T -f csv -d $OUT/prof -o run -- python3 bench.py --steps 256 --warmup 64 --roofline-steps 6 --cpu-sample 0 --host-steps 0
         json rocprof
         python3 tools/prof_summary.py $(find $OUT/prof -name "*kernel_trace.csv" | head -1) 6 $OUT/prof/isolated.json ;;
-  pmc) PB="python3 bench.py --steps 8 --warmup 8 --roofline-steps 2 --cpu-sample 0"
+  pmc) PB="python3 bench.py --steps 8 --warmup 8 --roofline-steps 2 --cpu-sample 0 --host-steps 0"
        rm -rf $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_valu $OUT/pmc_calib
        step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -T -f csv -d $OUT/pmc_fetch -o run -- $PB
        json pmc_fetch
