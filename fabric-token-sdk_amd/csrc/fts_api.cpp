@@ -407,6 +407,15 @@ struct fts_ctx {
   // latency whatever their number up to ~8k proofs (tools/gt_sweep.sh, C5 1 % tampered:
   // 64/2048 -> 256/8192 = 485k -> 533k actions/s)
   int gt1 = 256, gt2_min = 8192;
+  // FTS_GT_ADAPT: round-1 group size follows the bad-proof density of the last
+  // failed pass.  Dense (more than half the proofs in failing 256-groups, or more
+  // than 2 % in failing 8-groups: ~0.3 % bad proofs and up) starts at groups of 8
+  // on the small-group kernels; a 256-group round there is one whole grouped
+  // Pippenger MSM that clears almost nothing (C2 with 1 % tampered, 81,920-proof
+  // pass: 51.8 -> 41.4 ms; C5's sparse bad proofs keep 256, where 8 was slower,
+  // tools/sweeps/gt1_small.txt)
+  int gt_adapt = 1;
+  std::atomic<int> gt_dense{0};
   // FTS_LAT_ORDER: latency-path launch order (RpBatchDev::lat_order).  5 = the MSM's
   // digits / sort before k_rp_fixed_all + the x0 prefix behind k_rp_xd: lone
   // 4,096-proof batch 2.82 vs 2.88 ms in tools/pass_times.py, but 2.83 vs 2.84 ms
@@ -571,6 +580,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_SHALLOW_CAP")) c->shallow_cap = atoi(e) != 0;
   if (const char* e = getenv("FTS_GT1")) c->gt1 = std::max(8, std::min(1024, atoi(e)));
   if (const char* e = getenv("FTS_GT2_MIN")) c->gt2_min = std::max(0, atoi(e));
+  if (const char* e = getenv("FTS_GT_ADAPT")) c->gt_adapt = atoi(e) != 0;
   // process-wide launch knobs of rp_kernels.hip: read once, before any context can
   // launch (contexts are created concurrently by fts_ctx_create_devices, and the
   // launch code of live contexts reads these values)
@@ -1105,7 +1115,9 @@ static int lane_reserve(fts_ctx* c, Lane& L, int B, bool inputs) {
 constexpr int RP_GT2 = 8;
 static int rp_group_fallback(fts_ctx* c, Lane& L, const RpBatchDev& d, const RlcDev& r,
                              const std::vector<int>& groups) {
-  const int RP_GT1 = c->gt1, RP_GT2_MIN = c->gt2_min;
+  const bool adapt = c->gt_adapt && c->gt1 > RP_GT2;
+  const int RP_GT1 = adapt && c->gt_dense.load(std::memory_order_relaxed) ? RP_GT2 : c->gt1;
+  const int RP_GT2_MIN = c->gt2_min;
   const int B = d.B, n = d.n, npts = rp_npts(d.k);
   Workspace& w = L.ws;
   L.tl.fallback();
@@ -1142,12 +1154,14 @@ static int rp_group_fallback(fts_ctx* c, Lane& L, const RpBatchDev& d, const Rlc
     HIP_OK(hipMemcpyAsync(&L.pin->flag, cnt, 4, hipMemcpyDeviceToHost, L.s));
     HIP_OK(L.sync());
     const int nfail = L.pin->flag;
+    if (round == 0 && adapt)
+      c->gt_dense.store(gs == RP_GT2 ? nfail > 0.02 * B : nfail > 0.5 * B, std::memory_order_relaxed);
     if (nfail == 0) return FTS_API_OK;
     std::swap(cur, nxt);
     // per-proof checks of what is left; a second group test only pays when round 1
     // left many proofs (the per-proof check's latency is one GLV chain whatever
     // their number, its work grows with it)
-    if (round == 1 || nfail <= RP_GT2_MIN) {
+    if (round == 1 || gs <= RP_GT2 || nfail <= RP_GT2_MIN) {
       launch_rp_fallback(d, c->d_tables, cur, nfail, L.s, &L.tl);
       HIP_OK(hipGetLastError());
       return FTS_API_OK;
