@@ -294,3 +294,64 @@ def test_group_test_round2_exact_verdicts(pp_raw):
     for b in batches + [blocker]:
         b.close()
     pp.close()
+
+
+def test_group_test_adaptive_dense_exact_verdicts(pp_raw):
+    """fts_api.cpp rp_group_fallback, FTS_GT_ADAPT (default on): after a failed
+    pass whose bad proofs were dense (more than half the proofs in failing
+    256-groups) the context starts the next fallback at groups of 8 on the
+    small-group kernels, with no second round.  One caller batch of 512 rp16
+    proofs, 16 of them tampered (every 32nd: both 256-groups fail), verified
+    twice on one lane: both calls must give the oracle's verdicts; the first
+    runs the 256-group kernels, the second only the small-group ones and sends
+    at most the 16 failing 8-groups to the per-proof stage."""
+    import os
+
+    import fts_gpu
+
+    saved = {k: os.environ.get(k) for k in ("FTS_LANES", "FTS_GT1", "FTS_GT2_MIN", "FTS_GT_ADAPT")}
+    for k in ("FTS_GT1", "FTS_GT2_MIN", "FTS_GT_ADAPT"):
+        os.environ.pop(k, None)
+    os.environ["FTS_LANES"] = "1"
+    try:
+        pp = fts_gpu.PublicParams(pp_raw, bit_length=16, device=0)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    from oracle import pp as oppm
+    opp = oppm.load_pp(pp_raw).with_bit_length(16)
+    rng = random.Random(0xAD4F7)
+    m = 512
+    vals = [rng.getrandbits(16) for _ in range(m)]
+    bfs = [rng.randrange(bn.R).to_bytes(32, "big") for _ in range(m)]
+    proofs, coms = pp.prove_range_batch_gpu(vals, bfs, seed=9300)
+    expect = [0] * m
+    for i in range(7, m, 32):
+        r = zkat.RangeProof.deserialize(proofs[i])
+        if (i // 32) % 2:
+            r.data.T1 = bn.g1_add(r.data.T1, bn.GEN)
+        else:
+            j = rng.randrange(4)
+            r.ipa.L[j] = bn.g1_add(r.ipa.L[j], bn.GEN)
+        proofs[i] = r.serialize()
+        err = zkat.rp_verify(bn.g1_from_bytes(coms[i]), opp.ped[1:], opp.left, opp.right, opp.P, opp.Q,
+                             opp.rounds, 16, zkat.RangeProof.deserialize(proofs[i]))
+        assert err is not None
+        expect[i] = fts_gpu.FTS_E_RP_INVALID if "IPA" not in err else fts_gpu.FTS_E_IPA_INVALID
+    batch = pp.stage_range_proofs(proofs, coms)
+    runs = []
+    for _ in range(2):
+        out = [int(s) for s in batch.verify()]
+        assert out == expect, {i: (out[i], expect[i]) for i in range(m) if out[i] != expect[i]}
+        runs.append(_raw_timing_names(batch))
+    (n1, _), (n2, w2) = runs
+    assert "fb:k_rlc_group_columns" in n1 and n1.count("fb:k_rlc_group_final") == 1, n1
+    assert "fb:k_rlc_group_columns" not in n2 and "fb:k_rlc_group_cols" in n2, n2
+    assert n2.count("fb:k_rlc_group_final") == 1, n2   # groups of 8, no second round
+    per_proof = w2["fb:k_rp_terms_fixed"] / ((3 + 2 * 16) * 15 * 11 * 136)
+    assert 1 <= round(per_proof) <= 8 * 16, per_proof
+    batch.close()
+    pp.close()
