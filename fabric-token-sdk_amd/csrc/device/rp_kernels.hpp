@@ -72,9 +72,6 @@ constexpr double COST_STRAUS2 = 2.0 * (7.0 + 6.0 * COST_ADD) + 124.0 * COST_DBL 
 // doublings and ~60 mixed additions
 constexpr double COST_STRAUS2_ATAB = (COST_DBL + 6.0 * COST_MADD) + (COST_DBL + 6.0 * COST_ADD) + 109.0 +
                                      124.0 * COST_DBL + 60.0 * COST_MADD;
-// straus1_atab (split com, k_rp_com_s): 1..8 S (Jacobian), 8-entry normalisation,
-// 124 doublings, ~30 mixed additions
-constexpr double COST_STRAUS1_ATAB = (COST_DBL + 6.0 * COST_ADD) + 55.0 + 124.0 * COST_DBL + 30.0 * COST_MADD;
 constexpr double COST_NORM = 7.0;
      // batched affine normalisation, per point
 
@@ -188,13 +185,6 @@ struct RpBatchDev {
   hipEvent_t ev_coef = nullptr;  // recorded on the check's stream after k_rlc_prep (column Q on s waits for it)
   uint32_t* x0_mid = nullptr;    // [B][8] SHA-256 midstate of the x0 prefix (work path; nullptr: one-piece hash)
   int32_t* excl = nullptr;       // [B] optional: 1 = left out of the batch check (set by the pre_rlc hook), NOT_RUN
-  int com_split = 0;             // work path: x*D on the side stream from the challenges (k_rp_xd), the
-                                 //    com chain then runs z^2*S alone (k_rp_com_s); 0: joint chain (k_rp_com_var)
-  hipEvent_t ev_xd = nullptr;    // recorded on s2 after k_rp_xd (com_split, lat_order bit 2)
-  int lat_order = 0;             // latency path (com_fixed) launch order: bits 0-1 = MSM stage (1: counting
-                                 //    sort, 2: bucket accumulation) k_rp_fixed_all waits for; bit 2 = x0
-                                 //    prefix on s2 after k_rp_xd (needs x0_mid)
-  hipEvent_t ev_msm = nullptr;   // recorded on the check's stream at that MSM stage
 };
 
 }  // namespace fts

@@ -61,9 +61,6 @@ void launch_msm_load(int N, const uint8_t* raw_pts, const uint8_t* raw_sc, uint3
 void launch_msm_to_bytes(const uint32_t* jac, uint8_t* out, hipStream_t s);
 void launch_sig_prep(const SigBatchDev& d, hipStream_t s);
 void launch_sig_finish(const SigBatchDev& d, const uint32_t* tables, int n, hipStream_t s);
-extern int g_lat_bs;
-extern int g_fx_proof_fastest;  // rp_kernels.hip (FTS_FX_ORDER)
-extern int g_chain_bs;          // rp_kernels.hip (FTS_CHAIN_BS)
 void launch_sig_exclude(const SigBatchDev& d, int32_t* rp_excl, hipStream_t s);
 size_t table_build_scratch_bytes(int nb);
 size_t fb_words_per_base();
@@ -194,7 +191,7 @@ struct Lane {
   bool alone = true;
   hipStream_t s = nullptr, s2 = nullptr;
   hipStream_t s3 = nullptr;         // sigma proofs of action batches (beside the range-proof pass)
-  hipStream_t s4 = nullptr;         // latency path: the x0 transcript prefix beside the x*D chain
+  hipStream_t s4 = nullptr;         // the batch check's x0-free columns beside its MSM
   hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr, ev_d = nullptr, ev_e = nullptr;  // cross-stream ordering (no timing)
   Workspace ws;
   Timeline tl;
@@ -356,6 +353,20 @@ struct RpReq {
   RpReq(fts_rp_batch* bb, int32_t* st) : b(bb), status(st) {}
 };
 
+// fts_rp_verify_batch staging slot (host DER bytes -> device): pinned host
+// records and device input buffers, grown geometrically and reused across
+// calls, so a call neither allocates nor frees device memory (hipFree
+// synchronises the whole device, stalling every other lane's pass)
+struct RpSlot {
+  fts_rp_batch* b = nullptr;  // device pointers into `dev` (not owned by the batch)
+  uint8_t* pin = nullptr;
+  size_t pin_cap = 0;
+  uint8_t* dev = nullptr;
+  size_t dev_cap = 0;
+  hipStream_t s = nullptr;
+  hipEvent_t done = nullptr;  // blocking-sync: the waiting caller sleeps
+};
+
 struct fts_ctx {
   int device = 0;
   // multi-device context (fts_ctx_create_devices): one child context per device;
@@ -416,18 +427,7 @@ struct fts_ctx {
   // tools/sweeps/gt1_small.txt)
   int gt_adapt = 1;
   std::atomic<int> gt_dense{0};
-  // FTS_LAT_ORDER: latency-path launch order (RpBatchDev::lat_order).  5 = the MSM's
-  // digits / sort before k_rp_fixed_all + the x0 prefix behind k_rp_xd: lone
-  // 4,096-proof batch 2.82 vs 2.88 ms in tools/pass_times.py, but 2.83 vs 2.84 ms
-  // in bench.py's isolated batch and a lower 20-step line (3.56 vs 3.74 M/s mean
-  // of 3 alternating runs, tools/sweeps/lat_bench_ab.txt): off by default
-  int lat_order = 0;
-  int x0_split = 1;                 // FTS_X0_SPLIT: work path hashes the x0 prefix beside the com chain
-  int com_split = 0;                // FTS_COM_SPLIT: work path computes x*D beside the exact phase (k_rp_xd)
-  int idle_gather_us = 0;           // FTS_IDLE_GATHER_US: gather window on an idle device (0: start at once)
-  bool split = false;               // FTS_SPLIT: a pass leaves half the queue to a free lane (bursts; measured no gain)
-  bool split_go = false;            // the queue's head was left by a split: start without gathering
-  bool shallow_cap = false;         // FTS_SHALLOW_CAP: passes from a shallow queue take at most gather_target
+  int x0_split = 1;  // FTS_X0_SPLIT: work path hashes the x0 prefix beside the com chain
   // FTS_RLC_FORK: the batch check forks after the fixed-base products (1) or after the
   // challenges (0); 2 (default): after the challenges on the latency path (a lone small
   // pass: its MSM chain is the critical path, 3.16 -> 2.98 ms per 4,096-proof batch),
@@ -442,6 +442,8 @@ struct fts_ctx {
   }
   std::once_flag prover_once;
   ProverTables ptab;
+  std::mutex slot_mu;
+  std::vector<RpSlot*> slots, free_slots;  // fts_rp_verify_batch staging (all / idle)
 };
 
 // RAII lane acquisition (want < 0: any free lane)
@@ -573,68 +575,27 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_COM_FIXED_MAX")) c->com_fixed_max = (size_t)std::max(0L, atol(e));
   if (const char* e = getenv("FTS_RLC_FORK")) c->rlc_fork = std::max(0, std::min(2, atoi(e)));
   if (const char* e = getenv("FTS_X0_SPLIT")) c->x0_split = atoi(e) != 0;
-  if (const char* e = getenv("FTS_LAT_ORDER")) c->lat_order = atoi(e) & 7;
-  if (const char* e = getenv("FTS_COM_SPLIT")) c->com_split = atoi(e) != 0;
-  if (const char* e = getenv("FTS_IDLE_GATHER_US")) c->idle_gather_us = std::max(0, atoi(e));
-  if (const char* e = getenv("FTS_SPLIT")) c->split = atoi(e) != 0;
-  if (const char* e = getenv("FTS_SHALLOW_CAP")) c->shallow_cap = atoi(e) != 0;
   if (const char* e = getenv("FTS_GT1")) c->gt1 = std::max(8, std::min(1024, atoi(e)));
   if (const char* e = getenv("FTS_GT2_MIN")) c->gt2_min = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_GT_ADAPT")) c->gt_adapt = atoi(e) != 0;
-  // process-wide launch knobs of rp_kernels.hip: read once, before any context can
-  // launch (contexts are created concurrently by fts_ctx_create_devices, and the
-  // launch code of live contexts reads these values)
-  static std::once_flag knobs_once;
-  std::call_once(knobs_once, [] {
-    if (const char* e = getenv("FTS_FX_ORDER")) g_fx_proof_fastest = atoi(e) != 0;
-    if (const char* e = getenv("FTS_CHAIN_BS")) g_chain_bs = atoi(e) >= 256 ? 256 : atoi(e) >= 128 ? 128 : 64;
-    if (const char* e = getenv("FTS_LAT_BS")) {  // block size of the latency-bound kernels (64, 128 or 256)
-      const int v = atoi(e);
-      g_lat_bs = v <= 64 ? 64 : v <= 128 ? 128 : 256;
-    }
-  });
-  // FTS_SIDE_STREAM=0: run each lane's side work on its main stream
-  bool side = true;
-  if (const char* e = getenv("FTS_SIDE_STREAM")) side = atoi(e) != 0;
   // the batch check's stream (s3: RLC weights + MSM, the longest chain of a small
   // pass) gets the device's highest stream priority, so its few waves are
   // dispatched ahead of the exact phase's wide fixed-base launches
   int prio_lo = 0, prio_hi = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
-  int s3_prio = prio_hi;
-  if (const char* e = getenv("FTS_S3_PRIO")) s3_prio = atoi(e) ? prio_hi : prio_lo;
-  // FTS_RESERVE_CUS=R: the lanes' main streams (the exact phase's wide launches,
-  // e.g. k_rp_fixed_all's two rounds of waves) leave R CUs, spread evenly over
-  // the XCDs, to the side and batch-check streams, whose latency-bound chains
-  // (x*D, RLC weights, MSM) would otherwise queue behind them
-  std::vector<uint32_t> cu_mask;
-  {
-    int reserve = 0;
-    if (const char* e = getenv("FTS_RESERVE_CUS")) reserve = std::max(0, atoi(e));
-    hipDeviceProp_t prop;
-    if (reserve > 0 && hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 2 * reserve) {
-      const int ncu = prop.multiProcessorCount, stride = ncu / reserve;
-      cu_mask.assign((ncu + 31) / 32, 0u);
-      for (int i = 0; i < ncu; i++)
-        if (i % stride != stride - 1 || i / stride >= reserve) cu_mask[i / 32] |= 1u << (i % 32);
-    }
-  }
   for (int i = 0; i < nl; i++) {
     Lane* L = new Lane();
     L->id = i;
     c->lanes.push_back(L);
     c->free_lanes.push_back(i);
-    if ((cu_mask.empty() ? hipStreamCreateWithFlags(&L->s, hipStreamNonBlocking)
-                         : hipExtStreamCreateWithCUMask(&L->s, (uint32_t)cu_mask.size(), cu_mask.data())) != hipSuccess)
-      return fail(FTS_API_EDEVICE);
+    if (hipStreamCreateWithFlags(&L->s, hipStreamNonBlocking) != hipSuccess) return fail(FTS_API_EDEVICE);
     if (hipEventCreateWithFlags(&L->done, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)
       return fail(FTS_API_EDEVICE);
     if (hipHostMalloc((void**)&L->pin, sizeof(Lane::Pinned), 0) != hipSuccess) return fail(FTS_API_ENOMEM);
-    if (!side) L->s2 = L->s4 = L->s;
-    else if (hipStreamCreateWithFlags(&L->s2, hipStreamNonBlocking) != hipSuccess ||
-             hipStreamCreateWithFlags(&L->s4, hipStreamNonBlocking) != hipSuccess)
+    if (hipStreamCreateWithFlags(&L->s2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&L->s4, hipStreamNonBlocking) != hipSuccess)
       return fail(FTS_API_EDEVICE);
-    if (hipStreamCreateWithPriority(&L->s3, hipStreamNonBlocking, s3_prio) != hipSuccess ||
+    if (hipStreamCreateWithPriority(&L->s3, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipEventCreateWithFlags(&L->ev_a, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&L->ev_b, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&L->ev_c, hipEventDisableTiming) != hipSuccess ||
@@ -890,6 +851,15 @@ void fts_ctx_destroy(fts_ctx* c) {
   if (c->d_wtables) hipFree(c->d_wtables);
   if (c->d_x0const) hipFree(c->d_x0const);
   if (c->d_x0tmpl) hipFree(c->d_x0tmpl);
+  for (RpSlot* sl : c->slots) {
+    if (sl->s) hipStreamSynchronize(sl->s);
+    if (sl->dev) hipFree(sl->dev);
+    if (sl->pin) (void)hipHostFree(sl->pin);
+    if (sl->done) hipEventDestroy(sl->done);
+    if (sl->s) hipStreamDestroy(sl->s);
+    delete sl->b;
+    delete sl;
+  }
   delete c;
 }
 
@@ -970,6 +940,29 @@ struct RpHost {
   std::vector<int32_t> status, ipa;
 };
 
+// DER range proofs -> device input records (raw BE points with the caller's
+// commitment in slot V, canonical scalars, host-parse verdicts), written into
+// caller-provided host memory (pageable or pinned); parallel over chunks of
+// 256 proofs on the host pool
+static void parse_rp_into(int k, size_t B, const uint8_t* const* der_p, const size_t* der_len, const uint8_t* com64,
+                          uint8_t* raw, uint32_t* sc, int32_t* status, int32_t* ipa) {
+  const int npts = rp_npts(k);
+  constexpr size_t CH = 256;
+  parallel_for((B + CH - 1) / CH, 2, [&](size_t c) {
+    for (size_t i = c * CH; i < std::min(B, (c + 1) * CH); i++) {
+      uint8_t* pts = raw + i * npts * 64;
+      memset(pts, 0, (size_t)npts * 64);
+      memset(sc + i * RP_NSC * 8, 0, RP_NSC * 32);
+      status[i] = 0;
+      ipa[i] = 0;
+      der::Span s{der_p[i], der_len[i]};
+      if (!der_p[i]) s.n = 0;
+      parse_range_proof(s, k, pts, sc + i * RP_NSC * 8, status[i], ipa[i]);
+      memcpy(pts + RP_PT_V * 64, com64 + i * 64, 64);
+    }
+  });
+}
+
 static void parse_rp_batch(int k, size_t B, const uint8_t* const* der_p, const size_t* der_len, const uint8_t* com64,
                            RpHost& h) {
   const int npts = rp_npts(k);
@@ -977,23 +970,7 @@ static void parse_rp_batch(int k, size_t B, const uint8_t* const* der_p, const s
   h.sc.assign(B * RP_NSC * 8, 0);
   h.status.assign(B, 0);
   h.ipa.assign(B, 0);
-  auto work = [&](size_t lo, size_t hi) {
-    for (size_t i = lo; i < hi; i++) {
-      uint8_t* pts = &h.raw[i * npts * 64];
-      der::Span s{der_p[i], der_len[i]};
-      if (!der_p[i]) s.n = 0;
-      parse_range_proof(s, k, pts, &h.sc[i * RP_NSC * 8], h.status[i], h.ipa[i]);
-      memcpy(pts + RP_PT_V * 64, com64 + i * 64, 64);
-    }
-  };
-  unsigned nth = B >= 256 ? host_threads() : 1u;
-  std::vector<std::thread> th;
-  size_t chunk = (B + nth - 1) / nth;
-  for (unsigned t = 0; t < nth; t++) {
-    size_t lo = t * chunk, hi = std::min(B, lo + chunk);
-    if (lo < hi) th.emplace_back(work, lo, hi);
-  }
-  for (auto& t : th) t.join();
+  parse_rp_into(k, B, der_p, der_len, com64, h.raw.data(), h.sc.data(), h.status.data(), h.ipa.data());
 }
 
 static void collect_timings(fts_ctx* c, Lane& L, fts_rp_batch* b) {
@@ -1220,14 +1197,10 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   d.pre_rlc_arg = pre_rlc_arg;
   d.rlc_fork = c->rlc_fork == 2 ? (d.com_fixed ? 0 : 1) : c->rlc_fork;
   d.ev_coef = L.ev_c;
-  // x0 prefix beside the com chain on the work path; on the latency path only
-  // queued behind k_rp_xd (lat_order bit 2): started beside com_tree it shared
-  // CUs with it and the MSM's chunks and delayed both (3.51 vs 3.06 ms, round 2)
-  d.lat_order = d.com_fixed ? c->lat_order : 0;
-  d.x0_mid = c->x0_split && (!d.com_fixed || (d.lat_order & 4)) ? w.x0mid.as<uint32_t>() : nullptr;
-  d.ev_msm = L.ev_e;
-  d.com_split = c->com_split && !d.com_fixed;
-  d.ev_xd = L.ev_d;
+  // x0 prefix beside the com chain on the work path only: on the latency path,
+  // started beside com_tree it shared CUs with it and the MSM's chunks and
+  // delayed both (3.51 vs 3.06 ms, round 2)
+  d.x0_mid = c->x0_split && !d.com_fixed ? w.x0mid.as<uint32_t>() : nullptr;
   d.excl = pre_rlc ? w.rp_excl.as<int32_t>() : nullptr;
   RlcDev r{w.r_key.as<uint32_t>(), w.r_msc.as<uint32_t>(),   w.r_coef.as<uint32_t>(), w.r_colsum.as<uint32_t>(),
            w.r_fixed.as<uint32_t>(), w.r_flag.as<int32_t>(), w.m_scratch.as<uint32_t>(), mp};
@@ -1452,7 +1425,7 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
       continue;
     }
     const bool device_busy = c->free_lanes.size() < c->lanes.size();
-    const int wait_us = c->split_go ? 0 : device_busy ? c->gather_us : c->idle_gather_us;
+    const int wait_us = device_busy ? c->gather_us : 0;
     if (wait_us > 0 && c->rp_pending.front() == &me && c->pending_proofs < c->gather_target) {
       const auto deadline = me.arrived + std::chrono::microseconds(wait_us);
       if (std::chrono::steady_clock::now() < deadline) {
@@ -1468,18 +1441,7 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
     Lane* L = c->lanes[c->free_lanes.back()];
     c->free_lanes.pop_back();
     L->alone = c->free_lanes.size() + 1 == c->lanes.size();
-    // even split (bursts): while another lane is free, a pass leaves half of the
-    // queued proofs to it, and that remainder starts at once instead of waiting
-    // out the gather window -- two concurrent passes instead of one long one
-    // (FTS_SPLIT=1; default off: 20-batch bursts 3.70-3.85 vs 3.90 M/s without)
-    c->split_go = false;
-    size_t cap = c->coalesce_max;
-    // a shallow queue (less than a full pass) gives at most gather_target to one
-    // pass, so how many batches a burst's first gathered pass catches does not
-    // decide whether the rest runs beside it or after it (FTS_SHALLOW_CAP)
-    if (c->shallow_cap && c->pending_proofs < c->coalesce_max) cap = std::min(cap, c->gather_target);
-    const bool split = c->split && !c->free_lanes.empty() && c->pending_proofs >= c->gather_target;
-    if (split) cap = std::min(cap, (c->pending_proofs + 1) / 2);
+    const size_t cap = c->coalesce_max;
     std::vector<RpReq*> grp;
     size_t tot = 0;
     while (!c->rp_pending.empty()) {
@@ -1491,7 +1453,6 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
       c->rp_pending.pop_front();
     }
     // the next head (if any) may lead a pass on another free lane
-    if (split && !c->rp_pending.empty()) c->split_go = true;
     if (!c->rp_pending.empty() && !c->free_lanes.empty()) c->rp_pending.front()->cv.notify_one();
     lk.unlock();
     const int rc = run_rp_group(c, *L, grp);
@@ -1685,22 +1646,97 @@ void fts_rp_batch_free(fts_rp_batch* b) {
   delete b;
 }
 
+// a staging slot sized for n proofs (idle one reused, else a new one); nullptr on
+// allocation failure
+static RpSlot* slot_acquire(fts_ctx* c, size_t n) {
+  RpSlot* sl = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->slot_mu);
+    if (!c->free_slots.empty()) {
+      sl = c->free_slots.back();
+      c->free_slots.pop_back();
+    }
+  }
+  if (!sl) {
+    sl = new RpSlot();
+    sl->b = new fts_rp_batch();
+    sl->b->device = c->device;
+    if (hipStreamCreateWithFlags(&sl->s, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&sl->done, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess) {
+      if (sl->s) hipStreamDestroy(sl->s);
+      delete sl->b;
+      delete sl;
+      return nullptr;
+    }
+    std::lock_guard<std::mutex> g(c->slot_mu);
+    c->slots.push_back(sl);
+  }
+  const size_t npts = (size_t)rp_npts(c->k);
+  const size_t in_bytes = n * (npts * 64 + RP_NSC * 32 + 8), dev_bytes = in_bytes + n * 4;
+  bool ok = true;
+  if (in_bytes > sl->pin_cap) {
+    if (sl->pin) (void)hipHostFree(sl->pin);
+    sl->pin = nullptr;
+    const size_t want = std::max(in_bytes, sl->pin_cap + sl->pin_cap / 2);
+    sl->pin_cap = 0;
+    if (hipHostMalloc((void**)&sl->pin, want, 0) == hipSuccess) sl->pin_cap = want;
+    else ok = false;
+  }
+  if (ok && dev_bytes > sl->dev_cap) {
+    if (sl->dev) hipFree(sl->dev);
+    sl->dev = nullptr;
+    const size_t want = std::max(dev_bytes, sl->dev_cap + sl->dev_cap / 2);
+    sl->dev_cap = 0;
+    if (hipMalloc((void**)&sl->dev, want) == hipSuccess) sl->dev_cap = want;
+    else ok = false;
+  }
+  if (!ok) {
+    std::lock_guard<std::mutex> g(c->slot_mu);
+    c->free_slots.push_back(sl);
+    return nullptr;
+  }
+  return sl;
+}
+
 int fts_rp_verify_batch(fts_ctx* c, size_t n, const uint8_t* const* rp_der, const size_t* rp_len, const uint8_t* com64,
                         int32_t* status) {
   if (!c || !status) return FTS_API_EINVAL;
   if (n == 0) return FTS_API_OK;
-  if (!c->shards.empty()) {
-    if (!rp_der || !rp_len || !com64) return FTS_API_EINVAL;
-    return multi_rp_verify(c, n, rp_der, rp_len, com64, status);
-  }
-  fts_rp_batch* b = nullptr;
-  int rc = fts_rp_batch_stage(c, n, rp_der, rp_len, com64, &b);
-  if (rc != FTS_API_OK) {
+  if (!rp_der || !rp_len || !com64) return FTS_API_EINVAL;
+  if (!c->shards.empty()) return multi_rp_verify(c, n, rp_der, rp_len, com64, status);
+  auto not_run = [&](int rc) {
     for (size_t i = 0; i < n; i++) status[i] = FTS_E_NOT_RUN;
     return rc;
+  };
+  if (c->device < 0) return not_run(FTS_API_EDEVICE);
+  if (n > (size_t)INT32_MAX) return not_run(FTS_API_ESIZE);
+  if (hipSetDevice(c->device) != hipSuccess) return not_run(FTS_API_EDEVICE);
+  // host DER -> pinned records (parallel), one async upload on the slot's stream,
+  // then the staged batch joins the coalescing dispatcher like any other
+  RpSlot* sl = slot_acquire(c, n);
+  if (!sl) return not_run(FTS_API_ENOMEM);
+  const size_t npts = (size_t)rp_npts(c->k);
+  const size_t raw_b = n * npts * 64, sc_b = n * RP_NSC * 32, st_b = n * 4;
+  uint8_t* p = sl->pin;
+  parse_rp_into(c->k, n, rp_der, rp_len, com64, p, reinterpret_cast<uint32_t*>(p + raw_b),
+                reinterpret_cast<int32_t*>(p + raw_b + sc_b), reinterpret_cast<int32_t*>(p + raw_b + sc_b + st_b));
+  fts_rp_batch* b = sl->b;
+  b->B = (int)n;
+  b->raw = sl->dev;
+  b->sc = reinterpret_cast<uint32_t*>(sl->dev + raw_b);
+  b->status0 = reinterpret_cast<int32_t*>(sl->dev + raw_b + sc_b);
+  b->ipa_flag = reinterpret_cast<int32_t*>(sl->dev + raw_b + sc_b + st_b);
+  b->status = reinterpret_cast<int32_t*>(sl->dev + raw_b + sc_b + 2 * st_b);
+  int rc = FTS_API_OK;
+  if (hipMemcpyAsync(sl->dev, sl->pin, raw_b + sc_b + 2 * st_b, hipMemcpyHostToDevice, sl->s) != hipSuccess ||
+      hipEventRecord(sl->done, sl->s) != hipSuccess || hipEventSynchronize(sl->done) != hipSuccess)
+    rc = FTS_API_EDEVICE;
+  if (rc == FTS_API_OK) rc = fts_rp_batch_verify(c, b, status);
+  else not_run(rc);
+  {
+    std::lock_guard<std::mutex> g(c->slot_mu);
+    c->free_slots.push_back(sl);
   }
-  rc = fts_rp_batch_verify(c, b, status);
-  fts_rp_batch_free(b);
   return rc;
 }
 

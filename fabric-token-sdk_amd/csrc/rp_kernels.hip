@@ -36,14 +36,10 @@ namespace fts {
 // 256-thread blocks put a block's 4 waves on the 4 SIMDs of one CU, and the
 // dispatcher spreads blocks over CUs, so concurrent small kernels of the
 // pass's streams rarely share a SIMD (64-thread blocks of two such kernels
-// slowed each other by ~26 %, tools/experiments/colocate.cpp).  FTS_LAT_BS.
+// slowed each other by ~26 %, tools/experiments/colocate.cpp)
 int g_lat_bs = 256;
-// k_rp_fixed_exact lane order (FTS_FX_ORDER): 1 = proof index fastest (a wave's
-// gathers stay inside one base's table: 6.9 -> 6.2 ms per 81,920-proof launch,
-// tools/run_fxorder.sh), 0 = one proof's 66 items side by side (round 1)
-int g_fx_proof_fastest = 1;
-// block size of the work path's S / com chain kernels (FTS_CHAIN_BS: 64 or 256)
-int g_chain_bs = 64;
+// block size of the work path's S / com chain kernels
+constexpr int g_chain_bs = 64;
 
 
 constexpr int NORM_BS = 256;
@@ -354,13 +350,14 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, c
                                                           const uint32_t* __restrict__ sc, const uint32_t* __restrict__ ch,
                                                           const uint32_t* __restrict__ ypow,
                                                           const uint32_t* __restrict__ wtables, uint32_t* __restrict__ hpj,
-                                                          uint32_t* __restrict__ terms, int proof_fastest) {
+                                                          uint32_t* __restrict__ terms) {
   const int ni = n + 2;
   const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (size_t)B * ni) return;
-  // proof_fastest: a wave's 64 lanes gather from the same base's table (and read
-  // ypow[t][b] coalesced); else one proof's items side by side
-  const int b = proof_fastest ? (int)(gid % B) : (int)(gid / ni), t = proof_fastest ? (int)(gid / B) : (int)(gid % ni);
+  // proof index fastest: a wave's 64 lanes gather from the same base's table (and
+  // read ypow[t][b] coalesced): 6.9 -> 6.2 ms per 81,920-proof launch and 4.77 ->
+  // 1.79 GB fetched against one proof's items side by side (round 2)
+  const int b = (int)(gid % B), t = (int)(gid / B);
   if (status[b] != 0) return;
   const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
   uint32_t* out;
@@ -462,58 +459,6 @@ __global__ void __launch_bounds__(256, FTS_COMVAR_OCC) k_rp_com_var(int B, int n
   // adds its fixed-base term (z K or -delta P, k_rp_fixed_exact), lane 0 also C,
   // then lane 0 adds lane 1's partial (cross-lane shuffle) and writes com
   add_inl(r, load_g1j(terms + ((size_t)b * COM_NTERMS + h) * 24));
-  G1J c = g1j_identity();
-  if (h == 0) c = g1j_from_affine(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_C) * 16));
-  add_inl(r, c);
-  G1J o;
-#pragma unroll
-  for (int q = 0; q < 8; q++) {
-    o.x.v[q] = __shfl_xor(r.x.v[q], 1);
-    o.y.v[q] = __shfl_xor(r.y.v[q], 1);
-    o.z.v[q] = __shfl_xor(r.z.v[q], 1);
-  }
-  if (h == 0) {
-    add_inl(r, o);
-    store_g1j(hpj + ((size_t)b * (n + 1) + n) * 24, r);
-  }
-}
-
-// Split form of k_rp_com_var (d.com_split): x*D comes from k_rp_xd (terms[b][2 + h],
-// computed beside the exact phase), so a lane's chain is w_h phi^h(S) alone over an
-// 8-entry affine table (124 doublings, 32 mixed additions); the two lanes of a
-// proof then add their fixed-base term, their x*D half and (lane 0) C -> com
-__global__ void __launch_bounds__(256, FTS_COMVAR_OCC) k_rp_com_s(int B, int n, int k, const int32_t* __restrict__ status,
-                                                               const uint32_t* __restrict__ pts,
-                                                               const uint32_t* __restrict__ ch,
-                                                               const uint32_t* __restrict__ chunks,
-                                                               uint32_t* __restrict__ atab,
-                                                               const uint32_t* __restrict__ terms,
-                                                               uint32_t* __restrict__ hpj) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int b = gid >> 1, h = gid & 1;
-  if (b >= B || status[b] != 0) return;
-  const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
-  Fr z2;
-  load_f(C + CH_Z2 * 8, z2);
-  uint32_t wk[2][4], ws[2];
-  glv_decompose(fr_canon(z2).v, wk[0], ws[0], wk[1], ws[1]);
-  const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
-  const uint32_t* Sc = chunks + (size_t)b * nc * 24;
-  G1J S = load_g1j(Sc + (nc - 1) * 24);
-  for (int c = nc - 2; c >= 0; c--) {
-    for (int q = 0; q < HS_CHUNK; q++) S = g1j_dbl(S);
-    add_inl(S, load_g1j(Sc + c * 24));
-  }
-  const bool idS = f_is_zero(S.z);
-  if (h) S.x = fp_mul(S.x, glv_beta());
-  if (ws[h]) S.y = f_neg(S.y);
-  const ATab T{atab, (size_t)2 * B, (size_t)gid};
-  Fp pre;
-  atab_build8<false>(T, 0, S, pre, idS);
-  atab_normalize<8>(T);
-  G1J r = straus1_atab(T, wk[h], idS);
-  add_inl(r, load_g1j(terms + ((size_t)b * COM_NTERMS + 2 + h) * 24));  // x_h phi^h(D)
-  add_inl(r, load_g1j(terms + ((size_t)b * COM_NTERMS + h) * 24));      // z K or -delta P
   G1J c = g1j_identity();
   if (h == 0) c = g1j_from_affine(load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_C) * 16));
   add_inl(r, c);
@@ -1564,15 +1509,6 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     FTS_LAUNCH(k_rp_xd, 2 * B, g_lat_bs, s2, B, n, k, d.status, d.pts, d.small_msgs, d.scratch + (size_t)B * (k + 1) * 8,
                d.terms, com_fx_slots(n), n + 2);
     tl->mark("k_rp_xd", s2, (double)B * 2 * COST_VB128);
-    if (d.lat_order & 4) (void)hipEventRecord(d.ev_xd, s2);
-  } else if (d.com_split) {
-    // work path, split com: x*D (terms[b][2 + h]) beside the exact phase from the
-    // x digest on; lane tables past the S chunks and the com lanes' tables
-    tl->fork(s, s2);
-    FTS_LAUNCH(k_rp_xd, 2 * B, g_lat_bs, s2, B, n, k, d.status, d.pts, d.small_msgs,
-               d.scratch + (size_t)B * HS_SCRATCH + (size_t)2 * B * ATAB_WORDS, d.terms, COM_NTERMS, 2);
-    tl->mark("k_rp_xd", s2, (double)B * 2 * COST_VB128);
-    (void)hipEventRecord(d.ev_xd, s2);
   }
   FTS_LAUNCH(k_rp_chal_fr, B, g_lat_bs, s, B, n, k, d.status, d.ch, d.scratch);
   tl->mark("k_rp_chal_fr", s, (double)B * (3 * k + 4 * (k + 1) + 12));
@@ -1599,8 +1535,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     tl->mark("k_rlc_columns", s4, (double)B * 4 * n);
     FTS_LAUNCH(k_rlc_fixed, (size_t)(NC - 1) * FB_NW, RF_ITEMS * FB_NW, s4, n, 1, 0, NC - 1, r.colsum, tables, r.fixed);
     tl->mark("k_rlc_fixed", s4, (double)(NC - 1) * (FB_NW * 3 + (FB_NW - 1) * COST_ADD));
-    launch_msm(r.plan, d.pts, r.msc, r.fixed, NC - 1, r.msm_scratch, s3, s4, tl, d.com_fixed ? d.ev_msm : nullptr,
-               d.com_fixed ? (d.lat_order & 3) : 0);
+    launch_msm(r.plan, d.pts, r.msc, r.fixed, NC - 1, r.msm_scratch, s3, s4, tl);
   };
   if (!d.rlc_fork) rlc_prep();
   FTS_LAUNCH(k_rp_powers, B * (n >> std::min(PW_LC, k)), 64, s, B, n, k, d.status, d.ch, d.ypow, d.svec, d.zvec);
@@ -1612,37 +1547,19 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   if (!d.rlc_fork) rlc_side();
   // exact per-proof phase on s
   if (d.com_fixed) {
-    // lat_order & 3: the MSM's digit / sort launches are short but latency-bound;
-    // sharing the CUs with k_rp_fixed_all stretches them ~6x, so they may go first
-    if ((d.lat_order & 3) && d.ev_msm) (void)hipStreamWaitEvent(s, d.ev_msm, 0);
     FTS_LAUNCH(k_rp_fixed_all, (size_t)B * (2 * n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, d.zvec, wtables,
                d.hpj, d.terms);
     tl->mark("k_rp_fixed_all", s, (double)B * (2.0 * n + 2.0) * COST_FBW_FRESH);
     if (d.rlc_fork) rlc_side();
     launch_normalize(nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be, s);
     tl->mark("k_rp_normalize", s, (double)nhp * (2.0 * 8.0 / NORM_E + 9.0));
-    // x0 prefix (H' records + shared template: all but the last 3 blocks): on s2
-    // queued behind k_rp_xd (lat_order bit 2; com_tree waits for x*D alone), else
-    // on s4 beside the x*D chain; only the suffix waits for com
-    hipStream_t xs = (d.lat_order & 4) ? s2 : s4;
-    if (d.x0_mid) {
-      tl->fork(s, xs);
-      hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), xs, B, n, d.status, d.hp_be, x0_const,
-                         d.sc, d.x0_msgs, 0);
-      tl->mark("k_rp_x0_build", xs, 0);
-      FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, xs, B, n, k, d.status, d.x0_msgs, x0_tmpl, 0u, x0_cb1(n), d.x0_mid, d.ch);
-      tl->mark("k_rp_x0_prefix", xs, 0);
-    }
-    if (d.lat_order & 4)
-      (void)hipStreamWaitEvent(s, d.ev_xd, 0);
-    else
-      tl->fork(s2, s);
+    tl->fork(s2, s);
     hipLaunchKernelGGL(k_rp_com_tree, dim3((B + CT_PROOFS - 1) / CT_PROOFS), dim3(CT_LANES * CT_PROOFS), 0, s, B, n,
                        k, d.status, d.pts, d.terms, d.hpj);
     tl->mark("k_rp_com_sum", s, (double)B * (com_fx_slots(n) + 1) * COST_ADD);
   } else {
     FTS_LAUNCH(k_rp_fixed_exact, (size_t)B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, wtables, d.hpj,
-               d.terms, g_fx_proof_fastest);
+               d.terms);
     tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FBW_FRESH);
     if (d.rlc_fork) rlc_side();
     // H'_i -> affine + BE bytes (x0 transcript) now; com is normalised after com_sum
@@ -1663,18 +1580,10 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     FTS_LAUNCH(k_rp_hsum_chunks, B * nch, g_chain_bs, s, B, n, d.status, d.hpa, d.scratch);
     tl->mark("k_rp_hsum_chunks", s, (double)B * (n - nch) * (COST_DBL + COST_MADD));
     // scratch: [0, B*HS_SCRATCH) Horner chunks of S, then the 2B lanes' affine tables
-    if (d.com_split) {
-      (void)hipStreamWaitEvent(s, d.ev_xd, 0);
-      FTS_LAUNCH(k_rp_com_s, 2 * B, g_chain_bs, s, B, n, k, d.status, d.pts, d.ch, d.scratch,
-                 d.scratch + (size_t)B * HS_SCRATCH, d.terms, d.hpj);
-      tl->mark("k_rp_com_s", s,
-               (double)B * 2 * ((nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD) + COST_STRAUS1_ATAB + 3.5 * COST_ADD));
-    } else {
-      FTS_LAUNCH(k_rp_com_var, 2 * B, g_chain_bs, s, B, n, k, d.status, d.pts, d.ch, d.scratch,
-                 d.scratch + (size_t)B * HS_SCRATCH, d.terms, d.hpj);
-      tl->mark("k_rp_com_var", s,
-               (double)B * 2 * ((nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD) + COST_STRAUS2_ATAB + 2.5 * COST_ADD));
-    }
+    FTS_LAUNCH(k_rp_com_var, 2 * B, g_chain_bs, s, B, n, k, d.status, d.pts, d.ch, d.scratch,
+               d.scratch + (size_t)B * HS_SCRATCH, d.terms, d.hpj);
+    tl->mark("k_rp_com_var", s,
+             (double)B * 2 * ((nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD) + COST_STRAUS2_ATAB + 2.5 * COST_ADD));
   }
   launch_normalize(B, 1, n + 1, n, d.status, d.hpj, d.hpa, d.hp_be, s);
   tl->mark("k_rp_normalize_com", s, (double)B * (2.0 * 8.0 / NORM_E + 9.0));
@@ -1682,7 +1591,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s, B, n, d.status, d.hp_be, x0_const, d.sc,
                      d.x0_msgs, split ? 1 : 2);
   tl->mark(split ? "k_rp_x0_build_tail" : "k_rp_x0_build", s, 0);
-  if (split) tl->fork(d.com_fixed && !(d.lat_order & 4) ? s4 : s2, s);  // the prefix's midstate
+  if (split) tl->fork(s2, s);  // the prefix's midstate
   FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s, B, n, k, d.status, d.x0_msgs, x0_tmpl, split ? x0_cb1(n) : 0u, 0xffffffffu,
              d.x0_mid, d.ch);
   tl->mark("k_rp_x0_hash", s, 0);

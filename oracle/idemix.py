@@ -47,12 +47,15 @@ MSG_INVALID = "pseudonym signature invalid: zero-knowledge proof is invalid"
 
 # ------------------------------------------------------------ protobuf (wire)
 def _varint(b, i):
+    """protowire.ConsumeVarint: at most 10 bytes, the 10th carrying only bit 63"""
     s = sh = 0
     while True:
         if i >= len(b):
             raise ValueError("truncated varint")
         c = b[i]
         i += 1
+        if sh == 63 and c > 1:
+            raise ValueError("varint overflow")
         s |= (c & 0x7F) << sh
         sh += 7
         if c < 0x80:
@@ -61,31 +64,50 @@ def _varint(b, i):
             raise ValueError("varint overflow")
 
 
+def _field_value(b, i, f, wt, depth=0):
+    """(value, next index) of one field; groups (wire type 3 up to the matching 4)
+    are consumed as protowire.ConsumeFieldValue does and return None"""
+    if wt == 0:
+        return _varint(b, i)
+    if wt == 1:
+        if i + 8 > len(b):
+            raise ValueError("truncated fixed64")
+        return b[i:i + 8], i + 8
+    if wt == 5:
+        if i + 4 > len(b):
+            raise ValueError("truncated fixed32")
+        return b[i:i + 4], i + 4
+    if wt == 2:
+        n, i = _varint(b, i)
+        if i + n > len(b):
+            raise ValueError("truncated bytes")
+        return b[i:i + n], i + n
+    if wt == 3:
+        if depth >= 64:
+            raise ValueError("group nesting")
+        while True:
+            key, i = _varint(b, i)
+            gf, gw = key >> 3, key & 7
+            if gf == 0 or gf > 0x1FFFFFFF:
+                raise ValueError("bad field number")
+            if gw == 4:
+                if gf != f:
+                    raise ValueError("mismatched end group")
+                return None, i
+            _, i = _field_value(b, i, gf, gw, depth + 1)
+    raise ValueError("wire type %d" % wt)
+
+
 def pb_fields(b):
-    """[(field, wire_type, value)] of a protobuf message (wire types 0, 1, 2, 5)."""
+    """[(field, wire_type, value)] of a protobuf message (wire types 0, 1, 2, 5;
+    skipped groups appear with wire type 3 and value None)."""
     out, i = [], 0
     while i < len(b):
         key, i = _varint(b, i)
         f, wt = key >> 3, key & 7
-        if f == 0:
-            raise ValueError("field 0")
-        if wt == 0:
-            v, i = _varint(b, i)
-        elif wt == 1:
-            if i + 8 > len(b):
-                raise ValueError("truncated fixed64")
-            v, i = b[i:i + 8], i + 8
-        elif wt == 5:
-            if i + 4 > len(b):
-                raise ValueError("truncated fixed32")
-            v, i = b[i:i + 4], i + 4
-        elif wt == 2:
-            n, i = _varint(b, i)
-            if i + n > len(b):
-                raise ValueError("truncated bytes")
-            v, i = b[i:i + n], i + n
-        else:
-            raise ValueError("wire type %d" % wt)
+        if f == 0 or f > 0x1FFFFFFF:
+            raise ValueError("bad field number")
+        v, i = _field_value(b, i, f, wt)
         out.append((f, wt, v))
     return out
 
