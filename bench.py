@@ -183,6 +183,8 @@ def main():
     ap.add_argument("--prove-kind", choices=["rp", "transfer"], default="rp",
                     help="prove workload: standalone range proofs, or whole 2-in/2-out transfers")
     ap.add_argument("--msm-log", type=int, default=20, help="msm workload: log2 of the point count")
+    ap.add_argument("--msm-tiled", action="store_true",
+                    help="msm workload: 2^16 distinct points tiled (rounds 2-3) instead of 2^msm-log distinct ones")
     ap.add_argument("--transfers", type=int, default=8192, help="transfer/mixed workloads: transfers per GPU per step")
     ap.add_argument("--action-inflight", type=int, default=3,
                     help="transfer/mixed workloads: concurrent verify calls (host threads)")
@@ -534,10 +536,10 @@ def _seq_points(m):
     return out
 
 
-def _mul_g(k):
-    """k G (double-and-add, affine; used once to check the MSM result)"""
+def _mul_g(k, base=(1, 2)):
+    """k P (double-and-add, affine; P = G by default; used once to check the MSM result)"""
     p = 21888242871839275222246405745257275088696311157297823662689037894645226208583
-    acc, base = None, (1, 2)
+    acc = None
     while k:
         if k & 1:
             acc = base if acc is None else _add(acc, base, p)
@@ -602,17 +604,35 @@ def bench_msm(args):
     pp = fts_gpu.PublicParams(pp_raw, bit_length=args.bits, device=local)
     n = 1 << args.msm_log
     t0 = time.time()
-    m = min(n, 1 << 16)
-    base = b"".join(x.to_bytes(32, "big") + y.to_bytes(32, "big") for x, y in _seq_points(m))
-    pts = base * (n // m)
     rng = random.Random(0xF7A50003 + rank)
     ks = [rng.randrange(R_ORDER) for _ in range(n)]
     scs = b"".join(k.to_bytes(32, "big") for k in ks)
-    st = pp.stage_msm(pts, scs)
+    if args.msm_tiled:
+        # round-2/3 input: 2^16 distinct points (i + 1) G tiled n / 2^16 times (L2-resident)
+        m = min(n, 1 << 16)
+        base = b"".join(x.to_bytes(32, "big") + y.to_bytes(32, "big") for x, y in _seq_points(m))
+        pts = base * (n // m)
+        st = pp.stage_msm(pts, scs)
+        data = "synthetic: P_i = (i mod 2^16 + 1) G (tiled), uniform scalars mod r (seed 0xF7A50003 + rank)"
+        e = _mul_g(sum(k * (i % m + 1) for i, k in enumerate(ks)) % R_ORDER)
+    else:
+        # n DISTINCT points k'_i * ped1, uniform k'_i, generated on the device
+        # (fts_msm_stage_multiples) from 32-byte BE k'_i; closed form (sum s_i k'_i) * ped1
+        kp = [rng.randrange(R_ORDER) for _ in range(n)]
+        st = pp.stage_msm_multiples(b"".join(k.to_bytes(32, "big") for k in kp), scs)
+        c1 = pp.token_commit(b"C3", 1, bytes(32))
+        c0 = pp.token_commit(b"C3", 0, bytes(32))
+        P = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+        a = (int.from_bytes(c1[:32], "big"), int.from_bytes(c1[32:], "big"))
+        b_ = (int.from_bytes(c0[:32], "big"), (-int.from_bytes(c0[32:], "big")) % P)
+        ped1 = _add(a, b_, P)
+        pts = None
+        data = "synthetic: 2^%d distinct points P_i = k'_i ped1 (uniform k'_i, made on the device), uniform " \
+               "scalars mod r (seed 0xF7A50003 + rank)" % args.msm_log
+        e = _mul_g(sum(k * q for k, q in zip(ks, kp)) % R_ORDER, ped1)
     setup_s = time.time() - t0
     for _ in range(max(1, args.warmup)):
         res = st.run()
-    e = _mul_g(sum(k * (i % m + 1) for i, k in enumerate(ks)) % R_ORDER)
     assert res == (bytes(64) if e is None else e[0].to_bytes(32, "big") + e[1].to_bytes(32, "big")), "MSM mismatch"
     if dist is not None:
         dist.barrier()
@@ -632,8 +652,12 @@ def bench_msm(args):
         done, cs = 0, 0.0
         while cs < args.cpu_seconds and done < n:
             c = min(1024, n - done)
+            if pts is None:  # the CPU port reads points: the first sample's k'_i ped1 on the host
+                pts = b"".join(x.to_bytes(32, "big") + y.to_bytes(32, "big")
+                               for x, y in (_mul_g(k, ped1) for k in kp[:min(n, 1024)]))
             t1 = time.perf_counter()
-            cref.msm(pts[64 * done:64 * (done + c)], scs[32 * done:32 * (done + c)], threads=thr)
+            off = done % (len(pts) // 64)  # c divides the sample's point count
+            cref.msm(pts[64 * off:64 * (off + c)], scs[32 * done:32 * (done + c)], threads=thr)
             cs += time.perf_counter() - t1
             done += c
         cpu = {"value": round(done / cs, 1), "unit": "terms/s", "cores": thr, "kind": "port",
@@ -645,7 +669,7 @@ def bench_msm(args):
             "unit": "terms/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u32 (BN254 Fp 8x32-bit Montgomery)",
-            "data": "synthetic: P_i = (i mod 2^16 + 1) G, uniform scalars mod r (seed 0xF7A50003 + rank)",
+            "data": data,
             "config": {"workload": "C3: standalone G1 MSM, 2^%d points per GPU (fts_msm_run, inputs resident in HBM)"
                                    % args.msm_log, "points": n, "parallelism": "shard%d" % world},
             "roofline": _roofline_from(kt, args.steps), "cpu_baseline": cpu,

@@ -59,6 +59,8 @@ void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalar
 void launch_msm_load(int N, const uint8_t* raw_pts, const uint8_t* raw_sc, uint32_t* pts, uint32_t* sc, uint32_t* bad,
                      hipStream_t s);
 void launch_msm_to_bytes(const uint32_t* jac, uint8_t* out, hipStream_t s);
+void launch_msm_gen_points(int N, const uint8_t* raw_k, const uint8_t* raw_s, const uint32_t* table, uint32_t* jac,
+                           uint32_t* pts, uint32_t* sc, hipStream_t s);
 void launch_sig_prep(const SigBatchDev& d, hipStream_t s);
 void launch_sig_finish(const SigBatchDev& d, const uint32_t* tables, int n, hipStream_t s);
 void launch_sig_exclude(const SigBatchDev& d, int32_t* rp_excl, hipStream_t s);
@@ -1150,20 +1152,29 @@ static int rp_group_fallback(fts_ctx* c, Lane& L, const RpBatchDev& d, const Rlc
   return FTS_API_OK;
 }
 
+// One range-proof pass enqueued on a lane (rp_enqueue), finished by rp_finish.
+struct RpPass {
+  RpBatchDev d{};
+  RlcDev r{};
+  std::vector<int> groups;
+  double t_start = 0, t_prep = 0, t_enq = 0;
+};
+
 // Range-proof pipeline on B proofs already on the device: exact phase, RLC
-// batch check, and the group-test fallback when the combination fails.
-// `between` (optional) is launched after the RLC check and before the flag
-// sync (the sigma-proof kernels of transfer/issue batches).
+// batch check, and (rp_finish) the group-test fallback when the combination
+// fails.  `between` (optional) is launched after the RLC check and before the
+// flag sync (the sigma-proof kernels of transfer/issue batches).
 // `groups`: first proof of every caller batch in the pass, then B ({0, B}: one batch)
 // `pre_rlc` (optional): launched on the batch check's stream (lane s3) right before k_rlc_prep
 template <class F>
-static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc, int32_t* d_status, int32_t* d_ipa,
-                       F&& between, const std::vector<int>& groups, void (*pre_rlc)(void*, hipStream_t) = nullptr,
-                       void* pre_rlc_arg = nullptr) {
+static int rp_enqueue(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc, int32_t* d_status, int32_t* d_ipa,
+                      F&& between, const std::vector<int>& groups, RpPass& P,
+                      void (*pre_rlc)(void*, hipStream_t) = nullptr, void* pre_rlc_arg = nullptr) {
   const int n = c->n, k = c->k, npts = rp_npts(k);
   Workspace& w = L.ws;
   const int N = B * npts;
-  const double t_start = now_ms();
+  P.t_start = now_ms();
+  P.groups = groups;
   // first range-proof pass of this lane: size the workspace for the largest
   // coalesced pass at once (no re-allocation, i.e. no device-wide sync, later)
   if (!L.presized && c->coalesce_max > (size_t)B && c->coalesce_max <= (1u << 20))
@@ -1207,86 +1218,120 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
   // fresh RLC weights key (getrandom), unpredictable to the provers
   if (getrandom(L.pin->key, sizeof L.pin->key, 0) != (ssize_t)sizeof L.pin->key) return FTS_API_EDEVICE;
   HIP_OK(hipMemcpyAsync(r.key, L.pin->key, sizeof L.pin->key, hipMemcpyHostToDevice, L.s));
-  const double t_prep = now_ms();
+  P.t_prep = now_ms();
   L.tl.begin(L.s);
   launch_rp_batch(d, r, c->d_tables, c->d_wtables, c->d_x0const, c->d_x0tmpl, L.s, L.s2, L.s3, L.s4, &L.tl);
   between();
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(&L.pin->flag, r.flag, 4, hipMemcpyDeviceToHost, L.s));
-  const double t_enq = now_ms();
+  P.t_enq = now_ms();
+  P.d = d;
+  P.r = r;
+  return FTS_API_OK;
+}
+
+// wait for an enqueued pass; on a failed combination, the group-test fallback
+static int rp_finish(fts_ctx* c, Lane& L, RpPass& P) {
   HIP_OK(L.sync());
   const double t_wait = now_ms();
-  L.host_prep_ms = (float)(t_prep - t_start);
-  L.host_enqueue_ms = (float)(t_enq - t_prep);
-  L.host_wait_ms = (float)(t_wait - t_enq);
+  L.host_prep_ms = (float)(P.t_prep - P.t_start);
+  L.host_enqueue_ms = (float)(P.t_enq - P.t_prep);
+  L.host_wait_ms = (float)(t_wait - P.t_enq);
   const int32_t flag = L.pin->flag;
   c->last_fallback = flag ? 0 : 1;
-  if (!flag) return rp_group_fallback(c, L, d, r, groups);
+  if (!flag) return rp_group_fallback(c, L, P.d, P.r, P.groups);
   return FTS_API_OK;
 }
 
-static int run_rp(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc, int32_t* d_status, int32_t* d_ipa,
-                  int32_t* host_status, fts_rp_batch* batch) {
-  int rc = rp_pipeline(c, L, B, d_raw, d_sc, d_status, d_ipa, [] {}, std::vector<int>{0, B});
-  if (rc != FTS_API_OK) return rc;
-  int32_t* pst = host_status ? L.status_buf((size_t)B) : nullptr;
-  if (host_status && !pst) return FTS_API_ENOMEM;
-  if (host_status) HIP_OK(hipMemcpyAsync(pst, d_status, (size_t)B * 4, hipMemcpyDeviceToHost, L.s));
-  HIP_OK(L.sync());
-  if (host_status) memcpy(host_status, pst, (size_t)B * 4);
-  collect_timings(c, L, batch);
-  return FTS_API_OK;
+template <class F>
+static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc, int32_t* d_status, int32_t* d_ipa,
+                       F&& between, const std::vector<int>& groups, void (*pre_rlc)(void*, hipStream_t) = nullptr,
+                       void* pre_rlc_arg = nullptr) {
+  RpPass P;
+  if (int rc = rp_enqueue(c, L, B, d_raw, d_sc, d_status, d_ipa, between, groups, P, pre_rlc, pre_rlc_arg)) return rc;
+  return rp_finish(c, L, P);
 }
 
-// One device pass over a group of staged batches: a single batch runs in
-// place; several are gathered (D2D) into the lane's contiguous input buffers,
-// verified as one batch, and their verdicts scattered back.
-static int run_rp_group(fts_ctx* c, Lane& L, const std::vector<RpReq*>& grp) {
-  if (grp.size() == 1) {
-    fts_rp_batch* b = grp[0]->b;
-    HIP_OK(hipMemcpyAsync(b->status, b->status0, (size_t)b->B * 4, hipMemcpyDeviceToDevice, L.s));
-    b->merged = 1;
-    return run_rp(c, L, b->B, b->raw, b->sc, b->status, b->ipa_flag, grp[0]->status, b);
-  }
+// Device passes over groups of staged batches, group j on lanes[j] (the
+// dispatcher passes one group; several are enqueued back to back before any is
+// waited for): a single batch runs in place; several are gathered (D2D) into the
+// lane's contiguous input buffers, verified as one batch, and their verdicts
+// scattered back.  rc[j] is the status of group j's requests.  (Round 4 measured
+// staggered sub-passes of one coalesced group -- sub-pass j's fixed-base launch
+// after sub-pass j-1's -- and dropped them: 20-batch bursts 3.77-3.89 vs 3.95-3.97
+// M rp64/s as one pass)
+static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std::vector<std::vector<RpReq*>>& sub,
+                             std::vector<int>& rc) {
+  const size_t m = sub.size();
   const int npts = rp_npts(c->k);
-  size_t B = 0;
-  for (RpReq* q : grp) B += (size_t)q->b->B;
-  Workspace& w = L.ws;
-  const size_t Bal = std::max(B, std::min(c->coalesce_max, (size_t)1 << 20));  // sized once for the largest pass
-  if (w.rp_raw.ensure(Bal * npts * 64) || w.rp_sc.ensure(Bal * RP_NSC * 32) || w.rp_status.ensure(Bal * 4) ||
-      w.rp_ipa.ensure(Bal * 4))
-    return FTS_API_ENOMEM;
-  RpGather g{};
-  g.G = (int)grp.size();
-  size_t off = 0;
-  for (int i = 0; i < g.G; i++) {
-    const fts_rp_batch* b = grp[i]->b;
-    g.raw[i] = b->raw;
-    g.sc[i] = b->sc;
-    g.status0[i] = b->status0;
-    g.ipa[i] = b->ipa_flag;
-    g.off[i] = (int)off;
-    off += (size_t)b->B;
+  std::vector<RpPass> P(m);
+  std::vector<int32_t*> d_status(m, nullptr);
+  std::vector<size_t> Bs(m, 0);
+  rc.assign(m, FTS_API_OK);
+  for (size_t j = 0; j < m; j++) {
+    Lane& L = *lanes[j];
+    const std::vector<RpReq*>& grp = sub[j];
+    auto enq = [&]() -> int {
+      if (grp.size() == 1) {
+        fts_rp_batch* b = grp[0]->b;
+        HIP_OK(hipMemcpyAsync(b->status, b->status0, (size_t)b->B * 4, hipMemcpyDeviceToDevice, L.s));
+        Bs[j] = (size_t)b->B;
+        d_status[j] = b->status;
+        return rp_enqueue(c, L, b->B, b->raw, b->sc, b->status, b->ipa_flag, [] {}, std::vector<int>{0, b->B}, P[j],
+                          nullptr, nullptr);
+      }
+      size_t B = 0;
+      for (RpReq* q : grp) B += (size_t)q->b->B;
+      Workspace& w = L.ws;
+      const size_t Bal = std::max(B, std::min(c->coalesce_max, (size_t)1 << 20));  // sized once for the largest pass
+      if (w.rp_raw.ensure(Bal * npts * 64) || w.rp_sc.ensure(Bal * RP_NSC * 32) || w.rp_status.ensure(Bal * 4) ||
+          w.rp_ipa.ensure(Bal * 4))
+        return FTS_API_ENOMEM;
+      RpGather g{};
+      g.G = (int)grp.size();
+      size_t off = 0;
+      for (int i = 0; i < g.G; i++) {
+        const fts_rp_batch* b = grp[i]->b;
+        g.raw[i] = b->raw;
+        g.sc[i] = b->sc;
+        g.status0[i] = b->status0;
+        g.ipa[i] = b->ipa_flag;
+        g.off[i] = (int)off;
+        off += (size_t)b->B;
+      }
+      g.off[g.G] = (int)off;
+      launch_rp_gather(g, c->k, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
+                       w.rp_ipa.as<int32_t>(), L.s);
+      Bs[j] = B;
+      d_status[j] = w.rp_status.as<int32_t>();
+      return rp_enqueue(c, L, (int)B, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
+                        w.rp_ipa.as<int32_t>(), [] {}, std::vector<int>(g.off, g.off + g.G + 1), P[j]);
+    };
+    rc[j] = enq();
   }
-  g.off[g.G] = (int)off;
-  launch_rp_gather(g, c->k, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
-                   w.rp_ipa.as<int32_t>(), L.s);
-  std::vector<int> bounds(g.off, g.off + g.G + 1);
-  int rc = rp_pipeline(c, L, (int)B, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
-                       w.rp_ipa.as<int32_t>(), [] {}, bounds);
-  if (rc != FTS_API_OK) return rc;
-  int32_t* pst = L.status_buf(B);
-  if (!pst) return FTS_API_ENOMEM;
-  HIP_OK(hipMemcpyAsync(pst, w.rp_status.as<int32_t>(), B * 4, hipMemcpyDeviceToHost, L.s));
-  HIP_OK(L.sync());
-  off = 0;
-  for (RpReq* q : grp) {
-    if (q->status) memcpy(q->status, pst + off, (size_t)q->b->B * 4);
-    off += (size_t)q->b->B;
-    collect_timings(c, L, q->b);
-    q->b->merged = (int)grp.size();
+  for (size_t j = 0; j < m; j++) {
+    Lane& L = *lanes[j];
+    if (rc[j] != FTS_API_OK) {
+      (void)L.sync();  // drain whatever was enqueued before the failure
+      continue;
+    }
+    auto fin = [&]() -> int {
+      if (int r = rp_finish(c, L, P[j])) return r;
+      int32_t* pst = L.status_buf(Bs[j]);
+      if (!pst) return FTS_API_ENOMEM;
+      HIP_OK(hipMemcpyAsync(pst, d_status[j], Bs[j] * 4, hipMemcpyDeviceToHost, L.s));
+      HIP_OK(L.sync());
+      size_t off = 0;
+      for (RpReq* q : sub[j]) {
+        if (q->status) memcpy(q->status, pst + off, (size_t)q->b->B * 4);
+        off += (size_t)q->b->B;
+        collect_timings(c, L, q->b);
+        q->b->merged = (int)sub[j].size();
+      }
+      return FTS_API_OK;
+    };
+    rc[j] = fin();
   }
-  return FTS_API_OK;
 }
 
 extern "C" {
@@ -1452,17 +1497,21 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
       c->pending_proofs -= (size_t)q->b->B;
       c->rp_pending.pop_front();
     }
+    std::vector<Lane*> lanes{L};
+    std::vector<std::vector<RpReq*>> sub{grp};
     // the next head (if any) may lead a pass on another free lane
     if (!c->rp_pending.empty() && !c->free_lanes.empty()) c->rp_pending.front()->cv.notify_one();
     lk.unlock();
-    const int rc = run_rp_group(c, *L, grp);
+    std::vector<int> rcs;
+    run_rp_groups(c, lanes, sub, rcs);
     lk.lock();
-    for (RpReq* q : grp) {
-      q->rc = rc;
-      q->done = true;
-      if (q != &me) q->cv.notify_one();
-    }
-    c->free_lanes.push_back(L->id);
+    for (size_t j = 0; j < sub.size(); j++)
+      for (RpReq* q : sub[j]) {
+        q->rc = rcs[j];
+        q->done = true;
+        if (q != &me) q->cv.notify_one();
+      }
+    for (Lane* x : lanes) c->free_lanes.push_back(x->id);
     c->wake_lane_waiters();
   }
   return me.rc;
@@ -1560,6 +1609,44 @@ int fts_msm_stage(fts_ctx* c, size_t n, const uint8_t* points64, const uint8_t* 
   if (nbad) {  // a point failed NewG1FromBytes (flags, range, on-curve)
     fts_msm_free(b);
     return FTS_API_EINVAL;
+  }
+  *out = b;
+  return FTS_API_OK;
+}
+
+int fts_msm_stage_multiples(fts_ctx* c, size_t n, const uint8_t* k32, const uint8_t* scalars32, fts_msm_batch** out) {
+  if (c && !c->shards.empty()) return fts_msm_stage_multiples(c->shards[0], n, k32, scalars32, out);
+  if (!c || !out || !n || !k32 || !scalars32 || n > (size_t)(1u << 26)) return FTS_API_EINVAL;
+  if (c->device < 0) return FTS_API_EDEVICE;
+  HIP_OK(hipSetDevice(c->device));
+  fts_msm_batch* b = new fts_msm_batch();
+  b->N = (int)n;
+  b->device = c->device;
+  uint8_t *rk = nullptr, *rs = nullptr;
+  uint32_t* jac = nullptr;
+  if (hipMalloc(&b->pts, n * 64) != hipSuccess || hipMalloc(&b->sc, n * 32) != hipSuccess ||
+      hipMalloc(&b->out, 64) != hipSuccess || hipMalloc(&rk, n * 32) != hipSuccess || hipMalloc(&rs, n * 32) != hipSuccess ||
+      hipMalloc(&jac, n * 96) != hipSuccess) {
+    for (void* p : {(void*)rk, (void*)rs, (void*)jac})
+      if (p) hipFree(p);
+    fts_msm_free(b);
+    return FTS_API_ENOMEM;
+  }
+  hipError_t e = hipMemcpy(rk, k32, n * 32, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(rs, scalars32, n * 32, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    // B = the PP's ped[1] (table slot tb_G): a generator of G1
+    launch_msm_gen_points((int)n, rk, rs, c->d_tables + (size_t)tb_G(c->n) * fb_words_per_base(), jac, b->pts, b->sc,
+                          nullptr);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  hipFree(rk);
+  hipFree(rs);
+  hipFree(jac);
+  if (e != hipSuccess) {
+    fts_msm_free(b);
+    return FTS_API_EDEVICE;
   }
   *out = b;
   return FTS_API_OK;

@@ -28,9 +28,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/fts_gpu.h"
@@ -352,6 +354,82 @@ FTS_DEV bool decode_g2<FbnCurve>(const uint8_t* raw, pair::F2<pair::FbnField>& x
   return g2_on_twist<pair::FbnField>(x, y);
 }
 
+// ---------------------------------------------------- BN254 G2 subgroup check
+// gnark-crypto's G2Affine.SetBytes (under mathlib's NewG2FromBytes) rejects twist
+// points outside the order-r subgroup; the twist's cofactor is not 1, so decode_g2's
+// on-twist check alone fails open.  [r - 1] Q == -Q  <=>  [r] Q == O, by
+// double-and-add over Jacobian Fp2 coordinates with complete handling of the
+// exceptional additions (points of small order hit them).
+template <class B>
+struct G2J {
+  pair::F2<B> x, y, z;
+};
+template <class B>
+FTS_DEV void g2j_dbl(G2J<B>& p) {  // dbl-2009-l (a = 0); the identity (z = 0) stays the identity
+  using namespace pair;
+  const F2<B> A = sqr(p.x), Bq = sqr(p.y), C = sqr(Bq);
+  const F2<B> D = dbl(sub(sub(sqr(add(p.x, Bq)), A), C));
+  const F2<B> E = add(dbl(A), A);
+  const F2<B> X3 = sub(sqr(E), dbl(D));
+  const F2<B> Y3 = sub(mul(E, sub(D, X3)), dbl(dbl(dbl(C))));
+  p.z = dbl(mul(p.y, p.z));
+  p.x = X3;
+  p.y = Y3;
+}
+template <class B>
+FTS_DEV void g2j_madd(G2J<B>& p, const pair::F2<B>& qx, const pair::F2<B>& qy) {  // madd-2007-bl, complete
+  using namespace pair;
+  if (is_zero(p.z)) {
+    p.x = qx, p.y = qy, p.z = f2_one<B>();
+    return;
+  }
+  const F2<B> Z1Z1 = sqr(p.z);
+  const F2<B> U2 = mul(qx, Z1Z1), S2 = mul(mul(qy, p.z), Z1Z1);
+  const F2<B> H = sub(U2, p.x), r = sub(S2, p.y);
+  if (is_zero(H)) {
+    if (is_zero(r)) g2j_dbl(p);  // p == q
+    else p.z = f2_zero<B>();     // p == -q
+    return;
+  }
+  const F2<B> HH = sqr(H), I = dbl(dbl(HH)), J = mul(H, I), rr = dbl(r), V = mul(p.x, I);
+  const F2<B> X3 = sub(sub(sqr(rr), J), dbl(V));
+  const F2<B> Y3 = sub(mul(rr, sub(V, X3)), dbl(mul(p.y, J)));
+  p.z = sub(sub(sqr(add(p.z, H)), Z1Z1), HH);
+  p.x = X3;
+  p.y = Y3;
+}
+// (qx, qy) affine Montgomery on the twist, not the identity
+FTS_DEV bool g2_in_subgroup_bn(const pair::F2<pair::BnField>& qx, const pair::F2<pair::BnField>& qy) {
+  using namespace pair;
+  using B = BnField;
+  // r - 1 of BN254 (254 bits, little-endian words)
+  constexpr uint32_t RM1[8] = {0xf0000000u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
+                               0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  G2J<B> acc{f2_zero<B>(), f2_one<B>(), f2_zero<B>()};
+#pragma unroll 1
+  for (int bit = 253; bit >= 0; bit--) {
+    g2j_dbl(acc);
+    if ((RM1[bit >> 5] >> (bit & 31)) & 1u) g2j_madd(acc, qx, qy);
+  }
+  if (is_zero(acc.z)) return false;
+  const F2<B> z2 = sqr(acc.z), z3 = mul(z2, acc.z);
+  return eq(acc.x, mul(qx, z2)) && eq(acc.y, neg(mul(qy, z3)));
+}
+
+// U distinct epoch keys (128 raw bytes each, BN254): ok[u] <- the key decodes (on the
+// twist, canonical) and lies in the subgroup (the identity does)
+__global__ void __launch_bounds__(64) k_idv_g2_check(int U, const uint8_t* __restrict__ keys, int32_t* __restrict__ ok) {
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= U) return;
+  pair::F2<pair::BnField> x, y;
+  const uint8_t* kr = keys + (size_t)u * 128;
+  bool good = decode_g2<BnCurve>(kr, x, y);
+  bool zero = true;
+  for (int q = 0; q < 128; q++) zero = zero && kr[q] == 0;
+  if (good && !zero) good = g2_in_subgroup_bn(x, y);
+  ok[u] = good ? 1 : 0;
+}
+
 // ----------------------------------------------------------------- kernels
 // lines of W (lane 0) and g2 (lane 1); wraw: W as 128 raw bytes; ok[0] <- W valid
 template <class CV>
@@ -366,6 +444,12 @@ __global__ void __launch_bounds__(64) k_idv_lines(const uint8_t* __restrict__ wr
     if (!decode_g2<CV>(wraw, qx, qy) || (pair::is_zero(qx) && pair::is_zero(qy))) {
       ok[0] = 0;
       return;
+    }
+    if constexpr (std::is_same<CV, BnCurve>::value) {  // gnark SetBytes: subgroup check
+      if (!g2_in_subgroup_bn(qx, qy)) {
+        ok[0] = 0;
+        return;
+      }
     }
     ok[0] = 1;
   } else {
@@ -385,7 +469,8 @@ __global__ void __launch_bounds__(256) k_idv_tvals(int n, const uint32_t* __rest
                                                    const uint32_t* __restrict__ ipk_hash,  // 8 BE words
                                                    uint32_t* __restrict__ scratch, uint8_t* __restrict__ msg,
                                                    uint32_t* __restrict__ pin, int32_t* __restrict__ zk,
-                                                   int32_t* __restrict__ status) {
+                                                   int32_t* __restrict__ status, const int32_t* __restrict__ eidx,
+                                                   const int32_t* __restrict__ g2ok) {
   using B = typename CV::B;
   using F = typename CV::F;
   using PJ = typename CV::PJ;
@@ -428,6 +513,8 @@ __global__ void __launch_bounds__(256) k_idv_tvals(int n, const uint32_t* __rest
   {
     pair::F2<B> ex, ey;
     all = all && decode_g2<CV>(epk + (size_t)i * 128, ex, ey);
+    // BN254: the key's subgroup check, once per distinct key (k_idv_g2_check)
+    if (g2ok) all = all && g2ok[eidx[i]] != 0;
   }
   if (!all || (flags & F_LATE_MALFORMED)) {
     status[i] = FTS_E_ID_MALFORMED;
@@ -1094,14 +1181,17 @@ int fts_idemix_identity_verify_batch(fts_idemix_idv* K, size_t n, const uint8_t*
   } guard{K, k};
   Slot& D = K->slot[k];
   ICHK(hipSetDevice(K->device));
-  // staged (host + device): rec | pts | epk | status; device only: zk | pin | scratch | msg
+  // staged (host + device): rec | pts | epk | status | eidx | distinct epoch keys (BN254);
+  // device only: zk | pin | scratch | msg | g2ok
   const size_t rec_b = n * REC_STRIDE * 4, pts_b = n * NPT * 64, epk_b = n * 128, st_b = n * 4;
-  const size_t o_pts = rec_b, o_epk = o_pts + pts_b, o_st = o_epk + epk_b;
-  const size_t h_need = (o_st + st_b + 255) & ~size_t(255);
+  const size_t o_pts = rec_b, o_epk = o_pts + pts_b, o_st = o_epk + epk_b, o_eidx = o_st + st_b,
+               o_uk = o_eidx + n * 4;
+  const size_t h_need = (o_uk + epk_b + 255) & ~size_t(255);
   const size_t o_zk = h_need, o_pin = (o_zk + n * 4 + 255) & ~size_t(255), o_scr = o_pin + n * 32 * 4;
   const size_t scr_w = (size_t)(5 * 24 + AT_WORDS + NPT * 16) * n;
   const size_t o_msg = (o_scr + scr_w * 4 + 255) & ~size_t(255);
-  const size_t d_need = o_msg + (size_t)MSG_MAX * n;
+  const size_t o_g2ok = (o_msg + (size_t)MSG_MAX * n + 255) & ~size_t(255);
+  const size_t d_need = o_g2ok + n * 4;
   if (D.h_cap < h_need) {
     if (D.h_buf) (void)hipHostFree(D.h_buf);
     D.h_buf = nullptr, D.h_cap = 0;
@@ -1123,8 +1213,48 @@ int fts_idemix_identity_verify_batch(fts_idemix_idv* K, size_t n, const uint8_t*
           parse_identity(ids[i], id_len[i], bn, rmod, reinterpret_cast<uint32_t*>(h) + i * REC_STRIDE,
                          h + o_pts + i * NPT * 64, h + o_epk + i * 128);
   });
+  // BN254 epoch keys: one subgroup check per DISTINCT key (honest batches carry one)
+  size_t U = 0;
+  int32_t* eidx = reinterpret_cast<int32_t*>(h + o_eidx);
+  if (bn) {
+    const uint8_t* E = h + o_epk;
+    uint8_t* UK = h + o_uk;
+    std::atomic<bool> same{true};
+    host_parallel_for(nch, [&](size_t c) {
+      for (size_t i = c * CH; i < std::min(n, (c + 1) * CH) && same.load(std::memory_order_relaxed); i++)
+        if (memcmp(E + i * 128, E, 128) != 0) same = false;
+    });
+    if (same) {
+      memcpy(UK, E, 128);
+      std::fill(eidx, eidx + n, 0);
+      U = 1;
+    } else {  // sort by (hash, bytes), then one entry per run of equal keys
+      std::vector<std::pair<uint64_t, uint32_t>> hk(n);
+      for (size_t i = 0; i < n; i++) {
+        uint64_t x = 0x9e3779b97f4a7c15ull;
+        for (int q = 0; q < 16; q++) {
+          uint64_t w;
+          memcpy(&w, E + i * 128 + 8 * q, 8);
+          x = (x ^ w) * 0xff51afd7ed558ccdull;
+          x ^= x >> 29;
+        }
+        hk[i] = {x, (uint32_t)i};
+      }
+      std::sort(hk.begin(), hk.end(), [&](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) {
+        if (a.first != b.first) return a.first < b.first;
+        return memcmp(E + (size_t)a.second * 128, E + (size_t)b.second * 128, 128) < 0;
+      });
+      for (size_t j = 0; j < n; j++) {
+        const uint32_t i = hk[j].second;
+        if (j == 0 || hk[j].first != hk[j - 1].first ||
+            memcmp(E + (size_t)i * 128, E + (size_t)hk[j - 1].second * 128, 128) != 0)
+          memcpy(UK + 128 * U++, E + (size_t)i * 128, 128);
+        eidx[i] = (int32_t)(U - 1);
+      }
+    }
+  }
   uint8_t* d = D.d_buf;
-  ICHK(hipMemcpyAsync(d, h, h_need, hipMemcpyHostToDevice, D.stream));
+  ICHK(hipMemcpyAsync(d, h, o_uk + U * 128, hipMemcpyHostToDevice, D.stream));
   ICHK(hipEventRecord(D.ev[0], D.stream));
   const unsigned g256 = (unsigned)((n + 255) / 256), g64 = (unsigned)((n + 63) / 64);
   const uint32_t* rec = reinterpret_cast<const uint32_t*>(d);
@@ -1133,14 +1263,17 @@ int fts_idemix_identity_verify_batch(fts_idemix_idv* K, size_t n, const uint8_t*
   int32_t* zk = reinterpret_cast<int32_t*>(d + o_zk);
   int32_t* st = reinterpret_cast<int32_t*>(d + o_st);
   const size_t nl = (size_t)nlines(bn) * pair::LINE_WORDS;
+  int32_t* g2ok = reinterpret_cast<int32_t*>(d + o_g2ok);
   if (bn) {
+    k_idv_g2_check<<<(unsigned)((U + 63) / 64), 64, 0, D.stream>>>((int)U, d + o_uk, g2ok);
     k_idv_tvals<BnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, d + o_pts, d + o_epk, K->d_tables, K->d_hash, scr,
-                                                      d + o_msg, pin, zk, st);
+                                                      d + o_msg, pin, zk, st, reinterpret_cast<const int32_t*>(d + o_eidx),
+                                                      g2ok);
     ICHK(hipEventRecord(D.ev[1], D.stream));
     k_idv_pairing<BnCurve><<<g64, 64, 0, D.stream>>>((int)n, pin, K->d_lines, zk, st);
   } else {
     k_idv_tvals<FbnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, d + o_pts, d + o_epk, K->d_tables, K->d_hash, scr,
-                                                       d + o_msg, pin, zk, st);
+                                                       d + o_msg, pin, zk, st, nullptr, nullptr);
     ICHK(hipEventRecord(D.ev[1], D.stream));
     k_idv_pairing<FbnCurve><<<g64, 64, 0, D.stream>>>((int)n, pin, K->d_lines, zk, st);
   }

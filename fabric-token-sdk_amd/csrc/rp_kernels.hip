@@ -2,22 +2,26 @@
 //
 // One launch sequence verifies a whole batch of B proofs of bit length n
 // (k = log2 n rounds).  Work is laid out per (proof, item) so a batch of a
-// few thousand proofs fills the 256 CUs.  Stream S is the batch's main
-// stream, S2 its side stream (fork/join through events):
+// few thousand proofs fills the 256 CUs.  Streams of a lane: S main, S2 the
+// x0 prefix (work path) / x*D (latency path), S3 the batch check's weights and
+// MSM, S4 its x0-free fixed-base columns (fork/join through events).
+// Work path (passes above FTS_COM_FIXED_MAX proofs):
 //
 //   S   k_rp_decode        (proof, point)   NewG1FromBytes checks + Montgomery form
 //   S   k_rp_hash_small    (proof, msg)     x, y, x_j transcripts (SHA-256 over hex)  bulletproof.go:266-281, ipa.go:230
 //   S   k_rp_chal_fr       proof            z, polEval, batch inversion of y, x_j       bulletproof.go:282-311, ipa.go:236-244
+//   S   k_rp_powers        (chunk, proof)   y^-i, s_i, z^2 2^i y^-i                     ipa.go:343-356 (unrolled)
 //   S   k_rp_fixed_exact   (proof, item)    H'_i = y^-i H_i, z K, -delta P (fixed base) bulletproof.go:483-489
+//   S   k_rp_normalize     point (block)    batch affine normalisation of H'_i (one inversion per block)
 //   S   k_rp_hsum_chunks   (proof, chunk)   S_c = sum_j 2^j H'_{16c+j} (Horner)
-//   S   k_rp_com_var       2 lanes/proof    S = sum_c 2^(16c) S_c, then x*D + z^2*S
-//                                           (joint GLV/Straus over affine lane tables)
-//   S   (k_rp_com_var)     lane pair        com = C + z K - delta P + x D + z^2 S       bulletproof.go:477-492
-//   S   k_rp_normalize     point (block)    batch affine normalisation of H'_i and com (one inversion per 256 points)
-//   S2  k_rp_x0_build      (proof, record)  DER(hex(H'..., G..., Q, com) "||" Zb(ip))   ipa.go:200-212
-//   S2  k_rp_x0_hash       proof            x0 = HashToZr(...)                          ipa.go:213
-//   S2  k_rlc_columns/fixed                 fixed-base columns of the batch equation (need x0)
-//   S   k_rlc_prep + MSM                    variable points of the batch equation (no x0)
+//   S   k_rp_hsum_join     proof            S = sum_c 2^(16c) S_c
+//   S   k_rp_com_var       2 lanes/proof    x*D + z^2*S (joint GLV/Straus, affine lane tables),
+//                                           com = C + z K - delta P + x D + z^2 S       bulletproof.go:477-492
+//   S2  k_rp_x0_build/hash proof            x0 prefix: H' records + shared template     ipa.go:200-213
+//   S   k_rp_x0_build/hash proof            x0 suffix after com: x0 = HashToZr(...)     ipa.go:213
+//   S3  k_rlc_prep + MSM                    weights, variable points of the batch equation (no x0)
+//   S4  k_rlc_columns/fixed                 x0-free fixed-base columns of the batch equation
+//   S   k_rlc_columns/fixed (Q), finalize   column Q (needs x0), verdict
 //   k_rp_terms_fixed / k_rp_terms_var / k_rp_check: per-proof fallback
 //
 #include "device/g1.hpp"
@@ -337,8 +341,8 @@ __global__ void __launch_bounds__(64) k_rp_powers(int B, int n, int k, const int
 // Terms per proof (com_terms): 0 z*K, 1 -delta*P, 2,3 the GLV halves of x*D,
 // 4,5 the GLV halves of z^2*S.
 constexpr int COM_NTERMS = 4;  // z K, -delta P, the two joint GLV halves
-// Horner chunks of S = sum_i 2^i H'_i: 16 H' per chunk (4 chunks at n = 64);
-// k_rp_com_var joins them in both of a proof's lanes
+// Horner chunks of S = sum_i 2^i H'_i: 16 H' per chunk (4 chunks at n = 64),
+// joined once per proof by k_rp_hsum_join (slot 0 of the proof's chunks)
 constexpr int HS_CHUNK = 16;
 constexpr int HS_SCRATCH = 4 * 24;  // scratch words per proof for the chunks (n <= 64)
 inline __host__ __device__ int com_nterms(int n) { return COM_NTERMS; }
@@ -407,12 +411,28 @@ __global__ void __launch_bounds__(256) k_rp_hsum_chunks(int B, int n, const int3
   store_g1j(chunks + (size_t)gid * 24, acc);
 }
 
+// lane per proof: S = sum_c 2^(16c) S_c (Horner over k_rp_hsum_chunks' chunk sums,
+// 3 x (16 doublings + 1 addition) at n = 64) -> slot 0 of the proof's chunks.
+// Once per proof: the two lanes of k_rp_com_var used to join S each, 17 % of
+// their chain
+__global__ void __launch_bounds__(256) k_rp_hsum_join(int B, int n, const int32_t* __restrict__ status,
+                                                     uint32_t* __restrict__ chunks) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B || status[b] != 0) return;
+  const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
+  uint32_t* Sc = chunks + (size_t)b * nc * 24;
+  G1J S = load_g1j(Sc + (nc - 1) * 24);
+  for (int c = nc - 2; c >= 0; c--) {
+    for (int q = 0; q < HS_CHUNK; q++) S = g1j_dbl(S);
+    add_inl(S, load_g1j(Sc + c * 24));
+  }
+  store_g1j(Sc, S);
+}
+
 // x*D + z^2*S (bulletproof.go:478, 486-489 via S), two lanes per proof: with
 // x = x1 + x2 lambda and z^2 = w1 + w2 lambda (GLV), lane h computes
 // x_h phi^h(D) + w_h phi^h(S) in one joint Straus chain over an affine lane
-// table (glv.hpp straus2_atab).  Both lanes first join S = sum_c 2^(16c) S_c
-// from k_rp_hsum_chunks' Horner chunks (3 x (16 doublings + 1 addition) at
-// n = 64; no separate one-lane-per-proof join launch) -> terms[b][2 + h]
+// table (glv.hpp straus2_atab); S from k_rp_hsum_join -> terms[b][2 + h]
 #ifndef FTS_COMVAR_OCC
 #define FTS_COMVAR_OCC 3  // waves per SIMD the register budget allows (A/B builds: -DFTS_COMVAR_OCC=4)
 #endif
@@ -430,14 +450,8 @@ __global__ void __launch_bounds__(256, FTS_COMVAR_OCC) k_rp_com_var(int B, int n
   uint32_t xk[2][4], xs[2], wk[2][4], ws[2];
   glv_decompose(fr_canon(x).v, xk[0], xs[0], xk[1], xs[1]);
   glv_decompose(fr_canon(z2).v, wk[0], ws[0], wk[1], ws[1]);
-  // S = sum_c 2^(16c) S_c (Horner over the chunk sums)
   const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
-  const uint32_t* Sc = chunks + (size_t)b * nc * 24;
-  G1J S = load_g1j(Sc + (nc - 1) * 24);
-  for (int c = nc - 2; c >= 0; c--) {
-    for (int q = 0; q < HS_CHUNK; q++) S = g1j_dbl(S);
-    add_inl(S, load_g1j(Sc + c * 24));
-  }
+  G1J S = load_g1j(chunks + (size_t)b * nc * 24);  // k_rp_hsum_join
   const G1A Da = load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_D) * 16);
   const bool idD = g1a_is_identity(Da), idS = f_is_zero(S.z);
   G1J D = g1j_from_affine(Da);
@@ -1579,11 +1593,12 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     const int nch = (n + HS_CHUNK - 1) / HS_CHUNK;
     FTS_LAUNCH(k_rp_hsum_chunks, B * nch, g_chain_bs, s, B, n, d.status, d.hpa, d.scratch);
     tl->mark("k_rp_hsum_chunks", s, (double)B * (n - nch) * (COST_DBL + COST_MADD));
+    FTS_LAUNCH(k_rp_hsum_join, B, g_chain_bs, s, B, n, d.status, d.scratch);
+    tl->mark("k_rp_hsum_join", s, (double)B * (nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD));
     // scratch: [0, B*HS_SCRATCH) Horner chunks of S, then the 2B lanes' affine tables
     FTS_LAUNCH(k_rp_com_var, 2 * B, g_chain_bs, s, B, n, k, d.status, d.pts, d.ch, d.scratch,
                d.scratch + (size_t)B * HS_SCRATCH, d.terms, d.hpj);
-    tl->mark("k_rp_com_var", s,
-             (double)B * 2 * ((nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD) + COST_STRAUS2_ATAB + 2.5 * COST_ADD));
+    tl->mark("k_rp_com_var", s, (double)B * 2 * (COST_STRAUS2_ATAB + 2.5 * COST_ADD));
   }
   launch_normalize(B, 1, n + 1, n, d.status, d.hpj, d.hpa, d.hp_be, s);
   tl->mark("k_rp_normalize_com", s, (double)B * (2.0 * 8.0 / NORM_E + 9.0));
@@ -1674,6 +1689,43 @@ void launch_rlc_group_test(const RpBatchDev& d, const RlcDev& r, const uint32_t*
   tl->mark("k_rlc_group_final", s, 0);
 }
 
+}  // namespace fts
+
+namespace fts {
+// Config C3 staging (fts_msm_stage_multiples): N distinct points P_i = k_i * B
+// from a fixed-base table (16-bit windows), k_i = 32-byte BE integers mod r,
+// as Jacobian into jac (normalised by the caller), and the MSM scalars s_i
+// (BE, reduced mod r as G1.Mul does) as canonical limbs
+__global__ void __launch_bounds__(256) k_msm_gen_points(int N, const uint8_t* __restrict__ raw_k,
+                                                       const uint8_t* __restrict__ raw_s,
+                                                       const uint32_t* __restrict__ table, uint32_t* __restrict__ jac,
+                                                       uint32_t* __restrict__ sc) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  auto be_fr = [](const uint8_t* p) {
+    uint32_t w[8];
+    const uint4* s4 = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const uint4 u = s4[q];
+      w[4 * q + 0] = __builtin_bswap32(u.x);
+      w[4 * q + 1] = __builtin_bswap32(u.y);
+      w[4 * q + 2] = __builtin_bswap32(u.z);
+      w[4 * q + 3] = __builtin_bswap32(u.w);
+    }
+    return digest_to_fr(w);  // canonical limbs mod r
+  };
+  const Fr k = be_fr(raw_k + (size_t)i * 32), sv = be_fr(raw_s + (size_t)i * 32);
+  Scalar ks;
+#pragma unroll
+  for (int q = 0; q < 8; q++) ks.v[q] = k.v[q], sc[(size_t)i * 8 + q] = sv.v[q];
+  store_g1j(jac + (size_t)i * 24, fb_mul(table, ks));
+}
+void launch_msm_gen_points(int N, const uint8_t* raw_k, const uint8_t* raw_s, const uint32_t* table, uint32_t* jac,
+                           uint32_t* pts, uint32_t* sc, hipStream_t s) {
+  FTS_LAUNCH(k_msm_gen_points, N, 256, s, N, raw_k, raw_s, table, jac, sc);
+  launch_normalize(N, 1, 1, 0, (const int32_t*)nullptr, jac, pts, (uint8_t*)nullptr, s);
+}
 }  // namespace fts
 
 namespace fts {

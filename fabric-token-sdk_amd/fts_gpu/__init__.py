@@ -171,6 +171,10 @@ class PublicParams:
     def stage_msm(self, points, scalars):
         return StagedMsm(self, points, scalars)
 
+    def stage_msm_multiples(self, ks, scalars):
+        """n distinct points k_i * ped1 generated on the device (ks: 32-byte BE each)"""
+        return StagedMsm(self, None, scalars, multiples=ks)
+
     def verify_transfers(self, transfers):
         """transfers: list of (inputs[list of 64B], outputs[list], proof bytes) ->
         (status, fail_index) arrays."""
@@ -471,12 +475,21 @@ class ActionBatch:
 class StagedMsm:
     """MSM inputs validated and resident in HBM; ``run()`` is the device MSM only."""
 
-    def __init__(self, pp, points, scalars):
+    def __init__(self, pp, points, scalars, multiples=None):
+        """points: n x 64-byte X||Y BE; or, with multiples = n x 32-byte BE k_i and
+        points None, the distinct points k_i * ped1 generated on the device
+        (fts_msm_stage_multiples, config C3 at scale)"""
         self.pp = pp
-        pts = points if isinstance(points, (bytes, bytearray)) else b"".join(points)
         scs = scalars if isinstance(scalars, (bytes, bytearray)) else b"".join(scalars)
-        self.n = len(pts) // 64
         self._b = C.c_void_p()
+        if multiples is not None:
+            ks = multiples if isinstance(multiples, (bytes, bytearray)) else b"".join(multiples)
+            self.n = len(ks) // 32
+            L.check("fts_msm_stage_multiples",
+                    L.lib.fts_msm_stage_multiples(pp._ctx, self.n, ks, scs, C.byref(self._b)))
+            return
+        pts = points if isinstance(points, (bytes, bytearray)) else b"".join(points)
+        self.n = len(pts) // 64
         L.check("fts_msm_stage", L.lib.fts_msm_stage(pp._ctx, self.n, pts, scs, C.byref(self._b)))
 
     def run(self):

@@ -236,6 +236,11 @@ int fts_msm_g1(fts_ctx* ctx, size_t n, const uint8_t* points64, const uint8_t* s
 /* device-resident variant: upload + validate once, run many times */
 int fts_msm_stage(fts_ctx* ctx, size_t n, const uint8_t* points64, const uint8_t* scalars32, fts_msm_batch** out);
 int fts_msm_run(fts_ctx* ctx, fts_msm_batch* b, uint8_t* out64);
+/* config C3 at scale (points k_i G with uniform k_i): n DISTINCT points
+ * P_i = k_i * ped1 (the PP's ped[1], a generator of G1) computed on the device from the
+ * context's fixed-base table, k32 / scalars32: n x 32-byte BE integers used mod r.  The
+ * result of fts_msm_run is then (sum_i s_i k_i mod r) * ped1 (closed form for tests). */
+int fts_msm_stage_multiples(fts_ctx* ctx, size_t n, const uint8_t* k32, const uint8_t* scalars32, fts_msm_batch** out);
 /* per-kernel device time (ms) and algorithmic u32 MADs of b's last run */
 int fts_msm_timings(const fts_msm_batch* b, const char** names, float* ms, double* mads, int cap);
 void fts_msm_free(fts_msm_batch* b);

@@ -1,0 +1,134 @@
+"""GPU: every library knob (FTS_* environment variable read at context creation,
+fts_api.cpp ctx_create) at a non-default value gives the reference's verdicts
+(rp/rangecorrectness.go:141-160) and, where the knob changes the com / x0 code
+path, the same exact intermediates (com, H'_i, x0: ipa.go:200-213).
+
+Knobs covered elsewhere: FTS_LANES, FTS_COM_FIXED_MAX (test_gpu_rp.py,
+test_gpu_scale.py), FTS_GT1 / FTS_GT2_MIN / FTS_GT_ADAPT (test_gpu_scale.py),
+FTS_NYM_TILE (test_idemix.py).  Here: FTS_RLC_FORK, FTS_X0_SPLIT,
+FTS_COALESCE_MAX, FTS_GATHER_US."""
+import json
+import os
+import random
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+from oracle import bn254 as bn, zkat
+
+pytestmark = pytest.mark.gpu
+
+with open(os.path.join(GOLDEN, "rp_golden.json")) as f:
+    RP_GOLDEN = json.load(f)
+STATUS_OF = {None: 0, "invalid range proof": 3, "invalid IPA": 6, "invalid range proof: nil elements": 2,
+             "invalid IPA proof: nil elements": 4, "invalid IPA proof": 5}
+
+
+def _ctx(pp_raw, bits, **env):
+    import fts_gpu
+    env = {k: str(v) for k, v in env.items()}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return fts_gpu.PublicParams(pp_raw, bit_length=bits, device=0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _golden_check(pp, bits, work_path):
+    from test_gpu_rp import _intermediates
+    cases = [c for c in RP_GOLDEN if c["bits"] == bits]
+    st = pp.verify_range_proofs([bytes.fromhex(c["proof"]) for c in cases],
+                                [bytes.fromhex(c["commitment"]) for c in cases])
+    assert [int(s) for s in st] == [STATUS_OF[c["expect"]] for c in cases]
+    lt = pp.last_timings()
+    assert ("k_rp_com_var" in lt) == work_path and ("k_rp_fixed_all" in lt) == (not work_path), sorted(lt)
+    for i, c in enumerate(cases):
+        vals, com, hp = _intermediates(pp, i)
+        if "com" in c:
+            assert com.hex() == c["com"] and [h.hex() for h in hp] == c["hprime"] and vals[7] == int(c["x0"])
+
+
+@pytest.mark.parametrize("fork", [0, 1])
+@pytest.mark.parametrize("work_path", [False, True])
+def test_knob_rlc_fork(pp_raw, fork, work_path):
+    """FTS_RLC_FORK=0/1 (default 2 = adaptive): the batch check forks after the
+    challenges or after the fixed-base products, on both com paths"""
+    env = dict(FTS_RLC_FORK=fork, FTS_LANES=1)
+    if work_path:
+        env["FTS_COM_FIXED_MAX"] = 0
+    pp = _ctx(pp_raw, 32, **env)
+    try:
+        _golden_check(pp, 32, work_path)
+    finally:
+        pp.close()
+
+
+def test_knob_x0_split_off(pp_raw):
+    """FTS_X0_SPLIT=0: the work path hashes the whole x0 message after com (no
+    prefix midstate on the side stream) -- the same x0 bytes"""
+    pp = _ctx(pp_raw, 32, FTS_X0_SPLIT=0, FTS_COM_FIXED_MAX=0, FTS_LANES=1)
+    try:
+        _golden_check(pp, 32, True)
+    finally:
+        pp.close()
+
+
+def _tampered_batches(pp, nb, per, seed):
+    rng = random.Random(seed)
+    R = bn.R
+    vals = [rng.getrandbits(32) for _ in range(per)]
+    bfs = [rng.randrange(R).to_bytes(32, "big") for _ in range(per)]
+    proofs, coms = pp.prove_range_batch_gpu(vals, bfs, seed=seed)
+    out = []
+    for b in range(nb):
+        ps, want = list(proofs), np.zeros(per, dtype=np.int32)
+        for q, i in enumerate(rng.sample(range(per), 3)):
+            t = zkat.RangeProof.deserialize(ps[i])
+            if q == 0:
+                t.data.T1 = bn.g1_add(t.data.T1, bn.GEN)
+                want[i] = 3
+            else:
+                t.ipa.L[q] = bn.g1_add(t.ipa.L[q], bn.GEN)
+                want[i] = 6
+            ps[i] = t.serialize()
+        out.append((pp.stage_range_proofs(ps, coms), want))
+    return out
+
+
+@pytest.mark.parametrize("env", [
+    dict(FTS_COALESCE_MAX=4096, FTS_GATHER_US=3000),   # small coalescing cap, long gather window
+    dict(FTS_GATHER_US=0),                             # no gather window
+], ids=["coalesce4096", "gather0"])
+def test_knob_coalescing(pp_raw, env):
+    """8 staged batches of 512 rp32 (3 tampered each) verified concurrently from 8
+    threads: however the dispatcher groups them (coalesced passes up to the cap,
+    lone passes), every batch gets its own exact verdicts"""
+    pp = _ctx(pp_raw, 32, FTS_LANES=4, FTS_COM_FIXED_MAX=0, **env)
+    try:
+        batches = _tampered_batches(pp, 8, 512, 0xC0A1)
+        for rep in range(3):
+            res = [None] * len(batches)
+            gate = threading.Barrier(len(batches))
+
+            def run(j):
+                gate.wait()
+                res[j] = (batches[j][0].verify(), batches[j][0].merged())
+            th = [threading.Thread(target=run, args=(j,)) for j in range(len(batches))]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            for (st, merged), (_, want) in zip(res, batches):
+                assert (st == want).all(), (rep, np.nonzero(st != want)[0][:8], merged)
+        for b, _ in batches:
+            b.close()
+    finally:
+        pp.close()

@@ -104,3 +104,25 @@ def test_msm_2p20_linearity_and_identity(gpu_pp):
     sl = slice(lo, lo + 300)
     got = pp.msm(pts[64 * lo:64 * (lo + 300)], _scs(a[sl]))
     assert got == bn.g1_bytes(bn.g1_msm([base[i % m] for i in range(lo, lo + 300)], a[sl]))
+
+
+@pytest.mark.parametrize("log", [8, 18])
+def test_msm_distinct_device_points_closed_form(gpu_pp, oracle_pp, log):
+    """config C3 as SURVEY §8(d) specifies it: 2^log DISTINCT points k_i ped1 made on
+    the device (fts_msm_stage_multiples), scalars above r included (used mod r):
+    sum s_i k_i ped1 = (sum s_i k_i mod r) ped1; at 2^8 the points are also compared
+    with the oracle's through the host-staged MSM of the same points"""
+    pp = gpu_pp(64)
+    rng = random.Random(0xC3D0 + log)
+    n = 1 << log
+    ks = [rng.getrandbits(256) for _ in range(n)]
+    ss = [rng.getrandbits(256) for _ in range(n)]
+    st = pp.stage_msm_multiples(_scs(ks), _scs(ss))
+    ped1 = oracle_pp.ped[1]
+    want = bn.g1_bytes(bn.g1_mul(ped1, sum(s * k for s, k in zip(ss, ks)) % bn.R))
+    assert st.run() == want
+    assert st.run() == want  # re-run on the resident inputs
+    st.close()
+    if log == 8:
+        pts = [bn.g1_mul(ped1, k % bn.R) for k in ks]
+        assert pp.msm(_pts(pts), _scs(ss)) == want

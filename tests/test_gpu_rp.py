@@ -81,7 +81,7 @@ def test_golden_work_path_com(pp_raw, bits):
                                 [bytes.fromhex(c["commitment"]) for c in cases])
     assert [int(s) for s in st] == [STATUS_OF[c["expect"]] for c in cases]
     lt = pp.last_timings()
-    assert ("k_rp_com_var" in lt or "k_rp_com_s" in lt) and "k_rp_fixed_all" not in lt
+    assert "k_rp_com_var" in lt and "k_rp_fixed_all" not in lt
     for i, c in enumerate(cases):
         vals, com, hp = _intermediates(pp, i)
         if "com" in c:

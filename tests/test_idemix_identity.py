@@ -118,3 +118,63 @@ def test_large_batch_exact_positions(verifiers, tag):
     assert all(msgs[k] == pool[k][1] for k in msgs)
     t = verifiers[tag].last_kernel_ms()
     assert t[0] > 0 and t[1] > 0
+
+
+def _key(f, wt):
+    k, out = (f << 3) | wt, b""
+    while True:
+        c = k & 0x7F
+        k >>= 7
+        out += bytes([c | (0x80 if k else 0)])
+        if not k:
+            return out
+
+
+def _overlong(f, wt, last):
+    """the key of (f, wt) as a 10-byte varint whose last byte is `last`"""
+    k = (f << 3) | wt
+    body = [(k >> (7 * i)) & 0x7F for i in range(9)]
+    return bytes(b | 0x80 for b in body) + bytes([last])
+
+
+@pytest.mark.parametrize("tag", ["bn254", "fp256bn"])
+def test_identity_proto_wire_edge_cases(verifiers, tag):
+    """protowire semantics of the SerializedIdemixIdentity reader (host/pb.hpp):
+    a 10-byte key varint is accepted when its last byte is 0 or 1 and rejected as an
+    overflow above (protowire.ConsumeVarint); an unknown group field is skipped
+    (ConsumeFieldValue), a group without its end is malformed"""
+    from fts_gpu import idemix as I
+    from oracle import idemix as OI
+    by = {c["name"]: c for c in _doc()[tag]["cases"]}
+    raw = bytes.fromhex(by["honest_1"]["identity"])
+    fields = OI.pb_fields(raw)
+    rebuilt = b"".join(OI.pb_bytes_field(f, v) for f, wt, v in fields)
+    assert rebuilt == raw and all(wt == 2 for _, wt, _ in fields)
+
+    def with_key(i, key):
+        out = b""
+        for j, (f, wt, v) in enumerate(fields):
+            enc = OI.pb_bytes_field(f, v)
+            out += (key + enc[len(_key(f, 2)):]) if j == i else enc
+        return out
+    group = _key(100, 3) + _key(1, 0) + b"\x05" + _key(2, 2) + b"\x01Z" + _key(100, 4)
+    cases = [
+        (with_key(0, _overlong(fields[0][0], 2, 0x00)), 0),                        # overlong, no overflow
+        (with_key(0, _overlong(fields[0][0], 2, 0x02)), I.FTS_E_ID_MALFORMED),     # 10th byte > 1: overflow
+        (with_key(len(fields) - 1, _overlong(fields[-1][0], 2, 0x7F)), I.FTS_E_ID_MALFORMED),
+        (raw + group, 0),                                                          # unknown group skipped
+        (group + raw, 0),
+        (raw + _key(100, 3) + _key(1, 0) + b"\x05", I.FTS_E_ID_MALFORMED),         # group without its end
+        (raw + _key(100, 3) + _key(101, 4), I.FTS_E_ID_MALFORMED),                 # mismatched end group
+        (raw + _key(100, 4), I.FTS_E_ID_MALFORMED),                                # end group alone
+    ]
+    st = verifiers[tag].verify_batch([c for c, _ in cases])
+    assert [int(s) for s in st] == [w for _, w in cases]
+    # the oracle's wire reader agrees on which encodings parse
+    for c, w in cases:
+        try:
+            OI.pb_fields(c)
+            ok = True
+        except ValueError:
+            ok = False
+        assert ok == (w == 0), c.hex()[:40]
