@@ -1311,15 +1311,25 @@ int fts_idemix_pairing_debug(fts_idemix_idv* K, int which, const uint8_t* p64, i
   }
   std::lock_guard<std::mutex> l(K->mu);
   ICHK(hipSetDevice(K->device));
-  uint32_t *d_p = nullptr, *d_o = nullptr;
-  ICHK(hipMalloc(&d_p, 64));
-  ICHK(hipMalloc(&d_o, 192 * 4));
-  ICHK(hipMemcpy(d_p, pm, 64, hipMemcpyHostToDevice));
-  k_idv_pairing_debug<BnCurve><<<1, 64>>>(K->d_lines, which, d_p, d_o, final_exp);
+  // private stream and buffers, released on every exit path
+  struct Res {
+    uint32_t *p = nullptr, *o = nullptr;
+    hipStream_t s = nullptr;
+    ~Res() {
+      if (s) (void)hipStreamSynchronize(s);
+      if (p) (void)hipFree(p);
+      if (o) (void)hipFree(o);
+      if (s) (void)hipStreamDestroy(s);
+    }
+  } r;
+  ICHK(hipStreamCreateWithFlags(&r.s, hipStreamNonBlocking));
+  ICHK(hipMalloc(&r.p, 64));
+  ICHK(hipMalloc(&r.o, 192 * 4));
+  ICHK(hipMemcpyAsync(r.p, pm, 64, hipMemcpyHostToDevice, r.s));
+  k_idv_pairing_debug<BnCurve><<<1, 64, 0, r.s>>>(K->d_lines, which, r.p, r.o, final_exp);
   ICHK(hipGetLastError());
-  ICHK(hipMemcpy(out192, d_o, 192 * 4, hipMemcpyDeviceToHost));
-  (void)hipFree(d_p);
-  (void)hipFree(d_o);
+  ICHK(hipMemcpyAsync(out192, r.o, 192 * 4, hipMemcpyDeviceToHost, r.s));
+  ICHK(hipStreamSynchronize(r.s));
   return FTS_API_OK;
 }
 

@@ -92,7 +92,54 @@ def parse_ecp2(curve_pr, raw):
         return None
     if not curve_pr.g2_on_curve(Q):
         raise I.PointError("G2 point not on curve")
+    if curve_pr is PR.BN254 and not g2_in_subgroup(curve_pr, Q):
+        # gnark-crypto G2Affine.SetBytes (mathlib NewG2FromBytes) checks the subgroup;
+        # AMCL's ECP2_fromBytes (FP256BN) does not
+        raise I.PointError("G2 point not in the r-torsion subgroup")
     return Q
+
+
+def twist_point(curve_pr, x0):
+    """a point of the twist y^2 = x^3 + b' with x = (x0 + k, 1) for the first k that
+    gives a square (any subgroup: the test vectors' off-subgroup points); p = 3 mod 4
+    square root in Fp2 = Fp[u]/(u^2 + 1) (Adj / Rodriguez-Henriquez, algorithm 9)"""
+    p = curve_pr.p
+    assert p % 4 == 3
+
+    def f2pow(a, e):
+        r = (1, 0)
+        while e:
+            if e & 1:
+                r = PR.f2mul(r, a, p)
+            a = PR.f2mul(a, a, p)
+            e >>= 1
+        return r
+    k = 0
+    while True:
+        x = ((x0 + k) % p, 1)
+        a = PR.f2add(PR.f2mul(PR.f2mul(x, x, p), x, p), curve_pr.b2, p)
+        a1 = f2pow(a, (p - 3) // 4)
+        alpha = PR.f2mul(PR.f2mul(a1, a1, p), a, p)
+        a0 = PR.f2mul((alpha[0], (-alpha[1]) % p), alpha, p)  # alpha^p * alpha
+        if a0 != (p - 1, 0):
+            x_0 = PR.f2mul(a1, a, p)
+            if alpha == (p - 1, 0):
+                y = PR.f2mul((0, 1), x_0, p)
+            else:
+                y = PR.f2mul(f2pow(PR.f2add((1, 0), alpha, p), (p - 1) // 2), x_0, p)
+            if PR.f2mul(y, y, p) == a:
+                return (x, y)
+        k += 1
+
+
+def g2_in_subgroup(curve_pr, Q):
+    """[r] Q == O, by double-and-add without reducing the scalar mod r"""
+    acc = None
+    for bit in bin(curve_pr.r)[2:]:
+        acc = curve_pr.g2_add(acc, acc)
+        if bit == "1":
+            acc = curve_pr.g2_add(acc, Q)
+    return acc is None
 
 
 def _varint_field(f, v):

@@ -178,3 +178,53 @@ def test_identity_proto_wire_edge_cases(verifiers, tag):
         except ValueError:
             ok = False
         assert ok == (w == 0), c.hex()[:40]
+
+
+def _with_epoch_key(raw, key_proto):
+    """an identity whose Signature carries another revocation epoch key (field 14);
+    the key is not in the proof's transcript, so only its decoding decides"""
+    from oracle import idemix as OI, idemix_identity as ID
+    outer = OI.pb_fields(raw)
+    out = b""
+    for f, wt, v in outer:
+        if f == 4:
+            sig = b""
+            for sf, swt, sv in OI.pb_fields(v):
+                if sf == 14:
+                    sv = key_proto
+                sig += OI.pb_bytes_field(sf, sv) if swt == 2 else ID._varint_field(sf, sv)
+            v = sig
+        out += OI.pb_bytes_field(f, v)
+    return out
+
+
+def test_bn254_g2_subgroup_checks(verifiers):
+    """gnark-crypto's G2Affine.SetBytes (mathlib NewG2FromBytes, BN254) rejects twist
+    points outside the order-r subgroup: an epoch key on the twist but off the
+    subgroup makes the identity malformed (ADVICE r03), a subgroup key does not;
+    distinct keys in one batch are each checked once (host dedupe), every verdict at
+    its position; an issuer key whose W is off the subgroup is refused"""
+    from fts_gpu import idemix as I
+    from fts_gpu import _lib as L
+    from oracle import idemix as OI, idemix_identity as ID, pairing as PR
+    C = PR.BN254
+    by = {c["name"]: c for c in _doc()["bn254"]["cases"]}
+    honest = bytes.fromhex(by["honest_1"]["identity"])
+    bad = [ID.twist_point(C, x) for x in (7, 1234567)]
+    assert all(C.g2_on_curve(q) and not ID.g2_in_subgroup(C, q) for q in bad)
+    good = [C.g2_gen, C.g2_add(C.g2_gen, C.g2_gen), C.g2_mul(C.g2_gen, 0xC0FFEE)]
+    keys = [(ID.ecp2(C, q), 0) for q in good] + [(ID.ecp2(C, q), I.FTS_E_ID_MALFORMED) for q in bad]
+    ids = [(_with_epoch_key(honest, k), w) for k, w in keys]
+    st = verifiers["bn254"].verify_batch([x for x, _ in ids])
+    assert [int(s) for s in st] == [w for _, w in ids]
+    rng = random.Random(11)
+    pick = [rng.randrange(len(ids)) for _ in range(2000)]
+    st = verifiers["bn254"].verify_batch([ids[k][0] for k in pick])
+    assert [int(s) for s in st] == [ids[k][1] for k in pick]
+    # issuer key with W off the subgroup (field 5 of IssuerPublicKey)
+    ipk = _ipk("bn254_charlie")
+    fields = OI.pb_fields(ipk)
+    w_bad = b"".join(OI.pb_bytes_field(f, ID.ecp2(C, bad[0]) if f == 5 else v) if wt == 2 else ID._varint_field(f, v)
+                     for f, wt, v in fields)
+    with pytest.raises(L.FtsError):
+        I.IdentityVerifier(w_bad, device=0, curve=I.FTS_CURVE_BN254)

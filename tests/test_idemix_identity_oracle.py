@@ -125,3 +125,22 @@ def test_golden_fixture_verdicts_reproduce():
             assert got == c["error"], name
         errs = [c["error"] for c in doc[tag]["cases"]]
         assert errs.count(None) >= 4 and len(set(errs)) >= 8
+
+
+def test_bn254_g2_subgroup_check():
+    """BN254 G2 decoding (oracle parse_ecp2) follows gnark-crypto's SetBytes: twist
+    points outside the order-r subgroup are rejected; subgroup points, both issuer
+    keys' W and the CRI epoch key (GenG2) decode; FP256BN (AMCL) has no such check"""
+    C = PR.BN254
+    for x in (7, 1234567, 99):
+        q = ID.twist_point(C, x)
+        assert C.g2_on_curve(q) and not ID.g2_in_subgroup(C, q)
+        with pytest.raises(I.PointError):
+            ID.parse_ecp2(C, ID.ecp2(C, q))
+    for q in (C.g2_gen, C.g2_mul(C.g2_gen, 0xC0FFEE)):
+        assert ID.parse_ecp2(C, ID.ecp2(C, q)) == q
+    for tag in ("bn254", "fp256bn"):
+        _, _, cred, W, _, PC = _material(tag)
+        assert ID.g2_in_subgroup(PC, W) and ID.cri_epoch_pk(PC, cred["cri"]) == PC.g2_gen
+    q = ID.twist_point(PR.FP256BN, 5)
+    assert ID.parse_ecp2(PR.FP256BN, ID.ecp2(PR.FP256BN, q)) == q
