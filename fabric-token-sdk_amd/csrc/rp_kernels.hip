@@ -392,21 +392,22 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, c
   store_g1j(out, r);
 }
 
-// lane per (proof, chunk c): S_c = sum_{j < 16} 2^j H'_{16c+j} (Horner over the affine H')
+// lane per (proof, chunk c): S_c = sum_{j < 16} 2^j H'_{16c+j} (Horner over the
+// Jacobian H' of k_rp_fixed_exact: full additions, so the chain does not wait for
+// the H' normalisation, which runs beside it on the x0 stream)
 __global__ void __launch_bounds__(256) k_rp_hsum_chunks(int B, int n, const int32_t* __restrict__ status,
-                                                       const uint32_t* __restrict__ hpa, uint32_t* __restrict__ chunks) {
+                                                       const uint32_t* __restrict__ hpj, uint32_t* __restrict__ chunks) {
   const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * nc) return;
   const int b = gid / nc, c = gid % nc;
   if (status[b] != 0) return;
   const int lo = c * HS_CHUNK, hi = min(n, lo + HS_CHUNK);
-  const uint32_t* H = hpa + (size_t)b * (n + 1) * 16;  // affine H' (mixed additions)
-  G1J acc = g1j_from_affine(load_g1a(H + (hi - 1) * 16));
+  const uint32_t* H = hpj + (size_t)b * (n + 1) * 24;  // Jacobian H'
+  G1J acc = load_g1j(H + (hi - 1) * 24);
   for (int i = hi - 2; i >= lo; i--) {
     acc = g1j_dbl(acc);
-    const G1A q = load_g1a(H + i * 16);
-    if (!g1a_is_identity(q)) madd_inl(acc, q);
+    add_inl(acc, load_g1j(H + i * 24));
   }
   store_g1j(chunks + (size_t)gid * 24, acc);
 }
@@ -749,11 +750,14 @@ FTS_DEV uint32_t x0_unit(const X0Src& m, uint32_t u) {
   return 0u;
 }
 
-// One block per proof: the proof's variable message blocks (everything but
-// the shared template blocks) are assembled in LDS -- hex records of H'_i and
-// com (one 16-byte quarter of a point per work item), the DER header, the
-// constant bytes that share a block with variable ones, Zb(ip) and the SHA-256
-// padding -- then written to the compact slot with coalesced uint4 stores.
+// One wave per proof, X0_PPB proofs per block: the proof's variable message
+// blocks (everything but the shared template blocks) are assembled in the
+// wave's LDS region -- hex records of H'_i and com (one 16-byte quarter of a
+// point per work item), the DER header, the constant bytes that share a block
+// with variable ones, Zb(ip) and the SHA-256 padding -- then written to the
+// compact slot with coalesced uint4 stores.  (One 256-thread block per proof,
+// rounds 1-3, launched 4x the waves for the same work: at 81,920 proofs the
+// launch's span beside the com chain was 5.8-6.8 ms.)
 // LDS offset of message byte `pos` (outside the template blocks):
 FTS_DEV uint32_t x0_lds_off(uint32_t pos, uint32_t cb0, uint32_t cb1) {
   return pos < 64u * cb0 ? pos : pos - 64u * (cb1 - cb0);
@@ -762,21 +766,25 @@ FTS_DEV uint32_t x0_lds_off(uint32_t pos, uint32_t cb0, uint32_t cb1) {
 // (header, H'_0..H'_{n-1}: available right after their normalisation); 1 = the
 // blocks after it (com, DER tail, Zb(ip), padding).  Parts 0 and 1 write
 // disjoint byte ranges of the proof's slot.
-__global__ void __launch_bounds__(256) k_rp_x0_build(int B, int n, const int32_t* __restrict__ status,
-                                                     const uint8_t* __restrict__ hp_be,
-                                                     const uint8_t* __restrict__ x0_const, const uint32_t* __restrict__ sc,
-                                                     uint8_t* __restrict__ msgs, int part) {
+constexpr int X0_PPB = 4;
+__global__ void __launch_bounds__(64 * X0_PPB) k_rp_x0_build(int B, int n, const int32_t* __restrict__ status,
+                                                            const uint8_t* __restrict__ hp_be,
+                                                            const uint8_t* __restrict__ x0_const,
+                                                            const uint32_t* __restrict__ sc, uint8_t* __restrict__ msgs,
+                                                            int part) {
   extern __shared__ uint4 x0_lds[];
-  uint8_t* Lb = reinterpret_cast<uint8_t*>(x0_lds);
-  const int b = blockIdx.x;
-  if (b >= B || status[b] != 0) return;  // uniform per block
   const uint32_t A = x0_array_len(n), len = x0_msg_len(n), end = x0_slot_bytes(n);
   const uint32_t cb0 = x0_cb0(n), cb1 = x0_cb1(n), var = x0_var_bytes(n);
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int b = blockIdx.x * X0_PPB + wv;
+  const bool live = b < B && status[b] == 0;  // uniform per wave
+  uint4* L4 = x0_lds + (size_t)wv * (var / 16u);
+  uint8_t* Lb = reinterpret_cast<uint8_t*>(L4);
   const uint32_t c_off = x0_const_off(n), c_end = x0_const_end(n);
   const uint8_t* hp = hp_be + (size_t)b * (n + 1) * 64;
   // hex records: H'_0..H'_{n-1} (records 0..n-1) and com (record 2n+1, no "||")
   const int r_lo = part == 1 ? n : 0, r_hi = part == 0 ? n : n + 1;  // records of this part
-  for (int it = threadIdx.x + 4 * r_lo; it < r_hi * 4; it += blockDim.x) {
+  for (int it = lane + 4 * r_lo; live && it < r_hi * 4; it += 64) {
     const int r = it >> 2, q = it & 3;
     const uint4 v = *reinterpret_cast<const uint4*>(hp + r * 64 + q * 16);
     const uint32_t rec = r < n ? (uint32_t)r : 2u * n + 1u;
@@ -787,7 +795,7 @@ __global__ void __launch_bounds__(256) k_rp_x0_build(int B, int n, const int32_t
     if (q == 3 && r < n) d[16] = 0x7c7cu;
   }
   // header, constant bytes in variable blocks, trailer (DER tail, Zb(ip), padding, length)
-  const uint32_t* ip = sc + ((size_t)b * RP_NSC + RP_SC_IP) * 8;
+  const uint32_t* ip = sc + ((size_t)(live ? b : 0) * RP_NSC + RP_SC_IP) * 8;
   const uint32_t t0 = 8u + A;
   auto put = [&](uint32_t pos) {
     uint32_t v;
@@ -815,7 +823,7 @@ __global__ void __launch_bounds__(256) k_rp_x0_build(int B, int n, const int32_t
   const uint32_t nh = 8u, nc0 = 64u * cb0 - c_off, nc1 = c_end - 64u * cb1, nt = end - t0;
   // part 0: header + constants before the template; part 1: constants after it + trailer
   const uint32_t i_lo = part == 1 ? nh + nc0 : 0u, i_hi = part == 0 ? nh + nc0 : nh + nc0 + nc1 + nt;
-  for (uint32_t it = threadIdx.x + i_lo; it < i_hi; it += blockDim.x) {
+  for (uint32_t it = lane + i_lo; live && it < i_hi; it += 64) {
     uint32_t pos;
     if (it < nh) pos = it;
     else if (it < nh + nc0) pos = c_off + (it - nh);
@@ -824,11 +832,13 @@ __global__ void __launch_bounds__(256) k_rp_x0_build(int B, int n, const int32_t
     put(pos);
   }
   __syncthreads();
+  if (!live) return;
   uint4* dst = reinterpret_cast<uint4*>(msgs + (size_t)b * var);
   const uint32_t c_lo = part == 1 ? 4u * cb0 : 0u, c_hi = part == 0 ? 4u * cb0 : var / 16u;
-  for (uint32_t c = threadIdx.x + c_lo; c < c_hi; c += blockDim.x) dst[c] = x0_lds[c];
+  for (uint32_t c = lane + c_lo; c < c_hi; c += 64) dst[c] = L4[c];
 }
-inline size_t x0_build_lds(int n) { return x0_var_bytes(n); }
+inline size_t x0_build_lds(int n) { return (size_t)X0_PPB * x0_var_bytes(n); }
+inline unsigned x0_build_grid(int B) { return (unsigned)((B + X0_PPB - 1) / X0_PPB); }
 
 // SHA-256 over message blocks [b0, b1) of each proof's x0 message: b0 == 0
 // starts from the initial state, else from mid[b]; b1 == every block finishes
@@ -1576,23 +1586,25 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
                d.terms);
     tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FBW_FRESH);
     if (d.rlc_fork) rlc_side();
-    // H'_i -> affine + BE bytes (x0 transcript) now; com is normalised after com_sum
-    launch_normalize(nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be, s);
-    tl->mark("k_rp_normalize", s, (double)nhp * (2.0 * 8.0 / NORM_E + 9.0));
+    // H'_i -> affine + BE bytes (x0 transcript) on the side stream: the S / com
+    // chain on s works on the Jacobian H' (k_rp_hsum_chunks) and does not wait
+    // for it; com is normalised after com_var
+    tl->fork(s, s2);
+    launch_normalize(nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be, s2);
+    tl->mark("k_rp_normalize", s2, (double)nhp * (2.0 * 8.0 / NORM_E + 9.0));
     if (d.x0_mid) {
       // x0 prefix on the side stream: the H' records and the shared template
       // (cb1 of the message's blocks) do not depend on com, so they are hashed
       // beside the S / com chain; only the suffix waits for com
-      tl->fork(s, s2);
-      hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s2, B, n, d.status, d.hp_be, x0_const,
+      hipLaunchKernelGGL(k_rp_x0_build, dim3(x0_build_grid(B)), dim3(64 * X0_PPB), x0_build_lds(n), s2, B, n, d.status, d.hp_be, x0_const,
                          d.sc, d.x0_msgs, 0);
       tl->mark("k_rp_x0_build", s2, 0);
       FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s2, B, n, k, d.status, d.x0_msgs, x0_tmpl, 0u, x0_cb1(n), d.x0_mid, d.ch);
       tl->mark("k_rp_x0_prefix", s2, 0);
     }
     const int nch = (n + HS_CHUNK - 1) / HS_CHUNK;
-    FTS_LAUNCH(k_rp_hsum_chunks, B * nch, g_chain_bs, s, B, n, d.status, d.hpa, d.scratch);
-    tl->mark("k_rp_hsum_chunks", s, (double)B * (n - nch) * (COST_DBL + COST_MADD));
+    FTS_LAUNCH(k_rp_hsum_chunks, B * nch, g_chain_bs, s, B, n, d.status, d.hpj, d.scratch);
+    tl->mark("k_rp_hsum_chunks", s, (double)B * (n - nch) * (COST_DBL + COST_ADD));
     FTS_LAUNCH(k_rp_hsum_join, B, g_chain_bs, s, B, n, d.status, d.scratch);
     tl->mark("k_rp_hsum_join", s, (double)B * (nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD));
     // scratch: [0, B*HS_SCRATCH) Horner chunks of S, then the 2B lanes' affine tables
@@ -1603,7 +1615,9 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   launch_normalize(B, 1, n + 1, n, d.status, d.hpj, d.hpa, d.hp_be, s);
   tl->mark("k_rp_normalize_com", s, (double)B * (2.0 * 8.0 / NORM_E + 9.0));
   const bool split = d.x0_mid != nullptr;
-  hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s, B, n, d.status, d.hp_be, x0_const, d.sc,
+  // work path without the prefix split: the whole message needs the H' bytes of s2
+  if (!d.com_fixed && !split) tl->fork(s2, s);
+  hipLaunchKernelGGL(k_rp_x0_build, dim3(x0_build_grid(B)), dim3(64 * X0_PPB), x0_build_lds(n), s, B, n, d.status, d.hp_be, x0_const, d.sc,
                      d.x0_msgs, split ? 1 : 2);
   tl->mark(split ? "k_rp_x0_build_tail" : "k_rp_x0_build", s, 0);
   if (split) tl->fork(s2, s);  // the prefix's midstate
@@ -1735,7 +1749,7 @@ namespace fts {
 void launch_x0(int B, int n, int k, const int32_t* status, const uint8_t* hp_be, const uint8_t* x0_const,
                const uint8_t* x0_tmpl, const uint32_t* sc, uint8_t* msgs, uint32_t* ch, hipStream_t s) {
   if (B <= 0) return;
-  hipLaunchKernelGGL(k_rp_x0_build, dim3(B), dim3(256), x0_build_lds(n), s, B, n, status, hp_be, x0_const, sc, msgs, 2);
+  hipLaunchKernelGGL(k_rp_x0_build, dim3(x0_build_grid(B)), dim3(64 * X0_PPB), x0_build_lds(n), s, B, n, status, hp_be, x0_const, sc, msgs, 2);
   FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s, B, n, k, status, msgs, x0_tmpl, 0u, 0xffffffffu, (uint32_t*)nullptr, ch);
 }
 }  // namespace fts
