@@ -409,6 +409,103 @@ FTS_DEV G1J straus2_atab(const ATab& T, const uint32_t a[4], const uint32_t b[4]
   return acc;
 }
 
+// ------------------------------------------- per-proof shared tables (com chain)
+// k_rp_com_var's two lanes of a proof share ONE affine table: lane 0 builds and
+// normalises 1..8 D (entries 0..7), lane 1 1..8 S (entries 8..15), unsigned and
+// without phi; each entry also carries beta*x, so the lane of the phi half reads
+// phi(e P) = (beta x, y) and applies its GLV sign to y at lookup.  Half the table
+// work and one inversion per lane of the per-lane tables (ATab).
+// Region layout: XY [16][B][16] | BX [16][B][8] | Z [16][B][8] | PRE [16][B][8]
+// (2,560 B per proof), row (e, proof) entry-major.
+constexpr int CTAB_WORDS = 16 * 40;  // words per proof
+struct CTab {
+  uint32_t* base;
+  size_t L, p;  // proofs in the launch, this proof
+  FTS_DEV uint32_t* xy(int e) const { return base + ((size_t)e * L + p) * 16; }
+  FTS_DEV uint32_t* bx(int e) const { return base + (size_t)16 * L * 16 + ((size_t)e * L + p) * 8; }
+  FTS_DEV uint32_t* z(int e) const { return base + (size_t)16 * L * 24 + ((size_t)e * L + p) * 8; }
+  FTS_DEV uint32_t* pre(int e) const { return base + (size_t)16 * L * 32 + ((size_t)e * L + p) * 8; }
+};
+// entries e0 .. e0+7 <- 1..8 * P (Jacobian, then normalised with one inversion):
+// AFF: P.z == 1 (mixed additions).  An identity P gives (0, 0) entries (skipped by
+// the chain, which knows the identity flags).
+template <bool AFF>
+FTS_DEV void ctab_build8(const CTab& T, int e0, const G1J& P, bool ident) {
+  G1J cur = P;
+  G1A pa;
+  if (AFF) pa.x = P.x, pa.y = P.y;
+  if (ident) {
+    cur.x = f_zero<FpP>();
+    cur.y = f_zero<FpP>();
+    cur.z = f_one<FpP>();
+  }
+  Fp pre;
+  for (int e = 0; e < 8; e++) {
+    if (!ident && e == 1) cur = g1j_dbl(P);
+    if (!ident && e > 1) {
+      if (AFF) madd_inl(cur, pa);
+      else add_inl(cur, P);
+    }
+    store_fp(T.xy(e0 + e), cur.x);
+    store_fp(T.xy(e0 + e) + 8, cur.y);
+    store_fp(T.z(e0 + e), cur.z);
+    pre = e == 0 ? cur.z : fp_mul(pre, cur.z);
+    store_fp(T.pre(e0 + e), pre);
+  }
+  Fp inv = nl_fp_inv(pre);
+  const Fp beta = glv_beta();
+  for (int e = 7; e >= 0; e--) {
+    Fp zi = inv;
+    if (e > 0) {
+      Fp pp, z;
+      load_fp(T.pre(e0 + e - 1), pp);
+      load_fp(T.z(e0 + e), z);
+      zi = fp_mul(inv, pp);
+      inv = fp_mul(inv, z);
+    }
+    Fp x, y;
+    load_fp(T.xy(e0 + e), x);
+    load_fp(T.xy(e0 + e) + 8, y);
+    const Fp zi2 = fp_sqr(zi);
+    x = fp_mul(x, zi2);
+    store_fp(T.xy(e0 + e), x);
+    store_fp(T.xy(e0 + e) + 8, fp_mul(fp_mul(y, zi2), zi));
+    store_fp(T.bx(e0 + e), fp_mul(x, beta));
+  }
+}
+// a phi^h(sa D) + b phi^h(sb S) over the shared table (sa, sb: the GLV signs of the
+// two half scalars, folded into y at lookup): 124 doublings, <= 64 mixed additions
+FTS_DEV G1J straus2_ctab(const CTab& T, int h, const uint32_t a[4], bool sa, const uint32_t b[4], bool sb, bool ida,
+                         bool idb) {
+  const uint32_t ca = recode_carries(a), cb = recode_carries(b);
+  G1J acc = g1j_identity();
+  for (int w = 31; w >= 0; w--) {
+    const int da = ida ? 0 : window_digit(a, ca, w), db = idb ? 0 : window_digit(b, cb, w);
+    G1A qa, qb;
+    if (da != 0) {
+      const int e = (da < 0 ? -da : da) - 1;
+      load_fp(h ? T.bx(e) : T.xy(e), qa.x);
+      load_fp(T.xy(e) + 8, qa.y);
+    }
+    if (db != 0) {
+      const int e = 8 + (db < 0 ? -db : db) - 1;
+      load_fp(h ? T.bx(e) : T.xy(e), qb.x);
+      load_fp(T.xy(e) + 8, qb.y);
+    }
+    if (w != 31)
+      for (int r = 0; r < 4; r++) acc = g1j_dbl(acc);
+    if (da != 0) {
+      if ((da < 0) != sa) qa.y = f_neg(qa.y);
+      madd_inl(acc, qa);
+    }
+    if (db != 0) {
+      if ((db < 0) != sb) qb.y = f_neg(qb.y);
+      madd_inl(acc, qb);
+    }
+  }
+  return acc;
+}
+
 // k * P for a canonical scalar k < r in one lane: GLV split k = k1 + k2 lambda,
 // then the joint chain k1 P + k2 phi(P) (124 doublings instead of 252);
 // tab/stride/idx: the lane's 16-entry table (straus2_128).  Keep it inlined

@@ -72,6 +72,11 @@ constexpr double COST_STRAUS2 = 2.0 * (7.0 + 6.0 * COST_ADD) + 124.0 * COST_DBL 
 // doublings and ~60 mixed additions
 constexpr double COST_STRAUS2_ATAB = (COST_DBL + 6.0 * COST_MADD) + (COST_DBL + 6.0 * COST_ADD) + 109.0 +
                                      124.0 * COST_DBL + 60.0 * COST_MADD;
+// straus2_ctab (k_rp_com_var, per lane): the lane's half of the shared table -- 1..8
+// of one point (1 dbl + 6 full additions), its normalisation with beta*x (61
+// products; the one inversion is not priced) -- then 124 doublings and ~60 mixed
+// additions
+constexpr double COST_STRAUS2_CTAB = (COST_DBL + 6.0 * COST_ADD) + 61.0 + 124.0 * COST_DBL + 60.0 * COST_MADD;
 constexpr double COST_NORM = 7.0;
      // batched affine normalisation, per point
 

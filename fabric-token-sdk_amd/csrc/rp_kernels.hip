@@ -455,20 +455,15 @@ __global__ void __launch_bounds__(256, FTS_COMVAR_OCC) k_rp_com_var(int B, int n
   G1J S = load_g1j(chunks + (size_t)b * nc * 24);  // k_rp_hsum_join
   const G1A Da = load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_D) * 16);
   const bool idD = g1a_is_identity(Da), idS = f_is_zero(S.z);
-  G1J D = g1j_from_affine(Da);
-  if (h) {  // phi
-    const Fp beta = glv_beta();
-    D.x = fp_mul(D.x, beta);
-    S.x = fp_mul(S.x, beta);
-  }
-  if (xs[h]) D.y = f_neg(D.y);
-  if (ws[h]) S.y = f_neg(S.y);
-  const ATab T{atab, (size_t)2 * B, (size_t)gid};
-  Fp pre;
-  atab_build8<true>(T, 0, D, pre, idD);
-  atab_build8<false>(T, 8, S, pre, idS);
-  atab_normalize(T);
-  G1J r = straus2_atab(T, xk[h], wk[h], idD, idS);
+  // the proof's shared table: lane 0 builds 1..8 D, lane 1 1..8 S (one instruction
+  // stream on the lane's own point: no divergence); both lanes of a proof are
+  // adjacent lanes of one wave, so the workgroup fence orders each lane's rows
+  // before the other reads them
+  const CTab T{atab, (size_t)B, (size_t)b};
+  const G1J Dj = g1j_from_affine(Da);
+  ctab_build8<false>(T, 8 * h, h ? S : Dj, h ? idS : idD);
+  __threadfence_block();
+  G1J r = straus2_ctab(T, h, xk[h], xs[h] != 0, wk[h], ws[h] != 0, idD, idS);
   // com = C + z K - delta P + x D + z^2 S (bulletproof.go:477-492), summed by the
   // proof's two lanes (adjacent lanes of one wave; both exit or both run): lane h
   // adds its fixed-base term (z K or -delta P, k_rp_fixed_exact), lane 0 also C,
@@ -1610,7 +1605,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     // scratch: [0, B*HS_SCRATCH) Horner chunks of S, then the 2B lanes' affine tables
     FTS_LAUNCH(k_rp_com_var, 2 * B, g_chain_bs, s, B, n, k, d.status, d.pts, d.ch, d.scratch,
                d.scratch + (size_t)B * HS_SCRATCH, d.terms, d.hpj);
-    tl->mark("k_rp_com_var", s, (double)B * 2 * (COST_STRAUS2_ATAB + 2.5 * COST_ADD));
+    tl->mark("k_rp_com_var", s, (double)B * 2 * (COST_STRAUS2_CTAB + 2.5 * COST_ADD));
   }
   launch_normalize(B, 1, n + 1, n, d.status, d.hpj, d.hpa, d.hp_be, s);
   tl->mark("k_rp_normalize_com", s, (double)B * (2.0 * 8.0 / NORM_E + 9.0));
