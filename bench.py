@@ -170,7 +170,8 @@ def main():
                     help="rp workload: calls of fts_rp_verify_batch from host DER bytes after the timed region "
                          "(the PCIe-inclusive rate, reported apart; 0: skip)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall-time bound of the CPU baseline sample")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC traffic per launch (tools/pmc_traffic.py); default: the newest profiles/traffic_rNN.json")
     ap.add_argument("--workload", choices=["rp", "msm", "transfer", "mixed", "request", "audit", "prove", "ecdsa",
                                            "idemix", "identity"],
                     default="rp")
@@ -378,8 +379,13 @@ def main():
     # this pipeline's own cost model: algorithmic MADs of every kernel of one pass / proofs
     own_mads = sum(v[1] for v in kt.values()) / (m * B)
     traffic = None
+    tj_path = args.traffic_json
+    if tj_path is None:
+        import glob
+        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_r[0-9][0-9].json")))
+        tj_path = cands[-1] if cands else ""
     try:
-        with open(args.traffic_json) as f:
+        with open(tj_path) as f:
             tj = json.load(f)
             # HBM bytes per launch of THIS pass size: FETCH_SIZE (scaled by the factor calibrated for the
             # kernel's access pattern, tools/fetch_calib) + WRITE_SIZE, from separate PMC runs of the same command
@@ -391,6 +397,7 @@ def main():
     rd = kernel_roof(dom)
     roofline = {"bound": "int32_valu (v_mad_u64_u32)", "kernel": dom, "achieved": rd["achieved"],
                 "peak": round(PEAK_TMAD, 3), "unit": "TMAD/s", "frac": rd["frac"], "traffic": traffic,
+                "traffic_source": os.path.basename(tj_path) if traffic is not None else None,
                 "kernel_ms": rd["kernel_ms"], "mads_per_launch": rd["mads_per_launch"],
                 "measured": "HIP events, %d isolated passes of %d proofs (%d coalesced batches, the timed region's "
                             "pass size) alone on the GPU after the timed region" % (R, m * B, m),

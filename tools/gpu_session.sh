@@ -14,7 +14,7 @@
 # Output: gpurun_out/$TAG (TAG default r03).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$OLDPWD}"
-TAG=${TAG:-r03}
+TAG=${TAG:-r04}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 step() {  # name limit cmd...
@@ -40,7 +40,7 @@ for s in "$@"; do case $s in
        step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -T -f csv -d $OUT/pmc_fetch -o run -- $PB
        json pmc_fetch
        step pmc_write 300 rocprofv3 --pmc WRITE_SIZE -T -f csv -d $OUT/pmc_write -o run -- $PB
-       step pmc_valu 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE -T -f csv -d $OUT/pmc_valu -o run -- $PB
+       step pmc_valu 300 rocprofv3 --pmc VALUBusy SIMD_UTILIZATION SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_SALU -T -f csv -d $OUT/pmc_valu -o run -- $PB
        step pmc_calib 120 rocprofv3 --pmc FETCH_SIZE -T -f csv -d $OUT/pmc_calib -o run -- fabric-token-sdk_amd/lib/fetch_calib
        json pmc_calib
        python3 tools/pmc_traffic.py $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_calib $OUT/pmc_calib.json $OUT/pmc_fetch.json 2 $OUT/traffic_$TAG.json $OUT/pmc_valu ;;

@@ -19,7 +19,9 @@ as measured.
     python tools/pmc_r02.py <fetch_dir> <write_dir> <calib_dir> <calib.json> <bench.json> <R> <out.json> [valu_dir]
 
 With valu_dir (the SQ_* pass), each entry also carries the per-launch VALU
-instruction counts, including SQ_INSTS_VALU_MFMA_MOPS_F16 (0: no MFMA).
+instruction counts (INT32 / INT64 split, SQ_INSTS_VALU_MFMA_MOPS_F16 = 0: no
+MFMA) and the derived VALUBusy (% of the launch's GPU time with VALU
+instructions issuing, per CU) and SIMD_UTILIZATION.
 """
 import csv
 import glob
@@ -62,7 +64,9 @@ def main():
     LATENCY_ONLY = {"k_rp_fixed_all", "k_rp_xd", "k_rp_com_tree"}
     fetch, write = per_kernel(fdir, "FETCH_SIZE"), per_kernel(wdir, "WRITE_SIZE")
     vdir = sys.argv[8] if len(sys.argv) > 8 else None
-    SQ = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_F16")
+    # raw SQ counts and the derived VALU-busy / SIMD-utilisation metrics of the pass
+    SQ = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64",
+          "SQ_INSTS_VALU_MFMA_MOPS_F16", "VALUBusy", "SIMD_UTILIZATION")
     valu = {c: per_kernel(vdir, c) for c in SQ} if vdir else {}
     out = {"_calibration": calib, "_source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate runs) of bench.py, "
                                              "last %d dispatches per kernel = the isolated pass of %d proofs"
@@ -78,7 +82,7 @@ def main():
         for c, per in valu.items():
             v = per.get(k, [])[-R:]
             if v:
-                e[c] = round(sum(v) / len(v))
+                e[c] = round(sum(v) / len(v), 4) if c in ("VALUBusy", "SIMD_UTILIZATION") else round(sum(v) / len(v))
         out["%s@pass%d" % (k, batch if k in LATENCY_ONLY and proofs > batch else proofs)] = e
     json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
     print(json.dumps(calib))
