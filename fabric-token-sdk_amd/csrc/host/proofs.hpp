@@ -31,10 +31,12 @@ struct Elem {
 };
 
 struct Unmarshaller {
-  std::vector<der::Span> v;
+  std::vector<der::Span> own;
+  std::vector<der::Span>& v;  // own, or a caller's reused buffer (no allocation per proof)
   size_t i = 0;
   bool ok = false;
-  Unmarshaller(der::Span raw) { ok = der::unmarshal_values(raw, v); }
+  Unmarshaller(der::Span raw) : v(own) { ok = der::unmarshal_values(raw, v); }
+  Unmarshaller(der::Span raw, std::vector<der::Span>& buf) : v(buf) { ok = der::unmarshal_values(raw, v); }
   // returns false on a deserialization error
   bool next(Elem& e) {
     e.present = false;
@@ -94,7 +96,8 @@ inline void parse_range_proof(der::Span rp, int k, uint8_t* pts, uint32_t* sc, i
   for (int j = 0; j < npts; j++)
     if (j != 4) filler_point(pts + j * 64);
   memset(sc, 0, 5 * 32);
-  std::vector<der::Span> vals;
+  // per-thread reused buffers: the host pool parses thousands of proofs per call
+  thread_local std::vector<der::Span> vals, ubuf, Ls, Rs;
   if (!der::unmarshal_values(rp, vals) || vals.size() != 2) {
     status = FTS_E_MALFORMED;
     return;
@@ -104,7 +107,7 @@ inline void parse_range_proof(der::Span rp, int k, uint8_t* pts, uint32_t* sc, i
   if (vals[0].n == 0) {
     nil = true;
   } else {
-    Unmarshaller u(vals[0]);
+    Unmarshaller u(vals[0], ubuf);
     if (!u.ok) {
       status = FTS_E_MALFORMED;
       return;
@@ -137,7 +140,7 @@ inline void parse_range_proof(der::Span rp, int k, uint8_t* pts, uint32_t* sc, i
   if (vals[1].n == 0) {
     ipa_flag = FTS_E_IPA_NIL;
   } else {
-    Unmarshaller u(vals[1]);
+    Unmarshaller u(vals[1], ubuf);
     if (!u.ok) {
       status = FTS_E_MALFORMED;
       return;
@@ -149,7 +152,8 @@ inline void parse_range_proof(der::Span rp, int k, uint8_t* pts, uint32_t* sc, i
     }
     if (eL.present) scalar_from_bytes(eL.raw, sc + 3 * 8, nullptr);
     if (eR.present) scalar_from_bytes(eR.raw, sc + 4 * 8, nullptr);
-    std::vector<der::Span> Ls, Rs;
+    Ls.clear();
+    Rs.clear();
     if (aL.present && !der::unmarshal_values(aL.raw, Ls, true)) {
       status = FTS_E_MALFORMED;
       return;
