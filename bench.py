@@ -161,6 +161,9 @@ def main():
                          "library runs under load; the PMC traffic file is keyed by this pass size)")
     ap.add_argument("--roofline-steps", type=int, default=6,
                     help="isolated steps (one batch alone on the GPU) for the per-kernel roofline")
+    ap.add_argument("--tamper-every", type=int, default=1,
+                    help="with --tamper: tamper only every M-th staged batch (e.g. --tamper 1e-9 --tamper-every 20: "
+                         "one bad proof per 81,920-proof pass)")
     ap.add_argument("--tamper", type=float, default=0.0,
                     help="rp workload: fraction of tampered proofs per batch (SURVEY 8d: the C2 variant with 1 %% "
                          "tampered proofs exercises the group-test fallback); verdicts are checked every step")
@@ -241,7 +244,7 @@ def main():
     # proofs, the rest re-stage them (verification work does not depend on it)
     inflight = max(1, args.inflight)
     t0 = time.time()
-    batches, sets, wants = [], [], []
+    batches, sets, wants, staged = [], [], [], []
     for ln in range(inflight):
         if ln >= max(1, args.distinct):
             proofs, coms = sets[ln % len(sets)]
@@ -251,24 +254,27 @@ def main():
             bfs = [rng.randrange(R_ORDER).to_bytes(32, "big") for _ in range(B)]
             # device prover: byte-identical to the host prover (tests/test_gpu_prove.py), seconds faster
             proofs, coms = pp.prove_range_batch_gpu(vals, bfs, seed=0xF7A50002 + 1000003 * rank + 7777 * ln)
-            want = np.zeros(B, dtype=np.int32)
-            if args.tamper > 0:  # T1 (-> invalid range proof) or one L_j (-> invalid IPA), before the clock
-                from oracle import bn254 as obn, zkat
-                trng = random.Random(0x7A3 + 31 * ln + 7919 * rank)
-                for i in trng.sample(range(B), max(1, round(args.tamper * B))):
-                    r = zkat.RangeProof.deserialize(proofs[i])
-                    if trng.random() < 0.5:
-                        r.data.T1 = obn.g1_add(r.data.T1, obn.GEN)
-                        want[i] = fts_gpu.FTS_E_RP_INVALID
-                    else:
-                        j = trng.randrange(k)
-                        r.ipa.L[j] = obn.g1_add(r.ipa.L[j], obn.GEN)
-                        want[i] = fts_gpu.FTS_E_IPA_INVALID
-                    proofs[i] = r.serialize()
             sets.append((proofs, coms))
-            wants.append(want)
+        want = np.zeros(B, dtype=np.int32)
+        if args.tamper > 0 and ln % max(1, args.tamper_every) == 0:
+            # T1 (-> invalid range proof) or one L_j (-> invalid IPA), before the clock
+            from oracle import bn254 as obn, zkat
+            proofs = list(proofs)
+            trng = random.Random(0x7A3 + 31 * ln + 7919 * rank)
+            for i in trng.sample(range(B), max(1, round(args.tamper * B))):
+                r = zkat.RangeProof.deserialize(proofs[i])
+                if trng.random() < 0.5:
+                    r.data.T1 = obn.g1_add(r.data.T1, obn.GEN)
+                    want[i] = fts_gpu.FTS_E_RP_INVALID
+                else:
+                    j = trng.randrange(k)
+                    r.ipa.L[j] = obn.g1_add(r.ipa.L[j], obn.GEN)
+                    want[i] = fts_gpu.FTS_E_IPA_INVALID
+                proofs[i] = r.serialize()
+        wants.append(want)
+        staged.append((proofs, coms))
         batches.append(pp.stage_range_proofs(proofs, coms))
-    proofs0, coms0 = sets[0]
+    proofs0, coms0 = staged[0]  # batch 0 (tampered when --tamper is given; its verdicts are wants[0])
     prove_s = time.time() - t0
 
     def run(ln, nsteps, sink):
@@ -276,7 +282,7 @@ def main():
             st = batches[ln].verify(want_status=True)
             sink.append((st, batches[ln].merged()))
             if args.tamper > 0:
-                assert (st == wants[ln % len(wants)]).all(), "verdicts differ from the tampered positions"
+                assert (st == wants[ln]).all(), "verdicts differ from the tampered positions"
 
     def pipelined(nsteps, on_ready=None):
         """nsteps batch verifications spread over the in-flight slots (one host
@@ -358,7 +364,7 @@ def main():
 
     kt1, iso_ms = isolated(batches[0], R, wants[0])
     m = args.pass_batches or max(1, int(os.environ.get("FTS_COALESCE_MAX", "81920")) // B)
-    pass_proofs = [sets[i % len(sets)] for i in range(m)]
+    pass_proofs = [staged[i % len(staged)] for i in range(m)]
     big = pp.stage_range_proofs([p for ps, _ in pass_proofs for p in ps], [c for _, cs in pass_proofs for c in cs])
     kt, pass_ms = isolated(big, R, np.concatenate([wants[i % len(wants)] for i in range(m)]))
     big.close()
@@ -469,7 +475,7 @@ def main():
                     "(byte-identical to its host prover)" % (B, n),
             "config": {"workload": "C2: batch of %d standalone %d-bit Bulletproof range proofs per GPU "
                                    "(exact transcripts per proof + RLC batch check via one Pippenger MSM)%s"
-                                   % (B, n, ", %g %% tampered" % (100 * args.tamper) if args.tamper > 0 else ""),
+                                   % (B, n, _tamper_note(args, B)),
                        "batch_per_gpu": B, "bit_length": n, "rounds": k, "parallelism": "shard%d" % world},
             "accepted": ok,
             "verified": world * B * args.steps,
@@ -490,6 +496,7 @@ def main():
             "cpu_baseline": cpu,
             "kernel_ms_isolated": {kname: round(v, 4) for kname, v in avg.items()},
             "tampered": args.tamper,
+            "tamper_every": args.tamper_every,
             "fallback": _fallback_share(kt, R, pass_ms),
             "prove_s": round(prove_s, 2),
         }
@@ -1467,6 +1474,14 @@ def bench_mixed(args):
             flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _tamper_note(args, B):
+    if args.tamper <= 0:
+        return ""
+    if args.tamper_every > 1:
+        return ", %d tampered proof(s) in every %d-th batch" % (max(1, round(args.tamper * B)), args.tamper_every)
+    return ", %g %% tampered" % (100 * args.tamper)
 
 
 def _fallback_share(kt, steps, call_ms):

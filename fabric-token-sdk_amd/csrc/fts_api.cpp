@@ -420,15 +420,16 @@ struct fts_ctx {
   // latency whatever their number up to ~8k proofs (tools/gt_sweep.sh, C5 1 % tampered:
   // 64/2048 -> 256/8192 = 485k -> 533k actions/s)
   int gt1 = 256, gt2_min = 8192;
-  // FTS_GT_ADAPT: round-1 group size follows the bad-proof density of the last
-  // failed pass.  Dense (more than half the proofs in failing 256-groups, or more
-  // than 2 % in failing 8-groups: ~0.3 % bad proofs and up) starts at groups of 8
-  // on the small-group kernels; a 256-group round there is one whole grouped
-  // Pippenger MSM that clears almost nothing (C2 with 1 % tampered, 81,920-proof
-  // pass: 51.8 -> 41.4 ms; C5's sparse bad proofs keep 256, where 8 was slower,
-  // tools/sweeps/gt1_small.txt)
+  // FTS_GT_ADAPT: a staged caller batch's round-1 group size follows the bad-proof
+  // density of ITS last failed verification (fts_rp_batch::dense; per caller batch,
+  // so one caller's tampered batches never change the fallback of another's).
+  // Dense (more than half the batch's proofs in failing 256-groups, or more than
+  // 2 % in failing 8-groups: ~0.3 % bad proofs and up) starts at groups of 8 on the
+  // small-group kernels; a 256-group round there is one whole grouped Pippenger MSM
+  // that clears almost nothing (C2 with 1 % tampered, 81,920-proof pass: 51.8 ->
+  // 41.4 ms; C5's sparse bad proofs keep 256, where 8 was slower,
+  // tools/sweeps/gt1_small.txt).  Action calls have no batch across calls: 256.
   int gt_adapt = 1;
-  std::atomic<int> gt_dense{0};
   int x0_split = 1;  // FTS_X0_SPLIT: work path hashes the x0 prefix beside the com chain
   // FTS_RLC_FORK: the batch check forks after the fixed-base products (1) or after the
   // challenges (0); 2 (default): after the challenges on the latency path (a lone small
@@ -479,6 +480,7 @@ struct fts_rp_batch {
   std::vector<fts_ctx*> part_ctx;
   std::vector<size_t> bounds;
   int merged = 1;  // batches in the device pass that verified it last
+  bool dense = false;  // its last failed verification found dense bad proofs (FTS_GT_ADAPT)
   // timings of this batch's last verification
   int ntim = 0;
   const char* tim_name[Timeline::CAP];
@@ -1092,63 +1094,102 @@ static int lane_reserve(fts_ctx* c, Lane& L, int B, bool inputs) {
 // RP_GT1 per-proof checks, all of them in its own caller batch (RP_GT1, RP_GT2_MIN:
 // fts_ctx::gt1, gt2_min).
 constexpr int RP_GT2 = 8;
+// dense[q] (caller batch q = [groups[q], groups[q+1])): its round-1 groups are of
+// RP_GT2 proofs instead of gt1; with FTS_GT_ADAPT the flags are updated from this
+// fallback's round-1 failures (a batch's own density).  An empty `dense` = all sparse.
 static int rp_group_fallback(fts_ctx* c, Lane& L, const RpBatchDev& d, const RlcDev& r,
-                             const std::vector<int>& groups) {
+                             const std::vector<int>& groups, std::vector<uint8_t>& dense) {
   const bool adapt = c->gt_adapt && c->gt1 > RP_GT2;
-  const int RP_GT1 = adapt && c->gt_dense.load(std::memory_order_relaxed) ? RP_GT2 : c->gt1;
   const int RP_GT2_MIN = c->gt2_min;
   const int B = d.B, n = d.n, npts = rp_npts(d.k);
+  const size_t nb = groups.size() > 0 ? groups.size() - 1 : 0;
+  dense.resize(nb, 0);
   Workspace& w = L.ws;
   L.tl.fallback();
-  // round-1 selection: each batch cut into groups of RP_GT1, -1 padded
-  std::vector<int32_t> sel;
-  for (size_t q = 0; q + 1 < groups.size(); q++)
-    for (int lo = groups[q]; lo < groups[q + 1]; lo += RP_GT1)
-      for (int j = 0; j < RP_GT1; j++) sel.push_back(lo + j < groups[q + 1] ? lo + j : -1);
-  const size_t slots = std::max<size_t>(sel.size(), (size_t)B + RP_GT2);
-  // groups of either round: round 1 has sel.size() / RP_GT1, round 2 at most slots / RP_GT2
-  const size_t gmax = std::max(sel.size() / RP_GT1, (slots + RP_GT2 - 1) / RP_GT2);
-  if (w.r_sel.ensure(slots * 4) || w.r_next.ensure(slots * 4) || w.r_cnt.ensure(8) ||
+  // round-1 selections, -1 padded: groups of gt1 over the sparse batches, of RP_GT2 over the dense ones
+  std::vector<int32_t> sel_big, sel_small;
+  for (size_t q = 0; q < nb; q++) {
+    const bool small = adapt && dense[q];
+    const int gs = small ? RP_GT2 : c->gt1;
+    std::vector<int32_t>& sel = small ? sel_small : sel_big;
+    for (int lo = groups[q]; lo < groups[q + 1]; lo += gs)
+      for (int j = 0; j < gs; j++) sel.push_back(lo + j < groups[q + 1] ? lo + j : -1);
+  }
+  const size_t slots = std::max<size_t>(sel_big.size() + sel_small.size(), (size_t)B + RP_GT2);
+  // groups of any round: round 1 has sel_big / gt1 + sel_small / RP_GT2, round 2 at most slots / RP_GT2
+  const size_t gmax = std::max(sel_big.size() / c->gt1 + sel_small.size() / RP_GT2, (slots + RP_GT2 - 1) / RP_GT2);
+  if (w.r_sel.ensure(2 * slots * 4) || w.r_next.ensure(slots * 4) || w.r_cnt.ensure(8) ||
       w.r_gcol.ensure(gmax * rlc_ncols(n) * 32) || w.r_gfix.ensure(gmax * rlc_ncols(n) * 96))
     return FTS_API_ENOMEM;
-  uint8_t* hs = L.stage_buf(sel.size() * 4);
+  uint8_t* hs = L.stage_buf((sel_big.size() + sel_small.size()) * 4);
   if (!hs) return FTS_API_ENOMEM;
-  memcpy(hs, sel.data(), sel.size() * 4);
-  HIP_OK(hipMemcpyAsync(w.r_sel.p, hs, sel.size() * 4, hipMemcpyHostToDevice, L.s));
-  int32_t* cur = w.r_sel.as<int32_t>();
+  memcpy(hs, sel_big.data(), sel_big.size() * 4);
+  memcpy(hs + sel_big.size() * 4, sel_small.data(), sel_small.size() * 4);
+  int32_t* cur_big = w.r_sel.as<int32_t>();
+  int32_t* cur_small = cur_big + sel_big.size();
   int32_t* nxt = w.r_next.as<int32_t>();
   uint32_t* cnt = w.r_cnt.as<uint32_t>();
-  int G = (int)(sel.size() / RP_GT1), gs = RP_GT1;
-  for (int round = 0; round < 2; round++) {
+  HIP_OK(hipMemcpyAsync(cur_big, hs, (sel_big.size() + sel_small.size()) * 4, hipMemcpyHostToDevice, L.s));
+  HIP_OK(hipMemsetAsync(nxt, 0xff, slots * 4, L.s));  // -1: empty slots of the next round
+  HIP_OK(hipMemsetAsync(cnt, 0, 4, L.s));
+  // one grouped test per group size; both append their failing proofs to nxt
+  auto group_test = [&](const int32_t* sel, int G, int gs) -> int {
+    if (G == 0) return FTS_API_OK;
     MsmPlan gp{};
     msm_layout_groups(G * gs * npts, G, gs * npts, gp);
-    gp.sel = cur;
+    gp.sel = sel;
     gp.sel_pts = npts;
     if (int rc = msm_prepare_plan(L, gp)) return rc;
-    HIP_OK(hipMemsetAsync(nxt, 0xff, slots * 4, L.s));  // -1: empty slots of the next round
-    HIP_OK(hipMemsetAsync(cnt, 0, 4, L.s));
-    launch_rlc_group_test(d, r, c->d_tables, gp, cur, G, gs, w.r_gcol.as<uint32_t>(), w.r_gfix.as<uint32_t>(), nxt,
+    launch_rlc_group_test(d, r, c->d_tables, gp, sel, G, gs, w.r_gcol.as<uint32_t>(), w.r_gfix.as<uint32_t>(), nxt,
                           cnt, L.s, &L.tl);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(&L.pin->flag, cnt, 4, hipMemcpyDeviceToHost, L.s));
+    return FTS_API_OK;
+  };
+  if (int rc = group_test(cur_big, (int)(sel_big.size() / c->gt1), c->gt1)) return rc;
+  if (int rc = group_test(cur_small, (int)(sel_small.size() / RP_GT2), RP_GT2)) return rc;
+  HIP_OK(hipMemcpyAsync(&L.pin->flag, cnt, 4, hipMemcpyDeviceToHost, L.s));
+  HIP_OK(L.sync());
+  const int nfail = L.pin->flag;
+  if (adapt && nfail > 0) {
+    // each batch's own density from its failing round-1 proofs
+    int32_t* hf = L.status_buf((size_t)nfail);
+    if (!hf) return FTS_API_ENOMEM;
+    HIP_OK(hipMemcpyAsync(hf, nxt, (size_t)nfail * 4, hipMemcpyDeviceToHost, L.s));
     HIP_OK(L.sync());
-    const int nfail = L.pin->flag;
-    if (round == 0 && adapt)
-      c->gt_dense.store(gs == RP_GT2 ? nfail > 0.02 * B : nfail > 0.5 * B, std::memory_order_relaxed);
-    if (nfail == 0) return FTS_API_OK;
-    std::swap(cur, nxt);
-    // per-proof checks of what is left; a second group test only pays when round 1
-    // left many proofs (the per-proof check's latency is one GLV chain whatever
-    // their number, its work grows with it)
-    if (round == 1 || gs <= RP_GT2 || nfail <= RP_GT2_MIN) {
-      launch_rp_fallback(d, c->d_tables, cur, nfail, L.s, &L.tl);
-      HIP_OK(hipGetLastError());
-      return FTS_API_OK;
+    std::vector<int> fails(nb, 0);
+    for (int i = 0; i < nfail; i++) {
+      const size_t q = (size_t)(std::upper_bound(groups.begin(), groups.end(), hf[i]) - groups.begin()) - 1;
+      if (q < nb) fails[q]++;
     }
-    gs = RP_GT2;
-    G = (nfail + RP_GT2 - 1) / RP_GT2;
-    if ((size_t)G > gmax) return FTS_API_EINVAL;  // cannot happen: nfail <= B
+    for (size_t q = 0; q < nb; q++) {
+      const int sz = groups[q + 1] - groups[q];
+      dense[q] = dense[q] ? fails[q] > 0.02 * sz : fails[q] > 0.5 * sz;
+    }
+  } else if (adapt) {
+    std::fill(dense.begin(), dense.end(), 0);
   }
+  if (nfail == 0) return FTS_API_OK;
+  // per-proof checks of what is left; a second group test only pays when round 1
+  // left many proofs in large groups (the per-proof check's latency is one GLV
+  // chain whatever their number, its work grows with it)
+  if (sel_big.empty() || nfail <= RP_GT2_MIN) {
+    launch_rp_fallback(d, c->d_tables, nxt, nfail, L.s, &L.tl);
+    HIP_OK(hipGetLastError());
+    return FTS_API_OK;
+  }
+  int32_t* cur = w.r_sel.as<int32_t>();  // round 2 over the survivors, groups of RP_GT2
+  HIP_OK(hipMemcpyAsync(cur, nxt, slots * 4, hipMemcpyDeviceToDevice, L.s));
+  HIP_OK(hipMemsetAsync(nxt, 0xff, slots * 4, L.s));
+  HIP_OK(hipMemsetAsync(cnt, 0, 4, L.s));
+  const int G2 = (nfail + RP_GT2 - 1) / RP_GT2;
+  if ((size_t)G2 > gmax) return FTS_API_EINVAL;  // cannot happen: nfail <= B
+  if (int rc = group_test(cur, G2, RP_GT2)) return rc;
+  HIP_OK(hipMemcpyAsync(&L.pin->flag, cnt, 4, hipMemcpyDeviceToHost, L.s));
+  HIP_OK(L.sync());
+  const int nfail2 = L.pin->flag;
+  if (nfail2 == 0) return FTS_API_OK;
+  launch_rp_fallback(d, c->d_tables, nxt, nfail2, L.s, &L.tl);
+  HIP_OK(hipGetLastError());
   return FTS_API_OK;
 }
 
@@ -1157,6 +1198,7 @@ struct RpPass {
   RpBatchDev d{};
   RlcDev r{};
   std::vector<int> groups;
+  std::vector<uint8_t> dense;  // per caller batch (groups[q] .. groups[q+1]): round-1 groups of 8; updated by the fallback
   double t_start = 0, t_prep = 0, t_enq = 0;
 };
 
@@ -1239,7 +1281,7 @@ static int rp_finish(fts_ctx* c, Lane& L, RpPass& P) {
   L.host_wait_ms = (float)(t_wait - P.t_enq);
   const int32_t flag = L.pin->flag;
   c->last_fallback = flag ? 0 : 1;
-  if (!flag) return rp_group_fallback(c, L, P.d, P.r, P.groups);
+  if (!flag) return rp_group_fallback(c, L, P.d, P.r, P.groups, P.dense);
   return FTS_API_OK;
 }
 
@@ -1308,6 +1350,7 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
                         w.rp_ipa.as<int32_t>(), [] {}, std::vector<int>(g.off, g.off + g.G + 1), P[j]);
     };
     rc[j] = enq();
+    for (RpReq* q : grp) P[j].dense.push_back(q->b->dense ? 1 : 0);
   }
   for (size_t j = 0; j < m; j++) {
     Lane& L = *lanes[j];
@@ -1317,6 +1360,7 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
     }
     auto fin = [&]() -> int {
       if (int r = rp_finish(c, L, P[j])) return r;
+      for (size_t q = 0; q < sub[j].size() && q < P[j].dense.size(); q++) sub[j][q]->b->dense = P[j].dense[q] != 0;
       int32_t* pst = L.status_buf(Bs[j]);
       if (!pst) return FTS_API_ENOMEM;
       HIP_OK(hipMemcpyAsync(pst, d_status[j], Bs[j] * 4, hipMemcpyDeviceToHost, L.s));

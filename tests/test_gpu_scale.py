@@ -298,13 +298,15 @@ def test_group_test_round2_exact_verdicts(pp_raw):
 
 def test_group_test_adaptive_dense_exact_verdicts(pp_raw):
     """fts_api.cpp rp_group_fallback, FTS_GT_ADAPT (default on): after a failed
-    pass whose bad proofs were dense (more than half the proofs in failing
-    256-groups) the context starts the next fallback at groups of 8 on the
-    small-group kernels, with no second round.  One caller batch of 512 rp16
-    proofs, 16 of them tampered (every 32nd: both 256-groups fail), verified
-    twice on one lane: both calls must give the oracle's verdicts; the first
-    runs the 256-group kernels, the second only the small-group ones and sends
-    at most the 16 failing 8-groups to the per-proof stage."""
+    verification whose bad proofs were dense (more than half the batch's proofs
+    in failing 256-groups) THAT caller batch starts its next fallback at groups
+    of 8 on the small-group kernels, with no second round.  One caller batch of
+    512 rp16 proofs, 16 of them tampered (every 32nd: both 256-groups fail),
+    verified twice on one lane: both calls must give the oracle's verdicts; the
+    first runs the 256-group kernels, the second only the small-group ones and
+    sends at most the 16 failing 8-groups to the per-proof stage.  The state is
+    per caller batch: another staged batch with one bad proof,
+    verified after it on the same context, still starts at groups of 256."""
     import os
 
     import fts_gpu
@@ -353,5 +355,23 @@ def test_group_test_adaptive_dense_exact_verdicts(pp_raw):
     assert n2.count("fb:k_rlc_group_final") == 1, n2   # groups of 8, no second round
     per_proof = w2["fb:k_rp_terms_fixed"] / ((3 + 2 * 16) * 15 * 11 * 136)
     assert 1 <= round(per_proof) <= 8 * 16, per_proof
+    # a second caller's batch: one bad proof, its own (sparse) group size
+    vals2 = [rng.getrandbits(16) for _ in range(m)]
+    bfs2 = [rng.randrange(bn.R).to_bytes(32, "big") for _ in range(m)]
+    proofs2, coms2 = pp.prove_range_batch_gpu(vals2, bfs2, seed=9400)
+    r = zkat.RangeProof.deserialize(proofs2[300])
+    r.data.T1 = bn.g1_add(r.data.T1, bn.GEN)
+    proofs2[300] = r.serialize()
+    other = pp.stage_range_proofs(proofs2, coms2)
+    out2 = [int(s) for s in other.verify()]
+    assert out2 == [fts_gpu.FTS_E_RP_INVALID if i == 300 else 0 for i in range(m)]
+    n3, _ = _raw_timing_names(other)
+    assert "fb:k_rlc_group_columns" in n3 and "fb:k_rlc_group_cols" not in n3, n3
+    # and the dense batch keeps its own state
+    out = [int(s) for s in batch.verify()]
+    assert out == expect
+    n4, _ = _raw_timing_names(batch)
+    assert "fb:k_rlc_group_cols" in n4 and "fb:k_rlc_group_columns" not in n4, n4
+    other.close()
     batch.close()
     pp.close()
