@@ -169,9 +169,11 @@ def main():
                          "tampered proofs exercises the group-test fallback); verdicts are checked every step")
     ap.add_argument("--cpu-sample", type=int, default=256, help="CPU baseline chunk size (0: skip the CPU baseline)")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--host-steps", type=int, default=32,
+    ap.add_argument("--host-steps", type=int, default=64,
                     help="rp workload: calls of fts_rp_verify_batch from host DER bytes after the timed region "
                          "(the PCIe-inclusive rate, reported apart; 0: skip)")
+    ap.add_argument("--host-inflight", type=int, default=16,
+                    help="rp workload: host threads calling fts_rp_verify_batch concurrently for host_inclusive")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall-time bound of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic per launch (tools/pmc_traffic.py); default: the newest profiles/traffic_rNN.json")
@@ -429,7 +431,7 @@ def main():
                     pp._ctx, B, ptrs, lens, comsb, st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
                 assert (st == wants[0]).all()
                 return st
-        hs = [HostStep() for _ in range(min(8, args.host_steps))]
+        hs = [HostStep() for _ in range(max(1, min(args.host_inflight, args.host_steps)))]
         _run_action_steps(hs, len(hs), None, None)  # warm the host pool
         h_el, _ = _run_action_steps(hs, args.host_steps, None, None)
         host_inclusive = {"value": round(B * args.host_steps / h_el, 1), "unit": "verifies/s",

@@ -69,6 +69,11 @@ struct MsmPlan {
   int ptsg;        // points per group
   int NBg, NSg;    // buckets / segments per group
   int ch;          // points per bucket-accumulation chunk (MSM_CH)
+  // block-local counting sort (msm.hip k_msm_lhist / k_msm_lscatter) instead of
+  // k_msm_digits' global atomics: standalone MSMs only.  Beside the batch
+  // check's chain kernels its 1,024-thread, 128 KB-LDS blocks took whole CUs
+  // (81,920-proof bursts 4.10-4.20 -> 3.96-3.99 M rp64/s)
+  bool local_sort;
   const int32_t* sel;  // device: proof indirection (grouped fallback), or nullptr
   int sel_pts;         // points per proof of the indirection
   MsmWindow win[MSM_MAX_WINDOWS];  // host copy
@@ -145,7 +150,13 @@ inline void msm_layout_groups(int N, int G, int ptsg, MsmPlan& p) {
   p.NV = NV;
   p.sel = nullptr;
   p.sel_pts = 1;
+  p.local_sort = false;
 }
 inline void msm_layout(int N, MsmPlan& p) { msm_layout_groups(N, 1, N > 0 ? N : 1, p); }
+// points per bucket-accumulation chunk (and the chunk-slot count that follows)
+inline void msm_set_chunk(MsmPlan& p, int ch) {
+  p.ch = ch;
+  p.NC = p.nw * (p.NV / ch + 1) + p.NB;
+}
 
 }  // namespace fts

@@ -184,9 +184,14 @@ FTS_DEV F6<B> mul_fp(const F6<B>& x, const typename B::F& s) {
 // Karatsuba: 6 Fp2 products.  Fp6 / Fp12 operations are out of line (PAIR_FN): a
 // fully inlined pairing is ~10^6 instructions (compile time and instruction cache);
 // each callee stays far below the s_cbranch range (tools/long_branch_check.py).
+// The hot loops (Miller squaring + line products, the cyclotomic squarings of
+// expt) use the *_i inline bodies instead, so their Fp12 accumulator stays in
+// VGPRs: every out-of-line call passes its Fp6/Fp12 operands through the
+// private stack (round 3: 9.8 KB of stack per lane, ~1.7 MB of scratch traffic
+// per identity).
 #define PAIR_FN __device__ __noinline__
 template <class B>
-PAIR_FN F6<B> mul(const F6<B>& x, const F6<B>& y) {
+FTS_DEV F6<B> mul6_i(const F6<B>& x, const F6<B>& y) {
   const F2<B> t0 = mul(x.c0, y.c0), t1 = mul(x.c1, y.c1), t2 = mul(x.c2, y.c2);
   F6<B> r;
   r.c0 = add(t0, mul_xi(sub(sub(mul(add(x.c1, x.c2), add(y.c1, y.c2)), t1), t2)));
@@ -194,15 +199,23 @@ PAIR_FN F6<B> mul(const F6<B>& x, const F6<B>& y) {
   r.c2 = add(sub(sub(mul(add(x.c0, x.c2), add(y.c0, y.c2)), t0), t2), t1);
   return r;
 }
+template <class B>
+PAIR_FN F6<B> mul(const F6<B>& x, const F6<B>& y) {
+  return mul6_i(x, y);
+}
 // x * (A + B v): 5 Fp2 products
 template <class B>
-PAIR_FN F6<B> mul_01(const F6<B>& x, const F2<B>& A, const F2<B>& Bv) {
+FTS_DEV F6<B> mul01_i(const F6<B>& x, const F2<B>& A, const F2<B>& Bv) {
   const F2<B> t0 = mul(x.c0, A), t1 = mul(x.c1, Bv);
   F6<B> r;
   r.c0 = add(t0, mul_xi(mul(x.c2, Bv)));
   r.c1 = sub(sub(mul(add(x.c0, x.c1), add(A, Bv)), t0), t1);
   r.c2 = add(t1, mul(x.c2, A));
   return r;
+}
+template <class B>
+PAIR_FN F6<B> mul_01(const F6<B>& x, const F2<B>& A, const F2<B>& Bv) {
+  return mul01_i(x, A, Bv);
 }
 template <class B>
 PAIR_FN F6<B> inv(const F6<B>& x) {
@@ -230,22 +243,29 @@ FTS_DEV bool is_one(const F12<B>& x) {
   return eq(x.c0.c0, f2_one<B>()) && is_zero(x.c0.c1) && is_zero(x.c0.c2) && is_zero(x.c1.c0) &&
          is_zero(x.c1.c1) && is_zero(x.c1.c2);
 }
+// (Fp6 products inline: one call per Fp12 product, not four; every kernel that
+// reaches these functions has __launch_bounds__(64), so a callee may use the
+// full register file instead of the 128 VGPRs of a 1,024-thread block)
 template <class B>
 PAIR_FN F12<B> mul(const F12<B>& x, const F12<B>& y) {
-  const F6<B> t0 = mul(x.c0, y.c0), t1 = mul(x.c1, y.c1);
+  const F6<B> t0 = mul6_i(x.c0, y.c0), t1 = mul6_i(x.c1, y.c1);
   F12<B> r;
-  r.c1 = sub(sub(mul(add(x.c0, x.c1), add(y.c0, y.c1)), t0), t1);
+  r.c1 = sub(sub(mul6_i(add(x.c0, x.c1), add(y.c0, y.c1)), t0), t1);
   r.c0 = add(t0, mul_v(t1));
   return r;
 }
 // complex squaring: 2 Fp6 products
 template <class B>
-PAIR_FN F12<B> sqr(const F12<B>& x) {
-  const F6<B> t = mul(x.c0, x.c1);
+FTS_DEV F12<B> sqr12_i(const F12<B>& x) {
+  const F6<B> t = mul6_i(x.c0, x.c1);
   F12<B> r;
-  r.c0 = sub(sub(mul(add(x.c0, x.c1), add(x.c0, mul_v(x.c1))), t), mul_v(t));
+  r.c0 = sub(sub(mul6_i(add(x.c0, x.c1), add(x.c0, mul_v(x.c1))), t), mul_v(t));
   r.c1 = add(t, t);
   return r;
+}
+template <class B>
+PAIR_FN F12<B> sqr(const F12<B>& x) {
+  return sqr12_i(x);
 }
 // Granger-Scott squaring in the cyclotomic subgroup (after the easy part of the
 // final exponentiation): Fp12 = Fp4[w]/(w^3 - s), s = w^3, s^2 = xi;
@@ -263,7 +283,7 @@ FTS_DEV F2<B> three(const F2<B>& x) {
   return add(add(x, x), x);
 }
 template <class B>
-PAIR_FN F12<B> cyc_sqr(const F12<B>& x) {
+FTS_DEV F12<B> cyc_sqr_i(const F12<B>& x) {
   // z0 = c0.c0, z1 = c1.c0, z2 = c0.c1, z3 = c1.c1, z4 = c0.c2, z5 = c1.c2
   F2<B> a0, a1, b0, b1, c0, c1;
   sq4(x.c0.c0, x.c1.c1, a0, a1);
@@ -277,6 +297,10 @@ PAIR_FN F12<B> cyc_sqr(const F12<B>& x) {
   r.c0.c1 = sub(three(b0), dbl(x.c0.c1));          // z2'
   r.c1.c2 = add(three(b1), dbl(x.c1.c2));          // z5'
   return r;
+}
+template <class B>
+PAIR_FN F12<B> cyc_sqr(const F12<B>& x) {
+  return cyc_sqr_i(x);
 }
 
 template <class B>
@@ -381,74 +405,98 @@ FTS_DEV void precompute_lines(const F2<B>& qx, const F2<B>& qy, uint32_t* out) {
 
 // f <- f * l(P) for the line (lam, mu) at P = (xP, yP) (affine G1, Montgomery)
 template <class B>
-PAIR_FN void line_mul(F12<B>& f, const uint32_t* ln, const typename B::F& xP, const typename B::F& yP) {
+FTS_DEV void line_mul_i(F12<B>& f, const uint32_t* ln, const typename B::F& xP, const typename B::F& yP) {
   const F2<B> lam = load_f2<B>(ln), mu = load_f2<B>(ln + 16);
   const F2<B> A = neg(mul_fp(lam, xP));
   F12<B> r;
   if constexpr (!B::K::M_TWIST) {
     // l = yP + A w + mu v w:  c0 = (yP, 0, 0), c1 = (A, mu, 0)
-    r.c0 = add(mul_fp(f.c0, yP), mul_v(mul_01(f.c1, A, mu)));
-    r.c1 = add(mul_01(f.c0, A, mu), mul_fp(f.c1, yP));
+    r.c0 = add(mul_fp(f.c0, yP), mul_v(mul01_i(f.c1, A, mu)));
+    r.c1 = add(mul01_i(f.c0, A, mu), mul_fp(f.c1, yP));
   } else {
     // l w^3 = mu + A v + yP v w:  c0 = (mu, A, 0), c1 = (0, yP, 0)
-    r.c0 = add(mul_01(f.c0, mu, A), mul_fp(mul_v(mul_v(f.c1)), yP));
-    r.c1 = add(mul_fp(mul_v(f.c0), yP), mul_01(f.c1, mu, A));
+    r.c0 = add(mul01_i(f.c0, mu, A), mul_fp(mul_v(mul_v(f.c1)), yP));
+    r.c1 = add(mul_fp(mul_v(f.c0), yP), mul01_i(f.c1, mu, A));
   }
   f = r;
 }
 
-// prod_j e(Q_j, P_j) Miller value for NP pairs: lines[j] = Q_j's precomputed table
+// prod_j e(Q_j, P_j) Miller value for NP pairs: lines[j] = Q_j's precomputed table.
+// One rolled loop over the steps (i = ATE_BITS-2 .. 0, then the two Frobenius
+// lines as step -1) and, inside it, one rolled loop over the step's line
+// products: a single inlined copy of the squaring and of the line product, f in
+// VGPRs throughout.
 template <class B, int NP>
 FTS_DEV F12<B> miller(const uint32_t* const (&lines)[NP], const typename B::F (&xP)[NP],
                       const typename B::F (&yP)[NP]) {
   using K = typename B::K;
+  using F = typename B::F;
   F12<B> f = f12_one<B>();
   int idx = 0;
-  for (int i = K::ATE_BITS - 2; i >= 0; i--) {
-    if (i != K::ATE_BITS - 2) f = sqr(f);
+#pragma unroll 1
+  for (int i = K::ATE_BITS - 2; i >= -1; i--) {
+    if (i >= 0 && i != K::ATE_BITS - 2) f = sqr12_i(f);
+    if (i < 0 && K::ATE_NEG) f = conj(f);
+    const int nl = i < 0 ? 2 : 1 + (int)ate_bit<K>(i);
+#pragma unroll 1
+    for (int q = 0; q < nl * NP; q++) {
+      const int j = q % NP;
+      const uint32_t* L = lines[0];
+      F x = xP[0], y = yP[0];
 #pragma unroll
-    for (int j = 0; j < NP; j++) line_mul<B>(f, lines[j] + idx * LINE_WORDS, xP[j], yP[j]);
-    idx++;
-    if (ate_bit<K>(i)) {
-#pragma unroll
-      for (int j = 0; j < NP; j++) line_mul<B>(f, lines[j] + idx * LINE_WORDS, xP[j], yP[j]);
-      idx++;
+      for (int jj = 1; jj < NP; jj++)
+        if (j == jj) L = lines[jj], x = xP[jj], y = yP[jj];
+      line_mul_i<B>(f, L + (idx + q / NP) * LINE_WORDS, x, y);
     }
-  }
-  if (K::ATE_NEG) f = conj(f);
-  for (int s = 0; s < 2; s++) {
-#pragma unroll
-    for (int j = 0; j < NP; j++) line_mul<B>(f, lines[j] + idx * LINE_WORDS, xP[j], yP[j]);
-    idx++;
+    idx += nl;
   }
   return f;
 }
 
-// f^u in the cyclotomic subgroup (inverse = conjugate)
+// f^u in the cyclotomic subgroup (inverse = conjugate): the squarings inline,
+// the ~27 multiplications by f out of line
 template <class B>
-PAIR_FN F12<B> expt(const F12<B>& f) {
+FTS_DEV F12<B> expt_i(const F12<B>& f) {
   using K = typename B::K;
   constexpr int TOP = 63 - __builtin_clzll(K::U);
   F12<B> r = f;
+#pragma unroll 1
   for (int i = TOP - 1; i >= 0; i--) {
-    r = cyc_sqr(r);
-    if ((K::U >> i) & 1ull) r = mul(r, f);
+    r = cyc_sqr_i(r);
+    if ((K::U >> i) & 1ull) {  // the callee gets a copy: r itself never escapes to memory
+      const F12<B> t = r;
+      r = mul(t, f);
+    }
   }
   return K::U_NEG ? conj(r) : r;
 }
-
 template <class B>
-PAIR_FN F12<B> final_exp(const F12<B>& f0) {
+PAIR_FN F12<B> expt(const F12<B>& f) {
+  return expt_i(f);
+}
+
+// final exponentiation; the _i form is inlined into the kernel, so its three
+// exponentiations by u (one rolled loop, one copy of the squaring) run with the
+// kernel's register budget: a callee is held to 128 VGPRs and spilled its
+// Fp12 accumulator on every squaring
+template <class B>
+FTS_DEV F12<B> final_exp_i(const F12<B>& f0) {
   F12<B> f = mul(conj(f0), inv(f0));
   f = mul(frob<B, 2>(f), f);
-  const F12<B> fu = expt(f), fu2 = expt(fu), fu3 = expt(fu2);
+  F12<B> fu[3];
+  F12<B> cur = f;
+#pragma unroll 1
+  for (int e = 0; e < 3; e++) {
+    cur = expt_i(cur);
+    fu[e] = cur;
+  }
   const F12<B> y0 = mul(mul(frob<B, 1>(f), frob<B, 2>(f)), frob<B, 3>(f));
   const F12<B> y1 = conj(f);
-  const F12<B> y2 = frob<B, 2>(fu2);
-  const F12<B> y3 = conj(frob<B, 1>(fu));
-  const F12<B> y4 = conj(mul(fu, frob<B, 1>(fu2)));
-  const F12<B> y5 = conj(fu2);
-  const F12<B> y6 = conj(mul(fu3, frob<B, 1>(fu3)));
+  const F12<B> y2 = frob<B, 2>(fu[1]);
+  const F12<B> y3 = conj(frob<B, 1>(fu[0]));
+  const F12<B> y4 = conj(mul(fu[0], frob<B, 1>(fu[1])));
+  const F12<B> y5 = conj(fu[1]);
+  const F12<B> y6 = conj(mul(fu[2], frob<B, 1>(fu[2])));
   F12<B> t0 = mul(mul(cyc_sqr(y6), y4), y5);
   F12<B> t1 = mul(mul(y3, y5), t0);
   t0 = mul(t0, y2);
@@ -457,6 +505,10 @@ PAIR_FN F12<B> final_exp(const F12<B>& f0) {
   t1 = mul(t1, y0);
   t0 = cyc_sqr(t0);
   return mul(t0, t1);
+}
+template <class B>
+PAIR_FN F12<B> final_exp(const F12<B>& f0) {
+  return final_exp_i(f0);
 }
 
 }  // namespace pair

@@ -1011,9 +1011,11 @@ static void collect_timings(fts_ctx* c, Lane& L, fts_rp_batch* b) {
 // MSM plan for N real points on lane L's workspace (buffers grown as needed,
 // window table uploaded on L.s).  Returns 0 or FTS_API_ENOMEM.
 static int msm_prepare_plan(Lane& L, MsmPlan& mp);
-static int msm_prepare(Lane& L, int N, MsmPlan& mp) {
+static int msm_prepare(Lane& L, int N, MsmPlan& mp, int ch = MSM_CH, bool local_sort = false) {
   mp = MsmPlan{};
   msm_layout(N, mp);
+  if (ch != MSM_CH) msm_set_chunk(mp, ch);
+  mp.local_sort = local_sort;
   return msm_prepare_plan(L, mp);
 }
 // buffers of an already laid-out plan (msm_layout / msm_layout_groups) on lane L
@@ -1222,7 +1224,10 @@ static int rp_enqueue(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc
   if (!L.presized && c->coalesce_max > (size_t)B && c->coalesce_max <= (1u << 20))
     if (int rc = lane_reserve(c, L, (int)c->coalesce_max, false)) return rc;
   MsmPlan mp{};
-  if (int rc = msm_prepare(L, N, mp)) return rc;
+#ifndef FTS_RLC_LOCAL_SORT  // A/B only: the block-local MSM sort for the batch check (default off, msm.hpp)
+#define FTS_RLC_LOCAL_SORT 0
+#endif
+  if (int rc = msm_prepare(L, N, mp, MSM_CH, FTS_RLC_LOCAL_SORT != 0)) return rc;
   if (int rc = rp_buffers(c, L, B)) return rc;
   RpBatchDev d{B,
                n,
@@ -1704,7 +1709,9 @@ int fts_msm_run(fts_ctx* c, fts_msm_batch* b, uint8_t* out64) {
   LaneGuard lg(c);
   Lane& L = *lg.L;
   MsmPlan mp{};
-  if (int rc = msm_prepare(L, b->N, mp)) return rc;
+  // standalone MSMs: the block-local counting sort; from 2^20 points 32-point
+  // chunks (~8 partials per bucket instead of ~32 at 2^22)
+  if (int rc = msm_prepare(L, b->N, mp, b->N >= (1 << 20) ? 32 : MSM_CH, true)) return rc;
   L.tl.begin(L.s);
   launch_msm(mp, b->pts, b->sc, nullptr, 0, L.ws.m_scratch.as<uint32_t>(), L.s, L.s, &L.tl);
   launch_msm_to_bytes(mp.out, b->out, L.s);

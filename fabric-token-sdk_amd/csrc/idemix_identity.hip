@@ -459,29 +459,43 @@ __global__ void __launch_bounds__(64) k_idv_lines(const uint8_t* __restrict__ wr
   pair::precompute_lines<B>(qx, qy, lines + (size_t)t * pair::n_lines<K>() * pair::LINE_WORDS);
 }
 
-// one identity per lane: status (pre-set by the host for identity-level errors),
-// then decode + t-values + transcript; pin[i] <- (A', -ABar) affine Montgomery and
-// zk[i] <- 1 if c == c'' for the pairing kernel
+// Lane scratch ([word][lane], n lanes each): S = t1..t5 accumulators (5 x 24),
+// DP = decoded points (NPT x 16), IDM = identity mask of the decoded points (1),
+// VR = the NVAR variable-base products (NVAR x 24), TV = their GLV lane tables
+// (NVAR x AT_WORDS; TV[0] doubles as the normalisation's prefix products)
+FTS_DEV size_t sc_s(size_t) { return 0; }
+FTS_DEV size_t sc_dp(size_t n) { return (size_t)5 * 24 * n; }
+FTS_DEV size_t sc_idm(size_t n) { return sc_dp(n) + (size_t)NPT * 16 * n; }
+FTS_DEV size_t sc_vr(size_t n) { return sc_idm(n) + n; }
+FTS_DEV size_t sc_tv(size_t n) { return sc_vr(n) + (size_t)NVAR * 24 * n; }
+inline size_t idv_scratch_words(size_t n) { return (5 * 24 + NPT * 16 + 1 + NVAR * (24 + AT_WORDS)) * n; }
+
+// Three kernels per batch (round 4; one lane per identity for everything left
+// 1,024 waves at one per SIMD, 30 % of the MAD peak):
+//   k_idv_decode  identity per lane: status (pre-set by the host for identity-
+//                 level errors), point decoding in the reference's order of
+//                 checks, pin[i] <- (A', -ABar) for the pairing kernel
+//   k_idv_var     lane per (variable-base product, identity): the six GLV
+//                 products of the t-values, 6x the lanes
+//   k_idv_tvals   identity per lane: sum the products into t1..t5, the fourteen
+//                 fixed-base products, normalisation, transcript, challenge;
+//                 zk[i] <- 1 if c == c''
 template <class CV>
-__global__ void __launch_bounds__(256) k_idv_tvals(int n, const uint32_t* __restrict__ rec,
-                                                   const uint8_t* __restrict__ pts, const uint8_t* __restrict__ epk,
-                                                   const uint32_t* __restrict__ tables,
-                                                   const uint32_t* __restrict__ ipk_hash,  // 8 BE words
-                                                   uint32_t* __restrict__ scratch, uint8_t* __restrict__ msg,
-                                                   uint32_t* __restrict__ pin, int32_t* __restrict__ zk,
-                                                   int32_t* __restrict__ status, const int32_t* __restrict__ eidx,
-                                                   const int32_t* __restrict__ g2ok) {
+__global__ void __launch_bounds__(256) k_idv_decode(int n, const uint32_t* __restrict__ rec,
+                                                    const uint8_t* __restrict__ pts, const uint8_t* __restrict__ epk,
+                                                    uint32_t* __restrict__ scratch, uint32_t* __restrict__ pin,
+                                                    int32_t* __restrict__ zk, int32_t* __restrict__ status,
+                                                    const int32_t* __restrict__ eidx, const int32_t* __restrict__ g2ok) {
   using B = typename CV::B;
   using F = typename CV::F;
-  using PJ = typename CV::PJ;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || status[i] != FTS_OK) return;
+  if (i >= n) return;
+  zk[i] = 0;
+  if (status[i] != FTS_OK) return;
   const uint32_t* R = rec + (size_t)i * REC_STRIDE;
   const uint8_t* P = pts + (size_t)i * NPT * 64;
   const uint32_t flags = R[R_FLAGS];
-  zk[i] = 0;
-  // decoded points (affine Montgomery) in lane scratch: DP [7][16] words, identity mask
-  const LaneWords DP{scratch + (size_t)(5 * 24 + AT_WORDS) * n, (size_t)n, (size_t)i};
+  const LaneWords DP{scratch + sc_dp(n), (size_t)n, (size_t)i};
   uint32_t okm = 0, idm = 0;
 #pragma unroll 1
   for (int q = 0; q < NPT; q++) {
@@ -492,6 +506,7 @@ __global__ void __launch_bounds__(256) k_idv_tvals(int n, const uint32_t* __rest
     put_f<CV>(DP, q * 16, px);
     put_f<CV>(DP, q * 16 + 8, py);
   }
+  scratch[sc_idm(n) + i] = idm;
   // NymPublicKey import (crypto/deserializer.go:49-56) precedes the proof
   if (!(okm & (1u << P_NYMPK))) {
     status[i] = FTS_E_ID_BADNYM;
@@ -529,17 +544,57 @@ __global__ void __launch_bounds__(256) k_idv_tvals(int n, const uint32_t* __rest
     return;
   }
   // pairing inputs: A' and -ABar
-  {
-    uint32_t* pq = pin + (size_t)i * 32;
-    const F ax = get_f<CV>(DP, P_AP * 16), ay = get_f<CV>(DP, P_AP * 16 + 8);
-    const F bx = get_f<CV>(DP, P_ABAR * 16), by = get_f<CV>(DP, P_ABAR * 16 + 8);
-    const F nby = (idm & (1u << P_ABAR)) ? by : B::neg(by);
+  uint32_t* pq = pin + (size_t)i * 32;
+  const F ax = get_f<CV>(DP, P_AP * 16), ay = get_f<CV>(DP, P_AP * 16 + 8);
+  const F bx = get_f<CV>(DP, P_ABAR * 16), by = get_f<CV>(DP, P_ABAR * 16 + 8);
+  const F nby = (idm & (1u << P_ABAR)) ? by : B::neg(by);
 #pragma unroll
-    for (int q = 0; q < 8; q++) pq[q] = ax.v[q], pq[8 + q] = ay.v[q], pq[16 + q] = bx.v[q], pq[24 + q] = nby.v[q];
-  }
+  for (int q = 0; q < 8; q++) pq[q] = ax.v[q], pq[8 + q] = ay.v[q], pq[16 + q] = bx.v[q], pq[24 + q] = nby.v[q];
+}
+
+// lane g = v * n + i: identities fastest, so a wave runs one product kind
+template <class CV>
+__global__ void __launch_bounds__(256) k_idv_var(int n, const uint32_t* __restrict__ rec,
+                                                 uint32_t* __restrict__ scratch, const int32_t* __restrict__ status) {
+  using B = typename CV::B;
+  using PJ = typename CV::PJ;
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (size_t)NVAR * n) return;
+  const int v = (int)(g / n), i = (int)(g % n);
+  if (status[i] != FTS_OK) return;
+  const uint32_t* R = rec + (size_t)i * REC_STRIDE;
+  const LaneWords DP{scratch + sc_dp(n), (size_t)n, (size_t)i};
+  const uint32_t idm = scratch[sc_idm(n) + i];
+  const int pq_ = VAR_PT[v] < 0 ? P_ABAR : VAR_PT[v];
+  PJ base = (idm >> pq_) & 1u ? CV::inf() : CV::from_affine(get_f<CV>(DP, pq_ * 16), get_f<CV>(DP, pq_ * 16 + 8));
+  if (VAR_PT[v] < 0 && !((idm >> P_BP) & 1u))  // D = ABar - B'
+    CV::madd_to(base, get_f<CV>(DP, P_BP * 16), B::neg(get_f<CV>(DP, P_BP * 16 + 8)));
+  const LaneWords T{scratch + sc_tv(n) + (size_t)v * AT_WORDS * n, (size_t)n, (size_t)i};
+  const PJ r = glv_mul<CV>(base, R + R_SC + v * 8, T);
+  const LaneWords VR{scratch + sc_vr(n) + (size_t)v * 24 * n, (size_t)n, (size_t)i};
+  put_f<CV>(VR, 0, r.x);
+  put_f<CV>(VR, 8, r.y);
+  put_f<CV>(VR, 16, r.z);
+}
+
+template <class CV>
+__global__ void __launch_bounds__(256) k_idv_tvals(int n, const uint32_t* __restrict__ rec,
+                                                   const uint32_t* __restrict__ tables,
+                                                   const uint32_t* __restrict__ ipk_hash,  // 8 BE words
+                                                   uint32_t* __restrict__ scratch, uint8_t* __restrict__ msg,
+                                                   int32_t* __restrict__ zk, const int32_t* __restrict__ status) {
+  using B = typename CV::B;
+  using F = typename CV::F;
+  using PJ = typename CV::PJ;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || status[i] != FTS_OK) return;
+  const uint32_t* R = rec + (size_t)i * REC_STRIDE;
+  const uint32_t flags = R[R_FLAGS];
+  const LaneWords DP{scratch + sc_dp(n), (size_t)n, (size_t)i};
+  const uint32_t idm = scratch[sc_idm(n) + i];
   // t-values: accumulators t1..t5 in lane scratch ([word][lane]), Jacobian
-  const LaneWords S{scratch, (size_t)n, (size_t)i};  // 5 x 24 accumulator words, then the GLV table
-  const LaneWords T{scratch + (size_t)5 * 24 * n, (size_t)n, (size_t)i};
+  const LaneWords S{scratch + sc_s(n), (size_t)n, (size_t)i};
+  const LaneWords T{scratch + sc_tv(n), (size_t)n, (size_t)i};
   for (int t = 0; t < 5; t++) {
     const PJ z = CV::inf();
     put_f<CV>(S, t * 24, z.x);
@@ -548,12 +603,9 @@ __global__ void __launch_bounds__(256) k_idv_tvals(int n, const uint32_t* __rest
   }
 #pragma unroll 1
   for (int v = 0; v < NVAR; v++) {
-    PJ base;
-    const int pq_ = VAR_PT[v] < 0 ? P_ABAR : VAR_PT[v];
-    base = (idm >> pq_) & 1u ? CV::inf() : CV::from_affine(get_f<CV>(DP, pq_ * 16), get_f<CV>(DP, pq_ * 16 + 8));
-    if (VAR_PT[v] < 0 && !((idm >> P_BP) & 1u))  // D = ABar - B'
-      CV::madd_to(base, get_f<CV>(DP, P_BP * 16), B::neg(get_f<CV>(DP, P_BP * 16 + 8)));
-    const PJ r = glv_mul<CV>(base, R + R_SC + v * 8, T);
+    const LaneWords VR{scratch + sc_vr(n) + (size_t)v * 24 * n, (size_t)n, (size_t)i};
+    PJ r;
+    r.x = get_f<CV>(VR, 0), r.y = get_f<CV>(VR, 8), r.z = get_f<CV>(VR, 16);
     const int t = VAR_T[v];
     PJ acc;
     acc.x = get_f<CV>(S, t * 24), acc.y = get_f<CV>(S, t * 24 + 8), acc.z = get_f<CV>(S, t * 24 + 16);
@@ -649,8 +701,13 @@ __global__ void __launch_bounds__(256) k_idv_tvals(int n, const uint32_t* __rest
 }
 
 // e(W, A') * e(g2, -ABar) == 1, then the verdict (pairing before the ZK proof, as Ver checks)
+// waves per SIMD the pairing kernel is compiled for (A/B: -DFTS_IDV_OCC=2 caps it
+// at 256 registers, with spills in the inlined Fp12 bodies)
+#ifndef FTS_IDV_OCC
+#define FTS_IDV_OCC 1
+#endif
 template <class CV>
-__global__ void __launch_bounds__(64) k_idv_pairing(int n, const uint32_t* __restrict__ pin,
+__global__ void __launch_bounds__(64, FTS_IDV_OCC) k_idv_pairing(int n, const uint32_t* __restrict__ pin,
                                                     const uint32_t* __restrict__ lines, const int32_t* __restrict__ zk,
                                                     int32_t* __restrict__ status) {
   using B = typename CV::B;
@@ -670,14 +727,14 @@ __global__ void __launch_bounds__(64) k_idv_pairing(int n, const uint32_t* __res
   } else {
     f = pair::miller<B, 2>(L, xP, yP);
   }
-  const bool one = pair::is_one(pair::final_exp(f));
+  const bool one = pair::is_one(pair::final_exp_i(f));
   status[i] = !one ? FTS_E_ID_PAIRING : (zk[i] ? FTS_OK : FTS_E_ID_ZK);
 }
 
 // debug: e(Q, P) for Q = W (which 0) or g2 (1), P affine Montgomery -> GT (12 Fp2
 // coefficients w^0..w^5 as (c0.c0, c1.c0, c0.c1, c1.c1, c0.c2, c1.c2), plain LE limbs)
 template <class CV>
-__global__ void k_idv_pairing_debug(const uint32_t* __restrict__ lines, int which, const uint32_t* __restrict__ p16,
+__global__ void __launch_bounds__(64) k_idv_pairing_debug(const uint32_t* __restrict__ lines, int which, const uint32_t* __restrict__ p16,
                                     uint32_t* __restrict__ out, int final_exp) {
   using B = typename CV::B;
   using K = typename B::K;
@@ -1188,7 +1245,7 @@ int fts_idemix_identity_verify_batch(fts_idemix_idv* K, size_t n, const uint8_t*
                o_uk = o_eidx + n * 4;
   const size_t h_need = (o_uk + epk_b + 255) & ~size_t(255);
   const size_t o_zk = h_need, o_pin = (o_zk + n * 4 + 255) & ~size_t(255), o_scr = o_pin + n * 32 * 4;
-  const size_t scr_w = (size_t)(5 * 24 + AT_WORDS + NPT * 16) * n;
+  const size_t scr_w = idv_scratch_words(n);
   const size_t o_msg = (o_scr + scr_w * 4 + 255) & ~size_t(255);
   const size_t o_g2ok = (o_msg + (size_t)MSG_MAX * n + 255) & ~size_t(255);
   const size_t d_need = o_g2ok + n * 4;
@@ -1256,7 +1313,8 @@ int fts_idemix_identity_verify_batch(fts_idemix_idv* K, size_t n, const uint8_t*
   uint8_t* d = D.d_buf;
   ICHK(hipMemcpyAsync(d, h, o_uk + U * 128, hipMemcpyHostToDevice, D.stream));
   ICHK(hipEventRecord(D.ev[0], D.stream));
-  const unsigned g256 = (unsigned)((n + 255) / 256), g64 = (unsigned)((n + 63) / 64);
+  const unsigned g256 = (unsigned)((n + 255) / 256), g64 = (unsigned)((n + 63) / 64),
+                 gvar = (unsigned)((NVAR * n + 255) / 256);
   const uint32_t* rec = reinterpret_cast<const uint32_t*>(d);
   uint32_t* scr = reinterpret_cast<uint32_t*>(d + o_scr);
   uint32_t* pin = reinterpret_cast<uint32_t*>(d + o_pin);
@@ -1266,14 +1324,17 @@ int fts_idemix_identity_verify_batch(fts_idemix_idv* K, size_t n, const uint8_t*
   int32_t* g2ok = reinterpret_cast<int32_t*>(d + o_g2ok);
   if (bn) {
     k_idv_g2_check<<<(unsigned)((U + 63) / 64), 64, 0, D.stream>>>((int)U, d + o_uk, g2ok);
-    k_idv_tvals<BnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, d + o_pts, d + o_epk, K->d_tables, K->d_hash, scr,
-                                                      d + o_msg, pin, zk, st, reinterpret_cast<const int32_t*>(d + o_eidx),
-                                                      g2ok);
+    k_idv_decode<BnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, d + o_pts, d + o_epk, scr, pin, zk, st,
+                                                       reinterpret_cast<const int32_t*>(d + o_eidx), g2ok);
+    k_idv_var<BnCurve><<<gvar, 256, 0, D.stream>>>((int)n, rec, scr, st);
+    k_idv_tvals<BnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, K->d_tables, K->d_hash, scr, d + o_msg, zk, st);
     ICHK(hipEventRecord(D.ev[1], D.stream));
     k_idv_pairing<BnCurve><<<g64, 64, 0, D.stream>>>((int)n, pin, K->d_lines, zk, st);
   } else {
-    k_idv_tvals<FbnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, d + o_pts, d + o_epk, K->d_tables, K->d_hash, scr,
-                                                       d + o_msg, pin, zk, st, nullptr, nullptr);
+    k_idv_decode<FbnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, d + o_pts, d + o_epk, scr, pin, zk, st, nullptr,
+                                                        nullptr);
+    k_idv_var<FbnCurve><<<gvar, 256, 0, D.stream>>>((int)n, rec, scr, st);
+    k_idv_tvals<FbnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, K->d_tables, K->d_hash, scr, d + o_msg, zk, st);
     ICHK(hipEventRecord(D.ev[1], D.stream));
     k_idv_pairing<FbnCurve><<<g64, 64, 0, D.stream>>>((int)n, pin, K->d_lines, zk, st);
   }

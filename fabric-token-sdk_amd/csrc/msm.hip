@@ -195,6 +195,114 @@ __global__ void __launch_bounds__(256) k_msm_scatter(int NV, int nw, const int32
   }
 }
 
+// ------------------------------------------------ large one-group plans
+// Counting sort without global atomics (N >= MSM_LS_MIN_N, one group, no
+// indirection): k_msm_digits' 16 returning device-scope atomics per point were
+// its cost at 2^22 points (3 ms).  Here the sort runs per (slice of virtual
+// points, window) block with the window's histogram in LDS:
+//   k_msm_split     lane per point: GLV halves + the recoding constant
+//   k_msm_lhist     block (slice, window): LDS histogram -> hs[w][slice][b]
+//   k_msm_lscan     lane per (window, bucket): prefix over the slices, counts
+//   (k_msm_scan1/2/3 as before: bucket offsets and the chunk map)
+//   k_msm_lscatter  block (slice, window): LDS cursors = bucket offset + slice
+//                   prefix; each entry takes the next slot of its bucket
+// Signed digits as bit fields: with C = sum_w (2^(width_w-1) - 1) 2^off_w,
+// window w's digit of k is ((k + C) >> off_w mod 2^width_w) - (2^(width_w-1) - 1)
+// (the carries of k + C are exactly the recoding carries of k_msm_digits:
+// d > half <=> bits + carry + half - 1 >= 2^width), so every block extracts
+// its window's digit without the lower windows.  Same buckets and signs as
+// k_msm_digits; the order inside a bucket differs (bucket sums are the same
+// group elements, and only the affine result is observable).
+constexpr int MSM_LS_SLICES = 64;
+constexpr int MSM_LS_MIN_N = 1 << 18;  // points
+constexpr int MSM_LS_BS = 1024;
+
+__global__ void __launch_bounds__(256) k_msm_split(int N, uint4 rc, const uint32_t* __restrict__ scalars,
+                                                   uint4* __restrict__ hk) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  uint32_t s[8];
+#pragma unroll
+  for (int q = 0; q < 8; q++) s[q] = scalars[(size_t)i * 8 + q];
+  uint32_t k[2][4], sg[2];
+  glv_decompose(s, k[0], sg[0], k[1], sg[1]);
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    uint64_t t = (uint64_t)k[h][0] + rc.x;
+    const uint32_t w0 = (uint32_t)t;
+    t = (t >> 32) + k[h][1] + rc.y;
+    const uint32_t w1 = (uint32_t)t;
+    t = (t >> 32) + k[h][2] + rc.z;
+    const uint32_t w2 = (uint32_t)t;
+    t = (t >> 32) + k[h][3] + rc.w;
+    const uint32_t w3 = ((uint32_t)t & 0x7fffffffu) | (sg[h] ? 0x80000000u : 0u);  // k + C < 2^127
+    hk[(size_t)h * N + i] = make_uint4(w0, w1, w2, w3);
+  }
+}
+
+FTS_DEV int ls_digit(const uint4 q, const MsmWindow& W) {
+  const uint32_t k[4] = {q.x, q.y, q.z, q.w & 0x7fffffffu};
+  return (int)scalar_bits4(k, W.off, W.width) - ((1 << (W.width - 1)) - 1);
+}
+
+__global__ void __launch_bounds__(MSM_LS_BS) k_msm_lhist(int NV, int per, int S, int stride,
+                                                        const MsmWindow* __restrict__ win,
+                                                        const uint4* __restrict__ hk, uint32_t* __restrict__ hs) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lh[];
+  const int sl = blockIdx.x, w = blockIdx.y;
+  const MsmWindow W = win[w];
+  const int nb = 1 << (W.width - 1);
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) lh[b] = 0;
+  __syncthreads();
+  const int v1 = min(NV, (sl + 1) * per);
+  for (int v = sl * per + threadIdx.x; v < v1; v += blockDim.x) {
+    const int d = ls_digit(hk[v], W);
+    if (d != 0) atomicAdd(&lh[(d < 0 ? -d : d) - 1], 1u);
+  }
+  __syncthreads();
+  uint32_t* out = hs + ((size_t)w * S + sl) * stride;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) out[b] = lh[b];
+}
+
+__global__ void __launch_bounds__(256) k_msm_lscan(int S, int stride, const MsmWindow* __restrict__ win,
+                                                  uint32_t* __restrict__ hs, uint32_t* __restrict__ counts) {
+  const int w = blockIdx.y, b = blockIdx.x * blockDim.x + threadIdx.x;
+  const MsmWindow W = win[w];
+  if (b >= (1 << (W.width - 1))) return;
+  uint32_t acc = 0;
+  for (int sl = 0; sl < S; sl++) {
+    uint32_t* q = hs + ((size_t)w * S + sl) * stride + b;
+    const uint32_t c = *q;
+    *q = acc;
+    acc += c;
+  }
+  counts[W.bbase + b] = acc;
+}
+
+__global__ void __launch_bounds__(MSM_LS_BS) k_msm_lscatter(int NV, int per, int S, int stride,
+                                                           const MsmWindow* __restrict__ win,
+                                                           const uint4* __restrict__ hk,
+                                                           const uint32_t* __restrict__ hs,
+                                                           const uint32_t* __restrict__ offsets,
+                                                           uint32_t* __restrict__ sorted) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
+  const int sl = blockIdx.x, w = blockIdx.y;
+  const MsmWindow W = win[w];
+  const int nb = 1 << (W.width - 1);
+  const uint32_t* pre = hs + ((size_t)w * S + sl) * stride;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) cur[b] = offsets[W.bbase + b] + pre[b];
+  __syncthreads();
+  const int v1 = min(NV, (sl + 1) * per);
+  for (int v = sl * per + threadIdx.x; v < v1; v += blockDim.x) {
+    const uint4 q = hk[v];
+    const int d = ls_digit(q, W);
+    if (d != 0) {
+      const uint32_t pos = atomicAdd(&cur[(d < 0 ? -d : d) - 1], 1u);
+      sorted[pos] = (uint32_t)v | (((d < 0) != ((q.w >> 31) != 0)) ? 0x80000000u : 0u);
+    }
+  }
+}
+
 // one lane per chunk slot: <= p.ch mixed additions of sorted virtual points
 // (index >= N: phi(P_{index-N}) = (beta x, y))
 __global__ void __launch_bounds__(64, 4) k_msm_chunks(MsmIdx p, const uint32_t* __restrict__ nc_total,
@@ -215,7 +323,8 @@ __global__ void __launch_bounds__(64, 4) k_msm_chunks(MsmIdx p, const uint32_t* 
   const Fp beta = glv_beta();
   G1J acc = g1j_identity();
   // the next entry's point is gathered while the current addition runs
-  // (absent points never get a bucket entry, so msm_src is >= 0 here)
+  // (absent points never get a bucket entry, so msm_src is >= 0 here; a
+  // two-deep prefetch measured slower: 2.29 -> 2.36 ms at 2^20 points)
   uint32_t e = S[lo];
   G1A q = load_g1a(points + (size_t)msm_src(p, (int)((e & 0x7fffffffu) >= (uint32_t)N ? (e & 0x7fffffffu) - N
                                                                                       : (e & 0x7fffffffu))) * 16);
@@ -456,15 +565,55 @@ __global__ void k_msm_to_bytes(const uint32_t* __restrict__ jac, uint8_t* __rest
 // digits, counting sort, chunked bucket accumulation and bucket sums (every plan)
 static void launch_msm_buckets(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, hipStream_t s,
                                Timeline* tl, hipEvent_t ev_stage = nullptr, int stage = 0) {
-  (void)hipMemsetAsync(p.counts, 0, (size_t)p.NB * 4, s);
-  FTS_LAUNCH(k_msm_digits, p.N, 256, s, msm_idx(p), p.d_win, scalars, p.keys, p.cursor, p.counts);
-  tl->mark("k_msm_digits", s, 0);
-  FTS_LAUNCH(k_msm_scan1, (size_t)p.NBLK * 256, 256, s, p.NB, p.ch, p.counts, p.offsets, p.chunk_off, p.scratch);
-  hipLaunchKernelGGL(k_msm_scan2, dim3(1), dim3(256), 0, s, p.NBLK, p.scratch);
-  FTS_LAUNCH(k_msm_scan3, p.NB, 256, s, p.NB, p.ch, p.counts, p.offsets, p.cursor, p.chunk_off, p.chunk_bkt, p.scratch);
-  tl->mark("k_msm_scan", s, 0);
-  FTS_LAUNCH(k_msm_scatter, p.NV, 256, s, p.NV, p.nw, p.keys, p.cursor, p.offsets, p.sorted);
-  tl->mark("k_msm_scatter", s, 0);
+  // block-local counting sort for large one-group plans (keys: the split
+  // halves, NV x 16 B; cursor: the slice histograms, nw x S x stride words)
+  int nbmax = 1;
+  for (int w = 0; w < p.nw; w++) nbmax = std::max(nbmax, 1 << (p.win[w].width - 1));
+  const int S = std::min(MSM_LS_SLICES, p.NV / nbmax);
+  const bool ls = p.local_sort && p.G == 1 && !p.sel && p.N >= MSM_LS_MIN_N && nbmax <= (1 << 15) && S >= 8 &&
+                  p.nw >= 4;
+  if (ls) {
+    uint32_t rc[4] = {0, 0, 0, 0};  // C = sum_w (2^(width_w-1) - 1) 2^off_w (< 2^126)
+    for (int w = 0; w < p.nw; w++) {
+      uint64_t add = (uint64_t)((1u << (p.win[w].width - 1)) - 1u);
+      const int q = p.win[w].off >> 5, r = p.win[w].off & 31;
+      uint64_t c = add << r;
+      for (int j = q; j < 4 && c; j++) {
+        const uint64_t t = (uint64_t)rc[j] + (c & 0xffffffffu);
+        rc[j] = (uint32_t)t;
+        c = (c >> 32) + (t >> 32);
+      }
+    }
+    const int per = (p.NV + S - 1) / S;
+    uint4* hk = reinterpret_cast<uint4*>(p.keys);
+    FTS_LAUNCH(k_msm_split, p.N, 256, s, p.N, make_uint4(rc[0], rc[1], rc[2], rc[3]), scalars, hk);
+    tl->mark("k_msm_split", s, 0);
+    const size_t lds = (size_t)nbmax * 4;
+    hipLaunchKernelGGL(k_msm_lhist, dim3(S, p.nw), dim3(MSM_LS_BS), lds, s, p.NV, per, S, nbmax, p.d_win, hk,
+                       p.cursor);
+    hipLaunchKernelGGL(k_msm_lscan, dim3((nbmax + 255) / 256, p.nw), dim3(256), 0, s, S, nbmax, p.d_win, p.cursor,
+                       p.counts);
+    tl->mark("k_msm_lhist", s, 0);
+    FTS_LAUNCH(k_msm_scan1, (size_t)p.NBLK * 256, 256, s, p.NB, p.ch, p.counts, p.offsets, p.chunk_off, p.scratch);
+    hipLaunchKernelGGL(k_msm_scan2, dim3(1), dim3(256), 0, s, p.NBLK, p.scratch);
+    FTS_LAUNCH(k_msm_scan3, p.NB, 256, s, p.NB, p.ch, p.counts, p.offsets, nullptr, p.chunk_off, p.chunk_bkt,
+               p.scratch);
+    tl->mark("k_msm_scan", s, 0);
+    hipLaunchKernelGGL(k_msm_lscatter, dim3(S, p.nw), dim3(MSM_LS_BS), lds, s, p.NV, per, S, nbmax, p.d_win, hk,
+                       p.cursor, p.offsets, p.sorted);
+    tl->mark("k_msm_lscatter", s, 0);
+  } else {
+    (void)hipMemsetAsync(p.counts, 0, (size_t)p.NB * 4, s);
+    FTS_LAUNCH(k_msm_digits, p.N, 256, s, msm_idx(p), p.d_win, scalars, p.keys, p.cursor, p.counts);
+    tl->mark("k_msm_digits", s, 0);
+    FTS_LAUNCH(k_msm_scan1, (size_t)p.NBLK * 256, 256, s, p.NB, p.ch, p.counts, p.offsets, p.chunk_off, p.scratch);
+    hipLaunchKernelGGL(k_msm_scan2, dim3(1), dim3(256), 0, s, p.NBLK, p.scratch);
+    FTS_LAUNCH(k_msm_scan3, p.NB, 256, s, p.NB, p.ch, p.counts, p.offsets, p.cursor, p.chunk_off, p.chunk_bkt,
+               p.scratch);
+    tl->mark("k_msm_scan", s, 0);
+    FTS_LAUNCH(k_msm_scatter, p.NV, 256, s, p.NV, p.nw, p.keys, p.cursor, p.offsets, p.sorted);
+    tl->mark("k_msm_scatter", s, 0);
+  }
   if (ev_stage && stage == 1) (void)hipEventRecord(ev_stage, s);
   FTS_LAUNCH(k_msm_chunks, p.NC, 64, s, msm_idx(p), p.scratch + 2 * (size_t)p.NBLK + 1, p.d_win, points, p.offsets,
              p.counts, p.chunk_off,

@@ -6,7 +6,7 @@ path, the same exact intermediates (com, H'_i, x0: ipa.go:200-213).
 Knobs covered elsewhere: FTS_LANES, FTS_COM_FIXED_MAX (test_gpu_rp.py,
 test_gpu_scale.py), FTS_GT1 / FTS_GT2_MIN / FTS_GT_ADAPT (test_gpu_scale.py),
 FTS_NYM_TILE (test_idemix.py).  Here: FTS_RLC_FORK, FTS_X0_SPLIT,
-FTS_COALESCE_MAX, FTS_GATHER_US."""
+FTS_COALESCE_MAX, FTS_GATHER_US, FTS_GT_ADAPT=0."""
 import json
 import os
 import random
@@ -130,5 +130,39 @@ def test_knob_coalescing(pp_raw, env):
                 assert (st == want).all(), (rep, np.nonzero(st != want)[0][:8], merged)
         for b, _ in batches:
             b.close()
+    finally:
+        pp.close()
+
+
+def test_knob_gt_adapt_off(pp_raw):
+    """FTS_GT_ADAPT=0: a caller batch whose bad proofs are dense (every 32nd of
+    512 tampered) keeps starting its group test at 256-groups on every call
+    (with the default it moves to groups of 8 after the first, test_gpu_scale.py);
+    the verdicts are the same on every call"""
+    from test_gpu_scale import _raw_timing_names
+    pp = _ctx(pp_raw, 16, FTS_GT_ADAPT=0, FTS_LANES=1)
+    try:
+        rng = random.Random(0x6AD0)
+        m = 512
+        vals = [rng.getrandbits(16) for _ in range(m)]
+        bfs = [rng.randrange(bn.R).to_bytes(32, "big") for _ in range(m)]
+        proofs, coms = pp.prove_range_batch_gpu(vals, bfs, seed=0x6AD0)
+        want = np.zeros(m, dtype=np.int32)
+        for i in range(5, m, 32):
+            t = zkat.RangeProof.deserialize(proofs[i])
+            if (i // 32) % 2:
+                t.data.T1 = bn.g1_add(t.data.T1, bn.GEN)
+                want[i] = 3
+            else:
+                t.ipa.R[1] = bn.g1_add(t.ipa.R[1], bn.GEN)
+                want[i] = 6
+            proofs[i] = t.serialize()
+        b = pp.stage_range_proofs(proofs, coms)
+        for rep in range(3):
+            st = b.verify()
+            assert (st == want).all(), (rep, np.nonzero(st != want)[0][:8])
+            names, _ = _raw_timing_names(b)
+            assert "fb:k_rlc_group_columns" in names, (rep, names)
+        b.close()
     finally:
         pp.close()

@@ -7,6 +7,9 @@
   Makefile) must be flagged, so the guard is known to fire.
 * the product code issues no MFMA instruction (DESIGN.md §5 "No MFMA": this is
   carry-propagating modular arithmetic on the INT32 VALU).
+* every kernel the library's host side can launch has device code
+  (tools/kernel_symbol_check.py: an object whose host and device passes saw
+  different sources aborts at the first launch with "Cannot find Symbol").
 """
 import os
 import subprocess
@@ -16,6 +19,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
+import kernel_symbol_check as ksc  # noqa: E402
 import long_branch_check as lbc  # noqa: E402
 
 LIB = os.path.join(ROOT, "fabric-token-sdk_amd", "lib", "libfts_gpu.so")
@@ -54,3 +58,26 @@ def test_product_code_has_no_mfma(tmp_path):
     for co in cos:
         dis = subprocess.check_output([lbc.OBJDUMP, "-d", co], text=True)
         assert "v_mfma" not in dis, co
+
+
+def test_every_host_kernel_stub_has_device_code():
+    _need(LIB)
+    assert ksc.check(LIB) == []
+
+
+def test_kernel_symbol_guard_flags_a_host_device_mismatch(tmp_path):
+    """a translation unit whose device pass defines k_a but whose host pass
+    launches k_b: the library links, and the guard must name k_b"""
+    src = tmp_path / "mismatch.hip"
+    src.write_text("#include <hip/hip_runtime.h>\n"
+                   "#ifdef __HIP_DEVICE_COMPILE__\n"
+                   "__global__ void k_a(int* p) { *p = 1; }\n"
+                   "#else\n"
+                   "__global__ void k_b(int* p) { *p = 1; }\n"
+                   "extern \"C\" void launch(int* p) { hipLaunchKernelGGL(k_b, 1, 1, 0, 0, p); }\n"
+                   "#endif\n")
+    lib = tmp_path / "libmismatch.so"
+    subprocess.check_call([lbc.HIPCC, "--offload-arch=gfx950", "-O1", "-shared", "-fPIC", "-x", "hip", str(src),
+                           "-o", str(lib)])
+    missing = ksc.check(str(lib))
+    assert len(missing) == 1 and "k_b" in missing[0], missing
