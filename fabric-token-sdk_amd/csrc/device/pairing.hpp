@@ -421,6 +421,44 @@ FTS_DEV void line_mul_i(F12<B>& f, const uint32_t* ln, const typename B::F& xP, 
   f = r;
 }
 
+// f <- f * l1(P1) * l2(P2) for two lines of the same Miller step: the lines'
+// product first (sparse x sparse: 9 Fp2 + 8 Fp products; one Fp6 half has a
+// zero coefficient), then one Fp12 product with that sparse half (17 Fp2
+// products): ~73 base-field products instead of 2 x 44 for two line_mul_i
+//   D-type l_j: c0 = (yP_j, 0, 0), c1 = (A_j, mu_j, 0)
+//     L.c0 = (y1 y2 + xi mu1 mu2, A1 A2, A1 mu2 + mu1 A2), L.c1 = (y1 A2 + y2 A1, y1 mu2 + y2 mu1, 0)
+//   M-type l_j: c0 = (mu_j, A_j, 0), c1 = (0, yP_j, 0)
+//     L.c0 = (mu1 mu2 + xi y1 y2, mu1 A2 + A1 mu2, A1 A2), L.c1 = (0, y2 mu1 + y1 mu2, y2 A1 + y1 A2)
+template <class B>
+FTS_DEV void line2_mul_i(F12<B>& f, const uint32_t* ln1, const typename B::F& xP1, const typename B::F& yP1,
+                         const uint32_t* ln2, const typename B::F& xP2, const typename B::F& yP2) {
+  const F2<B> lam1 = load_f2<B>(ln1), mu1 = load_f2<B>(ln1 + 16);
+  const F2<B> lam2 = load_f2<B>(ln2), mu2 = load_f2<B>(ln2 + 16);
+  const F2<B> A1 = neg(mul_fp(lam1, xP1)), A2 = neg(mul_fp(lam2, xP2));
+  const F2<B> aa = mul(A1, A2), mm = mul(mu1, mu2);
+  const F2<B> am = sub(sub(mul(add(A1, mu1), add(A2, mu2)), aa), mm);  // A1 mu2 + mu1 A2
+  F2<B> yy;
+  yy.a = B::mul(yP1, yP2);
+  yy.b = B::zero();
+  F6<B> L0, L1;
+  if constexpr (!B::K::M_TWIST) {
+    L0 = {add(yy, mul_xi(mm)), aa, am};
+    L1 = {add(mul_fp(A2, yP1), mul_fp(A1, yP2)), add(mul_fp(mu2, yP1), mul_fp(mu1, yP2)), f2_zero<B>()};
+  } else {
+    L0 = {add(mm, mul_xi(yy)), am, aa};
+    L1 = {f2_zero<B>(), add(mul_fp(mu1, yP2), mul_fp(mu2, yP1)), add(mul_fp(A1, yP2), mul_fp(A2, yP1))};
+  }
+  const F6<B> t0 = mul6_i(f.c0, L0);
+  F6<B> t1;
+  if constexpr (!B::K::M_TWIST)
+    t1 = mul01_i(f.c1, L1.c0, L1.c1);
+  else  // (b1 v + b2 v^2) = v (b1 + b2 v)
+    t1 = mul_v(mul01_i(f.c1, L1.c1, L1.c2));
+  const F6<B> t2 = mul6_i(add(f.c0, f.c1), add(L0, L1));
+  f.c1 = sub(sub(t2, t0), t1);
+  f.c0 = add(t0, mul_v(t1));
+}
+
 // prod_j e(Q_j, P_j) Miller value for NP pairs: lines[j] = Q_j's precomputed table.
 // One rolled loop over the steps (i = ATE_BITS-2 .. 0, then the two Frobenius
 // lines as step -1) and, inside it, one rolled loop over the step's line
@@ -438,44 +476,75 @@ FTS_DEV F12<B> miller(const uint32_t* const (&lines)[NP], const typename B::F (&
     if (i >= 0 && i != K::ATE_BITS - 2) f = sqr12_i(f);
     if (i < 0 && K::ATE_NEG) f = conj(f);
     const int nl = i < 0 ? 2 : 1 + (int)ate_bit<K>(i);
+    if constexpr (NP == 2) {
 #pragma unroll 1
-    for (int q = 0; q < nl * NP; q++) {
-      const int j = q % NP;
-      const uint32_t* L = lines[0];
-      F x = xP[0], y = yP[0];
+      for (int q = 0; q < nl; q++)
+        line2_mul_i<B>(f, lines[0] + (idx + q) * LINE_WORDS, xP[0], yP[0], lines[1] + (idx + q) * LINE_WORDS, xP[1],
+                       yP[1]);
+    } else {
+#pragma unroll 1
+      for (int q = 0; q < nl * NP; q++) {
+        const int j = q % NP;
+        const uint32_t* L = lines[0];
+        F x = xP[0], y = yP[0];
 #pragma unroll
-      for (int jj = 1; jj < NP; jj++)
-        if (j == jj) L = lines[jj], x = xP[jj], y = yP[jj];
-      line_mul_i<B>(f, L + (idx + q / NP) * LINE_WORDS, x, y);
+        for (int jj = 1; jj < NP; jj++)
+          if (j == jj) L = lines[jj], x = xP[jj], y = yP[jj];
+        line_mul_i<B>(f, L + (idx + q / NP) * LINE_WORDS, x, y);
+      }
     }
     idx += nl;
   }
   return f;
 }
 
-// f^u in the cyclotomic subgroup (inverse = conjugate): the squarings inline,
-// the ~27 multiplications by f out of line
+// |u| in non-adjacent form: digit i is +1 (pos bit i), -1 (neg bit i) or 0;
+// BN254's u has 28 set bits and 24 NAF digits, FP256BN's 22 and 18
+struct Naf {
+  uint64_t pos, neg;
+  int top;
+};
+__host__ __device__ constexpr Naf naf_of(uint64_t k) {
+  Naf r{0, 0, -1};
+  for (int i = 0; k != 0; i++, k >>= 1) {
+    if (k & 1) {
+      if ((k & 3) == 1) {
+        r.pos |= 1ull << i;
+        k -= 1;
+      } else {
+        r.neg |= 1ull << i;
+        k += 1;
+      }
+    }
+    r.top = i;
+  }
+  return r;
+}
+
+// f^u in the cyclotomic subgroup (inverse = conjugate): signed digits of |u|
+// (f^-1 = conj f), the squarings inline, the multiplications out of line
 template <class B>
 FTS_DEV F12<B> expt_i(const F12<B>& f) {
   using K = typename B::K;
-  constexpr int TOP = 63 - __builtin_clzll(K::U);
+  constexpr Naf N = naf_of(K::U);
+  static_assert(N.top >= 1 && ((N.pos >> N.top) & 1ull), "leading NAF digit +1");
+  const F12<B> fc = conj(f);
   F12<B> r = f;
 #pragma unroll 1
-  for (int i = TOP - 1; i >= 0; i--) {
+  for (int i = N.top - 1; i >= 0; i--) {
     r = cyc_sqr_i(r);
-    if ((K::U >> i) & 1ull) {  // the callee gets a copy: r itself never escapes to memory
+    if (((N.pos | N.neg) >> i) & 1ull) {  // the callee gets a copy: r itself never escapes to memory
       const F12<B> t = r;
-      r = mul(t, f);
+      r = mul(t, ((N.pos >> i) & 1ull) ? f : fc);
     }
   }
   return K::U_NEG ? conj(r) : r;
 }
-template <class B>
-PAIR_FN F12<B> expt(const F12<B>& f) {
-  return expt_i(f);
-}
 
-// final exponentiation; the _i form is inlined into the kernel, so its three
+// final exponentiation, inlined into the kernels (no out-of-line form: the
+// round-4 build of an out-of-line wrapper around this body returned wrong GT
+// values from k_idv_pairing_debug while the same code inlined into
+// k_idv_pairing was right -- kept in kernels, like glv_mul); its three
 // exponentiations by u (one rolled loop, one copy of the squaring) run with the
 // kernel's register budget: a callee is held to 128 VGPRs and spilled its
 // Fp12 accumulator on every squaring
@@ -505,10 +574,6 @@ FTS_DEV F12<B> final_exp_i(const F12<B>& f0) {
   t1 = mul(t1, y0);
   t0 = cyc_sqr(t0);
   return mul(t0, t1);
-}
-template <class B>
-PAIR_FN F12<B> final_exp(const F12<B>& f0) {
-  return final_exp_i(f0);
 }
 
 }  // namespace pair

@@ -743,7 +743,7 @@ __global__ void __launch_bounds__(64) k_idv_pairing_debug(const uint32_t* __rest
   const uint32_t* const L[1] = {lines + (size_t)which * pair::n_lines<K>() * pair::LINE_WORDS};
   const F xP[1] = {B::ld(p16)}, yP[1] = {B::ld(p16 + 8)};
   pair::F12<B> f = pair::miller<B, 1>(L, xP, yP);
-  if (final_exp) f = pair::final_exp(f);
+  if (final_exp) f = pair::final_exp_i(f);
   const pair::F2<B> z[6] = {f.c0.c0, f.c1.c0, f.c0.c1, f.c1.c1, f.c0.c2, f.c1.c2};
   for (int k = 0; k < 6; k++) {
     pair::store_f2(out + k * 16, z[k]);

@@ -1,14 +1,15 @@
 #!/bin/bash
 # The measurement recipe behind profiles/ (run on the gpurun box from the repo root):
-#   bash tools/gpu_session.sh STEP...     STEP in: smoke tests rp prof pmc tamper identity extra
+#   bash tools/gpu_session.sh STEP...     STEP in: smoke tests rp prof pmc tamper identity identity_pmc extra
 # smoke     __graft_entry__.smoke()
 # tests     pytest -m gpu (full suite)
 # rp        C2 headline, driver shape (20 steps) and steady state (512 steps)
 # prof      rocprofv3 --kernel-trace --stats of the headline; isolated roofline pass summary
 # pmc       FETCH_SIZE / WRITE_SIZE / SQ_* passes (one counter group per run) + FETCH_SIZE
 #           calibration -> traffic_$TAG.json (tools/pmc_traffic.py)
-# tamper    C2 with 1 % tampered proofs
+# tamper    C2 with 1 % tampered proofs; one bad proof per 81,920-proof pass vs clean (160 steps)
 # identity  idemix identity validity, both curves, + rocprofv3 stats
+# identity_pmc  FETCH_SIZE / WRITE_SIZE per identity kernel (BN254) -> identity_traffic_$TAG.json
 # extra     C3-C5 and SURVEY 8f workloads
 # Every GPU step has its own time limit; the first failure ends the script.
 # Output: gpurun_out/$TAG (TAG default r03).
@@ -44,7 +45,15 @@ for s in "$@"; do case $s in
        step pmc_calib 120 rocprofv3 --pmc FETCH_SIZE -T -f csv -d $OUT/pmc_calib -o run -- fabric-token-sdk_amd/lib/fetch_calib
        json pmc_calib
        python3 tools/pmc_traffic.py $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_calib $OUT/pmc_calib.json $OUT/pmc_fetch.json 2 $OUT/traffic_$TAG.json $OUT/pmc_valu ;;
-  tamper) step bench_tamper 300 python3 -u bench.py --steps 20 --warmup 5 --tamper 0.01; json bench_tamper ;;
+  tamper) step bench_tamper 300 python3 -u bench.py --steps 20 --warmup 5 --tamper 0.01; json bench_tamper
+          step bench_clean160 300 python3 -u bench.py --steps 160 --warmup 20 --host-steps 0 --cpu-sample 0; json bench_clean160
+          step bench_onebad160 300 python3 -u bench.py --steps 160 --warmup 20 --host-steps 0 --cpu-sample 0 --tamper 1e-9 --tamper-every 20
+          json bench_onebad160 ;;
+  identity_pmc) IB="python3 bench.py --workload identity --idemix-curve bn254 --steps 2 --warmup 1 --cpu-sample 0 --action-inflight 1"
+          rm -rf $OUT/pmc_id_fetch $OUT/pmc_id_write
+          step pmc_id_fetch 300 rocprofv3 --pmc FETCH_SIZE -T -f csv -d $OUT/pmc_id_fetch -o run -- $IB
+          step pmc_id_write 300 rocprofv3 --pmc WRITE_SIZE -T -f csv -d $OUT/pmc_id_write -o run -- $IB
+          python3 tools/pmc_kernels.py $OUT/pmc_id_fetch $OUT/pmc_id_write $OUT/identity_traffic_$TAG.json k_idv ;;
   identity) for c in bn254 fp256bn; do
               step bench_identity_$c 300 python3 -u bench.py --workload identity --idemix-curve $c --steps 10 --warmup 2; json bench_identity_$c
             done
