@@ -247,12 +247,16 @@ FTS_DEV bool is_one(const F12<B>& x) {
 // reaches these functions has __launch_bounds__(64), so a callee may use the
 // full register file instead of the 128 VGPRs of a 1,024-thread block)
 template <class B>
-PAIR_FN F12<B> mul(const F12<B>& x, const F12<B>& y) {
+FTS_DEV F12<B> mul12_i(const F12<B>& x, const F12<B>& y) {
   const F6<B> t0 = mul6_i(x.c0, y.c0), t1 = mul6_i(x.c1, y.c1);
   F12<B> r;
   r.c1 = sub(sub(mul6_i(add(x.c0, x.c1), add(y.c0, y.c1)), t0), t1);
   r.c0 = add(t0, mul_v(t1));
   return r;
+}
+template <class B>
+PAIR_FN F12<B> mul(const F12<B>& x, const F12<B>& y) {
+  return mul12_i(x, y);
 }
 // complex squaring: 2 Fp6 products
 template <class B>
@@ -522,7 +526,9 @@ __host__ __device__ constexpr Naf naf_of(uint64_t k) {
 }
 
 // f^u in the cyclotomic subgroup (inverse = conjugate): signed digits of |u|
-// (f^-1 = conj f), the squarings inline, the multiplications out of line
+// (f^-1 = conj f), squarings and multiplications inline (round 4: with the
+// ~24 multiplications out of line, their stack arguments were ~2/3 of the
+// pairing kernel's 8 GB of memory traffic per 65,536 identities)
 template <class B>
 FTS_DEV F12<B> expt_i(const F12<B>& f) {
   using K = typename B::K;
@@ -533,10 +539,8 @@ FTS_DEV F12<B> expt_i(const F12<B>& f) {
 #pragma unroll 1
   for (int i = N.top - 1; i >= 0; i--) {
     r = cyc_sqr_i(r);
-    if (((N.pos | N.neg) >> i) & 1ull) {  // the callee gets a copy: r itself never escapes to memory
-      const F12<B> t = r;
-      r = mul(t, ((N.pos >> i) & 1ull) ? f : fc);
-    }
+    if (((N.pos | N.neg) >> i) & 1ull)  // inline: an out-of-line call passes three Fp12 values through the stack
+      r = mul12_i(r, ((N.pos >> i) & 1ull) ? f : fc);
   }
   return K::U_NEG ? conj(r) : r;
 }

@@ -32,7 +32,9 @@
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <string>
 #include <type_traits>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/fts_gpu.h"
@@ -418,9 +420,12 @@ FTS_DEV bool g2_in_subgroup_bn(const pair::F2<pair::BnField>& qx, const pair::F2
 
 // U distinct epoch keys (128 raw bytes each, BN254): ok[u] <- the key decodes (on the
 // twist, canonical) and lies in the subgroup (the identity does)
-__global__ void __launch_bounds__(64) k_idv_g2_check(int U, const uint8_t* __restrict__ keys, int32_t* __restrict__ ok) {
-  const int u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= U) return;
+// lane j checks distinct key idx[j] (the keys the context has not checked before)
+__global__ void __launch_bounds__(64) k_idv_g2_check(int M, const int32_t* __restrict__ idx,
+                                                     const uint8_t* __restrict__ keys, int32_t* __restrict__ ok) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= M) return;
+  const int u = idx[j];
   pair::F2<pair::BnField> x, y;
   const uint8_t* kr = keys + (size_t)u * 128;
   bool good = decode_g2<BnCurve>(kr, x, y);
@@ -1077,6 +1082,10 @@ struct fts_idemix_idv {
   idv::Slot slot[idv::NSLOT];
   bool busy[idv::NSLOT] = {false, false, false};
   float last_ms[2] = {0.f, 0.f};
+  // BN254 epoch keys already subgroup-checked by this context (128 raw bytes ->
+  // verdict): an honest stream carries one key per epoch, and k_idv_g2_check is
+  // one 254-step G2 chain on one lane (7.7 ms, on the call's critical path)
+  std::unordered_map<std::string, int32_t> g2_seen;
 };
 
 namespace idv {
@@ -1243,12 +1252,14 @@ int fts_idemix_identity_verify_batch(fts_idemix_idv* K, size_t n, const uint8_t*
   const size_t rec_b = n * REC_STRIDE * 4, pts_b = n * NPT * 64, epk_b = n * 128, st_b = n * 4;
   const size_t o_pts = rec_b, o_epk = o_pts + pts_b, o_st = o_epk + epk_b, o_eidx = o_st + st_b,
                o_uk = o_eidx + n * 4;
-  const size_t h_need = (o_uk + epk_b + 255) & ~size_t(255);
+  // host only: the distinct keys' verdicts (cached or read back) and the indices to check
+  const size_t o_gk = (o_uk + epk_b + 255) & ~size_t(255), o_miss = o_gk + n * 4;
+  const size_t h_need = (o_miss + n * 4 + 255) & ~size_t(255);
   const size_t o_zk = h_need, o_pin = (o_zk + n * 4 + 255) & ~size_t(255), o_scr = o_pin + n * 32 * 4;
   const size_t scr_w = idv_scratch_words(n);
   const size_t o_msg = (o_scr + scr_w * 4 + 255) & ~size_t(255);
   const size_t o_g2ok = (o_msg + (size_t)MSG_MAX * n + 255) & ~size_t(255);
-  const size_t d_need = o_g2ok + n * 4;
+  const size_t d_need = o_g2ok + 2 * n * 4;  // U verdicts, then the M key indices to check
   if (D.h_cap < h_need) {
     if (D.h_buf) (void)hipHostFree(D.h_buf);
     D.h_buf = nullptr, D.h_cap = 0;
@@ -1310,6 +1321,22 @@ int fts_idemix_identity_verify_batch(fts_idemix_idv* K, size_t n, const uint8_t*
       }
     }
   }
+  // cached key verdicts; the misses are checked on the device and cached after the call
+  int32_t* gk = reinterpret_cast<int32_t*>(h + o_gk);
+  int32_t* miss = reinterpret_cast<int32_t*>(h + o_miss);
+  size_t M = 0;
+  if (bn) {
+    std::lock_guard<std::mutex> l(K->mu);
+    for (size_t j = 0; j < U; j++) {
+      const auto it = K->g2_seen.find(std::string(reinterpret_cast<const char*>(h + o_uk + 128 * j), 128));
+      if (it != K->g2_seen.end()) {
+        gk[j] = it->second;
+      } else {
+        gk[j] = 0;
+        miss[M++] = (int32_t)j;
+      }
+    }
+  }
   uint8_t* d = D.d_buf;
   ICHK(hipMemcpyAsync(d, h, o_uk + U * 128, hipMemcpyHostToDevice, D.stream));
   ICHK(hipEventRecord(D.ev[0], D.stream));
@@ -1323,7 +1350,11 @@ int fts_idemix_identity_verify_batch(fts_idemix_idv* K, size_t n, const uint8_t*
   const size_t nl = (size_t)nlines(bn) * pair::LINE_WORDS;
   int32_t* g2ok = reinterpret_cast<int32_t*>(d + o_g2ok);
   if (bn) {
-    k_idv_g2_check<<<(unsigned)((U + 63) / 64), 64, 0, D.stream>>>((int)U, d + o_uk, g2ok);
+    ICHK(hipMemcpyAsync(g2ok, gk, U * 4, hipMemcpyHostToDevice, D.stream));
+    if (M) {
+      ICHK(hipMemcpyAsync(g2ok + U, miss, M * 4, hipMemcpyHostToDevice, D.stream));
+      k_idv_g2_check<<<(unsigned)((M + 63) / 64), 64, 0, D.stream>>>((int)M, g2ok + U, d + o_uk, g2ok);
+    }
     k_idv_decode<BnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, d + o_pts, d + o_epk, scr, pin, zk, st,
                                                        reinterpret_cast<const int32_t*>(d + o_eidx), g2ok);
     k_idv_var<BnCurve><<<gvar, 256, 0, D.stream>>>((int)n, rec, scr, st);
@@ -1342,8 +1373,17 @@ int fts_idemix_identity_verify_batch(fts_idemix_idv* K, size_t n, const uint8_t*
   ICHK(hipGetLastError());
   ICHK(hipEventRecord(D.ev[2], D.stream));
   ICHK(hipMemcpyAsync(h + o_st, d + o_st, st_b, hipMemcpyDeviceToHost, D.stream));
+  if (M) ICHK(hipMemcpyAsync(gk, g2ok, U * 4, hipMemcpyDeviceToHost, D.stream));
   ICHK(hipStreamSynchronize(D.stream));
   memcpy(status, h + o_st, st_b);
+  if (M) {
+    std::lock_guard<std::mutex> l(K->mu);
+    if (K->g2_seen.size() + M > 4096) K->g2_seen.clear();  // bounded: a new epoch's keys refill it
+    for (size_t q = 0; q < M; q++) {
+      const size_t j = (size_t)miss[q];
+      K->g2_seen.emplace(std::string(reinterpret_cast<const char*>(h + o_uk + 128 * j), 128), gk[j]);
+    }
+  }
   ICHK(hipEventElapsedTime(&D.ms[0], D.ev[0], D.ev[1]));
   ICHK(hipEventElapsedTime(&D.ms[1], D.ev[1], D.ev[2]));
   return FTS_API_OK;

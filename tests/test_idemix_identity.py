@@ -202,8 +202,9 @@ def test_bn254_g2_subgroup_checks(verifiers):
     """gnark-crypto's G2Affine.SetBytes (mathlib NewG2FromBytes, BN254) rejects twist
     points outside the order-r subgroup: an epoch key on the twist but off the
     subgroup makes the identity malformed (ADVICE r03), a subgroup key does not;
-    distinct keys in one batch are each checked once (host dedupe), every verdict at
-    its position; an issuer key whose W is off the subgroup is refused"""
+    distinct keys in one batch are each checked once (host dedupe) and once per
+    context (verdict cache), every verdict at its position; an issuer key whose W is
+    off the subgroup is refused"""
     from fts_gpu import idemix as I
     from fts_gpu import _lib as L
     from oracle import idemix as OI, idemix_identity as ID, pairing as PR
@@ -217,10 +218,17 @@ def test_bn254_g2_subgroup_checks(verifiers):
     ids = [(_with_epoch_key(honest, k), w) for k, w in keys]
     st = verifiers["bn254"].verify_batch([x for x, _ in ids])
     assert [int(s) for s in st] == [w for _, w in ids]
+    # the context caches each distinct key's verdict: a second batch mixes cached
+    # keys with ones it has not seen (a third off-subgroup point, a new subgroup
+    # point), every verdict at its position, and a third call hits only the cache
+    more = [(ID.ecp2(C, ID.twist_point(C, 99)), I.FTS_E_ID_MALFORMED), (ID.ecp2(C, C.g2_mul(C.g2_gen, 77)), 0)]
+    assert not ID.g2_in_subgroup(C, ID.twist_point(C, 99))
+    ids += [(_with_epoch_key(honest, k), w) for k, w in more]
     rng = random.Random(11)
-    pick = [rng.randrange(len(ids)) for _ in range(2000)]
-    st = verifiers["bn254"].verify_batch([ids[k][0] for k in pick])
-    assert [int(s) for s in st] == [ids[k][1] for k in pick]
+    for _ in range(2):
+        pick = [rng.randrange(len(ids)) for _ in range(2000)]
+        st = verifiers["bn254"].verify_batch([ids[k][0] for k in pick])
+        assert [int(s) for s in st] == [ids[k][1] for k in pick]
     # issuer key with W off the subgroup (field 5 of IssuerPublicKey)
     ipk = _ipk("bn254_charlie")
     fields = OI.pb_fields(ipk)
