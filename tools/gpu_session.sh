@@ -55,7 +55,7 @@ for s in "$@"; do case $s in
           step pmc_id_write 300 rocprofv3 --pmc WRITE_SIZE -T -f csv -d $OUT/pmc_id_write -o run -- $IB
           python3 tools/pmc_kernels.py $OUT/pmc_id_fetch $OUT/pmc_id_write $OUT/identity_traffic_$TAG.json k_idv ;;
   identity) for c in bn254 fp256bn; do
-              step bench_identity_$c 300 python3 -u bench.py --workload identity --idemix-curve $c --steps 10 --warmup 2; json bench_identity_$c
+              step bench_identity_$c 300 python3 -u bench.py --workload identity --idemix-curve $c --steps 40 --warmup 4; json bench_identity_$c
             done
             rm -rf $OUT/prof_identity
             step prof_identity 300 rocprofv3 --kernel-trace --stats -T -f csv -d $OUT/prof_identity -o prof -- python3 bench.py --workload identity --steps 4 --warmup 1 --cpu-sample 0 ;;
