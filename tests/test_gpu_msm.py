@@ -126,3 +126,41 @@ def test_msm_distinct_device_points_closed_form(gpu_pp, oracle_pp, log):
     if log == 8:
         pts = [bn.g1_mul(ped1, k % bn.R) for k in ks]
         assert pp.msm(_pts(pts), _scs(ss)) == want
+
+
+def test_msm_block_local_sort_adversarial_2p18(gpu_pp):
+    """The block-local counting sort (msm.hip k_msm_lhist / k_msm_lscatter, used by
+    standalone MSMs from 2^18 points) on adversarial inputs: one scalar repeated by
+    an eighth of the points (one bucket per window holds 32k entries), zero
+    scalars, r - 1 and scalars >= r (used mod r), identity points, and -P right
+    after +P with the same scalar (the pair cancels); closed form
+    sum s_i c_i G with P_i = c_i G"""
+    pp = gpu_pp(64)
+    n, m = 1 << 18, 1 << 16
+    rng = random.Random(0x15A0)
+    base, acc = [], None
+    for _ in range(m):
+        acc = bn.g1_add(acc, bn.GEN)
+        base.append(acc)
+    k_rep = rng.randrange(bn.R)
+    pts, scs, total = [], [], 0
+    for i in range(n):
+        c = i % m + 1
+        kind = i % 8
+        if kind == 4 and i % 64 == 4:
+            pts.append(None)  # identity point (64 zero bytes): contributes nothing
+            scs.append(rng.randrange(bn.R))
+            continue
+        if kind == 5 and pts[-1] is not None:  # -P_{i-1} with P_{i-1}'s scalar
+            c = -((i - 1) % m + 1)
+            pts.append(bn.g1_neg(base[(i - 1) % m]))
+            scs.append(scs[-1])
+        else:
+            s = {0: k_rep, 1: 0, 2: bn.R - 1, 3: rng.randrange(bn.R, 1 << 256)}.get(kind, rng.randrange(bn.R))
+            pts.append(base[i % m])
+            scs.append(s)
+        total += (scs[-1] % bn.R) * c
+    want = bn.g1_bytes(bn.g1_mul(bn.GEN, total % bn.R))
+    st = pp.stage_msm(_pts(pts), _scs(scs))
+    assert st.run() == want
+    st.close()
