@@ -466,24 +466,25 @@ __global__ void __launch_bounds__(64) k_idv_lines(const uint8_t* __restrict__ wr
 
 // Lane scratch ([word][lane], n lanes each): S = t1..t5 accumulators (5 x 24),
 // DP = decoded points (NPT x 16), IDM = identity mask of the decoded points (1),
-// VR = the NVAR variable-base products (NVAR x 24), TV = their GLV lane tables
+// VR = the NVAR variable-base then NFIX fixed-base products (NSC x 24), TV = the
+// variable-base products' GLV lane tables
 // (NVAR x AT_WORDS; TV[0] doubles as the normalisation's prefix products)
 FTS_DEV size_t sc_s(size_t) { return 0; }
 FTS_DEV size_t sc_dp(size_t n) { return (size_t)5 * 24 * n; }
 FTS_DEV size_t sc_idm(size_t n) { return sc_dp(n) + (size_t)NPT * 16 * n; }
 FTS_DEV size_t sc_vr(size_t n) { return sc_idm(n) + n; }
-FTS_DEV size_t sc_tv(size_t n) { return sc_vr(n) + (size_t)NVAR * 24 * n; }
-inline size_t idv_scratch_words(size_t n) { return (5 * 24 + NPT * 16 + 1 + NVAR * (24 + AT_WORDS)) * n; }
+FTS_DEV size_t sc_tv(size_t n) { return sc_vr(n) + (size_t)NSC * 24 * n; }
+inline size_t idv_scratch_words(size_t n) { return (5 * 24 + NPT * 16 + 1 + NSC * 24 + NVAR * AT_WORDS) * n; }
 
 // Three kernels per batch (round 4; one lane per identity for everything left
 // 1,024 waves at one per SIMD, 30 % of the MAD peak):
 //   k_idv_decode  identity per lane: status (pre-set by the host for identity-
 //                 level errors), point decoding in the reference's order of
 //                 checks, pin[i] <- (A', -ABar) for the pairing kernel
-//   k_idv_var     lane per (variable-base product, identity): the six GLV
-//                 products of the t-values, 6x the lanes
-//   k_idv_tvals   identity per lane: sum the products into t1..t5, the fourteen
-//                 fixed-base products, normalisation, transcript, challenge;
+//   k_idv_var     lane per (product, identity): the six GLV products and the
+//                 fourteen fixed-base products of the t-values, 20x the lanes
+//   k_idv_tvals   identity per lane: sum the products into t1..t5,
+//                 normalisation, transcript, challenge;
 //                 zk[i] <- 1 if c == c''
 template <class CV>
 __global__ void __launch_bounds__(256) k_idv_decode(int n, const uint32_t* __restrict__ rec,
@@ -560,14 +561,24 @@ __global__ void __launch_bounds__(256) k_idv_decode(int n, const uint32_t* __res
 // lane g = v * n + i: identities fastest, so a wave runs one product kind
 template <class CV>
 __global__ void __launch_bounds__(256) k_idv_var(int n, const uint32_t* __restrict__ rec,
+                                                 const uint32_t* __restrict__ tables,
                                                  uint32_t* __restrict__ scratch, const int32_t* __restrict__ status) {
   using B = typename CV::B;
   using PJ = typename CV::PJ;
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= (size_t)NVAR * n) return;
+  if (g >= (size_t)NSC * n) return;
   const int v = (int)(g / n), i = (int)(g % n);
   if (status[i] != FTS_OK) return;
   const uint32_t* R = rec + (size_t)i * REC_STRIDE;
+  const LaneWords VR{scratch + sc_vr(n) + (size_t)v * 24 * n, (size_t)n, (size_t)i};
+  if (v >= NVAR) {  // fixed-base product (issuer tables)
+    PJ acc = CV::inf();
+    CV::fixed_mul_acc(acc, tables, FIX_B[v - NVAR], R + R_SC + v * 8);
+    put_f<CV>(VR, 0, acc.x);
+    put_f<CV>(VR, 8, acc.y);
+    put_f<CV>(VR, 16, acc.z);
+    return;
+  }
   const LaneWords DP{scratch + sc_dp(n), (size_t)n, (size_t)i};
   const uint32_t idm = scratch[sc_idm(n) + i];
   const int pq_ = VAR_PT[v] < 0 ? P_ABAR : VAR_PT[v];
@@ -576,7 +587,6 @@ __global__ void __launch_bounds__(256) k_idv_var(int n, const uint32_t* __restri
     CV::madd_to(base, get_f<CV>(DP, P_BP * 16), B::neg(get_f<CV>(DP, P_BP * 16 + 8)));
   const LaneWords T{scratch + sc_tv(n) + (size_t)v * AT_WORDS * n, (size_t)n, (size_t)i};
   const PJ r = glv_mul<CV>(base, R + R_SC + v * 8, T);
-  const LaneWords VR{scratch + sc_vr(n) + (size_t)v * 24 * n, (size_t)n, (size_t)i};
   put_f<CV>(VR, 0, r.x);
   put_f<CV>(VR, 8, r.y);
   put_f<CV>(VR, 16, r.z);
@@ -607,24 +617,14 @@ __global__ void __launch_bounds__(256) k_idv_tvals(int n, const uint32_t* __rest
     put_f<CV>(S, t * 24 + 16, z.z);
   }
 #pragma unroll 1
-  for (int v = 0; v < NVAR; v++) {
+  for (int v = 0; v < NSC; v++) {
     const LaneWords VR{scratch + sc_vr(n) + (size_t)v * 24 * n, (size_t)n, (size_t)i};
     PJ r;
     r.x = get_f<CV>(VR, 0), r.y = get_f<CV>(VR, 8), r.z = get_f<CV>(VR, 16);
-    const int t = VAR_T[v];
+    const int t = v < NVAR ? VAR_T[v] : FIX_T[v - NVAR];
     PJ acc;
     acc.x = get_f<CV>(S, t * 24), acc.y = get_f<CV>(S, t * 24 + 8), acc.z = get_f<CV>(S, t * 24 + 16);
     CV::add_to(acc, r);
-    put_f<CV>(S, t * 24, acc.x);
-    put_f<CV>(S, t * 24 + 8, acc.y);
-    put_f<CV>(S, t * 24 + 16, acc.z);
-  }
-#pragma unroll 1
-  for (int f = 0; f < NFIX; f++) {
-    const int t = FIX_T[f];
-    PJ acc;
-    acc.x = get_f<CV>(S, t * 24), acc.y = get_f<CV>(S, t * 24 + 8), acc.z = get_f<CV>(S, t * 24 + 16);
-    CV::fixed_mul_acc(acc, tables, FIX_B[f], R + R_SC + (NVAR + f) * 8);
     put_f<CV>(S, t * 24, acc.x);
     put_f<CV>(S, t * 24 + 8, acc.y);
     put_f<CV>(S, t * 24 + 16, acc.z);
@@ -1341,7 +1341,7 @@ int fts_idemix_identity_verify_batch(fts_idemix_idv* K, size_t n, const uint8_t*
   ICHK(hipMemcpyAsync(d, h, o_uk + U * 128, hipMemcpyHostToDevice, D.stream));
   ICHK(hipEventRecord(D.ev[0], D.stream));
   const unsigned g256 = (unsigned)((n + 255) / 256), g64 = (unsigned)((n + 63) / 64),
-                 gvar = (unsigned)((NVAR * n + 255) / 256);
+                 gvar = (unsigned)((NSC * n + 255) / 256);
   const uint32_t* rec = reinterpret_cast<const uint32_t*>(d);
   uint32_t* scr = reinterpret_cast<uint32_t*>(d + o_scr);
   uint32_t* pin = reinterpret_cast<uint32_t*>(d + o_pin);
@@ -1357,14 +1357,14 @@ int fts_idemix_identity_verify_batch(fts_idemix_idv* K, size_t n, const uint8_t*
     }
     k_idv_decode<BnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, d + o_pts, d + o_epk, scr, pin, zk, st,
                                                        reinterpret_cast<const int32_t*>(d + o_eidx), g2ok);
-    k_idv_var<BnCurve><<<gvar, 256, 0, D.stream>>>((int)n, rec, scr, st);
+    k_idv_var<BnCurve><<<gvar, 256, 0, D.stream>>>((int)n, rec, K->d_tables, scr, st);
     k_idv_tvals<BnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, K->d_tables, K->d_hash, scr, d + o_msg, zk, st);
     ICHK(hipEventRecord(D.ev[1], D.stream));
     k_idv_pairing<BnCurve><<<g64, 64, 0, D.stream>>>((int)n, pin, K->d_lines, zk, st);
   } else {
     k_idv_decode<FbnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, d + o_pts, d + o_epk, scr, pin, zk, st, nullptr,
                                                         nullptr);
-    k_idv_var<FbnCurve><<<gvar, 256, 0, D.stream>>>((int)n, rec, scr, st);
+    k_idv_var<FbnCurve><<<gvar, 256, 0, D.stream>>>((int)n, rec, K->d_tables, scr, st);
     k_idv_tvals<FbnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, K->d_tables, K->d_hash, scr, d + o_msg, zk, st);
     ICHK(hipEventRecord(D.ev[1], D.stream));
     k_idv_pairing<FbnCurve><<<g64, 64, 0, D.stream>>>((int)n, pin, K->d_lines, zk, st);

@@ -1,9 +1,14 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r04y; mkdir -p $O
+O=gpurun_out/r04z; mkdir -p $O
 T="timeout -k 10"
-for i in 0 1 0 1 0 1; do
-  echo "shape=$i" >> $O/s20.txt
-  $T 200 python3 -u bench.py --steps 20 --warmup 5 --shape-warmup $i --host-steps 0 --cpu-sample 0 >> $O/s20.txt 2>> $O/s20.err || exit 1
+A=fabric-token-sdk_amd/lib/ab
+L=fabric-token-sdk_amd/lib/libfts_gpu.so
+$T 300 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_idemix_identity.py > $O/pytest.log 2>&1 || exit 1
+for v in $A/base.so $L $A/base.so $L; do
+  for c in bn254 fp256bn; do
+    echo "$(basename $v) $c" >> $O/id.txt
+    FTS_LIB=$v $T 200 python3 -u bench.py --workload identity --idemix-curve $c --steps 40 --warmup 4 --cpu-sample 0 >> $O/id.txt 2>> $O/id.err || exit 1
+  done
 done
 echo rc=$?
