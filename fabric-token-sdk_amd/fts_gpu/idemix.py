@@ -167,18 +167,30 @@ class IdentityVerifier:
         except Exception:
             pass
 
-    def verify_batch(self, identities):
-        """serialized identities -> int32 status array (FTS_OK or FTS_E_ID_*)"""
-        n = len(identities)
+    def prepare(self, identities):
+        """the C-ABI's pointer / length arrays for a batch of serialized identities,
+        built once: verify_prepared then calls the library with no per-call Python
+        marshaling (a Go caller hands its slices' pointers over the same way)"""
+        keep = [bytes(x) for x in identities]
+        n = len(keep)
+        ptrs = (C.c_void_p * max(1, n))(*[C.cast(C.c_char_p(b), C.c_void_p).value for b in keep])
+        lens = (C.c_size_t * max(1, n))(*[len(b) for b in keep])
+        return keep, ptrs, lens
+
+    def verify_prepared(self, prep):
+        """prepare()d identities -> int32 status array (FTS_OK or FTS_E_ID_*)"""
+        keep, ptrs, lens = prep
+        n = len(keep)
         st = np.zeros(n, dtype=np.int32)
         if n == 0:
             return st
-        keep = [bytes(x) for x in identities]
-        ptrs = (C.c_void_p * n)(*[C.cast(C.c_char_p(b), C.c_void_p).value for b in keep])
-        lens = (C.c_size_t * n)(*[len(b) for b in keep])
         L.check("fts_idemix_identity_verify_batch",
                 L.lib.fts_idemix_identity_verify_batch(self.h, n, ptrs, lens, st.ctypes.data_as(C.POINTER(C.c_int32))))
         return st
+
+    def verify_batch(self, identities):
+        """serialized identities -> int32 status array (FTS_OK or FTS_E_ID_*)"""
+        return self.verify_prepared(self.prepare(identities))
 
     def Deserialize(self, identity):
         """raises IdentityError with the reference's message, as Deserialize(raw, true) errors"""
