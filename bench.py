@@ -71,6 +71,35 @@ def _cpu_env():
     return {"cpu_model": model, "logical_cpus": os.cpu_count(), "cgroup_cpu_quota": quota}
 
 
+def _lib_record():
+    """which libfts_gpu.so this run loaded: its sha256, mtime and the record
+    __graft_entry__.build() left (compiled by that call, or found up to date)"""
+    import hashlib
+    so = os.path.join(ROOT, "fabric-token-sdk_amd", "lib", "libfts_gpu.so")
+    rec = {}
+    try:
+        with open(os.path.join(ROOT, "fabric-token-sdk_amd", "lib", "build_info.json")) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        rec = {"build_info": "absent (library not built by __graft_entry__.build())"}
+    try:
+        with open(so, "rb") as f:
+            dg = hashlib.sha256(f.read()).hexdigest()
+        rec["loaded_so_sha256"] = dg[:16]
+        rec["matches_build_record"] = dg == rec.get("so_sha256")
+        rec["so_mtime"] = time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime(os.path.getmtime(so)))
+    except OSError:
+        pass
+    rec.pop("so_sha256", None)
+    return rec
+
+
+# the reference-order C restatement beside the reference's own Go verifier
+PORT_NOTE = ("portable 4x64-bit Montgomery C (no GLV, no assembly, affine G1.Mul as bulletproof.go/ipa.go call "
+             "them); the reference's gnark-crypto uses assembly Montgomery products and GLV, so a Go run of the "
+             "reference would likely be 2-4x faster per core than this column (unmeasured: no Go toolchain here)")
+
+
 def _timed_sample(fn, total, chunk, seconds):
     """run fn(lo, hi) over chunks of [0, total) until `seconds` of wall time; -> (items, s)"""
     done, cs = 0, 0.0
@@ -456,7 +485,8 @@ def main():
                "value_1core": round(d1 / s1, 3),
                "sample": "%d (%d threads) and %d (1 thread) of the same rp%d proofs, reference-order C restatement "
                          "(oracle/c/ref_verify.c, %d affine G1.Mul per proof, no GLV / assembly), %.1f + %.1f s wall"
-                         % (dn, thr, d1, n, 7 * n + 2 * k + 9, sn, s1)}
+                         % (dn, thr, d1, n, 7 * n + 2 * k + 9, sn, s1),
+               "vs_reference_go": PORT_NOTE}
         cpu["optimized_batch"] = _cpu_batch_baseline(opp, coms0, proofs0, wants[0], thr, args)
         cpu.update(_cpu_env())
 
@@ -501,6 +531,7 @@ def main():
             "tamper_every": args.tamper_every,
             "fallback": _fallback_share(kt, R, pass_ms),
             "prove_s": round(prove_s, 2),
+            "library": _lib_record(),
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
@@ -665,20 +696,43 @@ def bench_msm(args):
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         from oracle import cref
         thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        done, cs = 0, 0.0
-        while cs < args.cpu_seconds and done < n:
-            c = min(1024, n - done)
-            if pts is None:  # the CPU port reads points: the first sample's k'_i ped1 on the host
-                pts = b"".join(x.to_bytes(32, "big") + y.to_bytes(32, "big")
-                               for x, y in (_mul_g(k, ped1) for k in kp[:min(n, 1024)]))
+        # "the build's C++ Pippenger" -- oracle/c/cpu_batch.c's GLV
+        # Pippenger (signed windows, threads over (window, part)) over the first
+        # 2^min(L, 20) of the SAME points (downloaded from the device: fts_msm_points),
+        # its result checked against the sample's closed form
+        ns = min(n, 1 << 20)
+        if pts is None:
+            spts = st.points(0, ns)
+            want_s = _mul_g(sum(k * q for k, q in zip(ks[:ns], kp[:ns])) % R_ORDER, ped1)
+        else:
+            spts = pts[:64 * ns]
+            want_s = _mul_g(sum(k * (i % (1 << 16) + 1) for i, k in enumerate(ks[:ns])) % R_ORDER)
+        want_b = bytes(64) if want_s is None else want_s[0].to_bytes(32, "big") + want_s[1].to_bytes(32, "big")
+        reps, cs = 0, 0.0
+        while reps == 0 or cs < args.cpu_seconds / 2:
             t1 = time.perf_counter()
-            off = done % (len(pts) // 64)  # c divides the sample's point count
-            cref.msm(pts[64 * off:64 * (off + c)], scs[32 * done:32 * (done + c)], threads=thr)
+            got = cref.msm_pippenger(spts, scs[:32 * ns], threads=thr)
             cs += time.perf_counter() - t1
+            reps += 1
+            assert got == want_b, "CPU Pippenger differs from the closed form"
+        # the reference's own call pattern beside it: term-by-term G1.Mul + Add (ipa.go:254-259)
+        done, ct = 0, 0.0
+        while ct < args.cpu_seconds / 4 and done < ns:
+            c = min(1024, ns - done)
+            t1 = time.perf_counter()
+            cref.msm(spts[64 * done:64 * (done + c)], scs[32 * done:32 * (done + c)], threads=thr)
+            ct += time.perf_counter() - t1
             done += c
-        cpu = {"value": round(done / cs, 1), "unit": "terms/s", "cores": thr, "kind": "port",
-               "sample": "%d terms of the same MSM, term-by-term G1.Mul + Add (oracle/c/ref_verify.c oracle_msm, "
-                         "no Pippenger), %d threads, %.1f s wall" % (done, thr, cs)}
+        cpu = {"value": round(reps * ns / cs, 1), "unit": "terms/s", "cores": thr, "kind": "port",
+               "sample": "%d x the MSM over the first %d of the same points (GLV Pippenger, oracle/c/cpu_batch.c "
+                         "cpu_msm_pippenger, portable 4x64 C), %d threads, %.1f s wall; result = the closed form"
+                         % (reps, ns, thr, cs),
+               "vs_reference_go": "gnark-crypto's MultiExp (assembly Montgomery, GLV, windowed Pippenger) would "
+                                  "likely be 2-4x faster per core than this portable C (unmeasured: no Go here)",
+               "term_by_term": {"value": round(done / ct, 1), "unit": "terms/s",
+                                "sample": "%d terms, G1.Mul + Add per term (oracle/c/ref_verify.c oracle_msm, the "
+                                          "reference's ipa.go:254-259 pattern), %d threads, %.1f s" % (done, thr, ct)}}
+        cpu.update(_cpu_env())
     if rank == 0:
         print(json.dumps({
             "metric": "BN254 G1 MSM terms/sec (2^%d points)" % args.msm_log, "value": round(value, 1),

@@ -249,8 +249,15 @@ FTS_DEV uint32_t recode_carries(const uint32_t s[4]) {
   }
   return cm;
 }
+// s[q] for a runtime (wave-uniform) q by selects: indexing the array with a
+// runtime value made the compiler promote it to LDS (k_rp_com_var: 16 KB per
+// 64-lane block, holding every CU's LDS beside the x0 build; round 5)
+FTS_DEV uint32_t word4(const uint32_t s[4], int q) {
+  const uint32_t lo = (q & 1) ? s[1] : s[0], hi = (q & 1) ? s[3] : s[2];
+  return (q & 2) ? hi : lo;
+}
 FTS_DEV int window_digit(const uint32_t s[4], uint32_t cm, int w) {
-  const int raw = (int)((s[w >> 3] >> (4 * (w & 7))) & 0xfu);
+  const int raw = (int)((word4(s, w >> 3) >> (4 * (w & 7))) & 0xfu);
   const int cin = (int)((cm >> w) & 1u);
   const int cout = w < 31 ? (int)((cm >> (w + 1)) & 1u) : 0;
   return raw + cin - 16 * cout;

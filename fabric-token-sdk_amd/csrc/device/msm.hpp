@@ -69,10 +69,10 @@ struct MsmPlan {
   int ptsg;        // points per group
   int NBg, NSg;    // buckets / segments per group
   int ch;          // points per bucket-accumulation chunk (MSM_CH)
-  // block-local counting sort (msm.hip k_msm_lhist / k_msm_lscatter) instead of
-  // k_msm_digits' global atomics: standalone MSMs only.  Beside the batch
-  // check's chain kernels its 1,024-thread, 128 KB-LDS blocks took whole CUs
-  // (81,920-proof bursts 4.10-4.20 -> 3.96-3.99 M rp64/s)
+  // the two-level counting sort (msm.hip k_rs_*, <= 32 KB LDS per 256-thread
+  // block, no device-scope atomics) instead of k_msm_digits' global atomics and
+  // k_msm_scatter's random writes, where the plan allows it (one group, windows
+  // of >= 128 buckets); false forces k_msm_digits (FTS_MSM_SORT=0, A/B)
   bool local_sort;
   const int32_t* sel;  // device: proof indirection (grouped fallback), or nullptr
   int sel_pts;         // points per proof of the indirection
@@ -150,7 +150,7 @@ inline void msm_layout_groups(int N, int G, int ptsg, MsmPlan& p) {
   p.NV = NV;
   p.sel = nullptr;
   p.sel_pts = 1;
-  p.local_sort = false;
+  p.local_sort = true;
 }
 inline void msm_layout(int N, MsmPlan& p) { msm_layout_groups(N, 1, N > 0 ? N : 1, p); }
 // points per bucket-accumulation chunk (and the chunk-slot count that follows)

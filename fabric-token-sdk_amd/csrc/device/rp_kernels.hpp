@@ -55,6 +55,10 @@ constexpr double MADS_PER_MUL = 136.0;
 constexpr double COST_MADD = 11.0;    // madd-2007-bl 7M + 4S
 constexpr double COST_ADD = 16.0;     // add-2007-bl 11M + 5S
 constexpr double COST_DBL = 7.0;      // dbl-2009-l 2M + 5S
+// one inversion is NOT priced in products (f_inv_gcd: ~17 x 2x2-matrix-times-256-bit
+// steps, a few hundred MADs): 0 keeps achieved MAD/s a lower bound
+constexpr double COST_INV = 0.0;
+constexpr double COST_NORM1 = COST_INV + 4.0;  // one point to affine: zi^2, x zi^2, y zi^2 zi (+ the inversion)
 // fixed-base products (fixed_base.hpp): one mixed addition per signed window; a
 // product computed into a fresh accumulator starts from the identity, so its first
 // window is a copy (fb_mul / fb_mul_w: 15 resp. 12 real additions), a product added
@@ -188,6 +192,7 @@ struct RpBatchDev {
   int rlc_fork = 1;    // batch check's stream forks after the fixed-base products (1) or after the challenges (0);
                        //    fts_api.cpp picks 0 on the latency path, 1 on the work path (FTS_RLC_FORK=2)
   hipEvent_t ev_coef = nullptr;  // recorded on the check's stream after k_rlc_prep (column Q on s waits for it)
+  hipEvent_t ev_fx = nullptr;    // rlc_fork 3: recorded on s after the fixed-base launch (the MSM accumulation waits)
   uint32_t* x0_mid = nullptr;    // [B][8] SHA-256 midstate of the x0 prefix (work path; nullptr: one-piece hash)
   int32_t* excl = nullptr;       // [B] optional: 1 = left out of the batch check (set by the pre_rlc hook), NOT_RUN
 };
@@ -219,5 +224,15 @@ struct RlcDev {
   int32_t* flag;     // [1]
   uint32_t* msm_scratch;
   MsmPlan plan;
+  // the combination per caller batch (round 5): G groups of gs proof slots sel[g gs + j]
+  // (-1 = padding); plan is then a G-group MSM over sel, the column sums / products are
+  // per group and the verdict is per group (gflag[g] = 1: group g closed).  G == 1: one
+  // combination over the whole pass (colsum / fixed above)
+  int G = 1, gs = 0;
+  const int32_t* sel = nullptr;
+  uint32_t* gcol = nullptr;   // [G][rlc_ncols][8]
+  uint32_t* gfix = nullptr;   // [G][rlc_ncols][24]: x0-free column products (the MSM's extras), slot Q zero
+  uint32_t* gqfix = nullptr;  // [G][rlc_ncols][24]: column Q's product in slot rlc_ncols - 1
+  int32_t* gflag = nullptr;   // [G]
 };
 }  // namespace fts

@@ -59,6 +59,7 @@ void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalar
 void launch_msm_load(int N, const uint8_t* raw_pts, const uint8_t* raw_sc, uint32_t* pts, uint32_t* sc, uint32_t* bad,
                      hipStream_t s);
 void launch_msm_to_bytes(const uint32_t* jac, uint8_t* out, hipStream_t s);
+void launch_msm_pts_to_bytes(int n, const uint32_t* pts, uint8_t* out, hipStream_t s);
 void launch_msm_gen_points(int N, const uint8_t* raw_k, const uint8_t* raw_s, const uint32_t* table, uint32_t* jac,
                            uint32_t* pts, uint32_t* sc, hipStream_t s);
 void launch_sig_prep(const SigBatchDev& d, hipStream_t s);
@@ -134,8 +135,9 @@ struct DBuf {
 struct Workspace {
   DBuf pts, ch, small, hpj, hpa, hpbe, x0, x0mid, terms, scratch, ypow, svec, zvec, rp_excl;
   // random-linear-combination check + MSM
-  DBuf r_key, r_msc, r_coef, r_colsum, r_fixed, r_flag, r_gcol, r_gfix, r_sel, r_next, r_cnt, m_keys, m_counts, m_offsets, m_cursor, m_sorted, m_buckets,
-      m_segs, m_wins, m_out, m_scratch, m_win, m_choff, m_chbkt, m_partials;
+  DBuf r_key, r_msc, r_coef, r_colsum, r_fixed, r_flag, r_gcol, r_gfix, r_sel, r_next, r_cnt, m_keys,
+      m_counts, m_offsets, m_cursor, m_sorted, m_buckets, m_segs, m_wins, m_out, m_scratch, m_win, m_choff, m_chbkt, m_partials;
+  DBuf r_msel, r_mcol, r_mfix, r_mqfix, r_mflag;  // the per-caller-batch combination of a coalesced pass
   // action (transfer / issue) batches
   DBuf rp_raw, rp_sc, rp_status, rp_ipa;
   DBuf s_act, s_raw, s_owner, s_pts, s_sc, s_status, s_work, s_terms, s_aff, s_affoff, s_msgs, s_jac, s_scratch;
@@ -146,7 +148,7 @@ struct Workspace {
     for (DBuf* b : {&open_rec, &pv, &sp, &pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &x0mid, &terms, &scratch, &ypow, &svec, &zvec, &rp_excl, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
                     &rp_status, &rp_ipa, &s_act, &s_raw, &s_owner, &s_pts, &s_sc, &s_status, &s_work, &s_terms, &s_aff,
                     &s_affoff, &s_msgs, &s_jac, &s_scratch, &r_key, &r_msc, &r_coef, &r_colsum, &r_fixed, &r_flag, &r_gcol, &r_gfix,
-                    &r_sel, &r_next, &r_cnt,
+                    &r_sel, &r_next, &r_cnt, &r_msel, &r_mcol, &r_mfix, &r_mqfix, &r_mflag,
                     &m_keys, &m_counts, &m_offsets, &m_cursor, &m_sorted, &m_buckets, &m_segs, &m_wins, &m_out,
                     &m_scratch, &m_win})
       b->release();
@@ -173,6 +175,9 @@ struct ParsedAction {
   std::vector<uint32_t> rp_sc;
   std::vector<int32_t> rp_status, rp_ipa;
 };
+
+// pinned window-table slots of Lane::Pinned (msm_prepare_plan)
+enum { MSM_SLOT_PASS = 0, MSM_SLOT_RESERVE, MSM_SLOT_GT_BIG, MSM_SLOT_GT_SMALL, MSM_WIN_SLOTS };
 
 struct Lane {
   int id = 0;
@@ -203,8 +208,13 @@ struct Lane {
   // pinned host staging (pageable async copies would block the enqueue)
   struct Pinned {
     uint32_t key[8];
-    MsmWindow win[MSM_MAX_WINDOWS];
+    // window tables of the MSM plans uploaded between two syncs of the lane
+    // (msm_prepare_plan's `slot`): the group test uploads two plans back to
+    // back, and one shared pinned source let the second memcpy overwrite the
+    // first before its DMA ran
+    MsmWindow win[MSM_WIN_SLOTS][MSM_MAX_WINDOWS];
     int32_t flag;
+    int32_t gflag[RP_GATHER_MAX];  // per caller batch of a grouped pass: its combination closed
   }* pin = nullptr;
   int32_t* pin_status = nullptr;
   size_t pin_status_cap = 0;
@@ -222,6 +232,21 @@ struct Lane {
     }
     return stage;
   }
+  // pinned source of the per-caller-batch slot map (its own buffer: `stage` may still
+  // be the source of an action batch's pending uploads)
+  int32_t* pin_sel = nullptr;
+  size_t pin_sel_cap = 0;
+  int32_t* sel_buf(size_t n) {
+    if (n > pin_sel_cap) {
+      if (pin_sel) (void)hipHostFree(pin_sel);
+      pin_sel = nullptr;
+      pin_sel_cap = 0;
+      const size_t want = std::max<size_t>(n, 1 << 16);
+      if (hipHostMalloc((void**)&pin_sel, want * 4, 0) != hipSuccess) return nullptr;
+      pin_sel_cap = want;
+    }
+    return pin_sel;
+  }
   int32_t* status_buf(size_t n) {
     if (n > pin_status_cap) {
       if (pin_status) (void)hipHostFree(pin_status);
@@ -235,6 +260,9 @@ struct Lane {
   void free_pinned() {
     if (pin) (void)hipHostFree(pin);
     if (pin_status) (void)hipHostFree(pin_status);
+    if (pin_sel) (void)hipHostFree(pin_sel);
+    pin_sel = nullptr;
+    pin_sel_cap = 0;
     if (stage) (void)hipHostFree(stage);
     pin = nullptr;
     pin_status = nullptr;
@@ -431,6 +459,13 @@ struct fts_ctx {
   // tools/sweeps/gt1_small.txt).  Action calls have no batch across calls: 256.
   int gt_adapt = 1;
   int x0_split = 1;  // FTS_X0_SPLIT: work path hashes the x0 prefix beside the com chain
+  // FTS_MSM_SORT: the MSMs' two-level counting sort (msm.hip k_rs_*; 0: k_msm_digits'
+  // device atomics + k_msm_scatter, the round-4 batch-check sort, for A/B)
+  int msm_sort = 1;
+  // FTS_MAIN_GROUPS: a coalesced pass checks one random linear combination PER CALLER
+  // BATCH (a G-group MSM + per-group column sums), so a bad proof's fallback covers
+  // its own batch only; 0: one combination over the pass (rounds 1-4)
+  int main_groups = 1;
   // FTS_RLC_FORK: the batch check forks after the fixed-base products (1) or after the
   // challenges (0); 2 (default): after the challenges on the latency path (a lone small
   // pass: its MSM chain is the critical path, 3.16 -> 2.98 ms per 4,096-proof batch),
@@ -577,8 +612,10 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   c->gather_target = c->coalesce_max / 2;
   if (const char* e = getenv("FTS_GATHER_US")) c->gather_us = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_COM_FIXED_MAX")) c->com_fixed_max = (size_t)std::max(0L, atol(e));
-  if (const char* e = getenv("FTS_RLC_FORK")) c->rlc_fork = std::max(0, std::min(2, atoi(e)));
+  if (const char* e = getenv("FTS_RLC_FORK")) c->rlc_fork = std::max(0, std::min(3, atoi(e)));
   if (const char* e = getenv("FTS_X0_SPLIT")) c->x0_split = atoi(e) != 0;
+  if (const char* e = getenv("FTS_MSM_SORT")) c->msm_sort = atoi(e) != 0;
+  if (const char* e = getenv("FTS_MAIN_GROUPS")) c->main_groups = atoi(e) != 0;
   if (const char* e = getenv("FTS_GT1")) c->gt1 = std::max(8, std::min(1024, atoi(e)));
   if (const char* e = getenv("FTS_GT2_MIN")) c->gt2_min = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_GT_ADAPT")) c->gt_adapt = atoi(e) != 0;
@@ -1010,16 +1047,18 @@ static void collect_timings(fts_ctx* c, Lane& L, fts_rp_batch* b) {
 
 // MSM plan for N real points on lane L's workspace (buffers grown as needed,
 // window table uploaded on L.s).  Returns 0 or FTS_API_ENOMEM.
-static int msm_prepare_plan(Lane& L, MsmPlan& mp);
-static int msm_prepare(Lane& L, int N, MsmPlan& mp, int ch = MSM_CH, bool local_sort = false) {
+static int msm_prepare_plan(Lane& L, MsmPlan& mp, int slot);
+static int msm_prepare(Lane& L, int N, MsmPlan& mp, int slot, int ch = MSM_CH, bool local_sort = false) {
   mp = MsmPlan{};
   msm_layout(N, mp);
   if (ch != MSM_CH) msm_set_chunk(mp, ch);
   mp.local_sort = local_sort;
-  return msm_prepare_plan(L, mp);
+  return msm_prepare_plan(L, mp, slot);
 }
-// buffers of an already laid-out plan (msm_layout / msm_layout_groups) on lane L
-static int msm_prepare_plan(Lane& L, MsmPlan& mp) {
+// buffers of an already laid-out plan (msm_layout / msm_layout_groups) on lane L.
+// `slot` (< MSM_WIN_SLOTS) is the pinned source of the window-table upload: plans
+// uploaded before the lane's next sync must use different slots (MSM_SLOT_*)
+static int msm_prepare_plan(Lane& L, MsmPlan& mp, int slot) {
   Workspace& w = L.ws;
   if (w.m_choff.ensure((size_t)mp.NB * 4) || w.m_chbkt.ensure((size_t)mp.NC * 4) ||
       w.m_partials.ensure((size_t)mp.NC * 96) || w.m_keys.ensure((size_t)mp.nw * mp.NV * 4) ||
@@ -1030,8 +1069,9 @@ static int msm_prepare_plan(Lane& L, MsmPlan& mp) {
       w.m_scratch.ensure(std::max((size_t)mp.NS * 96, msm_scratch_words(mp) * 4)) || w.m_win.ensure(sizeof(mp.win)))
     return FTS_API_ENOMEM;
   mp.d_win = w.m_win.as<MsmWindow>();
-  memcpy(L.pin->win, mp.win, sizeof(MsmWindow) * mp.nw);
-  if (hipMemcpyAsync(mp.d_win, L.pin->win, sizeof(MsmWindow) * mp.nw, hipMemcpyHostToDevice, L.s) != hipSuccess)
+  MsmWindow* src = L.pin->win[slot];
+  memcpy(src, mp.win, sizeof(MsmWindow) * mp.nw);
+  if (hipMemcpyAsync(mp.d_win, src, sizeof(MsmWindow) * mp.nw, hipMemcpyHostToDevice, L.s) != hipSuccess)
     return FTS_API_EDEVICE;
   mp.keys = w.m_keys.as<int32_t>();
   mp.counts = w.m_counts.as<uint32_t>();
@@ -1074,7 +1114,7 @@ static int rp_buffers(fts_ctx* c, Lane& L, int B) {
 static int lane_reserve(fts_ctx* c, Lane& L, int B, bool inputs) {
   const int npts = rp_npts(c->k);
   MsmPlan big{};
-  if (int rc = msm_prepare(L, B * npts, big)) return rc;
+  if (int rc = msm_prepare(L, B * npts, big, MSM_SLOT_RESERVE)) return rc;
   if (int rc = rp_buffers(c, L, B)) return rc;
   Workspace& w = L.ws;
   if (inputs && (w.rp_raw.ensure((size_t)B * npts * 64) || w.rp_sc.ensure((size_t)B * RP_NSC * 32) ||
@@ -1099,8 +1139,11 @@ constexpr int RP_GT2 = 8;
 // dense[q] (caller batch q = [groups[q], groups[q+1])): its round-1 groups are of
 // RP_GT2 proofs instead of gt1; with FTS_GT_ADAPT the flags are updated from this
 // fallback's round-1 failures (a batch's own density).  An empty `dense` = all sparse.
+// only (optional): only[q] != 0 for the caller batches whose own combination failed
+// (the per-caller-batch main check): the others are decided and stay out of it
 static int rp_group_fallback(fts_ctx* c, Lane& L, const RpBatchDev& d, const RlcDev& r,
-                             const std::vector<int>& groups, std::vector<uint8_t>& dense) {
+                             const std::vector<int>& groups, std::vector<uint8_t>& dense,
+                             const std::vector<uint8_t>* only = nullptr) {
   const bool adapt = c->gt_adapt && c->gt1 > RP_GT2;
   const int RP_GT2_MIN = c->gt2_min;
   const int B = d.B, n = d.n, npts = rp_npts(d.k);
@@ -1111,6 +1154,7 @@ static int rp_group_fallback(fts_ctx* c, Lane& L, const RpBatchDev& d, const Rlc
   // round-1 selections, -1 padded: groups of gt1 over the sparse batches, of RP_GT2 over the dense ones
   std::vector<int32_t> sel_big, sel_small;
   for (size_t q = 0; q < nb; q++) {
+    if (only && !(*only)[q]) continue;
     const bool small = adapt && dense[q];
     const int gs = small ? RP_GT2 : c->gt1;
     std::vector<int32_t>& sel = small ? sel_small : sel_big;
@@ -1141,7 +1185,7 @@ static int rp_group_fallback(fts_ctx* c, Lane& L, const RpBatchDev& d, const Rlc
     msm_layout_groups(G * gs * npts, G, gs * npts, gp);
     gp.sel = sel;
     gp.sel_pts = npts;
-    if (int rc = msm_prepare_plan(L, gp)) return rc;
+    if (int rc = msm_prepare_plan(L, gp, gs == RP_GT2 ? MSM_SLOT_GT_SMALL : MSM_SLOT_GT_BIG)) return rc;
     launch_rlc_group_test(d, r, c->d_tables, gp, sel, G, gs, w.r_gcol.as<uint32_t>(), w.r_gfix.as<uint32_t>(), nxt,
                           cnt, L.s, &L.tl);
     HIP_OK(hipGetLastError());
@@ -1165,7 +1209,8 @@ static int rp_group_fallback(fts_ctx* c, Lane& L, const RpBatchDev& d, const Rlc
     }
     for (size_t q = 0; q < nb; q++) {
       const int sz = groups[q + 1] - groups[q];
-      dense[q] = dense[q] ? fails[q] > 0.02 * sz : fails[q] > 0.5 * sz;
+      if (only && !(*only)[q]) dense[q] = 0;  // its combination closed: no bad proof
+      else dense[q] = dense[q] ? fails[q] > 0.02 * sz : fails[q] > 0.5 * sz;
     }
   } else if (adapt) {
     std::fill(dense.begin(), dense.end(), 0);
@@ -1224,10 +1269,35 @@ static int rp_enqueue(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc
   if (!L.presized && c->coalesce_max > (size_t)B && c->coalesce_max <= (1u << 20))
     if (int rc = lane_reserve(c, L, (int)c->coalesce_max, false)) return rc;
   MsmPlan mp{};
-#ifndef FTS_RLC_LOCAL_SORT  // A/B only: the block-local MSM sort for the batch check (default off, msm.hpp)
-#define FTS_RLC_LOCAL_SORT 0
-#endif
-  if (int rc = msm_prepare(L, N, mp, MSM_CH, FTS_RLC_LOCAL_SORT != 0)) return rc;
+  // the per-caller-batch combination: G groups of gs proof slots (padding -1)
+  const int G = (int)groups.size() - 1;
+  const bool grouped = c->main_groups && G > 1 && G <= RP_GATHER_MAX && !pre_rlc;
+  int gs = 0;
+  if (grouped) {
+    for (int q = 0; q < G; q++) gs = std::max(gs, groups[q + 1] - groups[q]);
+    msm_layout_groups(G * gs * npts, G, gs * npts, mp);
+    mp.local_sort = c->msm_sort != 0;
+    Workspace& w0 = L.ws;
+    const size_t NC = rlc_ncols(n);
+    if (w0.r_msel.ensure((size_t)G * gs * 4) || w0.r_mcol.ensure((size_t)G * NC * 32) ||
+        w0.r_mfix.ensure((size_t)G * NC * 96) || w0.r_mqfix.ensure((size_t)G * NC * 96) ||
+        w0.r_mflag.ensure((size_t)G * 4))
+      return FTS_API_ENOMEM;
+    int32_t* hs = L.sel_buf((size_t)G * gs);
+    if (!hs) return FTS_API_ENOMEM;
+    for (int q = 0; q < G; q++)
+      for (int j = 0; j < gs; j++) hs[(size_t)q * gs + j] = groups[q] + j < groups[q + 1] ? groups[q] + j : -1;
+    HIP_OK(hipMemcpyAsync(w0.r_msel.p, hs, (size_t)G * gs * 4, hipMemcpyHostToDevice, L.s));
+    // equal caller batches (the usual coalesced pass): slot = proof, no indirection in
+    // the MSM's point gathers
+    bool uniform = true;
+    for (int q = 0; q < G; q++) uniform = uniform && groups[q] == q * gs;
+    mp.sel = uniform && groups[G] == G * gs ? nullptr : w0.r_msel.as<int32_t>();
+    mp.sel_pts = npts;
+    if (int rc = msm_prepare_plan(L, mp, MSM_SLOT_PASS)) return rc;
+  } else if (int rc = msm_prepare(L, N, mp, MSM_SLOT_PASS, MSM_CH, c->msm_sort != 0)) {
+    return rc;
+  }
   if (int rc = rp_buffers(c, L, B)) return rc;
   RpBatchDev d{B,
                n,
@@ -1253,8 +1323,11 @@ static int rp_enqueue(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc
                (size_t)B <= c->com_fixed_max && L.alone ? 1 : 0};
   d.pre_rlc = pre_rlc;
   d.pre_rlc_arg = pre_rlc_arg;
-  d.rlc_fork = c->rlc_fork == 2 ? (d.com_fixed ? 0 : 1) : c->rlc_fork;
+  // 2 (adaptive): 0 on the latency path, 1 on the work path; 3: 0 on the latency
+  // path, on the work path the MSM's sort beside the fixed-base launch
+  d.rlc_fork = c->rlc_fork == 2 ? (d.com_fixed ? 0 : 1) : c->rlc_fork == 3 ? (d.com_fixed ? 0 : 3) : c->rlc_fork;
   d.ev_coef = L.ev_c;
+  d.ev_fx = L.ev_d;
   // x0 prefix beside the com chain on the work path only: on the latency path,
   // started beside com_tree it shared CUs with it and the MSM's chunks and
   // delayed both (3.51 vs 3.06 ms, round 2)
@@ -1262,6 +1335,15 @@ static int rp_enqueue(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc
   d.excl = pre_rlc ? w.rp_excl.as<int32_t>() : nullptr;
   RlcDev r{w.r_key.as<uint32_t>(), w.r_msc.as<uint32_t>(),   w.r_coef.as<uint32_t>(), w.r_colsum.as<uint32_t>(),
            w.r_fixed.as<uint32_t>(), w.r_flag.as<int32_t>(), w.m_scratch.as<uint32_t>(), mp};
+  if (grouped) {
+    r.G = G;
+    r.gs = gs;
+    r.sel = w.r_msel.as<int32_t>();
+    r.gcol = w.r_mcol.as<uint32_t>();
+    r.gfix = w.r_mfix.as<uint32_t>();
+    r.gqfix = w.r_mqfix.as<uint32_t>();
+    r.gflag = w.r_mflag.as<int32_t>();
+  }
   // fresh RLC weights key (getrandom), unpredictable to the provers
   if (getrandom(L.pin->key, sizeof L.pin->key, 0) != (ssize_t)sizeof L.pin->key) return FTS_API_EDEVICE;
   HIP_OK(hipMemcpyAsync(r.key, L.pin->key, sizeof L.pin->key, hipMemcpyHostToDevice, L.s));
@@ -1271,6 +1353,7 @@ static int rp_enqueue(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc
   between();
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(&L.pin->flag, r.flag, 4, hipMemcpyDeviceToHost, L.s));
+  if (grouped) HIP_OK(hipMemcpyAsync(L.pin->gflag, r.gflag, (size_t)G * 4, hipMemcpyDeviceToHost, L.s));
   P.t_enq = now_ms();
   P.d = d;
   P.r = r;
@@ -1286,8 +1369,13 @@ static int rp_finish(fts_ctx* c, Lane& L, RpPass& P) {
   L.host_wait_ms = (float)(t_wait - P.t_enq);
   const int32_t flag = L.pin->flag;
   c->last_fallback = flag ? 0 : 1;
-  if (!flag) return rp_group_fallback(c, L, P.d, P.r, P.groups, P.dense);
-  return FTS_API_OK;
+  if (flag) return FTS_API_OK;
+  if (P.r.G > 1) {  // per-caller-batch combination: only the failing batches go to the group test
+    std::vector<uint8_t> only((size_t)P.r.G, 0);
+    for (int q = 0; q < P.r.G; q++) only[q] = L.pin->gflag[q] ? 0 : 1;
+    return rp_group_fallback(c, L, P.d, P.r, P.groups, P.dense, &only);
+  }
+  return rp_group_fallback(c, L, P.d, P.r, P.groups, P.dense);
 }
 
 template <class F>
@@ -1671,34 +1759,67 @@ int fts_msm_stage_multiples(fts_ctx* c, size_t n, const uint8_t* k32, const uint
   fts_msm_batch* b = new fts_msm_batch();
   b->N = (int)n;
   b->device = c->device;
-  uint8_t *rk = nullptr, *rs = nullptr;
-  uint32_t* jac = nullptr;
   if (hipMalloc(&b->pts, n * 64) != hipSuccess || hipMalloc(&b->sc, n * 32) != hipSuccess ||
-      hipMalloc(&b->out, 64) != hipSuccess || hipMalloc(&rk, n * 32) != hipSuccess || hipMalloc(&rs, n * 32) != hipSuccess ||
-      hipMalloc(&jac, n * 96) != hipSuccess) {
-    for (void* p : {(void*)rk, (void*)rs, (void*)jac})
-      if (p) hipFree(p);
+      hipMalloc(&b->out, 64) != hipSuccess) {
     fts_msm_free(b);
     return FTS_API_ENOMEM;
   }
-  hipError_t e = hipMemcpy(rk, k32, n * 32, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(rs, scalars32, n * 32, hipMemcpyHostToDevice);
+  // the temporaries on a private stream with stream-ordered allocation, synchronised
+  // alone: a device-wide sync (hipDeviceSynchronize, or hipFree) here would stall
+  // every lane's in-flight pass on a shared context
+  uint8_t *rk = nullptr, *rs = nullptr;
+  uint32_t* jac = nullptr;
+  hipStream_t st = nullptr;
+  hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMallocAsync((void**)&rk, n * 32, st);
+  if (e == hipSuccess) e = hipMallocAsync((void**)&rs, n * 32, st);
+  if (e == hipSuccess) e = hipMallocAsync((void**)&jac, n * 96, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(rk, k32, n * 32, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(rs, scalars32, n * 32, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) {
     // B = the PP's ped[1] (table slot tb_G): a generator of G1
     launch_msm_gen_points((int)n, rk, rs, c->d_tables + (size_t)tb_G(c->n) * fb_words_per_base(), jac, b->pts, b->sc,
-                          nullptr);
+                          st);
     e = hipGetLastError();
   }
-  if (e == hipSuccess) e = hipDeviceSynchronize();
-  hipFree(rk);
-  hipFree(rs);
-  hipFree(jac);
+  for (void* p : {(void*)rk, (void*)rs, (void*)jac})
+    if (p) (void)hipFreeAsync(p, st);
+  if (st) {
+    const hipError_t e2 = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = e2;
+    hipStreamDestroy(st);
+  }
   if (e != hipSuccess) {
     fts_msm_free(b);
-    return FTS_API_EDEVICE;
+    return e == hipErrorOutOfMemory ? FTS_API_ENOMEM : FTS_API_EDEVICE;
   }
   *out = b;
   return FTS_API_OK;
+}
+
+int fts_msm_points(fts_ctx* c, const fts_msm_batch* b, size_t lo, size_t count, uint8_t* out64) {
+  if (c && !c->shards.empty()) return fts_msm_points(c->shards[0], b, lo, count, out64);
+  if (!c || !b || (count && !out64) || lo > (size_t)b->N || count > (size_t)b->N - lo) return FTS_API_EINVAL;
+  if (c->device < 0) return FTS_API_EDEVICE;
+  if (!count) return FTS_API_OK;
+  HIP_OK(hipSetDevice(c->device));
+  // private stream and stream-ordered scratch: no device-wide sync (see fts_msm_stage_multiples)
+  hipStream_t st = nullptr;
+  uint8_t* d = nullptr;
+  hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMallocAsync((void**)&d, count * 64, st);
+  if (e == hipSuccess) {
+    launch_msm_pts_to_bytes((int)count, b->pts + lo * 16, d, st);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(out64, d, count * 64, hipMemcpyDeviceToHost, st);
+  if (d) (void)hipFreeAsync(d, st);
+  if (st) {
+    const hipError_t e2 = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = e2;
+    hipStreamDestroy(st);
+  }
+  return e == hipSuccess ? FTS_API_OK : FTS_API_EDEVICE;
 }
 
 int fts_msm_run(fts_ctx* c, fts_msm_batch* b, uint8_t* out64) {
@@ -1711,7 +1832,7 @@ int fts_msm_run(fts_ctx* c, fts_msm_batch* b, uint8_t* out64) {
   MsmPlan mp{};
   // standalone MSMs: the block-local counting sort; from 2^20 points 32-point
   // chunks (~8 partials per bucket instead of ~32 at 2^22)
-  if (int rc = msm_prepare(L, b->N, mp, b->N >= (1 << 20) ? 32 : MSM_CH, true)) return rc;
+  if (int rc = msm_prepare(L, b->N, mp, MSM_SLOT_PASS, b->N >= (1 << 20) ? 32 : MSM_CH, c->msm_sort != 0)) return rc;
   L.tl.begin(L.s);
   launch_msm(mp, b->pts, b->sc, nullptr, 0, L.ws.m_scratch.as<uint32_t>(), L.s, L.s, &L.tl);
   launch_msm_to_bytes(mp.out, b->out, L.s);
@@ -1859,6 +1980,12 @@ int fts_rp_verify_batch(fts_ctx* c, size_t n, const uint8_t* const* rp_der, cons
   parse_rp_into(c->k, n, rp_der, rp_len, com64, p, reinterpret_cast<uint32_t*>(p + raw_b),
                 reinterpret_cast<int32_t*>(p + raw_b + sc_b), reinterpret_cast<int32_t*>(p + raw_b + sc_b + st_b));
   fts_rp_batch* b = sl->b;
+  // the slot's batch object serves unrelated callers in turn: the adaptive
+  // group-test state (FTS_GT_ADAPT) is per caller batch, so an honest call never
+  // inherits the dense schedule of the previous caller's tampered one
+  b->dense = false;
+  b->merged = 1;
+  b->ntim = 0;
   b->B = (int)n;
   b->raw = sl->dev;
   b->sc = reinterpret_cast<uint32_t*>(sl->dev + raw_b);

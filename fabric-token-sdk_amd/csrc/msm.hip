@@ -195,111 +195,215 @@ __global__ void __launch_bounds__(256) k_msm_scatter(int NV, int nw, const int32
   }
 }
 
-// ------------------------------------------------ large one-group plans
-// Counting sort without global atomics (N >= MSM_LS_MIN_N, one group, no
-// indirection): k_msm_digits' 16 returning device-scope atomics per point were
-// its cost at 2^22 points (3 ms).  Here the sort runs per (slice of virtual
-// points, window) block with the window's histogram in LDS:
-//   k_msm_split     lane per point: GLV halves + the recoding constant
-//   k_msm_lhist     block (slice, window): LDS histogram -> hs[w][slice][b]
-//   k_msm_lscan     lane per (window, bucket): prefix over the slices, counts
-//   (k_msm_scan1/2/3 as before: bucket offsets and the chunk map)
-//   k_msm_lscatter  block (slice, window): LDS cursors = bucket offset + slice
-//                   prefix; each entry takes the next slot of its bucket
-// Signed digits as bit fields: with C = sum_w (2^(width_w-1) - 1) 2^off_w,
-// window w's digit of k is ((k + C) >> off_w mod 2^width_w) - (2^(width_w-1) - 1)
-// (the carries of k + C are exactly the recoding carries of k_msm_digits:
-// d > half <=> bits + carry + half - 1 >= 2^width), so every block extracts
-// its window's digit without the lower windows.  Same buckets and signs as
-// k_msm_digits; the order inside a bucket differs (bucket sums are the same
-// group elements, and only the affine result is observable).
-constexpr int MSM_LS_SLICES = 64;
-constexpr int MSM_LS_MIN_N = 1 << 18;  // points
-constexpr int MSM_LS_BS = 1024;
+// ------------------------------------------------ two-level counting sort
+// (round 5; one-group plans whose windows all have >= 2^RS_PSH buckets: the
+// batch check's MSM and standalone MSMs).  k_msm_digits costs 2 x nw returning
+// device-scope atomics per point (VALUBusy 4.5 %, 0.89 GB written per
+// 81,920-proof pass) and k_msm_scatter one random 4-byte HBM write per entry
+// (0.70 GB); the round-4 block-local sort held a window's whole histogram in
+// 128 KB of LDS per 1,024-thread block and took whole CUs beside the chain
+// kernels.  Here every LDS table is <= 32 KB per 256-thread block and no
+// device-scope atomic is used:
+//   k_rs_hist     block per slice of RS_SP points: GLV split, every window's
+//                 signed digit, LDS histogram over PARTITIONS (bucket >> RS_PSH,
+//                 NP <= RS_MAX_NP counters) -> hist[slice][p] (one coalesced row)
+//   k_rs_pscan    lane per partition: exclusive prefix over the slices, in place
+//   k_rs_pbase    one block: exclusive scan of the partition totals -> pbase
+//   k_rs_scatter  block per slice: LDS cursors = pbase + the slice's prefix; each
+//                 entry takes the next slot of its partition (a slice writes
+//                 ~RS_SP * 2 nw / NP consecutive entries per partition: whole
+//                 lines, combined in L2), entry = virtual index | low bucket
+//                 bits << 24 | sign << 31
+//   k_rs_part     block per partition: LDS counting sort of its <= ~11 k entries
+//                 by the low bucket bits -> counts[b] and the final sorted array
+// (k_msm_scan1/2/3 then derive the bucket offsets -- the same positions, the
+// order is bucket-major in both -- and the chunk map).  Digits: with C = sum_w
+// (2^(width_w-1) - 1) 2^off_w, window w's signed digit of a GLV half k is
+// ((k + C) >> off_w mod 2^width_w) - (2^(width_w-1) - 1): the carries of k + C
+// are exactly k_msm_digits' recoding carries (tests/test_msm_recode_cpu.py), so
+// the digits are independent bit fields.  Same buckets and signs as
+// k_msm_digits; the order inside a bucket differs, which changes no group
+// element (only the affine result is observable).
+constexpr int RS_PSH = 7;                 // buckets per partition: 128
+constexpr int RS_SP = 2048;               // points per slice (block)
+constexpr int RS_MAX_NPG = 8192;          // partitions per group: LDS counters <= 32 KB
+constexpr int RS_MIN_N = 4096;            // smaller plans keep k_msm_digits
+constexpr uint32_t RS_IDX_MASK = 0x00ffffffu;  // virtual index bits of an entry (NV < 2^24)
+// Grouped plans (G > 1, e.g. the batch check per caller batch): slices never
+// straddle two groups (SPG slices per group), a slice's LDS table holds its own
+// group's NPg = NBg / 128 partitions, hist is [slice][NPg], and the global
+// partition g NPg + lp covers the group's buckets g NBg + 128 lp .. + 127.
 
-__global__ void __launch_bounds__(256) k_msm_split(int N, uint4 rc, const uint32_t* __restrict__ scalars,
+// lane per plan point: the GLV halves of its scalar with the recoding constant
+// folded in, hk[h N + i] = (k_h + C) | sign_h << 127 (absent padding points of a
+// grouped plan: k = 0, so every window's digit is 0).  One point per lane, so the
+// split is spread over the chip instead of the hist / scatter blocks' slices
+__global__ void __launch_bounds__(256) k_msm_split(MsmIdx p, uint4 rc, const uint32_t* __restrict__ scalars,
                                                    uint4* __restrict__ hk) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
-  uint32_t s[8];
-#pragma unroll
-  for (int q = 0; q < 8; q++) s[q] = scalars[(size_t)i * 8 + q];
-  uint32_t k[2][4], sg[2];
-  glv_decompose(s, k[0], sg[0], k[1], sg[1]);
+  if (i >= p.N) return;
+  const long src = msm_src(p, i);
+  uint32_t k[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, sg[2] = {0, 0};
+  if (src >= 0) {
+    uint32_t s[8];
+    const uint4* s4 = reinterpret_cast<const uint4*>(scalars + (size_t)src * 8);
+    const uint4 a = s4[0], b = s4[1];
+    s[0] = a.x, s[1] = a.y, s[2] = a.z, s[3] = a.w, s[4] = b.x, s[5] = b.y, s[6] = b.z, s[7] = b.w;
+    glv_decompose(s, k[0], sg[0], k[1], sg[1]);
+  }
 #pragma unroll
   for (int h = 0; h < 2; h++) {
-    uint64_t t = (uint64_t)k[h][0] + rc.x;
-    const uint32_t w0 = (uint32_t)t;
-    t = (t >> 32) + k[h][1] + rc.y;
-    const uint32_t w1 = (uint32_t)t;
-    t = (t >> 32) + k[h][2] + rc.z;
-    const uint32_t w2 = (uint32_t)t;
-    t = (t >> 32) + k[h][3] + rc.w;
-    const uint32_t w3 = ((uint32_t)t & 0x7fffffffu) | (sg[h] ? 0x80000000u : 0u);  // k + C < 2^127
-    hk[(size_t)h * N + i] = make_uint4(w0, w1, w2, w3);
+    uint32_t q0, q1, q2, q3, c;
+    q0 = addc(k[h][0], rc.x, 0, c);
+    q1 = addc(k[h][1], rc.y, c, c);
+    q2 = addc(k[h][2], rc.z, c, c);
+    q3 = addc(k[h][3], rc.w, c, c);  // k + C < 2^127
+    hk[(size_t)h * p.N + i] = make_uint4(q0, q1, q2, (q3 & 0x7fffffffu) | (sg[h] ? 0x80000000u : 0u));
   }
 }
 
-FTS_DEV int ls_digit(const uint4 q, const MsmWindow& W) {
-  const uint32_t k[4] = {q.x, q.y, q.z, q.w & 0x7fffffffu};
-  return (int)scalar_bits4(k, W.off, W.width) - ((1 << (W.width - 1)) - 1);
-}
-
-__global__ void __launch_bounds__(MSM_LS_BS) k_msm_lhist(int NV, int per, int S, int stride,
-                                                        const MsmWindow* __restrict__ win,
-                                                        const uint4* __restrict__ hk, uint32_t* __restrict__ hs) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lh[];
-  const int sl = blockIdx.x, w = blockIdx.y;
-  const MsmWindow W = win[w];
-  const int nb = 1 << (W.width - 1);
-  for (int b = threadIdx.x; b < nb; b += blockDim.x) lh[b] = 0;
-  __syncthreads();
-  const int v1 = min(NV, (sl + 1) * per);
-  for (int v = sl * per + threadIdx.x; v < v1; v += blockDim.x) {
-    const int d = ls_digit(hk[v], W);
-    if (d != 0) atomicAdd(&lh[(d < 0 ? -d : d) - 1], 1u);
+// the nonzero window digits of plan point i's two GLV halves (from k_msm_split);
+// f(local bucket, sign, virtual index) per digit
+template <class F>
+FTS_DEV void rs_point_digits(const MsmIdx& p, const MsmWindow* __restrict__ win, const uint4* __restrict__ hk, int i,
+                             F&& f) {
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint4 u = hk[(size_t)h * p.N + i];
+    const uint32_t q[4] = {u.x, u.y, u.z, u.w & 0x7fffffffu};
+    const bool sg = (u.w >> 31) != 0;
+    for (int w = 0; w < p.nw; w++) {
+      const MsmWindow W = win[w];
+      const int d = (int)scalar_bits4(q, W.off, W.width) - ((1 << (W.width - 1)) - 1);
+      if (d != 0) f(W.bbase + (d < 0 ? -d : d) - 1, (d < 0) != sg, (uint32_t)(h * p.N + i));
+    }
   }
-  __syncthreads();
-  uint32_t* out = hs + ((size_t)w * S + sl) * stride;
-  for (int b = threadIdx.x; b < nb; b += blockDim.x) out[b] = lh[b];
+}
+// points [i0, i1) of slice blockIdx.x (group g)
+FTS_DEV void rs_slice(const MsmIdx& p, int spg, int& g, int& i0, int& i1) {
+  g = blockIdx.x / spg;
+  const int ls = blockIdx.x % spg;
+  i0 = g * p.ptsg + ls * RS_SP;
+  i1 = min(min(i0 + RS_SP, (g + 1) * p.ptsg), p.N);
 }
 
-__global__ void __launch_bounds__(256) k_msm_lscan(int S, int stride, const MsmWindow* __restrict__ win,
-                                                  uint32_t* __restrict__ hs, uint32_t* __restrict__ counts) {
-  const int w = blockIdx.y, b = blockIdx.x * blockDim.x + threadIdx.x;
-  const MsmWindow W = win[w];
-  if (b >= (1 << (W.width - 1))) return;
+__global__ void __launch_bounds__(256) k_rs_hist(MsmIdx p, int spg, int npg, const MsmWindow* __restrict__ win,
+                                                 const uint4* __restrict__ hk, uint32_t* __restrict__ hist) {
+  extern __shared__ uint32_t rs_lds[];
+  for (int q = threadIdx.x; q < npg; q += blockDim.x) rs_lds[q] = 0;
+  __syncthreads();
+  int g, i0, i1;
+  rs_slice(p, spg, g, i0, i1);
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x)
+    rs_point_digits(p, win, hk, i, [&](int bl, bool, uint32_t) { atomicAdd(&rs_lds[bl >> RS_PSH], 1u); });
+  __syncthreads();
+  uint32_t* out = hist + (size_t)blockIdx.x * npg;
+  for (int q = threadIdx.x; q < npg; q += blockDim.x) out[q] = rs_lds[q];
+}
+
+// lane per global partition g npg + lp: exclusive prefix over the group's slices, in place
+__global__ void __launch_bounds__(256) k_rs_pscan(int G, int spg, int npg, uint32_t* __restrict__ hist,
+                                                  uint32_t* __restrict__ ptot) {
+  const int P = blockIdx.x * blockDim.x + threadIdx.x;
+  if (P >= G * npg) return;
+  const int g = P / npg, lp = P % npg;
+  uint32_t* h = hist + (size_t)g * spg * npg + lp;
   uint32_t acc = 0;
-  for (int sl = 0; sl < S; sl++) {
-    uint32_t* q = hs + ((size_t)w * S + sl) * stride + b;
-    const uint32_t c = *q;
-    *q = acc;
+  int s = 0;
+  for (; s + 8 <= spg; s += 8) {  // 8 loads in flight per lane
+    uint32_t c[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) c[q] = h[(size_t)(s + q) * npg];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      h[(size_t)(s + q) * npg] = acc;
+      acc += c[q];
+    }
+  }
+  for (; s < spg; s++) {
+    const uint32_t c = h[(size_t)s * npg];
+    h[(size_t)s * npg] = acc;
     acc += c;
   }
-  counts[W.bbase + b] = acc;
+  ptot[P] = acc;
 }
 
-__global__ void __launch_bounds__(MSM_LS_BS) k_msm_lscatter(int NV, int per, int S, int stride,
-                                                           const MsmWindow* __restrict__ win,
-                                                           const uint4* __restrict__ hk,
-                                                           const uint32_t* __restrict__ hs,
-                                                           const uint32_t* __restrict__ offsets,
-                                                           uint32_t* __restrict__ sorted) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
-  const int sl = blockIdx.x, w = blockIdx.y;
-  const MsmWindow W = win[w];
-  const int nb = 1 << (W.width - 1);
-  const uint32_t* pre = hs + ((size_t)w * S + sl) * stride;
-  for (int b = threadIdx.x; b < nb; b += blockDim.x) cur[b] = offsets[W.bbase + b] + pre[b];
+constexpr int RS_PB_BS = 1024;
+__global__ void __launch_bounds__(RS_PB_BS) k_rs_pbase(int NP, const uint32_t* __restrict__ ptot,
+                                                      uint32_t* __restrict__ pbase) {
+  __shared__ uint32_t sh[RS_PB_BS];
+  const int t = threadIdx.x, per = (NP + RS_PB_BS - 1) / RS_PB_BS;
+  uint32_t loc = 0;
+  for (int j = 0; j < per; j++) {
+    const int q = t * per + j;
+    if (q < NP) loc += ptot[q];
+  }
+  sh[t] = loc;
   __syncthreads();
-  const int v1 = min(NV, (sl + 1) * per);
-  for (int v = sl * per + threadIdx.x; v < v1; v += blockDim.x) {
-    const uint4 q = hk[v];
-    const int d = ls_digit(q, W);
-    if (d != 0) {
-      const uint32_t pos = atomicAdd(&cur[(d < 0 ? -d : d) - 1], 1u);
-      sorted[pos] = (uint32_t)v | (((d < 0) != ((q.w >> 31) != 0)) ? 0x80000000u : 0u);
+  for (int off = 1; off < RS_PB_BS; off <<= 1) {
+    const uint32_t v = t >= off ? sh[t - off] : 0u;
+    __syncthreads();
+    sh[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = sh[t] - loc;
+  for (int j = 0; j < per; j++) {
+    const int q = t * per + j;
+    if (q < NP) {
+      pbase[q] = run;
+      run += ptot[q];
     }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_rs_scatter(MsmIdx p, int spg, int npg, const MsmWindow* __restrict__ win,
+                                                    const uint4* __restrict__ hk, const uint32_t* __restrict__ hist,
+                                                    const uint32_t* __restrict__ pbase, uint32_t* __restrict__ tmp) {
+  extern __shared__ uint32_t rs_lds[];
+  int g, i0, i1;
+  rs_slice(p, spg, g, i0, i1);
+  const uint32_t* pre = hist + (size_t)blockIdx.x * npg;
+  const uint32_t* pb = pbase + (size_t)g * npg;
+  for (int q = threadIdx.x; q < npg; q += blockDim.x) rs_lds[q] = pb[q] + pre[q];
+  __syncthreads();
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x)
+    rs_point_digits(p, win, hk, i, [&](int bl, bool neg, uint32_t v) {
+      const uint32_t pos = atomicAdd(&rs_lds[bl >> RS_PSH], 1u);
+      tmp[pos] = v | ((uint32_t)(bl & ((1 << RS_PSH) - 1)) << 24) | (neg ? 0x80000000u : 0u);
+    });
+}
+
+// block per global partition P (buckets 128 P .. 128 P + 127: group P / npg's local
+// partition P % npg, as NBg = 128 npg)
+__global__ void __launch_bounds__(256) k_rs_part(const uint32_t* __restrict__ pbase, const uint32_t* __restrict__ ptot,
+                                                 const uint32_t* __restrict__ tmp, uint32_t* __restrict__ counts,
+                                                 uint32_t* __restrict__ sorted) {
+  constexpr int PB = 1 << RS_PSH;
+  __shared__ uint32_t cnt[PB], cur[PB];
+  const int P = blockIdx.x, t = threadIdx.x;
+  const uint32_t lo = pbase[P], n = ptot[P];
+  if (t < PB) cnt[t] = 0;
+  __syncthreads();
+  for (uint32_t e = t; e < n; e += blockDim.x) atomicAdd(&cnt[(tmp[lo + e] >> 24) & (PB - 1)], 1u);
+  __syncthreads();
+  if (t < PB) {
+    const uint32_t c = cnt[t];
+    counts[(size_t)P * PB + t] = c;
+    cur[t] = c;
+  }
+  __syncthreads();
+  for (int off = 1; off < PB; off <<= 1) {  // inclusive scan of the 128 counts
+    const uint32_t v = (t < PB && t >= off) ? cur[t - off] : 0u;
+    __syncthreads();
+    if (t < PB) cur[t] += v;
+    __syncthreads();
+  }
+  if (t < PB) cur[t] -= cnt[t];  // exclusive
+  __syncthreads();
+  for (uint32_t e = t; e < n; e += blockDim.x) {
+    const uint32_t x = tmp[lo + e];
+    const uint32_t pos = atomicAdd(&cur[(x >> 24) & (PB - 1)], 1u);
+    sorted[lo + pos] = (x & RS_IDX_MASK) | (x & 0x80000000u);
   }
 }
 
@@ -547,6 +651,14 @@ __global__ void __launch_bounds__(256) k_msm_load(int N, const uint8_t* __restri
   for (int q = 0; q < 8; q++) sc[(size_t)i * 8 + q] = k.v[q];
 }
 
+// staged affine Montgomery points [lo, lo + n) -> 64-byte BE (fts_msm_points)
+__global__ void __launch_bounds__(256) k_msm_pts_to_bytes(int n, const uint32_t* __restrict__ pts,
+                                                         uint8_t* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  store_point_be(out + (size_t)i * 64, load_g1a(pts + (size_t)i * 16));
+}
+
 // Jacobian result -> 64-byte BE affine (identity -> 64 zero bytes)
 __global__ void k_msm_to_bytes(const uint32_t* __restrict__ jac, uint8_t* __restrict__ out) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -562,17 +674,18 @@ __global__ void k_msm_to_bytes(const uint32_t* __restrict__ jac, uint8_t* __rest
 // scratch: NS * 24 words.  p.d_win must already hold p.win (uploaded by the caller).
 // `extra` (nextra Jacobian points) is produced on stream s_extra: joined
 // before the window reduction that sums it.
-// digits, counting sort, chunked bucket accumulation and bucket sums (every plan)
-static void launch_msm_buckets(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, hipStream_t s,
-                               Timeline* tl, hipEvent_t ev_stage = nullptr, int stage = 0) {
-  // block-local counting sort for large one-group plans (keys: the split
-  // halves, NV x 16 B; cursor: the slice histograms, nw x S x stride words)
-  int nbmax = 1;
-  for (int w = 0; w < p.nw; w++) nbmax = std::max(nbmax, 1 << (p.win[w].width - 1));
-  const int S = std::min(MSM_LS_SLICES, p.NV / nbmax);
-  const bool ls = p.local_sort && p.G == 1 && !p.sel && p.N >= MSM_LS_MIN_N && nbmax <= (1 << 15) && S >= 8 &&
-                  p.nw >= 4;
-  if (ls) {
+// digits and counting sort: every entry (window, virtual point) placed in its bucket
+// (p.sorted / p.counts / p.offsets) and the chunk map -- needs only the scalars
+void launch_msm_sort(const MsmPlan& p, const uint32_t* scalars, hipStream_t s, Timeline* tl) {
+  // two-level counting sort (every window >= 2^RS_PSH buckets): tmp entries in
+  // p.keys, slice histograms + partition totals / bases in p.cursor
+  bool rs = p.local_sort && p.N >= RS_MIN_N && p.NV <= (int)RS_IDX_MASK && (p.NBg & ((1 << RS_PSH) - 1)) == 0;
+  for (int w = 0; w < p.nw; w++) rs = rs && p.win[w].width > RS_PSH && (p.win[w].bbase & ((1 << RS_PSH) - 1)) == 0;
+  const int npg = p.NBg >> RS_PSH, NP = p.G * npg;
+  const int spg = (p.ptsg + RS_SP - 1) / RS_SP, S = p.G * spg;
+  rs = rs && npg <= RS_MAX_NPG && p.ptsg > 0 && (size_t)S * npg + 2 * (size_t)NP <= (size_t)p.nw * p.NV &&
+       p.nw >= 4;  // the split halves (NV x 16 B) fit in the sorted array (nw x NV x 4 B)
+  if (rs) {
     uint32_t rc[4] = {0, 0, 0, 0};  // C = sum_w (2^(width_w-1) - 1) 2^off_w (< 2^126)
     for (int w = 0; w < p.nw; w++) {
       uint64_t add = (uint64_t)((1u << (p.win[w].width - 1)) - 1u);
@@ -584,24 +697,32 @@ static void launch_msm_buckets(const MsmPlan& p, const uint32_t* points, const u
         c = (c >> 32) + (t >> 32);
       }
     }
-    const int per = (p.NV + S - 1) / S;
-    uint4* hk = reinterpret_cast<uint4*>(p.keys);
-    FTS_LAUNCH(k_msm_split, p.N, 256, s, p.N, make_uint4(rc[0], rc[1], rc[2], rc[3]), scalars, hk);
+    const uint4 rcv = make_uint4(rc[0], rc[1], rc[2], rc[3]);
+    uint32_t* hist = p.cursor;                       // [S][npg]
+    uint32_t* ptot = hist + (size_t)S * npg;         // [NP]
+    uint32_t* pbase = ptot + NP;                     // [NP]
+    uint32_t* tmp = reinterpret_cast<uint32_t*>(p.keys);
+    // the split halves (NV x 16 B) in the sorted array's space: k_rs_part overwrites
+    // it only after the scatter has read them
+    uint4* hk = reinterpret_cast<uint4*>(p.sorted);
+    const size_t lds = (size_t)npg * 4;
+    const MsmIdx ix = msm_idx(p);
+    FTS_LAUNCH(k_msm_split, p.N, 256, s, ix, rcv, scalars, hk);
     tl->mark("k_msm_split", s, 0);
-    const size_t lds = (size_t)nbmax * 4;
-    hipLaunchKernelGGL(k_msm_lhist, dim3(S, p.nw), dim3(MSM_LS_BS), lds, s, p.NV, per, S, nbmax, p.d_win, hk,
-                       p.cursor);
-    hipLaunchKernelGGL(k_msm_lscan, dim3((nbmax + 255) / 256, p.nw), dim3(256), 0, s, S, nbmax, p.d_win, p.cursor,
-                       p.counts);
-    tl->mark("k_msm_lhist", s, 0);
+    hipLaunchKernelGGL(k_rs_hist, dim3(S), dim3(256), lds, s, ix, spg, npg, p.d_win, hk, hist);
+    tl->mark("k_rs_hist", s, 0);
+    FTS_LAUNCH(k_rs_pscan, NP, 256, s, p.G, spg, npg, hist, ptot);
+    hipLaunchKernelGGL(k_rs_pbase, dim3(1), dim3(RS_PB_BS), 0, s, NP, ptot, pbase);
+    tl->mark("k_rs_pscan", s, 0);
+    hipLaunchKernelGGL(k_rs_scatter, dim3(S), dim3(256), lds, s, ix, spg, npg, p.d_win, hk, hist, pbase, tmp);
+    tl->mark("k_rs_scatter", s, 0);
+    hipLaunchKernelGGL(k_rs_part, dim3(NP), dim3(256), 0, s, pbase, ptot, tmp, p.counts, p.sorted);
+    tl->mark("k_rs_part", s, 0);
     FTS_LAUNCH(k_msm_scan1, (size_t)p.NBLK * 256, 256, s, p.NB, p.ch, p.counts, p.offsets, p.chunk_off, p.scratch);
     hipLaunchKernelGGL(k_msm_scan2, dim3(1), dim3(256), 0, s, p.NBLK, p.scratch);
     FTS_LAUNCH(k_msm_scan3, p.NB, 256, s, p.NB, p.ch, p.counts, p.offsets, nullptr, p.chunk_off, p.chunk_bkt,
                p.scratch);
     tl->mark("k_msm_scan", s, 0);
-    hipLaunchKernelGGL(k_msm_lscatter, dim3(S, p.nw), dim3(MSM_LS_BS), lds, s, p.NV, per, S, nbmax, p.d_win, hk,
-                       p.cursor, p.offsets, p.sorted);
-    tl->mark("k_msm_lscatter", s, 0);
   } else {
     (void)hipMemsetAsync(p.counts, 0, (size_t)p.NB * 4, s);
     FTS_LAUNCH(k_msm_digits, p.N, 256, s, msm_idx(p), p.d_win, scalars, p.keys, p.cursor, p.counts);
@@ -614,7 +735,11 @@ static void launch_msm_buckets(const MsmPlan& p, const uint32_t* points, const u
     FTS_LAUNCH(k_msm_scatter, p.NV, 256, s, p.NV, p.nw, p.keys, p.cursor, p.offsets, p.sorted);
     tl->mark("k_msm_scatter", s, 0);
   }
-  if (ev_stage && stage == 1) (void)hipEventRecord(ev_stage, s);
+}
+
+// chunked bucket accumulation and bucket sums over a sorted plan (every plan)
+static void launch_msm_accumulate(const MsmPlan& p, const uint32_t* points, hipStream_t s, Timeline* tl,
+                                  hipEvent_t ev_stage = nullptr, int stage = 0) {
   FTS_LAUNCH(k_msm_chunks, p.NC, 64, s, msm_idx(p), p.scratch + 2 * (size_t)p.NBLK + 1, p.d_win, points, p.offsets,
              p.counts, p.chunk_off,
              p.chunk_bkt, p.sorted, p.partials);
@@ -625,9 +750,35 @@ static void launch_msm_buckets(const MsmPlan& p, const uint32_t* points, const u
   tl->mark("k_msm_bucket_sum", s, 0);
 }
 
+static void launch_msm_buckets(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, hipStream_t s,
+                               Timeline* tl, hipEvent_t ev_stage = nullptr, int stage = 0) {
+  launch_msm_sort(p, scalars, s, tl);
+  if (ev_stage && stage == 1) (void)hipEventRecord(ev_stage, s);
+  launch_msm_accumulate(p, points, s, tl, ev_stage, stage);
+}
+
+// window reduction of the bucket sums: segments, windows (+ the extra points), final
+static void launch_msm_tail(const MsmPlan& p, const uint32_t* extra, int nextra, uint32_t* scratch, hipStream_t s,
+                            hipStream_t s_extra, Timeline* tl);
+
+// accumulation and reduction of a plan sorted by launch_msm_sort (the batch check
+// sorts beside the fixed-base launch and accumulates after it)
+void launch_msm_reduce(const MsmPlan& p, const uint32_t* points, const uint32_t* extra, int nextra, uint32_t* scratch,
+                       hipStream_t s, hipStream_t s_extra, Timeline* tl) {
+  launch_msm_accumulate(p, points, s, tl);
+  launch_msm_tail(p, extra, nextra, scratch, s, s_extra, tl);
+}
+
 void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
                 uint32_t* scratch, hipStream_t s, hipStream_t s_extra, Timeline* tl, hipEvent_t ev_stage, int stage) {
-  launch_msm_buckets(p, points, scalars, s, tl, ev_stage, stage);
+  launch_msm_sort(p, scalars, s, tl);
+  if (ev_stage && stage == 1) (void)hipEventRecord(ev_stage, s);
+  launch_msm_accumulate(p, points, s, tl, ev_stage, stage);
+  launch_msm_tail(p, extra, nextra, scratch, s, s_extra, tl);
+}
+
+static void launch_msm_tail(const MsmPlan& p, const uint32_t* extra, int nextra, uint32_t* scratch, hipStream_t s,
+                            hipStream_t s_extra, Timeline* tl) {
   FTS_LAUNCH(k_msm_segments, p.NS, g_lat_bs, s, p.nw, p.NS, p.NSg, p.NBg, p.d_win, p.buckets, p.segs, scratch);
   tl->mark("k_msm_segments", s, (double)p.NB * 2 * COST_ADD);
   if (s_extra != s) tl->fork(s_extra, s);
@@ -665,6 +816,9 @@ void launch_msm_small(const MsmPlan& p, const uint32_t* points, const uint32_t* 
 void launch_msm_load(int N, const uint8_t* raw_pts, const uint8_t* raw_sc, uint32_t* pts, uint32_t* sc, uint32_t* bad,
                      hipStream_t s) {
   FTS_LAUNCH(k_msm_load, N, 256, s, N, raw_pts, raw_sc, pts, sc, bad);
+}
+void launch_msm_pts_to_bytes(int n, const uint32_t* pts, uint8_t* out, hipStream_t s) {
+  FTS_LAUNCH(k_msm_pts_to_bytes, n, 256, s, n, pts, out);
 }
 void launch_msm_to_bytes(const uint32_t* jac, uint8_t* out, hipStream_t s) {
   hipLaunchKernelGGL(k_msm_to_bytes, dim3(1), dim3(64), 0, s, jac, out);

@@ -47,11 +47,10 @@ constexpr int g_chain_bs = 64;
 
 
 constexpr int NORM_BS = 256;
-// points per lane of k_rp_normalize: 8 for normalisations of >= NORM_BIG points
-// (half the blocks, scans and inversions: 1.23 -> 0.89 ms at 5.3 M points),
-// 4 below (more blocks to fill the chip: at 262 k points 8 was 0.07 ms slower)
-constexpr int NORM_E = 4;  // nominal, for the cost model
-constexpr size_t NORM_BIG = (size_t)1 << 20;
+// points per lane of k_rp_normalize (one inversion per lane, round 5): 16 for
+// normalisations of >= NORM_BIG points, 4 below (more lanes for small batches)
+constexpr int NORM_E = 16;  // nominal, for the cost model
+constexpr size_t NORM_BIG = (size_t)1 << 16;
 template <int E>
 __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, int stride, int first,
                                                           const int32_t* __restrict__ status,
@@ -59,6 +58,22 @@ __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, in
                                                           uint8_t* __restrict__ be);
 static void launch_normalize(size_t total, int per, int stride, int first, const int32_t* status, const uint32_t* jac,
                              uint32_t* aff, uint8_t* be, hipStream_t s);
+// Jacobian -> affine (Montgomery, 16 words) and BE bytes of ONE point by its own
+// inversion (identity -> (0, 0)): com at the end of its chain (round 5: instead of
+// a k_rp_normalize launch of one point per proof on the critical path)
+FTS_DEV void store_affine_one(const G1J& p, uint32_t* aff, uint8_t* be) {
+  G1A r;
+  if (f_is_zero(p.z)) {
+    r.x = f_zero<FpP>();
+    r.y = f_zero<FpP>();
+  } else {
+    const Fp zi = nl_fp_inv(p.z), zi2 = fp_sqr(zi);
+    r.x = fp_mul(p.x, zi2);
+    r.y = fp_mul(fp_mul(p.y, zi2), zi);
+  }
+  store_g1a(aff, r);
+  store_point_be(be, r);
+}
 
 // ---------------------------------------------------------- context tables
 // Built once per context (device/fixed_base.hpp layout), for nb bases:
@@ -440,7 +455,8 @@ __global__ void __launch_bounds__(256) k_rp_hsum_join(int B, int n, const int32_
 __global__ void __launch_bounds__(256, FTS_COMVAR_OCC) k_rp_com_var(int B, int n, int k, const int32_t* __restrict__ status,
                                                    const uint32_t* __restrict__ pts, const uint32_t* __restrict__ ch,
                                                    const uint32_t* __restrict__ chunks, uint32_t* __restrict__ atab,
-                                                   const uint32_t* __restrict__ terms, uint32_t* __restrict__ hpj) {
+                                                   const uint32_t* __restrict__ terms, uint32_t* __restrict__ hpj,
+                                                   uint32_t* __restrict__ hpa, uint8_t* __restrict__ hp_be) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = gid >> 1, h = gid & 1;
   if (b >= B || status[b] != 0) return;
@@ -448,22 +464,34 @@ __global__ void __launch_bounds__(256, FTS_COMVAR_OCC) k_rp_com_var(int B, int n
   Fr x, z2;
   load_f(C + CH_X * 8, x);
   load_f(C + CH_Z2 * 8, z2);
-  uint32_t xk[2][4], xs[2], wk[2][4], ws[2];
-  glv_decompose(fr_canon(x).v, xk[0], xs[0], xk[1], xs[1]);
-  glv_decompose(fr_canon(z2).v, wk[0], ws[0], wk[1], ws[1]);
+  // this lane's GLV halves by selects, not by indexing [h]: a runtime index made
+  // the compiler keep the arrays in LDS (16 KB per 64-lane block), and com_var's
+  // blocks then held every CU's LDS and starved the x0 build beside them (round 5)
+  uint32_t xa[4], xb[4], xs0, xs1, wa[4], wb[4], ws0, ws1, xh[4], wh[4];
+  glv_decompose(fr_canon(x).v, xa, xs0, xb, xs1);
+  glv_decompose(fr_canon(z2).v, wa, ws0, wb, ws1);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    xh[q] = h ? xb[q] : xa[q];
+    wh[q] = h ? wb[q] : wa[q];
+  }
+  const bool xsh = (h ? xs1 : xs0) != 0, wsh = (h ? ws1 : ws0) != 0;
   const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
   G1J S = load_g1j(chunks + (size_t)b * nc * 24);  // k_rp_hsum_join
   const G1A Da = load_g1a(pts + ((size_t)b * rp_npts(k) + RP_PT_D) * 16);
   const bool idD = g1a_is_identity(Da), idS = f_is_zero(S.z);
   // the proof's shared table: lane 0 builds 1..8 D, lane 1 1..8 S (one instruction
-  // stream on the lane's own point: no divergence); both lanes of a proof are
-  // adjacent lanes of one wave, so the workgroup fence orders each lane's rows
-  // before the other reads them
+  // stream on the lane's own point: no divergence).  Both lanes of a proof are
+  // adjacent lanes (gid 2b, 2b + 1) of ONE wave64 wave, which runs them in
+  // lockstep: the fence makes each lane's row stores visible, the wave barrier
+  // keeps the compiler from moving the other lane's reads above it
+  static_assert(256 % 64 == 0, "k_rp_com_var: a proof's lane pair must sit in one wave");
   const CTab T{atab, (size_t)B, (size_t)b};
   const G1J Dj = g1j_from_affine(Da);
   ctab_build8<false>(T, 8 * h, h ? S : Dj, h ? idS : idD);
   __threadfence_block();
-  G1J r = straus2_ctab(T, h, xk[h], xs[h] != 0, wk[h], ws[h] != 0, idD, idS);
+  __builtin_amdgcn_wave_barrier();
+  G1J r = straus2_ctab(T, h, xh, xsh, wh, wsh, idD, idS);
   // com = C + z K - delta P + x D + z^2 S (bulletproof.go:477-492), summed by the
   // proof's two lanes (adjacent lanes of one wave; both exit or both run): lane h
   // adds its fixed-base term (z K or -delta P, k_rp_fixed_exact), lane 0 also C,
@@ -481,7 +509,9 @@ __global__ void __launch_bounds__(256, FTS_COMVAR_OCC) k_rp_com_var(int B, int n
   }
   if (h == 0) {
     add_inl(r, o);
-    store_g1j(hpj + ((size_t)b * (n + 1) + n) * 24, r);
+    const size_t q = (size_t)b * (n + 1) + n;
+    store_g1j(hpj + q * 24, r);
+    store_affine_one(r, hpa + q * 16, hp_be + q * 64);  // com for the x0 suffix (no normalize_com launch)
   }
 }
 
@@ -568,7 +598,9 @@ __global__ void __launch_bounds__(CT_LANES * CT_PROOFS) k_rp_com_tree(int B, int
                                                                       const int32_t* __restrict__ status,
                                                                       const uint32_t* __restrict__ pts,
                                                                       const uint32_t* __restrict__ terms,
-                                                                      uint32_t* __restrict__ hpj) {
+                                                                      uint32_t* __restrict__ hpj,
+                                                                      uint32_t* __restrict__ hpa,
+                                                                      uint8_t* __restrict__ hp_be) {
   __shared__ uint32_t sh[CT_LANES * CT_PROOFS * 24];
   const int l = threadIdx.x % CT_LANES, pl = threadIdx.x / CT_LANES;
   const int b = blockIdx.x * CT_PROOFS + pl;
@@ -589,117 +621,80 @@ __global__ void __launch_bounds__(CT_LANES * CT_PROOFS) k_rp_com_tree(int B, int
     if (live && l < half) store_g1j(S + l * 24, acc);
     __syncthreads();
   }
-  if (live && l == 0) store_g1j(hpj + ((size_t)b * (n + 1) + n) * 24, acc);
+  if (live && l == 0) {
+    const size_t q = (size_t)b * (n + 1) + n;
+    store_g1j(hpj + q * 24, acc);
+    store_affine_one(acc, hpa + q * 16, hp_be + q * 64);
+  }
 }
 
-// Batch affine normalisation (Montgomery's trick), NORM_E points per lane and
-// NORM_BS * NORM_E points per block (point g of group g / per lives at index
-// (g / per) * stride + g % per + first;
-// points of proofs with status[g / per] != 0 are skipped, identities map to (0, 0)):
-//   1. lane-local prefix products of its NORM_E z's (strided by NORM_BS, so
-//      every load/store is coalesced),
-//   2. Hillis-Steele prefix + suffix scans of the lane totals in LDS,
-//   3. ONE inversion per block (f_inv_gcd, branch-free),
-//   4. lane-local back-sweep: z_j^-1, then x z^-2, y z^-3.
-// ~9 products per point (the scans cost 16 / NORM_E per point).  Writes affine
-// Montgomery (aff, 16 words) and the canonical 64-byte BE encoding (be).
+// Batch affine normalisation (Montgomery's trick), E points per lane and ONE
+// inversion per lane (point g of group g / per lives at index
+// (g / per) * stride + g % per + first; points of proofs with status[g / per]
+// != 0 are skipped, identities map to (0, 0)).  Lane l of wave w owns the points
+// (w E + j) 64 + l, j < E (every load / store coalesced across the wave):
+//   1. forward: the exclusive prefix product of the lane's z's, stored in the
+//      point's own affine slot (scratch until step 2 overwrites it);
+//   2. one inversion of the lane's product (f_inv_gcd, branch-free);
+//   3. back-sweep: z_j^-1 = inv * prefix_j, inv *= z_j; then x z^-2, y z^-3.
+// 7 products per point + one inversion per E points, no LDS and no barrier
+// (round 5; the round-1..4 kernel scanned the lanes' totals across a 256-lane
+// block in LDS and inverted once per block: ~13 products per point, 8 barrier
+// levels and one lane inverting while the block waited -- 0.05-0.11 of the MAD
+// peak beside the com chain).  Writes affine Montgomery (aff, 16 words) and,
+// when be != nullptr, the canonical 64-byte BE encoding.
 template <int E>
 __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, int stride, int first,
                                                           const int32_t* __restrict__ status,
                                                           const uint32_t* __restrict__ jac, uint32_t* __restrict__ aff,
                                                           uint8_t* __restrict__ be) {
-  __shared__ uint32_t pre[NORM_BS * 8], suf[NORM_BS * 8];
-  __shared__ uint32_t invs[8];
-  const int t = threadIdx.x;
-  const size_t g0 = (size_t)blockIdx.x * NORM_BS * E + t;
+  const size_t gid = (size_t)blockIdx.x * NORM_BS + threadIdx.x;
+  const size_t g0 = (gid >> 6) * (size_t)E * 64 + (gid & 63);
+  auto slot = [&](int j) {
+    const size_t g = g0 + (size_t)j * 64;
+    return (g / per) * stride + g % per + first;
+  };
   // liveness is read ONCE per point: status may change while this kernel runs
   // (k_sig_exclude on the batch-check stream marks excluded proofs NOT_RUN), and
-  // the prefix products and the back-sweep must skip exactly the same points
+  // the forward pass and the back-sweep must skip exactly the same points
   uint32_t livem = 0;
 #pragma unroll
   for (int j = 0; j < E; j++) {
-    const size_t g = g0 + (size_t)j * NORM_BS;
+    const size_t g = g0 + (size_t)j * 64;
     if (g < (size_t)total && !(status && status[g / per] != 0)) livem |= 1u << j;
   }
-  auto zload = [&](int j, Fp& z) -> bool {  // z of point j (1 if absent/skipped/identity); live?
-    const size_t g = g0 + (size_t)j * NORM_BS;
-    z = f_one<FpP>();
-    if (!((livem >> j) & 1u)) return false;
-    Fp zz;
-    load_fp(jac + ((g / per) * stride + g % per + first) * 24 + 16, zz);
-    if (!f_is_zero(zz)) z = zz;
-    return true;
-  };
-  Fp acc[E];
-  {
-    Fp run = f_one<FpP>();
+  if (!livem) return;
+  Fp run = f_one<FpP>();
 #pragma unroll
-    for (int j = 0; j < E; j++) {
-      Fp z;
-      zload(j, z);
-      run = j ? fp_mul(run, z) : z;
-      acc[j] = run;
-    }
+  for (int j = 0; j < E; j++) {
+    if (!((livem >> j) & 1u)) continue;
+    const size_t q = slot(j);
+    store_fp(aff + q * 16, run);  // exclusive prefix (scratch)
+    Fp z;
+    load_fp(jac + q * 24 + 16, z);
+    if (!f_is_zero(z)) run = fp_mul(run, z);
   }
-  const Fp tot = acc[E - 1];
-  store_fp(pre + t * 8, tot);
-  store_fp(suf + t * 8, tot);
-  __syncthreads();
-  // inclusive scans (Hillis-Steele): pre_t = T_0..T_t, suf_t = T_t..T_255
-  Fp a = tot, c = tot;
-  for (int off = 1; off < NORM_BS; off <<= 1) {
-    Fp o1, o2;
-    const bool h1 = t >= off, h2 = t + off < NORM_BS;
-    if (h1) load_fp(pre + (t - off) * 8, o1);
-    if (h2) load_fp(suf + (t + off) * 8, o2);
-    __syncthreads();
-    if (h1) {
-      a = fp_mul(a, o1);
-      store_fp(pre + t * 8, a);
-    }
-    if (h2) {
-      c = fp_mul(c, o2);
-      store_fp(suf + t * 8, c);
-    }
-    __syncthreads();
-  }
-  if (t == 0) store_fp(invs, nl_fp_inv(c));  // suf_0 = product of all
-  __syncthreads();
-  // inverse of this lane's total: inv(all) * pre_{t-1} * suf_{t+1}
-  Fp inv;
-  load_fp(invs, inv);
-  {
-    Fp o;
-    if (t > 0) {
-      load_fp(pre + (t - 1) * 8, o);
-      inv = fp_mul(inv, o);
-    }
-    if (t + 1 < NORM_BS) {
-      load_fp(suf + (t + 1) * 8, o);
-      inv = fp_mul(inv, o);
-    }
-  }
+  Fp inv = nl_fp_inv(run);
 #pragma unroll
   for (int j = E - 1; j >= 0; j--) {
-    Fp z;
-    const bool live = zload(j, z);
-    Fp zi = j ? fp_mul(inv, acc[j - 1]) : inv;  // z_j^-1
-    if (j) inv = fp_mul(inv, z);
-    if (!live) continue;
-    const size_t gg = g0 + (size_t)j * NORM_BS;
-    const size_t g = (gg / per) * stride + gg % per + first;
-    const G1J p = load_g1j(jac + g * 24);
+    if (!((livem >> j) & 1u)) continue;
+    const size_t q = slot(j);
+    const G1J p = load_g1j(jac + q * 24);
+    Fp pre;
+    load_fp(aff + q * 16, pre);
     G1A r;
     if (f_is_zero(p.z)) {
       r.x = f_zero<FpP>();
       r.y = f_zero<FpP>();
     } else {
-      Fp zi2 = fp_sqr(zi);
+      const Fp zi = fp_mul(inv, pre);
+      inv = fp_mul(inv, p.z);
+      const Fp zi2 = fp_sqr(zi);
       r.x = fp_mul(p.x, zi2);
       r.y = fp_mul(fp_mul(p.y, zi2), zi);
     }
-    store_g1a(aff + g * 16, r);
-    if (be) store_point_be(be + g * 64, r);
+    store_g1a(aff + q * 16, r);
+    if (be) store_point_be(be + q * 64, r);
   }
 }
 
@@ -1424,6 +1419,32 @@ __global__ void __launch_bounds__(64) k_rlc_finalize(int B, const uint32_t* __re
 // a group whose partial combination is the identity accepts its proofs (their
 // deferred IPA structural verdicts become final, as in k_rlc_finalize), the
 // proofs of the other groups are appended to `next` (the next round's list)
+// the per-caller-batch combination (RlcDev::G > 1): slot j of group j / gs; group g
+// closes when its MSM sum (x0-free columns included as extras) + column Q's product
+// is the identity -> its proofs take their exact-phase verdicts, gflag[g] = 1; a
+// failing group's proofs stay undecided (the group test runs over those batches only)
+__global__ void __launch_bounds__(256) k_rlc_finalize_groups(int slots, int gs, int NC, const int32_t* __restrict__ sel,
+                                                             const uint32_t* __restrict__ msm_out,
+                                                             const uint32_t* __restrict__ qfix,
+                                                             const int32_t* __restrict__ excl,
+                                                             int32_t* __restrict__ status,
+                                                             const int32_t* __restrict__ ipa_flag,
+                                                             int32_t* __restrict__ gflag, int32_t* __restrict__ flag) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= slots) return;
+  const int b = sel[j], g = j / gs;
+  if (b < 0) return;
+  if (excl && excl[b] && status[b] == 0) status[b] = FTS_E_NOT_RUN;
+  G1J e = load_g1j(msm_out + (size_t)g * 24);
+  add_inl(e, load_g1j(qfix + ((size_t)g * NC + NC - 1) * 24));
+  const bool pass = g1j_is_identity(e);
+  if (j % gs == 0) {  // a group's first slot is a real proof (padding trails)
+    gflag[g] = pass ? 1 : 0;
+    if (!pass) *flag = 0;
+  }
+  if (pass && status[b] == 0 && ipa_flag[b] != 0) status[b] = ipa_flag[b];
+}
+
 __global__ void __launch_bounds__(256) k_rlc_group_final(int slots, int gs, const int32_t* __restrict__ sel,
                                                          const uint32_t* __restrict__ msm_out,
                                                          int32_t* __restrict__ status,
@@ -1450,10 +1471,13 @@ __global__ void __launch_bounds__(256) k_rlc_group_final(int slots, int gs, cons
   } while (0)
 static void launch_normalize(size_t total, int per, int stride, int first, const int32_t* status, const uint32_t* jac,
                              uint32_t* aff, uint8_t* be, hipStream_t s) {
+  // lanes: one per E points, rounded to whole waves (E * 64 points per wave)
   if (total >= NORM_BIG)
-    FTS_LAUNCH(k_rp_normalize<8>, (total + 7) / 8, NORM_BS, s, (int)total, per, stride, first, status, jac, aff, be);
+    FTS_LAUNCH(k_rp_normalize<16>, (total + 16 * 64 - 1) / (16 * 64) * 64, NORM_BS, s, (int)total, per, stride, first,
+               status, jac, aff, be);
   else
-    FTS_LAUNCH(k_rp_normalize<4>, (total + 3) / 4, NORM_BS, s, (int)total, per, stride, first, status, jac, aff, be);
+    FTS_LAUNCH(k_rp_normalize<4>, (total + 4 * 64 - 1) / (4 * 64) * 64, NORM_BS, s, (int)total, per, stride, first,
+               status, jac, aff, be);
 }
 
 
@@ -1504,6 +1528,9 @@ void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalar
                 int stage = 0);
 void launch_msm_small(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra,
                       int nextra, hipStream_t s, Timeline* tl);
+void launch_msm_sort(const MsmPlan& p, const uint32_t* scalars, hipStream_t s, Timeline* tl);
+void launch_msm_reduce(const MsmPlan& p, const uint32_t* points, const uint32_t* extra, int nextra, uint32_t* scratch,
+                       hipStream_t s, hipStream_t s_extra, Timeline* tl);
 
 // Whole range-proof pipeline up to the batch verdict (flag): exact per-proof
 // phase (everything that is hashed: challenges, H'_i, com, x0) and the
@@ -1546,19 +1573,47 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     tl->mark("k_rlc_prep", s3, (double)B * (3 * k + 33));
     (void)hipEventRecord(d.ev_coef, s3);
   };
-  auto rlc_rest = [&]() {
+  const bool grouped = r.G > 1;
+  // presorted: the MSM's sort already ran on s3 (d.rlc_fork == 3); only its
+  // accumulation and reduction are left
+  auto rlc_rest = [&](bool presorted = false) {
+    auto msm = [&](const uint32_t* extra, int nextra) {
+      if (presorted) launch_msm_reduce(r.plan, d.pts, extra, nextra, r.msm_scratch, s3, s4, tl);
+      else launch_msm(r.plan, d.pts, r.msc, extra, nextra, r.msm_scratch, s3, s4, tl);
+    };
     tl->fork(s, s4);   // k_rp_powers' vectors
     tl->fork(s3, s4);  // the weights
+    if (grouped) {
+      // per caller batch: the x0-free column sums and products of every group (slot Q
+      // left as the identity: zero words), the MSM's extras with stride NC
+      (void)hipMemsetAsync(r.gfix, 0, (size_t)r.G * NC * 96, s4);
+      hipLaunchKernelGGL(k_rlc_columns, dim3(NC - 1, r.G), dim3(256), 0, s4, B, n, k, r.gs, 0, r.sel, d.ch, r.coef,
+                         d.ypow, d.svec, d.zvec, r.gcol);
+      tl->mark("k_rlc_columns", s4, (double)B * 4 * n);
+      FTS_LAUNCH(k_rlc_fixed, (size_t)r.G * (NC - 1) * FB_NW, RF_ITEMS * FB_NW, s4, n, r.G, 0, NC - 1, r.gcol, tables,
+                 r.gfix);
+      tl->mark("k_rlc_fixed", s4, (double)r.G * (NC - 1) * (FB_NW * 3 + (FB_NW - 1) * COST_ADD));
+      msm(r.gfix, NC);
+      return;
+    }
     hipLaunchKernelGGL(k_rlc_columns, dim3(NC - 1, 1), dim3(256), 0, s4, B, n, k, B, 0, (const int32_t*)nullptr, d.ch,
                        r.coef, d.ypow, d.svec, d.zvec, r.colsum);
     tl->mark("k_rlc_columns", s4, (double)B * 4 * n);
     FTS_LAUNCH(k_rlc_fixed, (size_t)(NC - 1) * FB_NW, RF_ITEMS * FB_NW, s4, n, 1, 0, NC - 1, r.colsum, tables, r.fixed);
     tl->mark("k_rlc_fixed", s4, (double)(NC - 1) * (FB_NW * 3 + (FB_NW - 1) * COST_ADD));
-    launch_msm(r.plan, d.pts, r.msc, r.fixed, NC - 1, r.msm_scratch, s3, s4, tl);
+    msm(r.fixed, NC - 1);
   };
   if (!d.rlc_fork) rlc_prep();
   FTS_LAUNCH(k_rp_powers, B * (n >> std::min(PW_LC, k)), 64, s, B, n, k, d.status, d.ch, d.ypow, d.svec, d.zvec);
   tl->mark("k_rp_powers", s, (double)B * (3.0 * n + 2.0 * k));
+  // d.rlc_fork == 3 (work path): the weights and the MSM's counting sort (memory /
+  // LDS work, no long chains) beside the fixed-base launch; its accumulation waits
+  // for that launch (after it, below), so the MSM chain starts sorted
+  const bool early_sort = d.rlc_fork == 3 && !d.com_fixed && d.ev_fx;
+  if (early_sort) {
+    rlc_prep();
+    launch_msm_sort(r.plan, r.msc, s3, tl);
+  }
   auto rlc_side = [&]() {
     if (d.rlc_fork) rlc_prep();
     rlc_rest();
@@ -1571,22 +1626,28 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     tl->mark("k_rp_fixed_all", s, (double)B * (2.0 * n + 2.0) * COST_FBW_FRESH);
     if (d.rlc_fork) rlc_side();
     launch_normalize(nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be, s);
-    tl->mark("k_rp_normalize", s, (double)nhp * (2.0 * 8.0 / NORM_E + 9.0));
+    tl->mark("k_rp_normalize", s, (double)nhp * (7.0 + COST_INV / NORM_E));
     tl->fork(s2, s);
     hipLaunchKernelGGL(k_rp_com_tree, dim3((B + CT_PROOFS - 1) / CT_PROOFS), dim3(CT_LANES * CT_PROOFS), 0, s, B, n,
-                       k, d.status, d.pts, d.terms, d.hpj);
-    tl->mark("k_rp_com_sum", s, (double)B * (com_fx_slots(n) + 1) * COST_ADD);
+                       k, d.status, d.pts, d.terms, d.hpj, d.hpa, d.hp_be);
+    tl->mark("k_rp_com_sum", s, (double)B * ((com_fx_slots(n) + 1) * COST_ADD + COST_NORM1));
   } else {
     FTS_LAUNCH(k_rp_fixed_exact, (size_t)B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, wtables, d.hpj,
                d.terms);
     tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FBW_FRESH);
-    if (d.rlc_fork) rlc_side();
+    if (early_sort) {
+      (void)hipEventRecord(d.ev_fx, s);
+      (void)hipStreamWaitEvent(s3, d.ev_fx, 0);
+      rlc_rest(true);
+    } else if (d.rlc_fork) {
+      rlc_side();
+    }
     // H'_i -> affine + BE bytes (x0 transcript) on the side stream: the S / com
     // chain on s works on the Jacobian H' (k_rp_hsum_chunks) and does not wait
     // for it; com is normalised after com_var
     tl->fork(s, s2);
     launch_normalize(nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be, s2);
-    tl->mark("k_rp_normalize", s2, (double)nhp * (2.0 * 8.0 / NORM_E + 9.0));
+    tl->mark("k_rp_normalize", s2, (double)nhp * (7.0 + COST_INV / NORM_E));
     if (d.x0_mid) {
       // x0 prefix on the side stream: the H' records and the shared template
       // (cb1 of the message's blocks) do not depend on com, so they are hashed
@@ -1604,11 +1665,9 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     tl->mark("k_rp_hsum_join", s, (double)B * (nch - 1) * (HS_CHUNK * COST_DBL + COST_ADD));
     // scratch: [0, B*HS_SCRATCH) Horner chunks of S, then the 2B lanes' affine tables
     FTS_LAUNCH(k_rp_com_var, 2 * B, g_chain_bs, s, B, n, k, d.status, d.pts, d.ch, d.scratch,
-               d.scratch + (size_t)B * HS_SCRATCH, d.terms, d.hpj);
-    tl->mark("k_rp_com_var", s, (double)B * 2 * (COST_STRAUS2_CTAB + 2.5 * COST_ADD));
+               d.scratch + (size_t)B * HS_SCRATCH, d.terms, d.hpj, d.hpa, d.hp_be);
+    tl->mark("k_rp_com_var", s, (double)B * (2 * (COST_STRAUS2_CTAB + 2.5 * COST_ADD) + COST_NORM1));
   }
-  launch_normalize(B, 1, n + 1, n, d.status, d.hpj, d.hpa, d.hp_be, s);
-  tl->mark("k_rp_normalize_com", s, (double)B * (2.0 * 8.0 / NORM_E + 9.0));
   const bool split = d.x0_mid != nullptr;
   // work path without the prefix split: the whole message needs the H' bytes of s2
   if (!d.com_fixed && !split) tl->fork(s2, s);
@@ -1622,6 +1681,18 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   // x0 tail: column Q (needs the weights of k_rlc_prep) and its product, then
   // the verdict once the MSM is in
   (void)hipStreamWaitEvent(s, d.ev_coef, 0);
+  if (grouped) {
+    hipLaunchKernelGGL(k_rlc_columns, dim3(1, r.G), dim3(256), 0, s, B, n, k, r.gs, NC - 1, r.sel, d.ch, r.coef,
+                       d.ypow, d.svec, d.zvec, r.gcol);
+    FTS_LAUNCH(k_rlc_fixed, (size_t)r.G * FB_NW, RF_ITEMS * FB_NW, s, n, r.G, NC - 1, 1, r.gcol, tables, r.gqfix);
+    tl->mark("k_rlc_q", s, (double)B + r.G * (FB_NW * 3 + (FB_NW - 1) * COST_ADD));
+    (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(r.flag), 1, 1, s);
+    tl->fork(s3, s);
+    FTS_LAUNCH(k_rlc_finalize_groups, (size_t)r.G * r.gs, 256, s, r.G * r.gs, r.gs, NC, r.sel, r.plan.out, r.gqfix,
+               d.excl, d.status, d.ipa_flag, r.gflag, r.flag);
+    tl->mark("k_rlc_finalize", s, 0);
+    return;
+  }
   {
     const int gsq = (B + RQ_PARTS - 1) / RQ_PARTS;  // proofs per partial sum
     hipLaunchKernelGGL(k_rlc_columns, dim3(1, RQ_PARTS), dim3(256), 0, s, B, n, k, gsq, NC - 1,

@@ -497,6 +497,13 @@ class StagedMsm:
         L.check("fts_msm_run", L.lib.fts_msm_run(self.pp._ctx, self._b, out))
         return out.raw
 
+    def points(self, lo=0, count=None):
+        """the staged points [lo, lo + count) as 64-byte X||Y BE (fts_msm_points)"""
+        count = self.n - lo if count is None else count
+        out = C.create_string_buffer(64 * max(1, count))
+        L.check("fts_msm_points", L.lib.fts_msm_points(self.pp._ctx, self._b, lo, count, out))
+        return out.raw[:64 * count]
+
     def timings(self):
         names = (C.c_char_p * 64)()
         ms = (C.c_float * 64)()

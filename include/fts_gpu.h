@@ -241,6 +241,9 @@ int fts_msm_run(fts_ctx* ctx, fts_msm_batch* b, uint8_t* out64);
  * context's fixed-base table, k32 / scalars32: n x 32-byte BE integers used mod r.  The
  * result of fts_msm_run is then (sum_i s_i k_i mod r) * ped1 (closed form for tests). */
 int fts_msm_stage_multiples(fts_ctx* ctx, size_t n, const uint8_t* k32, const uint8_t* scalars32, fts_msm_batch** out);
+/* the staged points [lo, lo + count) of b as 64-byte X||Y BE (identity = 64 zero bytes):
+ * the C3 CPU baseline runs its Pippenger over the same distinct points */
+int fts_msm_points(fts_ctx* ctx, const fts_msm_batch* b, size_t lo, size_t count, uint8_t* out64);
 /* per-kernel device time (ms) and algorithmic u32 MADs of b's last run */
 int fts_msm_timings(const fts_msm_batch* b, const char** names, float* ms, double* mads, int cap);
 void fts_msm_free(fts_msm_batch* b);

@@ -32,6 +32,10 @@
  *         the same, plus every proof's exact com (64 B) and x0 (32 B, BE) for
  *         parity checks at full batch size (zeros where the proof stopped earlier)
  *   void  cpu_batch_free(void* ctx)
+ *   int   cpu_msm_pippenger(const uint8_t* pts, const uint8_t* scs, size_t n, int threads, uint8_t* out64)
+ *         sum_i (k_i mod r) P_i with the batch's GLV Pippenger (msm_glv): the C3
+ *         CPU baseline (BASELINE.md "the build's C++ Pippenger"); pts as oracle_msm
+ *         (64-byte BE, NewG1FromBytes checks), scs 32-byte BE.  0, or -1 on a bad point
  * gens as in ref_verify.c: [G=ped1, H=ped2, P, Q, G_0..G_{n-1}, H_0..H_{n-1}].
  */
 #include "ref_verify.c"
@@ -835,4 +839,30 @@ int cpu_batch_verify_ex(void* ctx, int count, const uint8_t* coms, const uint8_t
 int cpu_batch_verify(void* ctx, int count, const uint8_t* coms, const uint8_t* const* ders, const size_t* lens,
                      int threads, int32_t* out) {
   return cpu_batch_verify_ex(ctx, count, coms, ders, lens, threads, out, NULL, NULL);
+}
+
+/* ------------------------------------------------ standalone MSM (config C3 baseline) */
+int cpu_msm_pippenger(const uint8_t* pts, const uint8_t* scs, size_t n, int threads, uint8_t* out64) {
+  init_consts();
+  aff* a = malloc(sizeof(aff) * (n ? n : 1));
+  uint8_t* inf = malloc(n ? n : 1);
+  fe* sc = malloc(sizeof(fe) * (n ? n : 1));
+  int bad = 0;
+  for (size_t i = 0; i < n; i++) {
+    g1 p;
+    if (!g1_from_bytes(pts + 64 * i, 64, &p)) {
+      bad = 1;
+      p.inf = 1;
+    }
+    inf[i] = (uint8_t)p.inf;
+    a[i].x = p.x;
+    a[i].y = p.y;
+    sc[i] = zr_red(be_to_fe(scs + 32 * i)); /* G1.Mul uses the scalar mod r */
+  }
+  g1j acc = msm_glv(a, inf, sc, n, threads);
+  g1_bytes(toaff(acc), out64);
+  free(a);
+  free(inf);
+  free(sc);
+  return bad ? -1 : 0;
 }

@@ -130,6 +130,8 @@ def _batch_lib():
                                               C.c_char_p]
         _blib.cpu_batch_verify_ex.restype = C.c_int
         _blib.cpu_batch_free.argtypes = [C.c_void_p]
+        _blib.cpu_msm_pippenger.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t, C.c_int, C.c_char_p]
+        _blib.cpu_msm_pippenger.restype = C.c_int
     return _blib
 
 
@@ -173,3 +175,13 @@ class CpuBatch:
 
     def __del__(self):
         self.close()
+
+
+def msm_pippenger(points64, scalars32, threads=1):
+    """sum (k_i mod r) P_i with oracle/c/cpu_batch.c's GLV Pippenger -> 64-byte BE result"""
+    n = len(points64) // 64
+    out = C.create_string_buffer(64)
+    rc = _batch_lib().cpu_msm_pippenger(points64, scalars32, n, threads, out)
+    if rc != 0:
+        raise ValueError("bad point")
+    return out.raw

@@ -166,3 +166,31 @@ def test_knob_gt_adapt_off(pp_raw):
         b.close()
     finally:
         pp.close()
+
+
+@pytest.mark.parametrize("sort", [0, 1])
+def test_knob_msm_sort(pp_raw, sort):
+    """FTS_MSM_SORT=0 forces the round-4 sort of the batch check's MSM (k_msm_digits'
+    device atomics + k_msm_scatter); 1 (default) the two-level counting sort
+    (k_rs_*).  A 768-proof rp32 pass (11,520 MSM points: the two-level sort's range)
+    with tampered proofs in it: the same exact verdicts either way, and the
+    timeline names the sort that ran"""
+    pp = _ctx(pp_raw, 32, FTS_MSM_SORT=sort, FTS_LANES=1, FTS_COM_FIXED_MAX=0)
+    try:
+        (b, want), = _tampered_batches(pp, 1, 768, 0x50A7 + sort)
+        got = b.verify(want_status=True)
+        assert (got == want).all(), np.nonzero(got != want)
+        names = set(b.timings())
+        if sort:
+            assert "k_rs_part" in names and "k_msm_digits" not in names, sorted(names)
+        else:
+            assert "k_msm_digits" in names and "k_rs_part" not in names, sorted(names)
+        # an honest batch closes the combination with either sort (no fallback)
+        vals = list(range(1, 769))
+        proofs, coms = pp.prove_range_batch_gpu(vals, [(7).to_bytes(32, "big")] * 768, seed=0x50A8)
+        st = pp.verify_range_proofs(proofs, coms)
+        assert not any(int(s) for s in st)
+        assert not any(k.startswith("fb:") for k in pp.last_timings()), sorted(pp.last_timings())
+        b.close()
+    finally:
+        pp.close()

@@ -106,7 +106,7 @@ def test_msm_2p20_linearity_and_identity(gpu_pp):
     assert got == bn.g1_bytes(bn.g1_msm([base[i % m] for i in range(lo, lo + 300)], a[sl]))
 
 
-@pytest.mark.parametrize("log", [8, 18])
+@pytest.mark.parametrize("log", [8, 18, 22])
 def test_msm_distinct_device_points_closed_form(gpu_pp, oracle_pp, log):
     """config C3 as SURVEY §8(d) specifies it: 2^log DISTINCT points k_i ped1 made on
     the device (fts_msm_stage_multiples), scalars above r included (used mod r):
@@ -122,19 +122,22 @@ def test_msm_distinct_device_points_closed_form(gpu_pp, oracle_pp, log):
     want = bn.g1_bytes(bn.g1_mul(ped1, sum(s * k for s, k in zip(ss, ks)) % bn.R))
     assert st.run() == want
     assert st.run() == want  # re-run on the resident inputs
+    # the staged points are the distinct k_i ped1 (fts_msm_points; a sample incl. both ends)
+    for i in sorted({0, n - 1} | {rng.randrange(n) for _ in range(6)}):
+        assert st.points(i, 1) == bn.g1_bytes(bn.g1_mul(ped1, ks[i] % bn.R)), i
     st.close()
     if log == 8:
         pts = [bn.g1_mul(ped1, k % bn.R) for k in ks]
         assert pp.msm(_pts(pts), _scs(ss)) == want
 
 
-def test_msm_block_local_sort_adversarial_2p18(gpu_pp):
-    """The block-local counting sort (msm.hip k_msm_lhist / k_msm_lscatter, used by
-    standalone MSMs from 2^18 points) on adversarial inputs: one scalar repeated by
-    an eighth of the points (one bucket per window holds 32k entries), zero
-    scalars, r - 1 and scalars >= r (used mod r), identity points, and -P right
-    after +P with the same scalar (the pair cancels); closed form
-    sum s_i c_i G with P_i = c_i G"""
+def test_msm_two_level_sort_adversarial_2p18(gpu_pp):
+    """The two-level counting sort (msm.hip k_rs_*: the sort of the batch check's
+    MSM and of standalone MSMs, round 5) on adversarial inputs: one scalar
+    repeated by an eighth of the points (one bucket per window holds 32k entries,
+    so one partition block sorts them all), zero scalars, r - 1 and scalars >= r
+    (used mod r), identity points, and -P right after +P with the same scalar
+    (the pair cancels); closed form sum s_i c_i G with P_i = c_i G"""
     pp = gpu_pp(64)
     n, m = 1 << 18, 1 << 16
     rng = random.Random(0x15A0)
@@ -163,4 +166,5 @@ def test_msm_block_local_sort_adversarial_2p18(gpu_pp):
     want = bn.g1_bytes(bn.g1_mul(bn.GEN, total % bn.R))
     st = pp.stage_msm(_pts(pts), _scs(scs))
     assert st.run() == want
+    assert "k_rs_part" in st.timings() and "k_msm_digits" not in st.timings(), sorted(st.timings())
     st.close()

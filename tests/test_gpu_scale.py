@@ -200,6 +200,10 @@ def test_one_bad_proof_in_coalesced_pass_group_test(pp_raw):
     per_proof = tb["fb:k_rp_terms_fixed"][1] / ((3 + 2 * 16) * 15 * 11 * 136)
     # the bad proof's round-1 group (256 proofs of its own batch), not the pass (4,096)
     assert 1 <= round(per_proof) <= 256, per_proof
+    # the per-caller-batch combination (FTS_MAIN_GROUPS, default on): the group test's
+    # grouped sums cover the bad proof's own batch (512 proofs), not the whole pass
+    grouped = tb["fb:k_rlc_group_columns"][1] / (4 * 16 * 136)
+    assert round(grouped) == m, grouped
     for b in batches:
         b.close()
     pp.close()
@@ -374,4 +378,76 @@ def test_group_test_adaptive_dense_exact_verdicts(pp_raw):
     assert "fb:k_rlc_group_cols" in n4 and "fb:k_rlc_group_columns" not in n4, n4
     other.close()
     batch.close()
+    pp.close()
+
+
+def test_dense_and_sparse_batches_in_one_pass(pp_raw):
+    """one coalesced pass holding a DENSE caller batch (its last
+    failure had many bad proofs: its group test starts at groups of 8) and a SPARSE
+    one (one bad proof: groups of 256).  Both group tests upload their MSM window
+    tables back to back with no sync between them (rp_group_fallback), from
+    separate pinned slots; every verdict must be the oracle's, and the per-proof
+    stage must see only the failing small groups and the sparse batch's one 256-group
+    -- not every proof of the pass."""
+    import os
+    import threading
+
+    import fts_gpu
+
+    old = os.environ.get("FTS_LANES")
+    os.environ["FTS_LANES"] = "1"
+    try:
+        pp = fts_gpu.PublicParams(pp_raw, bit_length=16, device=0)
+    finally:
+        if old is None:
+            del os.environ["FTS_LANES"]
+        else:
+            os.environ["FTS_LANES"] = old
+    from oracle import pp as oppm
+    opp = oppm.load_pp(pp_raw).with_bit_length(16)
+    rng = random.Random(0xD5A5)
+    m = 512
+
+    def make(seed, bad):
+        vals = [rng.getrandbits(16) for _ in range(m)]
+        bfs = [rng.randrange(bn.R).to_bytes(32, "big") for _ in range(m)]
+        proofs, coms = pp.prove_range_batch_gpu(vals, bfs, seed=seed)
+        exp = [0] * m
+        for i in bad:
+            r = zkat.RangeProof.deserialize(proofs[i])
+            if i % 2:
+                r.data.T1 = bn.g1_add(r.data.T1, bn.GEN)
+            else:
+                j = rng.randrange(4)
+                r.ipa.L[j] = bn.g1_add(r.ipa.L[j], bn.GEN)
+            proofs[i] = r.serialize()
+            err = zkat.rp_verify(bn.g1_from_bytes(coms[i]), opp.ped[1:], opp.left, opp.right, opp.P, opp.Q,
+                                 opp.rounds, 16, zkat.RangeProof.deserialize(proofs[i]))
+            assert err is not None
+            exp[i] = fts_gpu.FTS_E_RP_INVALID if "IPA" not in err else fts_gpu.FTS_E_IPA_INVALID
+        return pp.stage_range_proofs(proofs, coms), exp
+
+    dense, exp_d = make(9500, range(7, m, 32))   # 16 bad proofs: both 256-groups fail
+    sparse, exp_s = make(9600, [301])
+    assert [int(x) for x in dense.verify()] == exp_d  # alone: marks the batch dense
+    blocker = pp.stage_range_proofs(*pp.prove_range_batch_gpu([1] * 64, [(9).to_bytes(32, "big")] * 64, seed=1))
+    out = {}
+
+    def run(name, b):
+        out[name] = ([int(x) for x in b.verify()], b.merged(), _raw_timing_names(b))
+    th = [threading.Thread(target=blocker.verify), threading.Thread(target=run, args=("d", dense)),
+          threading.Thread(target=run, args=("s", sparse))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert out["d"][0] == exp_d
+    assert out["s"][0] == exp_s
+    assert out["d"][1] == 2 and out["s"][1] == 2, (out["d"][1], out["s"][1])  # one coalesced pass
+    names, work = out["s"][2]
+    assert "fb:k_rlc_group_columns" in names and "fb:k_rlc_group_cols" in names, names  # both group sizes ran
+    per_proof = work["fb:k_rp_terms_fixed"] / ((3 + 2 * 16) * 15 * 11 * 136)
+    assert 1 <= round(per_proof) <= 16 * 8 + 256, per_proof
+    for b in (dense, sparse, blocker):
+        b.close()
     pp.close()

@@ -43,9 +43,11 @@ def test_bn254_hash_to_zr_reduction_is_pinned():
     assert (dg % bn254.R).to_bytes(32, "big") == idemix.parse_ipk(raw)["hash"]
 
 
-def test_fp256bn_ipk_hash_and_curve():
-    # the validator's own fixture is an FP256BN key: same hash rule mod that curve's order
-    raw = _raw("fp256bn_validator", "IssuerPublicKey")
+@pytest.mark.parametrize("d", ["fp256bn_validator", "fp256bn_crypto"])
+def test_fp256bn_ipk_hash_and_curve(d):
+    # the validator's and the crypto package's fixtures are FP256BN keys: same hash
+    # rule mod that curve's order (two more independent HashToZr / Zr.Bytes pins)
+    raw = _raw(d, "IssuerPublicKey")
     f = idemix.pb_fields(raw)
     h = [v for k, _, v in f if k == 10][0]
     dg = int.from_bytes(hashlib.sha256(idemix.ipk_hash_input(raw)).digest(), "big")
@@ -135,3 +137,26 @@ def test_golden_nym_vectors(curve):
         except idemix.NymError as e:
             got = str(e)
         assert got == want, case["name"]
+
+
+def test_issuer_key_fixtures_are_the_references():
+    """the fixtures are the reference's files byte for byte (sha256 of the copies)"""
+    want = {
+        "bn254_tokengen": "701cea34637564a4921583877f4d19455f5a6cb28be8dc2023261637dea6569a",
+        "bn254_charlie": "765568cad59f56ea169a8651b99e40bc4a2157700cdf9f06c3b13fd8412f8792",
+        "fp256bn_validator": "74964ae62e43da2e41f12f43b1558317374748913f8dc4cb93d55a273141e1fa",
+        "fp256bn_crypto": "bb1dc7f3d81ca64ce510e724743336b0307d6349440c7801de39ac3c9d32cb38",
+    }
+    for d, h in want.items():
+        assert hashlib.sha256(_raw(d, "IssuerPublicKey")).hexdigest() == h, d
+
+
+def test_fp256bn_crypto_key_digest_reduction():
+    """nogh/v1/crypto's key: its SHA-256 digest exceeds BN254's r but not FP256BN's,
+    so the stored hash also tells the two curves' reductions apart"""
+    raw = _raw("fp256bn_crypto", "IssuerPublicKey")
+    h = [v for k, _, v in idemix.pb_fields(raw) if k == 10][0]
+    dg = int.from_bytes(hashlib.sha256(idemix.ipk_hash_input(raw)).digest(), "big")
+    assert bn254.R <= dg < FP256BN_R
+    assert (dg % bn254.R).to_bytes(32, "big") != h
+    assert dg.to_bytes(32, "big") == h

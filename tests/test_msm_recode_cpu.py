@@ -1,5 +1,5 @@
-"""CPU: the block-local MSM sort (msm.hip k_msm_split / k_msm_lhist /
-k_msm_lscatter) reads window w's signed digit of a GLV half k as a plain bit
+"""CPU: the two-level MSM sort (msm.hip rs_point_digits, used by k_rs_hist /
+k_rs_scatter) reads window w's signed digit of a GLV half k as a plain bit
 field of k + C, C = sum_w (2^(width_w-1) - 1) 2^off_w.  Check that this gives
 exactly k_msm_digits' sequential recoding (d = bits + carry; carry' = d > half;
 d -= 2^width if carry') for the balanced window layouts msm_layout_groups

@@ -101,3 +101,24 @@ def test_cpu_batch_rp_golden(built, oracle_pp):
         assert got == [RP_CODE[c["expect"]] for c in mix], bits
         assert nfb < len(mix) or all(c["expect"] for c in sel), bits
         cb.close()
+
+
+def test_cpu_pippenger_matches_term_by_term():
+    """oracle/c/cpu_batch.c cpu_msm_pippenger (the C3 CPU baseline): the same group
+    element as the term-by-term G1.Mul + Add oracle, with identities, scalars >= r
+    and a window-count edge (n spans the c = 4 .. 11 window choices)"""
+    import random
+
+    from oracle import bn254 as bn, cref
+    rng = random.Random(0xC3C3)
+    for n in (1, 2, 33, 257, 3000):
+        pts = [bn.g1_mul(bn.GEN, rng.randrange(1, bn.R)) for _ in range(n)]
+        ks = [rng.getrandbits(256) for _ in range(n)]
+        if n > 2:
+            pts[1] = None          # identity
+            ks[2] = bn.R           # = 0 mod r
+        pb = b"".join(bn.g1_bytes(p) for p in pts)
+        kb = b"".join(k.to_bytes(32, "big") for k in ks)
+        assert cref.msm_pippenger(pb, kb, threads=3) == cref.msm(pb, kb, threads=3), n
+    with pytest.raises(ValueError):
+        cref.msm_pippenger(b"\x01" * 64, bytes(32))
