@@ -192,7 +192,9 @@ struct RpBatchDev {
   int rlc_fork = 1;    // batch check's stream forks after the fixed-base products (1) or after the challenges (0);
                        //    fts_api.cpp picks 0 on the latency path, 1 on the work path (FTS_RLC_FORK=2)
   hipEvent_t ev_coef = nullptr;  // recorded on the check's stream after k_rlc_prep (column Q on s waits for it)
-  hipEvent_t ev_fx = nullptr;    // rlc_fork 3: recorded on s after the fixed-base launch (the MSM accumulation waits)
+  hipEvent_t ev_fx = nullptr;    // recorded on s after the fixed-base launch (rlc_fork 3: the MSM accumulation waits;
+                                 // FTS_FX_SERIAL: the next pass's fixed-base launch waits)
+  hipEvent_t fx_wait = nullptr;  // FTS_FX_SERIAL: s waits for it right before the fixed-base launch
   uint32_t* x0_mid = nullptr;    // [B][8] SHA-256 midstate of the x0 prefix (work path; nullptr: one-piece hash)
   int32_t* excl = nullptr;       // [B] optional: 1 = left out of the batch check (set by the pre_rlc hook), NOT_RUN
 };

@@ -438,6 +438,7 @@ struct fts_ctx {
   // of one lone 4,096-proof pass per free lane); an idle device starts at once
   size_t gather_target = 16384;
   int gather_us = 1000;
+  int idle_gather_us = 0;  // FTS_IDLE_GATHER_US: the same window when the device is idle (0: start at once)
   // passes of up to com_fixed_max proofs compute com on the latency path (fixed-base
   // groups, rp_kernels.hip k_rp_fixed_all), larger ones on the work path (Horner +
   // joint GLV chains): the same group element either way
@@ -462,10 +463,17 @@ struct fts_ctx {
   // FTS_MSM_SORT: the MSMs' two-level counting sort (msm.hip k_rs_*; 0: k_msm_digits'
   // device atomics + k_msm_scatter, the round-4 batch-check sort, for A/B)
   int msm_sort = 1;
-  // FTS_MAIN_GROUPS: a coalesced pass checks one random linear combination PER CALLER
+  // FTS_MAIN_GROUPS=1: a coalesced pass checks one random linear combination PER CALLER
   // BATCH (a G-group MSM + per-group column sums), so a bad proof's fallback covers
-  // its own batch only; 0: one combination over the pass (rounds 1-4)
-  int main_groups = 1;
+  // its own batch only.  Default 0 (one combination over the pass): the grouped MSM's
+  // extra windows and per-group bucket reductions cost 10-17 % of the clean 512-step
+  // rate (4.96 -> 4.47 M rp64/s, gpurun_out/r05b) for +10 % with one bad proof per pass
+  int main_groups = 0;
+  // FTS_FX_SERIAL: passes' fixed-base launches run one at a time across the lanes
+  // (device-side event chain under fx_mu), staggering concurrent passes
+  int fx_serial = 0;
+  std::mutex fx_mu;
+  hipEvent_t fx_last = nullptr;  // the fixed-base event of the pass enqueued last
   // FTS_RLC_FORK: the batch check forks after the fixed-base products (1) or after the
   // challenges (0); 2 (default): after the challenges on the latency path (a lone small
   // pass: its MSM chain is the critical path, 3.16 -> 2.98 ms per 4,096-proof batch),
@@ -610,12 +618,15 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_LANES")) nl = std::max(1, std::min(16, atoi(e)));
   if (const char* e = getenv("FTS_COALESCE_MAX")) c->coalesce_max = (size_t)std::max(0L, atol(e));
   c->gather_target = c->coalesce_max / 2;
+  if (const char* e = getenv("FTS_GATHER_TARGET")) c->gather_target = (size_t)std::max(1L, atol(e));
   if (const char* e = getenv("FTS_GATHER_US")) c->gather_us = std::max(0, atoi(e));
+  if (const char* e = getenv("FTS_IDLE_GATHER_US")) c->idle_gather_us = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_COM_FIXED_MAX")) c->com_fixed_max = (size_t)std::max(0L, atol(e));
-  if (const char* e = getenv("FTS_RLC_FORK")) c->rlc_fork = std::max(0, std::min(3, atoi(e)));
+  if (const char* e = getenv("FTS_RLC_FORK")) c->rlc_fork = std::max(0, std::min(4, atoi(e)));
   if (const char* e = getenv("FTS_X0_SPLIT")) c->x0_split = atoi(e) != 0;
   if (const char* e = getenv("FTS_MSM_SORT")) c->msm_sort = atoi(e) != 0;
   if (const char* e = getenv("FTS_MAIN_GROUPS")) c->main_groups = atoi(e) != 0;
+  if (const char* e = getenv("FTS_FX_SERIAL")) c->fx_serial = atoi(e) != 0;
   if (const char* e = getenv("FTS_GT1")) c->gt1 = std::max(8, std::min(1024, atoi(e)));
   if (const char* e = getenv("FTS_GT2_MIN")) c->gt2_min = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_GT_ADAPT")) c->gt_adapt = atoi(e) != 0;
@@ -1325,7 +1336,7 @@ static int rp_enqueue(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc
   d.pre_rlc_arg = pre_rlc_arg;
   // 2 (adaptive): 0 on the latency path, 1 on the work path; 3: 0 on the latency
   // path, on the work path the MSM's sort beside the fixed-base launch
-  d.rlc_fork = c->rlc_fork == 2 ? (d.com_fixed ? 0 : 1) : c->rlc_fork == 3 ? (d.com_fixed ? 0 : 3) : c->rlc_fork;
+  d.rlc_fork = c->rlc_fork == 2 ? (d.com_fixed ? 0 : 1) : c->rlc_fork >= 3 ? (d.com_fixed ? 0 : c->rlc_fork) : c->rlc_fork;
   d.ev_coef = L.ev_c;
   d.ev_fx = L.ev_d;
   // x0 prefix beside the com chain on the work path only: on the latency path,
@@ -1349,7 +1360,16 @@ static int rp_enqueue(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc
   HIP_OK(hipMemcpyAsync(r.key, L.pin->key, sizeof L.pin->key, hipMemcpyHostToDevice, L.s));
   P.t_prep = now_ms();
   L.tl.begin(L.s);
-  launch_rp_batch(d, r, c->d_tables, c->d_wtables, c->d_x0const, c->d_x0tmpl, L.s, L.s2, L.s3, L.s4, &L.tl);
+  if (c->fx_serial) {
+    // the wait, this pass's fixed-base launch and its event record are enqueued in
+    // one critical section, so the chain of events follows the enqueue order
+    std::lock_guard<std::mutex> g(c->fx_mu);
+    d.fx_wait = c->fx_last;
+    launch_rp_batch(d, r, c->d_tables, c->d_wtables, c->d_x0const, c->d_x0tmpl, L.s, L.s2, L.s3, L.s4, &L.tl);
+    c->fx_last = d.ev_fx;
+  } else {
+    launch_rp_batch(d, r, c->d_tables, c->d_wtables, c->d_x0const, c->d_x0tmpl, L.s, L.s2, L.s3, L.s4, &L.tl);
+  }
   between();
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(&L.pin->flag, r.flag, 4, hipMemcpyDeviceToHost, L.s));
@@ -1607,7 +1627,7 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
       continue;
     }
     const bool device_busy = c->free_lanes.size() < c->lanes.size();
-    const int wait_us = device_busy ? c->gather_us : 0;
+    const int wait_us = device_busy ? c->gather_us : c->idle_gather_us;
     if (wait_us > 0 && c->rp_pending.front() == &me && c->pending_proofs < c->gather_target) {
       const auto deadline = me.arrived + std::chrono::microseconds(wait_us);
       if (std::chrono::steady_clock::now() < deadline) {

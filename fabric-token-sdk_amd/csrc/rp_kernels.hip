@@ -55,9 +55,9 @@ template <int E>
 __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, int stride, int first,
                                                           const int32_t* __restrict__ status,
                                                           const uint32_t* __restrict__ jac, uint32_t* __restrict__ aff,
-                                                          uint8_t* __restrict__ be);
+                                                          uint8_t* __restrict__ be, uint8_t* __restrict__ x0msgs);
 static void launch_normalize(size_t total, int per, int stride, int first, const int32_t* status, const uint32_t* jac,
-                             uint32_t* aff, uint8_t* be, hipStream_t s);
+                             uint32_t* aff, uint8_t* be, hipStream_t s, uint8_t* x0msgs = nullptr);
 // Jacobian -> affine (Montgomery, 16 words) and BE bytes of ONE point by its own
 // inversion (identity -> (0, 0)): com at the end of its chain (round 5: instead of
 // a k_rp_normalize launch of one point per proof on the critical path)
@@ -643,11 +643,31 @@ __global__ void __launch_bounds__(CT_LANES * CT_PROOFS) k_rp_com_tree(int B, int
 // levels and one lane inverting while the block waited -- 0.05-0.11 of the MAD
 // peak beside the com chain).  Writes affine Montgomery (aff, 16 words) and,
 // when be != nullptr, the canonical 64-byte BE encoding.
+// x0 record r of a proof's message (ipa.go:200-213): hex(H'_r) + "||" at byte
+// 8 + 130 r of its slot (bytes < 64 cb0 sit at their own offset), from the point's
+// 16 BE words; 33 stores (4-byte ones where the record's parity allows)
+FTS_DEV void x0_put_record(uint8_t* msg, uint32_t r, const uint32_t pw[16]) {
+  uint8_t* d = msg + 8u + 130u * r;
+  auto hx = [&](int i) -> uint32_t { return hex2((pw[i >> 2] >> (24 - 8 * (i & 3))) & 0xffu); };  // byte i
+  if ((r & 1u) == 0) {  // 4-byte aligned
+    uint32_t* d4 = reinterpret_cast<uint32_t*>(d);
+#pragma unroll
+    for (int i = 0; i < 32; i++) d4[i] = hx(2 * i) | (hx(2 * i + 1) << 16);
+    reinterpret_cast<uint16_t*>(d)[64] = 0x7c7cu;
+  } else {  // 2 mod 4: one 2-byte store, 31 aligned words, then hex(byte 63) "||"
+    reinterpret_cast<uint16_t*>(d)[0] = (uint16_t)hx(0);
+    uint32_t* d4 = reinterpret_cast<uint32_t*>(d + 2);
+#pragma unroll
+    for (int i = 0; i < 31; i++) d4[i] = hx(2 * i + 1) | (hx(2 * i + 2) << 16);
+    d4[31] = hx(63) | (0x7c7cu << 16);
+  }
+}
+
 template <int E>
 __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, int stride, int first,
                                                           const int32_t* __restrict__ status,
                                                           const uint32_t* __restrict__ jac, uint32_t* __restrict__ aff,
-                                                          uint8_t* __restrict__ be) {
+                                                          uint8_t* __restrict__ be, uint8_t* __restrict__ x0msgs) {
   const size_t gid = (size_t)blockIdx.x * NORM_BS + threadIdx.x;
   const size_t g0 = (gid >> 6) * (size_t)E * 64 + (gid & 63);
   auto slot = [&](int j) {
@@ -694,7 +714,22 @@ __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, in
       r.y = fp_mul(fp_mul(p.y, zi2), zi);
     }
     store_g1a(aff + q * 16, r);
-    if (be) store_point_be(be + q * 64, r);
+    if (be || x0msgs) {
+      uint32_t pw[16];
+      g1_mont_to_be_words(r.x, r.y, pw);
+      if (be) {
+        uint4* d = reinterpret_cast<uint4*>(be + q * 64);
+#pragma unroll
+        for (int w = 0; w < 4; w++)
+          d[w] = make_uint4(__builtin_bswap32(pw[4 * w]), __builtin_bswap32(pw[4 * w + 1]),
+                            __builtin_bswap32(pw[4 * w + 2]), __builtin_bswap32(pw[4 * w + 3]));
+      }
+      // the x0 prefix's hex record of this point (H'_r of proof g / per)
+      if (x0msgs) {
+        const size_t g = g0 + (size_t)j * 64;
+        x0_put_record(x0msgs + (g / per) * x0_var_bytes(per), (uint32_t)(g % per), pw);
+      }
+    }
   }
 }
 
@@ -768,8 +803,10 @@ __global__ void __launch_bounds__(64 * X0_PPB) k_rp_x0_build(int B, int n, const
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int b = blockIdx.x * X0_PPB + wv;
   const bool live = b < B && status[b] == 0;  // uniform per wave
-  uint4* L4 = x0_lds + (size_t)wv * (var / 16u);
-  uint8_t* Lb = reinterpret_cast<uint8_t*>(L4);
+  // part 1 assembles only bytes >= 64 cb0 (its LDS region starts there)
+  const uint32_t lbase = part == 1 ? 64u * cb0 : 0u;
+  uint4* L4 = x0_lds + (size_t)wv * ((var - lbase) / 16u);
+  uint8_t* Lb = reinterpret_cast<uint8_t*>(L4) - lbase;
   const uint32_t c_off = x0_const_off(n), c_end = x0_const_end(n);
   const uint8_t* hp = hp_be + (size_t)b * (n + 1) * 64;
   // hex records: H'_0..H'_{n-1} (records 0..n-1) and com (record 2n+1, no "||")
@@ -825,10 +862,33 @@ __global__ void __launch_bounds__(64 * X0_PPB) k_rp_x0_build(int B, int n, const
   if (!live) return;
   uint4* dst = reinterpret_cast<uint4*>(msgs + (size_t)b * var);
   const uint32_t c_lo = part == 1 ? 4u * cb0 : 0u, c_hi = part == 0 ? 4u * cb0 : var / 16u;
-  for (uint32_t c = lane + c_lo; c < c_hi; c += 64) dst[c] = L4[c];
+  for (uint32_t c = lane + c_lo; c < c_hi; c += 64) dst[c] = L4[c - lbase / 16u];
 }
-inline size_t x0_build_lds(int n) { return (size_t)X0_PPB * x0_var_bytes(n); }
+// LDS bytes per proof of a part: part 1 assembles only the blocks after the template
+inline uint32_t x0_part_lds_base(int n, int part) { return part == 1 ? 64u * x0_cb0(n) : 0u; }
+inline size_t x0_build_lds(int n, int part = 2) {
+  return (size_t)X0_PPB * (x0_var_bytes(n) - x0_part_lds_base(n, part));
+}
 inline unsigned x0_build_grid(int B) { return (unsigned)((B + X0_PPB - 1) / X0_PPB); }
+
+// The bytes of part 0 of the x0 message that are not H' records (the DER header
+// and the constant bytes sharing block cb0 - 1 with the last record), lane per
+// proof; the records themselves are written by k_rp_normalize (x0msgs) as it
+// normalises H' (round 5: a separate LDS-assembled build of part 0 waited for CU
+// slots beside the com chain, and the x0 prefix it feeds became the pass's
+// critical path, 0.4 -> 5.2 ms)
+__global__ void __launch_bounds__(256) k_rp_x0_hdr(int B, int n, const int32_t* __restrict__ status,
+                                                   const uint8_t* __restrict__ x0_const, uint8_t* __restrict__ msgs) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B || status[b] != 0) return;
+  uint8_t* msg = msgs + (size_t)b * x0_var_bytes(n);
+  const uint32_t A = x0_array_len(n), L = A + 42u;
+  const uint8_t h[8] = {0x30, 0x82, (uint8_t)(L >> 8), (uint8_t)L, 0x04, 0x82, (uint8_t)(A >> 8), (uint8_t)A};
+#pragma unroll
+  for (int i = 0; i < 8; i++) msg[i] = h[i];
+  const uint32_t c_off = x0_const_off(n), c_end = 64u * x0_cb0(n);
+  for (uint32_t pos = c_off; pos < c_end; pos++) msg[pos] = x0_const[pos - c_off];
+}
 
 // SHA-256 over message blocks [b0, b1) of each proof's x0 message: b0 == 0
 // starts from the initial state, else from mid[b]; b1 == every block finishes
@@ -1470,14 +1530,14 @@ __global__ void __launch_bounds__(256) k_rlc_group_final(int slots, int gs, cons
     if (nt_) hipLaunchKernelGGL(kern, dim3((unsigned)((nt_ + (bs)-1) / (bs))), dim3(bs), 0, stream, __VA_ARGS__); \
   } while (0)
 static void launch_normalize(size_t total, int per, int stride, int first, const int32_t* status, const uint32_t* jac,
-                             uint32_t* aff, uint8_t* be, hipStream_t s) {
+                             uint32_t* aff, uint8_t* be, hipStream_t s, uint8_t* x0msgs) {
   // lanes: one per E points, rounded to whole waves (E * 64 points per wave)
   if (total >= NORM_BIG)
     FTS_LAUNCH(k_rp_normalize<16>, (total + 16 * 64 - 1) / (16 * 64) * 64, NORM_BS, s, (int)total, per, stride, first,
-               status, jac, aff, be);
+               status, jac, aff, be, x0msgs);
   else
     FTS_LAUNCH(k_rp_normalize<4>, (total + 4 * 64 - 1) / (4 * 64) * 64, NORM_BS, s, (int)total, per, stride, first,
-               status, jac, aff, be);
+               status, jac, aff, be, x0msgs);
 }
 
 
@@ -1609,10 +1669,23 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   // d.rlc_fork == 3 (work path): the weights and the MSM's counting sort (memory /
   // LDS work, no long chains) beside the fixed-base launch; its accumulation waits
   // for that launch (after it, below), so the MSM chain starts sorted
-  const bool early_sort = d.rlc_fork == 3 && !d.com_fixed && d.ev_fx;
+  // The weights run on s itself, ahead of the fixed-base launch (0.2 ms alone; on
+  // s3 beside that launch the 320 blocks starved for 6 ms), then the sort on s3.
+  // d.rlc_fork == 4: the whole sort on s itself (~0.6 ms alone, ahead of the
+  // fixed-base launch): beside the chain kernels the sort's small latency-bound
+  // launches starved (k_rs_hist 0.04 -> 2.2 ms in a 20-batch burst, round 5), and
+  // beside the fixed-base launch too (3: k_msm_split 6 ms)
+  const bool early_sort = (d.rlc_fork == 3 || d.rlc_fork == 4) && !d.com_fixed && d.ev_fx && !d.pre_rlc;
   if (early_sort) {
-    rlc_prep();
-    launch_msm_sort(r.plan, r.msc, s3, tl);
+    FTS_LAUNCH(k_rlc_prep, B, g_lat_bs, s, B, n, k, d.status, d.excl, d.ipa_flag, d.sc, d.ch, r.key, r.msc, r.coef);
+    tl->mark("k_rlc_prep", s, (double)B * (3 * k + 33));
+    (void)hipEventRecord(d.ev_coef, s);
+    if (d.rlc_fork == 4) {
+      launch_msm_sort(r.plan, r.msc, s, tl);
+    } else {
+      tl->fork(s, s3);
+      launch_msm_sort(r.plan, r.msc, s3, tl);
+    }
   }
   auto rlc_side = [&]() {
     if (d.rlc_fork) rlc_prep();
@@ -1620,10 +1693,15 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   };
   if (!d.rlc_fork) rlc_side();
   // exact per-proof phase on s
+  // FTS_FX_SERIAL: one pass's fixed-base launch at a time across the lanes (the
+  // previous pass's launch has ended), so the next pass's launch overlaps this
+  // pass's latency-bound chain instead of its own twin
+  if (d.fx_wait) (void)hipStreamWaitEvent(s, d.fx_wait, 0);
   if (d.com_fixed) {
     FTS_LAUNCH(k_rp_fixed_all, (size_t)B * (2 * n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, d.zvec, wtables,
                d.hpj, d.terms);
     tl->mark("k_rp_fixed_all", s, (double)B * (2.0 * n + 2.0) * COST_FBW_FRESH);
+    if (d.ev_fx) (void)hipEventRecord(d.ev_fx, s);
     if (d.rlc_fork) rlc_side();
     launch_normalize(nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be, s);
     tl->mark("k_rp_normalize", s, (double)nhp * (7.0 + COST_INV / NORM_E));
@@ -1635,8 +1713,8 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     FTS_LAUNCH(k_rp_fixed_exact, (size_t)B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, wtables, d.hpj,
                d.terms);
     tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FBW_FRESH);
+    if (d.ev_fx) (void)hipEventRecord(d.ev_fx, s);
     if (early_sort) {
-      (void)hipEventRecord(d.ev_fx, s);
       (void)hipStreamWaitEvent(s3, d.ev_fx, 0);
       rlc_rest(true);
     } else if (d.rlc_fork) {
@@ -1646,15 +1724,15 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     // chain on s works on the Jacobian H' (k_rp_hsum_chunks) and does not wait
     // for it; com is normalised after com_var
     tl->fork(s, s2);
-    launch_normalize(nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be, s2);
+    // with the x0 prefix split, the normalisation also writes the H' hex records of
+    // the x0 messages (k_rp_x0_hdr the header and constant bytes around them)
+    if (d.x0_mid) FTS_LAUNCH(k_rp_x0_hdr, B, 256, s2, B, n, d.status, x0_const, d.x0_msgs);
+    launch_normalize(nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be, s2, d.x0_mid ? d.x0_msgs : nullptr);
     tl->mark("k_rp_normalize", s2, (double)nhp * (7.0 + COST_INV / NORM_E));
     if (d.x0_mid) {
       // x0 prefix on the side stream: the H' records and the shared template
       // (cb1 of the message's blocks) do not depend on com, so they are hashed
       // beside the S / com chain; only the suffix waits for com
-      hipLaunchKernelGGL(k_rp_x0_build, dim3(x0_build_grid(B)), dim3(64 * X0_PPB), x0_build_lds(n), s2, B, n, d.status, d.hp_be, x0_const,
-                         d.sc, d.x0_msgs, 0);
-      tl->mark("k_rp_x0_build", s2, 0);
       FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s2, B, n, k, d.status, d.x0_msgs, x0_tmpl, 0u, x0_cb1(n), d.x0_mid, d.ch);
       tl->mark("k_rp_x0_prefix", s2, 0);
     }
@@ -1671,8 +1749,8 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   const bool split = d.x0_mid != nullptr;
   // work path without the prefix split: the whole message needs the H' bytes of s2
   if (!d.com_fixed && !split) tl->fork(s2, s);
-  hipLaunchKernelGGL(k_rp_x0_build, dim3(x0_build_grid(B)), dim3(64 * X0_PPB), x0_build_lds(n), s, B, n, d.status, d.hp_be, x0_const, d.sc,
-                     d.x0_msgs, split ? 1 : 2);
+  hipLaunchKernelGGL(k_rp_x0_build, dim3(x0_build_grid(B)), dim3(64 * X0_PPB), x0_build_lds(n, split ? 1 : 2), s, B,
+                     n, d.status, d.hp_be, x0_const, d.sc, d.x0_msgs, split ? 1 : 2);
   tl->mark(split ? "k_rp_x0_build_tail" : "k_rp_x0_build", s, 0);
   if (split) tl->fork(s2, s);  // the prefix's midstate
   FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s, B, n, k, d.status, d.x0_msgs, x0_tmpl, split ? x0_cb1(n) : 0u, 0xffffffffu,

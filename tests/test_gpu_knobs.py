@@ -5,8 +5,9 @@ path, the same exact intermediates (com, H'_i, x0: ipa.go:200-213).
 
 Knobs covered elsewhere: FTS_LANES, FTS_COM_FIXED_MAX (test_gpu_rp.py,
 test_gpu_scale.py), FTS_GT1 / FTS_GT2_MIN / FTS_GT_ADAPT (test_gpu_scale.py),
-FTS_NYM_TILE (test_idemix.py).  Here: FTS_RLC_FORK, FTS_X0_SPLIT,
-FTS_COALESCE_MAX, FTS_GATHER_US, FTS_GT_ADAPT=0."""
+FTS_NYM_TILE (test_idemix.py), FTS_MAIN_GROUPS (test_gpu_scale.py).  Here:
+FTS_RLC_FORK, FTS_X0_SPLIT, FTS_COALESCE_MAX, FTS_GATHER_US, FTS_GT_ADAPT=0,
+FTS_MSM_SORT."""
 import json
 import os
 import random
@@ -56,11 +57,12 @@ def _golden_check(pp, bits, work_path):
             assert com.hex() == c["com"] and [h.hex() for h in hp] == c["hprime"] and vals[7] == int(c["x0"])
 
 
-@pytest.mark.parametrize("fork", [0, 1])
+@pytest.mark.parametrize("fork", [0, 1, 3])
 @pytest.mark.parametrize("work_path", [False, True])
 def test_knob_rlc_fork(pp_raw, fork, work_path):
-    """FTS_RLC_FORK=0/1 (default 2 = adaptive): the batch check forks after the
-    challenges or after the fixed-base products, on both com paths"""
+    """FTS_RLC_FORK=0/1/3 (default 2 = adaptive): the batch check forks after the
+    challenges or after the fixed-base products, or (3, work path) sorts its MSM
+    beside the fixed-base launch and accumulates after it; on both com paths"""
     env = dict(FTS_RLC_FORK=fork, FTS_LANES=1)
     if work_path:
         env["FTS_COM_FIXED_MAX"] = 0

@@ -143,26 +143,30 @@ def test_coalesced_batches_keep_their_verdicts(pp_raw):
     pp.close()
 
 
-def test_one_bad_proof_in_coalesced_pass_group_test(pp_raw):
+@pytest.mark.parametrize("main_groups", [0, 1])
+def test_one_bad_proof_in_coalesced_pass_group_test(pp_raw, main_groups):
     """SURVEY Appendix B fallback: one tampered proof inside a coalesced pass of 8
     caller batches.  The failed batch check is narrowed by group tests (groups never
     straddle two caller batches) so only a handful of proofs -- all of the bad
     proof's own batch -- get the per-proof final equations; every verdict equals
-    the reference's (rangecorrectness.go:141-160)."""
+    the reference's (rangecorrectness.go:141-160).  FTS_MAIN_GROUPS=1: the pass
+    checks one combination per caller batch, so the group test covers the bad
+    proof's batch only; 0 (default): the whole pass."""
     import os
     import threading
 
     import fts_gpu
 
-    old = os.environ.get("FTS_LANES")
-    os.environ["FTS_LANES"] = "1"
+    saved = {k: os.environ.get(k) for k in ("FTS_LANES", "FTS_MAIN_GROUPS")}
+    os.environ.update(FTS_LANES="1", FTS_MAIN_GROUPS=str(main_groups))
     try:
         pp = fts_gpu.PublicParams(pp_raw, bit_length=16, device=0)
     finally:
-        if old is None:
-            del os.environ["FTS_LANES"]
-        else:
-            os.environ["FTS_LANES"] = old
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     rng = random.Random(0xB15EC7)
     m, nb, bad_batch, bad_idx = 512, 8, 3, 333
     batches, expect = [], []
@@ -200,10 +204,10 @@ def test_one_bad_proof_in_coalesced_pass_group_test(pp_raw):
     per_proof = tb["fb:k_rp_terms_fixed"][1] / ((3 + 2 * 16) * 15 * 11 * 136)
     # the bad proof's round-1 group (256 proofs of its own batch), not the pass (4,096)
     assert 1 <= round(per_proof) <= 256, per_proof
-    # the per-caller-batch combination (FTS_MAIN_GROUPS, default on): the group test's
-    # grouped sums cover the bad proof's own batch (512 proofs), not the whole pass
+    # the group test's grouped sums: the bad proof's own batch (512 proofs) with the
+    # per-caller-batch combination, else the whole pass
     grouped = tb["fb:k_rlc_group_columns"][1] / (4 * 16 * 136)
-    assert round(grouped) == m, grouped
+    assert round(grouped) == (m if main_groups else m * merged[bad_batch]), (grouped, merged[bad_batch])
     for b in batches:
         b.close()
     pp.close()
