@@ -532,6 +532,10 @@ def main():
             "fallback": _fallback_share(kt, R, pass_ms),
             "prove_s": round(prove_s, 2),
             "library": _lib_record(),
+            # fixed-base tables resident in HBM: 16-bit windows for the 2n + 6 public
+            # generators, 20- or 22-bit (the default where the memory allows) for H_i, K, P
+            "table_bytes": pp.table_bytes,
+            "wide_table_bits": 22 if pp.table_bytes > (2 * n + 6) * (32 << 20) + (n + 2) * 13 * (1 << 19) * 64 else 20,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:

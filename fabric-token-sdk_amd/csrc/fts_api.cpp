@@ -41,10 +41,11 @@ void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32
 void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const uint32_t* wtables,
                      const uint8_t* x0_const, const uint8_t* x0_tmpl, hipStream_t s, hipStream_t s2, hipStream_t s3,
                      hipStream_t s4,
-                     Timeline* tl);
-void launch_build_wide_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s);
-size_t wide_build_scratch_bytes(int nb);
-size_t fbw_words_per_base();
+                     Timeline* tl, int wbits);
+void launch_build_wide_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s,
+                              int wbits);
+size_t wide_build_scratch_bytes(int nb, int wbits);
+size_t fbw_words_per_base(int wbits);
 void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, const int32_t* sel, int nsel, hipStream_t s,
                         Timeline* tl);
 void launch_rlc_group_test(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const MsmPlan& p,
@@ -405,7 +406,10 @@ struct fts_ctx {
   PublicParams pp;
   int n = 0, k = 0;
   uint32_t* d_tables = nullptr;
-  uint32_t* d_wtables = nullptr;  // 20-bit tables of [H_0 .. H_{n-1}, K, P] (k_rp_fixed_exact)
+  uint32_t* d_wtables = nullptr;  // wide tables of [H_0 .. H_{n-1}, K, P] (k_rp_fixed_exact)
+  // their window width: 22 bits (12 additions per product, 1.5 GiB per base) when the
+  // device has the memory at context creation, else 20 (13, 436 MiB); FTS_WIDE_BITS
+  int wbits = 20;
   uint8_t* d_x0const = nullptr;
   uint8_t* d_x0tmpl = nullptr;  // x0 message blocks [x0_cb0, x0_cb1): shared by every proof
   size_t table_bytes = 0;
@@ -694,9 +698,23 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   for (int b0 = 0; b0 < nb; b0 += chunk)
     launch_build_tables(d_bases + (size_t)b0 * 16, std::min(chunk, nb - b0), c->d_tables + (size_t)b0 * fb_words_per_base(),
                         d_scr, s0);
-  // 20-bit tables of the per-proof bases H_i, K, P (same build, wider windows)
+  // wide tables of the per-proof bases H_i, K, P (same build, wider windows):
+  // 22-bit windows (one mixed addition fewer per product: -8 % of the pass's
+  // largest kernel) when the free HBM holds them with room to spare for the lanes'
+  // workspace (~7 GB each at n = 64) and other contexts; else 20-bit
   {
     const int nw = n + 2;
+    {
+      int wb = 20;
+      if (const char* e = getenv("FTS_WIDE_BITS")) {
+        wb = atoi(e) == 22 ? 22 : 20;
+      } else {
+        size_t fr = 0, tot = 0;
+        const size_t need22 = (size_t)nw * fbw_words_per_base(22) * 4;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > need22 + ((size_t)128 << 30)) wb = 22;
+      }
+      c->wbits = wb;
+    }
     std::vector<uint32_t> hw((size_t)nw * 16, 0);
     for (int i = 0; i < nw; i++) {
       const int src = i < n ? n + i : (i == n ? 2 * n + 4 : 2 * n + 2);  // H_i, K, P in `bases`
@@ -704,9 +722,10 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
     }
     uint32_t* d_wb = nullptr;
     uint32_t* d_wscr = nullptr;
-    const int wchunk = std::min(nw, 4);
-    if (hipMalloc(&c->d_wtables, (size_t)nw * fbw_words_per_base() * 4) != hipSuccess ||
-        hipMalloc(&d_wb, hw.size() * 4) != hipSuccess || hipMalloc(&d_wscr, wide_build_scratch_bytes(wchunk)) != hipSuccess) {
+    const int wchunk = std::min(nw, c->wbits == 22 ? 1 : 4);  // bounds the Jacobian build scratch (2.4 / 1.6 GB)
+    if (hipMalloc(&c->d_wtables, (size_t)nw * fbw_words_per_base(c->wbits) * 4) != hipSuccess ||
+        hipMalloc(&d_wb, hw.size() * 4) != hipSuccess ||
+        hipMalloc(&d_wscr, wide_build_scratch_bytes(wchunk, c->wbits)) != hipSuccess) {
       if (d_wb) hipFree(d_wb);
       hipFree(d_bases);
       hipFree(d_scr);
@@ -715,7 +734,8 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
     hipMemcpyAsync(d_wb, hw.data(), hw.size() * 4, hipMemcpyHostToDevice, s0);
     for (int b0 = 0; b0 < nw; b0 += wchunk)
       launch_build_wide_tables(d_wb + (size_t)b0 * 16, std::min(wchunk, nw - b0),
-                               c->d_wtables + (size_t)b0 * fbw_words_per_base(), d_wscr, s0);
+                               c->d_wtables + (size_t)b0 * fbw_words_per_base(c->wbits), d_wscr, s0, c->wbits);
+    c->table_bytes += (size_t)nw * fbw_words_per_base(c->wbits) * 4;
     hipError_t we = hipStreamSynchronize(s0);
     hipFree(d_wb);
     hipFree(d_wscr);
@@ -1365,10 +1385,12 @@ static int rp_enqueue(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc
     // one critical section, so the chain of events follows the enqueue order
     std::lock_guard<std::mutex> g(c->fx_mu);
     d.fx_wait = c->fx_last;
-    launch_rp_batch(d, r, c->d_tables, c->d_wtables, c->d_x0const, c->d_x0tmpl, L.s, L.s2, L.s3, L.s4, &L.tl);
+    launch_rp_batch(d, r, c->d_tables, c->d_wtables, c->d_x0const, c->d_x0tmpl, L.s, L.s2, L.s3, L.s4, &L.tl,
+                    c->wbits);
     c->fx_last = d.ev_fx;
   } else {
-    launch_rp_batch(d, r, c->d_tables, c->d_wtables, c->d_x0const, c->d_x0tmpl, L.s, L.s2, L.s3, L.s4, &L.tl);
+    launch_rp_batch(d, r, c->d_tables, c->d_wtables, c->d_x0const, c->d_x0tmpl, L.s, L.s2, L.s3, L.s4, &L.tl,
+                    c->wbits);
   }
   between();
   HIP_OK(hipGetLastError());

@@ -365,6 +365,7 @@ inline __host__ __device__ int com_nterms(int n) { return COM_NTERMS; }
 // lane per (proof, item): items 0..n-1: H'_i = y^-i H_i (-> hpj[b][i]);
 // n: z K; n+1: -delta P (-> terms[b][0..1])
 // wtables: the 20-bit tables of [H_0 .. H_{n-1}, K, P] (FbWide layout)
+template <int W>
 __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, const int32_t* __restrict__ status,
                                                           const uint32_t* __restrict__ sc, const uint32_t* __restrict__ ch,
                                                           const uint32_t* __restrict__ ypow,
@@ -385,13 +386,13 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, c
   if (t < n) {
     Fr yp;
     load_f(ypow + ((size_t)t * B + b) * 8, yp);
-    tab = wtables + (size_t)t * FbWide::WORDS_PER_BASE;
+    tab = wtables + (size_t)t * FbCfg<W>::WORDS_PER_BASE;
     sk = fr_canon(yp);
     out = hpj + ((size_t)b * (n + 1) + t) * 24;
   } else if (t == n) {
     Fr z;
     load_f(C + CH_Z * 8, z);
-    tab = wtables + (size_t)n * FbWide::WORDS_PER_BASE;
+    tab = wtables + (size_t)n * FbCfg<W>::WORDS_PER_BASE;
     sk = fr_canon(z);
     out = terms + ((size_t)b * COM_NTERMS + 0) * 24;
   } else {
@@ -400,10 +401,10 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, c
     Fr nd = f_neg(d);
 #pragma unroll
     for (int q = 0; q < 8; q++) sk.v[q] = nd.v[q];
-    tab = wtables + (size_t)(n + 1) * FbWide::WORDS_PER_BASE;
+    tab = wtables + (size_t)(n + 1) * FbCfg<W>::WORDS_PER_BASE;
     out = terms + ((size_t)b * COM_NTERMS + 1) * 24;
   }
-  G1J r = fb_mul_w<FBW_W>(tab, sk);
+  G1J r = fb_mul_w<W>(tab, sk);
   store_g1j(out, r);
 }
 
@@ -534,6 +535,7 @@ inline __host__ __device__ int com_fx_slots(int n) { return n + 4; }
 // the same table), one fixed-base product per lane: items i < n: H'_i = y^-i H_i
 // -> hpj[b][i]; items n + i: Z_i = (z^2 2^i y^-i) H_i -> terms[b][i]; item 2n:
 // z K -> terms[b][n]; item 2n + 1: -delta P -> terms[b][n + 1]
+template <int W>
 __global__ void __launch_bounds__(64, 4) k_rp_fixed_all(int B, int n, int k, const int32_t* __restrict__ status,
                                                         const uint32_t* __restrict__ sc, const uint32_t* __restrict__ ch,
                                                         const uint32_t* __restrict__ ypow,
@@ -562,7 +564,7 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_all(int B, int n, int k, con
 #pragma unroll
     for (int q = 0; q < 8; q++) sk.v[q] = nd.v[q];
   }
-  const G1J r = fb_mul_w<FBW_W>(wtables + (size_t)base * FbWide::WORDS_PER_BASE, sk);
+  const G1J r = fb_mul_w<W>(wtables + (size_t)base * FbCfg<W>::WORDS_PER_BASE, sk);
   uint32_t* out = t < n ? hpj + ((size_t)b * (n + 1) + t) * 24 : terms + ((size_t)b * com_fx_slots(n) + base) * 24;
   store_g1j(out, r);
 }
@@ -1550,7 +1552,9 @@ size_t rp_scratch_words(int B, int n, int k) {
 size_t rp_terms_words(int B, int n, int k) { return (size_t)B * rp_nterms(n, k) * 24; }
 
 size_t fb_words_per_base() { return FB_WORDS_PER_BASE; }
-size_t fbw_words_per_base() { return FbWide::WORDS_PER_BASE; }
+// the per-proof bases' wide tables: 20-bit windows (13 per scalar, 436 MiB per base)
+// or 22-bit (12, 1.5 GiB per base) where the device has the memory (fts_api.cpp)
+size_t fbw_words_per_base(int wbits) { return wbits == 22 ? FbCfg<22>::WORDS_PER_BASE : FbWide::WORDS_PER_BASE; }
 template <int W>
 static size_t build_scratch_bytes(int nb) {
   using C = FbCfg<W>;
@@ -1558,7 +1562,9 @@ static size_t build_scratch_bytes(int nb) {
   return nbw * 24 * 4 + nbw * (C::S + C::L) * 24 * 4 + nbw * C::E * 24 * 4;
 }
 size_t table_build_scratch_bytes(int nb) { return build_scratch_bytes<FB_W>(nb); }
-size_t wide_build_scratch_bytes(int nb) { return build_scratch_bytes<FBW_W>(nb); }
+size_t wide_build_scratch_bytes(int nb, int wbits) {
+  return wbits == 22 ? build_scratch_bytes<22>(nb) : build_scratch_bytes<FBW_W>(nb);
+}
 // tables: nb * WORDS_PER_BASE words; scratch: build_scratch_bytes<W>(nb)
 template <int W>
 static void build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s) {
@@ -1577,8 +1583,10 @@ static void build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32
 void launch_build_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s) {
   build_tables<FB_W>(bases, nb, tables, scratch, s);
 }
-void launch_build_wide_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s) {
-  build_tables<FBW_W>(bases, nb, tables, scratch, s);
+void launch_build_wide_tables(const uint32_t* bases, int nb, uint32_t* tables, uint32_t* scratch, hipStream_t s,
+                              int wbits) {
+  if (wbits == 22) build_tables<22>(bases, nb, tables, scratch, s);
+  else build_tables<FBW_W>(bases, nb, tables, scratch, s);
 }
 
 // ev_stage (optional): recorded on s after the counting sort (stage 1) or the bucket
@@ -1600,7 +1608,9 @@ void launch_msm_reduce(const MsmPlan& p, const uint32_t* points, const uint32_t*
 // (weights, x0-free columns, MSM), which needs only the challenges.
 void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const uint32_t* wtables,
                      const uint8_t* x0_const, const uint8_t* x0_tmpl, hipStream_t s, hipStream_t s2, hipStream_t s3,
-                     hipStream_t s4, Timeline* tl) {
+                     hipStream_t s4, Timeline* tl, int wbits) {
+  // fixed-base products over the wide tables: 12 (20-bit) or 11 (22-bit) additions each
+  const double cost_fbw = wbits == 22 ? 11.0 * COST_MADD : COST_FBW_FRESH;
   const int B = d.B, n = d.n, k = d.k, NC = rlc_ncols(n);
   if (!B) return;
   if (d.excl) (void)hipMemsetAsync(d.excl, 0, (size_t)B * 4, s);
@@ -1698,9 +1708,13 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   // pass's latency-bound chain instead of its own twin
   if (d.fx_wait) (void)hipStreamWaitEvent(s, d.fx_wait, 0);
   if (d.com_fixed) {
-    FTS_LAUNCH(k_rp_fixed_all, (size_t)B * (2 * n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, d.zvec, wtables,
-               d.hpj, d.terms);
-    tl->mark("k_rp_fixed_all", s, (double)B * (2.0 * n + 2.0) * COST_FBW_FRESH);
+    if (wbits == 22)
+      FTS_LAUNCH(k_rp_fixed_all<22>, (size_t)B * (2 * n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, d.zvec,
+                 wtables, d.hpj, d.terms);
+    else
+      FTS_LAUNCH(k_rp_fixed_all<FBW_W>, (size_t)B * (2 * n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, d.zvec,
+                 wtables, d.hpj, d.terms);
+    tl->mark("k_rp_fixed_all", s, (double)B * (2.0 * n + 2.0) * cost_fbw);
     if (d.ev_fx) (void)hipEventRecord(d.ev_fx, s);
     if (d.rlc_fork) rlc_side();
     launch_normalize(nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be, s);
@@ -1710,9 +1724,13 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
                        k, d.status, d.pts, d.terms, d.hpj, d.hpa, d.hp_be);
     tl->mark("k_rp_com_sum", s, (double)B * ((com_fx_slots(n) + 1) * COST_ADD + COST_NORM1));
   } else {
-    FTS_LAUNCH(k_rp_fixed_exact, (size_t)B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, wtables, d.hpj,
-               d.terms);
-    tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * COST_FBW_FRESH);
+    if (wbits == 22)
+      FTS_LAUNCH(k_rp_fixed_exact<22>, (size_t)B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, wtables,
+                 d.hpj, d.terms);
+    else
+      FTS_LAUNCH(k_rp_fixed_exact<FBW_W>, (size_t)B * (n + 2), 64, s, B, n, k, d.status, d.sc, d.ch, d.ypow, wtables,
+                 d.hpj, d.terms);
+    tl->mark("k_rp_fixed_exact", s, (double)B * (n + 2) * cost_fbw);
     if (d.ev_fx) (void)hipEventRecord(d.ev_fx, s);
     if (early_sort) {
       (void)hipStreamWaitEvent(s3, d.ev_fx, 0);

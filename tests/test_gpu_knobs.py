@@ -57,12 +57,13 @@ def _golden_check(pp, bits, work_path):
             assert com.hex() == c["com"] and [h.hex() for h in hp] == c["hprime"] and vals[7] == int(c["x0"])
 
 
-@pytest.mark.parametrize("fork", [0, 1, 3])
+@pytest.mark.parametrize("fork", [0, 1, 3, 4])
 @pytest.mark.parametrize("work_path", [False, True])
 def test_knob_rlc_fork(pp_raw, fork, work_path):
-    """FTS_RLC_FORK=0/1/3 (default 2 = adaptive): the batch check forks after the
-    challenges or after the fixed-base products, or (3, work path) sorts its MSM
-    beside the fixed-base launch and accumulates after it; on both com paths"""
+    """FTS_RLC_FORK=0/1/3/4 (default 2 = adaptive): the batch check forks after the
+    challenges or after the fixed-base products, or (work path) sorts its MSM
+    beside (3) or ahead of (4) the fixed-base launch and accumulates after it;
+    on both com paths"""
     env = dict(FTS_RLC_FORK=fork, FTS_LANES=1)
     if work_path:
         env["FTS_COM_FIXED_MAX"] = 0
@@ -194,5 +195,24 @@ def test_knob_msm_sort(pp_raw, sort):
         assert not any(int(s) for s in st)
         assert not any(k.startswith("fb:") for k in pp.last_timings()), sorted(pp.last_timings())
         b.close()
+    finally:
+        pp.close()
+
+
+@pytest.mark.parametrize("wbits", [20, 22])
+@pytest.mark.parametrize("work_path", [False, True])
+def test_knob_wide_bits(pp_raw, wbits, work_path):
+    """FTS_WIDE_BITS=20/22: the per-proof bases' fixed-base tables with 20- or
+    22-bit windows (the default picks 22 when the free HBM holds them): the same
+    H'_i, com and x0 bytes and verdicts on both com paths; table_bytes follows"""
+    env = dict(FTS_WIDE_BITS=wbits, FTS_LANES=1)
+    if work_path:
+        env["FTS_COM_FIXED_MAX"] = 0
+    pp = _ctx(pp_raw, 32, **env)
+    try:
+        # 16-bit tables of the 2n + 6 bases (32 MiB each) + the n + 2 wide ones
+        wide = (32 + 2) * (13 * (1 << 19) if wbits == 20 else 12 * (1 << 21)) * 64
+        assert pp.table_bytes == (2 * 32 + 6) * 32 * (1 << 20) + wide, pp.table_bytes
+        _golden_check(pp, 32, work_path)
     finally:
         pp.close()

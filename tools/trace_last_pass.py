@@ -7,7 +7,7 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
-             r["Kernel_Name"].split("(")[0].replace("fts::", "").split("<")[0], r["Queue_Id"],
+             r["Kernel_Name"].split("(")[0].replace("fts::", "").replace("void ", "").split("<")[0], r["Queue_Id"],
              int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])) for r in rows)
 fx = [e for e in ev if e[2] in ("k_rp_fixed_exact", "k_rp_fixed_all")]
 t_fx = fx[-1][0]
