@@ -345,7 +345,14 @@ def main():
                 fdist.allgather_verdicts(dist, st)
         return res, t0
 
-    pipelined(max(args.warmup, inflight))
+    # warmup in the timed region's shape: bursts of `steps` submissions while that is
+    # fewer than the in-flight slots (the driver's 20-step line), else one stream
+    warm = max(args.warmup, inflight)
+    if args.steps < inflight:
+        for _ in range(-(-warm // args.steps)):
+            pipelined(args.steps)
+    else:
+        pipelined(warm)
 
     def before_timed():
         if dist is not None:
@@ -621,6 +628,32 @@ def _roofline_from(timings, steps):
             "traffic": None, "kernel_ms": round(ms, 4), "mads_per_launch": mads}
 
 
+def _msm_roofline(kt, args):
+    """C3 roofline, with PMC HBM bytes per launch of the dominant kernel and of the
+    sort kernels from the newest profiles/msm22_traffic_rNN.json (tools/gpu_session.sh
+    msm_pmc: FETCH_SIZE + WRITE_SIZE, separate runs of this workload at 2^22 points)"""
+    roof = _roofline_from(kt, args.steps)
+    if args.msm_log != 22 or args.msm_tiled:
+        return roof
+    import glob
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "msm22_traffic_r[0-9][0-9].json")))
+    if not cands:
+        return roof
+    try:
+        with open(cands[-1]) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        return roof
+
+    def tb(k):
+        e = tj.get(k) or {}
+        return None if e.get("fetch_bytes_raw") is None else e["fetch_bytes_raw"] + e.get("write_bytes", 0)
+    roof["traffic"] = tb(roof["kernel"])
+    roof["traffic_source"] = os.path.basename(cands[-1])
+    roof["traffic_per_kernel"] = {k: tb(k) for k in tj if not k.startswith("_") and tb(k) is not None}
+    return roof
+
+
 def _run_action_steps(batches, steps, dist, gather):
     """`steps` verify() calls spread over one host thread per prepared batch
     (concurrent calls run on different device lanes, so one call's host DER
@@ -746,7 +779,7 @@ def bench_msm(args):
             "data": data,
             "config": {"workload": "C3: standalone G1 MSM, 2^%d points per GPU (fts_msm_run, inputs resident in HBM)"
                                    % args.msm_log, "points": n, "parallelism": "shard%d" % world},
-            "roofline": _roofline_from(kt, args.steps), "cpu_baseline": cpu,
+            "roofline": _msm_roofline(kt, args), "cpu_baseline": cpu,
             "kernel_ms": {k: round(v[0] / args.steps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),
             flush=True)
     if dist is not None:
@@ -1417,7 +1450,7 @@ def bench_transfer(args, raw_requests=False):
             "config": {"workload": "C4 per GPU: %d transfers (TypeAndSum + 2 rp%d each) per step via "
                                    "%s, %d calls in flight" % (args.transfers, args.bits, entry, nb),
                        "transfers_per_gpu": args.transfers, "parallelism": "shard%d" % world},
-            "roofline": _roofline_from(kt, args.steps), "cpu_baseline": cpu,
+            "roofline": _msm_roofline(kt, args), "cpu_baseline": cpu,
             "kernel_ms": {k: round(v[0] / args.steps, 4) for k, v in kt.items()}, "setup_s": round(setup_s, 2)}),
             flush=True)
     if dist is not None:

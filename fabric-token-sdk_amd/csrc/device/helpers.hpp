@@ -2,8 +2,34 @@
 #pragma once
 #include "g1.hpp"
 #include "transcript.hpp"
+#include "wave_prio.hpp"
 
 namespace fts {
+
+// Wave priority of the batch-verify pass's kernels (s_setprio).  A SIMD arbitrates
+// VALU issue by wave priority, then age (MI355X_MICROARCH.md, "Two waves per SIMD"):
+// the short dependent kernels of the batch check's MSM and of the x0 tail start while
+// the long issue-bound chain waves (k_rp_com_var, the x0 prefix hash) are resident, so
+// at equal priority they are the younger waves and get only the chain's leftover issue
+// slots (r05 trace: k_msm_scan1 0.005 ms alone, 0.64 ms beside com_var; the MSM's sort
+// 0.5 ms alone, 5.9 ms in the pass).  One static level per kernel group, set once at
+// kernel entry from this table (a uniform scalar load; FTS_WAVE_PRIO overrides it per
+// context, fts_api.cpp).
+static __constant__ int g_wave_prio[PS_N] = FTS_WAVE_PRIO_DEFAULT;
+template <int S>
+FTS_DEV void wave_prio() {
+  const int p = g_wave_prio[S];  // uniform: s_load + s_cbranch around one s_setprio
+  if (p == 1)
+    __builtin_amdgcn_s_setprio(1);
+  else if (p == 2)
+    __builtin_amdgcn_s_setprio(2);
+  else if (p >= 3)
+    __builtin_amdgcn_s_setprio(3);
+}
+// per translation unit (each holds its own copy of the table)
+static inline hipError_t upload_wave_prio(const int* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_wave_prio), p, sizeof(int) * PS_N, 0, hipMemcpyHostToDevice);
+}
 
 // ------------------------------------------------------------ small helpers
 FTS_DEV Fr fr_from_canon(const uint32_t* c) {

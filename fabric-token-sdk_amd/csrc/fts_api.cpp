@@ -31,6 +31,7 @@
 #include "host/request_parse.hpp"
 #include "host/proofs.hpp"
 #include "host/prover.hpp"
+#include "device/wave_prio.hpp"
 
 namespace fts {
 // device launchers (rp_kernels.hip)
@@ -46,6 +47,9 @@ void launch_build_wide_tables(const uint32_t* bases, int nb, uint32_t* tables, u
                               int wbits);
 size_t wide_build_scratch_bytes(int nb, int wbits);
 size_t fbw_words_per_base(int wbits);
+// wave priority table (helpers.hpp PrioSlot) of rp_kernels.hip and msm.hip's kernels
+hipError_t rp_set_wave_prio(const int* p);
+hipError_t msm_set_wave_prio(const int* p);
 void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, const int32_t* sel, int nsel, hipStream_t s,
                         Timeline* tl);
 void launch_rlc_group_test(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, const MsmPlan& p,
@@ -442,7 +446,16 @@ struct fts_ctx {
   // of one lone 4,096-proof pass per free lane); an idle device starts at once
   size_t gather_target = 16384;
   int gather_us = 1000;
-  int idle_gather_us = 0;  // FTS_IDLE_GATHER_US: the same window when the device is idle (0: start at once)
+  // An idle device's window (FTS_IDLE_GATHER_US / FTS_IDLE_QUIET_US): the head waits
+  // while batches keep arriving (each within idle_quiet_us of the last, at most
+  // idle_gather_us in all) or until gather_target proofs are queued, and its pass
+  // takes at most gather_target proofs.  A burst of 20 callers released together
+  // (the driver's 20-step line) becomes two passes of 10 batches whatever the
+  // threads' timing (r05: 4.19-4.32 M/s medians with passes of 1 + 10 + 9, formed by
+  // arrival luck; 4.35-4.40 with 10 + 10); a lone caller waits idle_quiet_us.
+  int idle_gather_us = 1000;
+  int idle_quiet_us = 150;
+  std::chrono::steady_clock::time_point last_arrival{};
   // passes of up to com_fixed_max proofs compute com on the latency path (fixed-base
   // groups, rp_kernels.hip k_rp_fixed_all), larger ones on the work path (Horner +
   // joint GLV chains): the same group element either way
@@ -625,6 +638,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_GATHER_TARGET")) c->gather_target = (size_t)std::max(1L, atol(e));
   if (const char* e = getenv("FTS_GATHER_US")) c->gather_us = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_IDLE_GATHER_US")) c->idle_gather_us = std::max(0, atoi(e));
+  if (const char* e = getenv("FTS_IDLE_QUIET_US")) c->idle_quiet_us = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_COM_FIXED_MAX")) c->com_fixed_max = (size_t)std::max(0L, atol(e));
   if (const char* e = getenv("FTS_RLC_FORK")) c->rlc_fork = std::max(0, std::min(4, atoi(e)));
   if (const char* e = getenv("FTS_X0_SPLIT")) c->x0_split = atoi(e) != 0;
@@ -634,6 +648,14 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_GT1")) c->gt1 = std::max(8, std::min(1024, atoi(e)));
   if (const char* e = getenv("FTS_GT2_MIN")) c->gt2_min = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_GT_ADAPT")) c->gt_adapt = atoi(e) != 0;
+  // FTS_WAVE_PRIO: one digit 0-3 per PrioSlot (device/helpers.hpp), e.g. 02211331313;
+  // the table is per device and process (the last context created on a device sets it)
+  if (const char* e = getenv("FTS_WAVE_PRIO")) {
+    int pr[PS_N] = FTS_WAVE_PRIO_DEFAULT;
+    for (int i = 0; i < PS_N && e[i]; i++)
+      if (e[i] >= '0' && e[i] <= '3') pr[i] = e[i] - '0';
+    if (rp_set_wave_prio(pr) != hipSuccess || msm_set_wave_prio(pr) != hipSuccess) return fail(FTS_API_EDEVICE);
+  }
   // the batch check's stream (s3: RLC weights + MSM, the longest chain of a small
   // pass) gets the device's highest stream priority, so its few waves are
   // dispatched ahead of the exact phase's wide fixed-base launches
@@ -701,7 +723,9 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   // wide tables of the per-proof bases H_i, K, P (same build, wider windows):
   // 22-bit windows (one mixed addition fewer per product: -8 % of the pass's
   // largest kernel) when the free HBM holds them with room to spare for the lanes'
-  // workspace (~7 GB each at n = 64) and other contexts; else 20-bit
+  // workspace (~7 GB each at n = 64) and other contexts (160 GiB: at n = 64 only the
+  // first context on an empty MI355X takes them); else, or when the allocation
+  // fails, 20-bit
   {
     const int nw = n + 2;
     {
@@ -711,7 +735,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
       } else {
         size_t fr = 0, tot = 0;
         const size_t need22 = (size_t)nw * fbw_words_per_base(22) * 4;
-        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > need22 + ((size_t)128 << 30)) wb = 22;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > need22 + ((size_t)160 << 30)) wb = 22;
       }
       c->wbits = wb;
     }
@@ -722,11 +746,22 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
     }
     uint32_t* d_wb = nullptr;
     uint32_t* d_wscr = nullptr;
-    const int wchunk = std::min(nw, c->wbits == 22 ? 1 : 4);  // bounds the Jacobian build scratch (2.4 / 1.6 GB)
-    if (hipMalloc(&c->d_wtables, (size_t)nw * fbw_words_per_base(c->wbits) * 4) != hipSuccess ||
-        hipMalloc(&d_wb, hw.size() * 4) != hipSuccess ||
-        hipMalloc(&d_wscr, wide_build_scratch_bytes(wchunk, c->wbits)) != hipSuccess) {
+    int wchunk = 1;
+    for (;;) {  // 22-bit tables that do not fit after all (other contexts' lanes): 20-bit
+      wchunk = std::min(nw, c->wbits == 22 ? 1 : 4);  // bounds the Jacobian build scratch (2.4 / 1.6 GB)
+      if (hipMalloc(&c->d_wtables, (size_t)nw * fbw_words_per_base(c->wbits) * 4) == hipSuccess &&
+          hipMalloc(&d_wb, hw.size() * 4) == hipSuccess &&
+          hipMalloc(&d_wscr, wide_build_scratch_bytes(wchunk, c->wbits)) == hipSuccess)
+        break;
       if (d_wb) hipFree(d_wb);
+      if (c->d_wtables) hipFree(c->d_wtables);
+      d_wb = nullptr;
+      c->d_wtables = nullptr;
+      (void)hipGetLastError();
+      if (c->wbits == 22 && !getenv("FTS_WIDE_BITS")) {
+        c->wbits = 20;
+        continue;
+      }
       hipFree(d_bases);
       hipFree(d_scr);
       return fail(FTS_API_ENOMEM);
@@ -1641,6 +1676,7 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
   std::unique_lock<std::mutex> lk(c->mu);
   c->rp_pending.push_back(&me);
   c->pending_proofs += (size_t)b->B;
+  c->last_arrival = me.arrived;
   // enough queued for a full pass: the head stops gathering
   if (c->pending_proofs >= c->gather_target && c->rp_pending.front() != &me) c->rp_pending.front()->cv.notify_one();
   while (!me.done) {
@@ -1651,7 +1687,9 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
     const bool device_busy = c->free_lanes.size() < c->lanes.size();
     const int wait_us = device_busy ? c->gather_us : c->idle_gather_us;
     if (wait_us > 0 && c->rp_pending.front() == &me && c->pending_proofs < c->gather_target) {
-      const auto deadline = me.arrived + std::chrono::microseconds(wait_us);
+      auto deadline = me.arrived + std::chrono::microseconds(wait_us);
+      if (!device_busy)  // idle: only while the burst is still arriving
+        deadline = std::min(deadline, c->last_arrival + std::chrono::microseconds(c->idle_quiet_us));
       if (std::chrono::steady_clock::now() < deadline) {
         me.cv.wait_until(lk, deadline);
         continue;
@@ -1665,7 +1703,9 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
     Lane* L = c->lanes[c->free_lanes.back()];
     c->free_lanes.pop_back();
     L->alone = c->free_lanes.size() + 1 == c->lanes.size();
-    const size_t cap = c->coalesce_max;
+    // an idle device's first pass stops at gather_target proofs (the rest of the
+    // burst forms the next pass on another lane)
+    const size_t cap = L->alone ? std::min(c->coalesce_max, std::max<size_t>(c->gather_target, 1)) : c->coalesce_max;
     std::vector<RpReq*> grp;
     size_t tot = 0;
     while (!c->rp_pending.empty()) {

@@ -51,6 +51,7 @@ FTS_DEV long msm_src(const MsmIdx& p, int i) {
 __global__ void __launch_bounds__(256) k_msm_digits(MsmIdx p, const MsmWindow* __restrict__ win,
                                                     const uint32_t* __restrict__ scalars, int32_t* __restrict__ keys,
                                                     uint32_t* __restrict__ ranks, uint32_t* __restrict__ counts) {
+  wave_prio<PS_SORT>();
   const int N = p.N, nw = p.nw;
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
@@ -91,6 +92,7 @@ __global__ void __launch_bounds__(256) k_msm_digits(MsmIdx p, const MsmWindow* _
 __global__ void __launch_bounds__(256) k_msm_scan1(int NB, int ch, const uint32_t* __restrict__ counts,
                                                    uint32_t* __restrict__ offsets, uint32_t* __restrict__ chunk_off,
                                                    uint32_t* __restrict__ blk) {
+  wave_prio<PS_SORT>();
   __shared__ uint32_t pe[256], pc[256];
   const int t = threadIdx.x;
   const int base = blockIdx.x * MSM_SCAN_ITEMS + t * 4;
@@ -128,6 +130,7 @@ __global__ void __launch_bounds__(256) k_msm_scan1(int NB, int ch, const uint32_
 }
 
 __global__ void __launch_bounds__(256) k_msm_scan2(int nblk, uint32_t* __restrict__ blk) {
+  wave_prio<PS_SORT>();
   __shared__ uint32_t pe[256], pc[256];
   const int t = threadIdx.x;
   const int per = (nblk + 255) / 256;
@@ -170,6 +173,7 @@ __global__ void __launch_bounds__(256) k_msm_scan3(int NB, int ch, const uint32_
                                                    uint32_t* __restrict__ offsets, uint32_t* __restrict__ cursor,
                                                    uint32_t* __restrict__ chunk_off, int32_t* __restrict__ chunk_bkt,
                                                    const uint32_t* __restrict__ blk) {
+  wave_prio<PS_SORT>();
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= NB) return;
   const int q = b / MSM_SCAN_ITEMS;
@@ -185,6 +189,7 @@ __global__ void __launch_bounds__(256) k_msm_scan3(int NB, int ch, const uint32_
 __global__ void __launch_bounds__(256) k_msm_scatter(int NV, int nw, const int32_t* __restrict__ keys,
                                                      const uint32_t* __restrict__ ranks,
                                                      const uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted) {
+  wave_prio<PS_SORT>();
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= NV) return;
   for (int w = 0; w < nw; w++) {
@@ -240,6 +245,7 @@ constexpr uint32_t RS_IDX_MASK = 0x00ffffffu;  // virtual index bits of an entry
 // split is spread over the chip instead of the hist / scatter blocks' slices
 __global__ void __launch_bounds__(256) k_msm_split(MsmIdx p, uint4 rc, const uint32_t* __restrict__ scalars,
                                                    uint4* __restrict__ hk) {
+  wave_prio<PS_SORT>();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.N) return;
   const long src = msm_src(p, i);
@@ -289,6 +295,7 @@ FTS_DEV void rs_slice(const MsmIdx& p, int spg, int& g, int& i0, int& i1) {
 
 __global__ void __launch_bounds__(256) k_rs_hist(MsmIdx p, int spg, int npg, const MsmWindow* __restrict__ win,
                                                  const uint4* __restrict__ hk, uint32_t* __restrict__ hist) {
+  wave_prio<PS_SORT>();
   extern __shared__ uint32_t rs_lds[];
   for (int q = threadIdx.x; q < npg; q += blockDim.x) rs_lds[q] = 0;
   __syncthreads();
@@ -304,6 +311,7 @@ __global__ void __launch_bounds__(256) k_rs_hist(MsmIdx p, int spg, int npg, con
 // lane per global partition g npg + lp: exclusive prefix over the group's slices, in place
 __global__ void __launch_bounds__(256) k_rs_pscan(int G, int spg, int npg, uint32_t* __restrict__ hist,
                                                   uint32_t* __restrict__ ptot) {
+  wave_prio<PS_SORT>();
   const int P = blockIdx.x * blockDim.x + threadIdx.x;
   if (P >= G * npg) return;
   const int g = P / npg, lp = P % npg;
@@ -331,6 +339,7 @@ __global__ void __launch_bounds__(256) k_rs_pscan(int G, int spg, int npg, uint3
 constexpr int RS_PB_BS = 1024;
 __global__ void __launch_bounds__(RS_PB_BS) k_rs_pbase(int NP, const uint32_t* __restrict__ ptot,
                                                       uint32_t* __restrict__ pbase) {
+  wave_prio<PS_SORT>();
   __shared__ uint32_t sh[RS_PB_BS];
   const int t = threadIdx.x, per = (NP + RS_PB_BS - 1) / RS_PB_BS;
   uint32_t loc = 0;
@@ -359,6 +368,7 @@ __global__ void __launch_bounds__(RS_PB_BS) k_rs_pbase(int NP, const uint32_t* _
 __global__ void __launch_bounds__(256) k_rs_scatter(MsmIdx p, int spg, int npg, const MsmWindow* __restrict__ win,
                                                     const uint4* __restrict__ hk, const uint32_t* __restrict__ hist,
                                                     const uint32_t* __restrict__ pbase, uint32_t* __restrict__ tmp) {
+  wave_prio<PS_SORT>();
   extern __shared__ uint32_t rs_lds[];
   int g, i0, i1;
   rs_slice(p, spg, g, i0, i1);
@@ -378,6 +388,7 @@ __global__ void __launch_bounds__(256) k_rs_scatter(MsmIdx p, int spg, int npg, 
 __global__ void __launch_bounds__(256) k_rs_part(const uint32_t* __restrict__ pbase, const uint32_t* __restrict__ ptot,
                                                  const uint32_t* __restrict__ tmp, uint32_t* __restrict__ counts,
                                                  uint32_t* __restrict__ sorted) {
+  wave_prio<PS_SORT>();
   constexpr int PB = 1 << RS_PSH;
   __shared__ uint32_t cnt[PB], cur[PB];
   const int P = blockIdx.x, t = threadIdx.x;
@@ -417,6 +428,7 @@ __global__ void __launch_bounds__(64, 4) k_msm_chunks(MsmIdx p, const uint32_t* 
                                                    const uint32_t* __restrict__ chunk_off,
                                                    const int32_t* __restrict__ chunk_bkt,
                                                    const uint32_t* __restrict__ sorted, uint32_t* __restrict__ partials) {
+  wave_prio<PS_CHUNKS>();
   const int N = p.N;
   int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= (int)*nc_total) return;
@@ -456,6 +468,7 @@ __global__ void __launch_bounds__(256) k_msm_bucket_sum(int NB, int ch, const ui
                                                        const uint32_t* __restrict__ chunk_off,
                                                        const uint32_t* __restrict__ partials,
                                                        uint32_t* __restrict__ buckets) {
+  wave_prio<PS_MSMTAIL>();
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= NB) return;
   const uint32_t nch = (counts[b] + ch - 1) / ch, c0 = chunk_off[b];
@@ -470,6 +483,7 @@ __global__ void __launch_bounds__(256) k_msm_bucket_sum(int NB, int ch, const ui
 __global__ void __launch_bounds__(256) k_msm_segments(int nw, int NS, int NSg, int NBg, const MsmWindow* __restrict__ win,
                                                      const uint32_t* __restrict__ buckets,
                                                      uint32_t* __restrict__ segs, uint32_t* __restrict__ scratch) {
+  wave_prio<PS_MSMTAIL>();
   int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= NS) return;
   const int grp = g / NSg, gl = g % NSg;
@@ -503,6 +517,7 @@ __global__ void __launch_bounds__(256) k_msm_segments(int nw, int NS, int NSg, i
 __global__ void __launch_bounds__(256) k_msm_windows(int nw, int WB, int NSg, const MsmWindow* __restrict__ win,
                                                      const uint32_t* __restrict__ segs, const uint32_t* __restrict__ extra,
                                                      int nextra, uint32_t* __restrict__ parts) {
+  wave_prio<PS_MSMTAIL>();
   __shared__ uint32_t sh[256 * 24];
   const int t = threadIdx.x, w = blockIdx.x, j = blockIdx.y, grp = blockIdx.z;
   const uint32_t* S;
@@ -541,6 +556,7 @@ constexpr int FINAL_MAXW = 4;           // waves per block (48 groups >= MSM win
 __global__ void __launch_bounds__(64 * FINAL_MAXW) k_msm_final(int nw, int WB, const MsmWindow* __restrict__ win,
                                                                const uint32_t* __restrict__ parts_all,
                                                                uint32_t* __restrict__ out_all) {
+  wave_prio<PS_MSMTAIL>();
   __shared__ uint32_t sh[FINAL_MAXW * FINAL_GPW * 24];
   const int t = threadIdx.x, grp = blockIdx.x;  // one block per MSM group
   const int wave = t / 64, lt = t % 64;
@@ -585,6 +601,7 @@ __global__ void __launch_bounds__(64 * FINAL_MAXW) k_msm_final(int nw, int WB, c
 __global__ void __launch_bounds__(256) k_msm_small_windows(int nw, int G, int NBg, const MsmWindow* __restrict__ win,
                                                           const uint32_t* __restrict__ buckets,
                                                           uint32_t* __restrict__ wparts) {
+  wave_prio<PS_MSMTAIL>();
   const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (size_t)nw * G) return;
   const int w = (int)(gid / G), grp = (int)(gid % G);
@@ -604,6 +621,7 @@ __global__ void __launch_bounds__(256) k_msm_small_windows(int nw, int G, int NB
 __global__ void __launch_bounds__(64) k_msm_small_final(int nw, const uint32_t* __restrict__ wparts,
                                                         const uint32_t* __restrict__ extra, int nextra,
                                                         uint32_t* __restrict__ out) {
+  wave_prio<PS_MSMTAIL>();
   __shared__ uint32_t sh[64 * 24];
   const int t = threadIdx.x, grp = blockIdx.x;
   G1J acc = g1j_identity();
@@ -824,4 +842,5 @@ void launch_msm_to_bytes(const uint32_t* jac, uint8_t* out, hipStream_t s) {
   hipLaunchKernelGGL(k_msm_to_bytes, dim3(1), dim3(64), 0, s, jac, out);
 }
 
+hipError_t msm_set_wave_prio(const int* p) { return upload_wave_prio(p); }
 }  // namespace fts

@@ -371,6 +371,7 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, c
                                                           const uint32_t* __restrict__ ypow,
                                                           const uint32_t* __restrict__ wtables, uint32_t* __restrict__ hpj,
                                                           uint32_t* __restrict__ terms) {
+  wave_prio<PS_FIXED>();
   const int ni = n + 2;
   const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (size_t)B * ni) return;
@@ -413,6 +414,7 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_exact(int B, int n, int k, c
 // the H' normalisation, which runs beside it on the x0 stream)
 __global__ void __launch_bounds__(256) k_rp_hsum_chunks(int B, int n, const int32_t* __restrict__ status,
                                                        const uint32_t* __restrict__ hpj, uint32_t* __restrict__ chunks) {
+  wave_prio<PS_HSUM>();
   const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * nc) return;
@@ -434,6 +436,7 @@ __global__ void __launch_bounds__(256) k_rp_hsum_chunks(int B, int n, const int3
 // their chain
 __global__ void __launch_bounds__(256) k_rp_hsum_join(int B, int n, const int32_t* __restrict__ status,
                                                      uint32_t* __restrict__ chunks) {
+  wave_prio<PS_HSUM>();
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B || status[b] != 0) return;
   const int nc = (n + HS_CHUNK - 1) / HS_CHUNK;
@@ -458,6 +461,7 @@ __global__ void __launch_bounds__(256, FTS_COMVAR_OCC) k_rp_com_var(int B, int n
                                                    const uint32_t* __restrict__ chunks, uint32_t* __restrict__ atab,
                                                    const uint32_t* __restrict__ terms, uint32_t* __restrict__ hpj,
                                                    uint32_t* __restrict__ hpa, uint8_t* __restrict__ hp_be) {
+  wave_prio<PS_COMVAR>();
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = gid >> 1, h = gid & 1;
   if (b >= B || status[b] != 0) return;
@@ -670,6 +674,7 @@ __global__ void __launch_bounds__(NORM_BS) k_rp_normalize(int total, int per, in
                                                           const int32_t* __restrict__ status,
                                                           const uint32_t* __restrict__ jac, uint32_t* __restrict__ aff,
                                                           uint8_t* __restrict__ be, uint8_t* __restrict__ x0msgs) {
+  wave_prio<PS_NORM>();
   const size_t gid = (size_t)blockIdx.x * NORM_BS + threadIdx.x;
   const size_t g0 = (gid >> 6) * (size_t)E * 64 + (gid & 63);
   auto slot = [&](int j) {
@@ -799,6 +804,7 @@ __global__ void __launch_bounds__(64 * X0_PPB) k_rp_x0_build(int B, int n, const
                                                             const uint8_t* __restrict__ x0_const,
                                                             const uint32_t* __restrict__ sc, uint8_t* __restrict__ msgs,
                                                             int part) {
+  wave_prio<PS_X0TAIL>();
   extern __shared__ uint4 x0_lds[];
   const uint32_t A = x0_array_len(n), len = x0_msg_len(n), end = x0_slot_bytes(n);
   const uint32_t cb0 = x0_cb0(n), cb1 = x0_cb1(n), var = x0_var_bytes(n);
@@ -881,6 +887,7 @@ inline unsigned x0_build_grid(int B) { return (unsigned)((B + X0_PPB - 1) / X0_P
 // critical path, 0.4 -> 5.2 ms)
 __global__ void __launch_bounds__(256) k_rp_x0_hdr(int B, int n, const int32_t* __restrict__ status,
                                                    const uint8_t* __restrict__ x0_const, uint8_t* __restrict__ msgs) {
+  wave_prio<PS_NORM>();
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B || status[b] != 0) return;
   uint8_t* msg = msgs + (size_t)b * x0_var_bytes(n);
@@ -901,6 +908,11 @@ __global__ void __launch_bounds__(256) k_rp_x0_hash(int B, int n, int k, const i
                                                    const uint8_t* __restrict__ msgs, const uint8_t* __restrict__ tmpl,
                                                    uint32_t b0, uint32_t b1, uint32_t* __restrict__ mid,
                                                    uint32_t* __restrict__ ch) {
+  // the suffix is the pass's short tail; the prefix runs beside the com chain
+  if (b0 != 0)
+    wave_prio<PS_X0TAIL>();
+  else
+    wave_prio<PS_X0PRE>();
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B || status[b] != 0) return;
   const uint32_t cb0 = x0_cb0(n), cb1 = x0_cb1(n), nb = sha_blocks(x0_msg_len(n));
@@ -1232,6 +1244,7 @@ __global__ void __launch_bounds__(256) k_rlc_prep(int B, int n, int k, const int
                                                  const int32_t* __restrict__ ipa_flag, const uint32_t* __restrict__ sc,
                                                  const uint32_t* __restrict__ ch, const uint32_t* __restrict__ key,
                                                  uint32_t* __restrict__ msc, uint32_t* __restrict__ coef) {
+  wave_prio<PS_SORT>();
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const int npts = rp_npts(k);
@@ -1336,6 +1349,7 @@ __global__ void __launch_bounds__(256) k_rlc_columns(int B, int n, int k, int gs
                                                      const uint32_t* __restrict__ coef, const uint32_t* __restrict__ ypow,
                                                      const uint32_t* __restrict__ svec,
                                                      const uint32_t* __restrict__ zvec, uint32_t* __restrict__ colsum) {
+  wave_prio<PS_COLS>();
   __shared__ uint32_t sh[256 * 8];
   const int col = col0 + blockIdx.x, grp = blockIdx.y, t = threadIdx.x, nt = blockDim.x;  // nt: 64 or 256
   Fr acc = f_zero<FrP>();
@@ -1363,6 +1377,7 @@ __global__ void __launch_bounds__(256) k_rlc_columns(int B, int n, int k, int gs
 // (One block over all B proofs took 0.76 ms at 81,920 on the x0-dependent tail.)
 constexpr int RQ_PARTS = 64;
 __global__ void __launch_bounds__(64) k_rlc_qsum(int ncols, int col, uint32_t* __restrict__ colsum) {
+  wave_prio<PS_FIN>();
   __shared__ uint32_t sh[RQ_PARTS * 8];
   const int t = threadIdx.x;
   Fr v;  // plain residues: the sum is the same in either representation
@@ -1395,6 +1410,7 @@ __global__ void __launch_bounds__(RF_ITEMS * FB_NW) k_rlc_fixed(int n, int G, in
                                                                const uint32_t* __restrict__ colsum,
                                                                const uint32_t* __restrict__ tables,
                                                                uint32_t* __restrict__ out) {
+  wave_prio<PS_COLS>();
   __shared__ uint32_t sh[RF_ITEMS * FB_NW * 24];
   const int w = threadIdx.x % FB_NW, it = blockIdx.x * RF_ITEMS + threadIdx.x / FB_NW;
   const bool live = it < G * ncl;
@@ -1468,6 +1484,7 @@ __global__ void __launch_bounds__(64) k_rlc_finalize(int B, const uint32_t* __re
                                                      const int32_t* __restrict__ excl,
                                                      int32_t* __restrict__ status, const int32_t* __restrict__ ipa_flag,
                                                      int32_t* __restrict__ flag) {
+  wave_prio<PS_FIN>();
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b < B && excl && excl[b] && status[b] == 0) status[b] = FTS_E_NOT_RUN;
   G1J e = load_g1j(msm_out);
@@ -1492,6 +1509,7 @@ __global__ void __launch_bounds__(256) k_rlc_finalize_groups(int slots, int gs, 
                                                              int32_t* __restrict__ status,
                                                              const int32_t* __restrict__ ipa_flag,
                                                              int32_t* __restrict__ gflag, int32_t* __restrict__ flag) {
+  wave_prio<PS_FIN>();
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= slots) return;
   const int b = sel[j], g = j / gs;
@@ -1914,4 +1932,5 @@ void launch_x0(int B, int n, int k, const int32_t* status, const uint8_t* hp_be,
   hipLaunchKernelGGL(k_rp_x0_build, dim3(x0_build_grid(B)), dim3(64 * X0_PPB), x0_build_lds(n), s, B, n, status, hp_be, x0_const, sc, msgs, 2);
   FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s, B, n, k, status, msgs, x0_tmpl, 0u, 0xffffffffu, (uint32_t*)nullptr, ch);
 }
+hipError_t rp_set_wave_prio(const int* p) { return upload_wave_prio(p); }
 }  // namespace fts

@@ -81,6 +81,25 @@ def test_concurrent_lanes_rp32(gpu_pp):
         batches[t].close()
 
 
+def _one_lane_ctx(pp_raw):
+    """a 16-bit context with ONE device lane, whose idle window is off
+    (FTS_IDLE_GATHER_US=0): the first submission (a blocker) starts at once and
+    the others queue behind it and coalesce"""
+    import os
+
+    import fts_gpu
+    saved = {k: os.environ.get(k) for k in ("FTS_LANES", "FTS_IDLE_GATHER_US")}
+    os.environ.update(FTS_LANES="1", FTS_IDLE_GATHER_US="0")
+    try:
+        return fts_gpu.PublicParams(pp_raw, bit_length=16, device=0)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 def test_coalesced_batches_keep_their_verdicts(pp_raw):
     """With ONE device lane, batches submitted concurrently are coalesced into
     shared device passes (fts_rp_batch_verify's dispatcher).  Each caller must
@@ -91,15 +110,7 @@ def test_coalesced_batches_keep_their_verdicts(pp_raw):
 
     import fts_gpu
 
-    old = os.environ.get("FTS_LANES")
-    os.environ["FTS_LANES"] = "1"
-    try:
-        pp = fts_gpu.PublicParams(pp_raw, bit_length=16, device=0)
-    finally:
-        if old is None:
-            del os.environ["FTS_LANES"]
-        else:
-            os.environ["FTS_LANES"] = old
+    pp = _one_lane_ctx(pp_raw)
     rng = random.Random(0xC0A1E5CE)
     sizes = [1, 7, 64, 200, 33, 128, 5, 90]
     batches, expect = [], []
@@ -157,8 +168,9 @@ def test_one_bad_proof_in_coalesced_pass_group_test(pp_raw, main_groups):
 
     import fts_gpu
 
-    saved = {k: os.environ.get(k) for k in ("FTS_LANES", "FTS_MAIN_GROUPS")}
+    saved = {k: os.environ.get(k) for k in ("FTS_LANES", "FTS_MAIN_GROUPS", "FTS_IDLE_GATHER_US")}
     os.environ.update(FTS_LANES="1", FTS_MAIN_GROUPS=str(main_groups))
+    os.environ["FTS_IDLE_GATHER_US"] = "0"  # the blocker starts at once; the rest queue behind it
     try:
         pp = fts_gpu.PublicParams(pp_raw, bit_length=16, device=0)
     finally:
@@ -240,8 +252,9 @@ def test_group_test_round2_exact_verdicts(pp_raw):
 
     import fts_gpu
 
-    saved = {k: os.environ.get(k) for k in ("FTS_LANES", "FTS_GT1", "FTS_GT2_MIN")}
+    saved = {k: os.environ.get(k) for k in ("FTS_LANES", "FTS_GT1", "FTS_GT2_MIN", "FTS_IDLE_GATHER_US")}
     os.environ.update(FTS_LANES="1", FTS_GT1="64", FTS_GT2_MIN="0")
+    os.environ["FTS_IDLE_GATHER_US"] = "0"  # the blocker starts at once; the rest queue behind it
     try:
         pp = fts_gpu.PublicParams(pp_raw, bit_length=16, device=0)
     finally:
@@ -319,10 +332,11 @@ def test_group_test_adaptive_dense_exact_verdicts(pp_raw):
 
     import fts_gpu
 
-    saved = {k: os.environ.get(k) for k in ("FTS_LANES", "FTS_GT1", "FTS_GT2_MIN", "FTS_GT_ADAPT")}
+    saved = {k: os.environ.get(k) for k in ("FTS_LANES", "FTS_GT1", "FTS_GT2_MIN", "FTS_GT_ADAPT", "FTS_IDLE_GATHER_US")}
     for k in ("FTS_GT1", "FTS_GT2_MIN", "FTS_GT_ADAPT"):
         os.environ.pop(k, None)
     os.environ["FTS_LANES"] = "1"
+    os.environ["FTS_IDLE_GATHER_US"] = "0"  # the blocker starts at once; the rest queue behind it
     try:
         pp = fts_gpu.PublicParams(pp_raw, bit_length=16, device=0)
     finally:
@@ -398,15 +412,7 @@ def test_dense_and_sparse_batches_in_one_pass(pp_raw):
 
     import fts_gpu
 
-    old = os.environ.get("FTS_LANES")
-    os.environ["FTS_LANES"] = "1"
-    try:
-        pp = fts_gpu.PublicParams(pp_raw, bit_length=16, device=0)
-    finally:
-        if old is None:
-            del os.environ["FTS_LANES"]
-        else:
-            os.environ["FTS_LANES"] = old
+    pp = _one_lane_ctx(pp_raw)
     from oracle import pp as oppm
     opp = oppm.load_pp(pp_raw).with_bit_length(16)
     rng = random.Random(0xD5A5)
@@ -453,5 +459,62 @@ def test_dense_and_sparse_batches_in_one_pass(pp_raw):
     per_proof = work["fb:k_rp_terms_fixed"] / ((3 + 2 * 16) * 15 * 11 * 136)
     assert 1 <= round(per_proof) <= 16 * 8 + 256, per_proof
     for b in (dense, sparse, blocker):
+        b.close()
+    pp.close()
+
+
+@pytest.mark.gpu
+def test_idle_burst_splits_into_even_passes(pp_raw):
+    """The dispatcher's idle window (fts_api.cpp fts_rp_batch_verify): 20 batches
+    submitted together on an idle device form two passes of 10 (the first pass
+    stops at gather_target = coalesce_max / 2 proofs), whatever the submitter
+    threads' timing; every caller keeps its own verdicts."""
+    import os
+    import threading
+
+    import fts_gpu
+
+    m, nb = 64, 20
+    env = dict(FTS_COALESCE_MAX=str(20 * m), FTS_IDLE_GATHER_US="50000", FTS_IDLE_QUIET_US="5000")
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        pp = fts_gpu.PublicParams(pp_raw, bit_length=16, device=0)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    rng = random.Random(0x1D1E)
+    batches, expect = [], []
+    for t in range(nb):
+        vals = [rng.getrandbits(16) for _ in range(m)]
+        bfs = [rng.randrange(bn.R).to_bytes(32, "big") for _ in range(m)]
+        proofs, coms = pp.prove_range_batch_gpu(vals, bfs, seed=12000 + t)
+        exp = [0] * m
+        if t == 7:
+            r = zkat.RangeProof.deserialize(proofs[5])
+            r.data.T1 = bn.g1_add(r.data.T1, bn.GEN)
+            proofs[5] = r.serialize()
+            exp[5] = fts_gpu.FTS_E_RP_INVALID
+        batches.append(pp.stage_range_proofs(proofs, coms))
+        expect.append(exp)
+    for rep in range(2):
+        out, merged = [None] * nb, [0] * nb
+        gate = threading.Barrier(nb)
+
+        def run(t):
+            gate.wait()
+            out[t] = [int(s) for s in batches[t].verify()]
+            merged[t] = batches[t].merged()
+        th = [threading.Thread(target=run, args=(t,)) for t in range(nb)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert out == expect
+        assert merged == [10] * nb, merged
+    for b in batches:
         b.close()
     pp.close()

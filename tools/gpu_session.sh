@@ -1,6 +1,6 @@
 #!/bin/bash
 # The measurement recipe behind profiles/ (run on the gpurun box from the repo root):
-#   bash tools/gpu_session.sh STEP...     STEP in: smoke tests rp prof pmc tamper identity identity_pmc extra
+#   bash tools/gpu_session.sh STEP...     STEP in: smoke tests rp prof pmc tamper identity identity_pmc msm_pmc extra
 # smoke     __graft_entry__.smoke()
 # tests     pytest -m gpu (full suite)
 # rp        C2 headline, driver shape (20 steps) and steady state (512 steps)
@@ -10,12 +10,13 @@
 # tamper    C2 with 1 % tampered proofs; one bad proof per 81,920-proof pass vs clean (160 steps)
 # identity  idemix identity validity, both curves, + rocprofv3 stats
 # identity_pmc  FETCH_SIZE / WRITE_SIZE per identity kernel (BN254) -> identity_traffic_$TAG.json
+# msm_pmc   FETCH_SIZE / WRITE_SIZE per MSM kernel of C3 at 2^22 points -> msm22_traffic_$TAG.json
 # extra     C3-C5 and SURVEY 8f workloads
 # Every GPU step has its own time limit; the first failure ends the script.
-# Output: gpurun_out/$TAG (TAG default r03).
+# Output: gpurun_out/$TAG (TAG default r05).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$OLDPWD}"
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 step() {  # name limit cmd...
@@ -54,6 +55,12 @@ for s in "$@"; do case $s in
           step pmc_id_fetch 300 rocprofv3 --pmc FETCH_SIZE -T -f csv -d $OUT/pmc_id_fetch -o run -- $IB
           step pmc_id_write 300 rocprofv3 --pmc WRITE_SIZE -T -f csv -d $OUT/pmc_id_write -o run -- $IB
           python3 tools/pmc_kernels.py $OUT/pmc_id_fetch $OUT/pmc_id_write $OUT/identity_traffic_$TAG.json k_idv ;;
+  msm_pmc) MB="python3 bench.py --workload msm --msm-log 22 --steps 2 --warmup 1 --cpu-sample 0"
+          rm -rf $OUT/pmc_msm_fetch $OUT/pmc_msm_write
+          step pmc_msm_fetch 300 rocprofv3 --pmc FETCH_SIZE -T -f csv -d $OUT/pmc_msm_fetch -o run -- $MB
+          json pmc_msm_fetch
+          step pmc_msm_write 300 rocprofv3 --pmc WRITE_SIZE -T -f csv -d $OUT/pmc_msm_write -o run -- $MB
+          python3 tools/pmc_kernels.py $OUT/pmc_msm_fetch $OUT/pmc_msm_write $OUT/msm22_traffic_$TAG.json k_msm k_rs ;;
   identity) for c in bn254 fp256bn; do
               step bench_identity_$c 300 python3 -u bench.py --workload identity --idemix-curve $c --steps 40 --warmup 4; json bench_identity_$c
             done

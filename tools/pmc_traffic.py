@@ -33,13 +33,21 @@ from collections import defaultdict
 GATHER = {"k_rp_fixed_exact", "k_rp_fixed_all", "k_rp_terms_fixed", "k_pv_fbsum", "k_sig_terms", "k_token_open"}
 
 
+def kernel_key(name):
+    """'void fts::k_rp_fixed_exact<22>(...)' -> 'k_rp_fixed_exact' (the library's timing name)"""
+    k = name.split("(")[0].replace("fts::", "")
+    if k.startswith("void "):
+        k = k[5:]
+    return k.split("<")[0].strip()
+
+
 def per_kernel(d, counter):
     acc = defaultdict(list)
     for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(p) as f:
             for r in sorted(csv.DictReader(f), key=lambda r: int(r["Start_Timestamp"])):
                 if r["Counter_Name"] == counter:
-                    acc[r["Kernel_Name"].split("(")[0].replace("fts::", "")].append(float(r["Counter_Value"]))
+                    acc[kernel_key(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     return acc
 
 
@@ -84,8 +92,14 @@ def main():
             if v:
                 e[c] = round(sum(v) / len(v), 4) if c in ("VALUBusy", "SIMD_UTILIZATION") else round(sum(v) / len(v))
         out["%s@pass%d" % (k, batch if k in LATENCY_ONLY and proofs > batch else proofs)] = e
-    json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
     print(json.dumps(calib))
+    # the batch check's MSM sort (digits / two-level counting sort): bytes written per pass
+    SORT = ("k_msm_digits", "k_msm_split", "k_rs_hist", "k_rs_pscan", "k_rs_pbase", "k_rs_scatter", "k_rs_part",
+            "k_msm_scatter", "k_msm_local_sort")
+    sw = sum(out[k].get("write_bytes", 0) for k in out if k.split("@")[0] in SORT and k.endswith("@pass%d" % proofs))
+    out["_msm_sort_write_bytes@pass%d" % proofs] = sw
+    print("msm sort kernels write %.3f GB per pass" % (sw / 1e9))
+    json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
     for k in ("k_rp_fixed_exact", "k_rp_fixed_all", "k_msm_chunks"):
         key = "%s@pass%d" % (k, proofs)
         if key in out:
