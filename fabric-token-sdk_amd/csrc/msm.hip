@@ -219,7 +219,7 @@ __global__ void __launch_bounds__(256) k_msm_scatter(int NV, int nw, const int32
 //                 ~RS_SP * 2 nw / NP consecutive entries per partition: whole
 //                 lines, combined in L2), entry = virtual index | low bucket
 //                 bits << 24 | sign << 31
-//   k_rs_part     block per partition: LDS counting sort of its <= ~11 k entries
+//   k_rs_part     block per partition: LDS counting sort of its ~5.4 k entries
 //                 by the low bucket bits -> counts[b] and the final sorted array
 // (k_msm_scan1/2/3 then derive the bucket offsets -- the same positions, the
 // order is bucket-major in both -- and the chunk map).  Digits: with C = sum_w
@@ -229,15 +229,16 @@ __global__ void __launch_bounds__(256) k_msm_scatter(int NV, int nw, const int32
 // the digits are independent bit fields.  Same buckets and signs as
 // k_msm_digits; the order inside a bucket differs, which changes no group
 // element (only the affine result is observable).
-constexpr int RS_PSH = 7;                 // buckets per partition: 128
-constexpr int RS_SP = 2048;               // points per slice (block)
+constexpr int RS_PSH = 6;                 // buckets per partition: 64
+constexpr int RS_SP = 4096;               // points per slice (block)
 constexpr int RS_MAX_NPG = 8192;          // partitions per group: LDS counters <= 32 KB
 constexpr int RS_MIN_N = 4096;            // smaller plans keep k_msm_digits
+constexpr int RS_PART_STAGE = 7680;       // k_rs_part: entries sorted in LDS (30 KB + 1 KB counters)
 constexpr uint32_t RS_IDX_MASK = 0x00ffffffu;  // virtual index bits of an entry (NV < 2^24)
 // Grouped plans (G > 1, e.g. the batch check per caller batch): slices never
 // straddle two groups (SPG slices per group), a slice's LDS table holds its own
-// group's NPg = NBg / 128 partitions, hist is [slice][NPg], and the global
-// partition g NPg + lp covers the group's buckets g NBg + 128 lp .. + 127.
+// group's NPg = NBg / 64 partitions, hist is [slice][NPg], and the global
+// partition g NPg + lp covers the group's buckets g NBg + 64 lp .. + 63.
 
 // lane per plan point: the GLV halves of its scalar with the recoding constant
 // folded in, hk[h N + i] = (k_h + C) | sign_h << 127 (absent padding points of a
@@ -285,10 +286,31 @@ FTS_DEV void rs_point_digits(const MsmIdx& p, const MsmWindow* __restrict__ win,
     }
   }
 }
-// points [i0, i1) of slice blockIdx.x (group g)
-FTS_DEV void rs_slice(const MsmIdx& p, int spg, int& g, int& i0, int& i1) {
-  g = blockIdx.x / spg;
-  const int ls = blockIdx.x % spg;
+// window w's digits of plan point i (both GLV halves): as rs_point_digits, one window
+template <class F>
+FTS_DEV void rs_point_digits_w(const MsmIdx& p, const MsmWindow& W, const uint4* __restrict__ hk, int i, F&& f) {
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint4 u = hk[(size_t)h * p.N + i];
+    const uint32_t q[4] = {u.x, u.y, u.z, u.w & 0x7fffffffu};
+    const bool sg = (u.w >> 31) != 0;
+    const int d = (int)scalar_bits4(q, W.off, W.width) - ((1 << (W.width - 1)) - 1);
+    if (d != 0) f(W.bbase + (d < 0 ? -d : d) - 1, (d < 0) != sg, (uint32_t)(h * p.N + i));
+  }
+}
+// points [i0, i1) of block blockIdx.x's slice (group g).  Blocks are dealt to the 8
+// XCDs round-robin; slices are dealt in contiguous ranges per XCD instead (a
+// bijection on [0, gridDim.x)), so the neighbouring runs of one partition, which
+// share cache lines at their ends, are written through the same L2 and leave it as
+// whole lines (round-robin: every such line left two L2s partially written)
+FTS_DEV int rs_xcd_slice(int b, int S) {
+  const int xcd = b & 7, local = b >> 3, q = S >> 3, r = S & 7;
+  return xcd < r ? xcd * (q + 1) + local : r * (q + 1) + (xcd - r) * q + local;
+}
+FTS_DEV void rs_slice(const MsmIdx& p, int spg, int& g, int& i0, int& i1, int& slice) {
+  slice = rs_xcd_slice((int)blockIdx.x, (int)gridDim.x);
+  g = slice / spg;
+  const int ls = slice % spg;
   i0 = g * p.ptsg + ls * RS_SP;
   i1 = min(min(i0 + RS_SP, (g + 1) * p.ptsg), p.N);
 }
@@ -299,12 +321,12 @@ __global__ void __launch_bounds__(256) k_rs_hist(MsmIdx p, int spg, int npg, con
   extern __shared__ uint32_t rs_lds[];
   for (int q = threadIdx.x; q < npg; q += blockDim.x) rs_lds[q] = 0;
   __syncthreads();
-  int g, i0, i1;
-  rs_slice(p, spg, g, i0, i1);
+  int g, i0, i1, slice;
+  rs_slice(p, spg, g, i0, i1, slice);
   for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x)
     rs_point_digits(p, win, hk, i, [&](int bl, bool, uint32_t) { atomicAdd(&rs_lds[bl >> RS_PSH], 1u); });
   __syncthreads();
-  uint32_t* out = hist + (size_t)blockIdx.x * npg;
+  uint32_t* out = hist + (size_t)slice * npg;
   for (int q = threadIdx.x; q < npg; q += blockDim.x) out[q] = rs_lds[q];
 }
 
@@ -370,27 +392,37 @@ __global__ void __launch_bounds__(256) k_rs_scatter(MsmIdx p, int spg, int npg, 
                                                     const uint32_t* __restrict__ pbase, uint32_t* __restrict__ tmp) {
   wave_prio<PS_SORT>();
   extern __shared__ uint32_t rs_lds[];
-  int g, i0, i1;
-  rs_slice(p, spg, g, i0, i1);
-  const uint32_t* pre = hist + (size_t)blockIdx.x * npg;
+  int g, i0, i1, slice;
+  rs_slice(p, spg, g, i0, i1, slice);
+  const uint32_t* pre = hist + (size_t)slice * npg;
   const uint32_t* pb = pbase + (size_t)g * npg;
   for (int q = threadIdx.x; q < npg; q += blockDim.x) rs_lds[q] = pb[q] + pre[q];
   __syncthreads();
-  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x)
-    rs_point_digits(p, win, hk, i, [&](int bl, bool neg, uint32_t v) {
-      const uint32_t pos = atomicAdd(&rs_lds[bl >> RS_PSH], 1u);
-      tmp[pos] = v | ((uint32_t)(bl & ((1 << RS_PSH) - 1)) << 24) | (neg ? 0x80000000u : 0u);
-    });
+  // window-major: while the block writes window w, its open partition runs are that
+  // window's NPg / nw partitions (~16 entries = one line each per slice), so L2
+  // combines them into whole-line writes; point-major, the runs of all nw windows
+  // were open at once (2,048 x 64 B per block) and left L2 as partial lines
+  // (0.55 GB written per 81,920-proof pass for 0.09 GB of entries, r05 PMC).
+  // The slice's hk rows are re-read per window from L2.
+  for (int w = 0; w < p.nw; w++) {
+    const MsmWindow W = win[w];
+    for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x)
+      rs_point_digits_w(p, W, hk, i, [&](int bl, bool neg, uint32_t v) {
+        const uint32_t pos = atomicAdd(&rs_lds[bl >> RS_PSH], 1u);
+        tmp[pos] = v | ((uint32_t)(bl & ((1 << RS_PSH) - 1)) << 24) | (neg ? 0x80000000u : 0u);
+      });
+  }
 }
 
-// block per global partition P (buckets 128 P .. 128 P + 127: group P / npg's local
-// partition P % npg, as NBg = 128 npg)
+// block per global partition P (buckets 64 P .. 64 P + 63: group P / npg's local
+// partition P % npg, as NBg = 64 npg)
 __global__ void __launch_bounds__(256) k_rs_part(const uint32_t* __restrict__ pbase, const uint32_t* __restrict__ ptot,
                                                  const uint32_t* __restrict__ tmp, uint32_t* __restrict__ counts,
                                                  uint32_t* __restrict__ sorted) {
   wave_prio<PS_SORT>();
   constexpr int PB = 1 << RS_PSH;
   __shared__ uint32_t cnt[PB], cur[PB];
+  __shared__ uint32_t stage[RS_PART_STAGE];
   const int P = blockIdx.x, t = threadIdx.x;
   const uint32_t lo = pbase[P], n = ptot[P];
   if (t < PB) cnt[t] = 0;
@@ -403,7 +435,7 @@ __global__ void __launch_bounds__(256) k_rs_part(const uint32_t* __restrict__ pb
     cur[t] = c;
   }
   __syncthreads();
-  for (int off = 1; off < PB; off <<= 1) {  // inclusive scan of the 128 counts
+  for (int off = 1; off < PB; off <<= 1) {  // inclusive scan of the PB counts
     const uint32_t v = (t < PB && t >= off) ? cur[t - off] : 0u;
     __syncthreads();
     if (t < PB) cur[t] += v;
@@ -411,7 +443,17 @@ __global__ void __launch_bounds__(256) k_rs_part(const uint32_t* __restrict__ pb
   }
   if (t < PB) cur[t] -= cnt[t];  // exclusive
   __syncthreads();
-  for (uint32_t e = t; e < n; e += blockDim.x) {
+  if (n <= (uint32_t)RS_PART_STAGE) {  // the usual partition: sorted in LDS, one coalesced write
+    for (uint32_t e = t; e < n; e += blockDim.x) {
+      const uint32_t x = tmp[lo + e];
+      const uint32_t pos = atomicAdd(&cur[(x >> 24) & (PB - 1)], 1u);
+      stage[pos] = (x & RS_IDX_MASK) | (x & 0x80000000u);
+    }
+    __syncthreads();
+    for (uint32_t e = t; e < n; e += blockDim.x) sorted[lo + e] = stage[e];
+    return;
+  }
+  for (uint32_t e = t; e < n; e += blockDim.x) {  // oversized (adversarial scalars): in place
     const uint32_t x = tmp[lo + e];
     const uint32_t pos = atomicAdd(&cur[(x >> 24) & (PB - 1)], 1u);
     sorted[lo + pos] = (x & RS_IDX_MASK) | (x & 0x80000000u);

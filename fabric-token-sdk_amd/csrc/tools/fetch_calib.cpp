@@ -81,6 +81,24 @@ __global__ void __launch_bounds__(64) k_calib_gather64w(const uint4* __restrict_
   if (acc == 0x9e3779b9u) sink[0] = acc;
 }
 
+// WRITE_SIZE calibration (round 5): stores of a KNOWN byte count
+//   k_calib_store16   16 B per lane, fully coalesced, 1 GiB
+//   k_calib_store4    4 B per lane, fully coalesced, 1 GiB
+//   k_calib_store4p   4 B per lane, a random permutation inside each block's
+//                     8 KiB region (k_rs_part's in-partition scatter), 256 MiB
+__global__ void __launch_bounds__(256) k_calib_store16(uint4* __restrict__ dst, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = make_uint4((uint32_t)i, 1u, 2u, 3u);
+}
+__global__ void __launch_bounds__(256) k_calib_store4(uint32_t* __restrict__ dst, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = (uint32_t)i;
+}
+__global__ void __launch_bounds__(256) k_calib_store4p(uint32_t* __restrict__ dst) {
+  uint32_t* r = dst + (size_t)blockIdx.x * 2048;
+  for (uint32_t e = threadIdx.x; e < 2048; e += 256) r[(e * 1103u + 977u * blockIdx.x) & 2047u] = e;  // odd stride: a permutation
+}
+
 int main() {
   const uint32_t log_rows = 27;  // 2^27 rows x 64 B = 8 GiB
   const size_t rows = (size_t)1 << log_rows, tab_bytes = rows * 64;
@@ -97,11 +115,15 @@ int main() {
     hipLaunchKernelGGL(k_calib_stream, dim3(4096), dim3(256), 0, 0, tab, stream_bytes / 16, sink);
     hipLaunchKernelGGL(k_calib_gather64, dim3((unsigned)(lanes / 64)), dim3(64), 0, 0, tab, log_rows, lanes, sink);
     hipLaunchKernelGGL(k_calib_gather64w, dim3((unsigned)(lanes / 64)), dim3(64), 0, 0, tab, log_rows, lanes, sink);
+    hipLaunchKernelGGL(k_calib_store16, dim3(4096), dim3(256), 0, 0, tab, stream_bytes / 16);
+    hipLaunchKernelGGL(k_calib_store4, dim3(4096), dim3(256), 0, 0, (uint32_t*)tab, stream_bytes / 4);
+    hipLaunchKernelGGL(k_calib_store4p, dim3((unsigned)((256u << 20) / 8192)), dim3(256), 0, 0, (uint32_t*)tab);
     CK(hipDeviceSynchronize());
   }
   CK(hipGetLastError());
-  printf("{\"k_calib_stream\": %zu, \"k_calib_gather64\": %zu, \"k_calib_gather64w\": %zu}\n", stream_bytes,
-         lanes * 64, lanes * 64);
+  printf("{\"k_calib_stream\": %zu, \"k_calib_gather64\": %zu, \"k_calib_gather64w\": %zu, \"k_calib_store16\": %zu, "
+         "\"k_calib_store4\": %zu, \"k_calib_store4p\": %zu}\n",
+         stream_bytes, lanes * 64, lanes * 64, stream_bytes, stream_bytes, (size_t)256 << 20);
   hipFree(tab);
   hipFree(sink);
   return 0;

@@ -59,6 +59,8 @@ def main():
     scale = {}
     calib = {}
     for k, b in known.items():
+        if k.startswith("k_calib_store"):  # WRITE_SIZE calibration (pmc_calib_write pass)
+            continue
         v = cal.get(k)
         if v:
             fs = sum(v) / len(v) * 1024
