@@ -15,8 +15,10 @@ enum PrioSlot {
   PS_MSMTAIL,  // k_msm_bucket_sum .. k_msm_final
   PS_COLS,     // k_rlc_columns / k_rlc_fixed: fixed-base column sums (s4)
   PS_FIN,      // k_rlc_qsum, k_rlc_finalize*
+  PS_HEAD,     // k_rp_gather / decode / hash_small / chal_fr / powers: the next pass's
+               // head, short kernels beside the previous pass's fixed-base launch
   PS_N
 };
-#define FTS_WAVE_PRIO_DEFAULT {0, 2, 2, 1, 1, 3, 3, 1, 3, 1, 3}
+#define FTS_WAVE_PRIO_DEFAULT {0, 2, 2, 1, 1, 3, 3, 1, 3, 1, 3, 3}
 
 }  // namespace fts

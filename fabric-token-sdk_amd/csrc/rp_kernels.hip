@@ -42,6 +42,12 @@ namespace fts {
 // pass's streams rarely share a SIMD (64-thread blocks of two such kernels
 // slowed each other by ~26 %, tools/experiments/colocate.cpp)
 int g_lat_bs = 256;
+// block size of the work path's per-proof latency kernels (k_rp_chal_fr, k_rlc_prep,
+// k_rp_x0_hash; FTS_WORK_BS): they start beside another pass's fixed-base launch
+// (64-thread blocks filling the register file), where a 256-thread block waits for
+// four wave slots of one CU at once (k_rp_chal_fr 0.12 ms alone, 1.1 ms there;
+// k_rlc_prep 0.18 -> 1.8 ms in a 20-batch burst, round 5)
+int g_work_bs = 64;
 // block size of the work path's S / com chain kernels
 constexpr int g_chain_bs = 64;
 
@@ -138,6 +144,7 @@ __global__ void __launch_bounds__(64) kt_entries(int nb, const uint32_t* __restr
 __global__ void __launch_bounds__(256) k_rp_gather(RpGather g, int npts, uint8_t* __restrict__ raw,
                                                    uint32_t* __restrict__ sc, int32_t* __restrict__ status,
                                                    int32_t* __restrict__ ipa) {
+  wave_prio<PS_HEAD>();
   const int per = npts * 4 + RP_NSC * 2 + 1;  // uint4 chunks of raw, sc, + 1 lane for the two flags
   const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int B = g.off[g.G];
@@ -162,6 +169,7 @@ __global__ void __launch_bounds__(256) k_rp_gather(RpGather g, int npts, uint8_t
 // canonical coordinates, on the curve; 64 zero bytes = identity.
 __global__ void __launch_bounds__(256) k_rp_decode(int B, int npts, const uint8_t* __restrict__ raw,
                                                    uint32_t* __restrict__ pts, int32_t* __restrict__ status) {
+  wave_prio<PS_HEAD>();
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * npts) return;
   G1A a;
@@ -176,6 +184,7 @@ __global__ void __launch_bounds__(256) k_rp_decode(int B, int npts, const uint8_
 __global__ void __launch_bounds__(64) k_rp_hash_small(int B, int n, int k, const uint8_t* __restrict__ raw,
                                                       const int32_t* __restrict__ status, uint32_t* __restrict__ ch,
                                                       uint8_t* __restrict__ small_msgs) {
+  wave_prio<PS_HEAD>();
   const int nm = 2 + k;
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * nm) return;
@@ -208,6 +217,7 @@ __global__ void __launch_bounds__(64) k_rp_hash_small(int B, int n, int k, const
 // inversion (Montgomery trick) for y and the k round challenges
 __global__ void __launch_bounds__(256) k_rp_chal_fr(int B, int n, int k, const int32_t* __restrict__ status,
                                                    uint32_t* __restrict__ ch, uint32_t* __restrict__ tmp) {
+  wave_prio<PS_HEAD>();
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B || status[b] != 0) return;
   uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
@@ -286,6 +296,7 @@ constexpr int PW_LC = 3, PW_CH = 1 << PW_LC;
 __global__ void __launch_bounds__(64) k_rp_powers(int B, int n, int k, const int32_t* __restrict__ status,
                                                   const uint32_t* __restrict__ ch, uint32_t* __restrict__ ypow,
                                                   uint32_t* __restrict__ svec, uint32_t* __restrict__ zvec) {
+  wave_prio<PS_HEAD>();
   const int lc = min(PW_LC, k), cs = 1 << lc, nch = n >> lc;
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * nch) return;
@@ -1632,7 +1643,11 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   const int B = d.B, n = d.n, k = d.k, NC = rlc_ncols(n);
   if (!B) return;
   if (d.excl) (void)hipMemsetAsync(d.excl, 0, (size_t)B * 4, s);
-  FTS_LAUNCH(k_rp_decode, B * rp_npts(k), 256, s, B, rp_npts(k), d.raw, d.pts, d.status);
+  // 64-thread blocks for the elementwise head kernels: beside the previous pass's
+  // fixed-base launch (64-thread blocks, the whole register file) a 256-thread block
+  // waits for four wave slots of one CU to free at once (k_rp_decode 0.07 ms alone,
+  // 1.15 ms there in a 20-batch burst, round 5)
+  FTS_LAUNCH(k_rp_decode, B * rp_npts(k), 64, s, B, rp_npts(k), d.raw, d.pts, d.status);
   tl->mark("k_rp_decode", s, 0);
   FTS_LAUNCH(k_rp_hash_small, B * (2 + k), 64, s, B, n, k, d.raw, d.status, d.ch, d.small_msgs);
   tl->mark("k_rp_hash_small", s, 0);
@@ -1644,7 +1659,8 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
                d.terms, com_fx_slots(n), n + 2);
     tl->mark("k_rp_xd", s2, (double)B * 2 * COST_VB128);
   }
-  FTS_LAUNCH(k_rp_chal_fr, B, g_lat_bs, s, B, n, k, d.status, d.ch, d.scratch);
+  const int lbs = d.com_fixed ? g_lat_bs : g_work_bs;
+  FTS_LAUNCH(k_rp_chal_fr, B, lbs, s, B, n, k, d.status, d.ch, d.scratch);
   tl->mark("k_rp_chal_fr", s, (double)B * (3 * k + 4 * (k + 1) + 12));
   // batch check on s3 (after the caller's hook, e.g. the exclusion of range
   // proofs whose action failed its sigma proof): the weights need only the
@@ -1657,7 +1673,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   auto rlc_prep = [&]() {
     tl->fork(s, s3);
     if (d.pre_rlc) d.pre_rlc(d.pre_rlc_arg, s3);
-    FTS_LAUNCH(k_rlc_prep, B, g_lat_bs, s3, B, n, k, d.status, d.excl, d.ipa_flag, d.sc, d.ch, r.key, r.msc, r.coef);
+    FTS_LAUNCH(k_rlc_prep, B, lbs, s3, B, n, k, d.status, d.excl, d.ipa_flag, d.sc, d.ch, r.key, r.msc, r.coef);
     tl->mark("k_rlc_prep", s3, (double)B * (3 * k + 33));
     (void)hipEventRecord(d.ev_coef, s3);
   };
@@ -1705,7 +1721,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   // beside the fixed-base launch too (3: k_msm_split 6 ms)
   const bool early_sort = (d.rlc_fork == 3 || d.rlc_fork == 4) && !d.com_fixed && d.ev_fx && !d.pre_rlc;
   if (early_sort) {
-    FTS_LAUNCH(k_rlc_prep, B, g_lat_bs, s, B, n, k, d.status, d.excl, d.ipa_flag, d.sc, d.ch, r.key, r.msc, r.coef);
+    FTS_LAUNCH(k_rlc_prep, B, lbs, s, B, n, k, d.status, d.excl, d.ipa_flag, d.sc, d.ch, r.key, r.msc, r.coef);
     tl->mark("k_rlc_prep", s, (double)B * (3 * k + 33));
     (void)hipEventRecord(d.ev_coef, s);
     if (d.rlc_fork == 4) {
@@ -1769,7 +1785,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
       // x0 prefix on the side stream: the H' records and the shared template
       // (cb1 of the message's blocks) do not depend on com, so they are hashed
       // beside the S / com chain; only the suffix waits for com
-      FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s2, B, n, k, d.status, d.x0_msgs, x0_tmpl, 0u, x0_cb1(n), d.x0_mid, d.ch);
+      FTS_LAUNCH(k_rp_x0_hash, B, lbs, s2, B, n, k, d.status, d.x0_msgs, x0_tmpl, 0u, x0_cb1(n), d.x0_mid, d.ch);
       tl->mark("k_rp_x0_prefix", s2, 0);
     }
     const int nch = (n + HS_CHUNK - 1) / HS_CHUNK;
@@ -1789,7 +1805,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
                      n, d.status, d.hp_be, x0_const, d.sc, d.x0_msgs, split ? 1 : 2);
   tl->mark(split ? "k_rp_x0_build_tail" : "k_rp_x0_build", s, 0);
   if (split) tl->fork(s2, s);  // the prefix's midstate
-  FTS_LAUNCH(k_rp_x0_hash, B, g_lat_bs, s, B, n, k, d.status, d.x0_msgs, x0_tmpl, split ? x0_cb1(n) : 0u, 0xffffffffu,
+  FTS_LAUNCH(k_rp_x0_hash, B, lbs, s, B, n, k, d.status, d.x0_msgs, x0_tmpl, split ? x0_cb1(n) : 0u, 0xffffffffu,
              d.x0_mid, d.ch);
   tl->mark("k_rp_x0_hash", s, 0);
   // x0 tail: column Q (needs the weights of k_rlc_prep) and its product, then
@@ -1828,7 +1844,7 @@ void launch_normalize_all(int total, const uint32_t* jac, uint32_t* aff, hipStre
 // per-proof final equations (fallback when the batch combination fails)
 void launch_rp_gather(const RpGather& g, int k, uint8_t* raw, uint32_t* sc, int32_t* status, int32_t* ipa, hipStream_t s) {
   const int per = rp_npts(k) * 4 + RP_NSC * 2 + 1;
-  FTS_LAUNCH(k_rp_gather, (size_t)g.off[g.G] * per, 256, s, g, rp_npts(k), raw, sc, status, ipa);
+  FTS_LAUNCH(k_rp_gather, (size_t)g.off[g.G] * per, 64, s, g, rp_npts(k), raw, sc, status, ipa);
 }
 
 // per-proof final equations of the nsel proofs sel[0 .. nsel) (all B if sel == nullptr)
