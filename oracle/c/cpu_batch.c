@@ -704,8 +704,10 @@ static g1j msm_glv(const aff* pts, const uint8_t* inf, const fe* sc, size_t N, i
   size_t M = 0;
   for (size_t i = 0; i < N; i++) M += !inf[i] && !fzero(sc[i]);
   if (!M) return jid();
+  /* c <= 15: a signed digit reaches +2^(c-1), which must fit the int16_t digit table
+   * (c = 16 wrapped +32768 to -32768: wrong sums from ~2^18 points on, round 5) */
   int c = 4;
-  while (c < 16 && ((size_t)1 << (c + 3)) < 2 * M) c++;
+  while (c < 15 && ((size_t)1 << (c + 3)) < 2 * M) c++;
   const int nwin = 128 / c + 1;
   aff* gp = malloc(sizeof(aff) * 2 * M);
   int16_t* dig = malloc(sizeof(int16_t) * 2 * M * nwin);

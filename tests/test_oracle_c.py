@@ -122,3 +122,23 @@ def test_cpu_pippenger_matches_term_by_term():
         assert cref.msm_pippenger(pb, kb, threads=3) == cref.msm(pb, kb, threads=3), n
     with pytest.raises(ValueError):
         cref.msm_pippenger(b"\x01" * 64, bytes(32))
+
+
+def test_cpu_pippenger_widest_window():
+    """2^18 points: the widest window (c = 15) with ~2^19 GLV halves x 9 windows of
+    random digits, so the edge digit +2^(c-1) occurs (an int16_t digit table
+    wrapped it at c = 16); P_i = (i mod 2^12 + 1) G, closed form sum k_i (i mod 2^12 + 1) G"""
+    import random
+
+    from oracle import bn254 as bn, cref
+    rng = random.Random(0xC3C4)
+    m, n = 1 << 12, 1 << 18
+    base, P = [], None
+    for i in range(m):
+        P = bn.GEN if P is None else bn.g1_add(P, bn.GEN)
+        base.append(bn.g1_bytes(P))
+    pb = b"".join(base) * (n // m)
+    ks = [rng.getrandbits(256) for _ in range(n)]
+    kb = b"".join(k.to_bytes(32, "big") for k in ks)
+    want = bn.g1_bytes(bn.g1_mul(bn.GEN, sum(k * (i % m + 1) for i, k in enumerate(ks)) % bn.R))
+    assert cref.msm_pippenger(pb, kb, threads=8) == want

@@ -4,6 +4,7 @@
 # smoke     __graft_entry__.smoke()
 # tests     pytest -m gpu (full suite)
 # rp        C2 headline, driver shape (20 steps) and steady state (512 steps)
+# s20x5     five consecutive driver-shape runs (20 steps, no CPU columns)
 # prof      rocprofv3 --kernel-trace --stats of the headline; isolated roofline pass summary
 # pmc       FETCH_SIZE / WRITE_SIZE / SQ_* passes (one counter group per run) + FETCH_SIZE
 #           calibration -> traffic_$TAG.json (tools/pmc_traffic.py)
@@ -31,6 +32,10 @@ for s in "$@"; do case $s in
   smoke) step smoke 240 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
   tests) step pytest_gpu 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
          tail -2 $OUT/pytest_gpu.log ;;
+  s20x5) for i in 1 2 3 4 5; do  # the driver-shape line, five consecutive runs
+           step bench_s20_$i 300 python3 -u bench.py --steps 20 --warmup 5 --cpu-sample 0 --host-steps 0
+           json bench_s20_$i
+         done ;;
   rp) step bench_s20 300 python3 -u bench.py --steps 20 --warmup 5; json bench_s20
       step bench 600 python3 -u bench.py --steps 512 --warmup 64; json bench ;;
   prof) rm -rf $OUT/prof
