@@ -4,9 +4,9 @@
 
 namespace fts {
 enum PrioSlot {
-  PS_FIXED,    // k_rp_fixed_exact: the pass's bulk work
+  PS_FIXED,    // k_rp_fixed_exact / k_rp_fixed_all: the pass's bulk work
   PS_HSUM,     // k_rp_hsum_chunks / _join: head of the com chain
-  PS_COMVAR,   // k_rp_com_var
+  PS_COMVAR,   // k_rp_com_var (work path); k_rp_com_tree, k_rp_xd (latency path)
   PS_NORM,     // k_rp_x0_hdr, k_rp_normalize: H' records (x0 stream)
   PS_X0PRE,    // k_rp_x0_hash prefix (beside com)
   PS_X0TAIL,   // k_rp_x0_build, k_rp_x0_hash suffix, Q columns: the pass's tail

@@ -646,16 +646,21 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_MSM_SORT")) c->msm_sort = atoi(e) != 0;
   if (const char* e = getenv("FTS_MAIN_GROUPS")) c->main_groups = atoi(e) != 0;
   if (const char* e = getenv("FTS_FX_SERIAL")) c->fx_serial = atoi(e) != 0;
-  if (const char* e = getenv("FTS_WORK_BS")) g_work_bs = atoi(e) == 256 ? 256 : 64;  // process-wide
+  {  // process-wide, like the priority table: every context sets it (the last one wins)
+    const char* e = getenv("FTS_WORK_BS");
+    g_work_bs = e && atoi(e) == 256 ? 256 : 64;
+  }
   if (const char* e = getenv("FTS_GT1")) c->gt1 = std::max(8, std::min(1024, atoi(e)));
   if (const char* e = getenv("FTS_GT2_MIN")) c->gt2_min = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_GT_ADAPT")) c->gt_adapt = atoi(e) != 0;
-  // FTS_WAVE_PRIO: one digit 0-3 per PrioSlot (device/helpers.hpp), e.g. 02211331313;
-  // the table is per device and process (the last context created on a device sets it)
-  if (const char* e = getenv("FTS_WAVE_PRIO")) {
+  // FTS_WAVE_PRIO: one digit 0-3 per PrioSlot (device/wave_prio.hpp), e.g.
+  // 022113313133; the table is per device and process: every context uploads its
+  // own (the default without the variable), the last one created on a device wins
+  {
     int pr[PS_N] = FTS_WAVE_PRIO_DEFAULT;
-    for (int i = 0; i < PS_N && e[i]; i++)
-      if (e[i] >= '0' && e[i] <= '3') pr[i] = e[i] - '0';
+    if (const char* e = getenv("FTS_WAVE_PRIO"))
+      for (int i = 0; i < PS_N && e[i]; i++)
+        if (e[i] >= '0' && e[i] <= '3') pr[i] = e[i] - '0';
     if (rp_set_wave_prio(pr) != hipSuccess || msm_set_wave_prio(pr) != hipSuccess) return fail(FTS_API_EDEVICE);
   }
   // the batch check's stream (s3: RLC weights + MSM, the longest chain of a small

@@ -557,6 +557,7 @@ __global__ void __launch_bounds__(64, 4) k_rp_fixed_all(int B, int n, int k, con
                                                         const uint32_t* __restrict__ zvec,
                                                         const uint32_t* __restrict__ wtables, uint32_t* __restrict__ hpj,
                                                         uint32_t* __restrict__ terms) {
+  wave_prio<PS_FIXED>();
   const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (size_t)(2 * n + 2) * B) return;
   const int t = (int)(gid / B), b = (int)(gid % B);
@@ -592,6 +593,7 @@ __global__ void __launch_bounds__(256) k_rp_xd(int B, int n, int k, const int32_
                                               const uint32_t* __restrict__ pts, const uint8_t* __restrict__ small_msgs,
                                               uint32_t* __restrict__ vtab, uint32_t* __restrict__ terms, int tstride,
                                               int toff) {
+  wave_prio<PS_COMVAR>();
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= 2 * B) return;
   const int h = gid / B, b = gid % B;
@@ -618,6 +620,7 @@ __global__ void __launch_bounds__(CT_LANES * CT_PROOFS) k_rp_com_tree(int B, int
                                                                       uint32_t* __restrict__ hpj,
                                                                       uint32_t* __restrict__ hpa,
                                                                       uint8_t* __restrict__ hp_be) {
+  wave_prio<PS_COMVAR>();
   __shared__ uint32_t sh[CT_LANES * CT_PROOFS * 24];
   const int l = threadIdx.x % CT_LANES, pl = threadIdx.x / CT_LANES;
   const int b = blockIdx.x * CT_PROOFS + pl;

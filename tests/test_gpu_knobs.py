@@ -7,7 +7,9 @@ Knobs covered elsewhere: FTS_LANES, FTS_COM_FIXED_MAX (test_gpu_rp.py,
 test_gpu_scale.py), FTS_GT1 / FTS_GT2_MIN / FTS_GT_ADAPT (test_gpu_scale.py),
 FTS_NYM_TILE (test_idemix.py), FTS_MAIN_GROUPS (test_gpu_scale.py).  Here:
 FTS_RLC_FORK, FTS_X0_SPLIT, FTS_COALESCE_MAX, FTS_GATHER_US, FTS_GT_ADAPT=0,
-FTS_MSM_SORT."""
+FTS_MSM_SORT, FTS_WIDE_BITS, FTS_WAVE_PRIO, FTS_WORK_BS, FTS_GATHER_TARGET,
+FTS_FX_SERIAL.  FTS_IDLE_GATHER_US /
+FTS_IDLE_QUIET_US: test_gpu_scale.py (the idle-burst split and the blocker tests)."""
 import json
 import os
 import random
@@ -109,7 +111,9 @@ def _tampered_batches(pp, nb, per, seed):
 @pytest.mark.parametrize("env", [
     dict(FTS_COALESCE_MAX=4096, FTS_GATHER_US=3000),   # small coalescing cap, long gather window
     dict(FTS_GATHER_US=0),                             # no gather window
-], ids=["coalesce4096", "gather0"])
+    dict(FTS_GATHER_TARGET=1024, FTS_IDLE_GATHER_US=2000),  # idle burst cut at 2 batches a pass
+    dict(FTS_FX_SERIAL=1),                             # one fixed-base launch at a time across lanes
+], ids=["coalesce4096", "gather0", "target1024", "fx_serial"])
 def test_knob_coalescing(pp_raw, env):
     """8 staged batches of 512 rp32 (3 tampered each) verified concurrently from 8
     threads: however the dispatcher groups them (coalesced passes up to the cap,
@@ -216,3 +220,22 @@ def test_knob_wide_bits(pp_raw, wbits, work_path):
         _golden_check(pp, 32, work_path)
     finally:
         pp.close()
+
+
+@pytest.mark.parametrize("env", [dict(FTS_WAVE_PRIO="000000000000"), dict(FTS_WAVE_PRIO="333333333333"),
+                                 dict(FTS_WORK_BS=256)])
+def test_knob_wave_prio_and_work_bs(pp_raw, env):
+    """FTS_WAVE_PRIO (the s_setprio level of each kernel group, device/wave_prio.hpp)
+    and FTS_WORK_BS (block size of the work path's per-proof latency kernels) are
+    scheduling only: a tampered rp32 pass on the work path gives the same exact
+    verdicts, and the golden vectors stay byte-exact"""
+    pp = _ctx(pp_raw, 32, FTS_LANES=1, FTS_COM_FIXED_MAX=0, **env)
+    try:
+        (b, want), = _tampered_batches(pp, 1, 768, 0x9410)
+        got = b.verify(want_status=True)
+        assert (got == want).all(), np.nonzero(got != want)
+        b.close()
+        _golden_check(pp, 32, True)
+    finally:
+        pp.close()
+        # the next context re-uploads the default priority table
