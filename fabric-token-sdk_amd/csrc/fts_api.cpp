@@ -57,6 +57,9 @@ void launch_rlc_group_test(const RpBatchDev& d, const RlcDev& r, const uint32_t*
                            const int32_t* sel, int G, int gs, uint32_t* gcol, uint32_t* gfix, int32_t* next,
                            uint32_t* next_count, hipStream_t s, Timeline* tl);
 void launch_rp_gather(const RpGather& g, int k, uint8_t* raw, uint32_t* sc, int32_t* status, int32_t* ipa, hipStream_t s);
+void launch_rlc_locate(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, uint32_t* save, int32_t* loc,
+                       hipStream_t s, Timeline* tl);
+void launch_rlc_accept_except(int B, int skip, int32_t* status, const int32_t* ipa_flag, hipStream_t s);
 // ev_stage (optional): recorded on s after the counting sort (stage 1) or the bucket
 // accumulation (stage 2)
 void launch_msm(const MsmPlan& p, const uint32_t* points, const uint32_t* scalars, const uint32_t* extra, int nextra,
@@ -144,6 +147,7 @@ struct Workspace {
   DBuf r_key, r_msc, r_coef, r_colsum, r_fixed, r_flag, r_gcol, r_gfix, r_sel, r_next, r_cnt, m_keys,
       m_counts, m_offsets, m_cursor, m_sorted, m_buckets, m_segs, m_wins, m_out, m_scratch, m_win, m_choff, m_chbkt, m_partials;
   DBuf r_msel, r_mcol, r_mfix, r_mqfix, r_mflag;  // the per-caller-batch combination of a coalesced pass
+  DBuf r_loc, r_save;  // the single-fault locator: located proof, the failed combination S
   // action (transfer / issue) batches
   DBuf rp_raw, rp_sc, rp_status, rp_ipa;
   DBuf s_act, s_raw, s_owner, s_pts, s_sc, s_status, s_work, s_terms, s_aff, s_affoff, s_msgs, s_jac, s_scratch;
@@ -154,7 +158,7 @@ struct Workspace {
     for (DBuf* b : {&open_rec, &pv, &sp, &pts, &ch, &small, &hpj, &hpa, &hpbe, &x0, &x0mid, &terms, &scratch, &ypow, &svec, &zvec, &rp_excl, &rp_raw, &rp_sc, &m_choff, &m_chbkt, &m_partials,
                     &rp_status, &rp_ipa, &s_act, &s_raw, &s_owner, &s_pts, &s_sc, &s_status, &s_work, &s_terms, &s_aff,
                     &s_affoff, &s_msgs, &s_jac, &s_scratch, &r_key, &r_msc, &r_coef, &r_colsum, &r_fixed, &r_flag, &r_gcol, &r_gfix,
-                    &r_sel, &r_next, &r_cnt, &r_msel, &r_mcol, &r_mfix, &r_mqfix, &r_mflag,
+                    &r_sel, &r_next, &r_cnt, &r_msel, &r_mcol, &r_mfix, &r_mqfix, &r_mflag, &r_loc, &r_save,
                     &m_keys, &m_counts, &m_offsets, &m_cursor, &m_sorted, &m_buckets, &m_segs, &m_wins, &m_out,
                     &m_scratch, &m_win})
       b->release();
@@ -467,6 +471,13 @@ struct fts_ctx {
   // latency whatever their number up to ~8k proofs (tools/gt_sweep.sh, C5 1 % tampered:
   // 64/2048 -> 256/8192 = 485k -> 533k actions/s)
   int gt1 = 256, gt2_min = 8192;
+  // FTS_LOCATE: after a failed (ungrouped) batch check whose caller batches are all
+  // sparse, first the single-fault locator (rp_locate_single): one index-weighted
+  // recombination + a lane per proof, instead of the group test's grouped MSM
+  bool locate = true;
+  // after a miss (several bad proofs) the next 8 failing passes skip the locator:
+  // a stream of multi-fault passes pays it on one failing pass in nine
+  std::atomic<int> locate_skip{0};
   // FTS_GT_ADAPT: a staged caller batch's round-1 group size follows the bad-proof
   // density of ITS last failed verification (fts_rp_batch::dense; per caller batch,
   // so one caller's tampered batches never change the fallback of another's).
@@ -653,6 +664,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_GT1")) c->gt1 = std::max(8, std::min(1024, atoi(e)));
   if (const char* e = getenv("FTS_GT2_MIN")) c->gt2_min = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_GT_ADAPT")) c->gt_adapt = atoi(e) != 0;
+  if (const char* e = getenv("FTS_LOCATE")) c->locate = atoi(e) != 0;
   // FTS_WAVE_PRIO: one digit 0-3 per PrioSlot (device/wave_prio.hpp), e.g.
   // 022113313133; the table is per device and process: every context uploads its
   // own (the default without the variable), the last one created on a device wins
@@ -1444,7 +1456,39 @@ static int rp_enqueue(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc
   return FTS_API_OK;
 }
 
-// wait for an enqueued pass; on a failed combination, the group-test fallback
+// The single-fault locator (rp_kernels.hip k_rlc_locate): S' = (j + 1) S locates
+// the one bad proof j of a failed combination S.  Its per-proof final equations
+// give its verdict (bulletproof.go:314-324, ipa.go:254-259), and every other proof
+// is accepted -- the combination of the others is S - rho_j E_j = 0 with the
+// batch check's own soundness.  -> 1 decided, 0 not a single fault (the group test
+// decides), < 0 an API error.  The workspace's weights are index-weighted after it,
+// which the group test accepts as its weights (any fresh random weights do).
+static int rp_locate_single(fts_ctx* c, Lane& L, RpPass& P) {
+  const int B = P.d.B;
+  Workspace& w = L.ws;
+  if (w.r_loc.ensure(4) || w.r_save.ensure(96)) return FTS_API_ENOMEM;
+  L.tl.fallback();
+  int32_t* loc = w.r_loc.as<int32_t>();
+  HIP_OK(hipMemsetAsync(loc, 0xff, 4, L.s));
+  launch_rlc_locate(P.d, P.r, c->d_tables, w.r_save.as<uint32_t>(), loc, L.s, &L.tl);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(&L.pin->flag, loc, 4, hipMemcpyDeviceToHost, L.s));
+  HIP_OK(L.sync());
+  const int i = L.pin->flag;
+  if (i < 0 || i >= B) return 0;
+  launch_rp_fallback(P.d, c->d_tables, loc, 1, L.s, &L.tl);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(&L.pin->flag, P.d.status + i, 4, hipMemcpyDeviceToHost, L.s));
+  HIP_OK(L.sync());
+  if (L.pin->flag == FTS_OK) return 0;  // not a fault after all: the group test decides
+  launch_rlc_accept_except(B, i, P.d.status, P.d.ipa_flag, L.s);
+  HIP_OK(hipGetLastError());
+  std::fill(P.dense.begin(), P.dense.end(), 0);
+  return 1;
+}
+
+// wait for an enqueued pass; on a failed combination, the single-fault locator,
+// then (several bad proofs) the group-test fallback
 static int rp_finish(fts_ctx* c, Lane& L, RpPass& P) {
   HIP_OK(L.sync());
   const double t_wait = now_ms();
@@ -1458,6 +1502,16 @@ static int rp_finish(fts_ctx* c, Lane& L, RpPass& P) {
     std::vector<uint8_t> only((size_t)P.r.G, 0);
     for (int q = 0; q < P.r.G; q++) only[q] = L.pin->gflag[q] ? 0 : 1;
     return rp_group_fallback(c, L, P.d, P.r, P.groups, P.dense, &only);
+  }
+  if (c->locate && P.d.B > 1 && std::none_of(P.dense.begin(), P.dense.end(), [](uint8_t x) { return x != 0; })) {
+    if (c->locate_skip.load() > 0) {
+      c->locate_skip--;
+    } else {
+      const int rc = rp_locate_single(c, L, P);
+      if (rc < 0) return rc;
+      if (rc == 1) return FTS_API_OK;
+      c->locate_skip = 8;
+    }
   }
   return rp_group_fallback(c, L, P.d, P.r, P.groups, P.dense);
 }

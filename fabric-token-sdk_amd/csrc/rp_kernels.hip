@@ -1257,7 +1257,7 @@ __global__ void __launch_bounds__(256) k_rlc_prep(int B, int n, int k, const int
                                                  const int32_t* __restrict__ excl,
                                                  const int32_t* __restrict__ ipa_flag, const uint32_t* __restrict__ sc,
                                                  const uint32_t* __restrict__ ch, const uint32_t* __restrict__ key,
-                                                 uint32_t* __restrict__ msc, uint32_t* __restrict__ coef) {
+                                                 uint32_t* __restrict__ msc, uint32_t* __restrict__ coef, int idxw = 0) {
   wave_prio<PS_SORT>();
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
@@ -1275,6 +1275,12 @@ __global__ void __launch_bounds__(256) k_rlc_prep(int B, int n, int k, const int
   for (int q = 0; q < 8; q++) kk[q] = key[q];
   chacha20_block(kk, (uint32_t)b, blk);
   Fr rho = fr_from_u256(blk), rho2 = fr_from_u256(blk + 8);
+  if (idxw) {  // the single-fault locator's sum: both weights of proof b times b + 1
+    const uint32_t w[8] = {(uint32_t)b + 1u, 0, 0, 0, 0, 0, 0, 0};
+    const Fr wb = fr_from_canon(w);
+    rho = fr_mul(rho, wb);
+    rho2 = fr_mul(rho2, wb);
+  }
   const uint32_t* C = ch + (size_t)b * rp_nch(k) * 8;
   const uint32_t* S = sc + (size_t)b * RP_NSC * 8;
   Fr x, x2, z2, pol;
@@ -1506,6 +1512,45 @@ __global__ void __launch_bounds__(64) k_rlc_finalize(int B, const uint32_t* __re
   const bool pass = g1j_is_identity(e);
   if (b == 0) *flag = pass ? 1 : 0;
   if (b < B && pass && status[b] == 0 && ipa_flag[b] != 0) status[b] = ipa_flag[b];
+}
+
+// Single-fault locator (round 5).  When the batch combination S = sum_b rho_b E_b
+// (E_b: proof b's final equations, rho_b its weights) is not the identity, the
+// same combination with weights (b + 1) rho_b gives S' = sum_b (b + 1) rho_b E_b.
+// If exactly one proof i is bad, S' = (i + 1) S; conversely S' = (j + 1) S means
+// sum_b (b - j) rho_b E_b = 0, which for two or more bad proofs (or one bad proof
+// other than j) holds only with probability ~1/r over the fresh random weights --
+// the same soundness as the batch check itself.  Lane j tests S' == (j + 1) S.
+__global__ void __launch_bounds__(64) k_rlc_total(const uint32_t* __restrict__ msm_out,
+                                                  const uint32_t* __restrict__ addend, uint32_t* __restrict__ out) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  G1J e = load_g1j(msm_out);
+  add_inl(e, load_g1j(addend));
+  store_g1j(out, e);
+}
+__global__ void __launch_bounds__(64) k_rlc_locate(int B, const uint32_t* __restrict__ total,
+                                                   const uint32_t* __restrict__ msm_out,
+                                                   const uint32_t* __restrict__ addend, int32_t* __restrict__ loc) {
+  wave_prio<PS_FIN>();
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= B) return;
+  G1J t = load_g1j(msm_out);
+  add_inl(t, load_g1j(addend));
+  const G1J S = load_g1j(total);
+  const uint32_t m = (uint32_t)j + 1u;
+  G1J P = g1j_identity();
+  for (int bit = 31 - __builtin_clz(m); bit >= 0; bit--) {
+    P = g1j_dbl(P);
+    if ((m >> bit) & 1u) P = g1j_add(P, S);
+  }
+  if (g1j_eq(P, t)) loc[0] = j;
+}
+// after the locator: every proof but `skip` whose deferred IPA structural verdict is
+// pending takes it (the combination of the others closed, as in k_rlc_finalize)
+__global__ void __launch_bounds__(256) k_rlc_accept_except(int B, int skip, int32_t* __restrict__ status,
+                                                           const int32_t* __restrict__ ipa_flag) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B && b != skip && status[b] == 0 && ipa_flag[b] != 0) status[b] = ipa_flag[b];
 }
 
 // group test verdicts: lane per proof slot j of the selection (group j / gs);
@@ -1838,6 +1883,35 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
   FTS_LAUNCH(k_rlc_finalize, B, 64, s, B, r.plan.out, r.fixed + (size_t)(NC - 1) * 24, d.excl, d.status, d.ipa_flag,
              r.flag);
   tl->mark("k_rlc_finalize", s, 0);
+}
+
+// the single-fault locator's device work on s, after a failed batch check of the
+// (ungrouped) pass d: saves S, recomputes the combination with index weights into
+// the same workspace (weights, columns, MSM, column Q) and writes to loc[0] the j
+// with S' = (j + 1) S (loc[0] must be -1 before)
+void launch_rlc_locate(const RpBatchDev& d, const RlcDev& r, const uint32_t* tables, uint32_t* save, int32_t* loc,
+                       hipStream_t s, Timeline* tl) {
+  const int B = d.B, n = d.n, k = d.k, NC = rlc_ncols(n);
+  hipLaunchKernelGGL(k_rlc_total, dim3(1), dim3(64), 0, s, r.plan.out, r.fixed + (size_t)(NC - 1) * 24, save);
+  FTS_LAUNCH(k_rlc_prep, B, 64, s, B, n, k, d.status, d.excl, d.ipa_flag, d.sc, d.ch, r.key, r.msc, r.coef, 1);
+  tl->mark("k_rlc_prep", s, (double)B * (3 * k + 34));
+  hipLaunchKernelGGL(k_rlc_columns, dim3(NC - 1, 1), dim3(256), 0, s, B, n, k, B, 0, (const int32_t*)nullptr, d.ch,
+                     r.coef, d.ypow, d.svec, d.zvec, r.colsum);
+  tl->mark("k_rlc_columns", s, (double)B * 4 * n);
+  FTS_LAUNCH(k_rlc_fixed, (size_t)(NC - 1) * FB_NW, RF_ITEMS * FB_NW, s, n, 1, 0, NC - 1, r.colsum, tables, r.fixed);
+  tl->mark("k_rlc_fixed", s, (double)(NC - 1) * (FB_NW * 3 + (FB_NW - 1) * COST_ADD));
+  launch_msm(r.plan, d.pts, r.msc, r.fixed, NC - 1, r.msm_scratch, s, s, tl);
+  const int gsq = (B + RQ_PARTS - 1) / RQ_PARTS;
+  hipLaunchKernelGGL(k_rlc_columns, dim3(1, RQ_PARTS), dim3(256), 0, s, B, n, k, gsq, NC - 1,
+                     (const int32_t*)nullptr, d.ch, r.coef, d.ypow, d.svec, d.zvec, r.colsum + (size_t)NC * 8);
+  hipLaunchKernelGGL(k_rlc_qsum, dim3(1), dim3(RQ_PARTS), 0, s, NC, NC - 1, r.colsum);
+  FTS_LAUNCH(k_rlc_fixed, FB_NW, RF_ITEMS * FB_NW, s, n, 1, NC - 1, 1, r.colsum, tables, r.fixed);
+  tl->mark("k_rlc_q", s, (double)B + FB_NW * 3 + (FB_NW - 1) * COST_ADD);
+  FTS_LAUNCH(k_rlc_locate, B, 64, s, B, save, r.plan.out, r.fixed + (size_t)(NC - 1) * 24, loc);
+  tl->mark("k_rlc_locate", s, (double)B * 28 * COST_ADD);
+}
+void launch_rlc_accept_except(int B, int skip, int32_t* status, const int32_t* ipa_flag, hipStream_t s) {
+  FTS_LAUNCH(k_rlc_accept_except, B, 256, s, B, skip, status, ipa_flag);
 }
 
 void launch_normalize_all(int total, const uint32_t* jac, uint32_t* aff, hipStream_t s) {

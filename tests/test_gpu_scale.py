@@ -162,7 +162,8 @@ def test_one_bad_proof_in_coalesced_pass_group_test(pp_raw, main_groups):
     proof's own batch -- get the per-proof final equations; every verdict equals
     the reference's (rangecorrectness.go:141-160).  FTS_MAIN_GROUPS=1: the pass
     checks one combination per caller batch, so the group test covers the bad
-    proof's batch only; 0 (default): the whole pass."""
+    proof's batch only; 0 (default): one combination over the pass, whose single
+    bad proof the locator finds (round 5; the group test only when it misses)."""
     import os
     import threading
 
@@ -212,14 +213,19 @@ def test_one_bad_proof_in_coalesced_pass_group_test(pp_raw, main_groups):
         assert out[t] == expect[t], t
     assert merged[bad_batch] > 1, merged
     tb = tim[bad_batch]
-    assert "fb:k_rlc_group_final" in tb and "fb:k_rp_terms_fixed" in tb, sorted(tb)
     per_proof = tb["fb:k_rp_terms_fixed"][1] / ((3 + 2 * 16) * 15 * 11 * 136)
-    # the bad proof's round-1 group (256 proofs of its own batch), not the pass (4,096)
-    assert 1 <= round(per_proof) <= 256, per_proof
-    # the group test's grouped sums: the bad proof's own batch (512 proofs) with the
-    # per-caller-batch combination, else the whole pass
-    grouped = tb["fb:k_rlc_group_columns"][1] / (4 * 16 * 136)
-    assert round(grouped) == (m if main_groups else m * merged[bad_batch]), (grouped, merged[bad_batch])
+    if not main_groups:
+        # one combination over the pass: the single-fault locator (rp_locate_single)
+        # finds the bad proof; only its own per-proof equations run, no group test
+        assert "fb:k_rlc_locate" in tb and "fb:k_rlc_group_final" not in tb, sorted(tb)
+        assert round(per_proof) == 1, per_proof
+    else:
+        assert "fb:k_rlc_group_final" in tb and "fb:k_rp_terms_fixed" in tb, sorted(tb)
+        # the bad proof's round-1 group (256 proofs of its own batch), not the pass (4,096)
+        assert 1 <= round(per_proof) <= 256, per_proof
+        # the group test's grouped sums: the bad proof's own batch (512 proofs) only
+        grouped = tb["fb:k_rlc_group_columns"][1] / (4 * 16 * 136)
+        assert round(grouped) == m, (grouped, merged[bad_batch])
     for b in batches:
         b.close()
     pp.close()
@@ -518,3 +524,93 @@ def test_idle_burst_splits_into_even_passes(pp_raw):
     for b in batches:
         b.close()
     pp.close()
+
+
+@pytest.mark.gpu
+def test_single_fault_locator(pp_raw):
+    """fts_api.cpp rp_locate_single / rp_kernels.hip k_rlc_locate: a failed batch
+    check with ONE bad proof is decided by the index-weighted recombination
+    (S' = (i + 1) S) and that proof's per-proof equations, without the group test;
+    the other proofs' deferred IPA structural verdicts (a truncated IPA: "invalid
+    IPA proof") still become final.  Two bad proofs: the locator misses, the group
+    test decides, and the next (sparse) failing pass skips the locator.  FTS_LOCATE=0: group
+    test only.  Every verdict is the oracle's (bulletproof.go:314-324, ipa.go:195-259)."""
+    import os
+
+    import fts_gpu
+    from oracle import pp as oppm
+
+    opp = oppm.load_pp(pp_raw).with_bit_length(16)
+    status_of = {None: 0, "invalid range proof": 3, "invalid IPA": 6, "invalid IPA proof": 5}
+
+    def ctx(**env):
+        env = {k: str(v) for k, v in dict(FTS_LANES="1", FTS_IDLE_GATHER_US="0", **env).items()}
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            return fts_gpu.PublicParams(pp_raw, bit_length=16, device=0)
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+
+    rng = random.Random(0x51F0)
+    m = 640
+
+    def batch(pp, bad, seed):
+        vals = [rng.getrandbits(16) for _ in range(m)]
+        bfs = [rng.randrange(bn.R).to_bytes(32, "big") for _ in range(m)]
+        proofs, coms = pp.prove_range_batch_gpu(vals, bfs, seed=seed)
+        for i, kind in bad.items():
+            r = zkat.RangeProof.deserialize(proofs[i])
+            if kind == "T1":
+                r.data.T1 = bn.g1_add(r.data.T1, bn.GEN)
+            elif kind == "L":
+                r.ipa.L[1] = bn.g1_add(r.ipa.L[1], bn.GEN)
+            else:  # "short": one IPA round missing (a deferred structural verdict)
+                r.ipa.L, r.ipa.R = r.ipa.L[:2], r.ipa.R[:2]
+            proofs[i] = r.serialize()
+        exp = [0] * m
+        for i in bad:
+            err = zkat.rp_verify(bn.g1_from_bytes(coms[i]), opp.ped[1:], opp.left, opp.right, opp.P, opp.Q,
+                                 opp.rounds, 16, zkat.RangeProof.deserialize(proofs[i]))
+            exp[i] = status_of[err]
+        return pp.stage_range_proofs(proofs, coms), exp
+
+    def run(b):
+        st = [int(x) for x in b.verify()]
+        names, _ = _raw_timing_names(b)
+        return st, names
+
+    pp = ctx()
+    try:
+        for bad in ({333: "T1", 17: "short"}, {0: "L"}, {m - 1: "T1"}):
+            b, exp = batch(pp, bad, 0x51F1 + len(bad))
+            st, names = run(b)
+            assert st == exp, {i: (st[i], exp[i]) for i in range(m) if st[i] != exp[i]}
+            assert "fb:k_rlc_locate" in names and "fb:k_rlc_group_final" not in names, names
+            b.close()
+        # two bad proofs: the locator misses, the group test decides
+        b2, exp2 = batch(pp, {5: "T1", 400: "L"}, 0x51F9)
+        st, names = run(b2)
+        assert st == exp2 and "fb:k_rlc_locate" in names and "fb:k_rlc_group_final" in names, names
+        st, names = run(b2)  # now a dense batch (FTS_GT_ADAPT): no locator
+        assert st == exp2 and "fb:k_rlc_locate" not in names and "fb:k_rlc_group_final" in names, names
+        b2.close()
+        # after the miss, the next failing passes skip the locator (fts_ctx::locate_skip)
+        b3, exp3 = batch(pp, {222: "L"}, 0x51FB)
+        st, names = run(b3)
+        assert st == exp3 and "fb:k_rlc_locate" not in names and "fb:k_rlc_group_final" in names, names
+        b3.close()
+    finally:
+        pp.close()
+    pp = ctx(FTS_LOCATE=0)
+    try:
+        b, exp = batch(pp, {100: "T1"}, 0x51FA)
+        st, names = run(b)
+        assert st == exp and "fb:k_rlc_locate" not in names and "fb:k_rlc_group_final" in names, names
+        b.close()
+    finally:
+        pp.close()
