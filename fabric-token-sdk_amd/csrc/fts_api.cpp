@@ -475,9 +475,10 @@ struct fts_ctx {
   // sparse, first the single-fault locator (rp_locate_single): one index-weighted
   // recombination + a lane per proof, instead of the group test's grouped MSM
   bool locate = true;
-  // after a miss (several bad proofs) the next 8 failing passes skip the locator:
-  // a stream of multi-fault passes pays it on one failing pass in nine
-  std::atomic<int> locate_skip{0};
+  // after a miss (several bad proofs) the next locate_backoff failing passes skip
+  // the locator, the backoff doubling per consecutive miss (8 .. 256) and reset
+  // by a hit: a stream of multi-fault passes (C5, tampered C2) pays it rarely
+  std::atomic<int> locate_skip{0}, locate_backoff{8};
   // FTS_GT_ADAPT: a staged caller batch's round-1 group size follows the bad-proof
   // density of ITS last failed verification (fts_rp_batch::dense; per caller batch,
   // so one caller's tampered batches never change the fallback of another's).
@@ -1509,8 +1510,13 @@ static int rp_finish(fts_ctx* c, Lane& L, RpPass& P) {
     } else {
       const int rc = rp_locate_single(c, L, P);
       if (rc < 0) return rc;
-      if (rc == 1) return FTS_API_OK;
-      c->locate_skip = 8;
+      if (rc == 1) {
+        c->locate_backoff = 8;
+        return FTS_API_OK;
+      }
+      const int bo = c->locate_backoff.load();
+      c->locate_skip = bo;
+      c->locate_backoff = std::min(2 * bo, 256);
     }
   }
   return rp_group_fallback(c, L, P.d, P.r, P.groups, P.dense);
