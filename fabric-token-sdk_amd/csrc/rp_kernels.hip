@@ -1396,10 +1396,11 @@ __global__ void __launch_bounds__(256) k_rlc_columns(int B, int n, int k, int gs
 // k_rlc_columns wrote per slice of proofs (rows 1..RQ_PARTS of colsum) into row 0.
 // (One block over all B proofs took 0.76 ms at 81,920 on the x0-dependent tail.)
 constexpr int RQ_PARTS = 64;
-__global__ void __launch_bounds__(64) k_rlc_qsum(int ncols, int col, uint32_t* __restrict__ colsum) {
+// (block x sums column col + x: the locator splits every column this way)
+__global__ void __launch_bounds__(64) k_rlc_qsum(int ncols, int col0, uint32_t* __restrict__ colsum) {
   wave_prio<PS_FIN>();
   __shared__ uint32_t sh[RQ_PARTS * 8];
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, col = col0 + blockIdx.x;
   Fr v;  // plain residues: the sum is the same in either representation
   load_f(colsum + ((size_t)(1 + t) * ncols + col) * 8, v);
   store_f(sh + t * 8, v);
@@ -1895,13 +1896,16 @@ void launch_rlc_locate(const RpBatchDev& d, const RlcDev& r, const uint32_t* tab
   hipLaunchKernelGGL(k_rlc_total, dim3(1), dim3(64), 0, s, r.plan.out, r.fixed + (size_t)(NC - 1) * 24, save);
   FTS_LAUNCH(k_rlc_prep, B, 64, s, B, n, k, d.status, d.excl, d.ipa_flag, d.sc, d.ch, r.key, r.msc, r.coef, 1);
   tl->mark("k_rlc_prep", s, (double)B * (3 * k + 34));
-  hipLaunchKernelGGL(k_rlc_columns, dim3(NC - 1, 1), dim3(256), 0, s, B, n, k, B, 0, (const int32_t*)nullptr, d.ch,
-                     r.coef, d.ypow, d.svec, d.zvec, r.colsum);
+  // alone on the GPU here: every column split over RQ_PARTS slices of proofs (NC x 64
+  // blocks instead of NC), the partial rows then summed per column
+  const int gsq = (B + RQ_PARTS - 1) / RQ_PARTS;
+  hipLaunchKernelGGL(k_rlc_columns, dim3(NC - 1, RQ_PARTS), dim3(256), 0, s, B, n, k, gsq, 0,
+                     (const int32_t*)nullptr, d.ch, r.coef, d.ypow, d.svec, d.zvec, r.colsum + (size_t)NC * 8);
+  hipLaunchKernelGGL(k_rlc_qsum, dim3(NC - 1), dim3(RQ_PARTS), 0, s, NC, 0, r.colsum);
   tl->mark("k_rlc_columns", s, (double)B * 4 * n);
   FTS_LAUNCH(k_rlc_fixed, (size_t)(NC - 1) * FB_NW, RF_ITEMS * FB_NW, s, n, 1, 0, NC - 1, r.colsum, tables, r.fixed);
   tl->mark("k_rlc_fixed", s, (double)(NC - 1) * (FB_NW * 3 + (FB_NW - 1) * COST_ADD));
   launch_msm(r.plan, d.pts, r.msc, r.fixed, NC - 1, r.msm_scratch, s, s, tl);
-  const int gsq = (B + RQ_PARTS - 1) / RQ_PARTS;
   hipLaunchKernelGGL(k_rlc_columns, dim3(1, RQ_PARTS), dim3(256), 0, s, B, n, k, gsq, NC - 1,
                      (const int32_t*)nullptr, d.ch, r.coef, d.ypow, d.svec, d.zvec, r.colsum + (size_t)NC * 8);
   hipLaunchKernelGGL(k_rlc_qsum, dim3(1), dim3(RQ_PARTS), 0, s, NC, NC - 1, r.colsum);
