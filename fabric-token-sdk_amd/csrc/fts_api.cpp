@@ -49,7 +49,7 @@ size_t wide_build_scratch_bytes(int nb, int wbits);
 size_t fbw_words_per_base(int wbits);
 // wave priority table (helpers.hpp PrioSlot) of rp_kernels.hip and msm.hip's kernels
 hipError_t rp_set_wave_prio(const int* p);
-extern int g_work_bs;  // rp_kernels.hip (FTS_WORK_BS)
+extern std::atomic<int> g_work_bs;  // rp_kernels.hip (FTS_WORK_BS)
 hipError_t msm_set_wave_prio(const int* p);
 void launch_rp_fallback(const RpBatchDev& d, const uint32_t* tables, const int32_t* sel, int nsel, hipStream_t s,
                         Timeline* tl);
@@ -660,7 +660,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_FX_SERIAL")) c->fx_serial = atoi(e) != 0;
   {  // process-wide, like the priority table: every context sets it (the last one wins)
     const char* e = getenv("FTS_WORK_BS");
-    g_work_bs = e && atoi(e) == 256 ? 256 : 64;
+    g_work_bs.store(e && atoi(e) == 256 ? 256 : 64, std::memory_order_relaxed);
   }
   if (const char* e = getenv("FTS_GT1")) c->gt1 = std::max(8, std::min(1024, atoi(e)));
   if (const char* e = getenv("FTS_GT2_MIN")) c->gt2_min = std::max(0, atoi(e));

@@ -24,6 +24,7 @@
 //   S   k_rlc_columns/fixed (Q), finalize   column Q (needs x0), verdict
 //   k_rp_terms_fixed / k_rp_terms_var / k_rp_check: per-proof fallback
 //
+#include <atomic>
 #include "device/g1.hpp"
 #include "device/fixed_base.hpp"
 #include "device/glv.hpp"
@@ -47,7 +48,7 @@ int g_lat_bs = 256;
 // (64-thread blocks filling the register file), where a 256-thread block waits for
 // four wave slots of one CU at once (k_rp_chal_fr 0.12 ms alone, 1.1 ms there;
 // k_rlc_prep 0.18 -> 1.8 ms in a 20-batch burst, round 5)
-int g_work_bs = 64;
+std::atomic<int> g_work_bs{64};  // written by context creation while other lanes launch
 // block size of the work path's S / com chain kernels
 constexpr int g_chain_bs = 64;
 
@@ -1708,7 +1709,7 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
                d.terms, com_fx_slots(n), n + 2);
     tl->mark("k_rp_xd", s2, (double)B * 2 * COST_VB128);
   }
-  const int lbs = d.com_fixed ? g_lat_bs : g_work_bs;
+  const int lbs = d.com_fixed ? g_lat_bs : g_work_bs.load(std::memory_order_relaxed);
   FTS_LAUNCH(k_rp_chal_fr, B, lbs, s, B, n, k, d.status, d.ch, d.scratch);
   tl->mark("k_rp_chal_fr", s, (double)B * (3 * k + 4 * (k + 1) + 12));
   // batch check on s3 (after the caller's hook, e.g. the exclusion of range
