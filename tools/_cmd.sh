@@ -1,6 +1,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r05z; mkdir -p $O
-timeout -k 10 240 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
-timeout -k 10 600 python3 -u -m pytest tests/test_gpu_rp.py tests/test_gpu_headline.py tests/test_gpu_knobs.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pt.log 2>&1 || { tail -30 $O/pt.log; exit 1; }
-tail -1 $O/pt.log
+O=gpurun_out/r05p2; mkdir -p $O
+L=fabric-token-sdk_amd/lib/libfts_gpu.so
+TAG=r05p2 LIBS="$L $L@FTS_WAVE_PRIO=022223313133 $L@FTS_WAVE_PRIO=022333313133" bash tools/trace_iso.sh > $O/traces.txt 2>&1 || exit 1
+grep "^==\|pass span" $O/traces.txt
+TAG=r05p2 LIBS="$L $L@FTS_WAVE_PRIO=022223313133 $L@FTS_WAVE_PRIO=022333313133" bash tools/ab_session.sh burst s512
