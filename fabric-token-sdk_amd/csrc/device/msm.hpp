@@ -103,12 +103,16 @@ inline double msm_cost(int N, int c) {
   return (double)nw * ((double)N * 11.0 + (double)(1 << c) * 16.0);
 }
 
+// largest window width a plan may take (FTS_MSM_MAXC, set by context creation;
+// process-wide): narrower windows trade bucket-phase work for a shorter reduction
+inline int g_msm_maxc = 16;
+
 // G groups of ptsg points (N = G * ptsg, or fewer in the last group); the window
 // width minimises the per-group bucket cost
 inline void msm_layout_groups(int N, int G, int ptsg, MsmPlan& p) {
   const int NV = 2 * N, NVg = 2 * ptsg;
   int best = 4;
-  for (int c = 5; c <= 16; c++)
+  for (int c = 5; c <= g_msm_maxc; c++)
     if (msm_cost(NVg, c) < msm_cost(NVg, best)) best = c;
   const int c = best;
   const int nw = (MSM_BITS + c - 1) / c;

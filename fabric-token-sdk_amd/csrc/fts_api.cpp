@@ -666,6 +666,10 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_GT2_MIN")) c->gt2_min = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_GT_ADAPT")) c->gt_adapt = atoi(e) != 0;
   if (const char* e = getenv("FTS_LOCATE")) c->locate = atoi(e) != 0;
+  {
+    const char* e = getenv("FTS_MSM_MAXC");
+    g_msm_maxc = e ? std::max(8, std::min(16, atoi(e))) : 16;
+  }
   // FTS_WAVE_PRIO: one digit 0-3 per PrioSlot (device/wave_prio.hpp), e.g.
   // 022113313133; the table is per device and process: every context uploads its
   // own (the default without the variable), the last one created on a device wins

@@ -8,7 +8,7 @@ test_gpu_scale.py), FTS_GT1 / FTS_GT2_MIN / FTS_GT_ADAPT (test_gpu_scale.py),
 FTS_NYM_TILE (test_idemix.py), FTS_MAIN_GROUPS (test_gpu_scale.py).  Here:
 FTS_RLC_FORK, FTS_X0_SPLIT, FTS_COALESCE_MAX, FTS_GATHER_US, FTS_GT_ADAPT=0,
 FTS_MSM_SORT, FTS_WIDE_BITS, FTS_WAVE_PRIO, FTS_WORK_BS, FTS_GATHER_TARGET,
-FTS_FX_SERIAL.  FTS_IDLE_GATHER_US /
+FTS_FX_SERIAL, FTS_MSM_MAXC.  FTS_IDLE_GATHER_US /
 FTS_IDLE_QUIET_US: test_gpu_scale.py (the idle-burst split and the blocker tests)."""
 import json
 import os
@@ -223,12 +223,13 @@ def test_knob_wide_bits(pp_raw, wbits, work_path):
 
 
 @pytest.mark.parametrize("env", [dict(FTS_WAVE_PRIO="000000000000"), dict(FTS_WAVE_PRIO="333333333333"),
-                                 dict(FTS_WORK_BS=256)])
+                                 dict(FTS_WORK_BS=256), dict(FTS_MSM_MAXC=12)])
 def test_knob_wave_prio_and_work_bs(pp_raw, env):
-    """FTS_WAVE_PRIO (the s_setprio level of each kernel group, device/wave_prio.hpp)
-    and FTS_WORK_BS (block size of the work path's per-proof latency kernels) are
-    scheduling only: a tampered rp32 pass on the work path gives the same exact
-    verdicts, and the golden vectors stay byte-exact"""
+    """FTS_WAVE_PRIO (the s_setprio level of each kernel group, device/wave_prio.hpp),
+    FTS_WORK_BS (block size of the work path's per-proof latency kernels) and
+    FTS_MSM_MAXC (the widest MSM window a plan takes) change scheduling and the MSM
+    plan only: a tampered rp32 pass on the work path gives the same exact verdicts,
+    and the golden vectors stay byte-exact"""
     pp = _ctx(pp_raw, 32, FTS_LANES=1, FTS_COM_FIXED_MAX=0, **env)
     try:
         (b, want), = _tampered_batches(pp, 1, 768, 0x9410)
@@ -238,4 +239,4 @@ def test_knob_wave_prio_and_work_bs(pp_raw, env):
         _golden_check(pp, 32, True)
     finally:
         pp.close()
-        # the next context re-uploads the default priority table
+        # the next context re-uploads the default priority table, block size and window cap
