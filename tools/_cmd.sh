@@ -1,9 +1,10 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r05mc; mkdir -p $O
-L=fabric-token-sdk_amd/lib/libfts_gpu.so
-timeout -k 10 300 python3 -u -m pytest tests/test_gpu_rp.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pt.log 2>&1 || { tail -30 $O/pt.log; exit 1; }
+O=gpurun_out/r05last; mkdir -p $O
+timeout -k 10 240 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_knobs.py tests/test_gpu_msm.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pt.log 2>&1 || { tail -30 $O/pt.log; exit 1; }
 tail -1 $O/pt.log
-TAG=r05mc LIBS="$L $L@FTS_MSM_MAXC=15 $L@FTS_MSM_MAXC=14" bash tools/trace_iso.sh > $O/traces.txt 2>&1 || exit 1
-grep "^==\|pass span" $O/traces.txt
-TAG=r05mc LIBS="$L $L@FTS_MSM_MAXC=15 $L@FTS_MSM_MAXC=14" bash tools/ab_session.sh burst s512
+timeout -k 10 400 python3 -u bench.py --steps 20 --warmup 5 > $O/bench_s20.log 2>&1 || { tail -20 $O/bench_s20.log; exit 1; }
+grep '^{' $O/bench_s20.log | tail -1 > $O/bench_s20.json
+python3 -c "import json; d=json.load(open('$O/bench_s20.json')); print(d['value'], d['merged_batches_avg'], d['roofline']['frac'], d['roofline']['traffic'], d['roofline']['traffic_source'], d['library'].get('matches_build_record'))"
