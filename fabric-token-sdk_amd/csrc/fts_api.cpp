@@ -173,25 +173,12 @@ struct Workspace {
 // aggregation goroutines, or bench.py's pipeline) run on different lanes, so
 // one batch's latency-bound phases (transcript hashing, doubling chains)
 // overlap another batch's throughput-bound kernels.
-// host-side decoding of one action (verify_actions); kept per lane across calls so
-// the buffers' capacity is reused instead of allocated and freed per action per call
-// (freeing ~50k small vectors that 16 parse threads allocated cost ~5 ms per
-// 8,192-transfer call on the caller's critical path)
-struct ParsedAction {
-  std::vector<uint8_t> sig_raw;   // CT, in..., out...  (64 B each)
-  std::vector<uint32_t> sig_sc;   // scalars
-  int chal_canonical = 0;
-  std::vector<uint8_t> rp_raw;
-  std::vector<uint32_t> rp_sc;
-  std::vector<int32_t> rp_status, rp_ipa;
-};
 
 // pinned window-table slots of Lane::Pinned (msm_prepare_plan)
 enum { MSM_SLOT_PASS = 0, MSM_SLOT_RESERVE, MSM_SLOT_GT_BIG, MSM_SLOT_GT_SMALL, MSM_WIN_SLOTS };
 
 struct Lane {
   int id = 0;
-  std::vector<ParsedAction> parsed;  // verify_actions' per-action decode buffers (reused)
   // completion event created with hipEventBlockingSync: waiting on it sleeps
   // instead of spinning (a spinning waiter per lane burns the process's CPU
   // quota; on a CFS-throttled box that stalls every host thread for ~50 ms
@@ -382,15 +369,61 @@ static inline double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// One fts_rp_batch_verify call waiting for (or being served by) a device pass.
+struct ActSlot;
+// One call waiting for (or being served by) a device pass: a staged range-proof
+// batch (fts_rp_batch_verify, fts_rp_verify_batch), or an action call (transfers /
+// issues / requests) whose range proofs are `b` and whose sigma batch is `act`.
 struct RpReq {
   fts_rp_batch* b;
-  int32_t* status;  // caller's host status array (may be null)
+  int32_t* status;  // caller's host status array of b's proofs (may be null)
+  ActSlot* act = nullptr;
   int rc = 0;
   bool done = false;
   std::chrono::steady_clock::time_point arrived = std::chrono::steady_clock::now();
   std::condition_variable cv;  // this caller's wake-up (targeted, no thundering herd)
-  RpReq(fts_rp_batch* bb, int32_t* st) : b(bb), status(st) {}
+  RpReq(fts_rp_batch* bb, int32_t* st, ActSlot* a = nullptr) : b(bb), status(st), act(a) {}
+};
+
+namespace {
+struct ActionIn {
+  int kind;                    // SIG_TAS / SIG_ST
+  const uint8_t* in;           // n_in * 64
+  size_t n_in;
+  const uint8_t* out;          // n_out * 64 (issue: tokens)
+  size_t n_out;
+  der::Span proof;
+};
+
+struct ActionState {
+  int32_t host_final = -1;     // verdict decided on the host (MALFORMED / TAS_INVALID)
+  int sig = -1;                // index in the call's sigma batch (-1: decided before the layout)
+  bool rc_applicable = false;
+  int rp_base = -1, rp_count = 0;
+  bool rc_count_bad = false;
+};
+}  // namespace
+
+// An action call staged for the dispatcher (act_stage), pooled per context like
+// RpSlot: the call's records parsed straight into pinned host memory in their
+// device layout, one upload into `dev`, and the call's sigma workspace behind
+// them in `dev`.  A device pass then verifies the range proofs of several calls
+// as one batch (gathered like staged range-proof batches) and runs each call's
+// sigma batch in place, so concurrent transfer / issue / request calls share
+// passes instead of taking a lane each.
+struct ActSlot {
+  fts_rp_batch* b = nullptr;  // the call's range proofs: raw / sc / status0 / ipa point into `dev`
+  uint8_t* pin = nullptr;
+  size_t pin_cap = 0;
+  uint8_t* dev = nullptr;
+  size_t dev_cap = 0;
+  hipStream_t s = nullptr;
+  hipEvent_t done = nullptr;   // blocking-sync: the staging caller sleeps
+  SigBatchDev sd{};            // the call's sigma batch (sd.A == 0: none); sd.rp_raw set by the pass
+  int32_t* sig_res = nullptr;  // pinned: sigma verdicts [sd.A], downloaded by the pass
+  std::vector<int32_t> rp_res;  // range-proof verdicts [b->B], scattered by the pass
+  std::vector<ActionState> st;
+  std::vector<int> sig_of;
+  float parse_ms = 0, stage_ms = 0;
 };
 
 // fts_rp_verify_batch staging slot (host DER bytes -> device): pinned host
@@ -419,6 +452,8 @@ struct fts_ctx {
   // their window width: 22 bits (12 additions per product, 1.5 GiB per base) when the
   // device has the memory at context creation, else 20 (13, 436 MiB); FTS_WIDE_BITS
   int wbits = 20;
+  int wbits_forced = 0;  // fts_ctx_opts.wide_bits / FTS_WIDE_BITS: no fallback to 20 bits
+  int nlanes = 0;
   uint8_t* d_x0const = nullptr;
   uint8_t* d_x0tmpl = nullptr;  // x0 message blocks [x0_cb0, x0_cb1): shared by every proof
   size_t table_bytes = 0;
@@ -461,6 +496,17 @@ struct fts_ctx {
   int idle_gather_us = 1000;
   int idle_quiet_us = 150;
   std::chrono::steady_clock::time_point last_arrival{};
+  // FTS_IDLE_FIRST_US: a caller that arrives at an idle device with no other arrival in
+  // the last idle_quiet_us (a lone caller, not part of a burst) waits only this long
+  // for company -- spinning, not on a condition variable whose wake-up alone cost
+  // ~0.1 ms -- and starts at once when nobody comes (round 5 paid the whole quiet gap
+  // plus a wake-up: 3.36 vs 2.75-2.86 ms for a lone 4,096-proof batch)
+  int idle_first_us = 30;
+  std::atomic<uint64_t> arrivals{0};
+  // test hook (fts_debug_hold): no pass starts until hold_n requests are queued
+  int hold_n = 0;
+  // dispatcher counters (fts_debug_dispatch_stats)
+  std::atomic<int64_t> st_passes{0}, st_reqs{0}, st_max_merged{0}, st_act_reqs{0};
   // passes of up to com_fixed_max proofs compute com on the latency path (fixed-base
   // groups, rp_kernels.hip k_rp_fixed_all), larger ones on the work path (Horner +
   // joint GLV chains): the same group element either way
@@ -520,6 +566,7 @@ struct fts_ctx {
   ProverTables ptab;
   std::mutex slot_mu;
   std::vector<RpSlot*> slots, free_slots;  // fts_rp_verify_batch staging (all / idle)
+  std::vector<ActSlot*> aslots, free_aslots;  // action-call staging (all / idle), under slot_mu
 };
 
 // RAII lane acquisition (want < 0: any free lane)
@@ -589,7 +636,8 @@ void build_prover_tables(const PublicParams& pp, int n, ProverTables& t) {
 }  // namespace host
 }  // namespace fts
 
-static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int device, fts_ctx** out) {
+static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int device, fts_ctx** out,
+                      const fts_ctx_opts* opts = nullptr) {
   if (!pp_bytes || !out) return FTS_API_EINVAL;
   *out = nullptr;
   fts_ctx* c = new fts_ctx();
@@ -646,12 +694,15 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (hipSetDevice(device) != hipSuccess) return fail(FTS_API_EDEVICE);
   int nl = 4;  // lanes (FTS_LANES): 4 beat 5 and 3 on the burst and the steady state (s20_sweep4.sh)
   if (const char* e = getenv("FTS_LANES")) nl = std::max(1, std::min(16, atoi(e)));
+  if (opts && opts->lanes > 0) nl = std::min(16, opts->lanes);
+  c->nlanes = nl;
   if (const char* e = getenv("FTS_COALESCE_MAX")) c->coalesce_max = (size_t)std::max(0L, atol(e));
   c->gather_target = c->coalesce_max / 2;
   if (const char* e = getenv("FTS_GATHER_TARGET")) c->gather_target = (size_t)std::max(1L, atol(e));
   if (const char* e = getenv("FTS_GATHER_US")) c->gather_us = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_IDLE_GATHER_US")) c->idle_gather_us = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_IDLE_QUIET_US")) c->idle_quiet_us = std::max(0, atoi(e));
+  if (const char* e = getenv("FTS_IDLE_FIRST_US")) c->idle_first_us = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_COM_FIXED_MAX")) c->com_fixed_max = (size_t)std::max(0L, atol(e));
   if (const char* e = getenv("FTS_RLC_FORK")) c->rlc_fork = std::max(0, std::min(4, atoi(e)));
   if (const char* e = getenv("FTS_X0_SPLIT")) c->x0_split = atoi(e) != 0;
@@ -753,15 +804,28 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   {
     const int nw = n + 2;
     {
-      int wb = 20;
-      if (const char* e = getenv("FTS_WIDE_BITS")) {
-        wb = atoi(e) == 22 ? 22 : 20;
+      // explicit width (fts_ctx_opts.wide_bits, else FTS_WIDE_BITS), else the budget:
+      // 22-bit only when the whole context's tables fit the caller's table_budget
+      // (fts_ctx_opts) or, without one, when the free HBM keeps every lane's
+      // workspace (~8 GiB each for 81,920-proof passes at n = 64) and 128 GiB for
+      // other contexts and processes on the device
+      int wb = 20, forced = 0;
+      if (opts && (opts->wide_bits == 20 || opts->wide_bits == 22)) {
+        wb = opts->wide_bits, forced = 1;
+      } else if (const char* e = getenv("FTS_WIDE_BITS")) {
+        wb = atoi(e) == 22 ? 22 : 20, forced = 1;
       } else {
         size_t fr = 0, tot = 0;
         const size_t need22 = (size_t)nw * fbw_words_per_base(22) * 4;
-        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > need22 + ((size_t)160 << 30)) wb = 22;
+        if (opts && opts->table_budget) {
+          if (c->table_bytes + need22 <= opts->table_budget) wb = 22;
+        } else if (hipMemGetInfo(&fr, &tot) == hipSuccess &&
+                   fr > need22 + (size_t)nl * ((size_t)8 << 30) + ((size_t)128 << 30)) {
+          wb = 22;
+        }
       }
       c->wbits = wb;
+      c->wbits_forced = forced;
     }
     std::vector<uint32_t> hw((size_t)nw * 16, 0);
     for (int i = 0; i < nw; i++) {
@@ -782,7 +846,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
       d_wb = nullptr;
       c->d_wtables = nullptr;
       (void)hipGetLastError();
-      if (c->wbits == 22 && !getenv("FTS_WIDE_BITS")) {
+      if (c->wbits == 22 && !c->wbits_forced) {
         c->wbits = 20;
         continue;
       }
@@ -945,6 +1009,9 @@ extern "C" {
 int fts_ctx_create(const uint8_t* pp, size_t pp_len, int device, fts_ctx** out) {
   return ctx_create(pp, pp_len, 0, device, out);
 }
+int fts_ctx_create_opts(const uint8_t* pp, size_t pp_len, int device, const fts_ctx_opts* opts, fts_ctx** out) {
+  return ctx_create(pp, pp_len, opts ? opts->bit_length : 0, device, out, opts);
+}
 int fts_ctx_create_bits(const uint8_t* pp, size_t pp_len, uint32_t bit_length, int device, fts_ctx** out) {
   return ctx_create(pp, pp_len, bit_length, device, out);
 }
@@ -991,6 +1058,15 @@ void fts_ctx_destroy(fts_ctx* c) {
     delete sl->b;
     delete sl;
   }
+  for (ActSlot* sl : c->aslots) {
+    if (sl->s) hipStreamSynchronize(sl->s);
+    if (sl->dev) hipFree(sl->dev);
+    if (sl->pin) (void)hipHostFree(sl->pin);
+    if (sl->done) hipEventDestroy(sl->done);
+    if (sl->s) hipStreamDestroy(sl->s);
+    delete sl->b;
+    delete sl;
+  }
   delete c;
 }
 
@@ -1007,6 +1083,8 @@ int fts_ctx_info(const fts_ctx* c, fts_pp_info* o) {
   o->device = c->device;
   o->max_token = c->pp.max_token;
   o->table_bytes = c->table_bytes;
+  o->wide_bits = (uint32_t)c->wbits;
+  o->lanes = (uint32_t)c->nlanes;
   return FTS_API_OK;
 }
 
@@ -1543,6 +1621,14 @@ static int rp_pipeline(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_s
 // staggered sub-passes of one coalesced group -- sub-pass j's fixed-base launch
 // after sub-pass j-1's -- and dropped them: 20-batch bursts 3.77-3.89 vs 3.95-3.97
 // M rp64/s as one pass)
+// the pre_rlc hook of a pass with action calls: wait for their sigma equations, then
+// exclude the range proofs of actions whose sigma proof failed (pass offsets `off`)
+struct SigHook {
+  Lane* L = nullptr;
+  std::vector<const SigBatchDev*> sig;
+  std::vector<int> off;  // first range proof of the call in the pass (-1: none)
+};
+
 static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std::vector<std::vector<RpReq*>>& sub,
                              std::vector<int>& rc) {
   const size_t m = sub.size();
@@ -1551,47 +1637,99 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
   std::vector<int32_t*> d_status(m, nullptr);
   std::vector<size_t> Bs(m, 0);
   rc.assign(m, FTS_API_OK);
+  // per group: its requests with range proofs (the caller batches of the pass, in
+  // pass order), their first proof, and the sigma-exclusion hook of its action calls
+  std::vector<std::vector<RpReq*>> rpq(m);
+  std::vector<std::vector<int>> first(m);
+  std::vector<SigHook> hooks(m);
+  std::vector<uint8_t> sig_only(m, 0);
   for (size_t j = 0; j < m; j++) {
     Lane& L = *lanes[j];
     const std::vector<RpReq*>& grp = sub[j];
+    for (RpReq* q : grp)
+      if (q->b->B > 0) rpq[j].push_back(q);
     auto enq = [&]() -> int {
-      if (grp.size() == 1) {
+      if (grp.size() == 1 && !grp[0]->act) {
         fts_rp_batch* b = grp[0]->b;
         HIP_OK(hipMemcpyAsync(b->status, b->status0, (size_t)b->B * 4, hipMemcpyDeviceToDevice, L.s));
         Bs[j] = (size_t)b->B;
         d_status[j] = b->status;
+        first[j] = {0};
         return rp_enqueue(c, L, b->B, b->raw, b->sc, b->status, b->ipa_flag, [] {}, std::vector<int>{0, b->B}, P[j],
                           nullptr, nullptr);
       }
       size_t B = 0;
-      for (RpReq* q : grp) B += (size_t)q->b->B;
+      for (RpReq* q : rpq[j]) B += (size_t)q->b->B;
       Workspace& w = L.ws;
-      const size_t Bal = std::max(B, std::min(c->coalesce_max, (size_t)1 << 20));  // sized once for the largest pass
-      if (w.rp_raw.ensure(Bal * npts * 64) || w.rp_sc.ensure(Bal * RP_NSC * 32) || w.rp_status.ensure(Bal * 4) ||
-          w.rp_ipa.ensure(Bal * 4))
-        return FTS_API_ENOMEM;
       RpGather g{};
-      g.G = (int)grp.size();
-      size_t off = 0;
-      for (int i = 0; i < g.G; i++) {
-        const fts_rp_batch* b = grp[i]->b;
-        g.raw[i] = b->raw;
-        g.sc[i] = b->sc;
-        g.status0[i] = b->status0;
-        g.ipa[i] = b->ipa_flag;
-        g.off[i] = (int)off;
-        off += (size_t)b->B;
+      if (B > 0) {
+        const size_t Bal = std::max(B, std::min(c->coalesce_max, (size_t)1 << 20));  // sized once for the largest pass
+        if (w.rp_raw.ensure(Bal * npts * 64) || w.rp_sc.ensure(Bal * RP_NSC * 32) || w.rp_status.ensure(Bal * 4) ||
+            w.rp_ipa.ensure(Bal * 4))
+          return FTS_API_ENOMEM;
+        g.G = (int)rpq[j].size();
+        size_t off = 0;
+        for (int i = 0; i < g.G; i++) {
+          const fts_rp_batch* b = rpq[j][i]->b;
+          g.raw[i] = b->raw;
+          g.sc[i] = b->sc;
+          g.status0[i] = b->status0;
+          g.ipa[i] = b->ipa_flag;
+          g.off[i] = (int)off;
+          first[j].push_back((int)off);
+          off += (size_t)b->B;
+        }
+        g.off[g.G] = (int)off;
+        launch_rp_gather(g, c->k, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
+                         w.rp_ipa.as<int32_t>(), L.s);
       }
-      g.off[g.G] = (int)off;
-      launch_rp_gather(g, c->k, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
-                       w.rp_ipa.as<int32_t>(), L.s);
       Bs[j] = B;
       d_status[j] = w.rp_status.as<int32_t>();
+      // the action calls' sigma batches, each in its own slot's workspace: decode + primes
+      // (writing the V slots of its range proofs in the gathered pass) on the main stream
+      SigHook& h = hooks[j];
+      h.L = &L;
+      for (RpReq* q : grp) {
+        if (!q->act || q->act->sd.A == 0) continue;
+        SigBatchDev& sd = q->act->sd;
+        int off = -1;
+        for (size_t i = 0; i < rpq[j].size(); i++)
+          if (rpq[j][i] == q) off = first[j][i];
+        sd.rp_raw = off >= 0 ? w.rp_raw.as<uint8_t>() + (size_t)off * npts * 64 : nullptr;
+        launch_sig_prep(sd, L.s);
+        h.sig.push_back(&sd);
+        h.off.push_back(off);
+      }
+      if (B == 0) {  // sigma proofs only (e.g. 1-in/1-out transfers)
+        sig_only[j] = 1;
+        for (const SigBatchDev* sd : h.sig) launch_sig_finish(*sd, c->d_tables, c->n, L.s);
+        HIP_OK(hipGetLastError());
+        return FTS_API_OK;
+      }
+      void (*pre)(void*, hipStream_t) = nullptr;
+      if (!h.sig.empty()) {
+        // the sigma equations on the lane's third stream beside the range-proof pass;
+        // the batch check's variable part follows them there and first drops the range
+        // proofs of actions whose sigma proof failed (k_sig_exclude)
+        HIP_OK(hipEventRecord(L.ev_a, L.s));
+        HIP_OK(hipStreamWaitEvent(L.s3, L.ev_a, 0));
+        for (const SigBatchDev* sd : h.sig) launch_sig_finish(*sd, c->d_tables, c->n, L.s3);
+        HIP_OK(hipEventRecord(L.ev_b, L.s3));
+        pre = [](void* arg, hipStream_t s) {
+          SigHook* hk = static_cast<SigHook*>(arg);
+          (void)hipStreamWaitEvent(s, hk->L->ev_b, 0);
+          // the mask is read at launch time: rp_enqueue sizes (and may re-allocate) it
+          for (size_t i = 0; i < hk->sig.size(); i++)
+            if (hk->off[i] >= 0) launch_sig_exclude(*hk->sig[i], hk->L->ws.rp_excl.as<int32_t>() + hk->off[i], s);
+        };
+      }
+      std::vector<int> groups = first[j];
+      groups.push_back((int)B);
       return rp_enqueue(c, L, (int)B, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
-                        w.rp_ipa.as<int32_t>(), [] {}, std::vector<int>(g.off, g.off + g.G + 1), P[j]);
+                        w.rp_ipa.as<int32_t>(), [] {}, groups, P[j], pre, pre ? &h : nullptr);
     };
     rc[j] = enq();
-    for (RpReq* q : grp) P[j].dense.push_back(q->b->dense ? 1 : 0);
+    for (RpReq* q : rpq[j]) P[j].dense.push_back(q->b->dense ? 1 : 0);
   }
   for (size_t j = 0; j < m; j++) {
     Lane& L = *lanes[j];
@@ -1600,17 +1738,31 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
       continue;
     }
     auto fin = [&]() -> int {
-      if (int r = rp_finish(c, L, P[j])) return r;
-      for (size_t q = 0; q < sub[j].size() && q < P[j].dense.size(); q++) sub[j][q]->b->dense = P[j].dense[q] != 0;
-      int32_t* pst = L.status_buf(Bs[j]);
+      if (!sig_only[j]) {
+        if (int r = rp_finish(c, L, P[j])) return r;
+        for (size_t q = 0; q < rpq[j].size() && q < P[j].dense.size(); q++) rpq[j][q]->b->dense = P[j].dense[q] != 0;
+      }
+      int32_t* pst = L.status_buf(std::max<size_t>(Bs[j], 1));
       if (!pst) return FTS_API_ENOMEM;
-      HIP_OK(hipMemcpyAsync(pst, d_status[j], Bs[j] * 4, hipMemcpyDeviceToHost, L.s));
+      if (Bs[j]) HIP_OK(hipMemcpyAsync(pst, d_status[j], Bs[j] * 4, hipMemcpyDeviceToHost, L.s));
+      for (RpReq* q : sub[j])
+        if (q->act && q->act->sd.A)
+          HIP_OK(hipMemcpyAsync(q->act->sig_res, q->act->sd.status, (size_t)q->act->sd.A * 4, hipMemcpyDeviceToHost,
+                                L.s));
       HIP_OK(L.sync());
-      size_t off = 0;
+      for (size_t i = 0; i < rpq[j].size(); i++) {
+        RpReq* q = rpq[j][i];
+        if (q->status) memcpy(q->status, pst + first[j][i], (size_t)q->b->B * 4);
+      }
+      // host-side timings of the pass: the first action call's parse and staging
+      for (RpReq* q : sub[j])
+        if (q->act) {
+          L.host_parse_ms = q->act->parse_ms;
+          L.host_stage_ms = q->act->stage_ms;
+          break;
+        }
       for (RpReq* q : sub[j]) {
-        if (q->status) memcpy(q->status, pst + off, (size_t)q->b->B * 4);
-        off += (size_t)q->b->B;
-        collect_timings(c, L, q->b);
+        if (!sig_only[j]) collect_timings(c, L, q->b);
         q->b->merged = (int)sub[j].size();
       }
       return FTS_API_OK;
@@ -1618,6 +1770,8 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
     rc[j] = fin();
   }
 }
+
+static int rp_dispatch(fts_ctx* c, RpReq& me);
 
 extern "C" {
 
@@ -1738,20 +1892,35 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
   if (c->device < 0) return FTS_API_EDEVICE;
   if (b->B == 0) return FTS_API_OK;
   HIP_OK(hipSetDevice(c->device));
-  // Work-sharing dispatcher: the request joins the pending queue; any waiting
-  // caller that finds a free lane takes the queue's head group (FIFO, up to
-  // coalesce_max proofs) and runs it as ONE device pass, so batches submitted
-  // while the lanes are busy are merged (a 4,096-proof batch alone fills only
-  // 64 waves in the per-proof chain kernels).  Verdicts stay per proof.
   RpReq me(b, status);
+  return rp_dispatch(c, me);
+}
+
+}  // extern "C"
+
+// Work-sharing dispatcher: the request joins the pending queue; any waiting
+// caller that finds a free lane takes the queue's head group (FIFO, up to
+// coalesce_max proofs) and runs it as ONE device pass, so batches submitted
+// while the lanes are busy are merged (a 4,096-proof batch alone fills only
+// 64 waves in the per-proof chain kernels).  Verdicts stay per proof.  Staged
+// range-proof batches and action calls share the queue and the passes.
+static int rp_dispatch(fts_ctx* c, RpReq& me) {
+  fts_rp_batch* b = me.b;
   std::unique_lock<std::mutex> lk(c->mu);
   c->rp_pending.push_back(&me);
   c->pending_proofs += (size_t)b->B;
+  // a lone arrival: nothing else arrived within the quiet gap before it
+  const bool lone = me.arrived - c->last_arrival > std::chrono::microseconds(c->idle_quiet_us);
   c->last_arrival = me.arrived;
+  c->arrivals++;
   // enough queued for a full pass: the head stops gathering
   if (c->pending_proofs >= c->gather_target && c->rp_pending.front() != &me) c->rp_pending.front()->cv.notify_one();
+  if (c->hold_n > 0 && (int)c->rp_pending.size() >= c->hold_n) {  // test hook: release the held queue
+    c->hold_n = 0;
+    for (RpReq* q : c->rp_pending) q->cv.notify_one();
+  }
   while (!me.done) {
-    if (c->free_lanes.empty() || c->rp_pending.empty()) {
+    if (c->free_lanes.empty() || c->rp_pending.empty() || c->hold_n > 0) {
       me.cv.wait(lk);
       continue;
     }
@@ -1759,8 +1928,20 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
     const int wait_us = device_busy ? c->gather_us : c->idle_gather_us;
     if (wait_us > 0 && c->rp_pending.front() == &me && c->pending_proofs < c->gather_target) {
       auto deadline = me.arrived + std::chrono::microseconds(wait_us);
-      if (!device_busy)  // idle: only while the burst is still arriving
+      if (!device_busy) {  // idle: only while the burst is still arriving
         deadline = std::min(deadline, c->last_arrival + std::chrono::microseconds(c->idle_quiet_us));
+        if (lone && c->rp_pending.size() == 1) {
+          // a lone caller: a short spin for company, then go (no wake-up latency)
+          deadline = std::min(deadline, me.arrived + std::chrono::microseconds(c->idle_first_us));
+          if (std::chrono::steady_clock::now() < deadline) {
+            const uint64_t a0 = c->arrivals.load();
+            lk.unlock();
+            while (std::chrono::steady_clock::now() < deadline && c->arrivals.load() == a0) std::this_thread::yield();
+            lk.lock();
+            continue;
+          }
+        }
+      }
       if (std::chrono::steady_clock::now() < deadline) {
         me.cv.wait_until(lk, deadline);
         continue;
@@ -1794,6 +1975,11 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
     lk.unlock();
     std::vector<int> rcs;
     run_rp_groups(c, lanes, sub, rcs);
+    c->st_passes++;
+    c->st_reqs += (int64_t)grp.size();
+    c->st_act_reqs += std::count_if(grp.begin(), grp.end(), [](const RpReq* q) { return q->act != nullptr; });
+    for (int64_t mx = c->st_max_merged.load(); (int64_t)grp.size() > mx && !c->st_max_merged.compare_exchange_weak(mx, (int64_t)grp.size());) {
+    }
     lk.lock();
     for (size_t j = 0; j < sub.size(); j++)
       for (RpReq* q : sub[j]) {
@@ -1806,6 +1992,8 @@ int fts_rp_batch_verify(fts_ctx* c, fts_rp_batch* b, int32_t* status) {
   }
   return me.rc;
 }
+
+extern "C" {
 
 int fts_rp_batch_timings(const fts_rp_batch* b, const char** names, float* ms, double* mads, int cap) {
   if (!b) return 0;
@@ -1820,6 +2008,29 @@ int fts_rp_batch_timings(const fts_rp_batch* b, const char** names, float* ms, d
 }
 
 int fts_rp_batch_merged(const fts_rp_batch* b) { return b ? b->merged : 0; }
+
+int fts_debug_hold(fts_ctx* c, int n) {
+  if (!c) return FTS_API_EINVAL;
+  for (fts_ctx* ch : c->shards) fts_debug_hold(ch, n);
+  if (c->lanes.empty()) return FTS_API_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->hold_n = std::max(0, n);
+  if (c->hold_n == 0 || (int)c->rp_pending.size() >= c->hold_n) {
+    c->hold_n = 0;
+    for (RpReq* q : c->rp_pending) q->cv.notify_one();
+  }
+  return FTS_API_OK;
+}
+
+int fts_debug_dispatch_stats(const fts_ctx* c, int64_t* out) {
+  if (!c || !out) return FTS_API_EINVAL;
+  if (!c->shards.empty()) return fts_debug_dispatch_stats(c->shards[0], out);
+  out[0] = c->st_passes.load();
+  out[1] = c->st_reqs.load();
+  out[2] = c->st_max_merged.load();
+  out[3] = c->st_act_reqs.load();
+  return FTS_API_OK;
+}
 
 int fts_ctx_reserve(fts_ctx* c, size_t max_pass_proofs) {
   if (!c) return FTS_API_EINVAL;
@@ -2162,181 +2373,108 @@ int fts_rp_verify_batch(fts_ctx* c, size_t n, const uint8_t* const* rp_der, cons
 // ------------------------------------------------------- transfers / issues
 // One action = a transfer (TypeAndSum + RangeCorrectness on Out_j - CT,
 // transfer/transfer.go:49-60,153-197) or an issue (SameType + RangeCorrectness
-// on Tok_i - CT, issue/verifier.go:24-57).
-namespace {
-struct ActionIn {
-  int kind;                    // SIG_TAS / SIG_ST
-  const uint8_t* in;           // n_in * 64
-  size_t n_in;
-  const uint8_t* out;          // n_out * 64 (issue: tokens)
-  size_t n_out;
-  der::Span proof;
-};
+// on Tok_i - CT, issue/verifier.go:24-57).  An action call is parsed straight into
+// a pooled slot's pinned records (act_stage), uploaded once, and verified by the
+// range-proof dispatcher (rp_dispatch) together with whatever else is queued.
 
-struct ActionState {
-  int32_t host_final = -1;     // verdict decided on the host (MALFORMED / TAS_INVALID)
-  bool sig_on_device = false;
-  int sig_index = -1;          // index in the device sigma batch
-  bool rc_applicable = false;
-  int rp_base = -1, rp_count = 0;
-  bool rc_count_bad = false;
-};
-}  // namespace
+// an idle action staging slot (or a new one); nullptr on failure
+static ActSlot* aslot_acquire(fts_ctx* c) {
+  {
+    std::lock_guard<std::mutex> g(c->slot_mu);
+    if (!c->free_aslots.empty()) {
+      ActSlot* sl = c->free_aslots.back();
+      c->free_aslots.pop_back();
+      return sl;
+    }
+  }
+  ActSlot* sl = new ActSlot();
+  sl->b = new fts_rp_batch();
+  sl->b->device = c->device;
+  if (hipStreamCreateWithFlags(&sl->s, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&sl->done, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess) {
+    if (sl->s) hipStreamDestroy(sl->s);
+    delete sl->b;
+    delete sl;
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> g(c->slot_mu);
+  c->aslots.push_back(sl);
+  return sl;
+}
 
-static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts, int32_t* status, int32_t* fail_index) {
-  const double t_fn0 = now_ms();
-  const int k = c->k, n = c->n, npts_rp = rp_npts(k);
+static void aslot_release(fts_ctx* c, ActSlot* sl) {
+  std::lock_guard<std::mutex> g(c->slot_mu);
+  c->free_aslots.push_back(sl);
+}
+
+// grow the slot's pinned and device buffers geometrically (hipFree synchronises the
+// whole device: a slot must not be re-allocated on every slightly larger call)
+static bool aslot_size(ActSlot* sl, size_t pin_bytes, size_t dev_bytes) {
+  if (pin_bytes > sl->pin_cap) {
+    if (sl->pin) (void)hipHostFree(sl->pin);
+    sl->pin = nullptr;
+    const size_t want = std::max(pin_bytes, sl->pin_cap + sl->pin_cap / 2);
+    sl->pin_cap = 0;
+    if (hipHostMalloc((void**)&sl->pin, want, 0) != hipSuccess) return false;
+    sl->pin_cap = want;
+  }
+  if (dev_bytes > sl->dev_cap) {
+    if (sl->dev) hipFree(sl->dev);
+    sl->dev = nullptr;
+    const size_t want = std::max(dev_bytes, sl->dev_cap + sl->dev_cap / 2);
+    sl->dev_cap = 0;
+    if (hipMalloc((void**)&sl->dev, want) != hipSuccess) return false;
+    sl->dev_cap = want;
+  }
+  return true;
+}
+
+// Parse an action call into slot sl: sigma batch + range-proof records in their
+// device layout, written straight into the slot's pinned buffer (no per-action
+// host vectors, no second copy), then one upload.  Three steps:
+//   1. (parallel) the proofs' outer structure: which actions reach the device and
+//      how many range proofs each carries -- the layout's only inputs;
+//   2. (serial) offsets of every action's records (integer prefix sums);
+//   3. (parallel) the full decode into those offsets.  An action rejected here keeps
+//      its records in the layout, marked so every kernel skips them (sigma status
+//      FTS_E_MALFORMED, its range proofs FTS_E_NOT_RUN); its verdict is the host's.
+// The per-action checks and their order are the reference's deserialisation
+// (transfer.go:29-40, typeandsum.go:37-93,230-251, sametype.go:32-64,167-171,
+// rangecorrectness.go:19-40, bulletproof.go:37-101, ipa.go:33-67).
+static int act_stage(fts_ctx* c, ActSlot* sl, const std::vector<ActionIn>& acts) {
+  const double t0 = now_ms();
+  const int k = c->k, npts_rp = rp_npts(k);
   const size_t A = acts.size();
-  std::vector<ActionState> st(A);
-  // host-side decoding (parallel over actions)
-  using Parsed = ParsedAction;
-  if (L.parsed.size() < A) L.parsed.resize(A);
-  std::vector<Parsed>& P = L.parsed;
-  const double t_parse0 = now_ms();
-  auto parse_one = [&](size_t i) {
+  std::vector<ActionState>& st = sl->st;
+  st.assign(A, ActionState{});
+  // ---- 1. shapes
+  parallel_for(A, 64, [&](size_t i) {
+    thread_local std::vector<der::Span> vals, rps;
     const ActionIn& ai = acts[i];
     ActionState& s = st[i];
-    Parsed& p = P[i];
-    std::vector<der::Span> vals;
     if (!der::unmarshal_values(ai.proof, vals) || vals.size() != 2) {
       s.host_final = FTS_E_MALFORMED;
       return;
     }
     s.rc_applicable = ai.kind == SIG_ST || ai.n_in != 1 || ai.n_out != 1;
-    // ---- range proofs (deserialised together with the sigma proof)
-    std::vector<der::Span> rps;
+    rps.clear();
     if (vals[1].n && !parse_range_correctness(vals[1], rps)) {
       s.host_final = FTS_E_MALFORMED;
       return;
     }
     s.rp_count = (int)rps.size();
-    p.rp_raw.assign(rps.size() * npts_rp * 64, 0);
-    p.rp_sc.assign(rps.size() * RP_NSC * 8, 0);
-    p.rp_status.assign(rps.size(), 0);
-    p.rp_ipa.assign(rps.size(), 0);
-    for (size_t j = 0; j < rps.size(); j++) {
-      uint8_t* pts = &p.rp_raw[j * npts_rp * 64];
-      parse_range_proof(rps[j], k, pts, &p.rp_sc[j * RP_NSC * 8], p.rp_status[j], p.rp_ipa[j]);
-      filler_point(pts + RP_PT_V * 64);
-      if (p.rp_status[j] == FTS_E_MALFORMED) {
-        s.host_final = FTS_E_MALFORMED;
-        return;
-      }
-      if (!s.rc_applicable) {  // never verified, but must deserialise (points decode)
-        G1A tmp;
-        for (int q = 0; q < npts_rp; q++)
-          if (q != RP_PT_V && !g1_from_bytes(pts + q * 64, 64, tmp)) {
-            s.host_final = FTS_E_MALFORMED;
-            return;
-          }
-      }
-    }
-    if (s.rc_applicable) s.rc_count_bad = rps.size() != ai.n_out;
-    // ---- sigma proof
-    p.sig_raw.assign((1 + ai.n_in + ai.n_out) * 64, 0);
-    for (size_t j = 0; j < ai.n_in; j++) memcpy(&p.sig_raw[(1 + j) * 64], ai.in + 64 * j, 64);
-    for (size_t j = 0; j < ai.n_out; j++) memcpy(&p.sig_raw[(1 + ai.n_in + j) * 64], ai.out + 64 * j, 64);
-    bool nil_fields = false, panic = false;
-    Elem e[7];
-    int ne = ai.kind == SIG_TAS ? 7 : 4;
-    if (vals[0].n) {
-      Unmarshaller u(vals[0]);
-      if (!u.ok) {
-        s.host_final = FTS_E_MALFORMED;
-        return;
-      }
-      for (int f = 0; f < ne; f++)
-        if (!u.next(e[f])) {
-          s.host_final = FTS_E_MALFORMED;
-          return;
-        }
-    }
-    // element kinds: TAS [CT g1, ibf arr, iv arr, Type, TBF, EqSum, Chal]; ST [Type, BF, Chal, CT g1]
-    const int ct_idx = ai.kind == SIG_TAS ? 0 : 3;
-    if (e[ct_idx].present) {
-      if (e[ct_idx].raw.n != 64) {
-        s.host_final = FTS_E_MALFORMED;
-        return;
-      }
-      memcpy(&p.sig_raw[0], e[ct_idx].raw.p, 64);
-    }
-    std::vector<der::Span> ibf, iv;
-    if (ai.kind == SIG_TAS) {
-      if (e[1].present && !der::unmarshal_values(e[1].raw, ibf, true)) return void(s.host_final = FTS_E_MALFORMED);
-      if (e[2].present && !der::unmarshal_values(e[2].raw, iv, true)) return void(s.host_final = FTS_E_MALFORMED);
-      // typeandsum.go:231: nil TBF/Type/CT/EqSum -> "invalid sum and type proof"
-      nil_fields = !e[4].present || !e[3].present || !e[0].present || !e[5].present;
-      if (!nil_fields) {
-        // :242-251 would panic on a nil challenge or short/nil InputValues / InputBlindingFactors
-        if (!e[6].present || !e[2].present || !e[1].present || iv.size() < ai.n_in || ibf.size() < ai.n_in)
-          panic = true;
-      }
-      // transfer.go:175: the range goroutine dereferences CommitmentToType
-      if (s.rc_applicable && !e[0].present) panic = true;
-      if (!nil_fields && !panic) {
-        p.sig_sc.assign((4 + 2 * ai.n_in) * 8, 0);
-        scalar_from_bytes(e[3].raw, &p.sig_sc[TAS_SC_TYPE * 8], nullptr);
-        scalar_from_bytes(e[4].raw, &p.sig_sc[TAS_SC_TBF * 8], nullptr);
-        scalar_from_bytes(e[5].raw, &p.sig_sc[TAS_SC_EQ * 8], nullptr);
-        bool canon;
-        scalar_from_bytes(e[6].raw, &p.sig_sc[TAS_SC_CHAL * 8], &canon);
-        p.chal_canonical = canon;
-        for (size_t j = 0; j < ai.n_in; j++) {
-          scalar_from_bytes(iv[j], &p.sig_sc[(TAS_SC_IV + j) * 8], nullptr);
-          scalar_from_bytes(ibf[j], &p.sig_sc[(TAS_SC_IV + ai.n_in + j) * 8], nullptr);
-        }
-      }
-    } else {
-      // sametype.go:169-171 dereferences every field
-      if (!e[0].present || !e[1].present || !e[2].present || !e[3].present) panic = true;
-      else {
-        p.sig_sc.assign(3 * 8, 0);
-        scalar_from_bytes(e[0].raw, &p.sig_sc[ST_SC_TYPE * 8], nullptr);
-        scalar_from_bytes(e[1].raw, &p.sig_sc[ST_SC_BF * 8], nullptr);
-        bool canon;
-        scalar_from_bytes(e[2].raw, &p.sig_sc[ST_SC_CHAL * 8], &canon);
-        p.chal_canonical = canon;
-      }
-    }
-    if (panic) {
-      s.host_final = FTS_E_MALFORMED;
-      return;
-    }
-    // element arrays / CT must still decode even when the proof is rejected for nil fields
-    if (nil_fields) {
-      G1A tmp;
-      if (e[0].present && !g1_from_bytes(&p.sig_raw[0], 64, tmp)) return void(s.host_final = FTS_E_MALFORMED);
-      s.host_final = FTS_E_TAS_INVALID;
-      // range proofs may still carry malformed points: check them on the host
-      for (size_t j = 0; j < rps.size(); j++)
-        for (int q = 0; q < npts_rp; q++)
-          if (q != RP_PT_V && !g1_from_bytes(&p.rp_raw[(j * npts_rp + q) * 64], 64, tmp))
-            return void(s.host_final = FTS_E_MALFORMED);
-      return;
-    }
-    s.sig_on_device = true;
-  };
-  parallel_for(A, 64, parse_one);
-  const double t_parse1 = now_ms();
-  L.host_parse_ms = (float)(t_parse1 - t_parse0);
-  // ---- assemble device batches: offsets on one thread (integer sums), then a
-  // parallel fill of the lane's pinned staging buffer and async uploads from it
-  struct Off {
-    int sig = -1;               // index in the device sigma batch
-    size_t scw = 0;             // word offset in s_sc
-    int fx = 0, vr = 0;         // first fixed-base / variable-base work item
-  };
-  std::vector<Off> off(A);
+  });
+  // ---- 2. layout
   std::vector<SigAction> sact;
+  std::vector<int> fx(A, 0), vr(A, 0), affo;
+  std::vector<int>& sig_of = sl->sig_of;
+  sig_of.assign(A, -1);
   int term_off = 0, aff_off = 0, pt_off = 0, sc_off = 0, rp_total = 0, nfix_total = 0;
-  size_t scw_total = 0;
   uint32_t msg_off = 0;
-  std::vector<int> sig_of(A, -1);
   for (size_t i = 0; i < A; i++) {
     ActionState& s = st[i];
     if (s.host_final >= 0) continue;
     const ActionIn& ai = acts[i];
-    Parsed& p = P[i];
     if (s.rc_applicable && s.rp_count > 0) {
       s.rp_base = rp_total;
       rp_total += s.rp_count;
@@ -2351,190 +2489,267 @@ static int verify_actions(fts_ctx* c, Lane& L, const std::vector<ActionIn>& acts
     sa.msg_off = (int32_t)msg_off;
     sa.rp_base = s.rp_base;
     sa.rp_count = s.rp_count;
-    sa.chal_canonical = p.chal_canonical;
-    off[i].sig = (int)sact.size();
-    off[i].scw = scw_total;
-    off[i].fx = nfix_total;
-    off[i].vr = term_off - nfix_total;
+    s.sig = sig_of[i] = (int)sact.size();
+    fx[i] = nfix_total;
+    vr[i] = term_off - nfix_total;
+    affo.push_back(aff_off);
     nfix_total += sig_nfixed(sa.kind, sa.n_in);
-    scw_total += p.sig_sc.size();
     pt_off += 1 + sa.n_in + sa.n_out;
     sc_off += sig_nscalars(sa.kind, sa.n_in);
     term_off += sig_nterms(sa.kind, sa.n_in);
     aff_off += sig_naff(sa.kind, sa.n_in, sa.n_out);
     msg_off += sig_msg_slot(sa.kind, sa.n_in, sa.n_out);
-    sig_of[i] = (int)sact.size();
     sact.push_back(sa);
   }
   const int SA = (int)sact.size();
   const size_t nwork = (size_t)term_off;
-  // staging layout (256-byte aligned regions)
   size_t o = 0;
-  auto region = [&](size_t bytes) {
+  auto region = [&](size_t bytes) {  // 256-byte aligned regions
     size_t r = o;
     o += (bytes + 255) & ~size_t(255);
     return r;
   };
+  // uploaded part (one copy), then the pinned verdict download, then device workspace
   const size_t o_act = region((size_t)SA * sizeof(SigAction)), o_raw = region((size_t)pt_off * 64),
-               o_owner = region((size_t)pt_off * 4), o_sc = region(scw_total * 4),
-               o_work = region(nwork * sizeof(int2)), o_affoff = region((size_t)SA * 4),
-               o_rraw = region((size_t)rp_total * npts_rp * 64), o_rsc = region((size_t)rp_total * RP_NSC * 8 * 4),
+               o_owner = region((size_t)pt_off * 4), o_sc = region((size_t)sc_off * 32),
+               o_work = region(nwork * sizeof(int2)), o_affoff = region((size_t)SA * 4), o_sst = region((size_t)SA * 4),
+               o_rraw = region((size_t)rp_total * npts_rp * 64), o_rsc = region((size_t)rp_total * RP_NSC * 32),
                o_rst = region((size_t)rp_total * 4), o_ripa = region((size_t)rp_total * 4);
-  uint8_t* hs = L.stage_buf(std::max<size_t>(o, 1));
-  if (!hs) return FTS_API_ENOMEM;
-  if (SA) memcpy(hs + o_act, sact.data(), (size_t)SA * sizeof(SigAction));
+  const size_t in_end = o;
+  const size_t o_res = region((size_t)SA * 4), pin_end = o;
+  o = in_end;
+  const size_t w_pts = region((size_t)pt_off * 64), w_terms = region(nwork * 96), w_aff = region((size_t)aff_off * 64),
+               w_jac = region((size_t)aff_off * 96), w_msgs = region(msg_off),
+               w_scratch = region(sig_scratch_words(nwork) * 4), dev_end = o;
+  if (!aslot_size(sl, std::max<size_t>(pin_end, 256), std::max<size_t>(dev_end, 256))) return FTS_API_ENOMEM;
+  uint8_t* hp = sl->pin;
+  SigAction* hact = reinterpret_cast<SigAction*>(hp + o_act);
+  int32_t* hsst = reinterpret_cast<int32_t*>(hp + o_sst);
+  int32_t* hrst = reinterpret_cast<int32_t*>(hp + o_rst);
+  int32_t* hripa = reinterpret_cast<int32_t*>(hp + o_ripa);
+  int32_t* howner = reinterpret_cast<int32_t*>(hp + o_owner);
+  int2* hwork = reinterpret_cast<int2*>(hp + o_work);
+  // ---- 3. decode into the layout
   parallel_for(A, 64, [&](size_t i) {
-    if (sig_of[i] < 0) return;
-    const SigAction& sa = sact[sig_of[i]];
-    const Parsed& p = P[i];
-    const ActionState& s = st[i];
-    const int npt = 1 + sa.n_in + sa.n_out, g = sig_of[i];
-    memcpy(hs + o_raw + (size_t)sa.pt_off * 64, p.sig_raw.data(), (size_t)npt * 64);
-    int32_t* own = (int32_t*)(hs + o_owner) + sa.pt_off;
-    for (int q = 0; q < npt; q++) own[q] = g;
-    if (!p.sig_sc.empty()) memcpy(hs + o_sc + off[i].scw * 4, p.sig_sc.data(), p.sig_sc.size() * 4);
+    thread_local std::vector<der::Span> vals, rps, ubuf, ibf, iv;
+    ActionState& s = st[i];
+    const int g = sig_of[i];
+    if (g < 0) return;
+    const ActionIn& ai = acts[i];
+    SigAction& sa = hact[g];
+    sa = sact[g];
+    hsst[g] = 0;
+    reinterpret_cast<int32_t*>(hp + o_affoff)[g] = affo[g];
+    const int npt = 1 + sa.n_in + sa.n_out;
+    for (int q = 0; q < npt; q++) howner[sa.pt_off + q] = g;
     // work list: every fixed-base term first, then every variable-base (GLV) term,
     // so no wave of k_sig_terms runs both kinds of product
-    int2* wk = (int2*)(hs + o_work);
-    for (int t = 0, nt = sig_nterms(sa.kind, sa.n_in), fi = off[i].fx, vi = nfix_total + off[i].vr; t < nt; t++)
-      wk[sig_term_var(sa.kind, sa.n_in, t) ? vi++ : fi++] = make_int2(g, t);
-    ((int32_t*)(hs + o_affoff))[g] = 0;
-    if (s.rp_base >= 0) {
-      const size_t rb = (size_t)s.rp_base, rc = (size_t)s.rp_count;
-      memcpy(hs + o_rraw + rb * npts_rp * 64, p.rp_raw.data(), rc * npts_rp * 64);
-      memcpy(hs + o_rsc + rb * RP_NSC * 8 * 4, p.rp_sc.data(), rc * RP_NSC * 8 * 4);
-      memcpy(hs + o_rst + rb * 4, p.rp_status.data(), rc * 4);
-      memcpy(hs + o_ripa + rb * 4, p.rp_ipa.data(), rc * 4);
-    }
-  });
-  const double t_copy1 = now_ms();
-  L.host_stage_copy_ms = (float)(t_copy1 - t_parse1);
-  {  // affine-table offsets: prefix sum in sigma-batch order
-    int32_t* ao = (int32_t*)(hs + o_affoff);
-    int acc = 0;
-    for (int g = 0; g < SA; g++) {
-      ao[g] = acc;
-      acc += sig_naff(sact[g].kind, sact[g].n_in, sact[g].n_out);
-    }
-  }
-  Workspace& w = L.ws;
-  if (SA) {
-    if (w.s_act.ensure(SA * sizeof(SigAction)) || w.s_raw.ensure((size_t)pt_off * 64) ||
-        w.s_owner.ensure((size_t)pt_off * 4) || w.s_pts.ensure((size_t)pt_off * 64) ||
-        w.s_sc.ensure(std::max<size_t>(scw_total, 1) * 4) || w.s_status.ensure(SA * 4) ||
-        w.s_work.ensure(nwork * sizeof(int2)) || w.s_terms.ensure((size_t)term_off * 96) ||
-        w.s_aff.ensure((size_t)aff_off * 64) || w.s_affoff.ensure(SA * 4) || w.s_msgs.ensure(msg_off) ||
-        w.s_jac.ensure((size_t)aff_off * 96) || w.s_scratch.ensure(sig_scratch_words(nwork) * 4))
-      return FTS_API_ENOMEM;
-    HIP_OK(hipMemcpyAsync(w.s_act.p, hs + o_act, SA * sizeof(SigAction), hipMemcpyHostToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(w.s_raw.p, hs + o_raw, (size_t)pt_off * 64, hipMemcpyHostToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(w.s_owner.p, hs + o_owner, (size_t)pt_off * 4, hipMemcpyHostToDevice, L.s));
-    if (scw_total) HIP_OK(hipMemcpyAsync(w.s_sc.p, hs + o_sc, scw_total * 4, hipMemcpyHostToDevice, L.s));
-    HIP_OK(hipMemsetAsync(w.s_status.p, 0, SA * 4, L.s));
-    HIP_OK(hipMemcpyAsync(w.s_work.p, hs + o_work, nwork * sizeof(int2), hipMemcpyHostToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(w.s_affoff.p, hs + o_affoff, SA * 4, hipMemcpyHostToDevice, L.s));
-  }
-  if (rp_total) {
-    if (w.rp_raw.ensure((size_t)rp_total * npts_rp * 64) || w.rp_sc.ensure((size_t)rp_total * RP_NSC * 8 * 4) ||
-        w.rp_status.ensure(rp_total * 4) || w.rp_ipa.ensure(rp_total * 4))
-      return FTS_API_ENOMEM;
-    HIP_OK(hipMemcpyAsync(w.rp_raw.p, hs + o_rraw, (size_t)rp_total * npts_rp * 64, hipMemcpyHostToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(w.rp_sc.p, hs + o_rsc, (size_t)rp_total * RP_NSC * 8 * 4, hipMemcpyHostToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(w.rp_status.p, hs + o_rst, rp_total * 4, hipMemcpyHostToDevice, L.s));
-    HIP_OK(hipMemcpyAsync(w.rp_ipa.p, hs + o_ripa, rp_total * 4, hipMemcpyHostToDevice, L.s));
-  }
-  SigBatchDev sd{};
-  if (SA) {
-    sd.A = SA;
-    sd.npts = pt_off;
-    sd.nwork = (int)nwork;
-    sd.act = w.s_act.as<SigAction>();
-    sd.raw = w.s_raw.as<uint8_t>();
-    sd.pt_owner = w.s_owner.as<int32_t>();
-    sd.pts = w.s_pts.as<uint32_t>();
-    sd.sc = w.s_sc.as<uint32_t>();
-    sd.status = w.s_status.as<int32_t>();
-    sd.work = w.s_work.as<int2>();
-    sd.terms = w.s_terms.as<uint32_t>();
-    sd.aff = w.s_aff.as<uint32_t>();
-    sd.aff_off = w.s_affoff.as<int32_t>();
-    sd.msgs = w.s_msgs.as<uint8_t>();
-    sd.jac = w.s_jac.as<uint32_t>();
-    sd.scratch = w.s_scratch.as<uint32_t>();
-    sd.rp_raw = rp_total ? w.rp_raw.as<uint8_t>() : nullptr;
-    sd.rp_k = k;
-    sd.naff = aff_off;
-    launch_sig_prep(sd, L.s);
-    L.host_stage_ms = (float)(now_ms() - t_parse1);
-  }
-  if (rp_total) {
-    // the sigma proofs run on the lane's third stream beside the range-proof pass;
-    // the batch check's variable part follows them on that stream and first drops
-    // the range proofs of actions whose sigma proof failed (k_sig_exclude)
-    struct Hook {
-      const SigBatchDev* sd;
-      Lane* L;
-    } hook{&sd, &L};
-    void (*pre)(void*, hipStream_t) = nullptr;
-    if (SA) {
-      HIP_OK(hipEventRecord(L.ev_a, L.s));
-      HIP_OK(hipStreamWaitEvent(L.s3, L.ev_a, 0));
-      launch_sig_finish(sd, c->d_tables, n, L.s3);
-      HIP_OK(hipEventRecord(L.ev_b, L.s3));
-      pre = [](void* arg, hipStream_t s) {
-        Hook* h = static_cast<Hook*>(arg);
-        (void)hipStreamWaitEvent(s, h->L->ev_b, 0);
-        // the mask is read at launch time: rp_pipeline sizes (and may re-allocate) it
-        launch_sig_exclude(*h->sd, h->L->ws.rp_excl.as<int32_t>(), s);
-      };
-    }
-    int rc = rp_pipeline(c, L, rp_total, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
-                         w.rp_ipa.as<int32_t>(), [] {}, std::vector<int>{0, rp_total}, pre, &hook);
-    if (rc != FTS_API_OK) return rc;
-  } else if (SA) {
-    launch_sig_finish(sd, c->d_tables, n, L.s);
-  }
-  HIP_OK(hipGetLastError());
-  std::vector<int32_t> sig_res(SA), rp_res(rp_total);
-  if (SA) HIP_OK(hipMemcpyAsync(sig_res.data(), w.s_status.p, SA * 4, hipMemcpyDeviceToHost, L.s));
-  if (rp_total) HIP_OK(hipMemcpyAsync(rp_res.data(), w.rp_status.p, rp_total * 4, hipMemcpyDeviceToHost, L.s));
-  HIP_OK(L.sync());
-  const double t_post0 = now_ms();
-  L.host_misc_ms = (float)((t_parse0 - t_fn0) + (now_ms() - t_post0));
-  L.host_total_ms = (float)(now_ms() - t_fn0);  // verify_actions up to the verdict merge
-  if (rp_total) collect_timings(c, L, nullptr);
-  // ---- combine with the reference's precedence
-  for (size_t i = 0; i < A; i++) {
-    const ActionState& s = st[i];
-    int32_t out = FTS_OK, idx = -1;
-    if (s.host_final >= 0) {
-      out = s.host_final;
-    } else {
-      int32_t sig = sig_res[sig_of[i]];
-      bool malformed = sig == FTS_E_MALFORMED;
-      for (int j = 0; j < s.rp_count && s.rp_base >= 0; j++) malformed |= rp_res[s.rp_base + j] == FTS_E_MALFORMED;
-      if (malformed) {
-        out = FTS_E_MALFORMED;                       // deserialisation precedes verification
-      } else if (sig != FTS_OK) {
-        out = sig;                                   // TypeAndSum / SameType error wins (transfer.go:192-196)
-      } else if (s.rc_applicable) {
-        if (s.rc_count_bad) {
-          out = FTS_E_RC_COUNT;                      // rangecorrectness.go:138-140
-        } else {
-          for (int j = 0; j < s.rp_count; j++)       // first failing index wins (:141-160)
-            if (rp_res[s.rp_base + j] != FTS_OK) {
-              out = rp_res[s.rp_base + j];
-              idx = j;
-              break;
-            }
-        }
+    for (int t = 0, nt = sig_nterms(sa.kind, sa.n_in), fi = fx[i], vi = nfix_total + vr[i]; t < nt; t++)
+      hwork[sig_term_var(sa.kind, sa.n_in, t) ? vi++ : fi++] = make_int2(g, t);
+    // a rejected action keeps its records, skipped by every kernel
+    auto fail = [&](int32_t v) {
+      s.host_final = v;
+      hsst[g] = FTS_E_MALFORMED;
+      for (int j = 0; j < s.rp_count && s.rp_base >= 0; j++) {
+        hrst[s.rp_base + j] = FTS_E_NOT_RUN;
+        hripa[s.rp_base + j] = 0;
+      }
+    };
+    (void)der::unmarshal_values(ai.proof, vals);  // held in step 1
+    rps.clear();
+    if (vals[1].n) (void)parse_range_correctness(vals[1], rps);
+    // ---- range proofs (deserialised together with the sigma proof)
+    thread_local std::vector<uint8_t> tpts;
+    thread_local std::vector<uint32_t> tsc;
+    for (size_t j = 0; j < rps.size(); j++) {
+      uint8_t* pts;
+      uint32_t* scp;
+      int32_t tst = 0, tipa = 0;
+      int32_t *pst = &tst, *pipa = &tipa;
+      if (s.rp_base >= 0) {
+        const size_t r = (size_t)s.rp_base + j;
+        pts = hp + o_rraw + r * npts_rp * 64;
+        scp = reinterpret_cast<uint32_t*>(hp + o_rsc) + r * RP_NSC * 8;
+        pst = hrst + r;
+        pipa = hripa + r;
+      } else {  // not verified (1-in/1-out transfer), but must deserialise
+        tpts.resize((size_t)npts_rp * 64);
+        tsc.resize(RP_NSC * 8);
+        pts = tpts.data();
+        scp = tsc.data();
+      }
+      parse_range_proof(rps[j], k, pts, scp, *pst, *pipa);
+      filler_point(pts + RP_PT_V * 64);
+      if (*pst == FTS_E_MALFORMED) return fail(FTS_E_MALFORMED);
+      if (!s.rc_applicable) {  // its points decode on the host (no device slot)
+        G1A tmp;
+        for (int q = 0; q < npts_rp; q++)
+          if (q != RP_PT_V && !g1_from_bytes(pts + q * 64, 64, tmp)) return fail(FTS_E_MALFORMED);
       }
     }
-    status[i] = out;
-    if (fail_index) fail_index[i] = idx;
+    if (s.rc_applicable) s.rc_count_bad = rps.size() != ai.n_out;
+    // ---- sigma proof: points [CT, in..., out...], scalars
+    uint8_t* raw = hp + o_raw + (size_t)sa.pt_off * 64;
+    memset(raw, 0, 64);
+    if (sa.n_in) memcpy(raw + 64, ai.in, (size_t)sa.n_in * 64);
+    if (ai.n_out) memcpy(raw + (size_t)(1 + sa.n_in) * 64, ai.out, ai.n_out * 64);
+    uint32_t* sc = reinterpret_cast<uint32_t*>(hp + o_sc) + (size_t)sa.sc_off * 8;
+    memset(sc, 0, (size_t)sig_nscalars(sa.kind, sa.n_in) * 32);
+    bool nil_fields = false, panic = false;
+    Elem e[7];
+    const int ne = ai.kind == SIG_TAS ? 7 : 4;
+    if (vals[0].n) {
+      Unmarshaller u(vals[0], ubuf);
+      if (!u.ok) return fail(FTS_E_MALFORMED);
+      for (int f = 0; f < ne; f++)
+        if (!u.next(e[f])) return fail(FTS_E_MALFORMED);
+    }
+    // element kinds: TAS [CT g1, ibf arr, iv arr, Type, TBF, EqSum, Chal]; ST [Type, BF, Chal, CT g1]
+    const int ct_idx = ai.kind == SIG_TAS ? 0 : 3;
+    if (e[ct_idx].present) {
+      if (e[ct_idx].raw.n != 64) return fail(FTS_E_MALFORMED);
+      memcpy(raw, e[ct_idx].raw.p, 64);
+    }
+    if (ai.kind == SIG_TAS) {
+      ibf.clear();
+      iv.clear();
+      if (e[1].present && !der::unmarshal_values(e[1].raw, ibf, true)) return fail(FTS_E_MALFORMED);
+      if (e[2].present && !der::unmarshal_values(e[2].raw, iv, true)) return fail(FTS_E_MALFORMED);
+      // typeandsum.go:231: nil TBF/Type/CT/EqSum -> "invalid sum and type proof"
+      nil_fields = !e[4].present || !e[3].present || !e[0].present || !e[5].present;
+      // :242-251 would panic on a nil challenge or short/nil InputValues / InputBlindingFactors
+      if (!nil_fields && (!e[6].present || !e[2].present || !e[1].present || iv.size() < ai.n_in || ibf.size() < ai.n_in))
+        panic = true;
+      // transfer.go:175: the range goroutine dereferences CommitmentToType
+      if (s.rc_applicable && !e[0].present) panic = true;
+      if (!nil_fields && !panic) {
+        scalar_from_bytes(e[3].raw, sc + TAS_SC_TYPE * 8, nullptr);
+        scalar_from_bytes(e[4].raw, sc + TAS_SC_TBF * 8, nullptr);
+        scalar_from_bytes(e[5].raw, sc + TAS_SC_EQ * 8, nullptr);
+        bool canon;
+        scalar_from_bytes(e[6].raw, sc + TAS_SC_CHAL * 8, &canon);
+        sa.chal_canonical = canon;
+        for (size_t j = 0; j < ai.n_in; j++) {
+          scalar_from_bytes(iv[j], sc + (TAS_SC_IV + j) * 8, nullptr);
+          scalar_from_bytes(ibf[j], sc + (TAS_SC_IV + ai.n_in + j) * 8, nullptr);
+        }
+      }
+    } else if (!e[0].present || !e[1].present || !e[2].present || !e[3].present) {
+      panic = true;  // sametype.go:169-171 dereferences every field
+    } else {
+      scalar_from_bytes(e[0].raw, sc + ST_SC_TYPE * 8, nullptr);
+      scalar_from_bytes(e[1].raw, sc + ST_SC_BF * 8, nullptr);
+      bool canon;
+      scalar_from_bytes(e[2].raw, sc + ST_SC_CHAL * 8, &canon);
+      sa.chal_canonical = canon;
+    }
+    if (panic) return fail(FTS_E_MALFORMED);
+    if (nil_fields) {
+      // element arrays / CT must still decode even when the proof is rejected for nil fields
+      G1A tmp;
+      if (e[0].present && !g1_from_bytes(raw, 64, tmp)) return fail(FTS_E_MALFORMED);
+      // the range proofs' slotted points too (the unslotted ones decoded above)
+      for (int j = 0; j < s.rp_count && s.rp_base >= 0; j++)
+        for (int q = 0; q < npts_rp; q++)
+          if (q != RP_PT_V && !g1_from_bytes(hp + o_rraw + ((size_t)(s.rp_base + j) * npts_rp + q) * 64, 64, tmp))
+            return fail(FTS_E_MALFORMED);
+      return fail(FTS_E_TAS_INVALID);
+    }
+  });
+  const double t1 = now_ms();
+  sl->parse_ms = (float)(t1 - t0);
+  // the slot's views: range-proof batch and sigma batch over the device copy
+  uint8_t* dv = sl->dev;
+  fts_rp_batch* b = sl->b;
+  b->B = rp_total;
+  b->raw = dv + o_rraw;
+  b->sc = reinterpret_cast<uint32_t*>(dv + o_rsc);
+  b->status0 = reinterpret_cast<int32_t*>(dv + o_rst);
+  b->ipa_flag = reinterpret_cast<int32_t*>(dv + o_ripa);
+  b->status = nullptr;  // never verified in place: the pass gathers it
+  b->dense = false;     // action calls have no batch across calls (FTS_GT_ADAPT)
+  b->merged = 1;
+  b->ntim = 0;
+  sl->rp_res.assign((size_t)rp_total, FTS_E_NOT_RUN);
+  sl->sig_res = reinterpret_cast<int32_t*>(hp + o_res);
+  SigBatchDev& sd = sl->sd;
+  sd = SigBatchDev{};
+  sd.A = SA;
+  sd.npts = pt_off;
+  sd.naff = aff_off;
+  sd.nwork = (int)nwork;
+  sd.act = reinterpret_cast<const SigAction*>(dv + o_act);
+  sd.raw = dv + o_raw;
+  sd.pt_owner = reinterpret_cast<int32_t*>(dv + o_owner);
+  sd.pts = reinterpret_cast<uint32_t*>(dv + w_pts);
+  sd.sc = reinterpret_cast<uint32_t*>(dv + o_sc);
+  sd.status = reinterpret_cast<int32_t*>(dv + o_sst);
+  sd.work = reinterpret_cast<int2*>(dv + o_work);
+  sd.terms = reinterpret_cast<uint32_t*>(dv + w_terms);
+  sd.aff = reinterpret_cast<uint32_t*>(dv + w_aff);
+  sd.aff_off = reinterpret_cast<int32_t*>(dv + o_affoff);
+  sd.msgs = dv + w_msgs;
+  sd.jac = reinterpret_cast<uint32_t*>(dv + w_jac);
+  sd.scratch = reinterpret_cast<uint32_t*>(dv + w_scratch);
+  sd.rp_k = k;
+  if (SA || rp_total) {
+    if (hipMemcpyAsync(dv, hp, in_end, hipMemcpyHostToDevice, sl->s) != hipSuccess ||
+        hipEventRecord(sl->done, sl->s) != hipSuccess || hipEventSynchronize(sl->done) != hipSuccess)
+      return FTS_API_EDEVICE;
   }
+  sl->stage_ms = (float)(now_ms() - t1);
   return FTS_API_OK;
 }
+
+// Verify an action call: stage it, let the dispatcher verify it (alone or with
+// other queued calls), then combine each action's sigma and range-proof verdicts
+// with the reference's precedence.
+static int act_verify(fts_ctx* c, const std::vector<ActionIn>& acts, int32_t* status, int32_t* fail_index) {
+  ActSlot* sl = aslot_acquire(c);
+  if (!sl) return FTS_API_ENOMEM;
+  int rc = act_stage(c, sl, acts);
+  if (rc == FTS_API_OK && (sl->sd.A || sl->b->B)) {
+    RpReq me(sl->b, sl->rp_res.data(), sl);
+    rc = rp_dispatch(c, me);
+  }
+  if (rc == FTS_API_OK) {
+    const std::vector<ActionState>& st = sl->st;
+    const int32_t* sig_res = sl->sig_res;
+    const int32_t* rp_res = sl->rp_res.data();
+    for (size_t i = 0; i < acts.size(); i++) {
+      const ActionState& s = st[i];
+      int32_t out = FTS_OK, idx = -1;
+      if (s.host_final >= 0) {
+        out = s.host_final;
+      } else {
+        const int32_t sig = sig_res[s.sig];
+        bool malformed = sig == FTS_E_MALFORMED;
+        for (int j = 0; j < s.rp_count && s.rp_base >= 0; j++) malformed |= rp_res[s.rp_base + j] == FTS_E_MALFORMED;
+        if (malformed) {
+          out = FTS_E_MALFORMED;                       // deserialisation precedes verification
+        } else if (sig != FTS_OK) {
+          out = sig;                                   // TypeAndSum / SameType error wins (transfer.go:192-196)
+        } else if (s.rc_applicable) {
+          if (s.rc_count_bad) {
+            out = FTS_E_RC_COUNT;                      // rangecorrectness.go:138-140
+          } else {
+            for (int j = 0; j < s.rp_count; j++)       // first failing index wins (:141-160)
+              if (rp_res[s.rp_base + j] != FTS_OK) {
+                out = rp_res[s.rp_base + j];
+                idx = j;
+                break;
+              }
+          }
+        }
+      }
+      status[i] = out;
+      if (fail_index) fail_index[i] = idx;
+    }
+  }
+  aslot_release(c, sl);
+  return rc;
+}
+
 
 extern "C" {
 
@@ -2556,8 +2771,7 @@ int fts_transfer_verify_batch(fts_ctx* c, size_t n, const fts_transfer_item* ite
     acts[i] = ActionIn{SIG_TAS, items[i].inputs, items[i].n_in, items[i].outputs, items[i].n_out,
                        der::Span{items[i].proof, items[i].proof ? items[i].proof_len : 0}};
   HIP_OK(hipSetDevice(c->device));
-  LaneGuard lg(c);
-  int rc = verify_actions(c, *lg.L, acts, status, fail_index);
+  int rc = act_verify(c, acts, status, fail_index);
   if (rc != FTS_API_OK)
     for (size_t i = 0; i < n; i++) status[i] = FTS_E_NOT_RUN;
   return rc;
@@ -2579,8 +2793,7 @@ int fts_issue_verify_batch(fts_ctx* c, size_t n, const fts_issue_item* items, in
     acts[i] = ActionIn{SIG_ST, nullptr, 0, items[i].tokens, items[i].n_tok,
                        der::Span{items[i].proof, items[i].proof ? items[i].proof_len : 0}};
   HIP_OK(hipSetDevice(c->device));
-  LaneGuard lg(c);
-  int rc = verify_actions(c, *lg.L, acts, status, fail_index);
+  int rc = act_verify(c, acts, status, fail_index);
   if (rc != FTS_API_OK)
     for (size_t i = 0; i < n; i++) status[i] = FTS_E_NOT_RUN;
   return rc;
@@ -2621,10 +2834,7 @@ int fts_actions_verify_batch(fts_ctx* c, size_t n_tr, const fts_transfer_item* t
   std::vector<int32_t> st(n, FTS_E_NOT_RUN), fi(n, -1);
   HIP_OK(hipSetDevice(c->device));
   int rc;
-  {
-    LaneGuard lg(c);
-    rc = verify_actions(c, *lg.L, acts, st.data(), fi.data());
-  }
+  rc = act_verify(c, acts, st.data(), fi.data());
   if (rc != FTS_API_OK) std::fill(st.begin(), st.end(), FTS_E_NOT_RUN);
   for (size_t i = 0; i < n_tr; i++) {
     status_tr[i] = st[i];
@@ -2683,8 +2893,7 @@ int fts_request_verify_batch(fts_ctx* c, size_t n, const uint8_t* const* req, co
   int rc = FTS_API_OK;
   if (!acts.empty()) {
     HIP_OK(hipSetDevice(c->device));
-    LaneGuard lg(c);
-    rc = verify_actions(c, *lg.L, acts, st.data(), fi.data());
+    rc = act_verify(c, acts, st.data(), fi.data());
   }
   // fold: first failing verified action, else the first structural verdict
   std::vector<int32_t> first(n, -1);  // index into acts of the request's first failing action

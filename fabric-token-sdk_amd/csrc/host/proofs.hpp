@@ -190,7 +190,7 @@ inline void parse_range_proof(der::Span rp, int k, uint8_t* pts, uint32_t* sc, i
 
 // Parse a RangeCorrectness (rangecorrectness.go:27-40): list of RangeProof DERs.
 inline bool parse_range_correctness(der::Span raw, std::vector<der::Span>& proofs) {
-  std::vector<der::Span> outer;
+  thread_local std::vector<der::Span> outer;  // reused (the host pool parses thousands per call)
   if (!der::unmarshal_values(raw, outer) || outer.size() != 1) return false;
   proofs.clear();
   if (outer[0].n == 0) return true;

@@ -108,12 +108,17 @@ class PublicParams:
     """A verification context: parsed public parameters plus their device
     tables (fixed-base windows of every generator) on one MI355X."""
 
-    def __init__(self, raw, bit_length=None, device=0, devices=None):
+    def __init__(self, raw, bit_length=None, device=0, devices=None, table_budget=None, wide_bits=None,
+                 lanes=None):
         """device: one HIP ordinal (FTS_DEVICE_NONE: host-only); devices: a list of
         ordinals -> a multi-device context (fts_ctx_create_devices) whose batch calls
-        shard over them and return verdicts in caller order"""
+        shard over them and return verdicts in caller order.  table_budget (bytes) /
+        wide_bits (20, 22) / lanes: fts_ctx_opts (fts_ctx_create_opts)"""
         self._ctx = C.c_void_p()
-        if devices is not None:
+        if devices is None and (table_budget or wide_bits or lanes):
+            o = L.CtxOpts(int(bit_length or 0), int(wide_bits or 0), int(table_budget or 0), int(lanes or 0), 0)
+            rc = L.lib.fts_ctx_create_opts(raw, len(raw), int(device), C.byref(o), C.byref(self._ctx))
+        elif devices is not None:
             arr = (C.c_int32 * len(devices))(*devices)
             rc = L.lib.fts_ctx_create_devices(raw, len(raw), int(bit_length or 0), arr, len(devices),
                                                C.byref(self._ctx))
@@ -126,6 +131,7 @@ class PublicParams:
         L.check("fts_ctx_info", L.lib.fts_ctx_info(self._ctx, C.byref(info)))
         self.bit_length, self.rounds, self.device = info.bit_length, info.rounds, info.device
         self.max_token, self.table_bytes = info.max_token, info.table_bytes
+        self.wide_bits, self.lanes = info.wide_bits, info.lanes
         devs = (C.c_int32 * 64)()
         self.devices = list(devs[:L.lib.fts_ctx_devices(self._ctx, devs, 64)])
 
@@ -139,6 +145,16 @@ class PublicParams:
             self.close()
         except Exception:
             pass
+
+    def hold(self, n):
+        """test hook (fts_debug_hold): no device pass starts until n calls are queued"""
+        L.check("fts_debug_hold", L.lib.fts_debug_hold(self._ctx, int(n)))
+
+    def dispatch_stats(self):
+        """(passes, calls served, most calls in one pass, action calls) since creation"""
+        out = (C.c_int64 * 4)()
+        L.check("fts_debug_dispatch_stats", L.lib.fts_debug_dispatch_stats(self._ctx, out))
+        return tuple(out)
 
     def reserve(self, max_pass_proofs=0):
         """pre-allocate every device lane for passes of up to max_pass_proofs

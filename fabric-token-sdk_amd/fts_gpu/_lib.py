@@ -61,13 +61,20 @@ EXPORTED = [
     "fts_ecdsa_last_timings", "fts_ctx_create_devices", "fts_ctx_create_mask", "fts_ctx_devices", "fts_shard_plan",
     "fts_idemix_ipk_create", "fts_idemix_ipk_destroy", "fts_nym_verify_batch", "fts_idemix_identity_nym",
     "fts_nym_last_timings", "fts_idemix_idv_create", "fts_idemix_idv_destroy", "fts_idemix_identity_verify_batch",
-    "fts_idemix_identity_last_timings", "fts_idemix_pairing_debug",
+    "fts_idemix_identity_last_timings", "fts_idemix_pairing_debug", "fts_ctx_create_opts", "fts_debug_hold",
+    "fts_debug_dispatch_stats",
 ]
 
 
 class PPInfo(C.Structure):
     _fields_ = [("bit_length", C.c_uint32), ("rounds", C.c_uint32), ("curve_id", C.c_uint32),
-                ("device", C.c_int32), ("max_token", C.c_uint64), ("table_bytes", C.c_uint64)]
+                ("device", C.c_int32), ("max_token", C.c_uint64), ("table_bytes", C.c_uint64),
+                ("wide_bits", C.c_uint32), ("lanes", C.c_uint32)]
+
+
+class CtxOpts(C.Structure):
+    _fields_ = [("bit_length", C.c_uint32), ("wide_bits", C.c_int32), ("table_budget", C.c_uint64),
+                ("lanes", C.c_int32), ("reserved", C.c_int32)]
 
 
 class TransferItem(C.Structure):
@@ -109,6 +116,9 @@ def _load():
         "fts_ctx_create_bits": ([U8P, S, C.c_uint32, C.c_int, C.POINTER(P)], C.c_int),
         "fts_ctx_destroy": ([P], None),
         "fts_ctx_info": ([P, C.POINTER(PPInfo)], C.c_int),
+        "fts_ctx_create_opts": ([U8P, S, C.c_int, C.POINTER(CtxOpts), C.POINTER(P)], C.c_int),
+        "fts_debug_hold": ([P, C.c_int], C.c_int),
+        "fts_debug_dispatch_stats": ([P, C.POINTER(C.c_int64)], C.c_int),
         "fts_rp_verify_batch": ([P, S, C.POINTER(C.c_void_p), C.POINTER(S), U8P, I32P], C.c_int),
         "fts_transfer_verify_batch": ([P, S, C.POINTER(TransferItem), I32P, I32P], C.c_int),
         "fts_issue_verify_batch": ([P, S, C.POINTER(IssueItem), I32P, I32P], C.c_int),

@@ -27,9 +27,12 @@
  * Return values: every function returns FTS_API_OK (0) or a negative
  * FTS_API_* code for API/driver errors (bad argument, HIP failure).
  * Per-item verdicts go to caller-owned int32 arrays as fts_status values.
- * Thread safety: a context runs up to FTS_LANES (default 4) calls concurrently,
- * each on its own HIP streams (main, side, batch check) and workspace; further
- * callers wait (range-proof batches are coalesced into the next free lane's pass).
+ * Thread safety: every verify entry point may be called concurrently.  Calls queue
+ * at one dispatcher per context; a free lane (FTS_LANES, default 4: its own HIP
+ * streams and workspace) takes the queue's head calls as ONE device pass -- the
+ * range proofs of staged batches, transfer, issue, mixed and request calls are
+ * verified together (up to FTS_COALESCE_MAX proofs), each call's sigma proofs beside
+ * them -- and every call gets exactly the verdicts it would get alone.
  */
 #ifndef FTS_GPU_H
 #define FTS_GPU_H
@@ -99,7 +102,24 @@ typedef struct fts_pp_info {
   int32_t device;           /* HIP device ordinal the context runs on */
   uint64_t max_token;
   uint64_t table_bytes;     /* device bytes of fixed-base tables */
+  uint32_t wide_bits;       /* window width of the per-proof bases' tables: 22 (11 additions per
+                               product, 1.5 GiB per base) or 20 (12, 436 MiB); fts_ctx_opts */
+  uint32_t lanes;           /* concurrent device passes (execution lanes) */
 } fts_pp_info;
+
+/* Context options (fts_ctx_create_opts); zero-initialise, then set what you need. */
+typedef struct fts_ctx_opts {
+  uint32_t bit_length;      /* 0: the PP's own (else as fts_ctx_create_bits) */
+  int32_t wide_bits;        /* 20 or 22: force the per-proof bases' window width; 0: by budget */
+  uint64_t table_budget;    /* with wide_bits 0: the most device bytes this context's fixed-base
+                               tables may take -- 22-bit tables only when all of them fit (at
+                               n = 64: 104 GiB; 20-bit: 33 GiB).  0: 22-bit only when the free
+                               HBM at creation exceeds them + 8 GiB per lane + 128 GiB (the first
+                               context on an empty MI355X), falling back to 20-bit if the
+                               allocation fails.  FTS_WIDE_BITS overrides the budget. */
+  int32_t lanes;            /* 0: FTS_LANES or 4 */
+  int32_t reserved;
+} fts_ctx_opts;
 
 /* One transfer action: commitments as 64-byte X||Y big-endian (G1.Bytes()). */
 typedef struct fts_transfer_item {
@@ -126,6 +146,8 @@ int fts_ctx_create(const uint8_t* pp, size_t pp_len, int device, fts_ctx** out);
 /* Same generators, range proofs truncated to bit_length (Setup(bit_length) semantics,
  * setup.go:388-406: labels do not depend on the bit length). */
 int fts_ctx_create_bits(const uint8_t* pp, size_t pp_len, uint32_t bit_length, int device, fts_ctx** out);
+/* Same, with explicit options (table budget, window width, lanes); opts may be NULL. */
+int fts_ctx_create_opts(const uint8_t* pp, size_t pp_len, int device, const fts_ctx_opts* opts, fts_ctx** out);
 /* Multi-device context (SURVEY §8b device_mask; the reference verifies every action
  * independently, core/common/validator.go:215-224): one child context per device (its
  * own tables, lanes, streams).  Every batch entry point below splits the caller's batch
@@ -205,6 +227,13 @@ int fts_rp_batch_verify(fts_ctx* ctx, fts_rp_batch* b, int32_t* status);
 int fts_ctx_reserve(fts_ctx* ctx, size_t max_pass_proofs);
 /* number of staged batches (including b) in the device pass that verified b last */
 int fts_rp_batch_merged(const fts_rp_batch* b);
+/* Test hook: no device pass starts until n calls (staged batches and action calls of any
+ * entry point) are queued, then the queue forms passes as usual (one-shot; n = 0 releases).
+ * Makes "these calls share one pass" deterministic in tests. */
+int fts_debug_hold(fts_ctx* ctx, int n);
+/* dispatcher counters since context creation: out[0] device passes, out[1] calls served,
+ * out[2] most calls in one pass, out[3] action calls (transfer / issue / actions / request) */
+int fts_debug_dispatch_stats(const fts_ctx* ctx, int64_t* out);
 /* per-kernel device time (ms) and algorithmic u32 MADs of b's last verification */
 int fts_rp_batch_timings(const fts_rp_batch* b, const char** names, float* ms, double* mads, int cap);
 void fts_rp_batch_free(fts_rp_batch* b);
