@@ -299,6 +299,10 @@ class HostPool {
     auto j = std::make_shared<Job>();
     j->n = n;
     j->f = &f;
+    // items are claimed in chunks: one atomic claim and one completion count per
+    // chunk, not per item (per-item counters bounced one cache line between every
+    // worker: ~0.8 us of overhead per parsed action with 8 threads)
+    j->grain = std::max<size_t>(1, std::min<size_t>(32, n / (8 * (size_t)host_threads())));
     {
       std::lock_guard<std::mutex> l(mu_);
       q_.push_back(j);
@@ -311,7 +315,7 @@ class HostPool {
 
  private:
   struct Job {
-    size_t n = 0;
+    size_t n = 0, grain = 1;
     const std::function<void(size_t)>* f = nullptr;
     std::atomic<size_t> next{0}, done{0};
     std::mutex m;
@@ -322,9 +326,10 @@ class HostPool {
     for (unsigned t = 0; t < nw; t++) std::thread([this] { loop(); }).detach();
   }
   static void work(Job& j) {
-    for (size_t i; (i = j.next++) < j.n;) {
-      (*j.f)(i);
-      if (++j.done == j.n) {
+    for (size_t i0; (i0 = j.next.fetch_add(j.grain)) < j.n;) {
+      const size_t i1 = std::min(j.n, i0 + j.grain);
+      for (size_t i = i0; i < i1; i++) (*j.f)(i);
+      if ((j.done += i1 - i0) == j.n) {
         std::lock_guard<std::mutex> l(j.m);
         j.cv.notify_all();
       }
@@ -422,8 +427,9 @@ struct ActSlot {
   int32_t* sig_res = nullptr;  // pinned: sigma verdicts [sd.A], downloaded by the pass
   std::vector<int32_t> rp_res;  // range-proof verdicts [b->B], scattered by the pass
   std::vector<ActionState> st;
-  std::vector<int> sig_of;
+  std::vector<uint8_t> host_buf;  // host-only contexts: the records (no device)
   float parse_ms = 0, stage_ms = 0;
+  float phase_ms[3] = {0, 0, 0};  // act_stage's shapes / layout / decode steps of the last call
 };
 
 // fts_rp_verify_batch staging slot (host DER bytes -> device): pinned host
@@ -1159,9 +1165,7 @@ static void parse_rp_into(int k, size_t B, const uint8_t* const* der_p, const si
   constexpr size_t CH = 256;
   parallel_for((B + CH - 1) / CH, 2, [&](size_t c) {
     for (size_t i = c * CH; i < std::min(B, (c + 1) * CH); i++) {
-      uint8_t* pts = raw + i * npts * 64;
-      memset(pts, 0, (size_t)npts * 64);
-      memset(sc + i * RP_NSC * 8, 0, RP_NSC * 32);
+      uint8_t* pts = raw + i * npts * 64;  // every slot written once below (no clearing pass)
       status[i] = 0;
       ipa[i] = 0;
       der::Span s{der_p[i], der_len[i]};
@@ -1415,6 +1419,7 @@ struct RpPass {
   std::vector<int> groups;
   std::vector<uint8_t> dense;  // per caller batch (groups[q] .. groups[q+1]): round-1 groups of 8; updated by the fallback
   double t_start = 0, t_prep = 0, t_enq = 0;
+  bool tl_started = false;  // the lane's timeline was begun by the caller (action passes: gather + sigma marks)
 };
 
 // Range-proof pipeline on B proofs already on the device: exact phase, RLC
@@ -1516,7 +1521,7 @@ static int rp_enqueue(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc
   if (getrandom(L.pin->key, sizeof L.pin->key, 0) != (ssize_t)sizeof L.pin->key) return FTS_API_EDEVICE;
   HIP_OK(hipMemcpyAsync(r.key, L.pin->key, sizeof L.pin->key, hipMemcpyHostToDevice, L.s));
   P.t_prep = now_ms();
-  L.tl.begin(L.s);
+  if (!P.tl_started) L.tl.begin(L.s);
   if (c->fx_serial) {
     // the wait, this pass's fixed-base launch and its event record are enqueued in
     // one critical section, so the chain of events follows the enqueue order
@@ -1661,6 +1666,8 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
       size_t B = 0;
       for (RpReq* q : rpq[j]) B += (size_t)q->b->B;
       Workspace& w = L.ws;
+      L.tl.begin(L.s);  // the gather and the sigma kernels on the pass's timeline
+      P[j].tl_started = true;
       RpGather g{};
       if (B > 0) {
         const size_t Bal = std::max(B, std::min(c->coalesce_max, (size_t)1 << 20));  // sized once for the largest pass
@@ -1682,6 +1689,7 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
         g.off[g.G] = (int)off;
         launch_rp_gather(g, c->k, w.rp_raw.as<uint8_t>(), w.rp_sc.as<uint32_t>(), w.rp_status.as<int32_t>(),
                          w.rp_ipa.as<int32_t>(), L.s);
+        L.tl.mark("k_rp_gather", L.s, 0);
       }
       Bs[j] = B;
       d_status[j] = w.rp_status.as<int32_t>();
@@ -1700,9 +1708,11 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
         h.sig.push_back(&sd);
         h.off.push_back(off);
       }
+      if (!h.sig.empty()) L.tl.mark("k_sig_prep", L.s, 0);
       if (B == 0) {  // sigma proofs only (e.g. 1-in/1-out transfers)
         sig_only[j] = 1;
         for (const SigBatchDev* sd : h.sig) launch_sig_finish(*sd, c->d_tables, c->n, L.s);
+        L.tl.mark("k_sig_finish", L.s, 0);
         HIP_OK(hipGetLastError());
         return FTS_API_OK;
       }
@@ -1711,9 +1721,9 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
         // the sigma equations on the lane's third stream beside the range-proof pass;
         // the batch check's variable part follows them there and first drops the range
         // proofs of actions whose sigma proof failed (k_sig_exclude)
-        HIP_OK(hipEventRecord(L.ev_a, L.s));
-        HIP_OK(hipStreamWaitEvent(L.s3, L.ev_a, 0));
+        L.tl.fork(L.s, L.s3);
         for (const SigBatchDev* sd : h.sig) launch_sig_finish(*sd, c->d_tables, c->n, L.s3);
+        L.tl.mark("k_sig_finish", L.s3, 0);
         HIP_OK(hipEventRecord(L.ev_b, L.s3));
         pre = [](void* arg, hipStream_t s) {
           SigHook* hk = static_cast<SigHook*>(arg);
@@ -1762,7 +1772,7 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
           break;
         }
       for (RpReq* q : sub[j]) {
-        if (!sig_only[j]) collect_timings(c, L, q->b);
+        collect_timings(c, L, q->b);
         q->b->merged = (int)sub[j].size();
       }
       return FTS_API_OK;
@@ -2447,61 +2457,63 @@ static int act_stage(fts_ctx* c, ActSlot* sl, const std::vector<ActionIn>& acts)
   const size_t A = acts.size();
   std::vector<ActionState>& st = sl->st;
   st.assign(A, ActionState{});
-  // ---- 1. shapes
-  parallel_for(A, 64, [&](size_t i) {
+  // Steps 1 and 3 run over chunks of CH consecutive actions; step 2 scans the
+  // chunks' totals only (a serial pass over every action re-read the per-action
+  // state the parse threads had just written: ~0.1 us per action of cache-line
+  // transfers), and step 3 lays its chunk out from the chunk's base.
+  constexpr size_t CH = 128;
+  const size_t nch = (A + CH - 1) / CH;
+  struct Run {
+    int sa = 0, pt = 0, sc = 0, term = 0, nfix = 0, aff = 0, rp = 0;
+    uint32_t msg = 0;
+    // advance past action (kind, n_in, n_out) with nrp slotted range proofs
+    void add(int kind, int n_in, int n_out, int nrp) {
+      sa++;
+      pt += 1 + n_in + n_out;
+      sc += sig_nscalars(kind, n_in);
+      term += sig_nterms(kind, n_in);
+      nfix += sig_nfixed(kind, n_in);
+      aff += sig_naff(kind, n_in, n_out);
+      msg += sig_msg_slot(kind, n_in, n_out);
+      rp += nrp;
+    }
+  };
+  std::vector<Run> base(nch);
+  // ---- 1. shapes, and each chunk's totals
+  parallel_for(nch, 2, [&](size_t q) {
     thread_local std::vector<der::Span> vals, rps;
-    const ActionIn& ai = acts[i];
-    ActionState& s = st[i];
-    if (!der::unmarshal_values(ai.proof, vals) || vals.size() != 2) {
-      s.host_final = FTS_E_MALFORMED;
-      return;
+    Run t;
+    for (size_t i = q * CH; i < std::min(A, (q + 1) * CH); i++) {
+      const ActionIn& ai = acts[i];
+      ActionState& s = st[i];
+      if (!der::unmarshal_values(ai.proof, vals) || vals.size() != 2) {
+        s.host_final = FTS_E_MALFORMED;
+        continue;
+      }
+      s.rc_applicable = ai.kind == SIG_ST || ai.n_in != 1 || ai.n_out != 1;
+      rps.clear();
+      if (vals[1].n && !parse_range_correctness(vals[1], rps)) {
+        s.host_final = FTS_E_MALFORMED;
+        continue;
+      }
+      s.rp_count = (int)rps.size();
+      const int n_in = ai.kind == SIG_TAS ? (int)ai.n_in : 0;
+      t.add(ai.kind, n_in, (int)ai.n_out, s.rc_applicable ? s.rp_count : 0);
     }
-    s.rc_applicable = ai.kind == SIG_ST || ai.n_in != 1 || ai.n_out != 1;
-    rps.clear();
-    if (vals[1].n && !parse_range_correctness(vals[1], rps)) {
-      s.host_final = FTS_E_MALFORMED;
-      return;
-    }
-    s.rp_count = (int)rps.size();
+    base[q] = t;
   });
-  // ---- 2. layout
-  std::vector<SigAction> sact;
-  std::vector<int> fx(A, 0), vr(A, 0), affo;
-  std::vector<int>& sig_of = sl->sig_of;
-  sig_of.assign(A, -1);
-  int term_off = 0, aff_off = 0, pt_off = 0, sc_off = 0, rp_total = 0, nfix_total = 0;
-  uint32_t msg_off = 0;
-  for (size_t i = 0; i < A; i++) {
-    ActionState& s = st[i];
-    if (s.host_final >= 0) continue;
-    const ActionIn& ai = acts[i];
-    if (s.rc_applicable && s.rp_count > 0) {
-      s.rp_base = rp_total;
-      rp_total += s.rp_count;
-    }
-    SigAction sa{};
-    sa.kind = ai.kind;
-    sa.n_in = ai.kind == SIG_TAS ? (int)ai.n_in : 0;
-    sa.n_out = (int)ai.n_out;
-    sa.pt_off = pt_off;
-    sa.sc_off = sc_off;
-    sa.term_off = term_off;
-    sa.msg_off = (int32_t)msg_off;
-    sa.rp_base = s.rp_base;
-    sa.rp_count = s.rp_count;
-    s.sig = sig_of[i] = (int)sact.size();
-    fx[i] = nfix_total;
-    vr[i] = term_off - nfix_total;
-    affo.push_back(aff_off);
-    nfix_total += sig_nfixed(sa.kind, sa.n_in);
-    pt_off += 1 + sa.n_in + sa.n_out;
-    sc_off += sig_nscalars(sa.kind, sa.n_in);
-    term_off += sig_nterms(sa.kind, sa.n_in);
-    aff_off += sig_naff(sa.kind, sa.n_in, sa.n_out);
-    msg_off += sig_msg_slot(sa.kind, sa.n_in, sa.n_out);
-    sact.push_back(sa);
+  const double t_p1 = now_ms();
+  // ---- 2. chunk bases (exclusive scan) and the totals
+  Run tot;
+  for (size_t q = 0; q < nch; q++) {
+    const Run t = base[q];
+    base[q] = tot;
+    tot.sa += t.sa, tot.pt += t.pt, tot.sc += t.sc, tot.term += t.term, tot.nfix += t.nfix, tot.aff += t.aff;
+    tot.rp += t.rp, tot.msg += t.msg;
   }
-  const int SA = (int)sact.size();
+  const int SA = tot.sa, pt_off = tot.pt, sc_off = tot.sc, term_off = tot.term, nfix_total = tot.nfix,
+            aff_off = tot.aff, rp_total = tot.rp;
+  const uint32_t msg_off = tot.msg;
   const size_t nwork = (size_t)term_off;
   size_t o = 0;
   auto region = [&](size_t bytes) {  // 256-byte aligned regions
@@ -2521,31 +2533,51 @@ static int act_stage(fts_ctx* c, ActSlot* sl, const std::vector<ActionIn>& acts)
   const size_t w_pts = region((size_t)pt_off * 64), w_terms = region(nwork * 96), w_aff = region((size_t)aff_off * 64),
                w_jac = region((size_t)aff_off * 96), w_msgs = region(msg_off),
                w_scratch = region(sig_scratch_words(nwork) * 4), dev_end = o;
-  if (!aslot_size(sl, std::max<size_t>(pin_end, 256), std::max<size_t>(dev_end, 256))) return FTS_API_ENOMEM;
-  uint8_t* hp = sl->pin;
+  uint8_t* hp;
+  if (c->device < 0) {  // host-only context (fts_debug_stage_actions): the parse alone, into host memory
+    sl->host_buf.resize(std::max<size_t>(pin_end, 256));
+    hp = sl->host_buf.data();
+  } else {
+    if (!aslot_size(sl, std::max<size_t>(pin_end, 256), std::max<size_t>(dev_end, 256))) return FTS_API_ENOMEM;
+    hp = sl->pin;
+  }
   SigAction* hact = reinterpret_cast<SigAction*>(hp + o_act);
   int32_t* hsst = reinterpret_cast<int32_t*>(hp + o_sst);
   int32_t* hrst = reinterpret_cast<int32_t*>(hp + o_rst);
   int32_t* hripa = reinterpret_cast<int32_t*>(hp + o_ripa);
   int32_t* howner = reinterpret_cast<int32_t*>(hp + o_owner);
+  int32_t* haffo = reinterpret_cast<int32_t*>(hp + o_affoff);
   int2* hwork = reinterpret_cast<int2*>(hp + o_work);
-  // ---- 3. decode into the layout
-  parallel_for(A, 64, [&](size_t i) {
+  // one action: its records at the running offsets, then its decode
+  auto decode_one = [&](size_t i, Run& run) {
     thread_local std::vector<der::Span> vals, rps, ubuf, ibf, iv;
     ActionState& s = st[i];
-    const int g = sig_of[i];
-    if (g < 0) return;
+    if (s.host_final >= 0) return;
     const ActionIn& ai = acts[i];
+    const int g = run.sa;
+    s.sig = g;
+    const int n_in = ai.kind == SIG_TAS ? (int)ai.n_in : 0;
     SigAction& sa = hact[g];
-    sa = sact[g];
+    sa = SigAction{};
+    sa.kind = ai.kind;
+    sa.n_in = n_in;
+    sa.n_out = (int)ai.n_out;
+    sa.pt_off = run.pt;
+    sa.sc_off = run.sc;
+    sa.term_off = run.term;
+    sa.msg_off = (int32_t)run.msg;
+    s.rp_base = s.rc_applicable && s.rp_count > 0 ? run.rp : -1;
+    sa.rp_base = s.rp_base;
+    sa.rp_count = s.rp_count;
     hsst[g] = 0;
-    reinterpret_cast<int32_t*>(hp + o_affoff)[g] = affo[g];
+    haffo[g] = run.aff;
     const int npt = 1 + sa.n_in + sa.n_out;
     for (int q = 0; q < npt; q++) howner[sa.pt_off + q] = g;
     // work list: every fixed-base term first, then every variable-base (GLV) term,
     // so no wave of k_sig_terms runs both kinds of product
-    for (int t = 0, nt = sig_nterms(sa.kind, sa.n_in), fi = fx[i], vi = nfix_total + vr[i]; t < nt; t++)
+    for (int t = 0, nt = sig_nterms(sa.kind, sa.n_in), fi = run.nfix, vi = nfix_total + run.term - run.nfix; t < nt; t++)
       hwork[sig_term_var(sa.kind, sa.n_in, t) ? vi++ : fi++] = make_int2(g, t);
+    run.add(ai.kind, n_in, (int)ai.n_out, s.rc_applicable ? s.rp_count : 0);
     // a rejected action keeps its records, skipped by every kernel
     auto fail = [&](int32_t v) {
       s.host_final = v;
@@ -2655,9 +2687,18 @@ static int act_stage(fts_ctx* c, ActSlot* sl, const std::vector<ActionIn>& acts)
             return fail(FTS_E_MALFORMED);
       return fail(FTS_E_TAS_INVALID);
     }
+  };
+  const double t_p2 = now_ms();
+  // ---- 3. lay out and decode, chunk by chunk from its base
+  parallel_for(nch, 2, [&](size_t q) {
+    Run run = base[q];
+    for (size_t i = q * CH; i < std::min(A, (q + 1) * CH); i++) decode_one(i, run);
   });
   const double t1 = now_ms();
   sl->parse_ms = (float)(t1 - t0);
+  sl->phase_ms[0] = (float)(t_p1 - t0);
+  sl->phase_ms[1] = (float)(t_p2 - t_p1);
+  sl->phase_ms[2] = (float)(t1 - t_p2);
   // the slot's views: range-proof batch and sigma batch over the device copy
   uint8_t* dv = sl->dev;
   fts_rp_batch* b = sl->b;
@@ -2692,7 +2733,7 @@ static int act_stage(fts_ctx* c, ActSlot* sl, const std::vector<ActionIn>& acts)
   sd.jac = reinterpret_cast<uint32_t*>(dv + w_jac);
   sd.scratch = reinterpret_cast<uint32_t*>(dv + w_scratch);
   sd.rp_k = k;
-  if (SA || rp_total) {
+  if ((SA || rp_total) && c->device >= 0) {
     if (hipMemcpyAsync(dv, hp, in_end, hipMemcpyHostToDevice, sl->s) != hipSuccess ||
         hipEventRecord(sl->done, sl->s) != hipSuccess || hipEventSynchronize(sl->done) != hipSuccess)
       return FTS_API_EDEVICE;
@@ -2748,6 +2789,34 @@ static int act_verify(fts_ctx* c, const std::vector<ActionIn>& acts, int32_t* st
   }
   aslot_release(c, sl);
   return rc;
+}
+
+// host-side cost of act_stage (parse + layout, no device): tools/host_parse_bench.py
+extern "C" int fts_debug_stage_actions(fts_ctx* c, size_t n_tr, const fts_transfer_item* transfers, size_t n_is,
+                                       const fts_issue_item* issues, int reps, float* ms_avg) {
+  if (!c || (n_tr && !transfers) || (n_is && !issues) || reps < 1 || c->device >= 0 || !c->shards.empty())
+    return FTS_API_EINVAL;
+  std::vector<ActionIn> acts;
+  for (size_t i = 0; i < n_tr; i++)
+    acts.push_back(ActionIn{SIG_TAS, transfers[i].inputs, transfers[i].n_in, transfers[i].outputs, transfers[i].n_out,
+                            der::Span{transfers[i].proof, transfers[i].proof ? transfers[i].proof_len : 0}});
+  for (size_t i = 0; i < n_is; i++)
+    acts.push_back(ActionIn{SIG_ST, nullptr, 0, issues[i].tokens, issues[i].n_tok,
+                            der::Span{issues[i].proof, issues[i].proof ? issues[i].proof_len : 0}});
+  ActSlot sl;
+  fts_rp_batch b;
+  sl.b = &b;
+  double tot[4] = {0, 0, 0, 0};
+  if (int rc = act_stage(c, &sl, acts)) return rc;  // untimed: the slot's buffers grow (page faults) once
+  for (int r = 0; r < reps; r++) {
+    if (int rc = act_stage(c, &sl, acts)) return rc;
+    tot[0] += sl.parse_ms;
+    for (int q = 0; q < 3; q++) tot[1 + q] += sl.phase_ms[q];
+  }
+  sl.b = nullptr;
+  if (ms_avg)
+    for (int q = 0; q < 4; q++) ms_avg[q] = (float)(tot[q] / reps);
+  return FTS_API_OK;
 }
 
 

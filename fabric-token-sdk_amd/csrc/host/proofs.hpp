@@ -88,90 +88,79 @@ inline void filler_point(uint8_t out[64]) {
 
 // Parse one RangeProof.  pts: (5 + 2k) x 64 raw slots (slot RP_PT_V untouched),
 // sc: 5 x 8 words.  status <- 0 / FTS_E_MALFORMED / FTS_E_RP_NIL;
-// ipa_flag <- 0 / FTS_E_IPA_NIL / FTS_E_IPA_LEN (deferred: reported only if E1 holds)
+// ipa_flag <- 0 / FTS_E_IPA_NIL / FTS_E_IPA_LEN (deferred: reported only if E1 holds).
+// Every slot is written once: the proof's point, or the filler where the proof has
+// none (nil element, unslotted IPA arrays, or a rejected proof) -- the records go
+// straight to pinned staging memory, where a filler pass before the copy would double
+// the bytes written per proof.
 inline void parse_range_proof(der::Span rp, int k, uint8_t* pts, uint32_t* sc, int32_t& status, int32_t& ipa_flag) {
   status = 0;
   ipa_flag = 0;
   const int npts = 5 + 2 * k;
-  for (int j = 0; j < npts; j++)
-    if (j != 4) filler_point(pts + j * 64);
   memset(sc, 0, 5 * 32);
+  bool data_pts = false, ipa_pts = false;  // slots 0-3 / 5.. written
+  auto reject = [&]() {
+    for (int j = 0; j < npts; j++)
+      if (j != 4) filler_point(pts + j * 64);
+    status = FTS_E_MALFORMED;
+  };
   // per-thread reused buffers: the host pool parses thousands of proofs per call
   thread_local std::vector<der::Span> vals, ubuf, Ls, Rs;
-  if (!der::unmarshal_values(rp, vals) || vals.size() != 2) {
-    status = FTS_E_MALFORMED;
-    return;
-  }
+  if (!der::unmarshal_values(rp, vals) || vals.size() != 2) return reject();
   bool nil = false;
   // ---- RangeProofData (bulletproof.go:49-83)
   if (vals[0].n == 0) {
     nil = true;
   } else {
     Unmarshaller u(vals[0], ubuf);
-    if (!u.ok) {
-      status = FTS_E_MALFORMED;
-      return;
-    }
+    if (!u.ok) return reject();
     // order T1, T2, Tau, C, D, Delta, IP ; kinds: 0 = G1 slot, 1 = Zr slot
     const int kind[7] = {0, 0, 1, 0, 0, 1, 1};
     const int slot[7] = {0, 1, 0, 2, 3, 1, 2};  // pt slot or scalar slot (Tau=0, Delta=1, IP=2)
+    data_pts = true;
     for (int f = 0; f < 7; f++) {
       Elem e;
-      if (!u.next(e)) {
-        status = FTS_E_MALFORMED;
-        return;
-      }
+      if (!u.next(e)) return reject();
       if (!e.present) {
         nil = true;
+        if (kind[f] == 0) filler_point(pts + slot[f] * 64);
         continue;
       }
       if (kind[f] == 0) {
-        if (e.raw.n != 64) {
-          status = FTS_E_MALFORMED;
-          return;
-        }
+        if (e.raw.n != 64) return reject();
         memcpy(pts + slot[f] * 64, e.raw.p, 64);
       } else {
         scalar_from_bytes(e.raw, sc + slot[f] * 8, nullptr);
       }
     }
   }
+  if (!data_pts)
+    for (int j = 0; j < 4; j++) filler_point(pts + j * 64);
   // ---- IPA (ipa.go:45-67)
   if (vals[1].n == 0) {
     ipa_flag = FTS_E_IPA_NIL;
   } else {
     Unmarshaller u(vals[1], ubuf);
-    if (!u.ok) {
-      status = FTS_E_MALFORMED;
-      return;
-    }
+    if (!u.ok) return reject();
     Elem eL, eR, aL, aR;
-    if (!u.next(eL) || !u.next(eR) || !u.next(aL) || !u.next(aR)) {
-      status = FTS_E_MALFORMED;
-      return;
-    }
+    if (!u.next(eL) || !u.next(eR) || !u.next(aL) || !u.next(aR)) return reject();
     if (eL.present) scalar_from_bytes(eL.raw, sc + 3 * 8, nullptr);
     if (eR.present) scalar_from_bytes(eR.raw, sc + 4 * 8, nullptr);
     Ls.clear();
     Rs.clear();
-    if (aL.present && !der::unmarshal_values(aL.raw, Ls, true)) {
-      status = FTS_E_MALFORMED;
-      return;
-    }
-    if (aR.present && !der::unmarshal_values(aR.raw, Rs, true)) {
-      status = FTS_E_MALFORMED;
-      return;
-    }
+    if (aL.present && !der::unmarshal_values(aL.raw, Ls, true)) return reject();
+    if (aR.present && !der::unmarshal_values(aR.raw, Rs, true)) return reject();
     for (auto& s : Ls)
-      if (s.n != 64) return void(status = FTS_E_MALFORMED);
+      if (s.n != 64) return reject();
     for (auto& s : Rs)
-      if (s.n != 64) return void(status = FTS_E_MALFORMED);
+      if (s.n != 64) return reject();
     if (!eL.present || !eR.present) {
       ipa_flag = FTS_E_IPA_NIL;
     } else if (Ls.size() != Rs.size() || (int)Ls.size() != k) {
       ipa_flag = FTS_E_IPA_LEN;
     }
     if (ipa_flag == 0) {
+      ipa_pts = true;
       for (int j = 0; j < k; j++) {
         memcpy(pts + (5 + j) * 64, Ls[j].p, 64);
         memcpy(pts + (5 + k + j) * 64, Rs[j].p, 64);
@@ -180,11 +169,13 @@ inline void parse_range_proof(der::Span rp, int k, uint8_t* pts, uint32_t* sc, i
       // unslotted points still have to decode (deserialization precedes verification)
       G1A tmp;
       for (auto& s : Ls)
-        if (!g1_from_bytes(s.p, 64, tmp)) return void(status = FTS_E_MALFORMED);
+        if (!g1_from_bytes(s.p, 64, tmp)) return reject();
       for (auto& s : Rs)
-        if (!g1_from_bytes(s.p, 64, tmp)) return void(status = FTS_E_MALFORMED);
+        if (!g1_from_bytes(s.p, 64, tmp)) return reject();
     }
   }
+  if (!ipa_pts)
+    for (int j = 5; j < npts; j++) filler_point(pts + j * 64);
   if (nil) status = FTS_E_RP_NIL;
 }
 

@@ -62,7 +62,7 @@ EXPORTED = [
     "fts_idemix_ipk_create", "fts_idemix_ipk_destroy", "fts_nym_verify_batch", "fts_idemix_identity_nym",
     "fts_nym_last_timings", "fts_idemix_idv_create", "fts_idemix_idv_destroy", "fts_idemix_identity_verify_batch",
     "fts_idemix_identity_last_timings", "fts_idemix_pairing_debug", "fts_ctx_create_opts", "fts_debug_hold",
-    "fts_debug_dispatch_stats",
+    "fts_debug_dispatch_stats", "fts_debug_stage_actions",
 ]
 
 
@@ -119,6 +119,8 @@ def _load():
         "fts_ctx_create_opts": ([U8P, S, C.c_int, C.POINTER(CtxOpts), C.POINTER(P)], C.c_int),
         "fts_debug_hold": ([P, C.c_int], C.c_int),
         "fts_debug_dispatch_stats": ([P, C.POINTER(C.c_int64)], C.c_int),
+        "fts_debug_stage_actions": ([P, S, C.POINTER(TransferItem), S, C.POINTER(IssueItem), C.c_int,
+                                     C.POINTER(C.c_float)], C.c_int),
         "fts_rp_verify_batch": ([P, S, C.POINTER(C.c_void_p), C.POINTER(S), U8P, I32P], C.c_int),
         "fts_transfer_verify_batch": ([P, S, C.POINTER(TransferItem), I32P, I32P], C.c_int),
         "fts_issue_verify_batch": ([P, S, C.POINTER(IssueItem), I32P, I32P], C.c_int),

@@ -231,6 +231,11 @@ int fts_rp_batch_merged(const fts_rp_batch* b);
  * entry point) are queued, then the queue forms passes as usual (one-shot; n = 0 releases).
  * Makes "these calls share one pass" deterministic in tests. */
 int fts_debug_hold(fts_ctx* ctx, int n);
+/* Host cost of an action call's staging (DER parse into the device layout, no device;
+ * ctx must be host-only: FTS_DEVICE_NONE): ms_avg[0..3] <- mean wall ms over reps of the
+ * whole staging and of its three steps (shapes, layout, decode). */
+int fts_debug_stage_actions(fts_ctx* ctx, size_t n_tr, const fts_transfer_item* transfers, size_t n_is,
+                            const fts_issue_item* issues, int reps, float* ms_avg);
 /* dispatcher counters since context creation: out[0] device passes, out[1] calls served,
  * out[2] most calls in one pass, out[3] action calls (transfer / issue / actions / request) */
 int fts_debug_dispatch_stats(const fts_ctx* ctx, int64_t* out);
