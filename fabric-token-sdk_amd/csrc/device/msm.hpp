@@ -103,16 +103,13 @@ inline double msm_cost(int N, int c) {
   return (double)nw * ((double)N * 11.0 + (double)(1 << c) * 16.0);
 }
 
-// largest window width a plan may take (FTS_MSM_MAXC, set by context creation;
-// process-wide): narrower windows trade bucket-phase work for a shorter reduction
-inline int g_msm_maxc = 16;
-
 // G groups of ptsg points (N = G * ptsg, or fewer in the last group); the window
-// width minimises the per-group bucket cost
-inline void msm_layout_groups(int N, int G, int ptsg, MsmPlan& p) {
+// width minimises the per-group bucket cost up to maxc (the context's FTS_MSM_MAXC:
+// narrower windows trade bucket-phase work for a shorter reduction)
+inline void msm_layout_groups(int N, int G, int ptsg, MsmPlan& p, int maxc = 16) {
   const int NV = 2 * N, NVg = 2 * ptsg;
   int best = 4;
-  for (int c = 5; c <= g_msm_maxc; c++)
+  for (int c = 5; c <= maxc; c++)
     if (msm_cost(NVg, c) < msm_cost(NVg, best)) best = c;
   const int c = best;
   const int nw = (MSM_BITS + c - 1) / c;
@@ -156,7 +153,7 @@ inline void msm_layout_groups(int N, int G, int ptsg, MsmPlan& p) {
   p.sel_pts = 1;
   p.local_sort = true;
 }
-inline void msm_layout(int N, MsmPlan& p) { msm_layout_groups(N, 1, N > 0 ? N : 1, p); }
+inline void msm_layout(int N, MsmPlan& p, int maxc = 16) { msm_layout_groups(N, 1, N > 0 ? N : 1, p, maxc); }
 // points per bucket-accumulation chunk (and the chunk-slot count that follows)
 inline void msm_set_chunk(MsmPlan& p, int ch) {
   p.ch = ch;

@@ -527,10 +527,12 @@ struct fts_ctx {
   // sparse, first the single-fault locator (rp_locate_single): one index-weighted
   // recombination + a lane per proof, instead of the group test's grouped MSM
   bool locate = true;
-  // after a miss (several bad proofs) the next locate_backoff failing passes skip
-  // the locator, the backoff doubling per consecutive miss (8 .. 256) and reset
-  // by a hit: a stream of multi-fault passes (C5, tampered C2) pays it rarely
-  std::atomic<int> locate_skip{0}, locate_backoff{8};
+  // after a miss (several bad proofs) each caller batch of the pass that holds a bad
+  // proof skips the locator in its next locate_backoff failing passes, the backoff
+  // doubling per consecutive miss (8 .. 256) and reset by a hit: a stream of
+  // multi-fault batches (C5, tampered C2) pays it rarely.  Kept per caller batch
+  // (fts_rp_batch::locate_skip), so one caller's multi-fault passes never make
+  // another caller's single-fault passes skip the locator
   // FTS_GT_ADAPT: a staged caller batch's round-1 group size follows the bad-proof
   // density of ITS last failed verification (fts_rp_batch::dense; per caller batch,
   // so one caller's tampered batches never change the fallback of another's).
@@ -545,6 +547,9 @@ struct fts_ctx {
   // FTS_MSM_SORT: the MSMs' two-level counting sort (msm.hip k_rs_*; 0: k_msm_digits'
   // device atomics + k_msm_scatter, the round-4 batch-check sort, for A/B)
   int msm_sort = 1;
+  // FTS_MSM_MAXC: the widest MSM window this context's plans take (per context: one
+  // context's setting never changes another's plans)
+  int msm_maxc = 16;
   // FTS_MAIN_GROUPS=1: a coalesced pass checks one random linear combination PER CALLER
   // BATCH (a G-group MSM + per-group column sums), so a bad proof's fallback covers
   // its own batch only.  Default 0 (one combination over the pass): the grouped MSM's
@@ -607,6 +612,7 @@ struct fts_rp_batch {
   std::vector<size_t> bounds;
   int merged = 1;  // batches in the device pass that verified it last
   bool dense = false;  // its last failed verification found dense bad proofs (FTS_GT_ADAPT)
+  int locate_skip = 0, locate_backoff = 8;  // single-fault locator backoff (fts_ctx::locate)
   // timings of this batch's last verification
   int ntim = 0;
   const char* tim_name[Timeline::CAP];
@@ -723,10 +729,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_GT2_MIN")) c->gt2_min = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_GT_ADAPT")) c->gt_adapt = atoi(e) != 0;
   if (const char* e = getenv("FTS_LOCATE")) c->locate = atoi(e) != 0;
-  {
-    const char* e = getenv("FTS_MSM_MAXC");
-    g_msm_maxc = e ? std::max(8, std::min(16, atoi(e))) : 16;
-  }
+  if (const char* e = getenv("FTS_MSM_MAXC")) c->msm_maxc = std::max(8, std::min(16, atoi(e)));
   // FTS_WAVE_PRIO: one digit 0-3 per PrioSlot (device/wave_prio.hpp), e.g.
   // 022113313133; the table is per device and process: every context uploads its
   // own (the default without the variable), the last one created on a device wins
@@ -1220,9 +1223,9 @@ static void collect_timings(fts_ctx* c, Lane& L, fts_rp_batch* b) {
 // MSM plan for N real points on lane L's workspace (buffers grown as needed,
 // window table uploaded on L.s).  Returns 0 or FTS_API_ENOMEM.
 static int msm_prepare_plan(Lane& L, MsmPlan& mp, int slot);
-static int msm_prepare(Lane& L, int N, MsmPlan& mp, int slot, int ch = MSM_CH, bool local_sort = false) {
+static int msm_prepare(Lane& L, int N, MsmPlan& mp, int slot, int ch, bool local_sort, int maxc) {
   mp = MsmPlan{};
-  msm_layout(N, mp);
+  msm_layout(N, mp, maxc);
   if (ch != MSM_CH) msm_set_chunk(mp, ch);
   mp.local_sort = local_sort;
   return msm_prepare_plan(L, mp, slot);
@@ -1286,7 +1289,7 @@ static int rp_buffers(fts_ctx* c, Lane& L, int B) {
 static int lane_reserve(fts_ctx* c, Lane& L, int B, bool inputs) {
   const int npts = rp_npts(c->k);
   MsmPlan big{};
-  if (int rc = msm_prepare(L, B * npts, big, MSM_SLOT_RESERVE)) return rc;
+  if (int rc = msm_prepare(L, B * npts, big, MSM_SLOT_RESERVE, MSM_CH, c->msm_sort != 0, c->msm_maxc)) return rc;
   if (int rc = rp_buffers(c, L, B)) return rc;
   Workspace& w = L.ws;
   if (inputs && (w.rp_raw.ensure((size_t)B * npts * 64) || w.rp_sc.ensure((size_t)B * RP_NSC * 32) ||
@@ -1354,7 +1357,8 @@ static int rp_group_fallback(fts_ctx* c, Lane& L, const RpBatchDev& d, const Rlc
   auto group_test = [&](const int32_t* sel, int G, int gs) -> int {
     if (G == 0) return FTS_API_OK;
     MsmPlan gp{};
-    msm_layout_groups(G * gs * npts, G, gs * npts, gp);
+    msm_layout_groups(G * gs * npts, G, gs * npts, gp, c->msm_maxc);
+    gp.local_sort = c->msm_sort != 0;  // FTS_MSM_SORT covers the group tests' MSMs too
     gp.sel = sel;
     gp.sel_pts = npts;
     if (int rc = msm_prepare_plan(L, gp, gs == RP_GT2 ? MSM_SLOT_GT_SMALL : MSM_SLOT_GT_BIG)) return rc;
@@ -1419,7 +1423,9 @@ struct RpPass {
   std::vector<int> groups;
   std::vector<uint8_t> dense;  // per caller batch (groups[q] .. groups[q+1]): round-1 groups of 8; updated by the fallback
   double t_start = 0, t_prep = 0, t_enq = 0;
-  bool tl_started = false;  // the lane's timeline was begun by the caller (action passes: gather + sigma marks)
+  bool tl_started = false;
+  std::vector<fts_rp_batch*> bats;  // the caller batches of the pass (groups order); empty: none
+  int located = -1;                 // the locator: 1 hit, 0 missed, -1 not run  // the lane's timeline was begun by the caller (action passes: gather + sigma marks)
 };
 
 // Range-proof pipeline on B proofs already on the device: exact phase, RLC
@@ -1448,7 +1454,7 @@ static int rp_enqueue(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc
   int gs = 0;
   if (grouped) {
     for (int q = 0; q < G; q++) gs = std::max(gs, groups[q + 1] - groups[q]);
-    msm_layout_groups(G * gs * npts, G, gs * npts, mp);
+    msm_layout_groups(G * gs * npts, G, gs * npts, mp, c->msm_maxc);
     mp.local_sort = c->msm_sort != 0;
     Workspace& w0 = L.ws;
     const size_t NC = rlc_ncols(n);
@@ -1468,7 +1474,7 @@ static int rp_enqueue(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc
     mp.sel = uniform && groups[G] == G * gs ? nullptr : w0.r_msel.as<int32_t>();
     mp.sel_pts = npts;
     if (int rc = msm_prepare_plan(L, mp, MSM_SLOT_PASS)) return rc;
-  } else if (int rc = msm_prepare(L, N, mp, MSM_SLOT_PASS, MSM_CH, c->msm_sort != 0)) {
+  } else if (int rc = msm_prepare(L, N, mp, MSM_SLOT_PASS, MSM_CH, c->msm_sort != 0, c->msm_maxc)) {
     return rc;
   }
   if (int rc = rp_buffers(c, L, B)) return rc;
@@ -1592,18 +1598,22 @@ static int rp_finish(fts_ctx* c, Lane& L, RpPass& P) {
     return rp_group_fallback(c, L, P.d, P.r, P.groups, P.dense, &only);
   }
   if (c->locate && P.d.B > 1 && std::none_of(P.dense.begin(), P.dense.end(), [](uint8_t x) { return x != 0; })) {
-    if (c->locate_skip.load() > 0) {
-      c->locate_skip--;
-    } else {
+    // a batch of the pass still in its backoff skips the locator for the whole pass
+    bool skip = false;
+    for (fts_rp_batch* b : P.bats)
+      if (b->locate_skip > 0) {
+        b->locate_skip--;
+        skip = true;
+      }
+    if (!skip) {
       const int rc = rp_locate_single(c, L, P);
       if (rc < 0) return rc;
+      P.located = rc;
       if (rc == 1) {
-        c->locate_backoff = 8;
+        for (fts_rp_batch* b : P.bats) b->locate_backoff = 8;
         return FTS_API_OK;
       }
-      const int bo = c->locate_backoff.load();
-      c->locate_skip = bo;
-      c->locate_backoff = std::min(2 * bo, 256);
+      // missed: the batches holding bad proofs back off once the verdicts are in (run_rp_groups)
     }
   }
   return rp_group_fallback(c, L, P.d, P.r, P.groups, P.dense);
@@ -1739,7 +1749,10 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
                         w.rp_ipa.as<int32_t>(), [] {}, groups, P[j], pre, pre ? &h : nullptr);
     };
     rc[j] = enq();
-    for (RpReq* q : rpq[j]) P[j].dense.push_back(q->b->dense ? 1 : 0);
+    for (RpReq* q : rpq[j]) {
+      P[j].dense.push_back(q->b->dense ? 1 : 0);
+      P[j].bats.push_back(q->b);
+    }
   }
   for (size_t j = 0; j < m; j++) {
     Lane& L = *lanes[j];
@@ -1762,7 +1775,12 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
       HIP_OK(L.sync());
       for (size_t i = 0; i < rpq[j].size(); i++) {
         RpReq* q = rpq[j][i];
-        if (q->status) memcpy(q->status, pst + first[j][i], (size_t)q->b->B * 4);
+        const int32_t* v = pst + first[j][i];
+        if (q->status) memcpy(q->status, v, (size_t)q->b->B * 4);
+        if (P[j].located == 0 && std::any_of(v, v + q->b->B, [](int32_t x) { return x != 0; })) {
+          q->b->locate_skip = q->b->locate_backoff;  // a batch of a multi-fault pass that holds bad proofs
+          q->b->locate_backoff = std::min(2 * q->b->locate_backoff, 256);
+        }
       }
       // host-side timings of the pass: the first action call's parse and staging
       for (RpReq* q : sub[j])
@@ -2206,7 +2224,8 @@ int fts_msm_run(fts_ctx* c, fts_msm_batch* b, uint8_t* out64) {
   MsmPlan mp{};
   // standalone MSMs: the block-local counting sort; from 2^20 points 32-point
   // chunks (~8 partials per bucket instead of ~32 at 2^22)
-  if (int rc = msm_prepare(L, b->N, mp, MSM_SLOT_PASS, b->N >= (1 << 20) ? 32 : MSM_CH, c->msm_sort != 0)) return rc;
+  if (int rc = msm_prepare(L, b->N, mp, MSM_SLOT_PASS, b->N >= (1 << 20) ? 32 : MSM_CH, c->msm_sort != 0, c->msm_maxc))
+    return rc;
   L.tl.begin(L.s);
   launch_msm(mp, b->pts, b->sc, nullptr, 0, L.ws.m_scratch.as<uint32_t>(), L.s, L.s, &L.tl);
   launch_msm_to_bytes(mp.out, b->out, L.s);
@@ -2358,6 +2377,7 @@ int fts_rp_verify_batch(fts_ctx* c, size_t n, const uint8_t* const* rp_der, cons
   // group-test state (FTS_GT_ADAPT) is per caller batch, so an honest call never
   // inherits the dense schedule of the previous caller's tampered one
   b->dense = false;
+  b->locate_skip = 0, b->locate_backoff = 8;
   b->merged = 1;
   b->ntim = 0;
   b->B = (int)n;
@@ -2708,7 +2728,8 @@ static int act_stage(fts_ctx* c, ActSlot* sl, const std::vector<ActionIn>& acts)
   b->status0 = reinterpret_cast<int32_t*>(dv + o_rst);
   b->ipa_flag = reinterpret_cast<int32_t*>(dv + o_ripa);
   b->status = nullptr;  // never verified in place: the pass gathers it
-  b->dense = false;     // action calls have no batch across calls (FTS_GT_ADAPT)
+  b->dense = false;     // action calls have no batch across calls (FTS_GT_ADAPT, locator backoff)
+  b->locate_skip = 0, b->locate_backoff = 8;
   b->merged = 1;
   b->ntim = 0;
   sl->rp_res.assign((size_t)rp_total, FTS_E_NOT_RUN);

@@ -536,7 +536,8 @@ def test_single_fault_locator(pp_raw):
     (S' = (i + 1) S) and that proof's per-proof equations, without the group test;
     the other proofs' deferred IPA structural verdicts (a truncated IPA: "invalid
     IPA proof") still become final.  Two bad proofs: the locator misses, the group
-    test decides, and the next (sparse) failing pass skips the locator.  FTS_LOCATE=0: group
+    test decides, and that batch's next failing pass skips the locator (another
+    batch's does not).  FTS_LOCATE=0: group
     test only.  Every verdict is the oracle's (bulletproof.go:314-324, ipa.go:195-259)."""
     import os
 
@@ -595,18 +596,21 @@ def test_single_fault_locator(pp_raw):
             assert st == exp, {i: (st[i], exp[i]) for i in range(m) if st[i] != exp[i]}
             assert "fb:k_rlc_locate" in names and "fb:k_rlc_group_final" not in names, names
             b.close()
-        # two bad proofs: the locator misses, the group test decides
-        b2, exp2 = batch(pp, {5: "T1", 400: "L"}, 0x51F9)
+        # two bad proofs in one 256-group: the locator misses, the group test decides
+        b2, exp2 = batch(pp, {5: "T1", 100: "L"}, 0x51F9)
         st, names = run(b2)
         assert st == exp2 and "fb:k_rlc_locate" in names and "fb:k_rlc_group_final" in names, names
-        st, names = run(b2)  # now a dense batch (FTS_GT_ADAPT): no locator
+        # the batch that missed skips the locator in its next failing passes
+        # (fts_rp_batch::locate_skip; still sparse: its bad proofs share one 256-group)
+        st, names = run(b2)
         assert st == exp2 and "fb:k_rlc_locate" not in names and "fb:k_rlc_group_final" in names, names
-        b2.close()
-        # after the miss, the next failing passes skip the locator (fts_ctx::locate_skip)
+        # ... while another caller's single fault still gets the locator (the
+        # backoff is per caller batch, not per context)
         b3, exp3 = batch(pp, {222: "L"}, 0x51FB)
         st, names = run(b3)
-        assert st == exp3 and "fb:k_rlc_locate" not in names and "fb:k_rlc_group_final" in names, names
+        assert st == exp3 and "fb:k_rlc_locate" in names and "fb:k_rlc_group_final" not in names, names
         b3.close()
+        b2.close()
     finally:
         pp.close()
     pp = ctx(FTS_LOCATE=0)

@@ -154,3 +154,41 @@ def test_multi_device_context_merges_in_caller_order():
             lo, hi = b[j], b[j + 1]
             out[lo:hi] = [verdict(x) for x in items[lo:hi]]
         assert out == [verdict(x) for x in items]
+
+
+def test_action_staging_host_only(host_pp):
+    """fts_api.cpp act_stage on a host-only context (fts_debug_stage_actions): the
+    chunked layout + direct-to-staging decode of transfers and issues, honest and
+    malformed (truncated, empty, garbage, 1-in/1-out, nil sigma), more actions than
+    one 128-action chunk -- no crash, FTS_API_OK, step timings filled"""
+    import ctypes as C
+    import random
+    import fts_gpu
+    from fts_gpu import _lib as L
+    pp = host_pp(8)
+    rng = random.Random(3)
+    T = b"ABC"
+
+    def bf():
+        return rng.randrange(bn.R).to_bytes(32, "big")
+    tr = []
+    for i in range(6):
+        n_in = 1 if i == 0 else 2
+        n_out = 1 if i == 0 else 2
+        iv = [rng.getrandbits(6) for _ in range(n_in)]
+        ov = [sum(iv)] if n_out == 1 else [iv[0], iv[1]]
+        ib, ob = [bf() for _ in iv], [bf() for _ in ov]
+        ins = [pp.token_commit(T, v, x) for v, x in zip(iv, ib)]
+        outs = [pp.token_commit(T, v, x) for v, x in zip(ov, ob)]
+        tr.append((ins, outs, pp.prove_transfer(T, iv, ib, ov, ob, 77 + i)))
+    ins, outs, p = tr[1]
+    bad = [(ins, outs, p[:len(p) // 2]), (ins, outs, b""), (ins, outs, bytes(rng.getrandbits(8) for _ in range(300))),
+           (ins, outs, p[:40] + b"\x00" * 20 + p[60:])]
+    vals = [rng.getrandbits(8) for _ in range(3)]
+    bfs = [bf() for _ in vals]
+    iss = [([pp.token_commit(T, v, x) for v, x in zip(vals, bfs)], pp.prove_issue(T, vals, bfs, 99))]
+    transfers = [(tr + bad)[i % (len(tr) + len(bad))] for i in range(300)]
+    bt, bi = fts_gpu.TransferBatch(pp, transfers), fts_gpu.IssueBatch(pp, iss * 40)
+    ms = (C.c_float * 4)()
+    L.check("fts_debug_stage_actions", L.lib.fts_debug_stage_actions(pp._ctx, bt.n, bt.items, bi.n, bi.items, 2, ms))
+    assert ms[0] > 0 and abs(ms[0] - (ms[1] + ms[2] + ms[3])) < 0.5 * ms[0] + 0.05
