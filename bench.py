@@ -183,8 +183,9 @@ def main():
     ap.add_argument("--lanes", type=int, default=int(os.environ.get("FTS_LANES", "4")),
                     help="device lanes (stream pairs) of the library (FTS_LANES); batches submitted while "
                          "all lanes are busy are coalesced into one device pass (FTS_COALESCE_MAX proofs)")
-    ap.add_argument("--distinct", type=int, default=4,
-                    help="batches with distinct proofs; the other in-flight batches re-stage them (setup time)")
+    ap.add_argument("--distinct", type=int, default=64,
+                    help="batches with distinct proofs (default: every in-flight batch, so every pass -- and the "
+                         "isolated roofline pass -- holds distinct proofs); the other in-flight batches re-stage them")
     ap.add_argument("--pass-batches", type=int, default=0,
                     help="batches in the isolated roofline pass (0: FTS_COALESCE_MAX / batch, the pass size the "
                          "library runs under load; the PMC traffic file is keyed by this pass size)")
@@ -510,8 +511,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32 (BN254 Fp/Fr 8x32-bit Montgomery)",
-            "data": "synthetic: %d seeded %d-bit range proofs per GPU from the library's device prover "
-                    "(byte-identical to its host prover)" % (B, n),
+            "data": "synthetic: %d seeded %d-bit range proofs per batch from the library's device prover "
+                    "(byte-identical to its host prover), %d distinct batches (%d distinct proofs)"
+                    % (B, n, min(inflight, max(1, args.distinct)), B * min(inflight, max(1, args.distinct))),
             "config": {"workload": "C2: batch of %d standalone %d-bit Bulletproof range proofs per GPU "
                                    "(exact transcripts per proof + RLC batch check via one Pippenger MSM)%s"
                                    % (B, n, _tamper_note(args, B)),
@@ -542,7 +544,8 @@ def main():
             # fixed-base tables resident in HBM: 16-bit windows for the 2n + 6 public
             # generators, 20- or 22-bit (the default where the memory allows) for H_i, K, P
             "table_bytes": pp.table_bytes,
-            "wide_table_bits": 22 if pp.table_bytes > (2 * n + 6) * (32 << 20) + (n + 2) * 13 * (1 << 19) * 64 else 20,
+            "wide_table_bits": pp.wide_bits,
+            "distinct_batches": min(inflight, max(1, args.distinct)),
         }
         print(json.dumps(out), flush=True)
     if dist is not None:

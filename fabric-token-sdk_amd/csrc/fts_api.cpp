@@ -411,10 +411,14 @@ struct ActionState {
 // An action call staged for the dispatcher (act_stage), pooled per context like
 // RpSlot: the call's records parsed straight into pinned host memory in their
 // device layout, one upload into `dev`, and the call's sigma workspace behind
-// them in `dev`.  A device pass then verifies the range proofs of several calls
-// as one batch (gathered like staged range-proof batches) and runs each call's
-// sigma batch in place, so concurrent transfer / issue / request calls share
-// passes instead of taking a lane each.
+// them in `dev`.  Its sigma proofs (TypeAndSum / SameType, independent of the
+// range proofs) run at once on the slot's own stream, while the call waits for a
+// pass; they also write the V slots of its range proofs.  A device pass then
+// verifies the range proofs of several calls as one batch (gathered like staged
+// range-proof batches) after the calls' sigma events, so concurrent transfer /
+// issue / request calls share passes instead of taking a lane each, and the sigma
+// work overlaps other passes instead of sitting on a pass's critical path
+// (DESIGN.md §3.4).
 struct ActSlot {
   fts_rp_batch* b = nullptr;  // the call's range proofs: raw / sc / status0 / ipa point into `dev`
   uint8_t* pin = nullptr;
@@ -423,7 +427,10 @@ struct ActSlot {
   size_t dev_cap = 0;
   hipStream_t s = nullptr;
   hipEvent_t done = nullptr;   // blocking-sync: the staging caller sleeps
-  SigBatchDev sd{};            // the call's sigma batch (sd.A == 0: none); sd.rp_raw set by the pass
+  // on s: [0] before the sigma kernels, [1] after decode + primes + V slots, [2] after
+  // the sigma equations (the pass waits for it before gathering the range proofs)
+  hipEvent_t ev_sig[3] = {nullptr, nullptr, nullptr};
+  SigBatchDev sd{};            // the call's sigma batch (sd.A == 0: none); rp_raw = the slot's range proofs
   int32_t* sig_res = nullptr;  // pinned: sigma verdicts [sd.A], downloaded by the pass
   std::vector<int32_t> rp_res;  // range-proof verdicts [b->B], scattered by the pass
   std::vector<ActionState> st;
@@ -1072,6 +1079,8 @@ void fts_ctx_destroy(fts_ctx* c) {
     if (sl->dev) hipFree(sl->dev);
     if (sl->pin) (void)hipHostFree(sl->pin);
     if (sl->done) hipEventDestroy(sl->done);
+    for (hipEvent_t e : sl->ev_sig)
+      if (e) hipEventDestroy(e);
     if (sl->s) hipStreamDestroy(sl->s);
     delete sl->b;
     delete sl;
@@ -1189,11 +1198,17 @@ static void parse_rp_batch(int k, size_t B, const uint8_t* const* der_p, const s
   parse_rp_into(k, B, der_p, der_len, com64, h.raw.data(), h.sc.data(), h.status.data(), h.ipa.data());
 }
 
-static void collect_timings(fts_ctx* c, Lane& L, fts_rp_batch* b) {
+// sig_ms (optional): the k_sig_prep / k_sig_finish spans of an action call's slot
+static void collect_timings(fts_ctx* c, Lane& L, fts_rp_batch* b, const float* sig_ms = nullptr) {
   std::lock_guard<std::mutex> g(c->tim_mu);
   c->ntim = 0;
   c->last_lane = L.id;
-  for (int i = 0; i < L.tl.n; i++) {
+  for (int q = 0; sig_ms && q < 2; q++) {
+    c->tim_name[c->ntim] = q ? "k_sig_finish" : "k_sig_prep";
+    c->tim_ms[c->ntim] = sig_ms[q];
+    c->tim_work[c->ntim++] = 0;
+  }
+  for (int i = 0; i < L.tl.n && c->ntim < Timeline::CAP; i++) {
     if (!L.tl.name[i]) continue;  // fork/join markers
     const int j = c->ntim++;
     c->tim_name[j] = L.tl.name[i];
@@ -1676,8 +1691,12 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
       size_t B = 0;
       for (RpReq* q : rpq[j]) B += (size_t)q->b->B;
       Workspace& w = L.ws;
-      L.tl.begin(L.s);  // the gather and the sigma kernels on the pass's timeline
+      L.tl.begin(L.s);  // the gather on the pass's timeline
       P[j].tl_started = true;
+      // the action calls' sigma kernels (their slots' streams, since staging) wrote the
+      // V slots of their range proofs: the gather waits for them
+      for (RpReq* q : grp)
+        if (q->act) HIP_OK(hipStreamWaitEvent(L.s, q->act->ev_sig[2], 0));
       RpGather g{};
       if (B > 0) {
         const size_t Bal = std::max(B, std::min(c->coalesce_max, (size_t)1 << 20));  // sized once for the largest pass
@@ -1703,41 +1722,27 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
       }
       Bs[j] = B;
       d_status[j] = w.rp_status.as<int32_t>();
-      // the action calls' sigma batches, each in its own slot's workspace: decode + primes
-      // (writing the V slots of its range proofs in the gathered pass) on the main stream
+      // the batch check's variable part drops the range proofs of actions whose sigma
+      // proof failed (k_sig_exclude at the call's pass offset, on the check's stream, which
+      // follows the main stream and so the sigma events)
       SigHook& h = hooks[j];
       h.L = &L;
       for (RpReq* q : grp) {
         if (!q->act || q->act->sd.A == 0) continue;
-        SigBatchDev& sd = q->act->sd;
         int off = -1;
         for (size_t i = 0; i < rpq[j].size(); i++)
           if (rpq[j][i] == q) off = first[j][i];
-        sd.rp_raw = off >= 0 ? w.rp_raw.as<uint8_t>() + (size_t)off * npts * 64 : nullptr;
-        launch_sig_prep(sd, L.s);
-        h.sig.push_back(&sd);
+        h.sig.push_back(&q->act->sd);
         h.off.push_back(off);
       }
-      if (!h.sig.empty()) L.tl.mark("k_sig_prep", L.s, 0);
-      if (B == 0) {  // sigma proofs only (e.g. 1-in/1-out transfers)
+      if (B == 0) {  // sigma proofs only: nothing left for the pass but the verdicts
         sig_only[j] = 1;
-        for (const SigBatchDev* sd : h.sig) launch_sig_finish(*sd, c->d_tables, c->n, L.s);
-        L.tl.mark("k_sig_finish", L.s, 0);
-        HIP_OK(hipGetLastError());
         return FTS_API_OK;
       }
       void (*pre)(void*, hipStream_t) = nullptr;
       if (!h.sig.empty()) {
-        // the sigma equations on the lane's third stream beside the range-proof pass;
-        // the batch check's variable part follows them there and first drops the range
-        // proofs of actions whose sigma proof failed (k_sig_exclude)
-        L.tl.fork(L.s, L.s3);
-        for (const SigBatchDev* sd : h.sig) launch_sig_finish(*sd, c->d_tables, c->n, L.s3);
-        L.tl.mark("k_sig_finish", L.s3, 0);
-        HIP_OK(hipEventRecord(L.ev_b, L.s3));
         pre = [](void* arg, hipStream_t s) {
           SigHook* hk = static_cast<SigHook*>(arg);
-          (void)hipStreamWaitEvent(s, hk->L->ev_b, 0);
           // the mask is read at launch time: rp_enqueue sizes (and may re-allocate) it
           for (size_t i = 0; i < hk->sig.size(); i++)
             if (hk->off[i] >= 0) launch_sig_exclude(*hk->sig[i], hk->L->ws.rp_excl.as<int32_t>() + hk->off[i], s);
@@ -1789,8 +1794,20 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
           L.host_stage_ms = q->act->stage_ms;
           break;
         }
+      // the sigma kernels of the pass's first action call (its slot's stream), beside
+      const ActSlot* sa = nullptr;
+      for (RpReq* q : sub[j])
+        if (q->act && q->act->sd.A) {
+          sa = q->act;
+          break;
+        }
+      float sig_ms[2] = {0, 0};
+      if (sa) {
+        (void)hipEventElapsedTime(&sig_ms[0], sa->ev_sig[0], sa->ev_sig[1]);
+        (void)hipEventElapsedTime(&sig_ms[1], sa->ev_sig[1], sa->ev_sig[2]);
+      }
       for (RpReq* q : sub[j]) {
-        collect_timings(c, L, q->b);
+        collect_timings(c, L, q->b, sa ? sig_ms : nullptr);
         q->b->merged = (int)sub[j].size();
       }
       return FTS_API_OK;
@@ -2421,7 +2438,12 @@ static ActSlot* aslot_acquire(fts_ctx* c) {
   sl->b = new fts_rp_batch();
   sl->b->device = c->device;
   if (hipStreamCreateWithFlags(&sl->s, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&sl->done, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&sl->done, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess ||
+      hipEventCreate(&sl->ev_sig[0]) != hipSuccess || hipEventCreate(&sl->ev_sig[1]) != hipSuccess ||
+      hipEventCreate(&sl->ev_sig[2]) != hipSuccess) {
+    for (hipEvent_t e : sl->ev_sig)
+      if (e) hipEventDestroy(e);
+    if (sl->done) hipEventDestroy(sl->done);
     if (sl->s) hipStreamDestroy(sl->s);
     delete sl->b;
     delete sl;
@@ -2755,9 +2777,18 @@ static int act_stage(fts_ctx* c, ActSlot* sl, const std::vector<ActionIn>& acts)
   sd.scratch = reinterpret_cast<uint32_t*>(dv + w_scratch);
   sd.rp_k = k;
   if ((SA || rp_total) && c->device >= 0) {
-    if (hipMemcpyAsync(dv, hp, in_end, hipMemcpyHostToDevice, sl->s) != hipSuccess ||
-        hipEventRecord(sl->done, sl->s) != hipSuccess || hipEventSynchronize(sl->done) != hipSuccess)
-      return FTS_API_EDEVICE;
+    // upload, then the sigma proofs at once on the slot's stream: decode + primes (and
+    // the V slots of the call's own range proofs, before any pass gathers them), the
+    // equations and transcripts.  No host wait: the pass waits for ev_sig[2], and the
+    // pinned records stay the slot's until the call returns.
+    sd.rp_raw = rp_total ? b->raw : nullptr;
+    HIP_OK(hipMemcpyAsync(dv, hp, in_end, hipMemcpyHostToDevice, sl->s));
+    HIP_OK(hipEventRecord(sl->ev_sig[0], sl->s));
+    if (SA) launch_sig_prep(sd, sl->s);
+    HIP_OK(hipEventRecord(sl->ev_sig[1], sl->s));
+    if (SA) launch_sig_finish(sd, c->d_tables, c->n, sl->s);
+    HIP_OK(hipEventRecord(sl->ev_sig[2], sl->s));
+    HIP_OK(hipGetLastError());
   }
   sl->stage_ms = (float)(now_ms() - t1);
   return FTS_API_OK;
@@ -2770,9 +2801,13 @@ static int act_verify(fts_ctx* c, const std::vector<ActionIn>& acts, int32_t* st
   ActSlot* sl = aslot_acquire(c);
   if (!sl) return FTS_API_ENOMEM;
   int rc = act_stage(c, sl, acts);
-  if (rc == FTS_API_OK && (sl->sd.A || sl->b->B)) {
+  if (rc == FTS_API_OK && sl->b->B) {
     RpReq me(sl->b, sl->rp_res.data(), sl);
     rc = rp_dispatch(c, me);
+  } else if (rc == FTS_API_OK && sl->sd.A) {  // sigma proofs only (1-in/1-out transfers): no pass
+    if (hipMemcpyAsync(sl->sig_res, sl->sd.status, (size_t)sl->sd.A * 4, hipMemcpyDeviceToHost, sl->s) != hipSuccess ||
+        hipEventRecord(sl->done, sl->s) != hipSuccess || hipEventSynchronize(sl->done) != hipSuccess)
+      rc = FTS_API_EDEVICE;
   }
   if (rc == FTS_API_OK) {
     const std::vector<ActionState>& st = sl->st;

@@ -332,8 +332,9 @@ def test_group_test_adaptive_dense_exact_verdicts(pp_raw):
     verified twice on one lane: both calls must give the oracle's verdicts; the
     first runs the 256-group kernels, the second only the small-group ones and
     sends at most the 16 failing 8-groups to the per-proof stage.  The state is
-    per caller batch: another staged batch with one bad proof,
-    verified after it on the same context, still starts at groups of 256."""
+    per caller batch: another staged batch with two bad proofs (a miss
+    of the single-fault locator), verified after it on the same context, still starts
+    at groups of 256."""
     import os
 
     import fts_gpu
@@ -387,12 +388,13 @@ def test_group_test_adaptive_dense_exact_verdicts(pp_raw):
     vals2 = [rng.getrandbits(16) for _ in range(m)]
     bfs2 = [rng.randrange(bn.R).to_bytes(32, "big") for _ in range(m)]
     proofs2, coms2 = pp.prove_range_batch_gpu(vals2, bfs2, seed=9400)
-    r = zkat.RangeProof.deserialize(proofs2[300])
-    r.data.T1 = bn.g1_add(r.data.T1, bn.GEN)
-    proofs2[300] = r.serialize()
+    for i in (300, 310):  # two bad proofs in one 256-group: the single-fault locator misses
+        r = zkat.RangeProof.deserialize(proofs2[i])
+        r.data.T1 = bn.g1_add(r.data.T1, bn.GEN)
+        proofs2[i] = r.serialize()
     other = pp.stage_range_proofs(proofs2, coms2)
     out2 = [int(s) for s in other.verify()]
-    assert out2 == [fts_gpu.FTS_E_RP_INVALID if i == 300 else 0 for i in range(m)]
+    assert out2 == [fts_gpu.FTS_E_RP_INVALID if i in (300, 310) else 0 for i in range(m)]
     n3, _ = _raw_timing_names(other)
     assert "fb:k_rlc_group_columns" in n3 and "fb:k_rlc_group_cols" not in n3, n3
     # and the dense batch keeps its own state
