@@ -118,6 +118,37 @@ FTS_DEV G1J fb_mul(const uint32_t* __restrict__ table, const Scalar& k) {
   return acc;
 }
 
+// ka * A + kb * B over two 16-bit-window tables in ONE accumulator: a
+// fixed-base product is a sum of table entries (no doublings), so the joint sum
+// takes the two products' additions with no final full addition; the next
+// window's entries are loaded during the current window's additions
+FTS_DEV G1J fb_mul2(const uint32_t* __restrict__ ta, const Scalar& ka, const uint32_t* __restrict__ tb,
+                    const Scalar& kb) {
+  uint32_t sa[8], sb[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) sa[i] = ka.v[i], sb[i] = kb.v[i];
+  G1J acc = g1j_identity();
+  int ca = 0, cb = 0;
+  int da = fb_next_digit(sa, ca), db = fb_next_digit(sb, cb);
+  G1A qa, qb;
+  if (da != 0) qa = fb_entry(ta, 0, da);
+  if (db != 0) qb = fb_entry(tb, 0, db);
+  for (int w = 0; w < FB_NW; w++) {
+    int dan = 0, dbn = 0;
+    G1A na, nb;
+    if (w + 1 < FB_NW) {
+      dan = fb_next_digit(sa, ca);
+      dbn = fb_next_digit(sb, cb);
+      if (dan != 0) na = fb_entry(ta, w + 1, dan);
+      if (dbn != 0) nb = fb_entry(tb, w + 1, dbn);
+    }
+    if (da != 0) madd_inl(acc, qa);
+    if (db != 0) madd_inl(acc, qb);
+    da = dan, db = dbn, qa = na, qb = nb;
+  }
+  return acc;
+}
+
 // k * B over a width-W table (FbCfg<W> layout)
 template <int W>
 FTS_DEV int fb_next_digit_w(uint32_t s[8], int& carry) {

@@ -27,12 +27,12 @@ struct SigAction {
 constexpr int TAS_SC_TYPE = 0, TAS_SC_TBF = 1, TAS_SC_EQ = 2, TAS_SC_CHAL = 3, TAS_SC_IV = 4;
 constexpr int ST_SC_TYPE = 0, ST_SC_BF = 1, ST_SC_CHAL = 2;
 
-// k_sig_terms scratch per work item: a 16-entry GLV/Straus table + one point
+// k_sig_var scratch per work item: a 16-entry GLV/Straus table + one point
 constexpr int SIG_VTAB_WORDS = 16 * 24;
 inline __host__ __device__ size_t sig_scratch_words(size_t nwork) { return nwork * (SIG_VTAB_WORDS + 24); }
 
 inline __host__ __device__ int sig_nterms(int kind, int n_in) { return kind == SIG_TAS ? 2 * n_in + 4 : 2; }
-// term t is a variable-base (GLV) product (k_sig_terms); the others are fixed-base
+// term t is a variable-base (GLV) product (k_sig_var); the others are fixed-base (k_sig_fixed)
 inline __host__ __device__ bool sig_term_var(int kind, int n_in, int t) {
   return kind == SIG_TAS ? (t < 2 * n_in ? (t & 1) != 0 : (t == 2 * n_in + 1 || t == 2 * n_in + 3)) : t != 0;
 }
@@ -56,6 +56,7 @@ struct SigBatchDev {
   int npts;           // total points
   int naff;           // total per-action affine / Jacobian slots (aff_off of the end)
   int nwork;          // total (action, term) work items
+  int nfix;           // the first nfix work items are the fixed-base terms (k_sig_fixed), the rest variable-base (k_sig_var)
   const SigAction* act;
   uint8_t* raw;       // [npts][64] raw BE
   int32_t* pt_owner;  // [npts] action index

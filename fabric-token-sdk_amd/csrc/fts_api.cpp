@@ -540,6 +540,11 @@ struct fts_ctx {
   // multi-fault batches (C5, tampered C2) pays it rarely.  Kept per caller batch
   // (fts_rp_batch::locate_skip), so one caller's multi-fault passes never make
   // another caller's single-fault passes skip the locator
+  // action calls (transfer / issue / mixed / request) have no batch object across
+  // calls: they share one locator backoff, carried into each call's slot batch and
+  // back (a stream of multi-fault calls -- C5 with 1 % tampered actions -- would
+  // otherwise pay a missed locator, one extra MSM, on every call)
+  std::atomic<int> act_locate_skip{0}, act_locate_backoff{8};
   // FTS_GT_ADAPT: a staged caller batch's round-1 group size follows the bad-proof
   // density of ITS last failed verification (fts_rp_batch::dense; per caller batch,
   // so one caller's tampered batches never change the fallback of another's).
@@ -2616,7 +2621,7 @@ static int act_stage(fts_ctx* c, ActSlot* sl, const std::vector<ActionIn>& acts)
     const int npt = 1 + sa.n_in + sa.n_out;
     for (int q = 0; q < npt; q++) howner[sa.pt_off + q] = g;
     // work list: every fixed-base term first, then every variable-base (GLV) term,
-    // so no wave of k_sig_terms runs both kinds of product
+    // so each kind has its own kernel (k_sig_fixed, k_sig_var)
     for (int t = 0, nt = sig_nterms(sa.kind, sa.n_in), fi = run.nfix, vi = nfix_total + run.term - run.nfix; t < nt; t++)
       hwork[sig_term_var(sa.kind, sa.n_in, t) ? vi++ : fi++] = make_int2(g, t);
     run.add(ai.kind, n_in, (int)ai.n_out, s.rc_applicable ? s.rp_count : 0);
@@ -2750,8 +2755,9 @@ static int act_stage(fts_ctx* c, ActSlot* sl, const std::vector<ActionIn>& acts)
   b->status0 = reinterpret_cast<int32_t*>(dv + o_rst);
   b->ipa_flag = reinterpret_cast<int32_t*>(dv + o_ripa);
   b->status = nullptr;  // never verified in place: the pass gathers it
-  b->dense = false;     // action calls have no batch across calls (FTS_GT_ADAPT, locator backoff)
-  b->locate_skip = 0, b->locate_backoff = 8;
+  b->dense = false;     // action calls have no batch across calls (FTS_GT_ADAPT: groups of 256)
+  b->locate_skip = c->act_locate_skip.load(std::memory_order_relaxed);  // the calls' shared backoff
+  b->locate_backoff = c->act_locate_backoff.load(std::memory_order_relaxed);
   b->merged = 1;
   b->ntim = 0;
   sl->rp_res.assign((size_t)rp_total, FTS_E_NOT_RUN);
@@ -2762,6 +2768,7 @@ static int act_stage(fts_ctx* c, ActSlot* sl, const std::vector<ActionIn>& acts)
   sd.npts = pt_off;
   sd.naff = aff_off;
   sd.nwork = (int)nwork;
+  sd.nfix = nfix_total;
   sd.act = reinterpret_cast<const SigAction*>(dv + o_act);
   sd.raw = dv + o_raw;
   sd.pt_owner = reinterpret_cast<int32_t*>(dv + o_owner);
@@ -2804,6 +2811,8 @@ static int act_verify(fts_ctx* c, const std::vector<ActionIn>& acts, int32_t* st
   if (rc == FTS_API_OK && sl->b->B) {
     RpReq me(sl->b, sl->rp_res.data(), sl);
     rc = rp_dispatch(c, me);
+    c->act_locate_skip.store(sl->b->locate_skip, std::memory_order_relaxed);
+    c->act_locate_backoff.store(sl->b->locate_backoff, std::memory_order_relaxed);
   } else if (rc == FTS_API_OK && sl->sd.A) {  // sigma proofs only (1-in/1-out transfers): no pass
     if (hipMemcpyAsync(sl->sig_res, sl->sd.status, (size_t)sl->sd.A * 4, hipMemcpyDeviceToHost, sl->s) != hipSuccess ||
         hipEventRecord(sl->done, sl->s) != hipSuccess || hipEventSynchronize(sl->done) != hipSuccess)

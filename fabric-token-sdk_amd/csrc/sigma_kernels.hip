@@ -4,7 +4,8 @@
 //   k_sig_prep     (action)        in'_i = In_i - CT, out'_j = Out_j - CT, sum = sum in' - sum out'
 //                                  (transfer/typeandsum.go:241-258); V_j = out'_j feeds the
 //                                  range-proof batch (transfer.go:171-185, issue/verifier.go:44-49)
-//   k_sig_terms    (action, term)  fixed-base (ped0/1/2 tables) and variable-base products
+//   k_sig_fixed    (action, term)  fixed-base products (ped0/1/2 tables; joint pairs in one accumulator)
+//   k_sig_var      (action, term)  variable-base products c * P (GLV, one chain per lane)
 //   k_sig_finish   (action)        inCom_i, sumCom, typeCom (typeandsum.go:249-265) or
 //                                  com (sametype.go:169-171), exact affine, hex transcript,
 //                                  SHA-256, Zr.Equals against the proof's challenge
@@ -86,73 +87,76 @@ __global__ void __launch_bounds__(256) k_sig_exclude(int A, const SigAction* __r
   for (int j = 0; j < ac.rp_count; j++) rp_excl[ac.rp_base + j] = 1;
 }
 
-__global__ void __launch_bounds__(64) k_sig_terms(int nwork, const int2* __restrict__ work,
-                                                  const SigAction* __restrict__ act, const uint32_t* __restrict__ pts,
-                                                  const uint32_t* __restrict__ sc, const int32_t* __restrict__ status,
-                                                  const uint32_t* __restrict__ aff, const int32_t* __restrict__ aff_off,
+// The sigma proofs' products, one lane per (action, term) work item.  The work
+// list holds every fixed-base term first (items [0, nfix)), then every
+// variable-base term, and each kind has its own kernel: the fixed-base one is
+// table lookups + mixed additions only (fb_mul / fb_mul2 inlined), the variable-
+// base one one inlined GLV chain.  One kernel with both paths kept an out-of-line
+// fixed-base product (the call ABI spilled the accumulator: 416 B of scratch per
+// lane) and ran at 45 % VALU busy, 0.33 of the MAD peak (round 6 PMC).
+FTS_DEV Scalar sig_canon(const uint32_t* p) {
+  Scalar s;
+#pragma unroll
+  for (int i = 0; i < 8; i++) s.v[i] = p[i];
+  return s;
+}
+
+__global__ void __launch_bounds__(64) k_sig_fixed(int nfix, const int2* __restrict__ work,
+                                                  const SigAction* __restrict__ act, const uint32_t* __restrict__ sc,
+                                                  const int32_t* __restrict__ status,
                                                   const uint32_t* __restrict__ tables, int n,
-                                                  uint32_t* __restrict__ terms, uint32_t* __restrict__ scratch) {
-  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+                                                  uint32_t* __restrict__ terms) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= nfix) return;
+  const int a = work[gid].x, t = work[gid].y;
+  if (status[a] != 0) return;
+  const SigAction ac = act[a];
+  const uint32_t* S = sc + (size_t)ac.sc_off * 8;
+  const uint32_t* t_ped0 = tables + (size_t)tb_ped0(n) * FB_WORDS_PER_BASE;
+  const uint32_t* t_ped1 = tables + (size_t)tb_G(n) * FB_WORDS_PER_BASE;
+  const uint32_t* t_ped2 = tables + (size_t)tb_H(n) * FB_WORDS_PER_BASE;
+  G1J r;
+  if (ac.kind == SIG_TAS) {
+    const int N = ac.n_in;
+    if (t < 2 * N)  // iv_i ped1 + ibf_i ped2   (t even)
+      r = fb_mul2(t_ped1, sig_canon(S + (TAS_SC_IV + (t >> 1)) * 8), t_ped2, sig_canon(S + (TAS_SC_IV + N + (t >> 1)) * 8));
+    else if (t == 2 * N)  // EqualityOfSum ped2
+      r = fb_mul(t_ped2, sig_canon(S + TAS_SC_EQ * 8));
+    else  // Type ped0 + TBF ped2   (t == 2N + 2)
+      r = fb_mul2(t_ped0, sig_canon(S + TAS_SC_TYPE * 8), t_ped2, sig_canon(S + TAS_SC_TBF * 8));
+  } else {  // Type ped0 + BF ped2   (t == 0)
+    r = fb_mul2(t_ped0, sig_canon(S + ST_SC_TYPE * 8), t_ped2, sig_canon(S + ST_SC_BF * 8));
+  }
+  store_g1j(terms + (size_t)(ac.term_off + t) * 24, r);
+}
+
+__global__ void __launch_bounds__(64) k_sig_var(int nfix, int nwork, const int2* __restrict__ work,
+                                                const SigAction* __restrict__ act, const uint32_t* __restrict__ pts,
+                                                const uint32_t* __restrict__ sc, const int32_t* __restrict__ status,
+                                                const uint32_t* __restrict__ aff, const int32_t* __restrict__ aff_off,
+                                                uint32_t* __restrict__ terms, uint32_t* __restrict__ scratch) {
+  const int gid = nfix + blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= nwork) return;
   const int a = work[gid].x, t = work[gid].y;
   if (status[a] != 0) return;
   const SigAction ac = act[a];
   const uint32_t* S = sc + (size_t)ac.sc_off * 8;
   const uint32_t* F = aff + (size_t)aff_off[a] * 16;
-  // lane tables of glv_mul: [16 entries][24 words][nwork lanes] (coalesced)
-  uint32_t* tmp = scratch + (size_t)nwork * SIG_VTAB_WORDS + (size_t)gid * 24;
-  const uint32_t* t_ped0 = tables + (size_t)tb_ped0(n) * FB_WORDS_PER_BASE;
-  const uint32_t* t_ped1 = tables + (size_t)tb_G(n) * FB_WORDS_PER_BASE;
-  const uint32_t* t_ped2 = tables + (size_t)tb_H(n) * FB_WORDS_PER_BASE;
-  auto canon = [](const uint32_t* p) {
-    Scalar s;
-#pragma unroll
-    for (int i = 0; i < 8; i++) s.v[i] = p[i];
-    return s;
-  };
-  G1J r;
-  bool var = false;  // variable-base term: r = vk * vp (one inlined GLV chain below)
+  // c in'_i (t = 2i + 1), c sum (t = 2N + 1), c CT (t = 2N + 3); ST: c CT (t = 1)
   G1A vp;
   Scalar vk;
   if (ac.kind == SIG_TAS) {
     const int N = ac.n_in;
-    const Scalar chal = canon(S + TAS_SC_CHAL * 8);
-    if (t < 2 * N) {
-      int i = t >> 1;
-      if ((t & 1) == 0) {  // iv_i ped1 + ibf_i ped2
-        r = nl_fb_mul(t_ped1, canon(S + (TAS_SC_IV + i) * 8));
-        r = add_via(tmp, r, nl_fb_mul(t_ped2, canon(S + (TAS_SC_IV + N + i) * 8)));
-      } else {  // c in'_i
-        var = true;
-        vp = load_g1a(F + i * 16);
-        vk = chal;
-      }
-    } else if (t == 2 * N) {  // EqualityOfSum ped2
-      r = nl_fb_mul(t_ped2, canon(S + TAS_SC_EQ * 8));
-    } else if (t == 2 * N + 1) {  // c sum
-      var = true;
-      vp = load_g1a(F + (N + ac.n_out) * 16);
-      vk = chal;
-    } else if (t == 2 * N + 2) {  // Type ped0 + TBF ped2
-      r = nl_fb_mul(t_ped0, canon(S + TAS_SC_TYPE * 8));
-      r = add_via(tmp, r, nl_fb_mul(t_ped2, canon(S + TAS_SC_TBF * 8)));
-    } else {  // c CT
-      var = true;
-      vp = load_g1a(pts + (size_t)ac.pt_off * 16);
-      vk = chal;
-    }
+    vk = sig_canon(S + TAS_SC_CHAL * 8);
+    if (t < 2 * N) vp = load_g1a(F + (t >> 1) * 16);
+    else if (t == 2 * N + 1) vp = load_g1a(F + (N + ac.n_out) * 16);
+    else vp = load_g1a(pts + (size_t)ac.pt_off * 16);
   } else {
-    if (t == 0) {  // Type ped0 + BF ped2
-      r = nl_fb_mul(t_ped0, canon(S + ST_SC_TYPE * 8));
-      r = add_via(tmp, r, nl_fb_mul(t_ped2, canon(S + ST_SC_BF * 8)));
-    } else {  // c CT
-      var = true;
-      vp = load_g1a(pts + (size_t)ac.pt_off * 16);
-      vk = canon(S + ST_SC_CHAL * 8);
-    }
+    vk = sig_canon(S + ST_SC_CHAL * 8);
+    vp = load_g1a(pts + (size_t)ac.pt_off * 16);
   }
-  if (var) r = glv_mul(vp, vk, scratch, nwork, gid);
-  store_g1j(terms + (size_t)(ac.term_off + t) * 24, r);
+  // lane tables of glv_mul: [16 entries][24 words][nwork lanes] (coalesced)
+  store_g1j(terms + (size_t)(ac.term_off + t) * 24, glv_mul(vp, vk, scratch, nwork, gid));
 }
 
 FTS_DEV void put_hex_aff(uint8_t* msg, int idx, const uint32_t* aff_pt, bool sep) {
@@ -243,8 +247,9 @@ void launch_sig_prep(const SigBatchDev& d, hipStream_t s) {
 }
 // phase 2: sigma equations (independent of the range proofs)
 void launch_sig_finish(const SigBatchDev& d, const uint32_t* tables, int n, hipStream_t s) {
-  FTS_LAUNCH(k_sig_terms, d.nwork, 64, s, d.nwork, d.work, d.act, d.pts, d.sc, d.status, d.aff, d.aff_off, tables, n,
-             d.terms, d.scratch);
+  FTS_LAUNCH(k_sig_fixed, d.nfix, 64, s, d.nfix, d.work, d.act, d.sc, d.status, tables, n, d.terms);
+  FTS_LAUNCH(k_sig_var, d.nwork - d.nfix, 64, s, d.nfix, d.nwork, d.work, d.act, d.pts, d.sc, d.status, d.aff,
+             d.aff_off, d.terms, d.scratch);
   FTS_LAUNCH(k_sig_coms, d.A, 64, s, d.A, d.act, d.status, d.terms, d.aff_off, d.jac);
   launch_normalize_all(d.naff, d.jac, d.aff, s);
   FTS_LAUNCH(k_sig_finish, d.A, 64, s, d.A, d.act, d.pts, d.sc, d.status, d.aff, d.aff_off, d.msgs);

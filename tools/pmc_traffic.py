@@ -30,7 +30,7 @@ import os
 import sys
 from collections import defaultdict
 
-GATHER = {"k_rp_fixed_exact", "k_rp_fixed_all", "k_rp_terms_fixed", "k_pv_fbsum", "k_sig_terms", "k_token_open"}
+GATHER = {"k_rp_fixed_exact", "k_rp_fixed_all", "k_rp_terms_fixed", "k_pv_fbsum", "k_sig_fixed", "k_token_open"}
 
 
 def kernel_key(name):
