@@ -222,9 +222,13 @@ def main():
     ap.add_argument("--msm-tiled", action="store_true",
                     help="msm workload: 2^16 distinct points tiled (rounds 2-3) instead of 2^msm-log distinct ones")
     ap.add_argument("--transfers", type=int, default=8192, help="transfer/mixed workloads: transfers per GPU per step")
-    ap.add_argument("--action-inflight", type=int, default=3,
-                    help="transfer/mixed workloads: concurrent verify calls (host threads)")
+    ap.add_argument("--action-inflight", type=int, default=None,
+                    help="concurrent verify calls (host threads) of the non-C2 workloads; default 8 for the "
+                         "action workloads (transfer / mixed / request: the library coalesces concurrent calls "
+                         "into shared passes, as a validator's goroutines would submit them), 3 otherwise")
     args = ap.parse_args()
+    if args.action_inflight is None:
+        args.action_inflight = 8 if args.workload in ("transfer", "mixed", "request") else 3
     if args.workload == "msm":
         return bench_msm(args)
     if args.workload == "transfer":

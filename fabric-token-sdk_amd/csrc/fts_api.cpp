@@ -1662,6 +1662,7 @@ struct SigHook {
   Lane* L = nullptr;
   std::vector<const SigBatchDev*> sig;
   std::vector<int> off;  // first range proof of the call in the pass (-1: none)
+  std::vector<hipEvent_t> ev;  // the call's sigma-done event (its slot's ev_sig[2])
 };
 
 static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std::vector<std::vector<RpReq*>>& sub,
@@ -1698,10 +1699,11 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
       Workspace& w = L.ws;
       L.tl.begin(L.s);  // the gather on the pass's timeline
       P[j].tl_started = true;
-      // the action calls' sigma kernels (their slots' streams, since staging) wrote the
-      // V slots of their range proofs: the gather waits for them
+      // the action calls' sigma decode (their slots' streams, since staging) wrote the
+      // V slots of their range proofs: the gather waits for that part only; the sigma
+      // equations are waited for by the exclusion hook, on the batch check's stream
       for (RpReq* q : grp)
-        if (q->act) HIP_OK(hipStreamWaitEvent(L.s, q->act->ev_sig[2], 0));
+        if (q->act) HIP_OK(hipStreamWaitEvent(L.s, q->act->ev_sig[1], 0));
       RpGather g{};
       if (B > 0) {
         const size_t Bal = std::max(B, std::min(c->coalesce_max, (size_t)1 << 20));  // sized once for the largest pass
@@ -1739,9 +1741,11 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
           if (rpq[j][i] == q) off = first[j][i];
         h.sig.push_back(&q->act->sd);
         h.off.push_back(off);
+        h.ev.push_back(q->act->ev_sig[2]);
       }
       if (B == 0) {  // sigma proofs only: nothing left for the pass but the verdicts
         sig_only[j] = 1;
+        for (hipEvent_t e : h.ev) HIP_OK(hipStreamWaitEvent(L.s, e, 0));
         return FTS_API_OK;
       }
       void (*pre)(void*, hipStream_t) = nullptr;
@@ -1749,8 +1753,10 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
         pre = [](void* arg, hipStream_t s) {
           SigHook* hk = static_cast<SigHook*>(arg);
           // the mask is read at launch time: rp_enqueue sizes (and may re-allocate) it
-          for (size_t i = 0; i < hk->sig.size(); i++)
+          for (size_t i = 0; i < hk->sig.size(); i++) {
+            (void)hipStreamWaitEvent(s, hk->ev[i], 0);  // the call's sigma verdicts
             if (hk->off[i] >= 0) launch_sig_exclude(*hk->sig[i], hk->L->ws.rp_excl.as<int32_t>() + hk->off[i], s);
+          }
         };
       }
       std::vector<int> groups = first[j];
