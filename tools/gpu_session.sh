@@ -17,7 +17,7 @@
 # Output: gpurun_out/$TAG (TAG default r05).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$OLDPWD}"
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 step() {  # name limit cmd...
