@@ -433,11 +433,23 @@ struct CTab {
   FTS_DEV uint32_t* z(int e) const { return base + (size_t)16 * L * 24 + ((size_t)e * L + p) * 8; }
   FTS_DEV uint32_t* pre(int e) const { return base + (size_t)16 * L * 32 + ((size_t)e * L + p) * 8; }
 };
+// One point's 8-entry table in one lane (the sigma proofs' variable-base products,
+// k_sig_var): the CTab row layout for entries 0..7 only.
+// Region layout: XY [8][L][16] | BX [8][L][8] | Z [8][L][8] | PRE [8][L][8] (1,280 B per lane)
+constexpr int CTAB8_WORDS = 8 * 40;  // words per lane
+struct CTab8 {
+  uint32_t* base;
+  size_t L, p;  // lanes in the launch, this lane
+  FTS_DEV uint32_t* xy(int e) const { return base + ((size_t)e * L + p) * 16; }
+  FTS_DEV uint32_t* bx(int e) const { return base + (size_t)8 * L * 16 + ((size_t)e * L + p) * 8; }
+  FTS_DEV uint32_t* z(int e) const { return base + (size_t)8 * L * 24 + ((size_t)e * L + p) * 8; }
+  FTS_DEV uint32_t* pre(int e) const { return base + (size_t)8 * L * 32 + ((size_t)e * L + p) * 8; }
+};
 // entries e0 .. e0+7 <- 1..8 * P (Jacobian, then normalised with one inversion):
 // AFF: P.z == 1 (mixed additions).  An identity P gives (0, 0) entries (skipped by
-// the chain, which knows the identity flags).
-template <bool AFF>
-FTS_DEV void ctab_build8(const CTab& T, int e0, const G1J& P, bool ident) {
+// the chain, which knows the identity flags).  TabT: CTab or CTab8.
+template <bool AFF, class TabT>
+FTS_DEV void ctab_build8(const TabT& T, int e0, const G1J& P, bool ident) {
   G1J cur = P;
   G1A pa;
   if (AFF) pa.x = P.x, pa.y = P.y;
@@ -507,6 +519,46 @@ FTS_DEV G1J straus2_ctab(const CTab& T, int h, const uint32_t a[4], bool sa, con
     }
     if (db != 0) {
       if ((db < 0) != sb) qb.y = f_neg(qb.y);
+      madd_inl(acc, qb);
+    }
+  }
+  return acc;
+}
+
+// k * P for a canonical scalar k < r and an affine P in one lane, over the lane's
+// own affine table: GLV split k = k1 + k2 lambda, entries 1..8 P carry beta*x so
+// phi(eP) = (beta x, y); the GLV signs fold into y at lookup.  124 doublings and
+// <= 64 MIXED additions (glv_mul below: full additions over Jacobian tables), for
+// one inversion and 8 beta products in the table.  One call site per kernel (as
+// glv_mul).
+FTS_DEV G1J glv_mul_ctab8(const CTab8& T, const G1A& p, const Scalar& k) {
+  if (g1a_is_identity(p)) return g1j_identity();
+  uint32_t k1[4], k2[4], s1, s2;
+  glv_decompose(k.v, k1, s1, k2, s2);
+  ctab_build8<true>(T, 0, g1j_from_affine(p), false);
+  const uint32_t c1 = recode_carries(k1), c2 = recode_carries(k2);
+  G1J acc = g1j_identity();
+  for (int w = 31; w >= 0; w--) {
+    const int da = window_digit(k1, c1, w), db = window_digit(k2, c2, w);
+    G1A qa, qb;
+    if (da != 0) {
+      const int e = (da < 0 ? -da : da) - 1;
+      load_fp(T.xy(e), qa.x);
+      load_fp(T.xy(e) + 8, qa.y);
+    }
+    if (db != 0) {
+      const int e = (db < 0 ? -db : db) - 1;
+      load_fp(T.bx(e), qb.x);
+      load_fp(T.xy(e) + 8, qb.y);
+    }
+    if (w != 31)
+      for (int r = 0; r < 4; r++) acc = g1j_dbl(acc);
+    if (da != 0) {
+      if ((da < 0) != (s1 != 0)) qa.y = f_neg(qa.y);
+      madd_inl(acc, qa);
+    }
+    if (db != 0) {
+      if ((db < 0) != (s2 != 0)) qb.y = f_neg(qb.y);
       madd_inl(acc, qb);
     }
   }

@@ -27,7 +27,8 @@ struct SigAction {
 constexpr int TAS_SC_TYPE = 0, TAS_SC_TBF = 1, TAS_SC_EQ = 2, TAS_SC_CHAL = 3, TAS_SC_IV = 4;
 constexpr int ST_SC_TYPE = 0, ST_SC_BF = 1, ST_SC_CHAL = 2;
 
-// k_sig_var scratch per work item: a 16-entry GLV/Straus table + one point
+// k_sig_var scratch per work item: its 8-entry affine table (glv.hpp CTab8,
+// 320 words) within a 16-entry Jacobian table's room + one point
 constexpr int SIG_VTAB_WORDS = 16 * 24;
 inline __host__ __device__ size_t sig_scratch_words(size_t nwork) { return nwork * (SIG_VTAB_WORDS + 24); }
 

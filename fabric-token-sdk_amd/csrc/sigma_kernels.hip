@@ -155,8 +155,10 @@ __global__ void __launch_bounds__(64) k_sig_var(int nfix, int nwork, const int2*
     vk = sig_canon(S + ST_SC_CHAL * 8);
     vp = load_g1a(pts + (size_t)ac.pt_off * 16);
   }
-  // lane tables of glv_mul: [16 entries][24 words][nwork lanes] (coalesced)
-  store_g1j(terms + (size_t)(ac.term_off + t) * 24, glv_mul(vp, vk, scratch, nwork, gid));
+  // the lane's affine table (glv.hpp CTab8, 320 words per lane, rows coalesced
+  // across lanes): mixed additions in the chain
+  const CTab8 T{scratch, (size_t)nwork, (size_t)gid};
+  store_g1j(terms + (size_t)(ac.term_off + t) * 24, glv_mul_ctab8(T, vp, vk));
 }
 
 FTS_DEV void put_hex_aff(uint8_t* msg, int idx, const uint32_t* aff_pt, bool sep) {
