@@ -1422,6 +1422,7 @@ def bench_transfer(args, raw_requests=False):
         batches = [pp.prepare_requests(reqs) for _ in range(nb)]
     else:
         batches = [pp.prepare_transfers(items) for _ in range(nb)]
+    pp.reserve()  # every lane's workspace sized for the largest pass, before the clock (as C2)
     setup_s = time.time() - t0
     for _ in range(max(1, args.warmup)):
         st, fi = batches[0].verify()[0], None
@@ -1512,6 +1513,7 @@ def bench_mixed(args):
     issues = [is_bad.get(i, is_base[i % di]) for i in range(n_is)]
     nb = max(1, min(args.action_inflight, args.steps))
     batches = [pp.prepare_actions(transfers, issues) for _ in range(nb)]
+    pp.reserve()  # every lane's workspace sized for the largest pass, before the clock (as C2)
     setup_s = time.time() - t0
     for _ in range(max(1, args.warmup)):
         st_t, fi_t, st_i, fi_i = batches[0].verify()

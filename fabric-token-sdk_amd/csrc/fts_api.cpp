@@ -1445,6 +1445,7 @@ struct RpPass {
   double t_start = 0, t_prep = 0, t_enq = 0;
   bool tl_started = false;
   std::vector<fts_rp_batch*> bats;  // the caller batches of the pass (groups order); empty: none
+  bool clean = false;               // the combination closed: no fallback ran (rp_finish)
   int located = -1;                 // the locator: 1 hit, 0 missed, -1 not run  // the lane's timeline was begun by the caller (action passes: gather + sigma marks)
 };
 
@@ -1611,6 +1612,7 @@ static int rp_finish(fts_ctx* c, Lane& L, RpPass& P) {
   L.host_wait_ms = (float)(t_wait - P.t_enq);
   const int32_t flag = L.pin->flag;
   c->last_fallback = flag ? 0 : 1;
+  P.clean = flag != 0;
   if (flag) return FTS_API_OK;
   if (P.r.G > 1) {  // per-caller-batch combination: only the failing batches go to the group test
     std::vector<uint8_t> only((size_t)P.r.G, 0);
@@ -1765,6 +1767,22 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
                         w.rp_ipa.as<int32_t>(), [] {}, groups, P[j], pre, pre ? &h : nullptr);
     };
     rc[j] = enq();
+    // the verdicts' downloads behind the pass, before its flag is read: a clean pass
+    // (no fallback) needs no second round trip (fin re-downloads after a fallback)
+    if (rc[j] == FTS_API_OK && !sig_only[j]) {
+      int32_t* pst = L.status_buf(std::max<size_t>(Bs[j], 1));
+      if (!pst) {
+        rc[j] = FTS_API_ENOMEM;
+      } else {
+        if (Bs[j] && hipMemcpyAsync(pst, d_status[j], Bs[j] * 4, hipMemcpyDeviceToHost, L.s) != hipSuccess)
+          rc[j] = FTS_API_EDEVICE;
+        for (RpReq* q : grp)
+          if (q->act && q->act->sd.A &&
+              hipMemcpyAsync(q->act->sig_res, q->act->sd.status, (size_t)q->act->sd.A * 4, hipMemcpyDeviceToHost,
+                             L.s) != hipSuccess)
+            rc[j] = FTS_API_EDEVICE;
+      }
+    }
     for (RpReq* q : rpq[j]) {
       P[j].dense.push_back(q->b->dense ? 1 : 0);
       P[j].bats.push_back(q->b);
@@ -1783,12 +1801,14 @@ static void run_rp_groups(fts_ctx* c, const std::vector<Lane*>& lanes, const std
       }
       int32_t* pst = L.status_buf(std::max<size_t>(Bs[j], 1));
       if (!pst) return FTS_API_ENOMEM;
-      if (Bs[j]) HIP_OK(hipMemcpyAsync(pst, d_status[j], Bs[j] * 4, hipMemcpyDeviceToHost, L.s));
-      for (RpReq* q : sub[j])
-        if (q->act && q->act->sd.A)
-          HIP_OK(hipMemcpyAsync(q->act->sig_res, q->act->sd.status, (size_t)q->act->sd.A * 4, hipMemcpyDeviceToHost,
-                                L.s));
-      HIP_OK(L.sync());
+      if (!P[j].clean) {  // a fallback (or a sigma-only pass) ran after the early downloads
+        if (Bs[j]) HIP_OK(hipMemcpyAsync(pst, d_status[j], Bs[j] * 4, hipMemcpyDeviceToHost, L.s));
+        for (RpReq* q : sub[j])
+          if (q->act && q->act->sd.A)
+            HIP_OK(hipMemcpyAsync(q->act->sig_res, q->act->sd.status, (size_t)q->act->sd.A * 4, hipMemcpyDeviceToHost,
+                                  L.s));
+        HIP_OK(L.sync());
+      }
       for (size_t i = 0; i < rpq[j].size(); i++) {
         RpReq* q = rpq[j][i];
         const int32_t* v = pst + first[j][i];
