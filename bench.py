@@ -228,7 +228,8 @@ def main():
                          "into shared passes, as a validator's goroutines would submit them), 3 otherwise")
     args = ap.parse_args()
     if args.action_inflight is None:
-        args.action_inflight = 8 if args.workload in ("transfer", "mixed", "request") else 3
+        args.action_inflight = (8 if args.workload in ("transfer", "mixed", "request")
+                                else 8 if args.workload == "identity" else 3)
     if args.workload == "msm":
         return bench_msm(args)
     if args.workload == "transfer":
@@ -1286,9 +1287,13 @@ def bench_idemix(args):
 #   exponentiations by u (62 cyclotomic squarings of 18 + 27 products each) + ~10 products,
 #   4 cyclotomic squarings, 8 Frobenius
 #   t-values: 6 GLV products (table 103 + normalisation 53 + 124 doublings of 7 + ~60 mixed
-#   additions of 11 + ~30 beta products) + 14 fixed-base products (16 mixed additions) + ~20 additions
+#   additions of 11 + ~30 beta products) + 11 distinct fixed-base products (16 mixed additions;
+#   round 6: three of the reference's 14 repeat with the same base and scalar) + 20 additions
 ID_PAIRING_MULS = 63 * 36 + (64 + 36 + 2) * 2 * 44 + 250 + 3 * (62 * 18 + 27 * 54) + 10 * 54 + 4 * 18 + 8 * 15
-ID_TVAL_MULS = 6 * (103 + 53 + 124 * 7 + 60 * 11 + 30) + 14 * 16 * 11 + 20 * 16 + 65
+ID_TVAL_MULS = 6 * (103 + 53 + 124 * 7 + 60 * 11 + 30) + 11 * 16 * 11 + 20 * 16 + 65
+#   batch pairing check: two 64-bit GLV chains (table 103 + normalisation 53 + 64 doublings
+#   of 7 + ~32 mixed additions of 11 + ~16 beta products) and one LDS-tree addition of 16 each
+ID_BATCH_MULS = 2 * (103 + 53 + 64 * 7 + 32 * 11 + 16 + 16)
 
 
 def bench_identity(args):
@@ -1339,13 +1344,22 @@ def bench_identity(args):
         a, b = V.last_kernel_ms()
         kt, kp = kt + a, kp + b
     kt, kp = kt / reps, kp / reps
-    mads = n * ID_PAIRING_MULS * MAD_PER_MUL
-    ach = mads / (kp * 1e-3) / 1e12
-    roof = {"bound": "int32_valu (v_mad_u64_u32)", "kernel": "k_idv_pairing", "achieved": round(ach, 3),
-            "peak": round(PEAK_TMAD, 3), "unit": "TMAD/s", "frac": round(ach / PEAK_TMAD, 4), "traffic": None,
-            "kernel_ms": round(kp, 4), "mads_per_launch": mads, "muls_per_identity": ID_PAIRING_MULS,
-            "measured": "HIP events around each launch on the library's stream, %d isolated calls after the "
+    groups, paired = V.last_pairing_stats()
+    # the dominant device work since the batch pairing check (round 6): the t-value
+    # kernels (k_idv_var's six GLV and fourteen fixed-base products per identity); the
+    # pairing phase is mostly the latency of the per-group pairings (a few waves)
+    mads = n * ID_TVAL_MULS * MAD_PER_MUL
+    ach = mads / (kt * 1e-3) / 1e12
+    roof = {"bound": "int32_valu (v_mad_u64_u32)", "kernel": "k_idv_decode + k_idv_var + k_idv_tvals",
+            "achieved": round(ach, 3), "peak": round(PEAK_TMAD, 3), "unit": "TMAD/s", "frac": round(ach / PEAK_TMAD, 4),
+            "traffic": None, "kernel_ms": round(kt, 4), "mads_per_launch": mads, "muls_per_identity": ID_TVAL_MULS,
+            "measured": "HIP events around the three launches on the library's stream, %d isolated calls after the "
                         "timed region (the Fp inversions are not counted as work)" % reps}
+    pairing = {"phase_ms": round(kp, 4), "groups": groups, "paired_one_by_one": paired,
+               "batch_muls_per_identity": ID_BATCH_MULS,
+               "note": "k_idv_bp_terms (two 64-bit GLV chains per identity), one randomised pairing product per "
+                       "group of 256 (k_idv_bp_pair), one-by-one pairings only for failing groups; "
+                       "FTS_IDV_BATCH=0 pairs every identity (%d Fp products each)" % ID_PAIRING_MULS}
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         from oracle import idemix as O, idemix_identity as ID, pairing as PR
@@ -1378,7 +1392,7 @@ def bench_identity(args):
                                    "fts_idemix_identity_verify_batch, %d calls in flight" % (n, inflight),
                        "identities_per_gpu": n, "parallelism": "shard%d" % world},
             "roofline": roof, "cpu_baseline": cpu,
-            "kernel_ms": {"k_idv_tvals": round(kt, 4), "k_idv_pairing": round(kp, 4)},
+            "kernel_ms": {"k_idv_tvals": round(kt, 4), "k_idv_pairing": round(kp, 4)}, "pairing_check": pairing,
             "tval_mads_per_identity": ID_TVAL_MULS * MAD_PER_MUL, "setup_s": round(setup_s, 2)}), flush=True)
     if dist is not None:
         dist.destroy_process_group()

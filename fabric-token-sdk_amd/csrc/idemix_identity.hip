@@ -14,7 +14,7 @@
 //   k_idv_tvals    decode the 7 points (nym key, A', ABar, B', Nym, EidNym, RhNym)
 //                  and the epoch key, the error precedence, then the five
 //                  t-values (6 variable-base GLV products over affine lane
-//                  tables + 14 fixed-base products from the issuer's tables),
+//                  tables + 11 fixed-base products from the issuer's tables),
 //                  one batch normalisation, the Fiat-Shamir transcript in lane
 //                  scratch ([byte][lane]: coalesced byte stores), SHA-256 and
 //                  c == HashToZr(c' || Nonce)
@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
+#include <sys/random.h>
 
 #include <algorithm>
 #include <atomic>
@@ -38,6 +39,7 @@
 #include <vector>
 
 #include "../../include/fts_gpu.h"
+#include "common/chacha20.hpp"
 #include "common/sha256.hpp"
 #include "device/fixed_base.hpp"
 #include "device/glv.hpp"
@@ -67,21 +69,28 @@ constexpr int NB = 7, B_HSK = 0, B_HRAND = 1, B_HA = 2, B_G1 = 6;
 constexpr int NPT = 7;   // raw points per item: nymPK, A', ABar, B', Nym, EidNym, RhNym
 constexpr int P_NYMPK = 0, P_AP = 1, P_ABAR = 2, P_BP = 3, P_NYM = 4, P_EID = 5, P_RH = 6;
 constexpr int NVAR = 6;  // variable-base products: A' sE, D (-c), B' sR3, Nym (-c), EidNym (-c), RhNym (-c)
-constexpr int NFIX = 14;
+constexpr int NFIX = 11;  // distinct fixed-base products (three serve two t-values each)
 constexpr int NSC = NVAR + NFIX;
 // record words: flags, c (raw LE limbs, compared), nonce (BE words, hashed), scalars
 constexpr int R_FLAGS = 0, R_C = 1, R_NONCE = 9, R_SC = 17;
-constexpr int REC_WORDS = R_SC + NSC * 8;  // 177
-constexpr int REC_STRIDE = 180;            // 16-byte aligned records
+constexpr int REC_WORDS = R_SC + NSC * 8;  // 153
+constexpr int REC_STRIDE = 156;            // 16-byte aligned records
+static_assert(REC_STRIDE >= REC_WORDS && REC_STRIDE % 4 == 0, "record stride");
 // flags (host parse), in the reference's order of checks
 constexpr uint32_t F_EARLY_MALFORMED = 1u, F_NO_EID = 2u, F_NO_RH = 4u, F_LATE_MALFORMED = 8u, F_REVOCATION = 16u,
                    F_C_BIG = 32u;
 // targets: t1..t5 = 0..4
 __device__ constexpr int VAR_PT[NVAR] = {P_AP, -1, P_BP, P_NYM, P_EID, P_RH};  // -1: D = ABar - B'
 __device__ constexpr int VAR_T[NVAR] = {0, 0, 1, 2, 3, 4};
+// Fixed-base products and the t-value(s) each is added to: sSk HSk, sA2 HAttrs[2] and
+// sA3 HAttrs[3] appear in t2 and again in t3 / t4 / t5 with the same scalar (the
+// reference's t3 = HSk^sSk HRand^sRNym ..., t4 = HAttrs[eid]^sEid ..., t5 =
+// HAttrs[rh]^sRh ...; IBM/idemix signature.go Ver), so each is computed once and
+// added twice (FIX_T2; round 6: 14 -> 11 table gathers of 16 rows per identity)
 __device__ constexpr int FIX_B[NFIX] = {B_HRAND, B_HRAND, B_HSK, B_HA + 0, B_HA + 1, B_HA + 2, B_HA + 3,
-                                         B_G1,    B_HSK,   B_HRAND, B_HA + 2, B_HRAND, B_HA + 3, B_HRAND};
-__device__ constexpr int FIX_T[NFIX] = {0, 1, 1, 1, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4};
+                                         B_G1,    B_HRAND, B_HRAND, B_HRAND};
+__device__ constexpr int FIX_T[NFIX] = {0, 1, 1, 1, 1, 1, 1, 1, 2, 3, 4};
+__device__ constexpr int FIX_T2[NFIX] = {-1, -1, 2, -1, -1, 3, 4, -1, -1, -1, -1};
 // transcript: label || t1 t2 t3 A' ABar B' Nym EidNym t4 RhNym t5 || ipk.Hash || Disclosure (4 zero bytes)
 constexpr char LABEL[] = "signWithEidNymRhNym";
 constexpr int LABEL_LEN = 19;
@@ -231,7 +240,7 @@ struct ByteSink {
   }
 };
 
-// affine lane table of 1..8 * P: XY [8][16] | Z [8][8] | PRE [8][8] words, [word][lane]
+// affine lane table of 1..8 * P: XY rows [8][L][16] | Z, PRE [16][8][L] words (GTab)
 constexpr int AT_WORDS = 8 * 16 + 8 * 8 + 8 * 8;
 template <class CV>
 FTS_DEV void put_f(const LaneWords& T, size_t w0, const typename CV::F& a) {
@@ -246,58 +255,82 @@ FTS_DEV typename CV::F get_f(const LaneWords& T, size_t w0) {
   return a;
 }
 
-// k * P (k canonical mod r, P Jacobian) by GLV: k = k1 + k2 lambda; one table of
-// 1..8 * P, normalised with one inversion; phi(mP) = (beta x, y) read from the
-// same entries; 32 signed 4-bit windows, 124 doublings, <= 64 mixed additions
+// Lane table of 1..8 * P for the GLV chains (round 6 layout): the affine entries as
+// 64-byte rows, entry-major ([8][L][16] words: a window lookup reads ONE row per lane,
+// four 16-byte loads, where the [word][lane] layout touched up to sixteen 128-byte
+// lines per word and wave), then the build's z's and running products [16][8][L].
+struct GTab {
+  uint32_t* base;
+  size_t L, lane;
+  FTS_DEV uint32_t* row(int e) const { return base + ((size_t)e * L + lane) * 16; }
+  FTS_DEV LaneWords zw() const { return LaneWords{base + (size_t)8 * 16 * L, L, lane}; }
+};
 template <class CV>
-FTS_DEV typename CV::PJ glv_mul(const typename CV::PJ& P, const uint32_t k[8], const LaneWords& T) {
+FTS_DEV void row_put(uint32_t* p, const typename CV::F& x, const typename CV::F& y) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+  q[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+  q[2] = make_uint4(y.v[0], y.v[1], y.v[2], y.v[3]);
+  q[3] = make_uint4(y.v[4], y.v[5], y.v[6], y.v[7]);
+}
+template <class CV>
+FTS_DEV void row_get(const uint32_t* p, typename CV::F& x, typename CV::F& y) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+  x.v[0] = a.x, x.v[1] = a.y, x.v[2] = a.z, x.v[3] = a.w, x.v[4] = b.x, x.v[5] = b.y, x.v[6] = b.z, x.v[7] = b.w;
+  y.v[0] = c.x, y.v[1] = c.y, y.v[2] = c.z, y.v[3] = c.w, y.v[4] = d.x, y.v[5] = d.y, y.v[6] = d.z, y.v[7] = d.w;
+}
+
+// 1..8 * P (P Jacobian, not the identity) into the lane table T, normalised to
+// affine with one inversion (Montgomery's trick over the eight z's)
+template <class CV>
+FTS_DEV void glv_table(const typename CV::PJ& P, const GTab& T) {
   using B = typename CV::B;
   using F = typename CV::F;
   using PJ = typename CV::PJ;
-  uint32_t nz = 0;
-#pragma unroll
-  for (int q = 0; q < 8; q++) nz |= k[q];
-  if (CV::is_inf(P) || !nz) return CV::inf();
-  // 1..8 P (Jacobian), running product of the z's
+  const LaneWords Z = T.zw();
   PJ cur = P;
   F pre = P.z;
   for (int e = 0; e < 8; e++) {
     if (e == 1) cur = CV::dbl(P);
     if (e > 1) CV::add_to(cur, P);
-    put_f<CV>(T, e * 16, cur.x);
-    put_f<CV>(T, e * 16 + 8, cur.y);
-    put_f<CV>(T, 128 + e * 8, cur.z);
+    row_put<CV>(T.row(e), cur.x, cur.y);
+    put_f<CV>(Z, e * 8, cur.z);
     if (e) pre = B::mul(pre, cur.z);
-    put_f<CV>(T, 192 + e * 8, pre);
+    put_f<CV>(Z, 64 + e * 8, pre);
   }
   F inv = B::inv(pre);
   for (int e = 7; e >= 0; e--) {
     F zi = inv;
     if (e > 0) {
-      zi = B::mul(inv, get_f<CV>(T, 192 + (e - 1) * 8));
-      inv = B::mul(inv, get_f<CV>(T, 128 + e * 8));
+      zi = B::mul(inv, get_f<CV>(Z, 64 + (e - 1) * 8));
+      inv = B::mul(inv, get_f<CV>(Z, e * 8));
     }
     const F zi2 = B::mul(zi, zi);
-    put_f<CV>(T, e * 16, B::mul(get_f<CV>(T, e * 16), zi2));
-    put_f<CV>(T, e * 16 + 8, B::mul(B::mul(get_f<CV>(T, e * 16 + 8), zi2), zi));
+    F x, y;
+    row_get<CV>(T.row(e), x, y);
+    row_put<CV>(T.row(e), B::mul(x, zi2), B::mul(B::mul(y, zi2), zi));
   }
-  uint32_t k1[4], k2[4], s1, s2;
-  CV::decompose(k, k1, s1, k2, s2);
+}
+
+// (-1)^s1 k1 * P + (-1)^s2 k2 * phi(P) over the table of glv_table: NW signed 4-bit
+// windows from the top (magnitudes below 2^(4 NW - 1)), 4 (NW - 1) doublings,
+// <= 2 NW mixed additions
+template <class CV, int NW>
+FTS_DEV typename CV::PJ glv_chain(const GTab& T, const uint32_t k1[4], uint32_t s1, const uint32_t k2[4],
+                                  uint32_t s2) {
+  using B = typename CV::B;
+  using F = typename CV::F;
+  using PJ = typename CV::PJ;
   const uint32_t c1 = recode_carries(k1), c2 = recode_carries(k2);
   const F beta = CV::beta();
   PJ acc = CV::inf();
-  for (int w = 31; w >= 0; w--) {
+  for (int w = NW - 1; w >= 0; w--) {
     const int d1 = window_digit(k1, c1, w), d2 = window_digit(k2, c2, w);
     F x1, y1, x2, y2;
-    if (d1) {
-      const int e = (d1 < 0 ? -d1 : d1) - 1;
-      x1 = get_f<CV>(T, e * 16), y1 = get_f<CV>(T, e * 16 + 8);
-    }
-    if (d2) {
-      const int e = (d2 < 0 ? -d2 : d2) - 1;
-      x2 = get_f<CV>(T, e * 16), y2 = get_f<CV>(T, e * 16 + 8);
-    }
-    if (w != 31)
+    if (d1) row_get<CV>(T.row((d1 < 0 ? -d1 : d1) - 1), x1, y1);
+    if (d2) row_get<CV>(T.row((d2 < 0 ? -d2 : d2) - 1), x2, y2);
+    if (w != NW - 1)
       for (int r = 0; r < 4; r++) acc = CV::dbl(acc);
     if (d1) {
       if ((d1 < 0) != (s1 != 0)) y1 = B::neg(y1);
@@ -309,6 +342,21 @@ FTS_DEV typename CV::PJ glv_mul(const typename CV::PJ& P, const uint32_t k[8], c
     }
   }
   return acc;
+}
+
+// k * P (k canonical mod r, P Jacobian) by GLV: k = k1 + k2 lambda; one table of
+// 1..8 * P, normalised with one inversion; phi(mP) = (beta x, y) read from the
+// same entries; 32 signed 4-bit windows, 124 doublings, <= 64 mixed additions
+template <class CV>
+FTS_DEV typename CV::PJ glv_mul(const typename CV::PJ& P, const uint32_t k[8], const GTab& T) {
+  uint32_t nz = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) nz |= k[q];
+  if (CV::is_inf(P) || !nz) return CV::inf();
+  glv_table<CV>(P, T);
+  uint32_t k1[4], k2[4], s1, s2;
+  CV::decompose(k, k1, s1, k2, s2);
+  return glv_chain<CV, 32>(T, k1, s1, k2, s2);
 }
 
 // G2 point (affine Montgomery Fp2) on the twist y^2 = x^3 + b'
@@ -418,6 +466,7 @@ FTS_DEV bool g2_in_subgroup_bn(const pair::F2<pair::BnField>& qx, const pair::F2
   return eq(acc.x, mul(qx, z2)) && eq(acc.y, neg(mul(qy, z3)));
 }
 
+#ifndef IDV_FBN_TU  // BN254 only: compiled in the main translation unit
 // U distinct epoch keys (128 raw bytes each, BN254): ok[u] <- the key decodes (on the
 // twist, canonical) and lies in the subgroup (the identity does)
 // lane j checks distinct key idx[j] (the keys the context has not checked before)
@@ -434,6 +483,7 @@ __global__ void __launch_bounds__(64) k_idv_g2_check(int M, const int32_t* __res
   if (good && !zero) good = g2_in_subgroup_bn(x, y);
   ok[u] = good ? 1 : 0;
 }
+#endif
 
 // ----------------------------------------------------------------- kernels
 // lines of W (lane 0) and g2 (lane 1); wraw: W as 128 raw bytes; ok[0] <- W valid
@@ -472,9 +522,9 @@ __global__ void __launch_bounds__(64) k_idv_lines(const uint8_t* __restrict__ wr
 FTS_DEV size_t sc_s(size_t) { return 0; }
 FTS_DEV size_t sc_dp(size_t n) { return (size_t)5 * 24 * n; }
 FTS_DEV size_t sc_idm(size_t n) { return sc_dp(n) + (size_t)NPT * 16 * n; }
-FTS_DEV size_t sc_vr(size_t n) { return sc_idm(n) + n; }
+FTS_DEV size_t sc_vr(size_t n) { return sc_idm(n) + ((n + 3) & ~size_t(3)); }  // keeps sc_tv 16-byte aligned (GTab rows)
 FTS_DEV size_t sc_tv(size_t n) { return sc_vr(n) + (size_t)NSC * 24 * n; }
-inline size_t idv_scratch_words(size_t n) { return (5 * 24 + NPT * 16 + 1 + NSC * 24 + NVAR * AT_WORDS) * n; }
+inline size_t idv_scratch_words(size_t n) { return (5 * 24 + NPT * 16 + 1 + NSC * 24 + NVAR * AT_WORDS) * n + 3; }
 
 // Three kernels per batch (round 4; one lane per identity for everything left
 // 1,024 waves at one per SIMD, 30 % of the MAD peak):
@@ -482,7 +532,7 @@ inline size_t idv_scratch_words(size_t n) { return (5 * 24 + NPT * 16 + 1 + NSC 
 //                 level errors), point decoding in the reference's order of
 //                 checks, pin[i] <- (A', -ABar) for the pairing kernel
 //   k_idv_var     lane per (product, identity): the six GLV products and the
-//                 fourteen fixed-base products of the t-values, 20x the lanes
+//                 eleven fixed-base products of the t-values, 17x the lanes
 //   k_idv_tvals   identity per lane: sum the products into t1..t5,
 //                 normalisation, transcript, challenge;
 //                 zk[i] <- 1 if c == c''
@@ -585,7 +635,7 @@ __global__ void __launch_bounds__(256) k_idv_var(int n, const uint32_t* __restri
   PJ base = (idm >> pq_) & 1u ? CV::inf() : CV::from_affine(get_f<CV>(DP, pq_ * 16), get_f<CV>(DP, pq_ * 16 + 8));
   if (VAR_PT[v] < 0 && !((idm >> P_BP) & 1u))  // D = ABar - B'
     CV::madd_to(base, get_f<CV>(DP, P_BP * 16), B::neg(get_f<CV>(DP, P_BP * 16 + 8)));
-  const LaneWords T{scratch + sc_tv(n) + (size_t)v * AT_WORDS * n, (size_t)n, (size_t)i};
+  const GTab T{scratch + sc_tv(n) + (size_t)v * AT_WORDS * n, (size_t)n, (size_t)i};
   const PJ r = glv_mul<CV>(base, R + R_SC + v * 8, T);
   put_f<CV>(VR, 0, r.x);
   put_f<CV>(VR, 8, r.y);
@@ -621,13 +671,16 @@ __global__ void __launch_bounds__(256) k_idv_tvals(int n, const uint32_t* __rest
     const LaneWords VR{scratch + sc_vr(n) + (size_t)v * 24 * n, (size_t)n, (size_t)i};
     PJ r;
     r.x = get_f<CV>(VR, 0), r.y = get_f<CV>(VR, 8), r.z = get_f<CV>(VR, 16);
-    const int t = v < NVAR ? VAR_T[v] : FIX_T[v - NVAR];
-    PJ acc;
-    acc.x = get_f<CV>(S, t * 24), acc.y = get_f<CV>(S, t * 24 + 8), acc.z = get_f<CV>(S, t * 24 + 16);
-    CV::add_to(acc, r);
-    put_f<CV>(S, t * 24, acc.x);
-    put_f<CV>(S, t * 24 + 8, acc.y);
-    put_f<CV>(S, t * 24 + 16, acc.z);
+    const int t1 = v < NVAR ? VAR_T[v] : FIX_T[v - NVAR], t2 = v < NVAR ? -1 : FIX_T2[v - NVAR];
+    for (int t : {t1, t2}) {
+      if (t < 0) continue;
+      PJ acc;
+      acc.x = get_f<CV>(S, t * 24), acc.y = get_f<CV>(S, t * 24 + 8), acc.z = get_f<CV>(S, t * 24 + 16);
+      CV::add_to(acc, r);
+      put_f<CV>(S, t * 24, acc.x);
+      put_f<CV>(S, t * 24 + 8, acc.y);
+      put_f<CV>(S, t * 24 + 16, acc.z);
+    }
   }
   // the five t-values -> affine with one inversion (Montgomery's trick; identity -> (0, 0))
   {
@@ -714,11 +767,16 @@ __global__ void __launch_bounds__(256) k_idv_tvals(int n, const uint32_t* __rest
 template <class CV>
 __global__ void __launch_bounds__(64, FTS_IDV_OCC) k_idv_pairing(int n, const uint32_t* __restrict__ pin,
                                                     const uint32_t* __restrict__ lines, const int32_t* __restrict__ zk,
-                                                    int32_t* __restrict__ status) {
+                                                    int32_t* __restrict__ status, const int32_t* __restrict__ list,
+                                                    const int32_t* __restrict__ count) {
   using B = typename CV::B;
   using K = typename B::K;
   using F = typename B::F;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (list) {  // the identities of the groups whose batch check failed (k_idv_bp_sel)
+    if (i >= *count) return;
+    i = list[i];
+  }
   if (i >= n || status[i] != FTS_OK) return;
   const uint32_t* pq = pin + (size_t)i * 32;
   const uint32_t* const L[2] = {lines, lines + (size_t)pair::n_lines<K>() * pair::LINE_WORDS};
@@ -734,6 +792,134 @@ __global__ void __launch_bounds__(64, FTS_IDV_OCC) k_idv_pairing(int n, const ui
   }
   const bool one = pair::is_one(pair::final_exp_i(f));
   status[i] = !one ? FTS_E_ID_PAIRING : (zk[i] ? FTS_OK : FTS_E_ID_ZK);
+}
+
+// ---- batch pairing check (round 6)
+// The equations e(W, A'_i) e(g2, -ABar_i) = 1 of a group of BP_G identities are
+// checked as ONE: e(W, sum rho_i A'_i) e(g2, sum rho_i (-ABar_i)) = 1, with secret
+// weights rho_i = a_i + b_i lambda (a_i, b_i: 64-bit ChaCha20 words under a key drawn
+// with getrandom for every call; the GLV lattice {(x, y): x + y lambda = 0 mod r} has
+// no nonzero vector shorter than ~2^126, so the 2^128 pairs are 2^128 distinct rho
+// mod r).  Pairing values live in the order-r subgroup of GT (r prime), so a group
+// holding an identity whose equation fails passes with probability <= 2^-128 (the
+// small-exponents batch test of Bellare, Garay and Rabin).  A group that fails has
+// its identities paired one by one (k_idv_pairing over the k_idv_bp_sel list), so
+// every verdict is the per-identity one.  Work per identity: two 64-bit GLV chains
+// (17 windows) instead of a 2-pairing Miller loop and a final exponentiation.
+constexpr int BP_G = 256;  // identities per group = threads of a k_idv_bp_terms block
+struct Key8 {
+  uint32_t k[8];
+};
+// scratch (the t-value kernels' scratch, free by then):
+//   lane tables [2][AT_WORDS][n] | group sums [ng][2][24] | gok [ng] | count | list [n]
+inline size_t bp_part_off(size_t n) { return (size_t)2 * AT_WORDS * n; }
+inline size_t bp_gok_off(size_t n, size_t ng) { return bp_part_off(n) + ng * 48; }
+inline size_t bp_cnt_off(size_t n, size_t ng) { return bp_gok_off(n, ng) + ng; }
+inline size_t bp_list_off(size_t n, size_t ng) { return bp_cnt_off(n, ng) + 64; }
+inline size_t bp_scratch_words(size_t n) {
+  const size_t ng = (n + BP_G - 1) / BP_G;
+  return bp_list_off(n, ng) + n;
+}
+
+// block = group g, blockIdx.y = which point (0: A', 1: -ABar): rho_i * P_i summed
+// over the group's identities still OK (the others contribute O), LDS tree
+template <class CV>
+__global__ void __launch_bounds__(BP_G) k_idv_bp_terms(int n, const uint32_t* __restrict__ pin,
+                                                       const int32_t* __restrict__ status, Key8 key,
+                                                       uint32_t* __restrict__ scratch, uint32_t* __restrict__ part) {
+  using B = typename CV::B;
+  using F = typename CV::F;
+  using PJ = typename CV::PJ;
+  __shared__ uint32_t sh[24 * BP_G];
+  const int t = threadIdx.x, which = blockIdx.y;
+  const int i = blockIdx.x * BP_G + t;
+  PJ r = CV::inf();
+  if (i < n && status[i] == FTS_OK) {
+    const uint32_t* pq = pin + (size_t)i * 32 + which * 16;
+    const F x = B::ld(pq), y = B::ld(pq + 8);
+    if (!(B::is_zero(x) && B::is_zero(y))) {  // -ABar = O: e(g2, O) = 1, no term
+      uint32_t blk[16];
+      fts::chacha20_block(key.k, (uint32_t)i, blk);
+      const uint32_t a[4] = {blk[0], blk[1], 0u, 0u}, b[4] = {blk[2], blk[3], 0u, 0u};
+      const GTab T{scratch + (size_t)which * AT_WORDS * n, (size_t)n, (size_t)i};
+      glv_table<CV>(CV::from_affine(x, y), T);
+      r = glv_chain<CV, 17>(T, a, 0u, b, 0u);
+    }
+  }
+  const LaneWords S{sh, (size_t)BP_G, (size_t)t};
+  put_f<CV>(S, 0, r.x);
+  put_f<CV>(S, 8, r.y);
+  put_f<CV>(S, 16, r.z);
+  for (int h = BP_G / 2; h > 0; h >>= 1) {
+    __syncthreads();
+    if (t < h) {
+      const LaneWords O{sh, (size_t)BP_G, (size_t)(t + h)};
+      PJ a, b;
+      a.x = get_f<CV>(S, 0), a.y = get_f<CV>(S, 8), a.z = get_f<CV>(S, 16);
+      b.x = get_f<CV>(O, 0), b.y = get_f<CV>(O, 8), b.z = get_f<CV>(O, 16);
+      CV::add_to(a, b);
+      put_f<CV>(S, 0, a.x);
+      put_f<CV>(S, 8, a.y);
+      put_f<CV>(S, 16, a.z);
+    }
+  }
+  if (t < 24) part[((size_t)blockIdx.x * 2 + which) * 24 + t] = sh[(size_t)t * BP_G];
+}
+
+// lane = group: the two sums to affine (one inversion), then the group's pairing
+// product; gok[g] <- 1 if it is 1 in GT.  Lane 0 also clears the list counter.
+template <class CV>
+__global__ void __launch_bounds__(64, FTS_IDV_OCC) k_idv_bp_pair(int ng, const uint32_t* __restrict__ part,
+                                                    const uint32_t* __restrict__ lines, int32_t* __restrict__ gok,
+                                                    int32_t* __restrict__ count) {
+  using B = typename CV::B;
+  using K = typename B::K;
+  using F = typename B::F;
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g == 0) *count = 0;
+  if (g >= ng) return;
+  const uint32_t* S = part + (size_t)g * 48;
+  const F z0 = B::ld(S + 16), z1 = B::ld(S + 40);
+  const bool o0 = B::is_zero(z0), o1 = B::is_zero(z1);
+  if (o0 && o1) {  // nothing left to check in this group
+    gok[g] = 1;
+    return;
+  }
+  const F w0 = o0 ? B::one() : z0, w1 = o1 ? B::one() : z1;
+  const F inv = B::inv(B::mul(w0, w1));
+  F x[2], y[2];
+  {
+    const F zi0 = B::mul(inv, w1), zi1 = B::mul(inv, w0);
+    const F a0 = B::mul(zi0, zi0), a1 = B::mul(zi1, zi1);
+    x[0] = B::mul(B::ld(S), a0), y[0] = B::mul(B::mul(B::ld(S + 8), a0), zi0);
+    x[1] = B::mul(B::ld(S + 24), a1), y[1] = B::mul(B::mul(B::ld(S + 32), a1), zi1);
+  }
+  const uint32_t* const L[2] = {lines, lines + (size_t)pair::n_lines<K>() * pair::LINE_WORDS};
+  pair::F12<B> f;
+  if (o0 || o1) {  // one pairing left: e(W, .) or e(g2, .)
+    const int q = o0 ? 1 : 0;
+    const uint32_t* const L1[1] = {L[q]};
+    const F x1[1] = {x[q]}, y1[1] = {y[q]};
+    f = pair::miller<B, 1>(L1, x1, y1);
+  } else {
+    f = pair::miller<B, 2>(L, x, y);
+  }
+  gok[g] = pair::is_one(pair::final_exp_i(f)) ? 1 : 0;
+}
+
+// identity per lane: verdict of the identities of passing groups; the others are
+// appended to the list k_idv_pairing pairs one by one
+template <class CV>  // (per-curve instance: one per translation unit)
+__global__ void __launch_bounds__(256) k_idv_bp_sel(int n, const int32_t* __restrict__ gok,
+                                                    const int32_t* __restrict__ zk, int32_t* __restrict__ status,
+                                                    int32_t* __restrict__ list, int32_t* __restrict__ count) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || status[i] != FTS_OK) return;
+  if (gok[i / BP_G]) {
+    status[i] = zk[i] ? FTS_OK : FTS_E_ID_ZK;
+    return;
+  }
+  list[atomicAdd(count, 1)] = i;
 }
 
 // debug: e(Q, P) for Q = W (which 0) or g2 (1), P affine Montgomery -> GT (12 Fp2
@@ -754,6 +940,58 @@ __global__ void __launch_bounds__(64) k_idv_pairing_debug(const uint32_t* __rest
     pair::store_f2(out + k * 16, z[k]);
   }
 }
+
+// ------------------------------------------------- per-curve launch sequences
+// Instantiated once per curve and translation unit: BN254 here, FP256BN in
+// idemix_identity_fbn.hip (each curve's pairing kernels are minutes of device
+// compilation; two units build in parallel).
+struct Chain {
+  hipStream_t s;
+  int n;
+  const uint32_t* rec;
+  const uint8_t *pts, *epk;
+  uint32_t *scr, *pin;
+  int32_t *zk, *st;
+  const int32_t *eidx, *g2ok;  // BN254 epoch keys (FP256BN: null)
+  const uint32_t *tables, *hash, *lines;
+  uint8_t* msg;
+  int32_t *gok, *cnt, *list;
+  Key8 key;
+};
+// decode, the t-value products, the t-values and the transcript
+template <class CV>
+void launch_tvals(const Chain& c) {
+  const unsigned g256 = (unsigned)((c.n + 255) / 256), gvar = (unsigned)(((size_t)NSC * c.n + 255) / 256);
+  k_idv_decode<CV><<<g256, 256, 0, c.s>>>(c.n, c.rec, c.pts, c.epk, c.scr, c.pin, c.zk, c.st, c.eidx, c.g2ok);
+  k_idv_var<CV><<<gvar, 256, 0, c.s>>>(c.n, c.rec, c.tables, c.scr, c.st);
+  k_idv_tvals<CV><<<g256, 256, 0, c.s>>>(c.n, c.rec, c.tables, c.hash, c.scr, c.msg, c.zk, c.st);
+}
+// the batch pairing check up to the list of identities to pair one by one
+template <class CV>
+void launch_batch(const Chain& c) {
+  const size_t n = (size_t)c.n, ng = (n + BP_G - 1) / BP_G;
+  k_idv_bp_terms<CV><<<dim3((unsigned)ng, 2), BP_G, 0, c.s>>>(c.n, c.pin, c.st, c.key, c.scr, c.scr + bp_part_off(n));
+  k_idv_bp_pair<CV><<<(unsigned)((ng + 63) / 64), 64, 0, c.s>>>((int)ng, c.scr + bp_part_off(n), c.lines, c.gok, c.cnt);
+  k_idv_bp_sel<CV><<<(unsigned)((n + 255) / 256), 256, 0, c.s>>>(c.n, c.gok, c.zk, c.st, c.list, c.cnt);
+}
+// one-by-one pairings: `lanes` identities of the list (list) or all n
+template <class CV>
+void launch_pairing(const Chain& c, unsigned lanes, bool list) {
+  k_idv_pairing<CV><<<(lanes + 63) / 64, 64, 0, c.s>>>(c.n, c.pin, c.lines, c.zk, c.st, list ? c.list : nullptr,
+                                                        list ? c.cnt : nullptr);
+}
+template <class CV>
+void launch_lines(const uint8_t* w, uint32_t* lines, int32_t* ok, hipStream_t s) {
+  k_idv_lines<CV><<<1, 64, 0, s>>>(w, lines, ok);
+}
+
+#ifdef IDV_FBN_TU
+}  // namespace idv (the FP256BN unit holds kernels only)
+#else  // the host side
+extern template void launch_tvals<FbnCurve>(const Chain&);
+extern template void launch_batch<FbnCurve>(const Chain&);
+extern template void launch_pairing<FbnCurve>(const Chain&, unsigned, bool);
+extern template void launch_lines<FbnCurve>(const uint8_t*, uint32_t*, int32_t*, hipStream_t);
 
 // ------------------------------------------------------------------- host
 const uint32_t kRbn[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
@@ -1044,9 +1282,8 @@ int32_t parse_identity(const uint8_t* id, size_t len, bool bn, const uint32_t* r
       }
     }
     const uint32_t* var[NVAR] = {sc[2], nc, sc[4], nc, nc, nc};
-    // fixed: sR2, sS', sSk, sA0..3, c, sSk, sRNym, sA2, sEid, sA3, sRh
-    const uint32_t* fix[NFIX] = {sc[3], sc[5], sc[1], sc[8], sc[9], sc[10], sc[11], cm, sc[1], sc[7],
-                                 sc[10], sc[12], sc[11], sc[13]};
+    // fixed: sR2, sS', sSk (t2, t3), sA0, sA1, sA2 (t2, t4), sA3 (t2, t5), c, sRNym, sEid, sRh
+    const uint32_t* fix[NFIX] = {sc[3], sc[5], sc[1], sc[8], sc[9], sc[10], sc[11], cm, sc[7], sc[12], sc[13]};
     for (int v = 0; v < NVAR; v++) memcpy(rec + R_SC + v * 8, var[v], 32);
     for (int q = 0; q < NFIX; q++) memcpy(rec + R_SC + (NVAR + q) * 8, fix[q], 32);
   }
@@ -1058,7 +1295,7 @@ int32_t parse_identity(const uint8_t* id, size_t len, bool bn, const uint32_t* r
     if ((x) != hipSuccess) return FTS_API_EDEVICE; \
   } while (0)
 
-constexpr int NSLOT = 3;
+constexpr int NSLOT = 8;  // calls in flight per handle (each slot: its own stream and buffers)
 struct Slot {
   hipStream_t stream = nullptr;
   uint8_t* d_buf = nullptr;
@@ -1067,6 +1304,7 @@ struct Slot {
   size_t h_cap = 0;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   float ms[2] = {0.f, 0.f};
+  uint32_t stats[2] = {0u, 0u};
 };
 
 }  // namespace idv
@@ -1080,8 +1318,12 @@ struct fts_idemix_idv {
   std::mutex mu;
   std::condition_variable cv;
   idv::Slot slot[idv::NSLOT];
-  bool busy[idv::NSLOT] = {false, false, false};
+  bool busy[idv::NSLOT] = {};
   float last_ms[2] = {0.f, 0.f};
+  // batch pairing check (k_idv_bp_*; FTS_IDV_BATCH=0 pairs every identity, the A/B
+  // and pre-round-6 path); last call's groups and identities paired one by one
+  bool batch = true;
+  uint32_t last_stats[2] = {0u, 0u};
   // BN254 epoch keys already subgroup-checked by this context (128 raw bytes ->
   // verdict): an honest stream carries one key per epoch, and k_idv_g2_check is
   // one 254-step G2 chain on one lane (7.7 ms, on the call's critical path)
@@ -1155,6 +1397,7 @@ int fts_idemix_idv_create(int device, const uint8_t* ipk, size_t ipk_len, int cu
   fts_idemix_idv* k = new fts_idemix_idv();
   k->device = device;
   k->curve = curve_id;
+  if (const char* e = getenv("FTS_IDV_BATCH")) k->batch = atoi(e) != 0;
   auto fail = [&](int rc) {
     idv_free(k);
     return rc;
@@ -1187,10 +1430,10 @@ int fts_idemix_idv_create(int device, const uint8_t* ipk, size_t ipk_len, int cu
   if (ok) {
     if (bn) {
       launch_build_tables(d_bases, NB, k->d_tables, d_scr, s0);
-      k_idv_lines<BnCurve><<<1, 64, 0, s0>>>(d_w, k->d_lines, d_ok + NB);
+      launch_lines<BnCurve>(d_w, k->d_lines, d_ok + NB, s0);
     } else {
       fbn_build_tables(d_bases, NB, d_scr, d_ok, k->d_tables, s0);
-      k_idv_lines<FbnCurve><<<1, 64, 0, s0>>>(d_w, k->d_lines, d_ok + NB);
+      launch_lines<FbnCurve>(d_w, k->d_lines, d_ok + NB, s0);
     }
     ok = hipGetLastError() == hipSuccess &&
          hipMemcpyAsync(hok, d_ok, sizeof hok, hipMemcpyDeviceToHost, s0) == hipSuccess &&
@@ -1241,6 +1484,7 @@ int fts_idemix_identity_verify_batch(fts_idemix_idv* K, size_t n, const uint8_t*
       if (K->slot[k].stream) (void)hipStreamSynchronize(K->slot[k].stream);
       std::lock_guard<std::mutex> l(K->mu);
       K->last_ms[0] = K->slot[k].ms[0], K->last_ms[1] = K->slot[k].ms[1];
+      K->last_stats[0] = K->slot[k].stats[0], K->last_stats[1] = K->slot[k].stats[1];
       K->busy[k] = false;
       K->cv.notify_one();
     }
@@ -1254,9 +1498,10 @@ int fts_idemix_identity_verify_batch(fts_idemix_idv* K, size_t n, const uint8_t*
                o_uk = o_eidx + n * 4;
   // host only: the distinct keys' verdicts (cached or read back) and the indices to check
   const size_t o_gk = (o_uk + epk_b + 255) & ~size_t(255), o_miss = o_gk + n * 4;
-  const size_t h_need = (o_miss + n * 4 + 255) & ~size_t(255);
+  const size_t o_cnt = o_miss + n * 4;  // the batch check's list length, read back
+  const size_t h_need = (o_cnt + 4 + 255) & ~size_t(255);
   const size_t o_zk = h_need, o_pin = (o_zk + n * 4 + 255) & ~size_t(255), o_scr = o_pin + n * 32 * 4;
-  const size_t scr_w = idv_scratch_words(n);
+  const size_t scr_w = std::max(idv_scratch_words(n), bp_scratch_words(n));
   const size_t o_msg = (o_scr + scr_w * 4 + 255) & ~size_t(255);
   const size_t o_g2ok = (o_msg + (size_t)MSG_MAX * n + 255) & ~size_t(255);
   const size_t d_need = o_g2ok + 2 * n * 4;  // U verdicts, then the M key indices to check
@@ -1340,42 +1585,50 @@ int fts_idemix_identity_verify_batch(fts_idemix_idv* K, size_t n, const uint8_t*
   uint8_t* d = D.d_buf;
   ICHK(hipMemcpyAsync(d, h, o_uk + U * 128, hipMemcpyHostToDevice, D.stream));
   ICHK(hipEventRecord(D.ev[0], D.stream));
-  const unsigned g256 = (unsigned)((n + 255) / 256), g64 = (unsigned)((n + 63) / 64),
-                 gvar = (unsigned)((NSC * n + 255) / 256);
-  const uint32_t* rec = reinterpret_cast<const uint32_t*>(d);
+  // batch pairing check: group sums, one pairing product per group, the identities
+  // of failing groups listed for k_idv_pairing
   uint32_t* scr = reinterpret_cast<uint32_t*>(d + o_scr);
-  uint32_t* pin = reinterpret_cast<uint32_t*>(d + o_pin);
-  int32_t* zk = reinterpret_cast<int32_t*>(d + o_zk);
-  int32_t* st = reinterpret_cast<int32_t*>(d + o_st);
-  const size_t nl = (size_t)nlines(bn) * pair::LINE_WORDS;
+  const size_t ng = (n + BP_G - 1) / BP_G;
+  Chain c;
+  c.s = D.stream, c.n = (int)n, c.rec = reinterpret_cast<const uint32_t*>(d), c.pts = d + o_pts, c.epk = d + o_epk;
+  c.scr = scr, c.pin = reinterpret_cast<uint32_t*>(d + o_pin);
+  c.zk = reinterpret_cast<int32_t*>(d + o_zk), c.st = reinterpret_cast<int32_t*>(d + o_st);
   int32_t* g2ok = reinterpret_cast<int32_t*>(d + o_g2ok);
+  c.eidx = bn ? reinterpret_cast<const int32_t*>(d + o_eidx) : nullptr, c.g2ok = bn ? g2ok : nullptr;
+  c.tables = K->d_tables, c.hash = K->d_hash, c.lines = K->d_lines, c.msg = d + o_msg;
+  c.gok = reinterpret_cast<int32_t*>(scr + bp_gok_off(n, ng));
+  c.cnt = reinterpret_cast<int32_t*>(scr + bp_cnt_off(n, ng));
+  c.list = reinterpret_cast<int32_t*>(scr + bp_list_off(n, ng));
+  if (K->batch && getrandom(c.key.k, sizeof c.key.k, 0) != (ssize_t)sizeof c.key.k) return FTS_API_EDEVICE;
   if (bn) {
     ICHK(hipMemcpyAsync(g2ok, gk, U * 4, hipMemcpyHostToDevice, D.stream));
     if (M) {
       ICHK(hipMemcpyAsync(g2ok + U, miss, M * 4, hipMemcpyHostToDevice, D.stream));
       k_idv_g2_check<<<(unsigned)((M + 63) / 64), 64, 0, D.stream>>>((int)M, g2ok + U, d + o_uk, g2ok);
     }
-    k_idv_decode<BnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, d + o_pts, d + o_epk, scr, pin, zk, st,
-                                                       reinterpret_cast<const int32_t*>(d + o_eidx), g2ok);
-    k_idv_var<BnCurve><<<gvar, 256, 0, D.stream>>>((int)n, rec, K->d_tables, scr, st);
-    k_idv_tvals<BnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, K->d_tables, K->d_hash, scr, d + o_msg, zk, st);
-    ICHK(hipEventRecord(D.ev[1], D.stream));
-    k_idv_pairing<BnCurve><<<g64, 64, 0, D.stream>>>((int)n, pin, K->d_lines, zk, st);
-  } else {
-    k_idv_decode<FbnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, d + o_pts, d + o_epk, scr, pin, zk, st, nullptr,
-                                                        nullptr);
-    k_idv_var<FbnCurve><<<gvar, 256, 0, D.stream>>>((int)n, rec, K->d_tables, scr, st);
-    k_idv_tvals<FbnCurve><<<g256, 256, 0, D.stream>>>((int)n, rec, K->d_tables, K->d_hash, scr, d + o_msg, zk, st);
-    ICHK(hipEventRecord(D.ev[1], D.stream));
-    k_idv_pairing<FbnCurve><<<g64, 64, 0, D.stream>>>((int)n, pin, K->d_lines, zk, st);
   }
-  (void)nl;
+  bn ? launch_tvals<BnCurve>(c) : launch_tvals<FbnCurve>(c);
+  ICHK(hipEventRecord(D.ev[1], D.stream));
+  unsigned nlist = 0;  // identities of failing groups (read back after k_idv_bp_sel)
+  if (K->batch) {
+    bn ? launch_batch<BnCurve>(c) : launch_batch<FbnCurve>(c);
+    ICHK(hipMemcpyAsync(h + o_cnt, c.cnt, 4, hipMemcpyDeviceToHost, D.stream));
+    ICHK(hipStreamSynchronize(D.stream));
+    nlist = *reinterpret_cast<const uint32_t*>(h + o_cnt);
+    // exact grid: idle pairing waves (256 VGPRs and scratch each) would still queue
+    // behind the other slots' kernels
+    if (nlist) bn ? launch_pairing<BnCurve>(c, nlist, true) : launch_pairing<FbnCurve>(c, nlist, true);
+  } else {
+    bn ? launch_pairing<BnCurve>(c, (unsigned)n, false) : launch_pairing<FbnCurve>(c, (unsigned)n, false);
+  }
   ICHK(hipGetLastError());
   ICHK(hipEventRecord(D.ev[2], D.stream));
   ICHK(hipMemcpyAsync(h + o_st, d + o_st, st_b, hipMemcpyDeviceToHost, D.stream));
   if (M) ICHK(hipMemcpyAsync(gk, g2ok, U * 4, hipMemcpyDeviceToHost, D.stream));
   ICHK(hipStreamSynchronize(D.stream));
   memcpy(status, h + o_st, st_b);
+  D.stats[0] = K->batch ? (uint32_t)ng : 0u;
+  D.stats[1] = K->batch ? nlist : (uint32_t)n;
   if (M) {
     std::lock_guard<std::mutex> l(K->mu);
     if (K->g2_seen.size() + M > 4096) K->g2_seen.clear();  // bounded: a new epoch's keys refill it
@@ -1393,6 +1646,13 @@ int fts_idemix_identity_last_timings(fts_idemix_idv* K, float* ms) {
   if (!K || !ms) return FTS_API_EINVAL;
   std::lock_guard<std::mutex> l(K->mu);
   ms[0] = K->last_ms[0], ms[1] = K->last_ms[1];
+  return FTS_API_OK;
+}
+
+int fts_idemix_identity_last_stats(fts_idemix_idv* K, uint32_t* out) {
+  if (!K || !out) return FTS_API_EINVAL;
+  std::lock_guard<std::mutex> l(K->mu);
+  out[0] = K->last_stats[0], out[1] = K->last_stats[1];
   return FTS_API_OK;
 }
 
@@ -1435,3 +1695,4 @@ int fts_idemix_pairing_debug(fts_idemix_idv* K, int which, const uint8_t* p64, i
 }
 
 }  // extern "C"
+#endif  // IDV_FBN_TU

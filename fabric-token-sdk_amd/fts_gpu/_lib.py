@@ -61,7 +61,7 @@ EXPORTED = [
     "fts_ecdsa_last_timings", "fts_ctx_create_devices", "fts_ctx_create_mask", "fts_ctx_devices", "fts_shard_plan",
     "fts_idemix_ipk_create", "fts_idemix_ipk_destroy", "fts_nym_verify_batch", "fts_idemix_identity_nym",
     "fts_nym_last_timings", "fts_idemix_idv_create", "fts_idemix_idv_destroy", "fts_idemix_identity_verify_batch",
-    "fts_idemix_identity_last_timings", "fts_idemix_pairing_debug", "fts_ctx_create_opts", "fts_debug_hold",
+    "fts_idemix_identity_last_timings", "fts_idemix_identity_last_stats", "fts_idemix_pairing_debug", "fts_ctx_create_opts", "fts_debug_hold",
     "fts_debug_dispatch_stats", "fts_debug_stage_actions",
 ]
 
@@ -181,6 +181,7 @@ def _load():
         "fts_idemix_idv_destroy": ([P], None),
         "fts_idemix_identity_verify_batch": ([P, S, C.POINTER(C.c_void_p), C.POINTER(S), I32P], C.c_int),
         "fts_idemix_identity_last_timings": ([P, C.POINTER(C.c_float)], C.c_int),
+        "fts_idemix_identity_last_stats": ([P, C.POINTER(C.c_uint32)], C.c_int),
         "fts_idemix_pairing_debug": ([P, C.c_int, U8P, C.c_int, C.POINTER(C.c_uint32)], C.c_int),
     }
     for name, (args, res) in sig.items():

@@ -204,6 +204,13 @@ class IdentityVerifier:
         L.check("fts_idemix_identity_last_timings", L.lib.fts_idemix_identity_last_timings(self.h, ms))
         return float(ms[0]), float(ms[1])
 
+    def last_pairing_stats(self):
+        """(groups checked with one randomised pairing product, identities paired one by
+        one) of the last batch; (0, n) with FTS_IDV_BATCH=0"""
+        out = (C.c_uint32 * 2)()
+        L.check("fts_idemix_identity_last_stats", L.lib.fts_idemix_identity_last_stats(self.h, out))
+        return int(out[0]), int(out[1])
+
     def pairing_debug(self, which, p64, final_exp=True):
         """e(W or g2, P) (BN254 only): 6 Fp2 coefficients (w^0..w^5) as Montgomery ints"""
         out = (C.c_uint32 * 192)()

@@ -456,8 +456,13 @@ void fts_idemix_idv_destroy(fts_idemix_idv* idv);
  * Owner); status[i] <- FTS_OK or FTS_E_ID_* (the first failing check). */
 int fts_idemix_identity_verify_batch(fts_idemix_idv* idv, size_t n, const uint8_t* const* ids, const size_t* id_len,
                                      int32_t* status);
-/* HIP-event durations (ms) of the last batch: [0] decode + t-values + transcript, [1] pairings. */
+/* HIP-event durations (ms) of the last batch: [0] decode + t-values + transcript, [1] pairings
+ * (the batch check and the one-by-one pairings of the identities of failing groups). */
 int fts_idemix_identity_last_timings(fts_idemix_idv* idv, float* ms);
+/* The last batch's pairing check: out[0] = groups of 256 identities checked with one
+ * randomised pairing product each (0 with FTS_IDV_BATCH=0), out[1] = identities paired one
+ * by one (those of the groups whose product was not 1; every identity with the batch off). */
+int fts_idemix_identity_last_stats(fts_idemix_idv* idv, uint32_t* out);
 /* Debug (tests): e(Q, P) for Q = W (which 0) or g2 (1) and P = 64 raw BE bytes (BN254),
  * after the final exponentiation (final_exp != 0) or the Miller value; out192 = 6 Fp2
  * coefficients of w^0..w^5, Montgomery, little-endian limbs. */

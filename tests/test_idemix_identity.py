@@ -236,3 +236,56 @@ def test_bn254_g2_subgroup_checks(verifiers):
                      for f, wt, v in fields)
     with pytest.raises(L.FtsError):
         I.IdentityVerifier(w_bad, device=0, curve=I.FTS_CURVE_BN254)
+
+
+@pytest.mark.parametrize("tag", ["bn254", "fp256bn"])
+def test_batch_pairing_check_groups(verifiers, tag, monkeypatch):
+    """the randomised group pairing check (k_idv_bp_*): a batch whose identities all
+    satisfy the pairing equation (honest and ZK-tampered ones) pairs no identity one
+    by one; identities failing the equation ("APrime and ABar don't have the expected
+    structure") at known positions send exactly their groups of 256 to the one-by-one
+    pairing, and every verdict at its position equals the per-identity path's
+    (FTS_IDV_BATCH=0)"""
+    from fts_gpu import idemix as I
+    doc = _doc()[tag]
+    V = verifiers[tag]
+    tile = [(bytes.fromhex(t["identity"]), t["error"]) for t in doc["tile"]]
+    n = 8192
+    ids = [tile[(7 * i) % len(tile)] for i in range(n)]
+    st = V.verify_batch([x for x, _ in ids])
+    assert [I.message(int(s)) for s in st] == [e for _, e in ids]
+    assert V.last_pairing_stats() == (n // 256, 0)
+    # pairing failures in groups 3 and 17 (two in group 17)
+    bad = [c for c in doc["cases"] if c["error"] == "signature invalid: APrime and ABar don't have the expected structure"]
+    assert bad
+    pos = [3 * 256 + 5, 17 * 256 + 100, 17 * 256 + 255]
+    for j, p in enumerate(pos):
+        ids[p] = (bytes.fromhex(bad[j % len(bad)]["identity"]), bad[j % len(bad)]["error"])
+    st = V.verify_batch([x for x, _ in ids])
+    assert [I.message(int(s)) for s in st] == [e for _, e in ids]
+    groups, paired = V.last_pairing_stats()
+    assert groups == n // 256 and paired == 2 * 256  # every identity of the two groups decodes
+    # the per-identity path agrees verdict for verdict
+    monkeypatch.setenv("FTS_IDV_BATCH", "0")
+    W = I.IdentityVerifier(_ipk(doc["issuer"]), device=0, curve=doc["curve_id"])
+    try:
+        st0 = W.verify_batch([x for x, _ in ids])
+        assert W.last_pairing_stats() == (0, n)
+    finally:
+        W.close()
+    assert (st0 == st).all()
+
+
+def test_batch_pairing_check_wrong_issuer():
+    """every group fails under another issuer's W: all identities are paired one by one"""
+    from fts_gpu import idemix as I
+    doc = _doc()
+    with open(os.path.join(GOLD, "idemix", "bn254_tokengen", "IssuerPublicKey"), "rb") as f:
+        other = I.IdentityVerifier(f.read(), device=0, curve=I.FTS_CURVE_BN254)
+    ids = [bytes.fromhex(t["identity"]) for t in doc["bn254"]["tile"]] * 8
+    try:
+        st = other.verify_batch(ids)
+        assert all(int(s) == I.FTS_E_ID_PAIRING for s in st)
+        assert other.last_pairing_stats() == (2, len(ids))
+    finally:
+        other.close()
