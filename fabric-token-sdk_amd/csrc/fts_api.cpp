@@ -555,7 +555,10 @@ struct fts_ctx {
   // 41.4 ms; C5's sparse bad proofs keep 256, where 8 was slower,
   // tools/sweeps/gt1_small.txt).  Action calls have no batch across calls: 256.
   int gt_adapt = 1;
-  int x0_split = 1;  // FTS_X0_SPLIT: work path hashes the x0 prefix beside the com chain
+  // FTS_X0_SPLIT: bit 0 the work path hashes the x0 prefix beside the com chain, bit 1
+  // the latency path beside com_tree (round 6: a lone 4,096-proof batch 3.15 -> 2.87 ms,
+  // profiles/r06_x0_split_ab/); 1 = the work path only (rounds 2-5)
+  int x0_split = 3;
   // FTS_MSM_SORT: the MSMs' two-level counting sort (msm.hip k_rs_*; 0: k_msm_digits'
   // device atomics + k_msm_scatter, the round-4 batch-check sort, for A/B)
   int msm_sort = 1;
@@ -729,7 +732,7 @@ static int ctx_create(const uint8_t* pp_bytes, size_t pp_len, uint32_t bits, int
   if (const char* e = getenv("FTS_IDLE_FIRST_US")) c->idle_first_us = std::max(0, atoi(e));
   if (const char* e = getenv("FTS_COM_FIXED_MAX")) c->com_fixed_max = (size_t)std::max(0L, atol(e));
   if (const char* e = getenv("FTS_RLC_FORK")) c->rlc_fork = std::max(0, std::min(4, atoi(e)));
-  if (const char* e = getenv("FTS_X0_SPLIT")) c->x0_split = atoi(e) != 0;
+  if (const char* e = getenv("FTS_X0_SPLIT")) c->x0_split = std::max(0, std::min(3, atoi(e)));
   if (const char* e = getenv("FTS_MSM_SORT")) c->msm_sort = atoi(e) != 0;
   if (const char* e = getenv("FTS_MAIN_GROUPS")) c->main_groups = atoi(e) != 0;
   if (const char* e = getenv("FTS_FX_SERIAL")) c->fx_serial = atoi(e) != 0;
@@ -1528,10 +1531,10 @@ static int rp_enqueue(fts_ctx* c, Lane& L, int B, uint8_t* d_raw, uint32_t* d_sc
   d.rlc_fork = c->rlc_fork == 2 ? (d.com_fixed ? 0 : 1) : c->rlc_fork >= 3 ? (d.com_fixed ? 0 : c->rlc_fork) : c->rlc_fork;
   d.ev_coef = L.ev_c;
   d.ev_fx = L.ev_d;
-  // x0 prefix beside the com chain on the work path only: on the latency path,
-  // started beside com_tree it shared CUs with it and the MSM's chunks and
-  // delayed both (3.51 vs 3.06 ms, round 2)
-  d.x0_mid = c->x0_split && !d.com_fixed ? w.x0mid.as<uint32_t>() : nullptr;
+  // x0 prefix beside the com chain (work path) or com_tree (latency path; round 2
+  // measured that slower, 3.51 vs 3.06 ms, when the normalisation did not yet write
+  // the H' records and the prefix waited for a separate build)
+  d.x0_mid = (c->x0_split & (d.com_fixed ? 2 : 1)) ? w.x0mid.as<uint32_t>() : nullptr;
   d.excl = pre_rlc ? w.rp_excl.as<int32_t>() : nullptr;
   RlcDev r{w.r_key.as<uint32_t>(), w.r_msc.as<uint32_t>(),   w.r_coef.as<uint32_t>(), w.r_colsum.as<uint32_t>(),
            w.r_fixed.as<uint32_t>(), w.r_flag.as<int32_t>(), w.m_scratch.as<uint32_t>(), mp};

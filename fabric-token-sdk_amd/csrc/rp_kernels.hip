@@ -1801,9 +1801,17 @@ void launch_rp_batch(const RpBatchDev& d, const RlcDev& r, const uint32_t* table
     tl->mark("k_rp_fixed_all", s, (double)B * (2.0 * n + 2.0) * cost_fbw);
     if (d.ev_fx) (void)hipEventRecord(d.ev_fx, s);
     if (d.rlc_fork) rlc_side();
-    launch_normalize(nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be, s);
+    // with the x0 prefix split (FTS_X0_SPLIT bit 1), the normalisation also writes the
+    // H' records of the x0 messages, and the prefix is hashed on s2 beside com_tree
+    if (d.x0_mid) FTS_LAUNCH(k_rp_x0_hdr, B, 256, s, B, n, d.status, x0_const, d.x0_msgs);
+    launch_normalize(nhp, n, n + 1, 0, d.status, d.hpj, d.hpa, d.hp_be, s, d.x0_mid ? d.x0_msgs : nullptr);
     tl->mark("k_rp_normalize", s, (double)nhp * (7.0 + COST_INV / NORM_E));
-    tl->fork(s2, s);
+    tl->fork(s2, s);  // x*D (k_rp_xd) before com_tree
+    if (d.x0_mid) {   // after the fork above, so com_tree does not wait for the prefix
+      tl->fork(s, s2);
+      FTS_LAUNCH(k_rp_x0_hash, B, lbs, s2, B, n, k, d.status, d.x0_msgs, x0_tmpl, 0u, x0_cb1(n), d.x0_mid, d.ch);
+      tl->mark("k_rp_x0_prefix", s2, 0);
+    }
     hipLaunchKernelGGL(k_rp_com_tree, dim3((B + CT_PROOFS - 1) / CT_PROOFS), dim3(CT_LANES * CT_PROOFS), 0, s, B, n,
                        k, d.status, d.pts, d.terms, d.hpj, d.hpa, d.hp_be);
     tl->mark("k_rp_com_sum", s, (double)B * ((com_fx_slots(n) + 1) * COST_ADD + COST_NORM1));

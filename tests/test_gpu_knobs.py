@@ -76,12 +76,30 @@ def test_knob_rlc_fork(pp_raw, fork, work_path):
         pp.close()
 
 
-def test_knob_x0_split_off(pp_raw):
-    """FTS_X0_SPLIT=0: the work path hashes the whole x0 message after com (no
+@pytest.mark.parametrize("work_path", [False, True])
+def test_knob_x0_split_off(pp_raw, work_path):
+    """FTS_X0_SPLIT=0: both com paths hash the whole x0 message after com (no
     prefix midstate on the side stream) -- the same x0 bytes"""
-    pp = _ctx(pp_raw, 32, FTS_X0_SPLIT=0, FTS_COM_FIXED_MAX=0, FTS_LANES=1)
+    env = dict(FTS_X0_SPLIT=0, FTS_LANES=1)
+    if work_path:
+        env["FTS_COM_FIXED_MAX"] = 0
+    pp = _ctx(pp_raw, 32, **env)
     try:
-        _golden_check(pp, 32, True)
+        _golden_check(pp, 32, work_path)
+        assert "k_rp_x0_prefix" not in pp.last_timings()
+    finally:
+        pp.close()
+
+
+@pytest.mark.parametrize("bits", [32, 64])
+def test_knob_x0_split_latency_path(pp_raw, bits):
+    """FTS_X0_SPLIT=3 (default since round 6): the latency path too hashes the x0 prefix (H' records written
+    by the normalisation, k_rp_x0_hdr) on the side stream beside com_tree, then the
+    suffix after com -- the same verdicts, com, H' and x0"""
+    pp = _ctx(pp_raw, bits, FTS_X0_SPLIT=3, FTS_LANES=1)
+    try:
+        _golden_check(pp, bits, False)
+        assert "k_rp_x0_prefix" in pp.last_timings()
     finally:
         pp.close()
 
