@@ -1295,7 +1295,9 @@ int32_t parse_identity(const uint8_t* id, size_t len, bool bn, const uint32_t* r
     if ((x) != hipSuccess) return FTS_API_EDEVICE; \
   } while (0)
 
-constexpr int NSLOT = 8;  // calls in flight per handle (each slot: its own stream and buffers)
+constexpr int NSLOT = 8;  // calls in flight per handle (each slot: its own stream and buffers, grown on first use;
+                          // 12 concurrent calls hit HSA_STATUS_ERROR_OUT_OF_RESOURCES dispatching the
+                          // scratch-using pairing kernels, gpurun_out/ns)
 struct Slot {
   hipStream_t stream = nullptr;
   uint8_t* d_buf = nullptr;
