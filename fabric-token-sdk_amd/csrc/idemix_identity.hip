@@ -863,6 +863,7 @@ __global__ void __launch_bounds__(BP_G) k_idv_bp_terms(int n, const uint32_t* __
       put_f<CV>(S, 16, a.z);
     }
   }
+  __syncthreads();  // lane 0's last sum, read by lanes 0..23
   if (t < 24) part[((size_t)blockIdx.x * 2 + which) * 24 + t] = sh[(size_t)t * BP_G];
 }
 
