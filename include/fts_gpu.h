@@ -453,7 +453,11 @@ typedef struct fts_idemix_idv fts_idemix_idv;
 int fts_idemix_idv_create(int device, const uint8_t* ipk, size_t ipk_len, int curve_id, fts_idemix_idv** out);
 void fts_idemix_idv_destroy(fts_idemix_idv* idv);
 /* ids[i] = a serialized idemix owner identity (SerializedIdemixIdentity proto, the token's
- * Owner); status[i] <- FTS_OK or FTS_E_ID_* (the first failing check). */
+ * Owner); status[i] <- FTS_OK or FTS_E_ID_* (the first failing check).  Thread-safe: up to
+ * 8 calls on one handle run concurrently (one device slot each); more callers wait for a
+ * slot.  The pairing equation is checked per group of 256 identities as one randomised
+ * product (fresh getrandom weights per call, soundness 2^-128); the identities of a
+ * failing group are paired one by one, so status[i] is the per-identity verdict. */
 int fts_idemix_identity_verify_batch(fts_idemix_idv* idv, size_t n, const uint8_t* const* ids, const size_t* id_len,
                                      int32_t* status);
 /* HIP-event durations (ms) of the last batch: [0] decode + t-values + transcript, [1] pairings
