@@ -1346,13 +1346,27 @@ def bench_identity(args):
     kt, kp = kt / reps, kp / reps
     groups, paired = V.last_pairing_stats()
     # the dominant device work since the batch pairing check (round 6): the t-value
-    # kernels (k_idv_var's six GLV and fourteen fixed-base products per identity); the
+    # kernels (k_idv_var's six GLV and eleven fixed-base products per identity); the
     # pairing phase is mostly the latency of the per-group pairings (a few waves)
     mads = n * ID_TVAL_MULS * MAD_PER_MUL
     ach = mads / (kt * 1e-3) / 1e12
+    # HBM bytes of the three t-value launches at 65,536 identities (BN254), from the newest
+    # profiles/identity_traffic_rNN.json (separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes)
+    traffic, tsrc = None, None
+    if tag == "bn254" and n == 65536:
+        import glob
+        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "identity_traffic_r[0-9][0-9].json")))
+        try:
+            tj = json.load(open(cands[-1]))
+            traffic = sum(int(tj[k]["fetch_bytes_raw"]) + int(tj[k]["write_bytes"])
+                          for k in ("k_idv_decode", "k_idv_var", "k_idv_tvals"))
+            tsrc = os.path.basename(cands[-1])
+        except (IndexError, OSError, KeyError, ValueError):
+            traffic = None
     roof = {"bound": "int32_valu (v_mad_u64_u32)", "kernel": "k_idv_decode + k_idv_var + k_idv_tvals",
             "achieved": round(ach, 3), "peak": round(PEAK_TMAD, 3), "unit": "TMAD/s", "frac": round(ach / PEAK_TMAD, 4),
-            "traffic": None, "kernel_ms": round(kt, 4), "mads_per_launch": mads, "muls_per_identity": ID_TVAL_MULS,
+            "traffic": traffic, "traffic_source": tsrc, "kernel_ms": round(kt, 4), "mads_per_launch": mads,
+            "muls_per_identity": ID_TVAL_MULS,
             "measured": "HIP events around the three launches on the library's stream, %d isolated calls after the "
                         "timed region (the Fp inversions are not counted as work)" % reps}
     pairing = {"phase_ms": round(kp, 4), "groups": groups, "paired_one_by_one": paired,
