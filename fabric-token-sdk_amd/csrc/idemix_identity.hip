@@ -867,8 +867,24 @@ __global__ void __launch_bounds__(BP_G) k_idv_bp_terms(int n, const uint32_t* __
   if (t < 24) part[((size_t)blockIdx.x * 2 + which) * 24 + t] = sh[(size_t)t * BP_G];
 }
 
-// lane = group: the two sums to affine (one inversion), then the group's pairing
-// product; gok[g] <- 1 if it is 1 in GT.  Lane 0 also clears the list counter.
+// lane pair per group (lanes 2g, 2g + 1 of one wave): lane h takes sum h to affine
+// and runs its single-pair Miller loop (h = 0: W with the A' sum, h = 1: g2 with the
+// -ABar sum; a sum at O contributes 1), lane 1 hands its Fp12 value to lane 0 by
+// shuffles, and lane 0 multiplies, exponentiates and writes gok[g] <- 1 if the
+// product is 1 in GT.  The two Miller loops run side by side instead of one 2-pair
+// loop on one lane (the group check is a call's latency, not its device work).
+// Lane 0 also clears the list counter.
+template <class B>
+FTS_DEV void shfl_f(typename B::F& a, int src) {
+#pragma unroll
+  for (int q = 0; q < 8; q++) a.v[q] = (uint32_t)__shfl((int)a.v[q], src, 64);
+}
+template <class B>
+FTS_DEV void shfl_f12(pair::F12<B>& f, int src) {
+  shfl_f<B>(f.c0.c0.a, src), shfl_f<B>(f.c0.c0.b, src), shfl_f<B>(f.c0.c1.a, src), shfl_f<B>(f.c0.c1.b, src);
+  shfl_f<B>(f.c0.c2.a, src), shfl_f<B>(f.c0.c2.b, src), shfl_f<B>(f.c1.c0.a, src), shfl_f<B>(f.c1.c0.b, src);
+  shfl_f<B>(f.c1.c1.a, src), shfl_f<B>(f.c1.c1.b, src), shfl_f<B>(f.c1.c2.a, src), shfl_f<B>(f.c1.c2.b, src);
+}
 template <class CV>
 __global__ void __launch_bounds__(64, FTS_IDV_OCC) k_idv_bp_pair(int ng, const uint32_t* __restrict__ part,
                                                     const uint32_t* __restrict__ lines, int32_t* __restrict__ gok,
@@ -876,36 +892,25 @@ __global__ void __launch_bounds__(64, FTS_IDV_OCC) k_idv_bp_pair(int ng, const u
   using B = typename CV::B;
   using K = typename B::K;
   using F = typename B::F;
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g == 0) *count = 0;
-  if (g >= ng) return;
-  const uint32_t* S = part + (size_t)g * 48;
-  const F z0 = B::ld(S + 16), z1 = B::ld(S + 40);
-  const bool o0 = B::is_zero(z0), o1 = B::is_zero(z1);
-  if (o0 && o1) {  // nothing left to check in this group
-    gok[g] = 1;
-    return;
-  }
-  const F w0 = o0 ? B::one() : z0, w1 = o1 ? B::one() : z1;
-  const F inv = B::inv(B::mul(w0, w1));
-  F x[2], y[2];
-  {
-    const F zi0 = B::mul(inv, w1), zi1 = B::mul(inv, w0);
-    const F a0 = B::mul(zi0, zi0), a1 = B::mul(zi1, zi1);
-    x[0] = B::mul(B::ld(S), a0), y[0] = B::mul(B::mul(B::ld(S + 8), a0), zi0);
-    x[1] = B::mul(B::ld(S + 24), a1), y[1] = B::mul(B::mul(B::ld(S + 32), a1), zi1);
-  }
-  const uint32_t* const L[2] = {lines, lines + (size_t)pair::n_lines<K>() * pair::LINE_WORDS};
-  pair::F12<B> f;
-  if (o0 || o1) {  // one pairing left: e(W, .) or e(g2, .)
-    const int q = o0 ? 1 : 0;
-    const uint32_t* const L1[1] = {L[q]};
-    const F x1[1] = {x[q]}, y1[1] = {y[q]};
+  static_assert(64 % 2 == 0, "a group's lane pair must sit in one wave");
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int g = gid >> 1, h = gid & 1;
+  if (gid == 0) *count = 0;
+  // no early return before the shuffle: both lanes of every pair reach it
+  const bool live = g < ng;
+  const uint32_t* S = part + (size_t)(live ? g : 0) * 48 + h * 24;
+  const F z = B::ld(S + 16);
+  const bool o = !live || B::is_zero(z);
+  pair::F12<B> f = pair::f12_one<B>();
+  if (!o) {
+    const F zi = B::inv(z), zi2 = B::mul(zi, zi);
+    const F x1[1] = {B::mul(B::ld(S), zi2)}, y1[1] = {B::mul(B::mul(B::ld(S + 8), zi2), zi)};
+    const uint32_t* const L1[1] = {lines + (size_t)h * pair::n_lines<K>() * pair::LINE_WORDS};
     f = pair::miller<B, 1>(L1, x1, y1);
-  } else {
-    f = pair::miller<B, 2>(L, x, y);
   }
-  gok[g] = pair::is_one(pair::final_exp_i(f)) ? 1 : 0;
+  pair::F12<B> f1 = f;
+  shfl_f12<B>(f1, (threadIdx.x & ~1) | 1);
+  if (h == 0 && live) gok[g] = pair::is_one(pair::final_exp_i(pair::mul12_i(f, f1))) ? 1 : 0;
 }
 
 // identity per lane: verdict of the identities of passing groups; the others are
@@ -972,7 +977,8 @@ template <class CV>
 void launch_batch(const Chain& c) {
   const size_t n = (size_t)c.n, ng = (n + BP_G - 1) / BP_G;
   k_idv_bp_terms<CV><<<dim3((unsigned)ng, 2), BP_G, 0, c.s>>>(c.n, c.pin, c.st, c.key, c.scr, c.scr + bp_part_off(n));
-  k_idv_bp_pair<CV><<<(unsigned)((ng + 63) / 64), 64, 0, c.s>>>((int)ng, c.scr + bp_part_off(n), c.lines, c.gok, c.cnt);
+  k_idv_bp_pair<CV><<<(unsigned)((2 * ng + 63) / 64), 64, 0, c.s>>>((int)ng, c.scr + bp_part_off(n), c.lines, c.gok,
+                                                                  c.cnt);
   k_idv_bp_sel<CV><<<(unsigned)((n + 255) / 256), 256, 0, c.s>>>(c.n, c.gok, c.zk, c.st, c.list, c.cnt);
 }
 // one-by-one pairings: `lanes` identities of the list (list) or all n
